@@ -1,0 +1,276 @@
+"""Benchmark: env.steps/s of batched CartPole worlds on MI355X (BASELINE.json config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds 4096]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+One "step" = one gym step of EVERY world of a rank: the action is applied, the
+physics runs (ABA + semi-implicit Euler, dt = 1 ms), and observation, reward,
+done, TimeLimit and auto-reset are computed -- all inside one HIP kernel
+launch per step (vecenv_step_kernel).  The K timed steps are replayed from
+HIP graphs of `--graph-chunk` launches each; per-step actions are written into
+the graph's action buffer before each replay (as a policy would), so the path
+is the closed-loop one.  Worlds shard across ranks with no data-path
+collective (weak scaling); the final observation tensor is all-gathered once
+over RCCL, as the north star asks.
+
+Printed JSON (rank 0): value = total env.steps/s over all ranks; roofline of
+the dominant kernel from per-launch HIP-event timing on its own stream;
+cpu_baseline = the fp64 C oracle on a bounded sample (rank 0, N = 1 only).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gym-ignition_amd", "python"))
+
+METRIC = "env·steps/sec (whole node) at N parallel worlds; obs max-abs-err vs DART"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_env_step(n_dofs: int, n_obs: int) -> int:
+    """Compulsory HBM bytes of one env step of one world:
+    read q, qd (4 B each per dof), action (4 B), steps + episode counters (8 B);
+    write q, qd, obs (4 B per element), reward (4 B), done (1 B), steps (4 B)."""
+    reads = 4 * 2 * n_dofs + 4 + 8
+    writes = 4 * 2 * n_dofs + 4 * n_obs + 4 + 1 + 4
+    return reads + writes
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--worlds", type=int, default=4096, help="worlds per GPU")
+    p.add_argument("--task", default="CartPoleDiscreteBalancing")
+    p.add_argument("--graph-chunk", type=int, default=100)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-rollout", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mwstep.shard import gather_obs
+    from mwstep.vecenv import VecEnv
+
+    W = args.worlds
+    env = VecEnv(args.task, n_worlds=W, device=local_rank, seed=args.seed, world_offset=rank * W)
+    stream = torch.cuda.Stream(device=dev)
+    env.sim.set_stream(stream.cuda_stream)
+    K = args.steps
+    G = max(1, min(args.graph_chunk, K))
+    n_full, rem = divmod(K, G)
+    total = args.warmup + K
+    gen = torch.Generator(device=dev).manual_seed(43 + rank)
+    if env.discrete:
+        actions = torch.randint(0, 2, (total, W), generator=gen, device=dev, dtype=torch.int32)
+    else:
+        actions = (torch.rand((total, W), generator=gen, device=dev) * 2 - 1) * 50.0
+    act_buf = torch.empty((G, W), dtype=actions.dtype, device=dev)
+
+    with torch.cuda.stream(stream):
+        env.reset()
+        # warmup (eager), then capture one graph of G step launches
+        for t in range(args.warmup):
+            env.step_raw(actions[t].data_ptr())
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for g in range(G):
+                env.step_raw(act_buf[g].data_ptr())
+        tail = None
+        if rem:
+            tail = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tail, stream=stream):
+                for g in range(rem):
+                    env.step_raw(act_buf[g].data_ptr())
+        # one untimed replay to settle
+        act_buf.copy_(actions[:G])
+        graph.replay()
+    stream.synchronize()
+
+    # -------------------------------------------------------- timed region
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for c in range(n_full):
+            base = args.warmup + c * G
+            act_buf.copy_(actions[base:base + G])
+            graph.replay()
+        if rem:
+            base = args.warmup + n_full * G
+            act_buf[:rem].copy_(actions[base:base + rem])
+            tail.replay()
+        if world_size > 1:
+            gathered = gather_obs(env.obs)  # final observation tensor, RCCL over xGMI
+    torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    value = world_size * W * K / elapsed
+
+    # ------------------------------------- per-launch kernel time (HIP events)
+    launches = 200
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(launches)]
+    with torch.cuda.stream(stream):
+        for i in range(launches):
+            ev[i][0].record(stream)
+            env.step_raw(actions[i % total].data_ptr())
+            ev[i][1].record(stream)
+    stream.synchronize()
+    kernel_us = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+    bpe = algorithmic_bytes_per_env_step(env.sim.dofs, env.obs_dim)
+    achieved_gbs = bpe * W / (kernel_us * 1e-6) / 1e9
+
+    # ------------------------------------------- fused open-loop rollout figure
+    rollout = None
+    if not args.no_rollout:
+        T = 1000
+        with torch.cuda.stream(stream):
+            env.rollout(actions[:T].contiguous())   # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            env.rollout(actions[:T].contiguous())
+            e1.record(stream)
+        stream.synchronize()
+        r_ms = e0.elapsed_time(e1)
+        rollout = {"steps_per_launch": T, "ms_per_launch": round(r_ms, 4),
+                   "env_steps_per_s_per_gpu": round(W * T / (r_ms * 1e-3), 1),
+                   "note": "open-loop (actions known ahead); not the headline value"}
+
+    # ------------------------------------------------------ CPU baseline (rank 0, N=1)
+    cpu = None
+    parity = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline_and_parity(args, env, actions, np, torch)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env·steps/s",
+            "n_gpus": world_size,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (Philox resets, uniform random actions, seed 42/43)",
+            "config": {
+                "workload": f"{args.task}: {W} worlds per GPU, dt=1ms, 1 physics step per env step "
+                            "(BASELINE.json configs[1])",
+                "task": args.task,
+                "worlds_per_gpu": W,
+                "global_worlds": W * world_size,
+                "dt": 1e-3,
+                "launch": f"hipGraph of {G} per-step kernels",
+                "parallelism": f"worlds sharded over {world_size} GPU(s)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
+                "traffic": None,
+                "kernel": "vecenv_step_kernel<2,0,false,true,false>",
+                "kernel_us_median": round(kernel_us, 3),
+                "bytes_per_env_step": bpe,
+            },
+            "cpu_baseline": cpu,
+            "obs_max_abs_err_vs_oracle": parity,
+            "rollout_fused": rollout,
+        }
+        print(json.dumps(out))
+    env.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_and_parity(args, env, actions, np, torch):
+    """fp64 C oracle (oracle/, test infrastructure) on a bounded sample of the
+    same workload, single thread; plus a teacher-forced one-step parity check
+    of the GPU kernel against it on the same sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from mwstep import get_model_file
+    from mwstep.vecenv import TASKS
+
+    kind, model = TASKS[args.task]
+    cm = pyoracle.load_urdf(get_model_file(model))
+    Wc = 4096
+    acts = actions[:, :Wc].cpu().numpy() if env.n_worlds >= Wc else None
+    if acts is None:
+        return None, None
+    acts = acts if kind == 0 else acts.astype(np.float64)
+    ref = pyoracle.VecEnv(cm, pyoracle.make_task(kind, seed=args.seed), Wc)
+    ref.reset()
+    t0 = time.perf_counter()
+    ref.rollout(acts[:20])
+    probe = time.perf_counter() - t0
+    T = int(max(20, min(acts.shape[0], args.cpu_seconds / max(probe / 20, 1e-9))))
+    T = min(T, acts.shape[0])
+    ref.reset()
+    t0 = time.perf_counter()
+    ref.rollout(acts[:T])
+    cpu_s = time.perf_counter() - t0
+    cpu = {"value": round(Wc * T / cpu_s, 1), "unit": "env·steps/s", "cores": 1, "kind": "port",
+           "sample": f"{Wc} worlds x {T} env steps of {args.task}, fp64 C oracle, 1 thread "
+                     f"({cpu_s:.1f} s); the reference's ign-gazebo+DART path is not buildable here"}
+
+    # teacher-forced one-step parity on 256 worlds x 100 steps
+    from mwstep.vecenv import VecEnv
+    Wp, Tp = 256, 100
+    gpu = VecEnv(args.task, n_worlds=Wp, device=env.device.index, seed=args.seed)
+    orc = pyoracle.VecEnv(cm, pyoracle.make_task(kind, seed=args.seed), Wp)
+    gpu.reset()
+    orc.reset()
+    worst = 0.0
+    n = cm.n
+    for t in range(Tp):
+        gpu.set_state(torch.from_numpy(orc.q.reshape(n, Wp)), torch.from_numpy(orc.qd.reshape(n, Wp)))
+        a = acts[t, :Wp]
+        o, _, d, _ = gpu.step(torch.from_numpy(np.ascontiguousarray(a).astype(
+            np.int32 if kind == 0 else np.float32)).to(gpu.device))
+        o, d = o.cpu().numpy(), d.cpu().numpy().astype(bool)
+        orf, _, drf, _ = orc.step(a)
+        m = ~(d | drf)
+        if m.any():
+            worst = max(worst, float(np.abs(o[m] - orf[m]).max()))
+    gpu.close()
+    return cpu, {"value": worst, "mode": "one-step teacher-forced, 256 worlds x 100 steps",
+                 "vs": "fp64 DART-semantics oracle (DART itself absent: parity unpinned)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,441 @@
+// chain_dyn.hpp -- one engine substep of a fixed-base chain, float32, one
+// world per lane.  This is the MI355X restatement of DART 6.x World::step as
+// driven by the reference's Physics system (Physics.cpp:1824-1835) [EXT]:
+//
+//   ABA with implicit joint damping  (Featherstone; DART GenericJoint::
+//       updateInvProjArtInertiaImplicit / updateTotalForceDynamic)
+//   qd += dt * qdd                   (integrateVelocities)
+//   joint-space boxed LCP            (limits / servo / Coulomb friction rows,
+//       projected Gauss-Seidel over an incrementally maintained dqd = M^-1 x)
+//   q  += dt * qd                    (integratePositions, semi-implicit Euler)
+//
+// Layout decisions for CDNA4:
+//   - N (dofs) is a template parameter and every per-body loop is unrolled, so
+//     all per-body state (transforms, articulated terms, Minv columns) lives
+//     in VGPRs; no runtime-indexed private arrays (they would go to scratch).
+//   - model parameters come from a uniform pointer with compile-time offsets:
+//     hipcc turns them into scalar (s_load) reads shared by the wave.
+//   - spatial inertias are kept in 3x3 blocks (A sym, B, C sym: 21 floats).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "chain_params.hpp"
+
+namespace mw {
+namespace dev {
+
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+struct M3 { float m[9]; };  // row-major
+struct Sy { float xx, yy, zz, xy, xz, yz; };
+struct SV { f3 w, v; };     // spatial vector [angular; linear]
+struct SI { Sy A; M3 B; Sy C; };  // symmetric 6x6 [[A, B], [B^T, C]]
+
+__device__ __forceinline__ f3 mul(const M3& R, f3 v) {
+    return {R.m[0] * v.x + R.m[1] * v.y + R.m[2] * v.z, R.m[3] * v.x + R.m[4] * v.y + R.m[5] * v.z,
+            R.m[6] * v.x + R.m[7] * v.y + R.m[8] * v.z};
+}
+__device__ __forceinline__ f3 mulT(const M3& R, f3 v) {
+    return {R.m[0] * v.x + R.m[3] * v.y + R.m[6] * v.z, R.m[1] * v.x + R.m[4] * v.y + R.m[7] * v.z,
+            R.m[2] * v.x + R.m[5] * v.y + R.m[8] * v.z};
+}
+__device__ __forceinline__ f3 mul(const Sy& S, f3 v) {
+    return {S.xx * v.x + S.xy * v.y + S.xz * v.z, S.xy * v.x + S.yy * v.y + S.yz * v.z,
+            S.xz * v.x + S.yz * v.y + S.zz * v.z};
+}
+__device__ __forceinline__ SV operator+(const SV& a, const SV& b) { return {a.w + b.w, a.v + b.v}; }
+__device__ __forceinline__ SV operator*(float s, const SV& a) { return {s * a.w, s * a.v}; }
+__device__ __forceinline__ float dot(const SV& a, const SV& b) { return dot(a.w, b.w) + dot(a.v, b.v); }
+
+// X = Ad_{T^-1}: parent motion -> child coordinates
+__device__ __forceinline__ SV ad_inv(const M3& R, f3 p, const SV& a) {
+    return {mulT(R, a.w), mulT(R, a.v - cross(p, a.w))};
+}
+// X^T: child force -> parent coordinates
+__device__ __forceinline__ SV dad_inv(const M3& R, f3 p, const SV& f) {
+    const f3 fv = mul(R, f.v);
+    return {mul(R, f.w) + cross(p, fv), fv};
+}
+__device__ __forceinline__ SV mul(const SI& I, const SV& x) {
+    // B^T w = (w^T B)^T
+    const f3 btw = {I.B.m[0] * x.w.x + I.B.m[3] * x.w.y + I.B.m[6] * x.w.z,
+                    I.B.m[1] * x.w.x + I.B.m[4] * x.w.y + I.B.m[7] * x.w.z,
+                    I.B.m[2] * x.w.x + I.B.m[5] * x.w.y + I.B.m[8] * x.w.z};
+    return {mul(I.A, x.w) + mul(I.B, x.v), btw + mul(I.C, x.v)};
+}
+
+// R S R^T for symmetric S
+__device__ __forceinline__ Sy rot_sym(const M3& R, const Sy& S) {
+    float T[9];  // T = R S
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const f3 row = {R.m[r * 3], R.m[r * 3 + 1], R.m[r * 3 + 2]};
+        const f3 c = mul(S, row);  // (R S)_r = S row (S symmetric)
+        T[r * 3] = c.x; T[r * 3 + 1] = c.y; T[r * 3 + 2] = c.z;
+    }
+    auto e = [&](int r, int c) {
+        return T[r * 3] * R.m[c * 3] + T[r * 3 + 1] * R.m[c * 3 + 1] + T[r * 3 + 2] * R.m[c * 3 + 2];
+    };
+    return {e(0, 0), e(1, 1), e(2, 2), e(0, 1), e(0, 2), e(1, 2)};
+}
+// R B R^T for general B
+__device__ __forceinline__ M3 rot_gen(const M3& R, const M3& B) {
+    M3 T, O;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            T.m[r * 3 + c] = R.m[r * 3] * B.m[c] + R.m[r * 3 + 1] * B.m[3 + c] + R.m[r * 3 + 2] * B.m[6 + c];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            O.m[r * 3 + c] = T.m[r * 3] * R.m[c * 3] + T.m[r * 3 + 1] * R.m[c * 3 + 1] + T.m[r * 3 + 2] * R.m[c * 3 + 2];
+    return O;
+}
+
+// X^T I X with X = Ad_{T^-1}, T = (R, p): child articulated inertia -> parent.
+//   A' = R A R^T, B' = R B R^T, C' = R C R^T, P = [p]x
+//   A_p = A' + P B'^T - B' P - P C' P,  B_p = B' + P C',  C_p = C'
+__device__ __forceinline__ SI to_parent(const M3& R, f3 p, const SI& I) {
+    const Sy A = rot_sym(R, I.A);
+    const M3 B = rot_gen(R, I.B);
+    const Sy C = rot_sym(R, I.C);
+    // PC = P C'  (column k of C' crossed: P x = p x x)
+    const f3 c0 = {C.xx, C.xy, C.xz}, c1 = {C.xy, C.yy, C.yz}, c2 = {C.xz, C.yz, C.zz};
+    const f3 pc0 = cross(p, c0), pc1 = cross(p, c1), pc2 = cross(p, c2);  // columns of P C'
+    // B_p = B' + P C'
+    M3 Bp;
+    Bp.m[0] = B.m[0] + pc0.x; Bp.m[1] = B.m[1] + pc1.x; Bp.m[2] = B.m[2] + pc2.x;
+    Bp.m[3] = B.m[3] + pc0.y; Bp.m[4] = B.m[4] + pc1.y; Bp.m[5] = B.m[5] + pc2.y;
+    Bp.m[6] = B.m[6] + pc0.z; Bp.m[7] = B.m[7] + pc1.z; Bp.m[8] = B.m[8] + pc2.z;
+    // Y = P B'^T : column k of B'^T is row k of B'
+    const f3 b0 = {B.m[0], B.m[1], B.m[2]}, b1 = {B.m[3], B.m[4], B.m[5]}, b2 = {B.m[6], B.m[7], B.m[8]};
+    const f3 y0 = cross(p, b0), y1 = cross(p, b1), y2 = cross(p, b2);  // columns of P B'^T
+    // Z = P C' P = (P C') P ; (M P)_{rc} = row_r(M) . column_c(P); P columns: P e_c = p x e_c
+    // row r of PC: (pc0.r, pc1.r, pc2.r);  M P = - (P^T M^T)^T ... use M P = -(P M^T)^T
+    const f3 r0 = {pc0.x, pc1.x, pc2.x}, r1 = {pc0.y, pc1.y, pc2.y}, r2 = {pc0.z, pc1.z, pc2.z};
+    // (PC P)_{rc} = - (p x row_r)_c
+    const f3 z0 = -cross(p, r0), z1 = -cross(p, r1), z2 = -cross(p, r2);  // rows of PC'P
+    // A_p = A' + Y + Y^T - Z  (since -B'P = (P B'^T)^T = Y^T)
+    Sy Ap;
+    Ap.xx = A.xx + 2.f * y0.x - z0.x;
+    Ap.yy = A.yy + 2.f * y1.y - z1.y;
+    Ap.zz = A.zz + 2.f * y2.z - z2.z;
+    Ap.xy = A.xy + y1.x + y0.y - z0.y;
+    Ap.xz = A.xz + y2.x + y0.z - z0.z;
+    Ap.yz = A.yz + y2.y + y1.z - z1.z;
+    return {Ap, Bp, C};
+}
+
+__device__ __forceinline__ SI& operator+=(SI& a, const SI& b) {
+    a.A.xx += b.A.xx; a.A.yy += b.A.yy; a.A.zz += b.A.zz; a.A.xy += b.A.xy; a.A.xz += b.A.xz; a.A.yz += b.A.yz;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a.B.m[k] += b.B.m[k];
+    a.C.xx += b.C.xx; a.C.yy += b.C.yy; a.C.zz += b.C.zz; a.C.xy += b.C.xy; a.C.xz += b.C.xz; a.C.yz += b.C.yz;
+    return a;
+}
+
+// AI - psi * U U^T
+__device__ __forceinline__ SI downdate(const SI& I, const SV& U, float psi) {
+    SI o = I;
+    const f3 a = U.w, b = U.v;
+    o.A.xx -= psi * a.x * a.x; o.A.yy -= psi * a.y * a.y; o.A.zz -= psi * a.z * a.z;
+    o.A.xy -= psi * a.x * a.y; o.A.xz -= psi * a.x * a.z; o.A.yz -= psi * a.y * a.z;
+    const float ax[3] = {a.x, a.y, a.z}, bx[3] = {b.x, b.y, b.z};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o.B.m[r * 3 + c] -= psi * ax[r] * bx[c];
+    o.C.xx -= psi * b.x * b.x; o.C.yy -= psi * b.y * b.y; o.C.zz -= psi * b.z * b.z;
+    o.C.xy -= psi * b.x * b.y; o.C.xz -= psi * b.x * b.z; o.C.yz -= psi * b.y * b.z;
+    return o;
+}
+
+// rigid-body spatial inertia about the body origin
+__device__ __forceinline__ SI rigid(const BodyF& b) {
+    SI I;
+    I.A = {b.Io[0], b.Io[1], b.Io[2], b.Io[3], b.Io[4], b.Io[5]};
+    const float m = b.mass, cx = b.com[0], cy = b.com[1], cz = b.com[2];
+    // B = m [c]x
+    I.B.m[0] = 0.f;     I.B.m[1] = -m * cz; I.B.m[2] = m * cy;
+    I.B.m[3] = m * cz;  I.B.m[4] = 0.f;     I.B.m[5] = -m * cx;
+    I.B.m[6] = -m * cy; I.B.m[7] = m * cx;  I.B.m[8] = 0.f;
+    I.C = {m, m, m, 0.f, 0.f, 0.f};
+    return I;
+}
+
+__device__ __forceinline__ SV motion(const BodyF& b, float s) {
+    const f3 a = {b.axis[0] * s, b.axis[1] * s, b.axis[2] * s};
+    const f3 z = {0.f, 0.f, 0.f};
+    return (b.jtype == 0) ? SV{a, z} : SV{z, a};
+}
+__device__ __forceinline__ float proj(const BodyF& b, const SV& x) {
+    const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
+    return (b.jtype == 0) ? dot(a, x.w) : dot(a, x.v);
+}
+
+// per-body factorization kept for the forward and impulse passes
+struct BodyState {
+    M3 R;
+    f3 p;
+    SV U;      // AI S (implicit)
+    float psi; // (S^T AI S + dt d)^-1
+    float tt;  // total joint force
+    SV eta;    // velocity-product acceleration
+};
+struct ImpulseFactor {  // non-implicit (only when the model has damping)
+    SV U;
+    float psi;
+};
+
+template <int N, bool DUAL>
+struct Work {
+    BodyState bs[N];
+    ImpulseFactor nf[DUAL ? N : 1];
+};
+
+__device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p) {
+    if (b.jtype == 0) {
+        float s, c;
+        sincosf(q, &s, &c);
+        const float ax = b.axis[0], ay = b.axis[1], az = b.axis[2], v = 1.f - c;
+        const float J[9] = {c + ax * ax * v,      ax * ay * v - az * s, ax * az * v + ay * s,
+                            ay * ax * v + az * s, c + ay * ay * v,      ay * az * v - ax * s,
+                            az * ax * v - ay * s, az * ay * v + ax * s, c + az * az * v};
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                R.m[r * 3 + k] = b.E[r * 3] * J[k] + b.E[r * 3 + 1] * J[3 + k] + b.E[r * 3 + 2] * J[6 + k];
+        p = {b.r[0], b.r[1], b.r[2]};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.m[k] = b.E[k];
+        p = {b.r[0] + q * b.Ea[0], b.r[1] + q * b.Ea[1], b.r[2] + q * b.Ea[2]};
+    }
+}
+
+// ABA with implicit damping: fills W and returns qdd.
+template <int N, bool DUAL>
+__device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&q)[N],
+                                    const float (&qd)[N], const float (&tau)[N], float dt,
+                                    float (&qdd)[N], Work<N, DUAL>& W) {
+    SV Bown[N];
+    // forward kinematics, velocities, bias forces
+    SV V = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    f3 g = {P->g[0], P->g[1], P->g[2]};
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const BodyF& b = P->b[i];
+        BodyState& s = W.bs[i];
+        joint_pose(b, q[i], s.R, s.p);
+        const SV Sq = motion(b, qd[i]);
+        V = ad_inv(s.R, s.p, V) + Sq;
+        g = mulT(s.R, g);
+        // eta = ad(V, S qd)
+        s.eta = {cross(V.w, Sq.w), cross(V.w, Sq.v) + cross(V.v, Sq.w)};
+        // h = I V (rigid)
+        const f3 c = {b.com[0], b.com[1], b.com[2]};
+        const Sy Io = {b.Io[0], b.Io[1], b.Io[2], b.Io[3], b.Io[4], b.Io[5]};
+        const f3 hw = mul(Io, V.w) + b.mass * cross(c, V.v);
+        const f3 hv = b.mass * (V.v - cross(c, V.w));
+        // B = -dad(V, IV) - I [0; g]
+        Bown[i].w = cross(V.w, hw) + cross(V.v, hv) - b.mass * cross(c, g);
+        Bown[i].v = cross(V.w, hv) - b.mass * g;
+    }
+    // backward pass
+    SI carry;
+    SI carryN;
+    SV carryB = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        const BodyF& b = P->b[i];
+        BodyState& s = W.bs[i];
+        SI AI = rigid(b);
+        if (i < N - 1) AI += carry;
+        const SV Bi = (i < N - 1) ? (Bown[i] + carryB) : Bown[i];
+        // U = AI S
+        s.U = (b.jtype == 0)
+                  ? SV{mul(AI.A, {b.axis[0], b.axis[1], b.axis[2]}),
+                       mulT(AI.B, {b.axis[0], b.axis[1], b.axis[2]})}
+                  : SV{mul(AI.B, {b.axis[0], b.axis[1], b.axis[2]}),
+                       mul(AI.C, {b.axis[0], b.axis[1], b.axis[2]})};
+        const float D = proj(b, s.U);
+        s.psi = 1.f / (D + dt * b.damping);
+        const SV AIeta = mul(AI, s.eta);
+        s.tt = tau[i] - b.damping * qd[i] - proj(b, AIeta + Bi);
+        if constexpr (DUAL) {
+            SI AIn = rigid(b);
+            if (i < N - 1) AIn += carryN;
+            const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
+            W.nf[i].U = (b.jtype == 0) ? SV{mul(AIn.A, a), mulT(AIn.B, a)} : SV{mul(AIn.B, a), mul(AIn.C, a)};
+            W.nf[i].psi = 1.f / proj(b, W.nf[i].U);
+            if (i > 0) carryN = to_parent(s.R, s.p, downdate(AIn, W.nf[i].U, W.nf[i].psi));
+        }
+        if (i > 0) {
+            carry = to_parent(s.R, s.p, downdate(AI, s.U, s.psi));
+            const SV beta = Bi + AIeta + (s.psi * s.tt) * s.U;
+            carryB = dad_inv(s.R, s.p, beta);
+        }
+    }
+    // forward accelerations
+    SV a = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const BodyF& b = P->b[i];
+        const BodyState& s = W.bs[i];
+        const SV ap = ad_inv(s.R, s.p, a);
+        qdd[i] = s.psi * (s.tt - dot(s.U, ap));
+        a = ap + s.eta + motion(b, qdd[i]);
+    }
+}
+
+// column j of M^-1 (velocity change of every dof for a unit impulse on dof j)
+template <int N, bool DUAL, int J>
+__device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const Work<N, DUAL>& W,
+                                            float (&col)[N]) {
+    float u[N];
+    SV Bimp = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        if (i > J) { u[i] = 0.f; continue; }
+        if (i == J) { u[i] = 1.f; continue; }
+        SV U1;
+        float psi1;
+        if constexpr (DUAL) { U1 = W.nf[i + 1].U; psi1 = W.nf[i + 1].psi; }
+        else { U1 = W.bs[i + 1].U; psi1 = W.bs[i + 1].psi; }
+        Bimp = dad_inv(W.bs[i + 1].R, W.bs[i + 1].p, Bimp + (psi1 * u[i + 1]) * U1);
+        u[i] = -proj(P->b[i], Bimp);
+    }
+    SV dv = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        SV U;
+        float psi;
+        if constexpr (DUAL) { U = W.nf[i].U; psi = W.nf[i].psi; }
+        else { U = W.bs[i].U; psi = W.bs[i].psi; }
+        const SV dvp = ad_inv(W.bs[i].R, W.bs[i].p, dv);
+        col[i] = psi * (u[i] - dot(U, dvp));
+        dv = dvp + motion(P->b[i], col[i]);
+    }
+}
+
+template <int N, bool DUAL, int J = 0>
+__device__ __forceinline__ void minv_columns(const ChainF* __restrict__ P, const Work<N, DUAL>& W,
+                                             const bool (&need)[N], float (&Minv)[N][N]) {
+    if constexpr (J < N) {
+        if (need[J]) {
+            float col[N];
+            minv_column<N, DUAL, J>(P, W, col);
+#pragma unroll
+            for (int k = 0; k < N; ++k) Minv[k][J] = col[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) Minv[k][J] = 0.f;
+        }
+        minv_columns<N, DUAL, J + 1>(P, W, need, Minv);
+    }
+}
+
+// DART constants [EXT]: ERP 0.01, max error-reduction velocity 10
+constexpr float kErp = 0.01f;
+constexpr float kMaxErv = 10.f;
+
+// One engine substep.  act[i]: kActForce (tau[i] is the clipped command) or
+// kActServo (vcmd[i] is the velocity command).  CONS enables the LCP rows.
+template <int N, bool DUAL, bool CONS>
+__device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
+                                        const float (&tau)[N], const uint8_t (&act)[N],
+                                        const float (&vcmd)[N], float dt, int pgs_iters,
+                                        float (&qdd)[N]) {
+    Work<N, DUAL> W;
+    aba<N, DUAL>(P, q, qd, tau, dt, qdd, W);
+#pragma unroll
+    for (int i = 0; i < N; ++i) qd[i] += dt * qdd[i];
+
+    if constexpr (CONS) {
+        // rows per dof: 0 limit, 1 servo, 2 Coulomb friction
+        bool on[N][3];
+        float bb[N][3], lo[N][3], hi[N][3];
+        bool need[N];
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const BodyF& b = P->b[i];
+            on[i][0] = on[i][1] = on[i][2] = false;
+            bb[i][0] = bb[i][1] = bb[i][2] = 0.f;
+            lo[i][0] = lo[i][1] = lo[i][2] = 0.f;
+            hi[i][0] = hi[i][1] = hi[i][2] = 0.f;
+            if (b.limited) {
+                float viol = q[i] - b.lower;
+                if (viol <= 0.f) {
+                    on[i][0] = true; lo[i][0] = 0.f; hi[i][0] = INFINITY;
+                } else {
+                    viol = q[i] - b.upper;
+                    if (viol >= 0.f) { on[i][0] = true; lo[i][0] = -INFINITY; hi[i][0] = 0.f; }
+                }
+                const float bounce = fminf(fmaxf(-viol * kErp / dt, -kMaxErv), kMaxErv);
+                bb[i][0] = -qd[i] + bounce;
+            }
+            if (act[i] == kActServo) {
+                const float vc = fminf(fmaxf(vcmd[i], -b.vel_limit), b.vel_limit);
+                const float err = vc - qd[i];
+                if (err != 0.f) {
+                    on[i][1] = true; bb[i][1] = err;
+                    lo[i][1] = -b.effort * dt; hi[i][1] = b.effort * dt;
+                }
+            }
+            if (b.friction != 0.f && qd[i] != 0.f) {
+                on[i][2] = true; bb[i][2] = -qd[i];
+                hi[i][2] = b.friction * dt; lo[i][2] = -hi[i][2];
+            }
+            need[i] = on[i][0] || on[i][1] || on[i][2];
+            any = any || need[i];
+        }
+        if (any) {
+            float Minv[N][N];
+            minv_columns<N, DUAL>(P, W, need, Minv);
+            float x[N][3], dq[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) { x[i][0] = x[i][1] = x[i][2] = 0.f; dq[i] = 0.f; }
+            for (int it = 0; it < pgs_iters; ++it) {
+#pragma unroll
+                for (int d = 0; d < N; ++d) {
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) {
+                        if (on[d][t]) {
+                            const float xn = fminf(fmaxf(x[d][t] + (bb[d][t] - dq[d]) / Minv[d][d], lo[d][t]), hi[d][t]);
+                            const float delta = xn - x[d][t];
+                            x[d][t] = xn;
+#pragma unroll
+                            for (int k = 0; k < N; ++k) dq[k] += delta * Minv[k][d];
+                        }
+                    }
+                }
+            }
+            const float inv_dt = 1.f / dt;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                qd[i] += dq[i];
+                qdd[i] += dq[i] * inv_dt;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] += dt * qd[i];
+}
+
+}  // namespace dev
+}  // namespace mw

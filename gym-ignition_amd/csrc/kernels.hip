@@ -1,0 +1,353 @@
+// kernels.hip -- HIP kernels of the many-worlds stepper (gfx950).
+//
+// One world per lane.  State is SoA [dof][world] so that every load/store of
+// a wave is 256 contiguous bytes; model parameters are uniform (scalar path).
+//
+//  scenario_run   : GazeboSimulator::run() semantics for the ScenarI/O shim
+//                   (resets -> commands -> substeps -> readback, force command
+//                   consumed by the first substep), Physics.cpp:646-685,
+//                   :1330-1440, :2226-2345.
+//  vecenv_step    : one gym step of every world with the Task logic of
+//                   python/gym_ignition_environments/tasks/*.py fused in
+//                   (obs, reward, done, TimeLimit, auto-reset).
+//  vecenv_reset   : initial reset of every world (Philox4x32-10).
+#include "chain_dyn.hpp"
+#include "kernels.hpp"
+
+namespace mw {
+namespace dev {
+
+// ------------------------------------------------------------ RNG -------
+__device__ __forceinline__ void philox(uint32_t seed_lo, uint32_t seed_hi, uint32_t world,
+                                       uint32_t episode, uint32_t (&out)[4]) {
+    uint32_t c0 = world, c1 = episode, c2 = 0u, c3 = 0u, k0 = seed_lo, k1 = seed_hi;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+__device__ __forceinline__ float unif(uint32_t x, float lo, float hi) {
+    return lo + (hi - lo) * (static_cast<float>(x >> 8) * (1.f / 16777216.f));
+}
+
+constexpr float kPi = 3.14159265358979323846f;
+
+// ----------------------------------------------------------- tasks ------
+// kinds: 0 CartPoleDiscreteBalancing, 1 CartPoleContinuousBalancing,
+//        2 CartPoleContinuousSwingup, 3 PendulumSwingUp
+template <int N, int KIND>
+__device__ __forceinline__ void task_reset(const TaskF& T, uint32_t w, uint32_t episode,
+                                           float (&q)[N], float (&qd)[N]) {
+    uint32_t r[4];
+    philox(T.seed_lo, T.seed_hi, w, episode, r);
+    if constexpr (KIND == 0 || KIND == 1) {
+        // x, dx, q, dq = U(-0.05, 0.05)   cartpole_discrete_balancing.py:137
+        q[0] = unif(r[0], -0.05f, 0.05f); qd[0] = unif(r[1], -0.05f, 0.05f);
+        q[1] = unif(r[2], -0.05f, 0.05f); qd[1] = unif(r[3], -0.05f, 0.05f);
+    } else if constexpr (KIND == 2) {
+        // q = pi - deg2rad(U(-60, 60)); x, dx, dq = U(-0.05, 0.05)  cartpole_continuous_swingup.py:145-146
+        q[1] = kPi - unif(r[0], -60.f, 60.f) * (kPi / 180.f);
+        q[0] = unif(r[1], -0.05f, 0.05f); qd[0] = unif(r[2], -0.05f, 0.05f);
+        qd[1] = unif(r[3], -0.05f, 0.05f);
+    } else {
+        // cos, sin, dq = observation_space.sample(); q = atan2(sin, cos)  pendulum_swingup.py:117-127
+        const float c = unif(r[0], -1.f, 1.f), s = unif(r[1], -1.f, 1.f);
+        q[0] = atan2f(s, c);
+        qd[0] = unif(r[2], -10.f, 10.f);
+    }
+}
+
+template <int N, int KIND>
+__device__ __forceinline__ void task_obs(const float (&q)[N], const float (&qd)[N], float (&o)[4]) {
+    if constexpr (KIND == 3) {
+        float s, c;
+        sincosf(q[0], &s, &c);
+        o[0] = c; o[1] = s; o[2] = qd[0]; o[3] = 0.f;
+    } else {
+        o[0] = q[0]; o[1] = qd[0]; o[2] = q[1]; o[3] = qd[1];   // [x, dx, q, dq]
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ bool task_done(const TaskF& T, const float (&o)[4]) {
+    constexpr int no = (KIND == 3) ? 3 : 4;
+    bool inside = true;
+#pragma unroll
+    for (int k = 0; k < no; ++k) inside = inside && (o[k] >= -T.hi[k]) && (o[k] <= T.hi[k]);
+    return !inside;
+}
+
+template <int N, int KIND>
+__device__ __forceinline__ float task_reward(const TaskF& T, const float (&q)[N], const float (&qd)[N],
+                                             const float (&o)[4], bool done) {
+    if constexpr (KIND == 0 || KIND == 1) {
+        float r = done ? 0.f : 1.f;
+        if (T.reward_cart_at_center)
+            r = r - 0.10f * fabsf(o[0]) - 0.10f * fabsf(o[1]) -
+                10.0f * (o[0] >= T.x_factor * 2.4f ? 1.f : 0.f);
+        return r;
+    } else if constexpr (KIND == 2) {
+        return (cosf(q[1]) + 1.f) * 0.5f - 0.1f * qd[0] * qd[0] -
+               10.0f * (q[0] >= T.x_factor * 2.4f ? 1.f : 0.f);
+    } else {
+        // the force target read after the run is the zero-filled JointForceCmd
+        // (Physics.cpp:2250-2254), so the 0.001 tau^2 term of
+        // pendulum_swingup.py:86-88 is identically zero
+        const float cost = (done ? 100.f : 0.f) + q[0] * q[0] + 0.1f * qd[0] * qd[0];
+        return -cost;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void load_state(const SimDev& S, int W, int w, float (&q)[N], float (&qd)[N]) {
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        q[d] = S.q[d * W + w];
+        qd[d] = S.qd[d * W + w];
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void store_state(const SimDev& S, int W, int w, const float (&q)[N],
+                                            const float (&qd)[N]) {
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        S.q[d * W + w] = q[d];
+        S.qd[d * W + w] = qd[d];
+    }
+}
+
+template <int NO>
+__device__ __forceinline__ void store_obs(float* __restrict__ dst, const float (&o)[4]) {
+    if constexpr (NO == 4) {
+        *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) dst[k] = o[k];
+    }
+}
+
+// ---------------------------------------------------------- kernels -----
+
+template <int N, bool DUAL, bool CONS>
+__global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restrict__ P, SimDev S, int W,
+                                                           float dt, int substeps, int paused,
+                                                           int pgs_iters) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    float q[N], qd[N];
+    load_state<N>(S, W, w, q, qd);
+    // UpdatePhysics: velocity reset, then position reset (Physics.cpp:1330-1375)
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        const uint8_t f = S.rflag[d * W + w];
+        if (f) {
+            if (f & 2u) qd[d] = S.rqd[d * W + w];
+            if (f & 1u) q[d] = S.rq[d * W + w];
+            S.rflag[d * W + w] = 0;
+        }
+    }
+    if (!paused) {
+        float cmd[N], vc[N], tau[N], qdd[N];
+        uint8_t act[N];
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            cmd[d] = S.cmd[d * W + w];
+            act[d] = S.act[d * W + w];
+            vc[d] = S.vtgt[d * W + w];
+        }
+        for (int s = 0; s < substeps; ++s) {
+#pragma unroll
+            for (int d = 0; d < N; ++d) {
+                // SetForce -> GenericJoint::setCommand clips to +-effort; the command
+                // only acts on the first substep (UpdateSim zero-fills it afterwards)
+                const float e = P->b[d].effort;
+                tau[d] = (act[d] == kActForce && s == 0) ? fminf(fmaxf(cmd[d], -e), e) : 0.f;
+            }
+            substep<N, DUAL, CONS>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
+        }
+#pragma unroll
+        for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];
+    }
+#pragma unroll
+    for (int d = 0; d < N; ++d) S.cmd[d * W + w] = 0.f;  // JointForceCmd zero-fill (paused too)
+    store_state<N>(S, W, w, q, qd);
+}
+
+template <int N, int KIND>
+__global__ void __launch_bounds__(256) vecenv_reset_kernel(TaskF T, SimDev S, VecDev V, float* __restrict__ obs,
+                                                           int W) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    float q[N], qd[N], o[4];
+    task_reset<N, KIND>(T, T.world_offset + static_cast<uint32_t>(w), 0u, q, qd);
+    task_obs<N, KIND>(q, qd, o);
+    constexpr int NO = (KIND == 3) ? 3 : 4;
+    store_obs<NO>(obs + static_cast<size_t>(w) * NO, o);
+    store_state<N>(S, W, w, q, qd);
+    V.episode[w] = 0u;
+    V.steps[w] = 0u;
+}
+
+// STEPS == 0: single step; otherwise loop over T_steps with [t, w] layouts.
+template <int N, int KIND, bool DUAL, bool CONS, bool ROLLOUT>
+__global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restrict__ P, TaskF T, SimDev S,
+                                                          VecDev V, const void* __restrict__ actions,
+                                                          float* __restrict__ obs, float* __restrict__ reward,
+                                                          uint8_t* __restrict__ done_out,
+                                                          float* __restrict__ term_obs, int W, float dt,
+                                                          int substeps, int pgs_iters, int T_steps) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    constexpr int NO = (KIND == 3) ? 3 : 4;
+    float q[N], qd[N];
+    load_state<N>(S, W, w, q, qd);
+    uint32_t episode = V.episode[w];
+    uint32_t steps = V.steps[w];
+    uint8_t act[N];
+    float vc[N];
+#pragma unroll
+    for (int d = 0; d < N; ++d) { act[d] = kActForce; vc[d] = 0.f; }
+    const int nsteps = ROLLOUT ? T_steps : 1;
+    for (int t = 0; t < nsteps; ++t) {
+        const size_t idx = static_cast<size_t>(t) * W + w;
+        float force;
+        if constexpr (KIND == 0) {
+            const int a = static_cast<const int32_t*>(actions)[idx];
+            force = (a == 1) ? T.force_mag : -T.force_mag;   // cartpole_discrete_balancing.py:70
+        } else {
+            force = static_cast<const float*>(actions)[idx];
+        }
+        // the driven joint ("linear" / "pivot") is dof 0; other joints are Idle
+        const float e = P->b[0].effort;
+        force = fminf(fmaxf(force, -e), e);
+        float tau[N], qdd[N];
+        for (int s = 0; s < substeps; ++s) {
+#pragma unroll
+            for (int d = 0; d < N; ++d) tau[d] = 0.f;
+            tau[0] = (s == 0) ? force : 0.f;
+            substep<N, DUAL, CONS>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
+        }
+        float o[4];
+        task_obs<N, KIND>(q, qd, o);
+        const bool tdone = task_done<KIND>(T, o);
+        reward[idx] = task_reward<N, KIND>(T, q, qd, o, tdone);
+        steps += 1u;
+        const bool d_ = tdone || (T.max_steps > 0 && steps >= static_cast<uint32_t>(T.max_steps));
+        done_out[idx] = d_ ? 1 : 0;
+        if (d_) {
+            store_obs<NO>(term_obs + idx * NO, o);
+            episode += 1u;
+            steps = 0u;
+            task_reset<N, KIND>(T, T.world_offset + static_cast<uint32_t>(w), episode, q, qd);
+            task_obs<N, KIND>(q, qd, o);
+        }
+        store_obs<NO>(obs + idx * NO, o);
+    }
+    store_state<N>(S, W, w, q, qd);
+    V.episode[w] = episode;
+    V.steps[w] = steps;
+}
+
+}  // namespace dev
+
+// ------------------------------------------------------- launchers ------
+namespace {
+
+dim3 grid_for(int W, int block) { return dim3(static_cast<unsigned>((W + block - 1) / block)); }
+
+// 64-thread blocks spread a small world count over as many CUs as possible
+// (each wave runs a long dependent chain); 256 once there is work for all.
+int block_for(int W) { return (W <= 64 * 256) ? 64 : 256; }
+
+template <int N>
+hipError_t scenario_n(const ChainF* P, bool cons, bool dual, const SimDev& S, int W, float dt,
+                      int substeps, int paused, int pgs, hipStream_t st) {
+    const int B = block_for(W);
+    if (!cons)
+        hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, false>), grid_for(W, B), dim3(B), 0, st, P,
+                           S, W, dt, substeps, paused, pgs);
+    else if (!dual)
+        hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, true>), grid_for(W, B), dim3(B), 0, st, P,
+                           S, W, dt, substeps, paused, pgs);
+    else
+        hipLaunchKernelGGL((dev::scenario_run_kernel<N, true, true>), grid_for(W, B), dim3(B), 0, st, P,
+                           S, W, dt, substeps, paused, pgs);
+    return hipGetLastError();
+}
+
+template <int N, int KIND, bool ROLLOUT>
+hipError_t vec_nk(const ChainF* P, bool cons, bool dual, const TaskF& T, const SimDev& S,
+                  const VecDev& V, const void* a, float* o, float* r, uint8_t* d, float* to, int W,
+                  float dt, int substeps, int pgs, int Ts, hipStream_t st) {
+    const int B = block_for(W);
+    if (!cons)
+        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, false, ROLLOUT>), grid_for(W, B), dim3(B),
+                           0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
+    else if (!dual)
+        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, true, ROLLOUT>), grid_for(W, B), dim3(B),
+                           0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
+    else
+        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, true, true, ROLLOUT>), grid_for(W, B), dim3(B),
+                           0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_scenario_run(const ChainF* P, int n, bool cons, bool dual, const SimDev& S, int W,
+                               float dt, int substeps, int paused, int pgs_iters, hipStream_t st) {
+    switch (n) {
+    case 1: return scenario_n<1>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 2: return scenario_n<2>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 3: return scenario_n<3>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 4: return scenario_n<4>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 5: return scenario_n<5>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 6: return scenario_n<6>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 7: return scenario_n<7>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 8: return scenario_n<8>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 9: return scenario_n<9>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_vecenv_reset(const ChainF* /*P*/, int n, const TaskF& T, const SimDev& S,
+                               const VecDev& V, float* obs, int W, hipStream_t st) {
+    const int B = block_for(W);
+    if (T.kind == 3 && n == 1)
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<1, 3>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+    else if (T.kind == 0 && n == 2)
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 0>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+    else if (T.kind == 1 && n == 2)
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 1>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+    else if (T.kind == 2 && n == 2)
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 2>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, const TaskF& T,
+                              const SimDev& S, const VecDev& V, const void* actions, float* obs,
+                              float* reward, uint8_t* done, float* term_obs, int W, float dt,
+                              int substeps, int pgs_iters, int T_steps, hipStream_t st) {
+#define MW_VEC(NN, KK)                                                                               \
+    return (T_steps > 0)                                                                             \
+               ? vec_nk<NN, KK, true>(P, cons, dual, T, S, V, actions, obs, reward, done, term_obs, W, \
+                                      dt, substeps, pgs_iters, T_steps, st)                          \
+               : vec_nk<NN, KK, false>(P, cons, dual, T, S, V, actions, obs, reward, done, term_obs, W, \
+                                       dt, substeps, pgs_iters, 1, st)
+    if (T.kind == 3 && n == 1) { MW_VEC(1, 3); }
+    if (T.kind == 0 && n == 2) { MW_VEC(2, 0); }
+    if (T.kind == 1 && n == 2) { MW_VEC(2, 1); }
+    if (T.kind == 2 && n == 2) { MW_VEC(2, 2); }
+#undef MW_VEC
+    return hipErrorInvalidValue;
+}
+
+}  // namespace mw

@@ -1,0 +1,58 @@
+// kernels.hpp -- host-callable launchers of the HIP kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "chain_params.hpp"
+
+namespace mw {
+
+// SoA device state of a simulator: every array is [n_dofs][n_worlds].
+struct SimDev {
+    float* q = nullptr;
+    float* qd = nullptr;
+    float* qdd = nullptr;
+    float* cmd = nullptr;     // JointForceCmd (consumed by the next substep)
+    float* vtgt = nullptr;   // JointVelocityTarget (VelocityFollowerDart)
+    float* rq = nullptr;     // JointPositionReset values
+    float* rqd = nullptr;    // JointVelocityReset values
+    uint8_t* act = nullptr;  // kActForce / kActServo
+    uint8_t* rflag = nullptr;  // bit0 position reset pending, bit1 velocity reset pending
+};
+
+// Task description for the device-side env (see sim.cpp for the sources).
+struct TaskF {
+    int32_t kind;
+    int32_t max_steps;
+    int32_t reward_cart_at_center;
+    int32_t n_obs;
+    uint32_t seed_lo, seed_hi;
+    uint32_t world_offset;
+    uint32_t pad_;
+    float force_mag;
+    float x_factor;   // reward rail factor (0.9 / 1.0 / 0.8)
+    float hi[4];      // float32 bounds of the done-space (reset_space / observation_space)
+};
+
+struct VecDev {
+    uint32_t* episode = nullptr;
+    uint32_t* steps = nullptr;
+};
+
+// Returns hipSuccess or the launch error.
+hipError_t launch_scenario_run(const ChainF* P, int n, bool cons, bool dual, const SimDev& S, int W,
+                               float dt, int substeps, int paused, int pgs_iters, hipStream_t st);
+
+hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
+                               const VecDev& V, float* obs, int W, hipStream_t st);
+
+// T_steps == 0: one step with the per-step output layout; otherwise a fused
+// open-loop rollout of T_steps steps ([T, W] inputs and outputs).
+hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, const TaskF& T,
+                              const SimDev& S, const VecDev& V, const void* actions, float* obs,
+                              float* reward, uint8_t* done, float* term_obs, int W, float dt,
+                              int substeps, int pgs_iters, int T_steps, hipStream_t st);
+
+}  // namespace mw

@@ -1,0 +1,434 @@
+// model.cpp -- minimal XML reader + URDF -> chain compiler (see model.hpp).
+#include "model.hpp"
+
+#include <cctype>
+#include <cmath>
+#include <cstdlib>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+
+namespace mw {
+namespace {
+
+// ------------------------------------------------------------------ XML ----
+struct XNode {
+    std::string tag;
+    std::map<std::string, std::string> attr;
+    std::vector<std::unique_ptr<XNode>> kids;
+
+    const XNode* child(const std::string& t) const {
+        for (auto& k : kids)
+            if (k->tag == t) return k.get();
+        return nullptr;
+    }
+    std::vector<const XNode*> children(const std::string& t) const {
+        std::vector<const XNode*> out;
+        for (auto& k : kids)
+            if (k->tag == t) out.push_back(k.get());
+        return out;
+    }
+    const std::string* get(const std::string& a) const {
+        auto it = attr.find(a);
+        return it == attr.end() ? nullptr : &it->second;
+    }
+};
+
+class XmlReader {
+public:
+    explicit XmlReader(const std::string& s) : s_(s) {}
+
+    std::unique_ptr<XNode> parse() {
+        std::unique_ptr<XNode> root;
+        while (skip_misc()) {
+            if (root) fail("multiple root elements");
+            root = element();
+        }
+        if (!root) fail("no root element");
+        return root;
+    }
+
+private:
+    const std::string& s_;
+    size_t i_ = 0;
+
+    [[noreturn]] void fail(const std::string& what) const {
+        throw std::runtime_error("XML parse error at offset " + std::to_string(i_) + ": " + what);
+    }
+    bool eof() const { return i_ >= s_.size(); }
+    bool starts(const char* p) const { return s_.compare(i_, std::char_traits<char>::length(p), p) == 0; }
+    void ws() {
+        while (!eof() && std::isspace(static_cast<unsigned char>(s_[i_]))) ++i_;
+    }
+    void skip_until(const char* end) {
+        size_t k = s_.find(end, i_);
+        if (k == std::string::npos) fail(std::string("unterminated construct, expected ") + end);
+        i_ = k + std::char_traits<char>::length(end);
+    }
+    // skips whitespace, comments, PIs, doctype, text; returns true when an
+    // element start tag follows
+    bool skip_misc() {
+        for (;;) {
+            ws();
+            if (eof()) return false;
+            if (starts("<?")) { skip_until("?>"); continue; }
+            if (starts("<!--")) { skip_until("-->"); continue; }
+            if (starts("<!")) { skip_until(">"); continue; }
+            if (s_[i_] == '<') return true;
+            ++i_;  // stray text
+        }
+    }
+    std::string name() {
+        size_t b = i_;
+        while (!eof() && (std::isalnum(static_cast<unsigned char>(s_[i_])) || s_[i_] == '_' ||
+                          s_[i_] == ':' || s_[i_] == '-' || s_[i_] == '.'))
+            ++i_;
+        if (b == i_) fail("expected a name");
+        return s_.substr(b, i_ - b);
+    }
+    std::unique_ptr<XNode> element() {
+        if (s_[i_] != '<') fail("expected '<'");
+        ++i_;
+        auto n = std::make_unique<XNode>();
+        n->tag = name();
+        for (;;) {
+            ws();
+            if (eof()) fail("unterminated start tag");
+            if (starts("/>")) { i_ += 2; return n; }
+            if (s_[i_] == '>') { ++i_; break; }
+            std::string a = name();
+            ws();
+            if (eof() || s_[i_] != '=') fail("expected '=' after attribute " + a);
+            ++i_;
+            ws();
+            if (eof() || (s_[i_] != '"' && s_[i_] != '\'')) fail("expected quoted value");
+            const char q = s_[i_++];
+            size_t e = s_.find(q, i_);
+            if (e == std::string::npos) fail("unterminated attribute value");
+            n->attr[a] = s_.substr(i_, e - i_);
+            i_ = e + 1;
+        }
+        // content
+        for (;;) {
+            if (eof()) fail("unterminated element <" + n->tag + ">");
+            if (starts("</")) {
+                i_ += 2;
+                std::string t = name();
+                if (t != n->tag) fail("mismatched </" + t + "> for <" + n->tag + ">");
+                ws();
+                if (eof() || s_[i_] != '>') fail("expected '>'");
+                ++i_;
+                return n;
+            }
+            if (starts("<!--")) { skip_until("-->"); continue; }
+            if (starts("<![CDATA[")) { skip_until("]]>"); continue; }
+            if (starts("<?")) { skip_until("?>"); continue; }
+            if (s_[i_] == '<') { n->kids.push_back(element()); continue; }
+            ++i_;  // character data is not used by URDF
+        }
+    }
+};
+
+// ------------------------------------------------------------ math -----
+using M3 = std::array<double, 9>;
+using V3 = std::array<double, 3>;
+
+M3 eye() { return {1, 0, 0, 0, 1, 0, 0, 0, 1}; }
+M3 mul(const M3& a, const M3& b) {
+    M3 c{};
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k)
+            c[r * 3 + k] = a[r * 3] * b[k] + a[r * 3 + 1] * b[3 + k] + a[r * 3 + 2] * b[6 + k];
+    return c;
+}
+V3 mul(const M3& a, const V3& v) {
+    return {a[0] * v[0] + a[1] * v[1] + a[2] * v[2], a[3] * v[0] + a[4] * v[1] + a[5] * v[2],
+            a[6] * v[0] + a[7] * v[1] + a[8] * v[2]};
+}
+M3 transpose(const M3& a) { return {a[0], a[3], a[6], a[1], a[4], a[7], a[2], a[5], a[8]}; }
+V3 add(const V3& a, const V3& b) { return {a[0] + b[0], a[1] + b[1], a[2] + b[2]}; }
+V3 sub(const V3& a, const V3& b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
+V3 scale(const V3& a, double s) { return {a[0] * s, a[1] * s, a[2] * s}; }
+
+// URDF rpy: fixed-axis roll (x), pitch (y), yaw (z): R = Rz * Ry * Rx
+M3 rpy(const V3& v) {
+    const double cr = std::cos(v[0]), sr = std::sin(v[0]);
+    const double cp = std::cos(v[1]), sp = std::sin(v[1]);
+    const double cy = std::cos(v[2]), sy = std::sin(v[2]);
+    const M3 Rx{1, 0, 0, 0, cr, -sr, 0, sr, cr};
+    const M3 Ry{cp, 0, sp, 0, 1, 0, -sp, 0, cp};
+    const M3 Rz{cy, -sy, 0, sy, cy, 0, 0, 0, 1};
+    return mul(Rz, mul(Ry, Rx));
+}
+
+M3 quat_wxyz(double w, double x, double y, double z) {
+    const double n = std::sqrt(w * w + x * x + y * y + z * z);
+    if (n == 0.0) throw std::runtime_error("zero quaternion in model pose");
+    w /= n; x /= n; y /= n; z /= n;
+    return {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+            2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+            2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+}
+
+std::vector<double> numbers(const std::string& s) {
+    std::vector<double> out;
+    const char* p = s.c_str();
+    char* end = nullptr;
+    for (;;) {
+        double v = std::strtod(p, &end);
+        if (end == p) break;
+        out.push_back(v);
+        p = end;
+    }
+    return out;
+}
+
+V3 vec_attr(const XNode* n, const char* a, V3 dflt) {
+    if (!n) return dflt;
+    const std::string* s = n->get(a);
+    if (!s) return dflt;
+    auto v = numbers(*s);
+    if (v.size() != 3) throw std::runtime_error(std::string("expected 3 numbers in attribute ") + a);
+    return {v[0], v[1], v[2]};
+}
+
+double num_attr(const XNode* n, const char* a, double dflt) {
+    if (!n) return dflt;
+    const std::string* s = n->get(a);
+    if (!s) return dflt;
+    auto v = numbers(*s);
+    if (v.size() != 1) throw std::runtime_error(std::string("expected a number in attribute ") + a);
+    return v[0];
+}
+
+// --------------------------------------------------------------- URDF ---
+struct Link {
+    double mass = 0.0;
+    V3 com{};
+    M3 I{};  // about COM, link frame
+};
+
+struct Joint {
+    std::string name, type, parent, child;
+    M3 R = eye();
+    V3 p{};
+    V3 axis{1, 0, 0};
+    double lower = -1e300, upper = 1e300, effort = 1e300, velocity = 1e300;
+    double damping = 0.0, friction = 0.0;
+};
+
+Link merge(const Link& a, const Link& b, const M3& R, const V3& p) {
+    Link out;
+    out.mass = a.mass + b.mass;
+    if (out.mass <= 0.0) return out;
+    const V3 cb = add(mul(R, b.com), p);
+    for (int k = 0; k < 3; ++k) out.com[k] = (a.mass * a.com[k] + b.mass * cb[k]) / out.mass;
+    const M3 Ib = mul(R, mul(b.I, transpose(R)));
+    auto shift = [](const M3& I, double m, const V3& d) {
+        M3 o = I;
+        const double dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) o[r * 3 + c] += m * ((r == c ? dd : 0.0) - d[r] * d[c]);
+        return o;
+    };
+    const M3 Ia = shift(a.I, a.mass, sub(a.com, out.com));
+    const M3 Ib2 = shift(Ib, b.mass, sub(cb, out.com));
+    for (int k = 0; k < 9; ++k) out.I[k] = Ia[k] + Ib2[k];
+    return out;
+}
+
+std::string read_source(const std::string& s) {
+    size_t k = s.find_first_not_of(" \t\r\n");
+    if (k != std::string::npos && s[k] == '<') return s;
+    std::ifstream f(s);
+    if (!f) throw std::runtime_error("cannot open model file '" + s + "'");
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+
+}  // namespace
+
+ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
+    const std::string text = read_source(path_or_xml);
+    XmlReader rd(text);
+    auto root = rd.parse();
+    if (root->tag != "robot")
+        throw std::runtime_error("only URDF <robot> models are supported (got <" + root->tag + ">)");
+
+    ChainModel out;
+    out.name = root->get("name") ? *root->get("name") : "model";
+
+    std::map<std::string, Link> links;
+    std::vector<std::string> link_order;
+    for (const XNode* le : root->children("link")) {
+        const std::string* nm = le->get("name");
+        if (!nm) throw std::runtime_error("<link> without name");
+        Link L;
+        if (const XNode* ine = le->child("inertial")) {
+            const XNode* o = ine->child("origin");
+            const M3 Ro = rpy(vec_attr(o, "rpy", {0, 0, 0}));
+            L.com = vec_attr(o, "xyz", {0, 0, 0});
+            const XNode* ms = ine->child("mass");
+            if (!ms) throw std::runtime_error("<inertial> without <mass> in link " + *nm);
+            L.mass = num_attr(ms, "value", 0.0);
+            const XNode* ie = ine->child("inertia");
+            M3 Iin{};
+            if (ie) {
+                const double ixx = num_attr(ie, "ixx", 0), iyy = num_attr(ie, "iyy", 0),
+                             izz = num_attr(ie, "izz", 0), ixy = num_attr(ie, "ixy", 0),
+                             ixz = num_attr(ie, "ixz", 0), iyz = num_attr(ie, "iyz", 0);
+                Iin = {ixx, ixy, ixz, ixy, iyy, iyz, ixz, iyz, izz};
+            }
+            L.I = mul(Ro, mul(Iin, transpose(Ro)));
+        }
+        links[*nm] = L;
+        link_order.push_back(*nm);
+    }
+
+    std::vector<Joint> joints;
+    for (const XNode* je : root->children("joint")) {
+        Joint J;
+        const std::string* nm = je->get("name");
+        const std::string* ty = je->get("type");
+        const XNode* pa = je->child("parent");
+        const XNode* ch = je->child("child");
+        if (!nm || !ty || !pa || !ch || !pa->get("link") || !ch->get("link"))
+            throw std::runtime_error("malformed <joint>");
+        J.name = *nm;
+        J.type = *ty;
+        J.parent = *pa->get("link");
+        J.child = *ch->get("link");
+        const XNode* o = je->child("origin");
+        J.R = rpy(vec_attr(o, "rpy", {0, 0, 0}));
+        J.p = vec_attr(o, "xyz", {0, 0, 0});
+        V3 ax = vec_attr(je->child("axis"), "xyz", {1, 0, 0});
+        const double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+        if (an == 0.0) throw std::runtime_error("zero joint axis in " + J.name);
+        J.axis = scale(ax, 1.0 / an);
+        if (const XNode* lim = je->child("limit")) {
+            J.effort = num_attr(lim, "effort", 1e300);
+            J.velocity = num_attr(lim, "velocity", 1e300);
+            if (J.type == "revolute" || J.type == "prismatic") {
+                J.lower = num_attr(lim, "lower", 0.0);
+                J.upper = num_attr(lim, "upper", 0.0);
+            }
+        }
+        if (const XNode* dyn = je->child("dynamics")) {
+            J.damping = num_attr(dyn, "damping", 0.0);
+            J.friction = num_attr(dyn, "friction", 0.0);
+        }
+        if (J.type != "fixed" && J.type != "revolute" && J.type != "continuous" &&
+            J.type != "prismatic")
+            throw std::runtime_error("unsupported joint type '" + J.type + "' (" + J.name + ")");
+        if (!links.count(J.parent) || !links.count(J.child))
+            throw std::runtime_error("joint " + J.name + " references an unknown link");
+        joints.push_back(J);
+    }
+
+    // root link
+    std::map<std::string, int> is_child;
+    for (auto& j : joints) is_child[j.child]++;
+    std::vector<std::string> roots;
+    for (auto& n : link_order)
+        if (!is_child.count(n)) roots.push_back(n);
+    if (roots.size() != 1) throw std::runtime_error("the model must have exactly one root link");
+
+    M3 baseR = quat_wxyz(pose[3], pose[4], pose[5], pose[6]);
+    V3 baseP{pose[0], pose[1], pose[2]};
+    std::string base = roots[0];
+    if (base == "world") {
+        int found = -1;
+        for (size_t k = 0; k < joints.size(); ++k)
+            if (joints[k].parent == "world") {
+                if (found >= 0) throw std::runtime_error("more than one joint attached to 'world'");
+                found = static_cast<int>(k);
+            }
+        if (found < 0 || joints[found].type != "fixed")
+            throw std::runtime_error("the 'world' link must be attached by one fixed joint");
+        baseP = add(baseP, mul(baseR, joints[found].p));
+        baseR = mul(baseR, joints[found].R);
+        base = joints[found].child;
+        joints.erase(joints.begin() + found);
+    } else {
+        throw std::runtime_error(
+            "floating-base models are not supported yet (root link '" + base +
+            "' is not attached to 'world')");
+    }
+
+    // lump fixed joints into their parent body
+    std::map<std::string, std::string> owner;
+    std::map<std::string, M3> offR;
+    std::map<std::string, V3> offP;
+    for (auto& n : link_order) { owner[n] = n; offR[n] = eye(); offP[n] = {0, 0, 0}; }
+    for (bool changed = true; changed;) {
+        changed = false;
+        for (size_t k = 0; k < joints.size(); ++k) {
+            if (joints[k].type != "fixed") continue;
+            const Joint j = joints[k];
+            const std::string po = owner[j.parent];
+            const M3 R = mul(offR[j.parent], j.R);
+            const V3 p = add(mul(offR[j.parent], j.p), offP[j.parent]);
+            links[po] = merge(links[po], links[j.child], R, p);
+            for (auto& n : link_order)
+                if (owner[n] == j.child) {
+                    owner[n] = po;
+                    offP[n] = add(mul(R, offP[n]), p);
+                    offR[n] = mul(R, offR[n]);
+                }
+            joints.erase(joints.begin() + static_cast<long>(k));
+            changed = true;
+            break;
+        }
+    }
+
+    // the moving joints must form a serial chain hanging from the base body
+    std::string cur = base;
+    std::vector<Joint> chain;
+    for (;;) {
+        std::vector<const Joint*> nxt;
+        for (auto& j : joints)
+            if (owner[j.parent] == cur) nxt.push_back(&j);
+        if (nxt.empty()) break;
+        if (nxt.size() > 1)
+            throw std::runtime_error("branched (tree) models are not supported yet: link '" + cur +
+                                     "' has several moving child joints");
+        chain.push_back(*nxt[0]);
+        cur = nxt[0]->child;
+    }
+    if (chain.size() != joints.size())
+        throw std::runtime_error("the model's moving joints do not form a single chain");
+
+    out.base_link = base;
+    out.base_R = baseR;
+    out.base_p = baseP;
+    for (const Joint& j : chain) {
+        ChainBody b;
+        b.joint_name = j.name;
+        b.link_name = j.child;
+        b.type = (j.type == "prismatic") ? JType::Prismatic : JType::Revolute;
+        b.continuous = (j.type == "continuous");
+        b.limited = (j.type == "revolute" || j.type == "prismatic");
+        b.E = mul(offR[j.parent], j.R);
+        b.r = add(mul(offR[j.parent], j.p), offP[j.parent]);
+        b.axis = j.axis;
+        const Link& L = links[j.child];
+        b.mass = L.mass;
+        b.com = L.com;
+        b.Ic = {L.I[0], L.I[4], L.I[8], L.I[1], L.I[2], L.I[5]};
+        b.damping = j.damping;
+        b.friction = j.friction;
+        b.lower = j.lower;
+        b.upper = j.upper;
+        b.effort = j.effort;
+        b.vel_limit = j.velocity;
+        if (b.mass <= 0.0) throw std::runtime_error("moving link '" + j.child + "' has no mass");
+        out.bodies.push_back(b);
+    }
+    if (out.bodies.empty()) throw std::runtime_error("the model has no moving joints");
+    return out;
+}
+
+}  // namespace mw

@@ -1,0 +1,54 @@
+// model.hpp -- host-side model compiler: URDF -> flat fixed-base chain.
+//
+// Mirrors what the reference does when a URDF is inserted
+// (World::insertModel, cpp/scenario/gazebo/src/World.cpp:70-180 ->
+// sdformat URDF import -> Physics::CreatePhysicsEntities,
+// cpp/scenario/plugins/Physics/Physics.cpp:687-1219):
+//   - links joined by fixed joints are lumped into one rigid body
+//     (sdformat's URDF fixed-joint reduction),
+//   - a root link named "world" fixes the model base to the world,
+//   - joint axis / limits / effort / damping / friction come from
+//     <axis>, <limit>, <dynamics> (ign-physics copies them into DART).
+// The output is shared by all worlds of a simulator (topology and
+// parameters are read-only on the device).
+#pragma once
+
+#include <array>
+#include <string>
+#include <vector>
+
+namespace mw {
+
+enum class JType : int { Revolute = 0, Prismatic = 1 };
+
+struct ChainBody {
+    std::string joint_name;
+    std::string link_name;
+    JType type = JType::Revolute;
+    bool continuous = false;       // URDF "continuous": revolute without limits
+    bool limited = false;          // position limits enforced
+    std::array<double, 9> E{};     // joint origin rotation in parent body frame
+    std::array<double, 3> r{};     // joint origin translation in parent body frame
+    std::array<double, 3> axis{};  // unit axis in the child (joint) frame
+    double mass = 0.0;
+    std::array<double, 3> com{};   // in body frame
+    std::array<double, 6> Ic{};    // about COM: xx yy zz xy xz yz
+    double damping = 0.0, friction = 0.0;
+    double lower = -1e300, upper = 1e300;
+    double effort = 1e300, vel_limit = 1e300;
+};
+
+struct ChainModel {
+    std::string name;              // robot name
+    std::string base_link;         // canonical (base) link
+    std::array<double, 9> base_R{};  // base pose in world
+    std::array<double, 3> base_p{};
+    std::vector<ChainBody> bodies; // bodies[i].parent == i-1 (-1 = base)
+    int dofs() const { return static_cast<int>(bodies.size()); }
+};
+
+// Parse a URDF file path or inline URDF string.  pose = {x,y,z,qw,qx,qy,qz}.
+// Throws std::runtime_error with a message on unsupported / malformed input.
+ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]);
+
+}  // namespace mw

@@ -1,0 +1,748 @@
+// sim.cpp -- C ABI (include/mwstep.h) of the many-worlds stepper.
+//
+// Host-side counterpart of the reference's GazeboSimulator + ECM components
+// (cpp/scenario/gazebo/src/GazeboSimulator.cpp, Joint.cpp, Model.cpp):
+// component reads/writes become reads/writes of a host mirror of the device
+// SoA arrays; one run() = [one H2D copy of the command slab if dirty] +
+// one kernel + one D2H copy of the readback slab.
+#include "mwstep.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "chain_params.hpp"
+#include "kernels.hpp"
+#include "model.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define MW_HIP(call)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(MW_EHIP, std::string(#call " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+}  // namespace
+
+struct mw_sim {
+    mw_config cfg{};
+    bool own_stream = false;
+    hipStream_t stream = nullptr;
+    bool loaded = false;
+    bool initialized = false;
+    bool stepped = false;     // model parameters become read-only after the first run
+    bool servo_used = false;  // a joint was put in VelocityFollowerDart
+    bool host_stale = false;  // device state changed by the VecEnv path
+    bool cmd_dirty = true;
+    mw::ChainModel model;
+    std::string model_name;
+    double gravity[3] = {0.0, 0.0, -9.8};  // sdformat default world gravity
+    int64_t iterations = 0;
+    int64_t dt_ns = 0;
+
+    int n = 0, W = 0;
+    size_t nw = 0;  // n * W
+    // device block layout: [q qd qdd | cmd vtgt rq rqd | act rflag]; the host
+    // mirror has the same layout so the command slab moves in one copy
+    void* d_block = nullptr;
+    uint8_t* h_block = nullptr;
+    size_t block_bytes = 0, cmd_off = 0, cmd_bytes = 0, state_bytes = 0;
+    mw::ChainF* d_params = nullptr;
+    mw::ChainF h_params{};
+    mw::SimDev dev;
+    // host-only component data
+    std::vector<int32_t> mode;      // JointControlMode per [d][w]
+    std::vector<double> ptgt;       // JointPositionTarget
+    std::vector<double> cmd64;      // JointForceCmd exactly as set (double)
+
+    float* hq() { return reinterpret_cast<float*>(h_block); }
+    float* hqd() { return hq() + nw; }
+    float* hqdd() { return hq() + 2 * nw; }
+    float* hcmd() { return hq() + 3 * nw; }
+    float* hvt() { return hq() + 4 * nw; }
+    float* hrq() { return hq() + 5 * nw; }
+    float* hrqd() { return hq() + 6 * nw; }
+    uint8_t* hact() { return h_block + 7 * nw * sizeof(float); }
+    uint8_t* hrflag() { return hact() + nw; }
+    size_t idx(int d, int w) const { return static_cast<size_t>(d) * W + w; }
+};
+
+struct mw_vecenv {
+    mw_sim* sim = nullptr;
+    mw_task_config cfg{};
+    mw::TaskF task{};
+    mw::VecDev dev{};
+    void* d_counters = nullptr;
+};
+
+namespace {
+
+int check_sim(const mw_sim* s, bool need_init = true) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    if (need_init && !s->initialized) return fail(MW_ESTATE, "the simulator was not initialized");
+    return MW_OK;
+}
+
+void build_params(mw_sim* s) {
+    mw::ChainF& P = s->h_params;
+    std::memset(&P, 0, sizeof(P));
+    P.n = s->n;
+    // gravity in the base frame: R_base^T g
+    const auto& R = s->model.base_R;
+    for (int k = 0; k < 3; ++k)
+        P.g[k] = static_cast<float>(R[k] * s->gravity[0] + R[3 + k] * s->gravity[1] + R[6 + k] * s->gravity[2]);
+    int flags = 0;
+    for (int i = 0; i < s->n; ++i) {
+        const mw::ChainBody& b = s->model.bodies[i];
+        mw::BodyF& f = P.b[i];
+        for (int k = 0; k < 9; ++k) f.E[k] = static_cast<float>(b.E[k]);
+        for (int k = 0; k < 3; ++k) {
+            f.r[k] = static_cast<float>(b.r[k]);
+            f.axis[k] = static_cast<float>(b.axis[k]);
+            f.com[k] = static_cast<float>(b.com[k]);
+            f.Ea[k] = static_cast<float>(b.E[k * 3] * b.axis[0] + b.E[k * 3 + 1] * b.axis[1] +
+                                         b.E[k * 3 + 2] * b.axis[2]);
+        }
+        f.jtype = (b.type == mw::JType::Prismatic) ? 1 : 0;
+        f.mass = static_cast<float>(b.mass);
+        // inertia about the body origin: Ic + m (|c|^2 1 - c c^T)
+        const double c2 = b.com[0] * b.com[0] + b.com[1] * b.com[1] + b.com[2] * b.com[2];
+        f.Io[0] = static_cast<float>(b.Ic[0] + b.mass * (c2 - b.com[0] * b.com[0]));
+        f.Io[1] = static_cast<float>(b.Ic[1] + b.mass * (c2 - b.com[1] * b.com[1]));
+        f.Io[2] = static_cast<float>(b.Ic[2] + b.mass * (c2 - b.com[2] * b.com[2]));
+        f.Io[3] = static_cast<float>(b.Ic[3] - b.mass * b.com[0] * b.com[1]);
+        f.Io[4] = static_cast<float>(b.Ic[4] - b.mass * b.com[0] * b.com[2]);
+        f.Io[5] = static_cast<float>(b.Ic[5] - b.mass * b.com[1] * b.com[2]);
+        f.damping = static_cast<float>(b.damping);
+        f.friction = static_cast<float>(b.friction);
+        auto clampf = [](double v) {
+            const double big = static_cast<double>(std::numeric_limits<float>::max());
+            return static_cast<float>(v > big ? INFINITY : (v < -big ? -INFINITY : v));
+        };
+        f.lower = clampf(b.lower);
+        f.upper = clampf(b.upper);
+        f.effort = clampf(b.effort);
+        f.vel_limit = clampf(b.vel_limit);
+        f.limited = b.limited ? 1 : 0;
+        if (b.damping != 0.0) flags |= mw::kHasDamping;
+        if (b.limited) flags |= mw::kHasLimits;
+        if (b.friction != 0.0) flags |= mw::kHasFriction;
+    }
+    P.flags = flags;
+}
+
+int upload_params(mw_sim* s) {
+    build_params(s);
+    MW_HIP(hipMemcpyAsync(s->d_params, &s->h_params, sizeof(mw::ChainF), hipMemcpyHostToDevice, s->stream));
+    return MW_OK;
+}
+
+bool needs_cons(const mw_sim* s) {
+    return (s->h_params.flags & (mw::kHasLimits | mw::kHasFriction)) != 0 || s->servo_used;
+}
+bool needs_dual(const mw_sim* s) { return (s->h_params.flags & mw::kHasDamping) != 0; }
+
+int pull_state(mw_sim* s) {
+    if (!s->host_stale) return MW_OK;
+    MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    s->host_stale = false;
+    return MW_OK;
+}
+
+// resolve a (dofs, ndofs) selection; dofs == NULL -> all dofs
+int selection(const mw_sim* s, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs,
+              std::vector<int32_t>& out) {
+    if (w0 < 0 || nw < 0 || w0 + nw > s->W)
+        return fail(MW_EINVAL, "world range [" + std::to_string(w0) + ", " + std::to_string(w0 + nw) +
+                                   ") out of [0, " + std::to_string(s->W) + ")");
+    out.clear();
+    if (!dofs) {
+        for (int d = 0; d < s->n; ++d) out.push_back(d);
+        return MW_OK;
+    }
+    for (int k = 0; k < ndofs; ++k) {
+        if (dofs[k] < 0 || dofs[k] >= s->n)
+            return fail(MW_EINVAL, "dof index " + std::to_string(dofs[k]) + " out of range");
+        out.push_back(dofs[k]);
+    }
+    return MW_OK;
+}
+
+template <typename Get>
+int getter(mw_sim* s, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out, Get get) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    std::vector<int32_t> sel;
+    if ((rc = selection(s, w0, nw, dofs, ndofs, sel))) return rc;
+    if ((rc = pull_state(s))) return rc;
+    const size_t m = sel.size();
+    for (int32_t w = 0; w < nw; ++w)
+        for (size_t k = 0; k < m; ++k) out[w * m + k] = get(sel[k], w0 + w);
+    return MW_OK;
+}
+
+template <typename Set>
+int setter(mw_sim* s, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, const double* v, Set set) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    std::vector<int32_t> sel;
+    if ((rc = selection(s, w0, nw, dofs, ndofs, sel))) return rc;
+    const size_t m = sel.size();
+    // validate everything first: a failing call changes nothing
+    for (int32_t w = 0; w < nw; ++w)
+        for (size_t k = 0; k < m; ++k)
+            if ((rc = set(sel[k], w0 + w, v[w * m + k], /*dry_run=*/true))) return rc;
+    for (int32_t w = 0; w < nw; ++w)
+        for (size_t k = 0; k < m; ++k) set(sel[k], w0 + w, v[w * m + k], false);
+    s->cmd_dirty = true;
+    return MW_OK;
+}
+
+int copy_str(const std::string& v, char* buf, int32_t len) {
+    if (!buf || len <= 0) return fail(MW_EINVAL, "invalid output buffer");
+    if (static_cast<int32_t>(v.size()) + 1 > len) return fail(MW_EINVAL, "output buffer too small");
+    std::memcpy(buf, v.c_str(), v.size() + 1);
+    return MW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mw_last_error(void) { return g_last_error.c_str(); }
+const char* mw_version(void) { return "mwstep 0.1.0 (gfx950)"; }
+
+int mw_create(const mw_config* cfg, mw_sim** out) {
+    if (!cfg || !out) return fail(MW_EINVAL, "null argument");
+    *out = nullptr;
+    if (!(cfg->step_size > 0.0)) return fail(MW_EINVAL, "the step size must be positive");
+    if (!(cfg->rtf > 0.0)) return fail(MW_EINVAL, "the real-time factor must be positive");
+    if (cfg->steps_per_run <= 0) return fail(MW_EINVAL, "steps_per_run must be positive");
+    if (cfg->n_worlds <= 0) return fail(MW_EINVAL, "n_worlds must be positive");
+    auto s = std::make_unique<mw_sim>();
+    s->cfg = *cfg;
+    if (s->cfg.pgs_iters <= 0) s->cfg.pgs_iters = 20;
+    s->W = cfg->n_worlds;
+    s->dt_ns = static_cast<int64_t>(std::llround(cfg->step_size * 1e9));
+    *out = s.release();
+    return MW_OK;
+}
+
+void mw_destroy(mw_sim* s) {
+    if (!s) return;
+    if (s->initialized) {
+        (void)hipSetDevice(s->cfg.device);
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        (void)hipFree(s->d_block);
+        (void)hipFree(s->d_params);
+        (void)hipHostFree(s->h_block);
+        if (s->own_stream) (void)hipStreamDestroy(s->stream);
+    }
+    delete s;
+}
+
+int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char* name) {
+    if (!s || !urdf) return fail(MW_EINVAL, "null argument");
+    if (s->initialized) return fail(MW_ESTATE, "models must be loaded before mw_initialize");
+    const double ident[7] = {0, 0, 0, 1, 0, 0, 0};
+    try {
+        s->model = mw::compile_urdf(urdf, pose ? pose : ident);
+    } catch (const std::exception& e) {
+        return fail(MW_EPARSE, e.what());
+    }
+    if (s->model.dofs() > mw::kMaxKernelDofs || s->model.dofs() > 9)
+        return fail(MW_EPARSE, "chains with more than 9 dofs are not supported by this build");
+    s->model_name = (name && *name) ? name : s->model.name;
+    s->loaded = true;
+    return MW_OK;
+}
+
+int mw_initialize(mw_sim* s) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    if (s->initialized) return MW_OK;
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    MW_HIP(hipSetDevice(s->cfg.device));
+    if (!s->stream) {
+        MW_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        s->own_stream = true;
+    }
+    s->n = s->model.dofs();
+    s->nw = static_cast<size_t>(s->n) * s->W;
+    s->state_bytes = 3 * s->nw * sizeof(float);
+    s->cmd_off = s->state_bytes;
+    s->cmd_bytes = 4 * s->nw * sizeof(float) + 2 * s->nw;
+    s->block_bytes = s->state_bytes + s->cmd_bytes;
+    MW_HIP(hipMalloc(&s->d_block, s->block_bytes));
+    MW_HIP(hipMalloc(&s->d_params, sizeof(mw::ChainF)));
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_block), s->block_bytes, hipHostMallocDefault));
+    std::memset(s->h_block, 0, s->block_bytes);
+    float* base = reinterpret_cast<float*>(s->d_block);
+    s->dev.q = base;
+    s->dev.qd = base + s->nw;
+    s->dev.qdd = base + 2 * s->nw;
+    s->dev.cmd = base + 3 * s->nw;
+    s->dev.vtgt = base + 4 * s->nw;
+    s->dev.rq = base + 5 * s->nw;
+    s->dev.rqd = base + 6 * s->nw;
+    s->dev.act = reinterpret_cast<uint8_t*>(base + 7 * s->nw);
+    s->dev.rflag = s->dev.act + s->nw;
+    s->mode.assign(s->nw, MW_MODE_IDLE);
+    s->ptgt.assign(s->nw, 0.0);
+    s->cmd64.assign(s->nw, 0.0);
+    s->initialized = true;
+    int rc = upload_params(s);
+    if (rc) return rc;
+    MW_HIP(hipMemcpyAsync(s->d_block, s->h_block, s->block_bytes, hipMemcpyHostToDevice, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    s->cmd_dirty = false;
+    return MW_OK;
+}
+
+int mw_initialized(const mw_sim* s) { return (s && s->initialized) ? 1 : 0; }
+
+int mw_set_stream(mw_sim* s, void* stream) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    if (s->initialized && s->stream) MW_HIP(hipStreamSynchronize(s->stream));
+    if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+    s->stream = static_cast<hipStream_t>(stream);
+    s->own_stream = false;
+    return MW_OK;
+}
+
+int mw_run(mw_sim* s, int paused) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if ((rc = pull_state(s))) return rc;
+    if (s->cmd_dirty) {
+        MW_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_block) + s->cmd_off, s->h_block + s->cmd_off,
+                              s->cmd_bytes, hipMemcpyHostToDevice, s->stream));
+        s->cmd_dirty = false;
+    }
+    MW_HIP(mw::launch_scenario_run(s->d_params, s->n, needs_cons(s), needs_dual(s), s->dev, s->W,
+                                   static_cast<float>(s->cfg.step_size), s->cfg.steps_per_run,
+                                   paused ? 1 : 0, s->cfg.pgs_iters, s->stream));
+    MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    // mirror the kernel's component semantics on the host copy
+    std::memset(s->hcmd(), 0, s->nw * sizeof(float));
+    std::memset(s->hrflag(), 0, s->nw);
+    std::fill(s->cmd64.begin(), s->cmd64.end(), 0.0);
+    if (!paused) {
+        s->iterations += s->cfg.steps_per_run;
+        s->stepped = true;
+    }
+    return MW_OK;
+}
+
+int mw_time(const mw_sim* s, double* t) {
+    if (!s || !t) return fail(MW_EINVAL, "null argument");
+    *t = static_cast<double>(s->iterations * s->dt_ns) / 1e9;
+    return MW_OK;
+}
+
+int mw_set_gravity(mw_sim* s, const double g[3]) {
+    if (!s || !g) return fail(MW_EINVAL, "null argument");
+    if (s->stepped) return fail(MW_ESTATE, "the gravity can be changed only before the first run");
+    std::memcpy(s->gravity, g, sizeof(s->gravity));
+    if (s->initialized) return upload_params(s);
+    return MW_OK;
+}
+
+int mw_gravity(const mw_sim* s, double g[3]) {
+    if (!s || !g) return fail(MW_EINVAL, "null argument");
+    std::memcpy(g, s->gravity, sizeof(s->gravity));
+    return MW_OK;
+}
+
+int mw_n_worlds(const mw_sim* s, int32_t* n) {
+    if (!s || !n) return fail(MW_EINVAL, "null argument");
+    *n = s->W;
+    return MW_OK;
+}
+
+int mw_dofs(const mw_sim* s, int32_t* n) {
+    if (!s || !n) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    *n = s->model.dofs();
+    return MW_OK;
+}
+
+int mw_joint_name(const mw_sim* s, int32_t dof, char* buf, int32_t len) {
+    if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
+    return copy_str(s->model.bodies[dof].joint_name, buf, len);
+}
+
+int mw_joint_index(const mw_sim* s, const char* name, int32_t* dof) {
+    if (!s || !name || !dof) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    for (int i = 0; i < s->model.dofs(); ++i)
+        if (s->model.bodies[i].joint_name == name) {
+            *dof = i;
+            return MW_OK;
+        }
+    return fail(MW_ENOTFOUND, std::string("joint '") + name + "' not found");
+}
+
+int mw_joint_type(const mw_sim* s, int32_t dof, int32_t* type) {
+    if (!s || !type) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
+    *type = (s->model.bodies[dof].type == mw::JType::Prismatic) ? MW_JOINT_PRISMATIC : MW_JOINT_REVOLUTE;
+    return MW_OK;
+}
+
+int mw_model_name(const mw_sim* s, char* buf, int32_t len) {
+    if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
+    return copy_str(s->model_name, buf, len);
+}
+
+int mw_base_frame(const mw_sim* s, char* buf, int32_t len) {
+    if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
+    return copy_str(s->model.base_link, buf, len);
+}
+
+int mw_set_joint_param(mw_sim* s, int32_t dof, int32_t which, double value) {
+    if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
+    // Joint.cpp:262-266: parameters can change only while the model was just created
+    if (s->stepped) return fail(MW_ESTATE, "The model has been already processed and its parameters cannot be modified");
+    mw::ChainBody& b = s->model.bodies[dof];
+    switch (which) {
+    case MW_PARAM_COULOMB_FRICTION: b.friction = value; break;
+    case MW_PARAM_VISCOUS_FRICTION: b.damping = value; break;
+    case MW_PARAM_MAX_GENERALIZED_FORCE: b.effort = value; break;
+    case MW_PARAM_POSITION_LIMIT_MIN: b.lower = value; break;
+    case MW_PARAM_POSITION_LIMIT_MAX: b.upper = value; break;
+    default: return fail(MW_EINVAL, "unknown joint parameter");
+    }
+    if (s->initialized) return upload_params(s);
+    return MW_OK;
+}
+
+int mw_joint_param(const mw_sim* s, int32_t dof, int32_t which, double* value) {
+    if (!s || !value) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
+    const mw::ChainBody& b = s->model.bodies[dof];
+    switch (which) {
+    case MW_PARAM_COULOMB_FRICTION: *value = b.friction; break;
+    case MW_PARAM_VISCOUS_FRICTION: *value = b.damping; break;
+    case MW_PARAM_MAX_GENERALIZED_FORCE: *value = b.effort; break;
+    case MW_PARAM_POSITION_LIMIT_MIN: *value = b.lower; break;
+    case MW_PARAM_POSITION_LIMIT_MAX: *value = b.upper; break;
+    default: return fail(MW_EINVAL, "unknown joint parameter");
+    }
+    return MW_OK;
+}
+
+int mw_model_export(const mw_sim* s, double* out, int32_t len) {
+    if (!s || !out) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    const int n = s->model.dofs();
+    if (len < 33 * n + 3) return fail(MW_EINVAL, "export buffer too small");
+    double* o = out;
+    for (const mw::ChainBody& b : s->model.bodies) {
+        *o++ = (b.type == mw::JType::Prismatic) ? 1.0 : 0.0;
+        *o++ = b.limited ? 1.0 : 0.0;
+        for (double v : b.E) *o++ = v;
+        for (double v : b.r) *o++ = v;
+        for (double v : b.axis) *o++ = v;
+        *o++ = b.mass;
+        for (double v : b.com) *o++ = v;
+        for (double v : b.Ic) *o++ = v;
+        *o++ = b.damping;
+        *o++ = b.friction;
+        *o++ = b.lower;
+        *o++ = b.upper;
+        *o++ = b.effort;
+        *o++ = b.vel_limit;
+    }
+    const auto& R = s->model.base_R;
+    for (int k = 0; k < 3; ++k) *o++ = R[k] * s->gravity[0] + R[3 + k] * s->gravity[1] + R[6 + k] * s->gravity[2];
+    return MW_OK;
+}
+
+int mw_get_joint_positions(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return double(s->hq()[s->idx(dof, w)]); });
+}
+int mw_get_joint_velocities(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return double(s->hqd()[s->idx(dof, w)]); });
+}
+int mw_get_joint_accelerations(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return double(s->hqdd()[s->idx(dof, w)]); });
+}
+int mw_get_joint_forces(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    // DART clears the joint forces at the end of World::step (clearInternalForces),
+    // so GetForce -- the JointForce component readback, Physics.cpp:2330-2345 -- is 0
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [](int, int) { return 0.0; });
+}
+int mw_get_joint_force_targets(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return s->cmd64[s->idx(dof, w)]; });
+}
+int mw_get_joint_velocity_targets(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return double(s->hvt()[s->idx(dof, w)]); });
+}
+int mw_get_joint_position_targets(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return s->ptgt[s->idx(dof, w)]; });
+}
+
+int mw_set_joint_force_targets(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
+    // Joint::setGeneralizedForceTarget, Joint.cpp:774-815: allowed in Force,
+    // Position, PositionInterpolated and Velocity modes
+    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+        const int m = s->mode[s->idx(dof, w)];
+        if (m != MW_MODE_FORCE && m != MW_MODE_POSITION && m != MW_MODE_POSITION_INTERPOLATED &&
+            m != MW_MODE_VELOCITY)
+            return fail(MW_ESTATE, "The active joint control mode does not accept a force target");
+        if (!dry) {
+            s->cmd64[s->idx(dof, w)] = x;
+            s->hcmd()[s->idx(dof, w)] = static_cast<float>(x);
+        }
+        return MW_OK;
+    });
+}
+
+int mw_set_joint_velocity_targets(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
+    // Joint::setVelocityTarget, Joint.cpp:728-754
+    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+        const int m = s->mode[s->idx(dof, w)];
+        if (m != MW_MODE_VELOCITY && m != MW_MODE_VELOCITY_FOLLOWER_DART && m != MW_MODE_FORCE)
+            return fail(MW_ESTATE, "The active joint control mode does not accept a velocity target");
+        if (!dry) s->hvt()[s->idx(dof, w)] = static_cast<float>(x);
+        return MW_OK;
+    });
+}
+
+int mw_set_joint_position_targets(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
+    // Joint::setPositionTarget, Joint.cpp:694-726
+    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+        const int m = s->mode[s->idx(dof, w)];
+        if (m != MW_MODE_POSITION && m != MW_MODE_POSITION_INTERPOLATED && m != MW_MODE_IDLE &&
+            m != MW_MODE_FORCE)
+            return fail(MW_ESTATE, "The active joint control mode does not accept a position target");
+        if (!dry) s->ptgt[s->idx(dof, w)] = x;
+        return MW_OK;
+    });
+}
+
+int mw_reset_joint_positions(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
+    // Joint::resetPosition writes JointPositionReset, applied by the next run (Joint.cpp:132-156)
+    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+        if (!dry) {
+            s->hrq()[s->idx(dof, w)] = static_cast<float>(x);
+            s->hrflag()[s->idx(dof, w)] |= 1u;
+        }
+        return MW_OK;
+    });
+}
+
+int mw_reset_joint_velocities(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
+    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+        if (!dry) {
+            s->hrqd()[s->idx(dof, w)] = static_cast<float>(x);
+            s->hrflag()[s->idx(dof, w)] |= 2u;
+        }
+        return MW_OK;
+    });
+}
+
+int mw_set_joint_control_mode(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, int32_t mode) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    // Joint::setControlMode, Joint.cpp:367-460
+    if (mode == MW_MODE_POSITION_INTERPOLATED) return fail(MW_EINVAL, "PositionInterpolated not yet supported");
+    if (mode == MW_MODE_POSITION || mode == MW_MODE_VELOCITY)
+        return fail(MW_EINVAL, "PID control modes (Position / Velocity) are not supported by this build yet");
+    if (mode != MW_MODE_IDLE && mode != MW_MODE_FORCE && mode != MW_MODE_VELOCITY_FOLLOWER_DART)
+        return fail(MW_EINVAL, "You cannot set the Invalid control mode");
+    std::vector<int32_t> sel;
+    if ((rc = selection(s, w0, nw, d, nd, sel))) return rc;
+    if ((rc = pull_state(s))) return rc;
+    for (int32_t w = w0; w < w0 + nw; ++w)
+        for (int32_t dof : sel) {
+            const size_t i = s->idx(dof, w);
+            s->mode[i] = mode;
+            // targets are deleted and re-initialised from the current state
+            s->hcmd()[i] = 0.f;
+            s->cmd64[i] = 0.0;
+            s->hvt()[i] = (mode == MW_MODE_VELOCITY_FOLLOWER_DART) ? s->hqd()[i] : 0.f;
+            s->ptgt[i] = s->hq()[i];
+            s->hact()[i] = (mode == MW_MODE_VELOCITY_FOLLOWER_DART) ? mw::kActServo : mw::kActForce;
+        }
+    if (mode == MW_MODE_VELOCITY_FOLLOWER_DART) s->servo_used = true;
+    s->cmd_dirty = true;
+    return MW_OK;
+}
+
+int mw_joint_control_mode(const mw_sim* s, int32_t w, int32_t dof, int32_t* mode) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!mode) return fail(MW_EINVAL, "null argument");
+    if (w < 0 || w >= s->W || dof < 0 || dof >= s->n) return fail(MW_EINVAL, "index out of range");
+    *mode = s->mode[s->idx(dof, w)];
+    return MW_OK;
+}
+
+int mw_device_ptr(mw_sim* s, const char* field, void** dptr, int64_t* stride) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!field || !dptr) return fail(MW_EINVAL, "null argument");
+    const std::string f(field);
+    if (f == "q") *dptr = s->dev.q;
+    else if (f == "qd") *dptr = s->dev.qd;
+    else if (f == "qdd") *dptr = s->dev.qdd;
+    else return fail(MW_ENOTFOUND, "unknown field '" + f + "'");
+    if (stride) *stride = s->W;
+    s->host_stale = true;  // the caller may write through the view
+    return MW_OK;
+}
+
+int mw_copy_state(mw_sim* s, float* q, float* qd, int to_sim) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!q || !qd) return fail(MW_EINVAL, "null argument");
+    const size_t bytes = s->nw * sizeof(float);
+    if (to_sim) {
+        MW_HIP(hipMemcpyAsync(s->dev.q, q, bytes, hipMemcpyDeviceToDevice, s->stream));
+        MW_HIP(hipMemcpyAsync(s->dev.qd, qd, bytes, hipMemcpyDeviceToDevice, s->stream));
+        s->host_stale = true;
+    } else {
+        MW_HIP(hipMemcpyAsync(q, s->dev.q, bytes, hipMemcpyDeviceToDevice, s->stream));
+        MW_HIP(hipMemcpyAsync(qd, s->dev.qd, bytes, hipMemcpyDeviceToDevice, s->stream));
+    }
+    return MW_OK;
+}
+
+// ------------------------------------------------------------- VecEnv ----
+
+int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!cfg || !out) return fail(MW_EINVAL, "null argument");
+    *out = nullptr;
+    const int n = s->n;
+    const bool cart = cfg->kind >= MW_TASK_CARTPOLE_DISCRETE && cfg->kind <= MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP;
+    if (cart && n != 2) return fail(MW_EINVAL, "CartPole tasks need the 2-dof cartpole model");
+    if (cfg->kind == MW_TASK_PENDULUM_SWINGUP && n != 1) return fail(MW_EINVAL, "PendulumSwingUp needs the 1-dof pendulum model");
+    if (!cart && cfg->kind != MW_TASK_PENDULUM_SWINGUP) return fail(MW_EINVAL, "unknown task kind");
+    auto e = std::make_unique<mw_vecenv>();
+    e->sim = s;
+    e->cfg = *cfg;
+    mw::TaskF& T = e->task;
+    T.kind = cfg->kind;
+    T.max_steps = cfg->max_episode_steps;
+    T.reward_cart_at_center = cfg->reward_cart_at_center;
+    T.n_obs = (cfg->kind == MW_TASK_PENDULUM_SWINGUP) ? 3 : 4;
+    T.seed_lo = static_cast<uint32_t>(cfg->seed);
+    T.seed_hi = static_cast<uint32_t>(cfg->seed >> 32);
+    if (cfg->world_offset < 0) return fail(MW_EINVAL, "world_offset must be >= 0");
+    T.world_offset = static_cast<uint32_t>(cfg->world_offset);
+    T.force_mag = 20.0f;  // cartpole_discrete_balancing.py:32
+    const double pi = 3.14159265358979323846;
+    switch (cfg->kind) {
+    case MW_TASK_CARTPOLE_DISCRETE:
+    case MW_TASK_CARTPOLE_CONTINUOUS_BALANCING:
+        T.x_factor = (cfg->kind == MW_TASK_CARTPOLE_DISCRETE) ? 0.9f : 1.0f;
+        T.hi[0] = 2.4f; T.hi[1] = 20.0f;
+        T.hi[2] = static_cast<float>(12.0 * pi / 180.0);
+        T.hi[3] = static_cast<float>(3.0 * 360.0 * pi / 180.0);
+        break;
+    case MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP:
+        T.x_factor = 0.8f;
+        T.hi[0] = 2.4f; T.hi[1] = 20.0f;
+        T.hi[2] = static_cast<float>(5.0 * 360.0 * pi / 180.0);
+        T.hi[3] = static_cast<float>(3.0 * 360.0 * pi / 180.0);
+        break;
+    case MW_TASK_PENDULUM_SWINGUP:
+        T.x_factor = 0.f;
+        T.hi[0] = 1.f; T.hi[1] = 1.f; T.hi[2] = 10.f; T.hi[3] = 0.f;
+        break;
+    }
+    MW_HIP(hipSetDevice(s->cfg.device));
+    MW_HIP(hipMalloc(&e->d_counters, 2 * static_cast<size_t>(s->W) * sizeof(uint32_t)));
+    MW_HIP(hipMemsetAsync(e->d_counters, 0, 2 * static_cast<size_t>(s->W) * sizeof(uint32_t), s->stream));
+    e->dev.episode = static_cast<uint32_t*>(e->d_counters);
+    e->dev.steps = e->dev.episode + s->W;
+    *out = e.release();
+    return MW_OK;
+}
+
+void mw_vecenv_destroy(mw_vecenv* e) {
+    if (!e) return;
+    if (e->sim && e->sim->stream) (void)hipStreamSynchronize(e->sim->stream);
+    (void)hipFree(e->d_counters);
+    delete e;
+}
+
+int mw_vecenv_obs_dim(const mw_vecenv* e, int32_t* n) {
+    if (!e || !n) return fail(MW_EINVAL, "null argument");
+    *n = e->task.n_obs;
+    return MW_OK;
+}
+
+int mw_vecenv_reset(mw_vecenv* e, float* obs) {
+    if (!e || !obs) return fail(MW_EINVAL, "null argument");
+    mw_sim* s = e->sim;
+    MW_HIP(mw::launch_vecenv_reset(s->d_params, s->n, e->task, s->dev, e->dev, obs, s->W, s->stream));
+    s->host_stale = true;
+    return MW_OK;
+}
+
+static int vec_common(mw_vecenv* e, int32_t T, const void* a, float* o, float* r, uint8_t* d, float* to) {
+    if (!e || !a || !o || !r || !d || !to) return fail(MW_EINVAL, "null argument");
+    if (e->task.n_obs == 4 &&
+        ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(to)) & 15u))
+        return fail(MW_EINVAL, "obs buffers must be 16-byte aligned");
+    mw_sim* s = e->sim;
+    MW_HIP(mw::launch_vecenv_step(s->d_params, s->n, needs_cons(s), needs_dual(s), e->task, s->dev, e->dev,
+                                  a, o, r, d, to, s->W, static_cast<float>(s->cfg.step_size),
+                                  s->cfg.steps_per_run, s->cfg.pgs_iters, T, s->stream));
+    s->host_stale = true;
+    s->iterations += static_cast<int64_t>(s->cfg.steps_per_run) * (T > 0 ? T : 1);
+    s->stepped = true;
+    return MW_OK;
+}
+
+int mw_vecenv_step(mw_vecenv* e, const void* a, float* o, float* r, uint8_t* d, float* to) {
+    return vec_common(e, 0, a, o, r, d, to);
+}
+
+int mw_vecenv_rollout(mw_vecenv* e, int32_t T, const void* a, float* o, float* r, uint8_t* d, float* to) {
+    if (T <= 0) return fail(MW_EINVAL, "T must be positive");
+    return vec_common(e, T, a, o, r, d, to);
+}
+
+int mw_vecenv_counters(mw_vecenv* e, uint32_t* episode, uint32_t* steps) {
+    if (!e || !episode || !steps) return fail(MW_EINVAL, "null argument");
+    const size_t bytes = static_cast<size_t>(e->sim->W) * sizeof(uint32_t);
+    MW_HIP(hipMemcpyAsync(episode, e->dev.episode, bytes, hipMemcpyDeviceToDevice, e->sim->stream));
+    MW_HIP(hipMemcpyAsync(steps, e->dev.steps, bytes, hipMemcpyDeviceToDevice, e->sim->stream));
+    return MW_OK;
+}
+
+}  // extern "C"

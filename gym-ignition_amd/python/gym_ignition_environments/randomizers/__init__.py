@@ -1,0 +1,1 @@
+from . import cartpole_no_rand, pendulum_no_rand  # noqa: F401

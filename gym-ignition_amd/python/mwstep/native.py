@@ -1,0 +1,151 @@
+"""ctypes binding of ``libmwstep.so`` (the C ABI declared in ``include/mwstep.h``).
+
+The library is built in-tree by ``make -C gym-ignition_amd`` (hipcc, gfx950).
+There is no CPU fallback: if the shared object is missing, importing the
+product raises immediately, and every compute entry point reports HIP errors
+as ``RuntimeError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.environ.get("MWSTEP_LIB", os.path.join(_PKG_ROOT, "libmwstep.so"))
+
+MW_OK = 0
+MW_EINVAL, MW_ESTATE, MW_EPARSE, MW_EHIP, MW_ENOTFOUND = 1, 2, 3, 4, 5
+
+MODE_INVALID, MODE_IDLE, MODE_FORCE, MODE_VELOCITY = 0, 1, 2, 3
+MODE_VELOCITY_FOLLOWER_DART, MODE_POSITION, MODE_POSITION_INTERPOLATED = 4, 5, 6
+
+JOINT_INVALID, JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_BALL = 0, 1, 2, 3, 4
+
+PARAM_COULOMB_FRICTION = 0
+PARAM_VISCOUS_FRICTION = 1
+PARAM_MAX_GENERALIZED_FORCE = 2
+PARAM_POSITION_LIMIT_MIN = 3
+PARAM_POSITION_LIMIT_MAX = 4
+
+TASK_CARTPOLE_DISCRETE = 0
+TASK_CARTPOLE_CONTINUOUS_BALANCING = 1
+TASK_CARTPOLE_CONTINUOUS_SWINGUP = 2
+TASK_PENDULUM_SWINGUP = 3
+
+
+class MwConfig(ctypes.Structure):
+    _fields_ = [
+        ("step_size", ctypes.c_double),
+        ("rtf", ctypes.c_double),
+        ("steps_per_run", ctypes.c_int32),
+        ("n_worlds", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("pgs_iters", ctypes.c_int32),
+    ]
+
+
+class MwTaskConfig(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("max_episode_steps", ctypes.c_int32),
+        ("reward_cart_at_center", ctypes.c_int32),
+        ("world_offset", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+# (name, restype, argtypes) of every symbol in include/mwstep.h
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_D = ctypes.POINTER(ctypes.c_double)
+_IP = ctypes.POINTER(ctypes.c_int32)
+_S = ctypes.c_char_p
+SIGNATURES = [
+    ("mw_last_error", ctypes.c_char_p, []),
+    ("mw_version", ctypes.c_char_p, []),
+    ("mw_create", ctypes.c_int, [ctypes.POINTER(MwConfig), ctypes.POINTER(_P)]),
+    ("mw_destroy", None, [_P]),
+    ("mw_load_model", ctypes.c_int, [_P, _S, _D, _S]),
+    ("mw_initialize", ctypes.c_int, [_P]),
+    ("mw_initialized", ctypes.c_int, [_P]),
+    ("mw_set_stream", ctypes.c_int, [_P, _P]),
+    ("mw_run", ctypes.c_int, [_P, ctypes.c_int]),
+    ("mw_time", ctypes.c_int, [_P, _D]),
+    ("mw_set_gravity", ctypes.c_int, [_P, _D]),
+    ("mw_gravity", ctypes.c_int, [_P, _D]),
+    ("mw_n_worlds", ctypes.c_int, [_P, _IP]),
+    ("mw_dofs", ctypes.c_int, [_P, _IP]),
+    ("mw_joint_name", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
+    ("mw_joint_index", ctypes.c_int, [_P, _S, _IP]),
+    ("mw_joint_type", ctypes.c_int, [_P, _I, _IP]),
+    ("mw_model_name", ctypes.c_int, [_P, ctypes.c_char_p, _I]),
+    ("mw_base_frame", ctypes.c_int, [_P, ctypes.c_char_p, _I]),
+    ("mw_set_joint_param", ctypes.c_int, [_P, _I, _I, ctypes.c_double]),
+    ("mw_joint_param", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_model_export", ctypes.c_int, [_P, _D, _I]),
+    ("mw_get_joint_positions", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_get_joint_velocities", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_get_joint_accelerations", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_get_joint_forces", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_get_joint_force_targets", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_get_joint_velocity_targets", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_get_joint_position_targets", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_set_joint_force_targets", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_set_joint_velocity_targets", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_set_joint_position_targets", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_reset_joint_positions", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_reset_joint_velocities", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
+    ("mw_set_joint_control_mode", ctypes.c_int, [_P, _I, _I, _IP, _I, _I]),
+    ("mw_joint_control_mode", ctypes.c_int, [_P, _I, _I, _IP]),
+    ("mw_device_ptr", ctypes.c_int, [_P, _S, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
+    ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    ("mw_vecenv_create", ctypes.c_int, [_P, ctypes.POINTER(MwTaskConfig), ctypes.POINTER(_P)]),
+    ("mw_vecenv_destroy", None, [_P]),
+    ("mw_vecenv_obs_dim", ctypes.c_int, [_P, _IP]),
+    ("mw_vecenv_reset", ctypes.c_int, [_P, _P]),
+    ("mw_vecenv_step", ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    ("mw_vecenv_rollout", ctypes.c_int, [_P, _I, _P, _P, _P, _P, _P]),
+    ("mw_vecenv_counters", ctypes.c_int, [_P, _P, _P]),
+]
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NativeLibraryMissing(ImportError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmwstep.so (once).  Raises NativeLibraryMissing if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build it with `make -C gym-ignition_amd` "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().mw_last_error().decode()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != MW_OK:
+        raise RuntimeError(f"{what}: {last_error()}" if what else last_error())
+
+
+def dptr(arr) -> ctypes.POINTER(ctypes.c_double):
+    return arr.ctypes.data_as(_D)
+
+
+def iptr(arr) -> ctypes.POINTER(ctypes.c_int32):
+    return None if arr is None else arr.ctypes.data_as(_IP)

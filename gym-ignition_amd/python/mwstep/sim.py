@@ -1,0 +1,176 @@
+"""Pythonic handle over one native ``mw_sim`` (many worlds, one model each)."""
+
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import native as N
+
+
+class Simulator:
+    """N parallel worlds of one articulated model on one GPU.
+
+    Mirrors ``scenario::gazebo::GazeboSimulator`` for the stepping path
+    (``/root/reference/cpp/scenario/gazebo/src/GazeboSimulator.cpp:202-251``):
+    ``run(paused)`` applies pending resets/commands, steps ``steps_per_run``
+    substeps, and refreshes the readback that the getters return.
+    """
+
+    def __init__(self, model: str, n_worlds: int = 1, step_size: float = 1e-3,
+                 steps_per_run: int = 1, rtf: float = 1.0, device: int = 0,
+                 pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "",
+                 pgs_iters: int = 20, gravity: Optional[Sequence[float]] = None,
+                 stream: Optional[int] = None, joint_params: Optional[dict] = None):
+        L = N.lib()
+        cfg = N.MwConfig(step_size, rtf, steps_per_run, n_worlds, device, pgs_iters)
+        h = ctypes.c_void_p()
+        N.check(L.mw_create(ctypes.byref(cfg), ctypes.byref(h)), "mw_create")
+        self._h = h
+        self.n_worlds = n_worlds
+        self.step_size = step_size
+        self.steps_per_run = steps_per_run
+        try:
+            p = np.ascontiguousarray(pose, dtype=np.float64)
+            N.check(L.mw_load_model(h, model.encode(), N.dptr(p), name.encode()), "mw_load_model")
+            if gravity is not None:
+                g = np.ascontiguousarray(gravity, dtype=np.float64)
+                N.check(L.mw_set_gravity(h, N.dptr(g)), "mw_set_gravity")
+            for (dof, which), value in (joint_params or {}).items():
+                N.check(L.mw_set_joint_param(h, dof, which, float(value)), "mw_set_joint_param")
+            if stream is not None:
+                N.check(L.mw_set_stream(h, ctypes.c_void_p(stream)), "mw_set_stream")
+            N.check(L.mw_initialize(h), "mw_initialize")
+        except Exception:
+            L.mw_destroy(h)
+            self._h = None
+            raise
+        n = ctypes.c_int32()
+        N.check(L.mw_dofs(h, ctypes.byref(n)))
+        self.dofs = n.value
+        buf = ctypes.create_string_buffer(256)
+        self.joint_names: List[str] = []
+        for d in range(self.dofs):
+            N.check(L.mw_joint_name(h, d, buf, 256))
+            self.joint_names.append(buf.value.decode())
+        N.check(L.mw_model_name(h, buf, 256))
+        self.model_name = buf.value.decode()
+        N.check(L.mw_base_frame(h, buf, 256))
+        self.base_frame = buf.value.decode()
+        self._index = {n_: i for i, n_ in enumerate(self.joint_names)}
+
+    # ------------------------------------------------------------------
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise RuntimeError("the simulator was closed")
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            N.lib().mw_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, paused: bool = False) -> None:
+        N.check(N.lib().mw_run(self.handle, 1 if paused else 0), "run")
+
+    def time(self) -> float:
+        t = ctypes.c_double()
+        N.check(N.lib().mw_time(self.handle, ctypes.byref(t)))
+        return t.value
+
+    def gravity(self) -> List[float]:
+        g = np.zeros(3)
+        N.check(N.lib().mw_gravity(self.handle, N.dptr(g)))
+        return g.tolist()
+
+    def set_gravity(self, g: Sequence[float]) -> None:
+        a = np.ascontiguousarray(g, dtype=np.float64)
+        N.check(N.lib().mw_set_gravity(self.handle, N.dptr(a)), "set_gravity")
+
+    # ------------------------------------------------------------------
+    def dof_indices(self, names: Optional[Sequence[str]]) -> Optional[np.ndarray]:
+        if names is None or len(names) == 0:
+            return None
+        try:
+            return np.array([self._index[n] for n in names], dtype=np.int32)
+        except KeyError as e:
+            raise RuntimeError(f"joint {e.args[0]!r} not found in model {self.model_name!r}") from None
+
+    def _get(self, fn, w0: int, nw: int, dofs: Optional[np.ndarray]) -> np.ndarray:
+        m = self.dofs if dofs is None else len(dofs)
+        out = np.zeros((nw, m))
+        N.check(fn(self.handle, w0, nw, N.iptr(dofs), 0 if dofs is None else len(dofs), N.dptr(out)))
+        return out
+
+    def _set(self, fn, w0: int, nw: int, dofs: Optional[np.ndarray], values) -> None:
+        m = self.dofs if dofs is None else len(dofs)
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.float64), (nw, m)))
+        N.check(fn(self.handle, w0, nw, N.iptr(dofs), 0 if dofs is None else len(dofs), N.dptr(v)))
+
+    def get(self, what: str, w0: int = 0, nw: Optional[int] = None, dofs=None) -> np.ndarray:
+        fn = {
+            "q": N.lib().mw_get_joint_positions,
+            "qd": N.lib().mw_get_joint_velocities,
+            "qdd": N.lib().mw_get_joint_accelerations,
+            "force": N.lib().mw_get_joint_forces,
+            "force_target": N.lib().mw_get_joint_force_targets,
+            "velocity_target": N.lib().mw_get_joint_velocity_targets,
+            "position_target": N.lib().mw_get_joint_position_targets,
+        }[what]
+        return self._get(fn, w0, self.n_worlds - w0 if nw is None else nw, dofs)
+
+    def set(self, what: str, values, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
+        fn = {
+            "force_target": N.lib().mw_set_joint_force_targets,
+            "velocity_target": N.lib().mw_set_joint_velocity_targets,
+            "position_target": N.lib().mw_set_joint_position_targets,
+            "reset_q": N.lib().mw_reset_joint_positions,
+            "reset_qd": N.lib().mw_reset_joint_velocities,
+        }[what]
+        self._set(fn, w0, self.n_worlds - w0 if nw is None else nw, dofs, values)
+
+    def set_control_mode(self, mode: int, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_set_joint_control_mode(self.handle, w0, nw, N.iptr(dofs),
+                                                  0 if dofs is None else len(dofs), mode))
+
+    def control_mode(self, w: int, dof: int) -> int:
+        m = ctypes.c_int32()
+        N.check(N.lib().mw_joint_control_mode(self.handle, w, dof, ctypes.byref(m)))
+        return m.value
+
+    def joint_type(self, dof: int) -> int:
+        t = ctypes.c_int32()
+        N.check(N.lib().mw_joint_type(self.handle, dof, ctypes.byref(t)))
+        return t.value
+
+    def set_joint_param(self, dof: int, which: int, value: float) -> None:
+        N.check(N.lib().mw_set_joint_param(self.handle, dof, which, float(value)))
+
+    def joint_param(self, dof: int, which: int) -> float:
+        v = ctypes.c_double()
+        N.check(N.lib().mw_joint_param(self.handle, dof, which, ctypes.byref(v)))
+        return v.value
+
+    def export_model(self) -> np.ndarray:
+        out = np.zeros(33 * self.dofs + 3)
+        N.check(N.lib().mw_model_export(self.handle, N.dptr(out), len(out)))
+        return out
+
+    def device_ptr(self, field: str):
+        p = ctypes.c_void_p()
+        stride = ctypes.c_int64()
+        N.check(N.lib().mw_device_ptr(self.handle, field.encode(), ctypes.byref(p), ctypes.byref(stride)))
+        return p.value, stride.value
+
+    def set_stream(self, stream: int) -> None:
+        N.check(N.lib().mw_set_stream(self.handle, ctypes.c_void_p(stream)))

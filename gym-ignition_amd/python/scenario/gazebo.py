@@ -1,0 +1,721 @@
+"""``scenario.gazebo`` -- ScenarI/O simulator API backed by the HIP stepper.
+
+Same names and return conventions as the reference's SWIG module
+(``/root/reference/bindings/gazebo/gazebo.i``): lifecycle calls and setters
+return ``bool`` and log the reason of a failure, getters raise
+``RuntimeError`` (the SWIG mapping of ``scenario::gazebo::exceptions``).
+
+Where the reference keeps entity state in an ign-gazebo ECM and steps it with
+DART on the CPU, every articulated model here owns one native simulator
+(``mwstep.Simulator``) whose state lives in HBM; ``GazeboSimulator.run()``
+steps all of them.  Component semantics that callers can observe are kept:
+
+  * resets and commands take effect on the next ``run()`` (paused or not),
+    and getters return the state refreshed by the last run
+    (``Physics.cpp:1330-1440, 2226-2345``);
+  * a joint force target is consumed by one physics step and reads back as
+    zero after the run (``Physics.cpp:2250-2254``);
+  * ``World.time()`` is the simulated time written by the physics system, so it
+    stays 0 until ``set_physics_engine`` and then follows the server iterations
+    (``Physics.cpp:656-666``; ``tests/test_scenario/test_world.py:149-219``).
+"""
+
+from __future__ import annotations
+
+import collections
+import math
+import os
+import re
+import sys
+import xml.etree.ElementTree as ET
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import core
+
+PhysicsEngine_dart = 0
+
+Verbosity_suppress_all, Verbosity_error, Verbosity_warning = 0, 1, 2
+Verbosity_info, Verbosity_debug = 3, 4
+_verbosity = Verbosity_warning
+
+
+def set_verbosity(level: int = Verbosity_warning) -> None:
+    global _verbosity
+    _verbosity = int(level)
+
+
+def _err(msg: str) -> None:
+    if _verbosity >= Verbosity_error:
+        print(f"[ERROR] {msg}", file=sys.stderr)
+
+
+def _warn(msg: str) -> None:
+    if _verbosity >= Verbosity_warning:
+        print(f"[WARNING] {msg}", file=sys.stderr)
+
+
+def _device() -> int:
+    return int(os.environ.get("MWSTEP_DEVICE", "0"))
+
+
+# ---------------------------------------------------------------- SDF helpers
+_EMPTY_WORLD = """<?xml version="1.0" ?>
+<sdf version="1.6">
+    <world name="default">
+        <physics default="true" type="dart">
+        </physics>
+    </world>
+</sdf>"""
+
+
+def get_empty_world() -> str:
+    """SDF of an empty world named "default" (utils.cpp:171-196)."""
+    return _EMPTY_WORLD
+
+
+def _read(path_or_string: str) -> str:
+    if path_or_string.lstrip().startswith("<"):
+        return path_or_string
+    with open(path_or_string) as f:
+        return f.read()
+
+
+def get_world_name_from_sdf(sdf: str, world_index: int = 0) -> str:
+    root = ET.fromstring(_read(sdf).strip())
+    worlds = root.findall("world")
+    return worlds[world_index].get("name", "") if world_index < len(worlds) else ""
+
+
+def get_model_name_from_sdf(sdf: str, model_index: int = 0) -> str:
+    root = ET.fromstring(_read(sdf).strip())
+    if root.tag == "robot":
+        return root.get("name", "")
+    models = root.findall("model")
+    return models[model_index].get("name", "") if model_index < len(models) else ""
+
+
+# ---------------------------------------------------------------------- Joint
+class Joint:
+    """One degree of freedom of an articulated model (all joints are 1-dof)."""
+
+    def __init__(self, model: "Model", dof: int, name: str):
+        self._model = model
+        self._dof = dof
+        self._name = name
+
+    # -- identity
+    def to_gazebo(self) -> "Joint":
+        return self
+
+    def valid(self) -> bool:
+        return self._model.valid()
+
+    def name(self, scoped: bool = False) -> str:
+        return f"{self._model.name()}::{self._name}" if scoped else self._name
+
+    def type(self) -> int:
+        return self._model._sim.joint_type(self._dof)
+
+    def dofs(self) -> int:
+        return 1
+
+    def _check_dof(self, dof: int) -> None:
+        if dof != 0:
+            raise RuntimeError(f"DOF mismatch: joint '{self._name}' has 1 DoF, requested #{dof}")
+
+    # -- state (refreshed by the last run)
+    def _read(self, what: str) -> float:
+        return float(self._model._get(what, [self._dof])[0])
+
+    def position(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self._read("q")
+
+    def velocity(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self._read("qd")
+
+    def acceleration(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self._read("qdd")
+
+    def generalized_force(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self._read("force")
+
+    def joint_position(self) -> List[float]:
+        return [self.position()]
+
+    def joint_velocity(self) -> List[float]:
+        return [self.velocity()]
+
+    def joint_acceleration(self) -> List[float]:
+        return [self.acceleration()]
+
+    def joint_generalized_force(self) -> List[float]:
+        return [self.generalized_force()]
+
+    # -- control
+    def control_mode(self) -> int:
+        return self._model._sim.control_mode(0, self._dof)
+
+    def set_control_mode(self, mode: int) -> bool:
+        return self._model.set_joint_control_mode(mode, [self._name])
+
+    def set_generalized_force_target(self, force: float, dof: int = 0) -> bool:
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        return self._model.set_joint_generalized_force_targets([force], [self._name])
+
+    def generalized_force_target(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return float(self._model._get("force_target", [self._dof])[0])
+
+    def set_velocity_target(self, velocity: float, dof: int = 0) -> bool:
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        return self._model.set_joint_velocity_targets([velocity], [self._name])
+
+    def velocity_target(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return float(self._model._get("velocity_target", [self._dof])[0])
+
+    def set_position_target(self, position: float, dof: int = 0) -> bool:
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        return self._model.set_joint_position_targets([position], [self._name])
+
+    def position_target(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return float(self._model._get("position_target", [self._dof])[0])
+
+    # -- resets (applied by the next run)
+    def reset_position(self, position: float, dof: int = 0) -> bool:
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        return self._model.reset_joint_positions([position], [self._name])
+
+    def reset_velocity(self, velocity: float, dof: int = 0) -> bool:
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        return self._model.reset_joint_velocities([velocity], [self._name])
+
+    def reset(self, position: float = 0.0, velocity: float = 0.0, dof: int = 0) -> bool:
+        return self.reset_position(position, dof) and self.reset_velocity(velocity, dof)
+
+    # -- parameters (only while the model was just created)
+    def _set_param(self, which: int, value: float) -> bool:
+        from mwstep import native as N
+        try:
+            self._model._sim.set_joint_param(self._dof, which, value)
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
+    def _param(self, which: int) -> float:
+        return self._model._sim.joint_param(self._dof, which)
+
+    def set_coulomb_friction(self, value: float) -> bool:
+        from mwstep import native as N
+        return self._set_param(N.PARAM_COULOMB_FRICTION, value)
+
+    def set_viscous_friction(self, value: float) -> bool:
+        from mwstep import native as N
+        return self._set_param(N.PARAM_VISCOUS_FRICTION, value)
+
+    def coulomb_friction(self) -> float:
+        from mwstep import native as N
+        return self._param(N.PARAM_COULOMB_FRICTION)
+
+    def viscous_friction(self) -> float:
+        from mwstep import native as N
+        return self._param(N.PARAM_VISCOUS_FRICTION)
+
+    def max_generalized_force(self, dof: int = 0) -> float:
+        from mwstep import native as N
+        self._check_dof(dof)
+        v = self._param(N.PARAM_MAX_GENERALIZED_FORCE)
+        return math.inf if v >= 1e299 else v
+
+    def set_max_generalized_force(self, max_force: float, dof: int = 0) -> bool:
+        from mwstep import native as N
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        return self._set_param(N.PARAM_MAX_GENERALIZED_FORCE, max_force)
+
+    def position_limit(self, dof: int = 0) -> core.Limit:
+        from mwstep import native as N
+        self._check_dof(dof)
+        lo = self._param(N.PARAM_POSITION_LIMIT_MIN)
+        hi = self._param(N.PARAM_POSITION_LIMIT_MAX)
+        return core.Limit(-math.inf if lo <= -1e299 else lo, math.inf if hi >= 1e299 else hi)
+
+    def joint_position_limit(self) -> core.Limit:
+        return self.position_limit()
+
+
+# ---------------------------------------------------------------------- Model
+class Model:
+    """An articulated model (one native simulator with a single world)."""
+
+    def __init__(self, world: "World", name: str, sim, pose: core.Pose):
+        self._world = world
+        self._name = name
+        self._sim = sim
+        self._pose = pose
+        self._joints = {n: Joint(self, i, n) for i, n in enumerate(sim.joint_names)}
+        self._period = world._simulator.step_size()
+        self._history: Optional[collections.deque] = None
+
+    # -- identity
+    def to_gazebo(self) -> "Model":
+        return self
+
+    def valid(self) -> bool:
+        return self._sim is not None
+
+    def name(self) -> str:
+        return self._name
+
+    def dofs(self, joint_names: Sequence[str] = ()) -> int:
+        return len(joint_names) if joint_names else self._sim.dofs
+
+    def joint_names(self, scoped: bool = False) -> List[str]:
+        return [f"{self._name}::{n}" if scoped else n for n in self._sim.joint_names]
+
+    def get_joint(self, joint_name: str) -> Joint:
+        if joint_name not in self._joints:
+            raise RuntimeError(f"Joint '{joint_name}' not found in model '{self._name}'")
+        return self._joints[joint_name]
+
+    def joints(self, joint_names: Sequence[str] = ()) -> List[Joint]:
+        return [self.get_joint(n) for n in (joint_names or self._sim.joint_names)]
+
+    def base_frame(self) -> str:
+        return self._sim.base_frame
+
+    def base_position(self) -> List[float]:
+        return list(self._pose.position)
+
+    def base_orientation(self) -> List[float]:
+        return list(self._pose.orientation)
+
+    def controller_period(self) -> float:
+        return self._period
+
+    def set_controller_period(self, period: float) -> bool:
+        if period <= 0:
+            _err("The controller period must be positive")
+            return False
+        self._period = float(period)
+        return True
+
+    # -- vectorised joint data (serialised in the requested name order)
+    def _dofs(self, names: Sequence[str]):
+        return self._sim.dof_indices(list(names) if names else None)
+
+    def _get(self, what: str, dof_idx) -> np.ndarray:
+        if self._sim is None:
+            raise RuntimeError(f"model '{self._name}' was removed")
+        if dof_idx is not None:
+            dof_idx = np.asarray(dof_idx, dtype=np.int32)
+        return self._sim.get(what, 0, 1, dof_idx)[0]
+
+    def joint_positions(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("q", self._dofs(joint_names)).tolist()
+
+    def joint_velocities(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("qd", self._dofs(joint_names)).tolist()
+
+    def joint_accelerations(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("qdd", self._dofs(joint_names)).tolist()
+
+    def joint_generalized_forces(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("force", self._dofs(joint_names)).tolist()
+
+    def joint_generalized_force_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("force_target", self._dofs(joint_names)).tolist()
+
+    def joint_velocity_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("velocity_target", self._dofs(joint_names)).tolist()
+
+    def joint_position_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return self._get("position_target", self._dofs(joint_names)).tolist()
+
+    def _set(self, what: str, values, joint_names: Sequence[str]) -> bool:
+        try:
+            idx = self._dofs(joint_names)
+            n = self._sim.dofs if idx is None else len(idx)
+            if len(values) != n:
+                _err(f"Wrong number of elements (joint_dofs={n})")
+                return False
+            self._sim.set(what, [list(values)], 0, 1, idx)
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
+    def set_joint_generalized_force_targets(self, forces, joint_names: Sequence[str] = ()) -> bool:
+        return self._set("force_target", forces, joint_names)
+
+    def set_joint_velocity_targets(self, velocities, joint_names: Sequence[str] = ()) -> bool:
+        return self._set("velocity_target", velocities, joint_names)
+
+    def set_joint_position_targets(self, positions, joint_names: Sequence[str] = ()) -> bool:
+        return self._set("position_target", positions, joint_names)
+
+    def reset_joint_positions(self, positions, joint_names: Sequence[str] = ()) -> bool:
+        return self._set("reset_q", positions, joint_names)
+
+    def reset_joint_velocities(self, velocities, joint_names: Sequence[str] = ()) -> bool:
+        return self._set("reset_qd", velocities, joint_names)
+
+    def set_joint_control_mode(self, mode: int, joint_names: Sequence[str] = ()) -> bool:
+        try:
+            self._sim.set_control_mode(int(mode), 0, 1, self._dofs(joint_names))
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
+    # -- history of applied joint forces (HistoryOfAppliedJointForces component)
+    def enable_history_of_applied_joint_forces(self, enable: bool = True,
+                                               max_history_size_per_joint: int = 100) -> bool:
+        if enable:
+            if self._history is None:
+                self._history = collections.deque(maxlen=max_history_size_per_joint * self.dofs())
+        else:
+            self._history = None
+        return True
+
+    def history_of_applied_joint_forces_enabled(self) -> bool:
+        return self._history is not None
+
+    def history_of_applied_joint_forces(self, joint_names: Sequence[str] = ()) -> List[float]:
+        if self._history is None:
+            return []
+        h = np.array(self._history).reshape(-1, self.dofs())
+        idx = self._dofs(joint_names)
+        return (h if idx is None else h[:, idx]).reshape(-1).tolist()
+
+    # -- stepping (called by GazeboSimulator.run)
+    def _run(self, paused: bool) -> None:
+        if self._history is not None and not paused:
+            self._history.extend(self._get("force_target", None).tolist())
+        self._sim.run(paused)
+
+    def _close(self) -> None:
+        if self._sim is not None:
+            self._sim.close()
+            self._sim = None
+
+
+class StaticModel:
+    """A model without degrees of freedom (e.g. the ground plane)."""
+
+    def __init__(self, name: str, pose: core.Pose):
+        self._name = name
+        self._pose = pose
+
+    def to_gazebo(self):
+        return self
+
+    def valid(self) -> bool:
+        return True
+
+    def name(self) -> str:
+        return self._name
+
+    def dofs(self, joint_names: Sequence[str] = ()) -> int:
+        return 0
+
+    def joint_names(self, scoped: bool = False) -> List[str]:
+        return []
+
+    def base_position(self) -> List[float]:
+        return list(self._pose.position)
+
+    def base_orientation(self) -> List[float]:
+        return list(self._pose.orientation)
+
+    def _run(self, paused: bool) -> None:
+        pass
+
+    def _close(self) -> None:
+        pass
+
+
+# ---------------------------------------------------------------------- World
+class World:
+    def __init__(self, simulator: "GazeboSimulator", name: str):
+        self._simulator = simulator
+        self._name = name
+        self._models: "collections.OrderedDict[str, object]" = collections.OrderedDict()
+        self._physics = False
+        self._time_ns = 0
+        self._gravity = [0.0, 0.0, -9.8]
+
+    def to_gazebo(self) -> "World":
+        return self
+
+    @property
+    def name(self):
+        # usable both as attribute-like `world.name` checks and as `world.name()`
+        return _NameProxy(self._name)
+
+    def time(self) -> float:
+        return self._time_ns / 1e9
+
+    def gravity(self) -> List[float]:
+        return list(self._gravity)
+
+    def set_gravity(self, gravity: Sequence[float]) -> bool:
+        if len(gravity) != 3:
+            _err("The gravity must have 3 elements")
+            return False
+        self._gravity = [float(g) for g in gravity]
+        for m in self._models.values():
+            if isinstance(m, Model):
+                try:
+                    m._sim.set_gravity(self._gravity)
+                except RuntimeError as e:
+                    _err(str(e))
+                    return False
+        return True
+
+    def model_names(self) -> List[str]:
+        return list(self._models.keys())
+
+    def get_model(self, model_name: str):
+        if model_name not in self._models:
+            raise RuntimeError(f"Model '{model_name}' not found in world '{self._name}'")
+        return self._models[model_name]
+
+    def models(self, model_names: Sequence[str] = ()) -> list:
+        return [self.get_model(n) for n in (model_names or self.model_names())]
+
+    def set_physics_engine(self, engine: int = PhysicsEngine_dart) -> bool:
+        if engine != PhysicsEngine_dart:
+            _err("Physics engine not supported")
+            return False
+        if self._physics:
+            _err("The physics engine was already inserted in this world")
+            return False
+        self._physics = True
+        return True
+
+    def insert_model(self, model_file: str, pose: core.Pose = None, override_model_name: str = "") -> bool:
+        try:
+            text = _read(model_file)
+        except OSError as e:
+            _err(f"Failed to read model file: {e}")
+            return False
+        return self.insert_model_from_string(text, pose, override_model_name)
+
+    def insert_model_from_string(self, model_string: str, pose: core.Pose = None,
+                                 override_model_name: str = "") -> bool:
+        if not self._simulator.initialized():
+            _err("The simulator was not initialized")
+            return False
+        pose = pose or core.Pose.identity()
+        try:
+            root = ET.fromstring(model_string.strip())
+        except ET.ParseError as e:
+            _err(f"Failed to parse the model: {e}")
+            return False
+        if root.tag == "robot":
+            name = override_model_name or root.get("name", "model")
+        else:
+            m = root.find("model")
+            if m is None:
+                _err("The SDF does not contain a <model>")
+                return False
+            name = override_model_name or m.get("name", "model")
+        if name in self._models:
+            _err(f"Model '{name}' already exists in world '{self._name}'")
+            return False
+        if root.tag != "robot":
+            static = (root.find("model/static") is not None and
+                      root.find("model/static").text.strip().lower() in ("1", "true"))
+            if not static or root.findall("model/joint"):
+                _err("only static SDF models and URDF robots are supported by this build")
+                return False
+            self._models[name] = StaticModel(name, pose)
+            return True
+        from mwstep.sim import Simulator
+        sim_cfg = self._simulator
+        try:
+            sim = Simulator(model_string, n_worlds=1, step_size=sim_cfg.step_size(),
+                            steps_per_run=sim_cfg.steps_per_run(), rtf=sim_cfg.real_time_factor(),
+                            device=_device(), pose=list(pose.position) + list(pose.orientation),
+                            name=name, gravity=self._gravity)
+        except RuntimeError as e:
+            _err(f"Failed to insert model '{name}': {e}")
+            return False
+        self._models[name] = Model(self, name, sim, pose)
+        return True
+
+    def remove_model(self, model_name: str) -> bool:
+        if model_name not in self._models:
+            _err(f"Model '{model_name}' not found in world '{self._name}'")
+            return False
+        self._models.pop(model_name)._close()
+        return True
+
+    # called by GazeboSimulator.run
+    def _update(self, paused: bool, sim_time_ns: int) -> None:
+        if not self._physics:
+            return
+        self._time_ns = sim_time_ns
+        for m in self._models.values():
+            m._run(paused)
+
+    def _close(self) -> None:
+        for m in self._models.values():
+            m._close()
+        self._models.clear()
+
+
+class _NameProxy(str):
+    """A str that can also be called: the reference exposes World.name() while
+    gym_ignition's Task checks ``world.name == ""``."""
+
+    def __call__(self) -> str:
+        return str(self)
+
+
+# ------------------------------------------------------------ GazeboSimulator
+class GazeboSimulator:
+    """Lifecycle of a set of worlds stepped in lockstep (GazeboSimulator.h)."""
+
+    def __init__(self, step_size: float = 0.001, rtf: float = 1.0, steps_per_run: int = 1):
+        self._step_size = float(step_size)
+        self._rtf = float(rtf)
+        self._steps_per_run = int(steps_per_run)
+        self._initialized = False
+        self._worlds: "collections.OrderedDict[str, World]" = collections.OrderedDict()
+        self._pending_worlds: List[str] = []
+        self._iterations = 0
+
+    def step_size(self) -> float:
+        return self._step_size
+
+    def real_time_factor(self) -> float:
+        return self._rtf
+
+    def steps_per_run(self) -> int:
+        return self._steps_per_run
+
+    def initialized(self) -> bool:
+        return self._initialized
+
+    def insert_world_from_sdf(self, world_file: str = "", world_name: str = "") -> bool:
+        if self._initialized:
+            _err("Worlds can be inserted only before initializing the simulator")
+            return False
+        if world_file:
+            try:
+                name = world_name or get_world_name_from_sdf(world_file)
+            except (OSError, ET.ParseError) as e:
+                _err(f"Failed to load the SDF world: {e}")
+                return False
+        else:
+            name = world_name or "default"
+        if name in self._pending_worlds:
+            _err(f"World '{name}' already exists")
+            return False
+        self._pending_worlds.append(name)
+        return True
+
+    def insert_worlds_from_sdf(self, world_file: str, world_names: Sequence[str] = ()) -> bool:
+        try:
+            root = ET.fromstring(_read(world_file).strip())
+        except (OSError, ET.ParseError) as e:
+            _err(f"Failed to load the SDF worlds: {e}")
+            return False
+        names = [w.get("name", "") for w in root.findall("world")]
+        if world_names:
+            if len(world_names) != len(names):
+                _err("The number of world names does not match the worlds in the SDF")
+                return False
+            names = list(world_names)
+        return all(self.insert_world_from_sdf("", n) for n in names)
+
+    def initialize(self) -> bool:
+        if self._initialized:
+            return True
+        # helpers.cpp:391-400 and GazeboSimulator.cpp:578-582
+        if self._step_size <= 0:
+            _err("The physics step size must be positive")
+            return False
+        if self._rtf <= 0:
+            _err("The real-time factor must be positive")
+            return False
+        if self._steps_per_run <= 0:
+            _err("The number of steps per run must be positive")
+            return False
+        if not self._pending_worlds:
+            self._pending_worlds.append("default")
+        for n in self._pending_worlds:
+            self._worlds[n] = World(self, n)
+        self._initialized = True
+        return True
+
+    def world_names(self) -> List[str]:
+        return list(self._worlds.keys())
+
+    def get_world(self, world_name: str = "") -> World:
+        if not self._initialized:
+            raise RuntimeError("The simulator was not initialized")
+        if not world_name:
+            return next(iter(self._worlds.values()))
+        if world_name not in self._worlds:
+            raise RuntimeError(f"World '{world_name}' not found")
+        return self._worlds[world_name]
+
+    def run(self, paused: bool = False) -> bool:
+        if not self._initialized:
+            _err("The simulator was not initialized")
+            return False
+        if not paused:
+            self._iterations += self._steps_per_run
+        t_ns = self._iterations * int(round(self._step_size * 1e9))
+        try:
+            for w in self._worlds.values():
+                w._update(paused, t_ns)
+        except RuntimeError as e:
+            _err(f"The server couldn't execute the step: {e}")
+            return False
+        return True
+
+    def gui(self, verbosity: int = -1) -> bool:
+        _warn("The GUI is not part of this build")
+        return False
+
+    def pause(self) -> bool:
+        return True
+
+    def running(self) -> bool:
+        return False
+
+    def close(self) -> bool:
+        for w in self._worlds.values():
+            w._close()
+        self._worlds.clear()
+        self._initialized = False
+        return True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,184 @@
+/*
+ * mwstep.h -- C ABI of the MI355X many-worlds articulated-body stepper.
+ *
+ * This is the drop-in boundary that replaces the reference's ScenarI/O Gazebo
+ * backend on the env-step hot path:
+ *   GazeboRuntime.step()            python/gym_ignition/runtimes/gazebo_runtime.py:91-120
+ *   -> scenario.GazeboSimulator.run cpp/scenario/gazebo/src/GazeboSimulator.cpp:202-251
+ *   -> Physics system Update        cpp/scenario/plugins/Physics/Physics.cpp:646-685
+ *   -> DART World::step             [EXT]
+ * Every world of a simulator is one slot of structure-of-arrays device state;
+ * one mw_run() steps all of them (the reference steps one ECM per world,
+ * GazeboSimulator.cpp:435-488 / Physics.cpp:1832-1834).
+ *
+ * Conventions
+ *   - every function returns MW_OK (0) or an MW_E* status; the message of the
+ *     last failure on the calling thread is mw_last_error().  Bool-returning
+ *     ScenarI/O calls map MW_OK -> true; getters that throw in the reference
+ *     (exceptions::DOFMismatch etc., cpp/scenario/gazebo/include/scenario/
+ *     gazebo/exceptions.h) map a failure to RuntimeError in the Python shim.
+ *   - host buffers are double precision, row-major [n_worlds_in_range, n_dofs];
+ *     device buffers are float32 and owned by the caller unless stated.
+ *   - no torch or HIP types appear in these signatures; a HIP stream is passed
+ *     as void*.
+ */
+#ifndef MWSTEP_H
+#define MWSTEP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MW_OK 0
+#define MW_EINVAL 1      /* bad argument (dof/world out of range, bad mode) */
+#define MW_ESTATE 2      /* wrong lifecycle state (not initialized, ...)    */
+#define MW_EPARSE 3      /* model file could not be parsed / unsupported    */
+#define MW_EHIP 4        /* HIP runtime failure                            */
+#define MW_ENOTFOUND 5   /* unknown joint / model / field name             */
+
+/* JointControlMode, same numbering as scenario::core::JointControlMode
+ * (cpp/scenario/core/include/scenario/core/Joint.h:37-75). */
+#define MW_MODE_INVALID 0
+#define MW_MODE_IDLE 1
+#define MW_MODE_FORCE 2
+#define MW_MODE_VELOCITY 3
+#define MW_MODE_VELOCITY_FOLLOWER_DART 4
+#define MW_MODE_POSITION 5
+#define MW_MODE_POSITION_INTERPOLATED 6
+
+/* JointType, same numbering as scenario::core::JointType (Joint.h:25-31). */
+#define MW_JOINT_INVALID 0
+#define MW_JOINT_FIXED 1
+#define MW_JOINT_REVOLUTE 2
+#define MW_JOINT_PRISMATIC 3
+#define MW_JOINT_BALL 4
+
+/* per-joint parameters that the reference lets a just-created model change
+ * (Joint::setCoulombFriction / setViscousFriction / setMaxGeneralizedForce,
+ * cpp/scenario/gazebo/src/Joint.cpp:258-318,622-640) */
+#define MW_PARAM_COULOMB_FRICTION 0
+#define MW_PARAM_VISCOUS_FRICTION 1
+#define MW_PARAM_MAX_GENERALIZED_FORCE 2
+#define MW_PARAM_POSITION_LIMIT_MIN 3
+#define MW_PARAM_POSITION_LIMIT_MAX 4
+
+typedef struct mw_sim mw_sim;
+typedef struct mw_vecenv mw_vecenv;
+
+typedef struct {
+    double step_size;        /* GazeboSimulator(step_size, rtf, steps_per_run) */
+    double rtf;              /* validated (> 0) like helpers.cpp:391-400;       */
+                             /* no wall-clock throttling is performed           */
+    int32_t steps_per_run;   /* physics substeps per mw_run (> 0)              */
+    int32_t n_worlds;        /* parallel worlds on this device (>= 1)          */
+    int32_t device;          /* HIP device ordinal                             */
+    int32_t pgs_iters;       /* boxed-LCP sweeps per substep (0 -> 20)          */
+} mw_config;
+
+/* ---- lifecycle (GazeboSimulator ctor / initialize / close) ---- */
+const char* mw_last_error(void);
+const char* mw_version(void);
+int mw_create(const mw_config* cfg, mw_sim** out);
+void mw_destroy(mw_sim* sim);
+/* Load the articulated model replicated into every world.  `urdf` is a file
+ * path or an inline URDF string; pose = {x, y, z, qw, qx, qy, qz}
+ * (World::insertModel, cpp/scenario/gazebo/src/World.cpp:70-180). */
+int mw_load_model(mw_sim* sim, const char* urdf, const double pose[7], const char* name);
+int mw_initialize(mw_sim* sim);
+int mw_initialized(const mw_sim* sim);
+/* Optional: launch on an external stream (e.g. torch's current stream). */
+int mw_set_stream(mw_sim* sim, void* hip_stream);
+
+/* ---- stepping (GazeboSimulator::run) ---- */
+/* Applies pending resets and commands, executes steps_per_run substeps unless
+ * paused, refreshes the host-side readback, and blocks until done. */
+int mw_run(mw_sim* sim, int paused);
+/* Simulated time in seconds after the last run (World::time, World.cpp:326-332). */
+int mw_time(const mw_sim* sim, double* seconds);
+int mw_set_gravity(mw_sim* sim, const double g[3]);
+int mw_gravity(const mw_sim* sim, double g[3]);
+
+/* ---- model / joint introspection ---- */
+int mw_n_worlds(const mw_sim* sim, int32_t* n);
+int mw_dofs(const mw_sim* sim, int32_t* n);
+int mw_joint_name(const mw_sim* sim, int32_t dof, char* buf, int32_t buflen);
+int mw_joint_index(const mw_sim* sim, const char* name, int32_t* dof);
+int mw_joint_type(const mw_sim* sim, int32_t dof, int32_t* type);
+int mw_model_name(const mw_sim* sim, char* buf, int32_t buflen);
+int mw_base_frame(const mw_sim* sim, char* buf, int32_t buflen);
+int mw_set_joint_param(mw_sim* sim, int32_t dof, int32_t which, double value);
+int mw_joint_param(const mw_sim* sim, int32_t dof, int32_t which, double* value);
+/* Export the compiled chain (fp64) for cross-checks: per dof
+ * {jtype, limited, E[9], r[3], axis[3], mass, com[3], Ic[6], damping,
+ *  friction, lower, upper, effort, vel_limit} = 33 doubles, then gravity_base[3]. */
+int mw_model_export(const mw_sim* sim, double* out, int32_t len);
+
+/* ---- batched ScenarI/O accessors over worlds [w0, w0 + nw) ----
+ * dofs == NULL selects all dofs in model order (ndofs ignored). */
+int mw_get_joint_positions(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_get_joint_velocities(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_get_joint_accelerations(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_get_joint_forces(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_get_joint_force_targets(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_get_joint_velocity_targets(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_get_joint_position_targets(const mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, double* out);
+int mw_set_joint_force_targets(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, const double* v);
+int mw_set_joint_velocity_targets(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, const double* v);
+int mw_set_joint_position_targets(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, const double* v);
+int mw_reset_joint_positions(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, const double* v);
+int mw_reset_joint_velocities(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, const double* v);
+int mw_set_joint_control_mode(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, int32_t mode);
+int mw_joint_control_mode(const mw_sim* sim, int32_t w, int32_t dof, int32_t* mode);
+
+/* Zero-copy device views of the SoA state, fields "q", "qd", "qdd":
+ * float32 [n_dofs][n_worlds] (world index fastest). */
+int mw_device_ptr(mw_sim* sim, const char* field, void** dptr, int64_t* world_stride);
+/* Device-to-device copy of the SoA state ([n_dofs][n_worlds] float32 each) to
+ * (to_sim = 0) or from (to_sim = 1) caller buffers, on the sim's stream. */
+int mw_copy_state(mw_sim* sim, float* q_dev, float* qd_dev, int to_sim);
+
+/* ---- batched environment (device-side Task logic) ----
+ * Tasks mirror python/gym_ignition_environments/tasks/ (CartPole x3,
+ * Pendulum); the TimeLimit of
+ * the gym registration (max_episode_steps, __init__.py:14-52) and
+ * auto-reset of done worlds (Philox4x32-10 keyed by seed) run in-kernel. */
+#define MW_TASK_CARTPOLE_DISCRETE 0
+#define MW_TASK_CARTPOLE_CONTINUOUS_BALANCING 1
+#define MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP 2
+#define MW_TASK_PENDULUM_SWINGUP 3
+
+typedef struct {
+    int32_t kind;
+    int32_t max_episode_steps;       /* 0 = no time limit                   */
+    int32_t reward_cart_at_center;   /* CartPole balancing tasks            */
+    int32_t world_offset;            /* global index of world 0 (sharding):  */
+                                     /* reset streams do not depend on P     */
+    uint64_t seed;
+} mw_task_config;
+
+int mw_vecenv_create(mw_sim* sim, const mw_task_config* cfg, mw_vecenv** out);
+void mw_vecenv_destroy(mw_vecenv* env);
+int mw_vecenv_obs_dim(const mw_vecenv* env, int32_t* n);
+/* Reset every world (episode 0); obs_dev float32 [n_worlds, obs_dim]. */
+int mw_vecenv_reset(mw_vecenv* env, float* obs_dev);
+/* One env step of every world, asynchronous on the sim's stream.
+ *   actions_dev: int32 [n_worlds] (discrete) or float32 [n_worlds]
+ *   obs_dev float32 [n_worlds, obs_dim]  (reset obs where done)
+ *   reward_dev float32 [n_worlds], done_dev uint8 [n_worlds]
+ *   terminal_obs_dev float32 [n_worlds, obs_dim] (written only where done) */
+int mw_vecenv_step(mw_vecenv* env, const void* actions_dev, float* obs_dev, float* reward_dev,
+                   uint8_t* done_dev, float* terminal_obs_dev);
+/* T env steps fused in one launch (open loop: actions [T, n_worlds]); outputs
+ * [T, ...]. */
+int mw_vecenv_rollout(mw_vecenv* env, int32_t T, const void* actions_dev, float* obs_dev,
+                      float* reward_dev, uint8_t* done_dev, float* terminal_obs_dev);
+/* Copy the per-world episode / step counters (uint32 [n_worlds]) into caller
+ * device buffers (async, on the sim's stream). */
+int mw_vecenv_counters(mw_vecenv* env, uint32_t* episode_dev, uint32_t* steps_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MWSTEP_H */

@@ -1,0 +1,693 @@
+/*
+ * oracle.c -- fp64 CPU restatement of the reference's physics step (TEST
+ * INFRASTRUCTURE ONLY; see oracle.h for who may load it).
+ *
+ * Reference call chain restated here:
+ *   GazeboRuntime.step            python/gym_ignition/runtimes/gazebo_runtime.py:91-120
+ *   Physics::Update               cpp/scenario/plugins/Physics/Physics.cpp:646-685
+ *     UpdatePhysics (resets/cmds) Physics.cpp:1330-1440 (velocity reset, then
+ *                                 position reset, then SetForce per dof)
+ *     Step -> dartsim ForwardStep Physics.cpp:1824-1835  [EXT: DART 6.x World::step]
+ *     UpdateSim readback          Physics.cpp:2250-2254 (zero JointForceCmd),
+ *                                 :2276-2345 (position/velocity/acceleration/force)
+ *
+ * DART 6.x World::step [EXT, restated from its published algorithm]:
+ *   computeForwardDynamics   articulated-body algorithm; the projected
+ *                            articulated inertia carries the implicit damping
+ *                            term S^T AI S + dt*d (GenericJoint::
+ *                            updateInvProjArtInertiaImplicit) and the joint
+ *                            force is tau - d*qd - S^T(AI eta + B)
+ *                            (GenericJoint::updateTotalForceDynamic)
+ *   integrateVelocities      qd += dt * qdd
+ *   ConstraintSolver::solve  joint-limit / servo / Coulomb-friction rows
+ *                            (JointLimitConstraint, ServoMotorConstraint,
+ *                            JointCoulombFrictionConstraint) as a boxed LCP
+ *                            A x = b + w with A = J M^-1 J^T (CFM 1e-9)
+ *   computeImpulseForwardDynamics  dqd = M^-1 J^T x (non-implicit AI)
+ *   integratePositions       q += dt * qd
+ * Force commands are clipped to +-effort (GenericJoint::setCommand, FORCE).
+ *
+ * Spatial conventions (DART): spatial vectors are [angular; linear] in body
+ * coordinates; T = (R, p) is the child pose in the parent; X = Ad_{T^-1}.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <string.h>
+
+/* ---------------- small dense helpers (6x6 row-major) ---------------- */
+
+static void m6_zero(double* A) { memset(A, 0, 36 * sizeof(double)); }
+
+static void m6_vec(const double* A, const double* x, double* y)
+{
+    for (int i = 0; i < 6; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < 6; ++k) s += A[i * 6 + k] * x[k];
+        y[i] = s;
+    }
+}
+
+static void m6t_vec(const double* A, const double* x, double* y)
+{
+    for (int i = 0; i < 6; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < 6; ++k) s += A[k * 6 + i] * x[k];
+        y[i] = s;
+    }
+}
+
+/* out = X^T I X */
+static void m6_congruence(const double* X, const double* I, double* out)
+{
+    double T[36];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 6; ++k) s += I[i * 6 + k] * X[k * 6 + j];
+            T[i * 6 + j] = s;
+        }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 6; ++k) s += X[k * 6 + i] * T[k * 6 + j];
+            out[i * 6 + j] = s;
+        }
+}
+
+static double dot6(const double* a, const double* b)
+{
+    double s = 0.0;
+    for (int i = 0; i < 6; ++i) s += a[i] * b[i];
+    return s;
+}
+
+static void cross3(const double* a, const double* b, double* c)
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+/* ad(V) W = [w x a ; w x b + v x a] */
+static void sp_ad(const double* V, const double* W, double* out)
+{
+    double t[3];
+    cross3(V, W, out);
+    cross3(V, W + 3, out + 3);
+    cross3(V + 3, W, t);
+    out[3] += t[0]; out[4] += t[1]; out[5] += t[2];
+}
+
+/* dad(V, F) = ad(V)^T F = [n x w + f x v ; f x w] */
+static void sp_dad(const double* V, const double* F, double* out)
+{
+    double t[3];
+    cross3(F, V, out);
+    cross3(F + 3, V + 3, t);
+    out[0] += t[0]; out[1] += t[1]; out[2] += t[2];
+    cross3(F + 3, V, out + 3);
+}
+
+/* ---------------- model kinematics / inertia ---------------- */
+
+static void joint_pose(const or_model* m, int i, double q, double R[9], double p[3])
+{
+    const double* E = m->E[i];
+    const double* a = m->axis[i];
+    if (m->jtype[i] == 0) {
+        const double c = cos(q), s = sin(q), v = 1.0 - c;
+        double J[9];
+        J[0] = c + a[0] * a[0] * v;        J[1] = a[0] * a[1] * v - a[2] * s; J[2] = a[0] * a[2] * v + a[1] * s;
+        J[3] = a[1] * a[0] * v + a[2] * s; J[4] = c + a[1] * a[1] * v;        J[5] = a[1] * a[2] * v - a[0] * s;
+        J[6] = a[2] * a[0] * v - a[1] * s; J[7] = a[2] * a[1] * v + a[0] * s; J[8] = c + a[2] * a[2] * v;
+        for (int r = 0; r < 3; ++r)
+            for (int cidx = 0; cidx < 3; ++cidx)
+                R[r * 3 + cidx] = E[r * 3] * J[cidx] + E[r * 3 + 1] * J[3 + cidx] + E[r * 3 + 2] * J[6 + cidx];
+        p[0] = m->r[i][0]; p[1] = m->r[i][1]; p[2] = m->r[i][2];
+    } else {
+        memcpy(R, E, 9 * sizeof(double));
+        for (int r = 0; r < 3; ++r)
+            p[r] = m->r[i][r] + q * (E[r * 3] * a[0] + E[r * 3 + 1] * a[1] + E[r * 3 + 2] * a[2]);
+    }
+}
+
+/* X = Ad_{T^-1} = [[R^T, 0], [-R^T [p]x, R^T]] */
+static void plucker(const double R[9], const double p[3], double X[36])
+{
+    m6_zero(X);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            X[r * 6 + c] = R[c * 3 + r];
+            X[(r + 3) * 6 + c + 3] = R[c * 3 + r];
+        }
+    const double P[9] = {0, -p[2], p[1], p[2], 0, -p[0], -p[1], p[0], 0};
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            for (int k = 0; k < 3; ++k) s += R[k * 3 + r] * P[k * 3 + c];
+            X[(r + 3) * 6 + c] = -s;
+        }
+}
+
+static void motion_subspace(const or_model* m, int i, double S[6])
+{
+    memset(S, 0, 6 * sizeof(double));
+    const int off = (m->jtype[i] == 0) ? 0 : 3;
+    S[off] = m->axis[i][0]; S[off + 1] = m->axis[i][1]; S[off + 2] = m->axis[i][2];
+}
+
+/* spatial inertia about the body origin, [angular; linear] ordering */
+static void body_inertia(const or_model* m, int i, double I[36])
+{
+    const double ms = m->mass[i];
+    const double* c = m->com[i];
+    const double* ic = m->Ic[i];
+    const double Icm[9] = {ic[0], ic[3], ic[4], ic[3], ic[1], ic[5], ic[4], ic[5], ic[2]};
+    const double C[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+    m6_zero(I);
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            double cc = 0.0; /* -[c]x[c]x */
+            for (int j = 0; j < 3; ++j) cc -= C[r * 3 + j] * C[j * 3 + k];
+            I[r * 6 + k] = Icm[r * 3 + k] + ms * cc;
+            I[r * 6 + k + 3] = ms * C[r * 3 + k];
+            I[(r + 3) * 6 + k] = -ms * C[r * 3 + k];
+            I[(r + 3) * 6 + k + 3] = (r == k) ? ms : 0.0;
+        }
+}
+
+/* ---------------- articulated-body algorithm ---------------- */
+
+typedef struct {
+    double X[OR_MAXB][36];
+    double S[OR_MAXB][6];
+    double U[OR_MAXB][6];    /* AI S (non-implicit)      */
+    double Psi[OR_MAXB];     /* (S^T AI S)^-1             */
+} or_impulse_factor;
+
+static void aba_full(const or_model* m, const double* q, const double* qd,
+                     const double* tau, double dt_implicit, double* qdd,
+                     or_impulse_factor* fac)
+{
+    const int n = m->n;
+    double X[OR_MAXB][36], S[OR_MAXB][6], eta[OR_MAXB][6], B[OR_MAXB][6];
+    double I[OR_MAXB][36], AIi[OR_MAXB][36], AI[OR_MAXB][36];
+    double Ui[OR_MAXB][6], Psii[OR_MAXB], tt[OR_MAXB];
+    double V[6] = {0}, g[3];
+    memcpy(g, m->gravity_base, sizeof g);
+
+    for (int i = 0; i < n; ++i) {
+        double R[9], p[3], Vp[6], Sq[6], IV[6], dd[6], gb[3], Fg[6], ga[6] = {0};
+        joint_pose(m, i, q[i], R, p);
+        plucker(R, p, X[i]);
+        motion_subspace(m, i, S[i]);
+        m6_vec(X[i], V, Vp);
+        for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[k] = Vp[k] + Sq[k]; }
+        for (int r = 0; r < 3; ++r) gb[r] = R[r] * g[0] + R[3 + r] * g[1] + R[6 + r] * g[2];
+        memcpy(g, gb, sizeof g);
+        sp_ad(V, Sq, eta[i]);
+        body_inertia(m, i, I[i]);
+        m6_vec(I[i], V, IV);
+        sp_dad(V, IV, dd);
+        ga[3] = g[0]; ga[4] = g[1]; ga[5] = g[2];
+        m6_vec(I[i], ga, Fg);
+        for (int k = 0; k < 6; ++k) B[i][k] = -dd[k] - Fg[k];
+        memcpy(AIi[i], I[i], sizeof(double) * 36);
+        memcpy(AI[i], I[i], sizeof(double) * 36);
+    }
+
+    for (int i = n - 1; i >= 0; --i) {
+        double U[6], AIeta[6], tmp[6];
+        m6_vec(AIi[i], S[i], Ui[i]);
+        Psii[i] = 1.0 / (dot6(S[i], Ui[i]) + dt_implicit * m->damping[i]);
+        m6_vec(AI[i], S[i], U);
+        const double psi = 1.0 / dot6(S[i], U);
+        if (fac) { memcpy(fac->U[i], U, sizeof U); fac->Psi[i] = psi; }
+        m6_vec(AIi[i], eta[i], AIeta);
+        for (int k = 0; k < 6; ++k) tmp[k] = AIeta[k] + B[i][k];
+        tt[i] = tau[i] - m->damping[i] * qd[i] - dot6(S[i], tmp);
+        if (i > 0) {
+            double Pi[36], Pn[36], beta[6], c[36], bp[6];
+            for (int r = 0; r < 6; ++r)
+                for (int k = 0; k < 6; ++k) {
+                    Pi[r * 6 + k] = AIi[i][r * 6 + k] - Psii[i] * Ui[i][r] * Ui[i][k];
+                    Pn[r * 6 + k] = AI[i][r * 6 + k] - psi * U[r] * U[k];
+                }
+            for (int k = 0; k < 6; ++k) beta[k] = B[i][k] + AIeta[k] + Ui[i][k] * Psii[i] * tt[i];
+            m6_congruence(X[i], Pi, c);
+            for (int k = 0; k < 36; ++k) AIi[i - 1][k] += c[k];
+            m6_congruence(X[i], Pn, c);
+            for (int k = 0; k < 36; ++k) AI[i - 1][k] += c[k];
+            m6t_vec(X[i], beta, bp);
+            for (int k = 0; k < 6; ++k) B[i - 1][k] += bp[k];
+        }
+    }
+
+    double a[6] = {0};
+    for (int i = 0; i < n; ++i) {
+        double ap[6];
+        m6_vec(X[i], a, ap);
+        qdd[i] = Psii[i] * (tt[i] - dot6(Ui[i], ap));
+        for (int k = 0; k < 6; ++k) a[k] = ap[k] + eta[i][k] + S[i][k] * qdd[i];
+    }
+    if (fac) {
+        for (int i = 0; i < n; ++i) {
+            memcpy(fac->X[i], X[i], sizeof(double) * 36);
+            memcpy(fac->S[i], S[i], sizeof(double) * 6);
+        }
+    }
+}
+
+void or_aba(const or_model* m, const double* q, const double* qd,
+            const double* tau, double dt_implicit, double* qdd)
+{
+    aba_full(m, q, qd, tau, dt_implicit, qdd, 0);
+}
+
+/* velocity change of every dof for a unit generalized impulse on dof j
+ * (DART computeImpulseForwardDynamics with only joint impulses). */
+static void impulse_column(const or_model* m, const or_impulse_factor* f, int j,
+                           double* col)
+{
+    const int n = m->n;
+    double u[OR_MAXB];
+    double Bimp[6] = {0};
+    for (int i = n - 1; i >= 0; --i) {
+        if (i > j) { u[i] = 0.0; continue; }
+        if (i == j) { u[i] = 1.0; memset(Bimp, 0, sizeof Bimp); continue; }
+        double t[6], bp[6];
+        for (int k = 0; k < 6; ++k) t[k] = Bimp[k] + f->U[i + 1][k] * f->Psi[i + 1] * u[i + 1];
+        m6t_vec(f->X[i + 1], t, bp);
+        memcpy(Bimp, bp, sizeof bp);
+        u[i] = -dot6(f->S[i], Bimp);
+    }
+    double dv[6] = {0};
+    for (int i = 0; i < n; ++i) {
+        double dvp[6];
+        m6_vec(f->X[i], dv, dvp);
+        col[i] = f->Psi[i] * (u[i] - dot6(f->U[i], dvp));
+        for (int k = 0; k < 6; ++k) dv[k] = dvp[k] + f->S[i][k] * col[i];
+    }
+}
+
+void or_crba(const or_model* m, const double* q, double* M)
+{
+    const int n = m->n;
+    double X[OR_MAXB][36], S[OR_MAXB][6], Ic[OR_MAXB][36];
+    for (int i = 0; i < n; ++i) {
+        double R[9], p[3];
+        joint_pose(m, i, q[i], R, p);
+        plucker(R, p, X[i]);
+        motion_subspace(m, i, S[i]);
+        body_inertia(m, i, Ic[i]);
+    }
+    for (int i = n - 1; i > 0; --i) {
+        double c[36];
+        m6_congruence(X[i], Ic[i], c);
+        for (int k = 0; k < 36; ++k) Ic[i - 1][k] += c[k];
+    }
+    for (int i = 0; i < n; ++i) {
+        double F[6];
+        m6_vec(Ic[i], S[i], F);
+        M[i * n + i] = dot6(S[i], F);
+        for (int j = i; j > 0; --j) {
+            double Fp[6];
+            m6t_vec(X[j], F, Fp);
+            memcpy(F, Fp, sizeof F);
+            M[i * n + (j - 1)] = dot6(S[j - 1], F);
+            M[(j - 1) * n + i] = M[i * n + (j - 1)];
+        }
+    }
+}
+
+void or_rnea(const or_model* m, const double* q, const double* qd,
+             const double* qdd, double* tau)
+{
+    const int n = m->n;
+    double X[OR_MAXB][36], S[OR_MAXB][6], f[OR_MAXB][6];
+    double V[6] = {0}, a[6] = {0};
+    a[3] = -m->gravity_base[0]; a[4] = -m->gravity_base[1]; a[5] = -m->gravity_base[2];
+    for (int i = 0; i < n; ++i) {
+        double R[9], p[3], Vp[6], ap[6], Sq[6], c[6], I[36], Ia[6], IV[6], dd[6];
+        joint_pose(m, i, q[i], R, p);
+        plucker(R, p, X[i]);
+        motion_subspace(m, i, S[i]);
+        m6_vec(X[i], V, Vp);
+        m6_vec(X[i], a, ap);
+        for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[k] = Vp[k] + Sq[k]; }
+        sp_ad(V, Sq, c);
+        for (int k = 0; k < 6; ++k) a[k] = ap[k] + S[i][k] * qdd[i] + c[k];
+        body_inertia(m, i, I);
+        m6_vec(I, a, Ia);
+        m6_vec(I, V, IV);
+        sp_dad(V, IV, dd);
+        for (int k = 0; k < 6; ++k) f[i][k] = Ia[k] - dd[k];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        tau[i] = dot6(S[i], f[i]);
+        if (i > 0) {
+            double fp[6];
+            m6t_vec(X[i], f[i], fp);
+            for (int k = 0; k < 6; ++k) f[i - 1][k] += fp[k];
+        }
+    }
+}
+
+/* ---------------- boxed LCP ---------------- */
+
+void or_pgs(int n, const double* A, const double* b, const double* lo,
+            const double* hi, double* x, int iters)
+{
+    for (int it = 0; it < iters; ++it) {
+        for (int r = 0; r < n; ++r) {
+            double s = b[r];
+            for (int c = 0; c < n; ++c) s -= A[r * n + c] * x[c];
+            double v = x[r] + s / A[r * n + r];
+            if (v < lo[r]) v = lo[r];
+            if (v > hi[r]) v = hi[r];
+            x[r] = v;
+        }
+    }
+}
+
+/* DART constants [EXT]: DART_ERP 0.01, DART_MAX_ERV 10, DART_CFM 1e-9,
+ * DART_ERROR_ALLOWANCE 0. */
+#define OR_ERP 0.01
+#define OR_MAX_ERV 10.0
+#define OR_CFM 1e-9
+
+int or_step(const or_model* m, double dt, double* q, double* qd,
+            const int32_t* mode, const double* cmd, int pgs_iters,
+            double* qdd_out, double* force_out)
+{
+    const int n = m->n;
+    double tau[OR_MAXB] = {0}, qdd[OR_MAXB] = {0};
+    or_impulse_factor fac;
+
+    /* GenericJoint::setCommand (FORCE): clip to the effort limits */
+    for (int i = 0; i < n; ++i) {
+        double t = 0.0;
+        if (mode[i] == OR_FORCE) {
+            t = cmd[i];
+            if (t < -m->effort[i]) t = -m->effort[i];
+            if (t > m->effort[i]) t = m->effort[i];
+        }
+        tau[i] = t;
+    }
+
+    aba_full(m, q, qd, tau, dt, qdd, &fac);
+    for (int i = 0; i < n; ++i) qd[i] += dt * qdd[i];
+
+    /* constraint rows: limit, servo, Coulomb friction (per joint, body order) */
+    int rd[3 * OR_MAXB];
+    double b[3 * OR_MAXB], lo[3 * OR_MAXB], hi[3 * OR_MAXB];
+    int nr = 0;
+    for (int i = 0; i < n; ++i) {
+        if (m->limited[i]) {
+            double viol = q[i] - m->lower[i];
+            int active = 0;
+            if (viol <= 0.0) { lo[nr] = 0.0; hi[nr] = INFINITY; active = 1; }
+            else {
+                viol = q[i] - m->upper[i];
+                if (viol >= 0.0) { lo[nr] = -INFINITY; hi[nr] = 0.0; active = 1; }
+            }
+            if (active) {
+                double bounce = -viol * OR_ERP / dt;
+                if (bounce > OR_MAX_ERV) bounce = OR_MAX_ERV;
+                if (bounce < -OR_MAX_ERV) bounce = -OR_MAX_ERV;
+                b[nr] = -qd[i] + bounce;
+                rd[nr++] = i;
+            }
+        }
+        if (mode[i] == OR_SERVO) {
+            double vc = cmd[i];
+            if (vc < -m->vel_limit[i]) vc = -m->vel_limit[i];
+            if (vc > m->vel_limit[i]) vc = m->vel_limit[i];
+            const double err = vc - qd[i];
+            if (err != 0.0) {
+                b[nr] = err;
+                lo[nr] = -m->effort[i] * dt;
+                hi[nr] = m->effort[i] * dt;
+                rd[nr++] = i;
+            }
+        }
+        if (m->friction[i] != 0.0 && qd[i] != 0.0) {
+            b[nr] = -qd[i];
+            hi[nr] = m->friction[i] * dt;
+            lo[nr] = -hi[nr];
+            rd[nr++] = i;
+        }
+    }
+
+    double imp[OR_MAXB];
+    for (int i = 0; i < n; ++i) imp[i] = 0.0;
+    if (nr > 0) {
+        double cols[OR_MAXB][OR_MAXB];
+        int have[OR_MAXB];
+        for (int i = 0; i < n; ++i) have[i] = 0;
+        for (int r = 0; r < nr; ++r)
+            if (!have[rd[r]]) { impulse_column(m, &fac, rd[r], cols[rd[r]]); have[rd[r]] = 1; }
+        double A[9 * OR_MAXB * OR_MAXB];
+        double x[3 * OR_MAXB];
+        for (int r = 0; r < nr; ++r) {
+            for (int c = 0; c < nr; ++c) A[r * nr + c] = cols[rd[c]][rd[r]];
+            A[r * nr + r] *= (1.0 + OR_CFM);
+            x[r] = 0.0;
+        }
+        or_pgs(nr, A, b, lo, hi, x, pgs_iters);
+        for (int r = 0; r < nr; ++r) imp[rd[r]] += x[r];
+        double dqd[OR_MAXB];
+        for (int i = 0; i < n; ++i) dqd[i] = 0.0;
+        for (int i = 0; i < n; ++i)
+            if (imp[i] != 0.0)
+                for (int k = 0; k < n; ++k) dqd[k] += cols[i][k] * imp[i];
+        for (int i = 0; i < n; ++i) {
+            qd[i] += dqd[i];
+            qdd[i] += dqd[i] / dt;
+        }
+    }
+
+    for (int i = 0; i < n; ++i) q[i] += dt * qd[i];
+    if (qdd_out)
+        for (int i = 0; i < n; ++i) qdd_out[i] = qdd[i];
+    if (force_out)
+        for (int i = 0; i < n; ++i) force_out[i] = tau[i] + imp[i] / dt;
+    return nr;
+}
+
+/* ---------------- Philox4x32-10 ---------------- */
+
+void or_philox(uint64_t seed, uint32_t world, uint32_t episode, uint32_t out[4])
+{
+    const uint32_t ctr[4] = {world, episode, 0u, 0u};
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    or_philox_raw(ctr, key, out);
+}
+
+void or_philox_raw(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4])
+{
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static double u01(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }
+static double unif(uint32_t x, double lo, double hi) { return lo + (hi - lo) * u01(x); }
+
+/* float32 bounds as gym.spaces.Box(dtype=float32) stores them */
+static double f32(double v) { return (double)(float)v; }
+
+#define OR_PI 3.14159265358979323846
+static double deg2rad(double d) { return d * OR_PI / 180.0; }
+
+void or_task_reset_state(const or_task* t, uint32_t world, uint32_t episode,
+                         double* q, double* qd)
+{
+    uint32_t r[4];
+    or_philox(t->seed, world, episode, r);
+    switch (t->kind) {
+    case OR_TASK_CARTPOLE_DISCRETE:
+    case OR_TASK_CARTPOLE_CONTINUOUS_BALANCING:
+        /* x, dx, q, dq = uniform(-0.05, 0.05, 4)  cartpole_discrete_balancing.py:137 */
+        q[0] = unif(r[0], -0.05, 0.05); qd[0] = unif(r[1], -0.05, 0.05);
+        q[1] = unif(r[2], -0.05, 0.05); qd[1] = unif(r[3], -0.05, 0.05);
+        break;
+    case OR_TASK_CARTPOLE_CONTINUOUS_SWINGUP:
+        /* q = pi - deg2rad(U(-60, 60)); x, dx, dq = U(-0.05, 0.05)
+         * cartpole_continuous_swingup.py:145-146 */
+        q[1] = OR_PI - deg2rad(unif(r[0], -60.0, 60.0));
+        q[0] = unif(r[1], -0.05, 0.05); qd[0] = unif(r[2], -0.05, 0.05);
+        qd[1] = unif(r[3], -0.05, 0.05);
+        break;
+    case OR_TASK_PENDULUM_SWINGUP: {
+        /* cos, sin, dq = observation_space.sample(); q = atan2(sin, cos)
+         * pendulum_swingup.py:117-127 */
+        const double c = unif(r[0], -1.0, 1.0), s = unif(r[1], -1.0, 1.0);
+        q[0] = atan2(s, c);
+        qd[0] = unif(r[2], -10.0, 10.0);
+        break;
+    }
+    }
+}
+
+int or_task_obs(const or_task* t, const double* q, const double* qd, double* obs)
+{
+    if (t->kind == OR_TASK_PENDULUM_SWINGUP) {
+        obs[0] = cos(q[0]); obs[1] = sin(q[0]); obs[2] = qd[0];
+        return 3;
+    }
+    /* [x, dx, q, dq]  cartpole_discrete_balancing.py:79-92 */
+    obs[0] = q[0]; obs[1] = qd[0]; obs[2] = q[1]; obs[3] = qd[1];
+    return 4;
+}
+
+static int task_done(const or_task* t, const double* obs)
+{
+    if (t->kind == OR_TASK_PENDULUM_SWINGUP) {
+        /* not observation_space.contains(obs), high = [1, 1, 10] */
+        return !(fabs(obs[0]) <= 1.0 && fabs(obs[1]) <= 1.0 && fabs(obs[2]) <= f32(10.0));
+    }
+    const double qth = (t->kind == OR_TASK_CARTPOLE_CONTINUOUS_SWINGUP) ? deg2rad(5 * 360) : deg2rad(12);
+    const double hi[4] = {f32(2.4), f32(20.0), f32(qth), f32(deg2rad(3 * 360))};
+    for (int k = 0; k < 4; ++k)
+        if (!(obs[k] >= -hi[k] && obs[k] <= hi[k])) return 1;
+    return 0;
+}
+
+static double task_reward(const or_task* t, const double* q, const double* qd,
+                          const double* obs, int done)
+{
+    switch (t->kind) {
+    case OR_TASK_CARTPOLE_DISCRETE:
+    case OR_TASK_CARTPOLE_CONTINUOUS_BALANCING: {
+        /* cartpole_discrete_balancing.py:94-109 (0.9 * x_thr) and
+         * cartpole_continuous_balancing.py:107 (1.0 * x_thr) */
+        double r = done ? 0.0 : 1.0;
+        if (t->reward_cart_at_center) {
+            const double f = (t->kind == OR_TASK_CARTPOLE_DISCRETE) ? 0.9 : 1.0;
+            r = r - 0.10 * fabs(obs[0]) - 0.10 * fabs(obs[1]) - 10.0 * (obs[0] >= f * 2.4 ? 1.0 : 0.0);
+        }
+        return r;
+    }
+    case OR_TASK_CARTPOLE_CONTINUOUS_SWINGUP: {
+        /* cartpole_continuous_swingup.py:116-127 */
+        double r = (cos(q[1]) + 1.0) / 2.0;
+        r -= 0.1 * qd[0] * qd[0];
+        r -= 10.0 * (q[0] >= 0.8 * 2.4 ? 1.0 : 0.0);
+        return r;
+    }
+    case OR_TASK_PENDULUM_SWINGUP: {
+        /* pendulum_swingup.py:73-90.  The force target it reads is the
+         * JointForceCmd that UpdateSim zero-filled after the run
+         * (Physics.cpp:2250-2254), so the tau^2 term is identically 0. */
+        double cost = done ? 100.0 : 0.0;
+        const double tau_after_run = 0.0;
+        cost += q[0] * q[0] + 0.1 * qd[0] * qd[0] + 0.001 * tau_after_run * tau_after_run;
+        return -cost;
+    }
+    }
+    return 0.0;
+}
+
+static void world_step(const or_model* m, const or_task* t, double* q, double* qd,
+                       double action, int pgs_iters)
+{
+    int32_t mode[OR_MAXB];
+    double cmd[OR_MAXB];
+    const int drive = 0; /* CartPole "linear" and Pendulum "pivot" are dof 0 */
+    for (int i = 0; i < m->n; ++i) { mode[i] = OR_PASSIVE; cmd[i] = 0.0; }
+    /* the driven joint ("linear" / "pivot") is in Force mode; the CartPole
+     * pivot stays Idle (passive) -- cartpole_discrete_balancing.py:121-131 */
+    mode[drive] = OR_FORCE;
+    for (int s = 0; s < t->steps_per_run; ++s) {
+        /* a force command acts on the first substep only: UpdateSim zero-fills
+         * JointForceCmd after every Update (Physics.cpp:2250-2254) */
+        cmd[drive] = (s == 0) ? action : 0.0;
+        or_step(m, t->dt, q, qd, mode, cmd, pgs_iters, 0, 0);
+    }
+}
+
+static void vec_step_one(const or_model* m, const or_task* t, int W, int w,
+                         double* q, double* qd, double action, uint32_t* episode,
+                         uint32_t* steps, double* obs, double* reward,
+                         uint8_t* done, double* terminal_obs, int pgs_iters)
+{
+    const int n = m->n;
+    double qw[OR_MAXB], qdw[OR_MAXB], o[4];
+    for (int d = 0; d < n; ++d) { qw[d] = q[d * W + w]; qdw[d] = qd[d * W + w]; }
+    world_step(m, t, qw, qdw, action, pgs_iters);
+    const int no = or_task_obs(t, qw, qdw, o);
+    const int tdone = task_done(t, o);
+    reward[w] = task_reward(t, qw, qdw, o, tdone);
+    steps[w] += 1;
+    int d_ = tdone;
+    if (t->max_episode_steps > 0 && steps[w] >= (uint32_t)t->max_episode_steps) d_ = 1;
+    done[w] = (uint8_t)d_;
+    if (d_) {
+        for (int k = 0; k < no; ++k) terminal_obs[w * no + k] = o[k];
+        episode[w] += 1;
+        steps[w] = 0;
+        or_task_reset_state(t, (uint32_t)w, episode[w], qw, qdw);
+        or_task_obs(t, qw, qdw, o);
+    }
+    for (int k = 0; k < no; ++k) obs[w * no + k] = o[k];
+    for (int d = 0; d < n; ++d) { q[d * W + w] = qw[d]; qd[d * W + w] = qdw[d]; }
+}
+
+static double action_of(const or_task* t, const void* actions, int idx)
+{
+    if (t->kind == OR_TASK_CARTPOLE_DISCRETE) {
+        const int a = ((const int32_t*)actions)[idx];
+        return (a == 1) ? 20.0 : -20.0;   /* _force_mag = 20  cartpole_discrete_balancing.py:32,70 */
+    }
+    return ((const double*)actions)[idx];
+}
+
+void or_vec_step(const or_model* m, const or_task* t, int W, double* q,
+                 double* qd, const void* actions, uint32_t* episode,
+                 uint32_t* steps, double* obs, double* reward, uint8_t* done,
+                 double* terminal_obs, int pgs_iters)
+{
+    for (int w = 0; w < W; ++w)
+        vec_step_one(m, t, W, w, q, qd, action_of(t, actions, w), episode, steps,
+                     obs, reward, done, terminal_obs, pgs_iters);
+}
+
+void or_vec_reset(const or_model* m, const or_task* t, int W, double* q,
+                  double* qd, uint32_t* episode, uint32_t* steps, double* obs)
+{
+    const int n = m->n;
+    for (int w = 0; w < W; ++w) {
+        double qw[OR_MAXB], qdw[OR_MAXB], o[4];
+        episode[w] = 0;
+        steps[w] = 0;
+        or_task_reset_state(t, (uint32_t)w, 0u, qw, qdw);
+        const int no = or_task_obs(t, qw, qdw, o);
+        for (int k = 0; k < no; ++k) obs[w * no + k] = o[k];
+        for (int d = 0; d < n; ++d) { q[d * W + w] = qw[d]; qd[d * W + w] = qdw[d]; }
+    }
+}
+
+void or_vec_rollout(const or_model* m, const or_task* t, int W, int T, double* q,
+                    double* qd, const void* actions, uint32_t* episode,
+                    uint32_t* steps, double* obs, double* reward, uint8_t* done,
+                    double* terminal_obs, int pgs_iters)
+{
+    for (int s = 0; s < T; ++s) {
+        const void* a = (t->kind == OR_TASK_CARTPOLE_DISCRETE)
+                            ? (const void*)((const int32_t*)actions + (size_t)s * W)
+                            : (const void*)((const double*)actions + (size_t)s * W);
+        or_vec_step(m, t, W, q, qd, a, episode, steps, obs, reward, done, terminal_obs,
+                    pgs_iters);
+    }
+}

@@ -1,0 +1,140 @@
+/*
+ * oracle.h -- fp64 CPU restatement of the reference's physics step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the
+ * checker.  The product (gym-ignition_amd/) never links or calls it.
+ *
+ * What it restates (see oracle.c for line-level citations):
+ *   - ScenarI/O Physics system step order: resets -> commands -> engine step ->
+ *     readback -> zero-fill of force commands
+ *     (/root/reference/cpp/scenario/plugins/Physics/Physics.cpp:646-685,
+ *      :1330-1440, :2226-2345).
+ *   - DART 6.x World::step [EXT, not vendored in the reference]: articulated
+ *     body algorithm with implicit joint damping, semi-implicit Euler,
+ *     joint-space constraint impulses (position limits, Coulomb friction,
+ *     servo = VelocityFollowerDart) solved as a boxed LCP.
+ *
+ * Parity status: pinned against the reference's analytic pendulum
+ * (tests/.python/test_pendulum_wrt_ground_truth.py:53-67) and the reference
+ * KATs listed in DESIGN.md; trajectory-level parity vs DART itself is
+ * "parity unpinned" (DART/Ignition are absent from this image).
+ */
+#ifndef MW_ORACLE_H
+#define MW_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_MAXB 48
+
+/* Fixed-base kinematic chain: body i's parent is body i-1 (body -1 = base). */
+typedef struct {
+    int32_t n;                   /* moving bodies == dofs                      */
+    int32_t jtype[OR_MAXB];      /* 0 revolute, 1 prismatic                    */
+    int32_t limited[OR_MAXB];    /* position limits enforced                   */
+    int32_t pad_;
+    double gravity_base[3];      /* gravity expressed in the base link frame   */
+    double E[OR_MAXB][9];        /* joint origin rotation in parent (row-major) */
+    double r[OR_MAXB][3];        /* joint origin translation in parent         */
+    double axis[OR_MAXB][3];     /* joint axis in child frame (unit)           */
+    double mass[OR_MAXB];
+    double com[OR_MAXB][3];      /* COM in body frame                          */
+    double Ic[OR_MAXB][6];       /* inertia about COM: xx yy zz xy xz yz       */
+    double damping[OR_MAXB];
+    double friction[OR_MAXB];    /* Coulomb                                    */
+    double lower[OR_MAXB];
+    double upper[OR_MAXB];
+    double effort[OR_MAXB];
+    double vel_limit[OR_MAXB];
+} or_model;
+
+/* joint actuation as seen by the engine (DART actuator types) */
+enum { OR_PASSIVE = 0, OR_FORCE = 1, OR_SERVO = 2 };
+
+/* ABA forward dynamics with DART's implicit damping term (dt_implicit = 0
+ * gives the plain ABA).  tau is the total applied generalized force. */
+void or_aba(const or_model* m, const double* q, const double* qd,
+            const double* tau, double dt_implicit, double* qdd);
+
+/* Composite-rigid-body mass matrix (independent algorithm; test cross-check). */
+void or_crba(const or_model* m, const double* q, double* M /* n*n */);
+
+/* Recursive Newton-Euler inverse dynamics: tau = M qdd + C(q,qd) + g(q). */
+void or_rnea(const or_model* m, const double* q, const double* qd,
+             const double* qdd, double* tau);
+
+/* One engine step (DART World::step restated).
+ *   mode[i]      OR_PASSIVE / OR_FORCE / OR_SERVO
+ *   cmd[i]       force command (FORCE) or velocity command (SERVO)
+ *   qdd_out[i]   joint acceleration readback (includes impulse/dt)
+ *   force_out[i] joint force readback (applied + constraint impulse/dt)
+ * q and qd are updated in place.  Returns the number of active LCP rows. */
+int or_step(const or_model* m, double dt, double* q, double* qd,
+            const int32_t* mode, const double* cmd, int pgs_iters,
+            double* qdd_out, double* force_out);
+
+/* Boxed LCP by projected Gauss-Seidel (A row-major n*n). */
+void or_pgs(int n, const double* A, const double* b, const double* lo,
+            const double* hi, double* x, int iters);
+
+/* ------------------------------------------------------------------ */
+/* Batched environment (task logic of the reference's CartPole /      */
+/* Pendulum tasks + gym TimeLimit + auto-reset with Philox4x32-10).   */
+/* ------------------------------------------------------------------ */
+enum {
+    OR_TASK_CARTPOLE_DISCRETE = 0,
+    OR_TASK_CARTPOLE_CONTINUOUS_BALANCING = 1,
+    OR_TASK_CARTPOLE_CONTINUOUS_SWINGUP = 2,
+    OR_TASK_PENDULUM_SWINGUP = 3,
+};
+
+typedef struct {
+    int32_t kind;
+    int32_t steps_per_run;
+    int32_t max_episode_steps;      /* 0 = no TimeLimit                        */
+    int32_t reward_cart_at_center;
+    double dt;
+    uint64_t seed;
+} or_task;
+
+/* Philox4x32-10 (Salmon et al. 2011), key = seed, counter = (world, episode, 0, 0). */
+void or_philox(uint64_t seed, uint32_t world, uint32_t episode, uint32_t out[4]);
+/* raw Philox4x32-10 on (ctr[4], key[2]) for the published known-answer vectors */
+void or_philox_raw(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* Sample the initial state of world w for its given episode index. */
+void or_task_reset_state(const or_task* t, uint32_t world, uint32_t episode,
+                         double* q, double* qd);
+
+/* Observation of one world (returns n_obs). */
+int or_task_obs(const or_task* t, const double* q, const double* qd, double* obs);
+
+/* One vectorised env step over W worlds, state SoA q[d*W + w].
+ * actions: int32 (discrete) or double (continuous) per world.
+ * Writes obs[W*n_obs] (reset obs where done), reward[W], done[W],
+ * terminal_obs[W*n_obs] (only where done), and advances episode/steps. */
+void or_vec_step(const or_model* m, const or_task* t, int W,
+                 double* q, double* qd, const void* actions,
+                 uint32_t* episode, uint32_t* steps,
+                 double* obs, double* reward, uint8_t* done,
+                 double* terminal_obs, int pgs_iters);
+
+/* Initial reset of all worlds (episode index 0). */
+void or_vec_reset(const or_model* m, const or_task* t, int W, double* q,
+                  double* qd, uint32_t* episode, uint32_t* steps, double* obs);
+
+/* CPU baseline: T vec steps, actions[T*W] (int32 for discrete, double else). */
+void or_vec_rollout(const or_model* m, const or_task* t, int W, int T,
+                    double* q, double* qd, const void* actions,
+                    uint32_t* episode, uint32_t* steps, double* obs,
+                    double* reward, uint8_t* done, double* terminal_obs,
+                    int pgs_iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,445 @@
+"""ctypes front-end of the fp64 CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker.  The product path
+(``gym-ignition_amd/``) never imports it.
+
+It carries its own URDF reader (``xml.etree``) so that the model the oracle
+steps is compiled independently of the product's C++ model compiler; a test
+cross-checks the two compilations.  URDF semantics follow what sdformat does
+on URDF import for the reference (fixed joints lumped into their parent link,
+``world`` link => fixed base), as used by
+``/root/reference/python/gym_ignition/runtimes/gazebo_runtime.py:249-262``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+OR_MAXB = 48
+PASSIVE, FORCE, SERVO = 0, 1, 2
+TASK_CARTPOLE_DISCRETE = 0
+TASK_CARTPOLE_CONTINUOUS_BALANCING = 1
+TASK_CARTPOLE_CONTINUOUS_SWINGUP = 2
+TASK_PENDULUM_SWINGUP = 3
+
+
+class OrModel(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32),
+        ("jtype", ctypes.c_int32 * OR_MAXB),
+        ("limited", ctypes.c_int32 * OR_MAXB),
+        ("pad_", ctypes.c_int32),
+        ("gravity_base", ctypes.c_double * 3),
+        ("E", (ctypes.c_double * 9) * OR_MAXB),
+        ("r", (ctypes.c_double * 3) * OR_MAXB),
+        ("axis", (ctypes.c_double * 3) * OR_MAXB),
+        ("mass", ctypes.c_double * OR_MAXB),
+        ("com", (ctypes.c_double * 3) * OR_MAXB),
+        ("Ic", (ctypes.c_double * 6) * OR_MAXB),
+        ("damping", ctypes.c_double * OR_MAXB),
+        ("friction", ctypes.c_double * OR_MAXB),
+        ("lower", ctypes.c_double * OR_MAXB),
+        ("upper", ctypes.c_double * OR_MAXB),
+        ("effort", ctypes.c_double * OR_MAXB),
+        ("vel_limit", ctypes.c_double * OR_MAXB),
+    ]
+
+
+class OrTask(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("steps_per_run", ctypes.c_int32),
+        ("max_episode_steps", ctypes.c_int32),
+        ("reward_cart_at_center", ctypes.c_int32),
+        ("dt", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+def build() -> str:
+    """Compile liboracle.so in place (gcc, no GPU needed)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or (
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "oracle.c"))
+        ):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        D = ctypes.POINTER(ctypes.c_double)
+        I32 = ctypes.POINTER(ctypes.c_int32)
+        U32 = ctypes.POINTER(ctypes.c_uint32)
+        U8 = ctypes.POINTER(ctypes.c_uint8)
+        M = ctypes.POINTER(OrModel)
+        T = ctypes.POINTER(OrTask)
+        L.or_aba.argtypes = [M, D, D, D, ctypes.c_double, D]
+        L.or_crba.argtypes = [M, D, D]
+        L.or_rnea.argtypes = [M, D, D, D, D]
+        L.or_step.argtypes = [M, ctypes.c_double, D, D, I32, D, ctypes.c_int, D, D]
+        L.or_step.restype = ctypes.c_int
+        L.or_pgs.argtypes = [ctypes.c_int, D, D, D, D, D, ctypes.c_int]
+        L.or_philox.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, U32]
+        L.or_philox_raw.argtypes = [U32, U32, U32]
+        L.or_task_reset_state.argtypes = [T, ctypes.c_uint32, ctypes.c_uint32, D, D]
+        L.or_vec_step.argtypes = [M, T, ctypes.c_int, D, D, ctypes.c_void_p, U32, U32, D, D,
+                                  U8, D, ctypes.c_int]
+        L.or_vec_reset.argtypes = [M, T, ctypes.c_int, D, D, U32, U32, D]
+        L.or_vec_rollout.argtypes = [M, T, ctypes.c_int, ctypes.c_int, D, D, ctypes.c_void_p,
+                                     U32, U32, D, D, U8, D, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, ct=ctypes.c_double):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+# --------------------------------------------------------------------------
+# independent URDF reader
+# --------------------------------------------------------------------------
+
+def _rpy(rpy: Sequence[float]) -> np.ndarray:
+    r, p, y = rpy
+    cr, sr, cp, sp, cy, sy = math.cos(r), math.sin(r), math.cos(p), math.sin(p), math.cos(y), math.sin(y)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def _quat_wxyz(q: Sequence[float]) -> np.ndarray:
+    w, x, y, z = q
+    n = math.sqrt(w * w + x * x + y * y + z * z)
+    w, x, y, z = w / n, x / n, y / n, z / n
+    return np.array([
+        [1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+        [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+        [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)],
+    ])
+
+
+def _vec(el, attr, default):
+    if el is None or el.get(attr) is None:
+        return np.array(default, dtype=float)
+    return np.array([float(v) for v in el.get(attr).split()], dtype=float)
+
+
+@dataclass
+class _Link:
+    mass: float = 0.0
+    com: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    I: np.ndarray = field(default_factory=lambda: np.zeros((3, 3)))  # about COM, link frame
+
+
+@dataclass
+class _Joint:
+    name: str
+    jtype: str
+    parent: str
+    child: str
+    R: np.ndarray
+    p: np.ndarray
+    axis: np.ndarray
+    lower: float = -math.inf
+    upper: float = math.inf
+    effort: float = math.inf
+    velocity: float = math.inf
+    damping: float = 0.0
+    friction: float = 0.0
+
+
+def _merge(parent: _Link, child: _Link, R: np.ndarray, p: np.ndarray) -> _Link:
+    """Rigidly merge `child` (pose R, p in parent) into `parent`."""
+    m = parent.mass + child.mass
+    if m <= 0.0:
+        return _Link()
+    c_child = R @ child.com + p
+    com = (parent.mass * parent.com + child.mass * c_child) / m
+    I_child = R @ child.I @ R.T
+
+    def shift(I, mass, d):
+        return I + mass * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+
+    I = shift(parent.I, parent.mass, parent.com - com) + shift(I_child, child.mass, c_child - com)
+    return _Link(m, com, I)
+
+
+@dataclass
+class ChainModel:
+    joint_names: List[str]
+    base_link: str
+    model: OrModel
+    base_R: np.ndarray
+    base_p: np.ndarray
+
+    @property
+    def n(self) -> int:
+        return self.model.n
+
+
+def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0.0),
+              gravity=(0.0, 0.0, -9.8)) -> ChainModel:
+    text = path_or_string
+    if not path_or_string.lstrip().startswith("<"):
+        with open(path_or_string) as f:
+            text = f.read()
+    root = ET.fromstring(text)
+    links: Dict[str, _Link] = {}
+    for le in root.findall("link"):
+        L = _Link()
+        ine = le.find("inertial")
+        if ine is not None:
+            o = ine.find("origin")
+            Ro = _rpy(_vec(o, "rpy", [0, 0, 0]))
+            L.com = _vec(o, "xyz", [0, 0, 0])
+            L.mass = float(ine.find("mass").get("value"))
+            ie = ine.find("inertia")
+            g = lambda k: float(ie.get(k, "0"))
+            Iin = np.array([[g("ixx"), g("ixy"), g("ixz")],
+                            [g("ixy"), g("iyy"), g("iyz")],
+                            [g("ixz"), g("iyz"), g("izz")]])
+            L.I = Ro @ Iin @ Ro.T
+        links[le.get("name")] = L
+    joints: List[_Joint] = []
+    for je in root.findall("joint"):
+        o = je.find("origin")
+        ax = _vec(je.find("axis"), "xyz", [1, 0, 0])
+        ax = ax / np.linalg.norm(ax)
+        J = _Joint(je.get("name"), je.get("type"), je.find("parent").get("link"),
+                   je.find("child").get("link"), _rpy(_vec(o, "rpy", [0, 0, 0])),
+                   _vec(o, "xyz", [0, 0, 0]), ax)
+        lim = je.find("limit")
+        if lim is not None:
+            J.effort = float(lim.get("effort", "inf"))
+            J.velocity = float(lim.get("velocity", "inf"))
+            if J.jtype in ("revolute", "prismatic"):
+                J.lower = float(lim.get("lower", "0"))
+                J.upper = float(lim.get("upper", "0"))
+        dyn = je.find("dynamics")
+        if dyn is not None:
+            J.damping = float(dyn.get("damping", "0"))
+            J.friction = float(dyn.get("friction", "0"))
+        joints.append(J)
+
+    children = {j.child for j in joints}
+    roots = [n for n in links if n not in children]
+    assert len(roots) == 1, roots
+    root_link = roots[0]
+    base_R = _quat_wxyz(pose_wxyz)
+    base_p = np.array(pose_xyz, dtype=float)
+    if root_link == "world":
+        wj = [j for j in joints if j.parent == "world"]
+        assert len(wj) == 1 and wj[0].jtype == "fixed", "only a fixed world joint is supported"
+        base_p = base_p + base_R @ wj[0].p
+        base_R = base_R @ wj[0].R
+        root_link = wj[0].child
+        joints = [j for j in joints if j is not wj[0]]
+    else:
+        raise ValueError("floating-base URDFs are not supported by the chain oracle")
+
+    # lump fixed joints into their parent (sdformat URDF import behaviour)
+    owner = {n: n for n in links}            # link -> body it was lumped into
+    off_R = {n: np.eye(3) for n in links}     # pose of link in its owner
+    off_p = {n: np.zeros(3) for n in links}
+    changed = True
+    while changed:
+        changed = False
+        for j in list(joints):
+            if j.jtype != "fixed":
+                continue
+            po = owner[j.parent]
+            R = off_R[j.parent] @ j.R
+            p = off_R[j.parent] @ j.p + off_p[j.parent]
+            links[po] = _merge(links[po], links[j.child], R, p)
+            for ln in links:
+                if owner[ln] == j.child:
+                    owner[ln] = po
+                    off_p[ln] = R @ off_p[ln] + p
+                    off_R[ln] = R @ off_R[ln]
+            joints.remove(j)
+            changed = True
+            break
+
+    # moving joints must form a chain from the base body
+    chain: List[_Joint] = []
+    cur = root_link
+    while True:
+        nxt = [j for j in joints if owner[j.parent] == cur]
+        if not nxt:
+            break
+        assert len(nxt) == 1, "the chain oracle supports serial chains only"
+        chain.append(nxt[0])
+        cur = nxt[0].child
+    assert len(chain) == len(joints)
+
+    M = OrModel()
+    M.n = len(chain)
+    g_base = base_R.T @ np.array(gravity, dtype=float)
+    for k in range(3):
+        M.gravity_base[k] = g_base[k]
+    for i, j in enumerate(chain):
+        E = off_R[j.parent] @ j.R
+        r = off_R[j.parent] @ j.p + off_p[j.parent]
+        L = links[j.child]
+        M.jtype[i] = 0 if j.jtype in ("revolute", "continuous") else 1
+        M.limited[i] = 1 if j.jtype in ("revolute", "prismatic") else 0
+        for k in range(9):
+            M.E[i][k] = E.flat[k]
+        for k in range(3):
+            M.r[i][k] = r[k]
+            M.axis[i][k] = j.axis[k]
+            M.com[i][k] = L.com[k]
+        M.mass[i] = L.mass
+        Ic = L.I
+        for k, v in enumerate([Ic[0, 0], Ic[1, 1], Ic[2, 2], Ic[0, 1], Ic[0, 2], Ic[1, 2]]):
+            M.Ic[i][k] = v
+        M.damping[i] = j.damping
+        M.friction[i] = j.friction
+        M.lower[i] = j.lower
+        M.upper[i] = j.upper
+        M.effort[i] = j.effort
+        M.vel_limit[i] = j.velocity
+    return ChainModel([j.name for j in chain], root_link, M, base_R, base_p)
+
+
+# --------------------------------------------------------------------------
+# thin wrappers
+# --------------------------------------------------------------------------
+
+def aba(cm: ChainModel, q, qd, tau, dt_implicit=0.0) -> np.ndarray:
+    q, qd, tau = (np.ascontiguousarray(x, dtype=np.float64) for x in (q, qd, tau))
+    out = np.zeros(cm.n)
+    lib().or_aba(ctypes.byref(cm.model), _p(q), _p(qd), _p(tau), dt_implicit, _p(out))
+    return out
+
+
+def crba(cm: ChainModel, q) -> np.ndarray:
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    out = np.zeros((cm.n, cm.n))
+    lib().or_crba(ctypes.byref(cm.model), _p(q), _p(out))
+    return out
+
+
+def rnea(cm: ChainModel, q, qd, qdd) -> np.ndarray:
+    q, qd, qdd = (np.ascontiguousarray(x, dtype=np.float64) for x in (q, qd, qdd))
+    out = np.zeros(cm.n)
+    lib().or_rnea(ctypes.byref(cm.model), _p(q), _p(qd), _p(qdd), _p(out))
+    return out
+
+
+def step(cm: ChainModel, dt, q, qd, mode, cmd, pgs_iters=50):
+    """One engine step; returns (q, qd, qdd, force, active_rows)."""
+    q = np.array(q, dtype=np.float64)
+    qd = np.array(qd, dtype=np.float64)
+    mode = np.ascontiguousarray(mode, dtype=np.int32)
+    cmd = np.ascontiguousarray(cmd, dtype=np.float64)
+    qdd = np.zeros(cm.n)
+    f = np.zeros(cm.n)
+    nr = lib().or_step(ctypes.byref(cm.model), dt, _p(q), _p(qd), _p(mode, ctypes.c_int32),
+                       _p(cmd), pgs_iters, _p(qdd), _p(f))
+    return q, qd, qdd, f, nr
+
+
+def pgs(A, b, lo, hi, iters=100):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b, lo, hi = (np.ascontiguousarray(x, dtype=np.float64) for x in (b, lo, hi))
+    x = np.zeros(len(b))
+    lib().or_pgs(len(b), _p(A), _p(b), _p(lo), _p(hi), _p(x), iters)
+    return x
+
+
+def philox(seed: int, world: int, episode: int) -> np.ndarray:
+    out = (ctypes.c_uint32 * 4)()
+    lib().or_philox(seed, world, episode, out)
+    return np.array(list(out), dtype=np.uint32)
+
+
+def philox_raw(ctr, key) -> np.ndarray:
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().or_philox_raw(_p(c, ctypes.c_uint32), _p(k, ctypes.c_uint32), _p(out, ctypes.c_uint32))
+    return out
+
+
+def make_task(kind: int, dt: float = 1e-3, steps_per_run: int = 1, max_episode_steps: int = 5000,
+              reward_cart_at_center: bool = True, seed: int = 42) -> OrTask:
+    t = OrTask()
+    t.kind = kind
+    t.dt = dt
+    t.steps_per_run = steps_per_run
+    t.max_episode_steps = max_episode_steps
+    t.reward_cart_at_center = 1 if reward_cart_at_center else 0
+    t.seed = seed
+    return t
+
+
+def n_obs(kind: int) -> int:
+    return 3 if kind == TASK_PENDULUM_SWINGUP else 4
+
+
+class VecEnv:
+    """fp64 batched env (SoA state) -- the CPU checker of the HIP VecEnv."""
+
+    def __init__(self, cm: ChainModel, task: OrTask, W: int, pgs_iters: int = 50):
+        self.cm, self.task, self.W, self.pgs_iters = cm, task, W, pgs_iters
+        n = cm.n
+        self.q = np.zeros(n * W)
+        self.qd = np.zeros(n * W)
+        self.episode = np.zeros(W, dtype=np.uint32)
+        self.steps = np.zeros(W, dtype=np.uint32)
+        no = n_obs(task.kind)
+        self.obs = np.zeros(W * no)
+        self.reward = np.zeros(W)
+        self.done = np.zeros(W, dtype=np.uint8)
+        self.terminal_obs = np.zeros(W * no)
+
+    def reset(self):
+        lib().or_vec_reset(ctypes.byref(self.cm.model), ctypes.byref(self.task), self.W,
+                           _p(self.q), _p(self.qd), _p(self.episode, ctypes.c_uint32),
+                           _p(self.steps, ctypes.c_uint32), _p(self.obs))
+        return self.obs.reshape(self.W, -1).copy()
+
+    def _actions(self, actions):
+        if self.task.kind == TASK_CARTPOLE_DISCRETE:
+            return np.ascontiguousarray(actions, dtype=np.int32)
+        return np.ascontiguousarray(actions, dtype=np.float64)
+
+    def step(self, actions):
+        a = self._actions(actions)
+        lib().or_vec_step(ctypes.byref(self.cm.model), ctypes.byref(self.task), self.W,
+                          _p(self.q), _p(self.qd), a.ctypes.data_as(ctypes.c_void_p),
+                          _p(self.episode, ctypes.c_uint32), _p(self.steps, ctypes.c_uint32),
+                          _p(self.obs), _p(self.reward), _p(self.done, ctypes.c_uint8),
+                          _p(self.terminal_obs), self.pgs_iters)
+        return (self.obs.reshape(self.W, -1).copy(), self.reward.copy(), self.done.astype(bool),
+                self.terminal_obs.reshape(self.W, -1).copy())
+
+    def rollout(self, actions):
+        """T steps in C (actions [T, W]); used for the CPU baseline timing."""
+        a = self._actions(actions)
+        T = a.shape[0]
+        lib().or_vec_rollout(ctypes.byref(self.cm.model), ctypes.byref(self.task), self.W, T,
+                             _p(self.q), _p(self.qd), a.ctypes.data_as(ctypes.c_void_p),
+                             _p(self.episode, ctypes.c_uint32), _p(self.steps, ctypes.c_uint32),
+                             _p(self.obs), _p(self.reward), _p(self.done, ctypes.c_uint8),
+                             _p(self.terminal_obs), self.pgs_iters)

@@ -1,0 +1,175 @@
+"""The C-ABI library without a GPU: it loads, exports every symbol that
+include/mwstep.h declares, compiles models (host side) exactly like the
+oracle's independent URDF reader, and validates its inputs."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mwstep.h")
+
+
+def _declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mw_[a-z_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def N():
+    from mwstep import native
+    native.lib()
+    return native
+
+
+def test_every_declared_symbol_is_exported(N):
+    L = ctypes.CDLL(N.LIB_PATH)
+    declared = _declared_symbols()
+    assert len(declared) >= 40
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    bound = {name for name, _, _ in N.SIGNATURES}
+    assert set(declared) == bound, set(declared) ^ bound
+
+
+def test_library_is_gfx950(N):
+    data = open(N.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def _create(N, n_worlds=4, step=1e-3, rtf=1.0, steps=1):
+    cfg = N.MwConfig(step, rtf, steps, n_worlds, 0, 0)
+    h = ctypes.c_void_p()
+    rc = N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h))
+    return rc, h
+
+
+@pytest.mark.parametrize("step,rtf,steps", [(0.0, 1.0, 1), (0.001, 0.0, 1), (0.001, -1.0, 1),
+                                            (0.001, 1.0, 0)])
+def test_create_validates_like_gazebo_simulator(N, step, rtf, steps):
+    # tests/test_scenario/test_gazebo_simulator.py:17-51
+    rc, h = _create(N, step=step, rtf=rtf, steps=steps)
+    assert rc == N.MW_EINVAL and not h.value
+    assert N.last_error()
+
+
+def _export(N, path, pose=(0, 0, 0, 1, 0, 0, 0)):
+    rc, h = _create(N)
+    assert rc == 0
+    try:
+        p = np.array(pose, dtype=np.float64)
+        N.check(N.lib().mw_load_model(h, path.encode(), N.dptr(p), b""))
+        n = ctypes.c_int32()
+        N.check(N.lib().mw_dofs(h, ctypes.byref(n)))
+        out = np.zeros(33 * n.value + 3)
+        N.check(N.lib().mw_model_export(h, N.dptr(out), len(out)))
+        names = []
+        buf = ctypes.create_string_buffer(64)
+        for d in range(n.value):
+            N.check(N.lib().mw_joint_name(h, d, buf, 64))
+            names.append(buf.value.decode())
+        N.lib().mw_base_frame(h, buf, 64)
+        return n.value, out, names, buf.value.decode()
+    finally:
+        N.lib().mw_destroy(h)
+
+
+@pytest.mark.parametrize("model", ["cartpole", "pendulum"])
+@pytest.mark.parametrize("pose", [(0, 0, 0, 1, 0, 0, 0), (0.3, -1, 2, 0.9238795, 0.3826834, 0, 0)])
+def test_model_compiler_matches_oracle_reader(N, oracle, cartpole_file, pendulum_file, model, pose):
+    path = cartpole_file if model == "cartpole" else pendulum_file
+    n, out, names, base = _export(N, path, pose)
+    cm = oracle.load_urdf(path, pose_xyz=pose[:3], pose_wxyz=pose[3:])
+    assert names == cm.joint_names and n == cm.n
+    assert base == cm.base_link
+    M = cm.model
+    big = lambda v: np.where(v > 1e299, np.inf, np.where(v < -1e299, -np.inf, v))
+    for i in range(n):
+        b = out[33 * i: 33 * (i + 1)]
+        assert b[0] == M.jtype[i] and b[1] == M.limited[i]
+        np.testing.assert_allclose(b[2:11], list(M.E[i]), atol=1e-12)
+        np.testing.assert_allclose(b[11:14], list(M.r[i]), atol=1e-12)
+        np.testing.assert_allclose(b[14:17], list(M.axis[i]), atol=1e-12)
+        assert b[17] == pytest.approx(M.mass[i])
+        np.testing.assert_allclose(b[18:21], list(M.com[i]), atol=1e-12)
+        np.testing.assert_allclose(b[21:27], list(M.Ic[i]), atol=1e-12)
+        np.testing.assert_allclose(big(b[27:33]), [M.damping[i], M.friction[i], M.lower[i], M.upper[i],
+                                                   M.effort[i], M.vel_limit[i]])
+    np.testing.assert_allclose(out[33 * n:], list(M.gravity_base), atol=1e-12)
+
+
+def test_fixed_joint_lumping(N, oracle):
+    urdf = """<robot name="r"><link name="world"/>
+      <joint name="w" type="fixed"><parent link="world"/><child link="a"/></joint>
+      <link name="a"><inertial><mass value="1"/><inertia ixx="1" iyy="1" izz="1"/></inertial></link>
+      <joint name="j1" type="revolute"><parent link="a"/><child link="b"/><axis xyz="0 0 1"/>
+        <origin xyz="0 0 1" rpy="0.1 0.2 0.3"/><limit lower="-1" upper="1" effort="10" velocity="3"/></joint>
+      <link name="b"><inertial><origin xyz="0.1 0 0" rpy="0 0.5 0"/><mass value="2"/>
+        <inertia ixx="0.1" iyy="0.2" izz="0.3" ixy="0.01"/></inertial></link>
+      <joint name="fx" type="fixed"><parent link="b"/><child link="c"/><origin xyz="0 0.5 0" rpy="0.3 0 0"/></joint>
+      <link name="c"><inertial><mass value="0.5"/><inertia ixx="0.01" iyy="0.01" izz="0.01"/></inertial></link>
+      <joint name="j2" type="prismatic"><parent link="c"/><child link="d"/><axis xyz="1 1 0"/>
+        <origin xyz="0.2 0 0"/><limit lower="-0.5" upper="0.5" effort="100" velocity="1"/>
+        <dynamics damping="0.3" friction="0.05"/></joint>
+      <link name="d"><inertial><mass value="0.3"/><inertia ixx="0.001" iyy="0.001" izz="0.001"/></inertial></link>
+    </robot>"""
+    n, out, names, base = _export(N, urdf)
+    cm = oracle.load_urdf(urdf)
+    assert names == ["j1", "j2"] == cm.joint_names and base == "a"
+    np.testing.assert_allclose(out[33 + 2:33 + 11], list(cm.model.E[1]), atol=1e-12)
+    np.testing.assert_allclose(out[33 + 11:33 + 14], list(cm.model.r[1]), atol=1e-12)
+    np.testing.assert_allclose(out[21:27], list(cm.model.Ic[0]), atol=1e-12)
+    np.testing.assert_allclose(out[18:21], list(cm.model.com[0]), atol=1e-12)
+    assert out[17] == pytest.approx(2.5)
+
+
+@pytest.mark.parametrize("bad, why", [
+    ("<robot name='x'><link name='a'/><link name='b'/>"
+     "<joint name='j' type='revolute'><parent link='a'/><child link='b'/></joint></robot>", "floating"),
+    ("<robot name='x'><link name='world'/>", "XML"),
+    ("<sdf><model name='m'/></sdf>", "URDF"),
+    ("<robot name='x'><link name='world'/><link name='a'/><joint name='w' type='fixed'>"
+     "<parent link='world'/><child link='a'/></joint><link name='b'/><link name='c'/>"
+     "<joint name='j1' type='revolute'><parent link='a'/><child link='b'/></joint>"
+     "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>", "branched"),
+])
+def test_unsupported_models_fail_loudly(N, bad, why):
+    rc, h = _create(N)
+    try:
+        p = np.array([0, 0, 0, 1, 0, 0, 0], dtype=np.float64)
+        rc = N.lib().mw_load_model(h, bad.encode(), N.dptr(p), b"")
+        assert rc == N.MW_EPARSE
+        assert why.lower() in N.last_error().lower()
+    finally:
+        N.lib().mw_destroy(h)
+
+
+def test_initialize_without_model_or_gpu_reports_error(N, cartpole_file):
+    rc, h = _create(N)
+    try:
+        assert N.lib().mw_initialize(h) == N.MW_ESTATE
+        p = np.array([0, 0, 0, 1, 0, 0, 0], dtype=np.float64)
+        N.check(N.lib().mw_load_model(h, cartpole_file.encode(), N.dptr(p), b""))
+        rc = N.lib().mw_run(h, 0)
+        assert rc == N.MW_ESTATE  # not initialized: run refuses, like GazeboSimulator::run
+    finally:
+        N.lib().mw_destroy(h)
+
+
+def test_joint_params_before_first_run(N, pendulum_file):
+    rc, h = _create(N)
+    try:
+        p = np.array([0, 0, 0, 1, 0, 0, 0], dtype=np.float64)
+        N.check(N.lib().mw_load_model(h, pendulum_file.encode(), N.dptr(p), b""))
+        N.check(N.lib().mw_set_joint_param(h, 0, N.PARAM_COULOMB_FRICTION, 0.01))
+        v = ctypes.c_double()
+        N.check(N.lib().mw_joint_param(h, 0, N.PARAM_COULOMB_FRICTION, ctypes.byref(v)))
+        assert v.value == 0.01
+        assert N.lib().mw_set_joint_param(h, 3, N.PARAM_COULOMB_FRICTION, 0.01) == N.MW_EINVAL
+    finally:
+        N.lib().mw_destroy(h)

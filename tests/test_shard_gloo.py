@@ -1,0 +1,62 @@
+"""Multi-rank path on CPU (gloo, world_size 2): shard layout and the final
+observation all-gather used by bench.py (RCCL on the GPU box)."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, ws, port, n_global, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gym-ignition_amd", "python"))
+    from mwstep.shard import gather_obs, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    b, e = shard_range(n_global, rank, ws)
+    obs = torch.arange(b, e, dtype=torch.float32).repeat_interleave(4).reshape(-1, 4)
+    g = gather_obs(obs)
+    q.put((rank, b, e, g.numpy().tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_obs_world_order():
+    ws, n = 2, 10
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, n, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(ws)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res.sort()
+    assert [(b, e) for _, b, e, _ in res] == [(0, 5), (5, 10)]
+    expect = [[float(w)] * 4 for w in range(n)]
+    for _, _, _, g in res:
+        assert g == expect
+
+
+@pytest.mark.parametrize("n,ws", [(4096, 8), (1024, 3), (5, 8)])
+def test_shard_range_partitions(n, ws):
+    import sys
+    from mwstep.shard import shard_range
+    spans = [shard_range(n, r, ws) for r in range(ws)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(ws - 1))
+    assert max(e - b for b, e in spans) - min(e - b for b, e in spans) <= 1
