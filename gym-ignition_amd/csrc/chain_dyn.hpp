@@ -18,7 +18,14 @@
 //   - spatial inertias are kept in 3x3 blocks (A sym, B, C sym: 21 floats).
 #pragma once
 
+#ifdef MW_HOST_TEST
+// test-only host build of this header (tests/host_dyn): same code, CPU float32
+#include <cmath>
+#define __device__
+#define __forceinline__ inline
+#else
 #include <hip/hip_runtime.h>
+#endif
 
 #include "chain_params.hpp"
 

@@ -43,6 +43,7 @@ int fail(int code, const std::string& msg) {
 struct mw_sim {
     mw_config cfg{};
     bool own_stream = false;
+    bool stream_set = false;  // mw_set_stream called (NULL = the legacy default stream)
     hipStream_t stream = nullptr;
     bool loaded = false;
     bool initialized = false;
@@ -271,6 +272,18 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         return fail(MW_EPARSE, "chains with more than 9 dofs are not supported by this build");
     s->model_name = (name && *name) ? name : s->model.name;
     s->loaded = true;
+    s->n = s->model.dofs();
+    build_params(s);
+    return MW_OK;
+}
+
+int mw_device_params(const mw_sim* s, void* out, int32_t bytes) {
+    if (!s || !out) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (bytes < static_cast<int32_t>(sizeof(mw::ChainF))) return fail(MW_EINVAL, "buffer too small");
+    mw_sim* m = const_cast<mw_sim*>(s);
+    build_params(m);
+    std::memcpy(out, &m->h_params, sizeof(mw::ChainF));
     return MW_OK;
 }
 
@@ -279,9 +292,10 @@ int mw_initialize(mw_sim* s) {
     if (s->initialized) return MW_OK;
     if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
     MW_HIP(hipSetDevice(s->cfg.device));
-    if (!s->stream) {
+    if (!s->stream_set) {
         MW_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         s->own_stream = true;
+        s->stream_set = true;
     }
     s->n = s->model.dofs();
     s->nw = static_cast<size_t>(s->n) * s->W;
@@ -319,10 +333,11 @@ int mw_initialized(const mw_sim* s) { return (s && s->initialized) ? 1 : 0; }
 
 int mw_set_stream(mw_sim* s, void* stream) {
     if (!s) return fail(MW_EINVAL, "null simulator handle");
-    if (s->initialized && s->stream) MW_HIP(hipStreamSynchronize(s->stream));
+    if (s->initialized) MW_HIP(hipStreamSynchronize(s->stream));
     if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
     s->stream = static_cast<hipStream_t>(stream);
     s->own_stream = false;
+    s->stream_set = true;
     return MW_OK;
 }
 
@@ -362,6 +377,7 @@ int mw_set_gravity(mw_sim* s, const double g[3]) {
     if (s->stepped) return fail(MW_ESTATE, "the gravity can be changed only before the first run");
     std::memcpy(s->gravity, g, sizeof(s->gravity));
     if (s->initialized) return upload_params(s);
+    if (s->loaded) build_params(s);
     return MW_OK;
 }
 
@@ -434,6 +450,7 @@ int mw_set_joint_param(mw_sim* s, int32_t dof, int32_t which, double value) {
     default: return fail(MW_EINVAL, "unknown joint parameter");
     }
     if (s->initialized) return upload_params(s);
+    build_params(s);
     return MW_OK;
 }
 

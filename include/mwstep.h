@@ -88,7 +88,9 @@ void mw_destroy(mw_sim* sim);
 int mw_load_model(mw_sim* sim, const char* urdf, const double pose[7], const char* name);
 int mw_initialize(mw_sim* sim);
 int mw_initialized(const mw_sim* sim);
-/* Optional: launch on an external stream (e.g. torch's current stream). */
+/* Optional: launch on an external stream (e.g. torch's current stream);
+ * NULL selects the default stream.  Without this call the simulator creates
+ * its own non-blocking stream at mw_initialize. */
 int mw_set_stream(mw_sim* sim, void* hip_stream);
 
 /* ---- stepping (GazeboSimulator::run) ---- */
@@ -114,6 +116,10 @@ int mw_joint_param(const mw_sim* sim, int32_t dof, int32_t which, double* value)
  * {jtype, limited, E[9], r[3], axis[3], mass, com[3], Ic[6], damping,
  *  friction, lower, upper, effort, vel_limit} = 33 doubles, then gravity_base[3]. */
 int mw_model_export(const mw_sim* sim, double* out, int32_t len);
+
+/* Copy of the float32 parameter block the kernels read (struct ChainF of
+ * gym-ignition_amd/csrc/chain_params.hpp), for tests and tools. */
+int mw_device_params(const mw_sim* sim, void* out, int32_t bytes);
 
 /* ---- batched ScenarI/O accessors over worlds [w0, w0 + nw) ----
  * dofs == NULL selects all dofs in model order (ndofs ignored). */

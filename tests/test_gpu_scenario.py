@@ -128,12 +128,13 @@ def test_force_target_modes_and_consumption(require_gpu):
     assert linear.generalized_force_target() == 10.0
     gz.run()
     assert linear.generalized_force_target() == 0.0            # zero-filled after the run
+    assert not model.set_joint_generalized_force_targets([1.0, 1.0])  # pivot is Idle
     assert model.enable_history_of_applied_joint_forces(True, 3)
     hist = []
     for k in range(6):
-        assert model.set_joint_generalized_force_targets([0.1 * (k + 1), 0.0])
+        assert model.set_joint_generalized_force_targets([0.1 * (k + 1)], ["linear"])
         gz.run()
-        hist += [0.1 * (k + 1), 0.0]
+        hist += [0.1 * (k + 1), 0.0]      # the Idle pivot has no force command
         assert model.history_of_applied_joint_forces() == pytest.approx(hist[-6:])
     gz.close()
 

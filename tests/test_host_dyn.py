@@ -1,0 +1,106 @@
+"""The device dynamics code (gym-ignition_amd/csrc/chain_dyn.hpp) compiled for
+the host (g++, float32, test-only harness tests/host_dyn/harness.cpp) against
+the fp64 oracle -- catches kernel-math bugs without a GPU.  The parameter
+block is the exact float32 block the library uploads (mw_device_params)."""
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HARNESS = os.path.join(ROOT, "tests", "host_dyn", "harness.cpp")
+CSRC = os.path.join(ROOT, "gym-ignition_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def hd(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("hd") / "libhd.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", CSRC, HARNESS, "-o", out],
+                   check=True)
+    L = ctypes.CDLL(out)
+    L.hd_substep.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.c_void_p]
+    return L
+
+
+def _params(hd, path, joint_params=()):
+    from mwstep import native as N
+    cfg = N.MwConfig(1e-3, 1.0, 1, 1, 0, 0)
+    h = ctypes.c_void_p()
+    N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
+    try:
+        p = np.array([0, 0, 0, 1, 0, 0, 0.0])
+        N.check(N.lib().mw_load_model(h, path.encode(), N.dptr(p), b""))
+        for dof, which, v in joint_params:
+            N.check(N.lib().mw_set_joint_param(h, dof, which, v))
+        size = hd.hd_sizeof_chain()
+        buf = ctypes.create_string_buffer(size)
+        N.check(N.lib().mw_device_params(h, buf, size))
+        return buf
+    finally:
+        N.lib().mw_destroy(h)
+
+
+def _substep(hd, P, q, qd, tau, act, vc, cons, dual, pgs=20):
+    n = len(q)
+    f = lambda a, t=np.float32: np.array(a, dtype=t)   # copies: the harness works in place
+    q, qd, tau, vc, act = f(q), f(qd), f(tau), f(vc), f(act, np.uint8)
+    qdd = np.zeros(n, np.float32)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    assert hd.hd_substep(P, ptr(q), ptr(qd), ptr(tau), ptr(act), ptr(vc), 1e-3, pgs, int(cons),
+                         int(dual), ptr(qdd)) == 0
+    return q.astype(float), qd.astype(float), qdd.astype(float)
+
+
+@pytest.mark.parametrize("model", ["cartpole", "pendulum"])
+def test_unconstrained_substep(hd, oracle, cartpole_file, pendulum_file, model):
+    path = cartpole_file if model == "cartpole" else pendulum_file
+    P = _params(hd, path)
+    cm = oracle.load_urdf(path)
+    n = cm.n
+    rng = np.random.default_rng(5)
+    for _ in range(300):
+        q = rng.uniform(-2, 2, n).astype(np.float32)
+        qd = rng.uniform(-3, 3, n).astype(np.float32)
+        tau = rng.uniform(-40, 40, n).astype(np.float32)
+        got = _substep(hd, P, q, qd, tau, np.zeros(n), np.zeros(n), cons=False, dual=False)
+        ref = oracle.step(cm, 1e-3, q.astype(float), qd.astype(float), [oracle.FORCE] * n,
+                          tau.astype(float))
+        scale = 1.0 + np.abs(ref[2]).max()
+        assert np.abs(got[2] - ref[2]).max() <= 2e-6 * scale * 10
+        assert np.abs(got[1] - ref[1]).max() <= 1e-5
+        assert np.abs(got[0] - ref[0]).max() <= 1e-5
+
+
+def test_constraint_rows_and_damping(hd, oracle, pendulum_file, cartpole_file):
+    from mwstep import native as N
+    # pendulum with Coulomb friction + viscous damping (DUAL path), servo rows
+    P = _params(hd, pendulum_file, [(0, N.PARAM_COULOMB_FRICTION, 0.01), (0, N.PARAM_VISCOUS_FRICTION, 0.2)])
+    pm = oracle.load_urdf(pendulum_file)
+    pm.model.friction[0] = 0.01
+    pm.model.damping[0] = 0.2
+    rng = np.random.default_rng(9)
+    for _ in range(200):
+        q = rng.uniform(-3, 3, 1).astype(np.float32)
+        qd = rng.uniform(-0.02, 0.02, 1).astype(np.float32)
+        servo = rng.uniform() < 0.5
+        act = [1 if servo else 0]
+        vc = rng.uniform(-4, 4, 1).astype(np.float32)
+        got = _substep(hd, P, q, qd, [0.0], act, vc, cons=True, dual=True)
+        ref = oracle.step(pm, 1e-3, q.astype(float), qd.astype(float),
+                          [oracle.SERVO if servo else oracle.FORCE], vc.astype(float) if servo else [0.0])
+        assert np.abs(got[1] - ref[1]).max() <= 2e-5, (servo, got, ref)
+    # cartpole driven into the rail limit (limit row, 2 coupled dofs)
+    P = _params(hd, cartpole_file)
+    cm = oracle.load_urdf(cartpole_file)
+    q, qd = np.array([4.79, 0.2], np.float32), np.array([0.5, -1.0], np.float32)
+    qg, qdg = q.copy(), qd.copy()
+    qo, qdo = q.astype(float), qd.astype(float)
+    for _ in range(300):
+        qg, qdg, _ = _substep(hd, P, qg, qdg, [300.0, 0.0], [0, 0], [0, 0], cons=True, dual=False)
+        qo, qdo, *_ = oracle.step(cm, 1e-3, qo, qdo, [oracle.FORCE, oracle.PASSIVE], [300.0, 0.0], 20)
+    assert qg[0] <= 4.85 and abs(qg[0] - qo[0]) <= 1e-3 and np.abs(qdg - qdo).max() <= 1e-2
