@@ -213,10 +213,44 @@ struct Work {
     ImpulseFactor nf[DUAL ? N : 1];
 };
 
+// 1/x: the hardware reciprocal (1 ulp) on the device, IEEE division on the host
+__device__ __forceinline__ float rcp(float x) {
+#if defined(MW_HOST_TEST) || !defined(MW_FAST_MATH)
+    return 1.f / x;
+#else
+    return __builtin_amdgcn_rcpf(x);
+#endif
+}
+
+// sin and cos of a joint angle.  Cody-Waite reduction by pi/2 with a 3-part
+// constant and minimax polynomials on [-pi/4, pi/4] (~1 ulp for |q| < 2^16 rad,
+// i.e. > 10^4 turns); avoids libm's Payne-Hanek slow path (scratch + branches).
+__device__ __forceinline__ void sincos_joint(float x, float* s_out, float* c_out) {
+#if defined(MW_FAST_MATH)
+    const float k = rintf(x * 0.636619772367581343f);
+    float r = fmaf(-k, 1.57079625129699707031f, x);
+    r = fmaf(-k, 7.54978941586159635335e-8f, r);
+    r = fmaf(-k, 5.39030252995776476554e-15f, r);
+    const float r2 = r * r;
+    // sin(r) ~ r + r^3 P(r^2), cos(r) ~ 1 - r^2/2 + r^4 Q(r^2)  (Cephes sinf/cosf coefficients)
+    const float ps = fmaf(fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f);
+    const float sn = fmaf(ps * r2, r, r);
+    const float pc = fmaf(fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2, 4.166664568298827e-2f);
+    const float cs = fmaf(pc * r2, r2, fmaf(-0.5f, r2, 1.0f));
+    const int quad = static_cast<int>(k) & 3;
+    const float s1 = (quad & 1) ? cs : sn;
+    const float c1 = (quad & 1) ? sn : cs;
+    *s_out = (quad & 2) ? -s1 : s1;
+    *c_out = ((quad + 1) & 2) ? -c1 : c1;
+#else
+    sincosf(x, s_out, c_out);
+#endif
+}
+
 __device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p) {
     if (b.jtype == 0) {
         float s, c;
-        sincosf(q, &s, &c);
+        sincos_joint(q, &s, &c);
         const float ax = b.axis[0], ay = b.axis[1], az = b.axis[2], v = 1.f - c;
         const float J[9] = {c + ax * ax * v,      ax * ay * v - az * s, ax * az * v + ay * s,
                             ay * ax * v + az * s, c + ay * ay * v,      ay * az * v - ax * s,
@@ -280,7 +314,7 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
                   : SV{mul(AI.B, {b.axis[0], b.axis[1], b.axis[2]}),
                        mul(AI.C, {b.axis[0], b.axis[1], b.axis[2]})};
         const float D = proj(b, s.U);
-        s.psi = 1.f / (D + dt * b.damping);
+        s.psi = rcp(D + dt * b.damping);
         const SV AIeta = mul(AI, s.eta);
         s.tt = tau[i] - b.damping * qd[i] - proj(b, AIeta + Bi);
         if constexpr (DUAL) {
@@ -288,7 +322,7 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
             if (i < N - 1) AIn += carryN;
             const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
             W.nf[i].U = (b.jtype == 0) ? SV{mul(AIn.A, a), mulT(AIn.B, a)} : SV{mul(AIn.B, a), mul(AIn.C, a)};
-            W.nf[i].psi = 1.f / proj(b, W.nf[i].U);
+            W.nf[i].psi = rcp(proj(b, W.nf[i].U));
             if (i > 0) carryN = to_parent(s.R, s.p, downdate(AIn, W.nf[i].U, W.nf[i].psi));
         }
         if (i > 0) {
@@ -393,7 +427,7 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
                     viol = q[i] - b.upper;
                     if (viol >= 0.f) { on[i][0] = true; lo[i][0] = -INFINITY; hi[i][0] = 0.f; }
                 }
-                const float bounce = fminf(fmaxf(-viol * kErp / dt, -kMaxErv), kMaxErv);
+                const float bounce = fminf(fmaxf(-viol * kErp * rcp(dt), -kMaxErv), kMaxErv);
                 bb[i][0] = -qd[i] + bounce;
             }
             if (act[i] == kActServo) {
@@ -423,7 +457,7 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
 #pragma unroll
                     for (int t = 0; t < 3; ++t) {
                         if (on[d][t]) {
-                            const float xn = fminf(fmaxf(x[d][t] + (bb[d][t] - dq[d]) / Minv[d][d], lo[d][t]), hi[d][t]);
+                            const float xn = fminf(fmaxf(x[d][t] + (bb[d][t] - dq[d]) * rcp(Minv[d][d]), lo[d][t]), hi[d][t]);
                             const float delta = xn - x[d][t];
                             x[d][t] = xn;
 #pragma unroll
@@ -432,7 +466,7 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
                     }
                 }
             }
-            const float inv_dt = 1.f / dt;
+            const float inv_dt = rcp(dt);
 #pragma unroll
             for (int i = 0; i < N; ++i) {
                 qd[i] += dq[i];

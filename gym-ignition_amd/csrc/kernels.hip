@@ -85,6 +85,9 @@ __device__ __forceinline__ bool task_done(const TaskF& T, const float (&o)[4]) {
 template <int N, int KIND>
 __device__ __forceinline__ float task_reward(const TaskF& T, const float (&q)[N], const float (&qd)[N],
                                              const float (&o)[4], bool done) {
+    // no FMA contraction: the reward is bit-identical in the per-step and the
+    // fused-rollout kernels (contraction would otherwise depend on context)
+#pragma clang fp contract(off)
     if constexpr (KIND == 0 || KIND == 1) {
         float r = done ? 0.f : 1.f;
         if (T.reward_cart_at_center)

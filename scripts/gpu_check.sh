@@ -31,4 +31,12 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$tag" -o run --
   python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline > "$OUT/bench_prof_$tag.json" 2> "$OUT/prof_$tag.err"
 rc=$?; echo "rocprof rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/prof_$tag.err"
 find "$OUT/prof_$tag" -name "*stats*" | head
+stop_if_fatal $rc rocprof
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  echo "== pmc $ctr" | tee -a "$OUT/session.log"
+  timeout -k 10 180 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/pmc_${ctr}_$tag" -o run -- \
+    python3 scripts/profile_step.py > "$OUT/pmc_${ctr}_$tag.log" 2>&1
+  rc=$?; echo "pmc $ctr rc=$rc" | tee -a "$OUT/session.log"
+  stop_if_fatal $rc pmc
+done
 exit 0
