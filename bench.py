@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
+    p.add_argument("--no-sweep", action="store_true")
     return p.parse_args()
 
 
@@ -115,7 +116,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(stream):
+        ev_start.record(stream)
         for c in range(n_full):
             base = args.warmup + c * G
             act_buf.copy_(actions[base:base + G])
@@ -124,6 +127,7 @@ def main():
             base = args.warmup + n_full * G
             act_buf[:rem].copy_(actions[base:base + rem])
             tail.replay()
+        ev_end.record(stream)
         if world_size > 1:
             gathered = gather_obs(env.obs)  # final observation tensor, RCCL over xGMI
     torch.cuda.synchronize(dev)
@@ -136,19 +140,12 @@ def main():
         elapsed = float(tt.item())
     value = world_size * W * K / elapsed
 
-    # ------------------------------------- per-launch kernel time (HIP events)
-    launches = 200
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(launches)]
-    with torch.cuda.stream(stream):
-        for i in range(launches):
-            ev[i][0].record(stream)
-            env.step_raw(actions[i % total].data_ptr())
-            ev[i][1].record(stream)
-    stream.synchronize()
-    kernel_us = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+    # ---------------- per-launch time of the step kernel: HIP events recorded on
+    # the launch stream around the timed graph replays (K launches)
+    kernel_us = ev_start.elapsed_time(ev_end) * 1e3 / K
     bpe = algorithmic_bytes_per_env_step(env.sim.dofs, env.obs_dim)
     achieved_gbs = bpe * W / (kernel_us * 1e-6) / 1e9
+    traffic = pmc_traffic(args.task, W)
 
     # ------------------------------------------- fused open-loop rollout figure
     rollout = None
@@ -165,6 +162,12 @@ def main():
         rollout = {"steps_per_launch": T, "ms_per_launch": round(r_ms, 4),
                    "env_steps_per_s_per_gpu": round(W * T / (r_ms * 1e-3), 1),
                    "note": "open-loop (actions known ahead); not the headline value"}
+
+    # ---------------- world-count sweep (same kernel, graph mode): where the
+    # latency regime ends and the HBM / VALU bound takes over
+    sweep = None
+    if not args.no_sweep and world_size == 1:
+        sweep = world_sweep(args, dev, torch)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
@@ -202,11 +205,15 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
-                "traffic": None,
+                "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "kernel": "vecenv_step_kernel<2,0,false,true,false>",
-                "kernel_us_median": round(kernel_us, 3),
+                "kernel_us_per_launch": round(kernel_us, 3),
+                "timing": "HIP events on the launch stream over the K timed launches",
                 "bytes_per_env_step": bpe,
+                "algorithmic_bytes_per_launch": bpe * W,
+                "traffic_source": traffic["source"] if traffic else None,
             },
+            "world_sweep": sweep,
             "cpu_baseline": cpu,
             "obs_max_abs_err_vs_oracle": parity,
             "rollout_fused": rollout,
@@ -215,6 +222,56 @@ def main():
     env.close()
     if world_size > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(task, W):
+    """HBM bytes per launch of the step kernel from the committed PMC summary
+    (profiles/pmc_summary.json, produced by scripts/pmc_summary.py from
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of scripts/profile_step.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("task") != task or d.get("worlds") != W:
+        return None
+    return {"bytes_per_launch": d["bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+
+
+def world_sweep(args, dev, torch):
+    from mwstep.vecenv import VecEnv
+    out = []
+    for W in (16384, 65536, 262144, 1048576):
+        env = VecEnv(args.task, n_worlds=W, device=dev.index, seed=args.seed)
+        stream = torch.cuda.Stream(device=dev)
+        env.sim.set_stream(stream.cuda_stream)
+        G, reps = 20, 5
+        acts = torch.randint(0, 2, (G, W), device=dev, dtype=torch.int32) if env.discrete else \
+            (torch.rand((G, W), device=dev) * 2 - 1) * 50.0
+        with torch.cuda.stream(stream):
+            env.reset()
+            for g in range(G):
+                env.step_raw(acts[g].data_ptr())
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                for g in range(G):
+                    env.step_raw(acts[g].data_ptr())
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                graph.replay()
+            e1.record(stream)
+        stream.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / (G * reps)
+        bpe = algorithmic_bytes_per_env_step(env.sim.dofs, env.obs_dim)
+        out.append({"worlds": W, "us_per_step": round(us, 3), "env_steps_per_s": round(W / (us * 1e-6), 1),
+                    "achieved_GBs": round(bpe * W / (us * 1e-6) / 1e9, 1),
+                    "hbm_frac": round(bpe * W / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)})
+        env.close()
+        del acts, graph
+    return out
 
 
 def cpu_baseline_and_parity(args, env, actions, np, torch):

@@ -183,14 +183,27 @@ __device__ __forceinline__ SI rigid(const BodyF& b) {
     return I;
 }
 
+// NOTE: select components, never whole structs: `cond ? SV{..} : SV{..}` on
+// the runtime joint type becomes a select between two stack objects, i.e.
+// scratch stores + loads (seen as 2x WRITE_SIZE in the r01 PMC pass).
 __device__ __forceinline__ SV motion(const BodyF& b, float s) {
-    const f3 a = {b.axis[0] * s, b.axis[1] * s, b.axis[2] * s};
-    const f3 z = {0.f, 0.f, 0.f};
-    return (b.jtype == 0) ? SV{a, z} : SV{z, a};
+    const bool rev = (b.jtype == 0);
+    const float sw = rev ? s : 0.f, sv = rev ? 0.f : s;
+    return {{b.axis[0] * sw, b.axis[1] * sw, b.axis[2] * sw}, {b.axis[0] * sv, b.axis[1] * sv, b.axis[2] * sv}};
 }
 __device__ __forceinline__ float proj(const BodyF& b, const SV& x) {
     const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
     return (b.jtype == 0) ? dot(a, x.w) : dot(a, x.v);
+}
+
+// AI S for the body's joint: revolute S = [a; 0] -> [A a; B^T a],
+// prismatic S = [0; a] -> [B a; C a]  (component selects, see motion())
+__device__ __forceinline__ SV ais(const SI& AI, const BodyF& b) {
+    const bool rev = (b.jtype == 0);
+    const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
+    const f3 Aa = mul(AI.A, a), Bta = mulT(AI.B, a), Ba = mul(AI.B, a), Ca = mul(AI.C, a);
+    return {{rev ? Aa.x : Ba.x, rev ? Aa.y : Ba.y, rev ? Aa.z : Ba.z},
+            {rev ? Bta.x : Ca.x, rev ? Bta.y : Ca.y, rev ? Bta.z : Ca.z}};
 }
 
 // per-body factorization kept for the forward and impulse passes
@@ -308,11 +321,7 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         if (i < N - 1) AI += carry;
         const SV Bi = (i < N - 1) ? (Bown[i] + carryB) : Bown[i];
         // U = AI S
-        s.U = (b.jtype == 0)
-                  ? SV{mul(AI.A, {b.axis[0], b.axis[1], b.axis[2]}),
-                       mulT(AI.B, {b.axis[0], b.axis[1], b.axis[2]})}
-                  : SV{mul(AI.B, {b.axis[0], b.axis[1], b.axis[2]}),
-                       mul(AI.C, {b.axis[0], b.axis[1], b.axis[2]})};
+        s.U = ais(AI, b);
         const float D = proj(b, s.U);
         s.psi = rcp(D + dt * b.damping);
         const SV AIeta = mul(AI, s.eta);
@@ -320,8 +329,7 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         if constexpr (DUAL) {
             SI AIn = rigid(b);
             if (i < N - 1) AIn += carryN;
-            const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
-            W.nf[i].U = (b.jtype == 0) ? SV{mul(AIn.A, a), mulT(AIn.B, a)} : SV{mul(AIn.B, a), mul(AIn.C, a)};
+            W.nf[i].U = ais(AIn, b);
             W.nf[i].psi = rcp(proj(b, W.nf[i].U));
             if (i > 0) carryN = to_parent(s.R, s.p, downdate(AIn, W.nf[i].U, W.nf[i].psi));
         }
