@@ -210,7 +210,8 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
     constexpr int NO = (KIND == 3) ? 3 : 4;
     float q[N], qd[N];
     load_state<N>(S, W, w, q, qd);
-    uint32_t episode = V.episode[w];
+    const uint32_t episode0 = V.episode[w];
+    uint32_t episode = episode0;
     uint32_t steps = V.steps[w];
     uint8_t act[N];
     float vc[N];
@@ -253,7 +254,7 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
         store_obs<NO>(obs + idx * NO, o);
     }
     store_state<N>(S, W, w, q, qd);
-    V.episode[w] = episode;
+    if (episode != episode0) V.episode[w] = episode;  // changes only on auto-reset
     V.steps[w] = steps;
 }
 
