@@ -206,7 +206,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
-                "kernel": "vecenv_step_kernel<2,0,false,true,false>",
+                "kernel": f"vecenv_step_kernel<2,0,false,true,false,{env.sim.baked_model()}>"
+                          + (" (model constant-folded)" if env.sim.baked_model() else ""),
                 "kernel_us_per_launch": round(kernel_us, 3),
                 "timing": "HIP events on the launch stream over the K timed launches",
                 "bytes_per_env_step": bpe,

@@ -50,7 +50,8 @@ hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const Sim
 
 // T_steps == 0: one step with the per-step output layout; otherwise a fused
 // open-loop rollout of T_steps steps ([T, W] inputs and outputs).
-hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, const TaskF& T,
+// baked: id of a bit-identical shipped model (baked_models.hpp) or 0 (generic)
+hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, int baked, const TaskF& T,
                               const SimDev& S, const VecDev& V, const void* actions, float* obs,
                               float* reward, uint8_t* done, float* term_obs, int W, float dt,
                               int substeps, int pgs_iters, int T_steps, hipStream_t st);

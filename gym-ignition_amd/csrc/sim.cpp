@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -18,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "baked_models.hpp"
 #include "chain_params.hpp"
 #include "kernels.hpp"
 #include "model.hpp"
@@ -159,6 +161,22 @@ bool needs_cons(const mw_sim* s) {
 }
 bool needs_dual(const mw_sim* s) { return (s->h_params.flags & mw::kHasDamping) != 0; }
 
+// id of the shipped model whose float32 parameter block is bit-identical to the
+// loaded one (constant-folded kernels, baked_models.hpp), else 0.
+// MWSTEP_DISABLE_BAKED=1 forces the generic kernels.
+int baked_id(const mw_sim* s) {
+    const char* off = std::getenv("MWSTEP_DISABLE_BAKED");
+    if (off && *off && *off != '0') return 0;
+    const size_t words = 8 + 40 * static_cast<size_t>(s->n);
+    if (words * 4 == sizeof(mw::baked::kCartpoleHost) &&
+        std::memcmp(&s->h_params, &mw::baked::kCartpoleHost, words * 4) == 0)
+        return mw::baked::kCartpoleId;
+    if (words * 4 == sizeof(mw::baked::kPendulumHost) &&
+        std::memcmp(&s->h_params, &mw::baked::kPendulumHost, words * 4) == 0)
+        return mw::baked::kPendulumId;
+    return 0;
+}
+
 int pull_state(mw_sim* s) {
     if (!s->host_stale) return MW_OK;
     MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
@@ -274,6 +292,13 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     s->loaded = true;
     s->n = s->model.dofs();
     build_params(s);
+    return MW_OK;
+}
+
+int mw_baked_model(const mw_sim* s, int32_t* id) {
+    if (!s || !id) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    *id = baked_id(s);
     return MW_OK;
 }
 
@@ -736,7 +761,7 @@ static int vec_common(mw_vecenv* e, int32_t T, const void* a, float* o, float* r
         ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(to)) & 15u))
         return fail(MW_EINVAL, "obs buffers must be 16-byte aligned");
     mw_sim* s = e->sim;
-    MW_HIP(mw::launch_vecenv_step(s->d_params, s->n, needs_cons(s), needs_dual(s), e->task, s->dev, e->dev,
+    MW_HIP(mw::launch_vecenv_step(s->d_params, s->n, needs_cons(s), needs_dual(s), baked_id(s), e->task, s->dev, e->dev,
                                   a, o, r, d, to, s->W, static_cast<float>(s->cfg.step_size),
                                   s->cfg.steps_per_run, s->cfg.pgs_iters, T, s->stream));
     s->host_stale = true;

@@ -86,6 +86,7 @@ SIGNATURES = [
     ("mw_joint_param", ctypes.c_int, [_P, _I, _I, _D]),
     ("mw_model_export", ctypes.c_int, [_P, _D, _I]),
     ("mw_device_params", ctypes.c_int, [_P, _P, _I]),
+    ("mw_baked_model", ctypes.c_int, [_P, _IP]),
     ("mw_get_joint_positions", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
     ("mw_get_joint_velocities", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
     ("mw_get_joint_accelerations", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),

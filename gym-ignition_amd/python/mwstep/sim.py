@@ -166,6 +166,12 @@ class Simulator:
         N.check(N.lib().mw_model_export(self.handle, N.dptr(out), len(out)))
         return out
 
+    def baked_model(self) -> int:
+        """1/2 when the batched env runs the constant-folded cartpole/pendulum kernel."""
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_baked_model(self.handle, ctypes.byref(v)))
+        return v.value
+
     def device_ptr(self, field: str):
         p = ctypes.c_void_p()
         stride = ctypes.c_int64()

@@ -120,6 +120,10 @@ int mw_model_export(const mw_sim* sim, double* out, int32_t len);
 /* Copy of the float32 parameter block the kernels read (struct ChainF of
  * gym-ignition_amd/csrc/chain_params.hpp), for tests and tools. */
 int mw_device_params(const mw_sim* sim, void* out, int32_t bytes);
+/* Id of the shipped model whose parameter block the loaded model matches bit
+ * for bit (1 cartpole, 2 pendulum): the batched env then runs a kernel with the
+ * model constant-folded.  0 = generic kernel.  MWSTEP_DISABLE_BAKED=1 forces 0. */
+int mw_baked_model(const mw_sim* sim, int32_t* id);
 
 /* ---- batched ScenarI/O accessors over worlds [w0, w0 + nw) ----
  * dofs == NULL selects all dofs in model order (ndofs ignored). */

@@ -173,3 +173,30 @@ def test_c2_config_properties(require_gpu):
     assert int(ep.min()) >= T // 100    # every world finished >= 4 episodes
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("task,kind,model", [TASKS[0], TASKS[3]])
+def test_baked_kernel_matches_generic(require_gpu, oracle, task, kind, model, monkeypatch):
+    """The constant-folded kernel of a shipped model against the generic kernel
+    on the same inputs (rounding may differ: <= 1e-5 after 200 steps)."""
+    import torch
+    W, T = 1024, 200
+    _, a, _ = _pair(oracle, task, kind, model, W, seed=9)
+    _, b, _ = _pair(oracle, task, kind, model, W, seed=9)
+    assert a.sim.baked_model() in (1, 2)
+    a.reset()
+    b.reset()
+    acts = _actions(kind, T, W, seed=4)
+    worst = 0.0
+    for t in range(T):
+        x = torch.from_numpy(acts[t]).cuda()
+        monkeypatch.delenv("MWSTEP_DISABLE_BAKED", raising=False)
+        oa, _, da, _ = a.step(x)
+        monkeypatch.setenv("MWSTEP_DISABLE_BAKED", "1")
+        ob, _, db, _ = b.step(x)
+        same = (da == db)
+        worst = max(worst, float((oa[same] - ob[same]).abs().max()))
+    monkeypatch.delenv("MWSTEP_DISABLE_BAKED", raising=False)
+    assert worst <= 1e-5
+    a.close()
+    b.close()
