@@ -1,5 +1,5 @@
-// chain_dyn.hpp -- one engine substep of a fixed-base chain, float32, one
-// world per lane.  This is the MI355X restatement of DART 6.x World::step as
+// chain_dyn.hpp -- one engine substep of a fixed-base kinematic tree (serial
+// chains and branched models such as the Panda), float32, one world per lane.  This is the MI355X restatement of DART 6.x World::step as
 // driven by the reference's Physics system (Physics.cpp:1824-1835) [EXT]:
 //
 //   ABA with implicit joint damping  (Featherstone; DART GenericJoint::
@@ -10,7 +10,8 @@
 //   q  += dt * qd                    (integratePositions, semi-implicit Euler)
 //
 // Layout decisions for CDNA4:
-//   - N (dofs) is a template parameter and every per-body loop is unrolled, so
+//   - N (dofs) and the topology TOPO (parent of every body, chain_params.hpp)
+//     are template parameters and every per-body loop is unrolled, so
 //     all per-body state (transforms, articulated terms, Minv columns) lives
 //     in VGPRs; no runtime-indexed private arrays (they would go to scratch).
 //   - model parameters come from a uniform pointer with compile-time offsets:
@@ -281,45 +282,60 @@ __device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p
     }
 }
 
-// ABA with implicit damping: fills W and returns qdd.
-template <int N, bool DUAL>
+// ABA with implicit damping over the kinematic tree TOPO: fills W, returns qdd.
+// Per-body temporaries are arrays indexed by compile-time body numbers (every
+// loop is unrolled and parent_of() folds), so they stay in VGPRs; for a
+// serial chain only one carried articulated inertia is live at a time.
+template <int N, bool DUAL, Topo TOPO>
 __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&q)[N],
                                     const float (&qd)[N], const float (&tau)[N], float dt,
                                     float (&qdd)[N], Work<N, DUAL>& W) {
     SV Bown[N];
-    // forward kinematics, velocities, bias forces
-    SV V = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-    f3 g = {P->g[0], P->g[1], P->g[2]};
+    SV V[N];
+    f3 g[N];
+    // outward pass: kinematics, velocities, bias forces
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const BodyF& b = P->b[i];
         BodyState& s = W.bs[i];
+        const int pa = parent_of(TOPO, i);
         joint_pose(b, q[i], s.R, s.p);
         const SV Sq = motion(b, qd[i]);
-        V = ad_inv(s.R, s.p, V) + Sq;
-        g = mulT(s.R, g);
+        if (pa >= 0) {
+            V[i] = ad_inv(s.R, s.p, V[pa]) + Sq;
+            g[i] = mulT(s.R, g[pa]);
+        } else {
+            V[i] = Sq;
+            g[i] = mulT(s.R, mk(P->g[0], P->g[1], P->g[2]));
+        }
+        const SV& Vi = V[i];
         // eta = ad(V, S qd)
-        s.eta = {cross(V.w, Sq.w), cross(V.w, Sq.v) + cross(V.v, Sq.w)};
+        s.eta = {cross(Vi.w, Sq.w), cross(Vi.w, Sq.v) + cross(Vi.v, Sq.w)};
         // h = I V (rigid)
         const f3 c = {b.com[0], b.com[1], b.com[2]};
         const Sy Io = {b.Io[0], b.Io[1], b.Io[2], b.Io[3], b.Io[4], b.Io[5]};
-        const f3 hw = mul(Io, V.w) + b.mass * cross(c, V.v);
-        const f3 hv = b.mass * (V.v - cross(c, V.w));
+        const f3 hw = mul(Io, Vi.w) + b.mass * cross(c, Vi.v);
+        const f3 hv = b.mass * (Vi.v - cross(c, Vi.w));
         // B = -dad(V, IV) - I [0; g]
-        Bown[i].w = cross(V.w, hw) + cross(V.v, hv) - b.mass * cross(c, g);
-        Bown[i].v = cross(V.w, hv) - b.mass * g;
+        Bown[i].w = cross(Vi.w, hw) + cross(Vi.v, hv) - b.mass * cross(c, g[i]);
+        Bown[i].v = cross(Vi.w, hv) - b.mass * g[i];
     }
-    // backward pass
-    SI carry;
-    SI carryN;
-    SV carryB = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    // inward pass: articulated inertias / biases accumulate into the parent
+    SI carry[N];
+    SI carryN[DUAL ? N : 1];
+    SV carryB[N];
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
         const BodyF& b = P->b[i];
         BodyState& s = W.bs[i];
+        const int pa = parent_of(TOPO, i);
+        const bool kids = has_child(TOPO, N, i);
         SI AI = rigid(b);
-        if (i < N - 1) AI += carry;
-        const SV Bi = (i < N - 1) ? (Bown[i] + carryB) : Bown[i];
+        SV Bi = Bown[i];
+        if (kids) {
+            AI += carry[i];
+            Bi = Bi + carryB[i];
+        }
         // U = AI S
         s.U = ais(AI, b);
         const float D = proj(b, s.U);
@@ -328,73 +344,96 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         s.tt = tau[i] - b.damping * qd[i] - proj(b, AIeta + Bi);
         if constexpr (DUAL) {
             SI AIn = rigid(b);
-            if (i < N - 1) AIn += carryN;
+            if (kids) AIn += carryN[i];
             W.nf[i].U = ais(AIn, b);
             W.nf[i].psi = rcp(proj(b, W.nf[i].U));
-            if (i > 0) carryN = to_parent(s.R, s.p, downdate(AIn, W.nf[i].U, W.nf[i].psi));
+            if (pa >= 0) {
+                const SI c = to_parent(s.R, s.p, downdate(AIn, W.nf[i].U, W.nf[i].psi));
+                if (first_inward(TOPO, N, i)) carryN[pa] = c;
+                else carryN[pa] += c;
+            }
         }
-        if (i > 0) {
-            carry = to_parent(s.R, s.p, downdate(AI, s.U, s.psi));
+        if (pa >= 0) {
+            const SI c = to_parent(s.R, s.p, downdate(AI, s.U, s.psi));
             const SV beta = Bi + AIeta + (s.psi * s.tt) * s.U;
-            carryB = dad_inv(s.R, s.p, beta);
+            const SV cb = dad_inv(s.R, s.p, beta);
+            if (first_inward(TOPO, N, i)) { carry[pa] = c; carryB[pa] = cb; }
+            else { carry[pa] += c; carryB[pa] = carryB[pa] + cb; }
         }
     }
-    // forward accelerations
-    SV a = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    // outward pass: accelerations
+    SV a[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const BodyF& b = P->b[i];
         const BodyState& s = W.bs[i];
-        const SV ap = ad_inv(s.R, s.p, a);
-        qdd[i] = s.psi * (s.tt - dot(s.U, ap));
-        a = ap + s.eta + motion(b, qdd[i]);
+        const int pa = parent_of(TOPO, i);
+        if (pa >= 0) {
+            const SV ap = ad_inv(s.R, s.p, a[pa]);
+            qdd[i] = s.psi * (s.tt - dot(s.U, ap));
+            a[i] = ap + s.eta + motion(b, qdd[i]);
+        } else {
+            qdd[i] = s.psi * s.tt;
+            a[i] = s.eta + motion(b, qdd[i]);
+        }
     }
 }
 
-// column j of M^-1 (velocity change of every dof for a unit impulse on dof j)
-template <int N, bool DUAL, int J>
+// column j of M^-1 (velocity change of every dof for a unit impulse on dof j):
+// the bias impulse climbs from J to the root (only J's ancestors are
+// touched), then the outward pass reaches every body.
+template <int N, bool DUAL, Topo TOPO, int J>
 __device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const Work<N, DUAL>& W,
                                             float (&col)[N]) {
     float u[N];
-    SV Bimp = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    SV Bimp[N];
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
-        if (i > J) { u[i] = 0.f; continue; }
-        if (i == J) { u[i] = 1.f; continue; }
-        SV U1;
-        float psi1;
-        if constexpr (DUAL) { U1 = W.nf[i + 1].U; psi1 = W.nf[i + 1].psi; }
-        else { U1 = W.bs[i + 1].U; psi1 = W.bs[i + 1].psi; }
-        Bimp = dad_inv(W.bs[i + 1].R, W.bs[i + 1].p, Bimp + (psi1 * u[i + 1]) * U1);
-        u[i] = -proj(P->b[i], Bimp);
+        if (!on_path(TOPO, i, J)) { u[i] = 0.f; continue; }
+        u[i] = (i == J) ? 1.f : -proj(P->b[i], Bimp[i]);
+        const int pa = parent_of(TOPO, i);
+        if (pa >= 0) {
+            SV U;
+            float psi;
+            if constexpr (DUAL) { U = W.nf[i].U; psi = W.nf[i].psi; }
+            else { U = W.bs[i].U; psi = W.bs[i].psi; }
+            if (i == J) Bimp[pa] = dad_inv(W.bs[i].R, W.bs[i].p, (psi * u[i]) * U);
+            else Bimp[pa] = dad_inv(W.bs[i].R, W.bs[i].p, Bimp[i] + (psi * u[i]) * U);
+        }
     }
-    SV dv = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    SV dv[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         SV U;
         float psi;
         if constexpr (DUAL) { U = W.nf[i].U; psi = W.nf[i].psi; }
         else { U = W.bs[i].U; psi = W.bs[i].psi; }
-        const SV dvp = ad_inv(W.bs[i].R, W.bs[i].p, dv);
-        col[i] = psi * (u[i] - dot(U, dvp));
-        dv = dvp + motion(P->b[i], col[i]);
+        const int pa = parent_of(TOPO, i);
+        if (pa >= 0) {
+            const SV dvp = ad_inv(W.bs[i].R, W.bs[i].p, dv[pa]);
+            col[i] = psi * (u[i] - dot(U, dvp));
+            dv[i] = dvp + motion(P->b[i], col[i]);
+        } else {
+            col[i] = psi * u[i];
+            dv[i] = motion(P->b[i], col[i]);
+        }
     }
 }
 
-template <int N, bool DUAL, int J = 0>
+template <int N, bool DUAL, Topo TOPO, int J = 0>
 __device__ __forceinline__ void minv_columns(const ChainF* __restrict__ P, const Work<N, DUAL>& W,
                                              const bool (&need)[N], float (&Minv)[N][N]) {
     if constexpr (J < N) {
         if (need[J]) {
             float col[N];
-            minv_column<N, DUAL, J>(P, W, col);
+            minv_column<N, DUAL, TOPO, J>(P, W, col);
 #pragma unroll
             for (int k = 0; k < N; ++k) Minv[k][J] = col[k];
         } else {
 #pragma unroll
             for (int k = 0; k < N; ++k) Minv[k][J] = 0.f;
         }
-        minv_columns<N, DUAL, J + 1>(P, W, need, Minv);
+        minv_columns<N, DUAL, TOPO, J + 1>(P, W, need, Minv);
     }
 }
 
@@ -404,13 +443,13 @@ constexpr float kMaxErv = 10.f;
 
 // One engine substep.  act[i]: kActForce (tau[i] is the clipped command) or
 // kActServo (vcmd[i] is the velocity command).  CONS enables the LCP rows.
-template <int N, bool DUAL, bool CONS>
+template <int N, bool DUAL, bool CONS, Topo TOPO = chain_topo(N)>
 __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
                                         const float (&tau)[N], const uint8_t (&act)[N],
                                         const float (&vcmd)[N], float dt, int pgs_iters,
                                         float (&qdd)[N]) {
     Work<N, DUAL> W;
-    aba<N, DUAL>(P, q, qd, tau, dt, qdd, W);
+    aba<N, DUAL, TOPO>(P, q, qd, tau, dt, qdd, W);
 #pragma unroll
     for (int i = 0; i < N; ++i) qd[i] += dt * qdd[i];
 
@@ -455,7 +494,7 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
         }
         if (any) {
             float Minv[N][N];
-            minv_columns<N, DUAL>(P, W, need, Minv);
+            minv_columns<N, DUAL, TOPO>(P, W, need, Minv);
             float x[N][3], dq[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) { x[i][0] = x[i][1] = x[i][2] = 0.f; dq[i] = 0.f; }

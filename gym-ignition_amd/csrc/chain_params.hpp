@@ -1,6 +1,6 @@
 // chain_params.hpp -- device-side (float32) model parameters of a fixed-base
-// chain, shared by every world of a simulator (read-only, uniform across a
-// wave, so the compiler keeps them on the scalar path).
+// kinematic tree, shared by every world of a simulator (read-only, uniform
+// across a wave, so the compiler keeps them on the scalar path).
 #pragma once
 
 #include <cstdint>
@@ -27,7 +27,8 @@ struct BodyF {
     float vel_limit;   // servo command clip
     int32_t limited;   // position limits enforced (LCP row)
     float Ea[3];       // E * axis (prismatic translation direction in the parent)
-    float pad_[4];
+    int32_t parent;    // parent body (< own index), -1 = base
+    float pad_[3];
 };
 static_assert(sizeof(BodyF) == 40 * 4, "BodyF layout");
 
@@ -41,7 +42,52 @@ struct ChainF {
     BodyF b[kMaxBodies];
 };
 
-// Per-dof actuation inside the engine (DART actuator types).
-enum : uint8_t { kActForce = 0, kActServo = 1 };
+// Per-dof actuation of a world's joint.  Force / Servo are DART actuator
+// types; PidPos / PidVel are joints in Position / Velocity control mode whose
+// force comes from the JointController PID (a force actuator to the engine).
+enum : uint8_t { kActForce = 0, kActServo = 1, kActPidPos = 2, kActPidVel = 3 };
+
+// ignition::math::PID parameters of one joint (float32 copy of the fp64
+// values; Joint::setPID, Joint.cpp:479-525).  Ranges with max < min disable
+// the corresponding clamp (ign-math semantics).
+struct PidF {
+    float p, i, d, imax, imin, cmdmax, cmdmin, offset;
+};
+
+// PIDs of every dof of a simulator (kernel argument, passed by value).
+struct PidSet {
+    PidF g[kMaxKernelDofs];
+};
+
+// Kinematic topology as a compile-time constant: 4 bits per body holding
+// parent + 1 (so 0 = the base).  Kernels are instantiated per topology.
+using Topo = uint64_t;
+constexpr Topo chain_topo(int n) {
+    Topo t = 0;
+    for (int i = 0; i < n; ++i) t |= static_cast<Topo>(i) << (4 * i);
+    return t;
+}
+constexpr int parent_of(Topo t, int i) { return static_cast<int>((t >> (4 * i)) & 15u) - 1; }
+// i has at least one child among bodies i+1..n-1
+constexpr bool has_child(Topo t, int n, int i) {
+    for (int k = i + 1; k < n; ++k)
+        if (parent_of(t, k) == i) return true;
+    return false;
+}
+// i is the highest-numbered child of its parent, i.e. the first one an
+// inward (n-1 .. 0) pass reaches
+constexpr bool first_inward(Topo t, int n, int i) {
+    for (int k = i + 1; k < n; ++k)
+        if (parent_of(t, k) == parent_of(t, i)) return false;
+    return true;
+}
+// i == j or i is an ancestor of j
+constexpr bool on_path(Topo t, int i, int j) {
+    for (int k = j; k >= 0; k = parent_of(t, k))
+        if (k == i) return true;
+    return false;
+}
+// the Franka Panda: joints 1..7 in a chain, both fingers hang off the hand
+constexpr Topo kPandaTopo = chain_topo(7) | (static_cast<Topo>(7) << 28) | (static_cast<Topo>(7) << 32);
 
 }  // namespace mw

@@ -154,42 +154,88 @@ __device__ __forceinline__ void store_obs(float* __restrict__ dst, const float (
 
 // ---------------------------------------------------------- kernels -----
 
-template <int N, bool DUAL, bool CONS>
-__global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restrict__ P, SimDev S, int W,
-                                                           float dt, int substeps, int paused,
-                                                           int pgs_iters) {
+// ignition::math::PID::Update [EXT: ign-math6, restated in oracle.c
+// or_pid_update]; returns false (and leaves the state) for a non-finite error
+__device__ __forceinline__ bool pid_update(const PidF& g, float err, float inv_dt, float dt, float& e_last,
+                                           float& ierr, float& cmd) {
+    if (!isfinite(err)) return false;
+    const float pterm = g.p * err;
+    ierr = ierr + g.i * dt * err;
+    if (g.imax >= g.imin) ierr = fminf(fmaxf(ierr, g.imin), g.imax);
+    const float derr = (err - e_last) * inv_dt;
+    e_last = err;
+    float u = -pterm - ierr - g.d * derr + g.offset;
+    if (g.cmdmax >= g.cmdmin) u = fminf(fmaxf(u, g.cmdmin), g.cmdmax);
+    cmd = u;
+    return true;
+}
+
+template <int N, bool DUAL, bool CONS, Topo TOPO>
+__global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restrict__ P, SimDev S, PidSet pid,
+                                                           int W, RunArgs A) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     float q[N], qd[N];
     load_state<N>(S, W, w, q, qd);
-    // UpdatePhysics: velocity reset, then position reset (Physics.cpp:1330-1375)
-#pragma unroll
-    for (int d = 0; d < N; ++d) {
-        const uint8_t f = S.rflag[d * W + w];
-        if (f) {
-            if (f & 2u) qd[d] = S.rqd[d * W + w];
-            if (f & 1u) q[d] = S.rq[d * W + w];
-            S.rflag[d * W + w] = 0;
-        }
-    }
-    if (!paused) {
-        float cmd[N], vc[N], tau[N], qdd[N];
-        uint8_t act[N];
+    if (A.first) {
+        // UpdatePhysics: velocity reset, then position reset (Physics.cpp:1330-1375);
+        // Joint::reset*/setControlMode/setPID also reset the joint PID (Joint.cpp:148-151)
 #pragma unroll
         for (int d = 0; d < N; ++d) {
-            cmd[d] = S.cmd[d * W + w];
+            const uint8_t f = S.rflag[d * W + w];
+            if (f) {
+                if (f & 2u) qd[d] = S.rqd[d * W + w];
+                if (f & 1u) q[d] = S.rq[d * W + w];
+                if (f & 4u) { S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; }
+                S.rflag[d * W + w] = 0;
+            }
+        }
+    }
+    if (!A.paused) {
+        float cmd[N], vc[N], tau[N], qdd[N];
+        uint8_t act[N];
+        bool any_pid = false;
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            cmd[d] = A.first ? S.cmd[d * W + w] : 0.f;
             act[d] = S.act[d * W + w];
             vc[d] = S.vtgt[d * W + w];
+            any_pid = any_pid || act[d] >= kActPidPos;
         }
-        for (int s = 0; s < substeps; ++s) {
+        for (int s = 0; s < A.substeps; ++s) {
+            const bool gate = (A.pid_gate >> s) & 1u;
 #pragma unroll
             for (int d = 0; d < N; ++d) {
-                // SetForce -> GenericJoint::setCommand clips to +-effort; the command
-                // only acts on the first substep (UpdateSim zero-fills it afterwards)
+                // SetForce -> GenericJoint::setCommand clips to +-effort; a Force-mode
+                // command only acts on the first substep (UpdateSim zero-fills it)
                 const float e = P->b[d].effort;
                 tau[d] = (act[d] == kActForce && s == 0) ? fminf(fmaxf(cmd[d], -e), e) : 0.f;
             }
-            substep<N, DUAL, CONS>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
+            if (any_pid) {
+                // JointController::PreUpdate (JointController.cpp:195-262): PID force of
+                // Position / Velocity joints, recomputed when the period gate opens,
+                // otherwise the last command (pid.Cmd()); error = current - target (:308)
+#pragma unroll
+                for (int d = 0; d < N; ++d) {
+                    if (act[d] >= kActPidPos) {
+                        const size_t k = static_cast<size_t>(d) * W + w;
+                        float u = S.pid_u[k];
+                        if (gate) {
+                            const bool pos = (act[d] == kActPidPos);
+                            const float err = pos ? (q[d] - S.ptgt[k]) : (qd[d] - vc[d]);
+                            float el = S.pid_e[k], ie = S.pid_i[k];
+                            if (pid_update(pid.g[d], err, A.inv_dt, A.dt, el, ie, u)) {
+                                S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
+                            } else {
+                                u = 0.f;
+                            }
+                        }
+                        const float e = P->b[d].effort;
+                        tau[d] = fminf(fmaxf(u, -e), e);
+                    }
+                }
+            }
+            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd);
         }
 #pragma unroll
         for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];
@@ -287,19 +333,19 @@ dim3 grid_for(int W, int block) { return dim3(static_cast<unsigned>((W + block -
 // (each wave runs a long dependent chain); 256 once there is work for all.
 int block_for(int W) { return (W <= 64 * 256) ? 64 : 256; }
 
-template <int N>
-hipError_t scenario_n(const ChainF* P, bool cons, bool dual, const SimDev& S, int W, float dt,
-                      int substeps, int paused, int pgs, hipStream_t st) {
+template <int N, Topo TOPO>
+hipError_t scenario_n(const ChainF* P, bool cons, bool dual, const SimDev& S, const PidSet& pid, int W,
+                      const RunArgs& a, hipStream_t st) {
     const int B = block_for(W);
     if (!cons)
-        hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, false>), grid_for(W, B), dim3(B), 0, st, P,
-                           S, W, dt, substeps, paused, pgs);
+        hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, false, TOPO>), grid_for(W, B), dim3(B), 0, st, P,
+                           S, pid, W, a);
     else if (!dual)
-        hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, true>), grid_for(W, B), dim3(B), 0, st, P,
-                           S, W, dt, substeps, paused, pgs);
+        hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, true, TOPO>), grid_for(W, B), dim3(B), 0, st, P,
+                           S, pid, W, a);
     else
-        hipLaunchKernelGGL((dev::scenario_run_kernel<N, true, true>), grid_for(W, B), dim3(B), 0, st, P,
-                           S, W, dt, substeps, paused, pgs);
+        hipLaunchKernelGGL((dev::scenario_run_kernel<N, true, true, TOPO>), grid_for(W, B), dim3(B), 0, st, P,
+                           S, pid, W, a);
     return hipGetLastError();
 }
 
@@ -337,18 +383,31 @@ hipError_t vec_nk(const ChainF* P, bool cons, bool dual, int baked, const TaskF&
 
 }  // namespace
 
-hipError_t launch_scenario_run(const ChainF* P, int n, bool cons, bool dual, const SimDev& S, int W,
-                               float dt, int substeps, int paused, int pgs_iters, hipStream_t st) {
+int kernel_topology(const int* parents, int n) {
+    bool chain = true, panda = (n == 9);
+    for (int i = 0; i < n; ++i) {
+        chain = chain && parents[i] == i - 1;
+        panda = panda && parents[i] == parent_of(kPandaTopo, i);
+    }
+    if (chain && n >= 1 && n <= 9) return 0;
+    if (panda) return 1;
+    return -1;
+}
+
+hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, const SimDev& S,
+                               const PidSet& pid, int W, const RunArgs& a, hipStream_t st) {
+    if (topo == 1) return scenario_n<9, kPandaTopo>(P, cons, dual, S, pid, W, a, st);
+    if (topo != 0) return hipErrorInvalidValue;
     switch (n) {
-    case 1: return scenario_n<1>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 2: return scenario_n<2>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 3: return scenario_n<3>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 4: return scenario_n<4>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 5: return scenario_n<5>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 6: return scenario_n<6>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 7: return scenario_n<7>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 8: return scenario_n<8>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
-    case 9: return scenario_n<9>(P, cons, dual, S, W, dt, substeps, paused, pgs_iters, st);
+    case 1: return scenario_n<1, chain_topo(1)>(P, cons, dual, S, pid, W, a, st);
+    case 2: return scenario_n<2, chain_topo(2)>(P, cons, dual, S, pid, W, a, st);
+    case 3: return scenario_n<3, chain_topo(3)>(P, cons, dual, S, pid, W, a, st);
+    case 4: return scenario_n<4, chain_topo(4)>(P, cons, dual, S, pid, W, a, st);
+    case 5: return scenario_n<5, chain_topo(5)>(P, cons, dual, S, pid, W, a, st);
+    case 6: return scenario_n<6, chain_topo(6)>(P, cons, dual, S, pid, W, a, st);
+    case 7: return scenario_n<7, chain_topo(7)>(P, cons, dual, S, pid, W, a, st);
+    case 8: return scenario_n<8, chain_topo(8)>(P, cons, dual, S, pid, W, a, st);
+    case 9: return scenario_n<9, chain_topo(9)>(P, cons, dual, S, pid, W, a, st);
     default: return hipErrorInvalidValue;
     }
 }

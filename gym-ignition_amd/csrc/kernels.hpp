@@ -18,8 +18,23 @@ struct SimDev {
     float* vtgt = nullptr;   // JointVelocityTarget (VelocityFollowerDart)
     float* rq = nullptr;     // JointPositionReset values
     float* rqd = nullptr;    // JointVelocityReset values
-    uint8_t* act = nullptr;  // kActForce / kActServo
-    uint8_t* rflag = nullptr;  // bit0 position reset pending, bit1 velocity reset pending
+    float* ptgt = nullptr;   // JointPositionTarget (Position mode)
+    uint8_t* act = nullptr;  // kActForce / kActServo / kActPidPos / kActPidVel
+    uint8_t* rflag = nullptr;  // bit0 position reset, bit1 velocity reset, bit2 PID reset pending
+    // JointPID state (ignition::math::PID pErrLast, iErr, cmd), device only
+    float* pid_e = nullptr;
+    float* pid_i = nullptr;
+    float* pid_u = nullptr;
+};
+
+// One launch of the scenario kernel covers up to 64 substeps of a run.
+struct RunArgs {
+    float dt, inv_dt;
+    int substeps;         // substeps of this launch (<= 64)
+    int paused;
+    int pgs_iters;
+    int first;            // first launch of the run: resets + force commands apply
+    uint64_t pid_gate;    // bit s: the JointController computes a new PID force at substep s
 };
 
 // Task description for the device-side env (see sim.cpp for the sources).
@@ -42,8 +57,12 @@ struct VecDev {
 };
 
 // Returns hipSuccess or the launch error.
-hipError_t launch_scenario_run(const ChainF* P, int n, bool cons, bool dual, const SimDev& S, int W,
-                               float dt, int substeps, int paused, int pgs_iters, hipStream_t st);
+// topology id of a model's parent list: 0 = serial chain, 1 = Panda tree,
+// -1 = not compiled into this build
+int kernel_topology(const int* parents, int n);
+
+hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, const SimDev& S,
+                               const PidSet& pid, int W, const RunArgs& a, hipStream_t st);
 
 hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
                                const VecDev& V, float* obs, int W, hipStream_t st);

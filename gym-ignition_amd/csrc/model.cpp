@@ -384,28 +384,42 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
         }
     }
 
-    // the moving joints must form a serial chain hanging from the base body
-    std::string cur = base;
-    std::vector<Joint> chain;
-    for (;;) {
-        std::vector<const Joint*> nxt;
-        for (auto& j : joints)
-            if (owner[j.parent] == cur) nxt.push_back(&j);
-        if (nxt.empty()) break;
-        if (nxt.size() > 1)
-            throw std::runtime_error("branched (tree) models are not supported yet: link '" + cur +
-                                     "' has several moving child joints");
-        chain.push_back(*nxt[0]);
-        cur = nxt[0]->child;
+    // the moving joints form a tree hanging from the base body; bodies are
+    // numbered depth-first (children in declaration order), so parent < child
+    std::vector<const Joint*> order;
+    std::vector<int> parent_of;
+    {
+        std::vector<std::pair<const Joint*, int>> st;  // (joint, parent body index)
+        auto push_children = [&](const std::string& link, int pidx) {
+            std::vector<const Joint*> kids;
+            for (auto& j : joints)
+                if (owner[j.parent] == link) kids.push_back(&j);
+            for (auto it = kids.rbegin(); it != kids.rend(); ++it) st.push_back({*it, pidx});
+        };
+        push_children(base, -1);
+        while (!st.empty()) {
+            const auto [j, pidx] = st.back();
+            st.pop_back();
+            const int me = static_cast<int>(order.size());
+            if (order.size() >= joints.size())
+                throw std::runtime_error("the model's joints do not form a tree (a link has several parents)");
+            order.push_back(j);
+            parent_of.push_back(pidx);
+            push_children(j->child, me);
+        }
     }
-    if (chain.size() != joints.size())
-        throw std::runtime_error("the model's moving joints do not form a single chain");
+    if (order.size() != joints.size())
+        throw std::runtime_error("the model's moving joints are not all connected to the base link");
+    std::vector<Joint> chain;
+    for (const Joint* j : order) chain.push_back(*j);
 
     out.base_link = base;
     out.base_R = baseR;
     out.base_p = baseP;
-    for (const Joint& j : chain) {
+    for (size_t k = 0; k < chain.size(); ++k) {
+        const Joint& j = chain[k];
         ChainBody b;
+        b.parent = parent_of[k];
         b.joint_name = j.name;
         b.link_name = j.child;
         b.type = (j.type == "prismatic") ? JType::Prismatic : JType::Revolute;

@@ -1,4 +1,4 @@
-// model.hpp -- host-side model compiler: URDF -> flat fixed-base chain.
+// model.hpp -- host-side model compiler: URDF -> flat fixed-base kinematic tree.
 //
 // Mirrors what the reference does when a URDF is inserted
 // (World::insertModel, cpp/scenario/gazebo/src/World.cpp:70-180 ->
@@ -24,6 +24,7 @@ enum class JType : int { Revolute = 0, Prismatic = 1 };
 struct ChainBody {
     std::string joint_name;
     std::string link_name;
+    int parent = -1;               // parent body index (< own index), -1 = base
     JType type = JType::Revolute;
     bool continuous = false;       // URDF "continuous": revolute without limits
     bool limited = false;          // position limits enforced
@@ -43,7 +44,7 @@ struct ChainModel {
     std::string base_link;         // canonical (base) link
     std::array<double, 9> base_R{};  // base pose in world
     std::array<double, 3> base_p{};
-    std::vector<ChainBody> bodies; // bodies[i].parent == i-1 (-1 = base)
+    std::vector<ChainBody> bodies; // depth-first: bodies[i].parent < i (-1 = base)
     int dofs() const { return static_cast<int>(bodies.size()); }
 };
 

@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -53,11 +54,24 @@ struct mw_sim {
     bool servo_used = false;  // a joint was put in VelocityFollowerDart
     bool host_stale = false;  // device state changed by the VecEnv path
     bool cmd_dirty = true;
+    bool ptgt_dirty = false;  // host position targets newer than the device copy
+    bool ptgt_stale = false;  // device position targets newer than the host mirror
+    bool ptgt_view = false;   // a device view of the targets was handed out (always re-read)
+    int topo = 0;             // kernel topology id (kernels.hpp: kernel_topology)
     mw::ChainModel model;
     std::string model_name;
     double gravity[3] = {0.0, 0.0, -9.8};  // sdformat default world gravity
     int64_t iterations = 0;
     int64_t dt_ns = 0;
+    // JointController (one per model): Model.cpp:181-185 initialises the period
+    // to the maximum duration; the plugin is inserted by the first Position /
+    // Velocity / VelocityFollowerDart joint (Joint.cpp:376-404)
+    bool controller = false;
+    int64_t period_ns = std::numeric_limits<int64_t>::max();
+    int64_t prev_ns = 0;      // JointController prevUpdateTime (0 = first iteration)
+    // JointPID per dof in scenario::core::PID order {p, i, d, cmdMin, cmdMax,
+    // cmdOffset, iMin, iMax}; default = Joint.cpp:63 DefaultPID
+    std::vector<std::array<double, 8>> pid;
 
     int n = 0, W = 0;
     size_t nw = 0;  // n * W
@@ -68,6 +82,9 @@ struct mw_sim {
     size_t block_bytes = 0, cmd_off = 0, cmd_bytes = 0, state_bytes = 0;
     mw::ChainF* d_params = nullptr;
     mw::ChainF h_params{};
+    // [ptgt | pid_e | pid_i | pid_u] on the device; h_ptgt mirrors ptgt
+    float* d_aux = nullptr;
+    float* h_ptgt = nullptr;
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -143,6 +160,7 @@ void build_params(mw_sim* s) {
         f.effort = clampf(b.effort);
         f.vel_limit = clampf(b.vel_limit);
         f.limited = b.limited ? 1 : 0;
+        f.parent = b.parent;
         if (b.damping != 0.0) flags |= mw::kHasDamping;
         if (b.limited) flags |= mw::kHasLimits;
         if (b.friction != 0.0) flags |= mw::kHasFriction;
@@ -184,6 +202,35 @@ int pull_state(mw_sim* s) {
     s->host_stale = false;
     return MW_OK;
 }
+
+// position targets written on the device (mw_device_ptr) -> host mirror
+int pull_ptgt(mw_sim* s) {
+    if (!s->ptgt_stale) return MW_OK;
+    MW_HIP(hipMemcpyAsync(s->h_ptgt, s->d_aux, s->nw * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    for (size_t k = 0; k < s->nw; ++k) s->ptgt[k] = s->h_ptgt[k];
+    s->ptgt_stale = s->ptgt_view;
+    return MW_OK;
+}
+
+float to_f32(double v) {
+    const double big = static_cast<double>(std::numeric_limits<float>::max());
+    return static_cast<float>(v > big ? INFINITY : (v < -big ? -INFINITY : v));
+}
+
+mw::PidSet pid_set(const mw_sim* s) {
+    mw::PidSet P{};
+    for (int d = 0; d < s->n && d < mw::kMaxKernelDofs; ++d) {
+        const auto& g = s->pid[d];
+        P.g[d] = {to_f32(g[0]), to_f32(g[1]), to_f32(g[2]), to_f32(g[7]), to_f32(g[6]),
+                  to_f32(g[4]), to_f32(g[3]), to_f32(g[5])};
+    }
+    return P;
+}
+
+// ignition::math::PID(1, 0.1, 0.01, -1, 0, -1, 0, 0) (Joint.cpp:63) as
+// {p, i, d, cmdMin, cmdMax, cmdOffset, iMin, iMax}
+constexpr std::array<double, 8> kDefaultPid = {1.0, 0.1, 0.01, 0.0, -1.0, 0.0, 0.0, -1.0};
 
 // resolve a (dofs, ndofs) selection; dofs == NULL -> all dofs
 int selection(const mw_sim* s, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs,
@@ -271,7 +318,9 @@ void mw_destroy(mw_sim* s) {
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         (void)hipFree(s->d_block);
         (void)hipFree(s->d_params);
+        (void)hipFree(s->d_aux);
         (void)hipHostFree(s->h_block);
+        (void)hipHostFree(s->h_ptgt);
         if (s->own_stream) (void)hipStreamDestroy(s->stream);
     }
     delete s;
@@ -287,7 +336,16 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         return fail(MW_EPARSE, e.what());
     }
     if (s->model.dofs() > mw::kMaxKernelDofs || s->model.dofs() > 9)
-        return fail(MW_EPARSE, "chains with more than 9 dofs are not supported by this build");
+        return fail(MW_EPARSE, "models with more than 9 dofs are not supported by this build");
+    {
+        std::vector<int> parents;
+        for (const auto& b : s->model.bodies) parents.push_back(b.parent);
+        s->topo = mw::kernel_topology(parents.data(), s->model.dofs());
+        if (s->topo < 0)
+            return fail(MW_EPARSE, "the kinematic topology of this branched model is not compiled into this "
+                                   "build (supported: serial chains of 1..9 dofs and the Panda tree)");
+    }
+    s->pid.assign(s->model.dofs(), kDefaultPid);
     s->model_name = (name && *name) ? name : s->model.name;
     s->loaded = true;
     s->n = s->model.dofs();
@@ -330,6 +388,10 @@ int mw_initialize(mw_sim* s) {
     s->block_bytes = s->state_bytes + s->cmd_bytes;
     MW_HIP(hipMalloc(&s->d_block, s->block_bytes));
     MW_HIP(hipMalloc(&s->d_params, sizeof(mw::ChainF)));
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_aux), 4 * s->nw * sizeof(float)));
+    MW_HIP(hipMemsetAsync(s->d_aux, 0, 4 * s->nw * sizeof(float), s->stream));
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ptgt), s->nw * sizeof(float), hipHostMallocDefault));
+    std::memset(s->h_ptgt, 0, s->nw * sizeof(float));
     MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_block), s->block_bytes, hipHostMallocDefault));
     std::memset(s->h_block, 0, s->block_bytes);
     float* base = reinterpret_cast<float*>(s->d_block);
@@ -342,6 +404,10 @@ int mw_initialize(mw_sim* s) {
     s->dev.rqd = base + 6 * s->nw;
     s->dev.act = reinterpret_cast<uint8_t*>(base + 7 * s->nw);
     s->dev.rflag = s->dev.act + s->nw;
+    s->dev.ptgt = s->d_aux;
+    s->dev.pid_e = s->d_aux + s->nw;
+    s->dev.pid_i = s->d_aux + 2 * s->nw;
+    s->dev.pid_u = s->d_aux + 3 * s->nw;
     s->mode.assign(s->nw, MW_MODE_IDLE);
     s->ptgt.assign(s->nw, 0.0);
     s->cmd64.assign(s->nw, 0.0);
@@ -375,9 +441,39 @@ int mw_run(mw_sim* s, int paused) {
                               s->cmd_bytes, hipMemcpyHostToDevice, s->stream));
         s->cmd_dirty = false;
     }
-    MW_HIP(mw::launch_scenario_run(s->d_params, s->n, needs_cons(s), needs_dual(s), s->dev, s->W,
-                                   static_cast<float>(s->cfg.step_size), s->cfg.steps_per_run,
-                                   paused ? 1 : 0, s->cfg.pgs_iters, s->stream));
+    if (s->ptgt_dirty) {
+        MW_HIP(hipMemcpyAsync(s->d_aux, s->h_ptgt, s->nw * sizeof(float), hipMemcpyHostToDevice, s->stream));
+        s->ptgt_dirty = false;
+    }
+    const mw::PidSet pid = pid_set(s);
+    mw::RunArgs a{};
+    a.dt = static_cast<float>(s->cfg.step_size);
+    a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
+    a.paused = paused ? 1 : 0;
+    a.pgs_iters = s->cfg.pgs_iters;
+    a.first = 1;
+    const int spr = s->cfg.steps_per_run;
+    int done = 0;
+    do {
+        const int chunk = paused ? 0 : std::min(64, spr - done);
+        a.substeps = chunk;
+        a.pid_gate = 0;
+        // JointController::PreUpdate period gating on the simulated time
+        // (JointController.cpp:130-169): integer nanoseconds like the
+        // reference's steady_clock durations; the first iteration always computes
+        for (int k = 0; k < chunk && s->controller; ++k) {
+            const int64_t sim_ns = (s->iterations + done + k + 1) * s->dt_ns;
+            const int64_t elapsed = (s->prev_ns == 0) ? s->period_ns : sim_ns - s->prev_ns;
+            if (elapsed >= s->period_ns) {
+                s->prev_ns = sim_ns;
+                a.pid_gate |= (uint64_t{1} << k);
+            }
+        }
+        MW_HIP(mw::launch_scenario_run(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), s->dev, pid,
+                                       s->W, a, s->stream));
+        a.first = 0;
+        done += chunk;
+    } while (!paused && done < spr);
     MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
     MW_HIP(hipStreamSynchronize(s->stream));
     // mirror the kernel's component semantics on the host copy
@@ -499,7 +595,7 @@ int mw_model_export(const mw_sim* s, double* out, int32_t len) {
     if (!s || !out) return fail(MW_EINVAL, "null argument");
     if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
     const int n = s->model.dofs();
-    if (len < 33 * n + 3) return fail(MW_EINVAL, "export buffer too small");
+    if (len < 34 * n + 3) return fail(MW_EINVAL, "export buffer too small");
     double* o = out;
     for (const mw::ChainBody& b : s->model.bodies) {
         *o++ = (b.type == mw::JType::Prismatic) ? 1.0 : 0.0;
@@ -516,6 +612,7 @@ int mw_model_export(const mw_sim* s, double* out, int32_t len) {
         *o++ = b.upper;
         *o++ = b.effort;
         *o++ = b.vel_limit;
+        *o++ = b.parent;
     }
     const auto& R = s->model.base_R;
     for (int k = 0; k < 3; ++k) *o++ = R[k] * s->gravity[0] + R[3 + k] * s->gravity[1] + R[6 + k] * s->gravity[2];
@@ -550,6 +647,10 @@ int mw_get_joint_velocity_targets(const mw_sim* cs, int32_t w0, int32_t nw, cons
 }
 int mw_get_joint_position_targets(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
     mw_sim* s = const_cast<mw_sim*>(cs);
+    if (s && s->initialized) {
+        int rc = pull_ptgt(s);
+        if (rc) return rc;
+    }
     return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return s->ptgt[s->idx(dof, w)]; });
 }
 
@@ -582,12 +683,20 @@ int mw_set_joint_velocity_targets(mw_sim* s, int32_t w0, int32_t nw, const int32
 
 int mw_set_joint_position_targets(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
     // Joint::setPositionTarget, Joint.cpp:694-726
+    if (s && s->initialized) {
+        int rc = pull_ptgt(s);
+        if (rc) return rc;
+    }
     return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
         const int m = s->mode[s->idx(dof, w)];
         if (m != MW_MODE_POSITION && m != MW_MODE_POSITION_INTERPOLATED && m != MW_MODE_IDLE &&
             m != MW_MODE_FORCE)
             return fail(MW_ESTATE, "The active joint control mode does not accept a position target");
-        if (!dry) s->ptgt[s->idx(dof, w)] = x;
+        if (!dry) {
+            s->ptgt[s->idx(dof, w)] = x;
+            s->h_ptgt[s->idx(dof, w)] = static_cast<float>(x);
+            s->ptgt_dirty = true;
+        }
         return MW_OK;
     });
 }
@@ -597,7 +706,7 @@ int mw_reset_joint_positions(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d
     return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
         if (!dry) {
             s->hrq()[s->idx(dof, w)] = static_cast<float>(x);
-            s->hrflag()[s->idx(dof, w)] |= 1u;
+            s->hrflag()[s->idx(dof, w)] |= 1u | 4u;  // Joint::resetPosition also resets the PID
         }
         return MW_OK;
     });
@@ -607,7 +716,7 @@ int mw_reset_joint_velocities(mw_sim* s, int32_t w0, int32_t nw, const int32_t* 
     return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
         if (!dry) {
             s->hrqd()[s->idx(dof, w)] = static_cast<float>(x);
-            s->hrflag()[s->idx(dof, w)] |= 2u;
+            s->hrflag()[s->idx(dof, w)] |= 2u | 4u;
         }
         return MW_OK;
     });
@@ -616,28 +725,84 @@ int mw_reset_joint_velocities(mw_sim* s, int32_t w0, int32_t nw, const int32_t* 
 int mw_set_joint_control_mode(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, int32_t mode) {
     int rc = check_sim(s);
     if (rc) return rc;
-    // Joint::setControlMode, Joint.cpp:367-460
+    // Joint::setControlMode, Joint.cpp:369-460
     if (mode == MW_MODE_POSITION_INTERPOLATED) return fail(MW_EINVAL, "PositionInterpolated not yet supported");
-    if (mode == MW_MODE_POSITION || mode == MW_MODE_VELOCITY)
-        return fail(MW_EINVAL, "PID control modes (Position / Velocity) are not supported by this build yet");
-    if (mode != MW_MODE_IDLE && mode != MW_MODE_FORCE && mode != MW_MODE_VELOCITY_FOLLOWER_DART)
+    if (mode != MW_MODE_IDLE && mode != MW_MODE_FORCE && mode != MW_MODE_VELOCITY_FOLLOWER_DART &&
+        mode != MW_MODE_POSITION && mode != MW_MODE_VELOCITY)
         return fail(MW_EINVAL, "You cannot set the Invalid control mode");
     std::vector<int32_t> sel;
     if ((rc = selection(s, w0, nw, d, nd, sel))) return rc;
     if ((rc = pull_state(s))) return rc;
+    if ((rc = pull_ptgt(s))) return rc;
     for (int32_t w = w0; w < w0 + nw; ++w)
         for (int32_t dof : sel) {
             const size_t i = s->idx(dof, w);
             s->mode[i] = mode;
-            // targets are deleted and re-initialised from the current state
+            // targets are deleted and re-initialised from the current state (:418-446)
             s->hcmd()[i] = 0.f;
             s->cmd64[i] = 0.0;
-            s->hvt()[i] = (mode == MW_MODE_VELOCITY_FOLLOWER_DART) ? s->hqd()[i] : 0.f;
+            const bool vel = (mode == MW_MODE_VELOCITY_FOLLOWER_DART || mode == MW_MODE_VELOCITY);
+            s->hvt()[i] = vel ? s->hqd()[i] : 0.f;
             s->ptgt[i] = s->hq()[i];
-            s->hact()[i] = (mode == MW_MODE_VELOCITY_FOLLOWER_DART) ? mw::kActServo : mw::kActForce;
+            s->h_ptgt[i] = s->hq()[i];
+            uint8_t act = mw::kActForce;
+            if (mode == MW_MODE_VELOCITY_FOLLOWER_DART) act = mw::kActServo;
+            else if (mode == MW_MODE_POSITION) act = mw::kActPidPos;
+            else if (mode == MW_MODE_VELOCITY) act = mw::kActPidVel;
+            s->hact()[i] = act;
+            s->hrflag()[i] |= 4u;  // pid.Reset() (:453-457)
         }
     if (mode == MW_MODE_VELOCITY_FOLLOWER_DART) s->servo_used = true;
+    if (mode == MW_MODE_POSITION || mode == MW_MODE_VELOCITY || mode == MW_MODE_VELOCITY_FOLLOWER_DART)
+        s->controller = true;
     s->cmd_dirty = true;
+    s->ptgt_dirty = true;
+    return MW_OK;
+}
+
+int mw_set_joint_pid(mw_sim* s, int32_t dof, const double gains[8]) {
+    if (!s || !gains) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->n) return fail(MW_EINVAL, "dof out of range");
+    // Joint::setPID, Joint.cpp:479-525: output limits less limiting than the
+    // joint's maximum generalized force are replaced by +-effort
+    std::array<double, 8> g;
+    std::memcpy(g.data(), gains, sizeof(double) * 8);
+    const double maxf = s->model.bodies[dof].effort;
+    if (g[3] < -maxf || g[4] > maxf) {
+        g[3] = -maxf;
+        g[4] = maxf;
+    }
+    s->pid[dof] = g;
+    // a new ignition::math::PID starts from a reset state (before mw_initialize
+    // the device state is zero-initialised anyway)
+    if (s->initialized) {
+        for (int32_t w = 0; w < s->W; ++w) s->hrflag()[s->idx(dof, w)] |= 4u;
+        s->cmd_dirty = true;
+    }
+    return MW_OK;
+}
+
+int mw_joint_pid(const mw_sim* s, int32_t dof, double gains[8]) {
+    if (!s || !gains) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
+    std::memcpy(gains, s->pid[dof].data(), sizeof(double) * 8);
+    return MW_OK;
+}
+
+int mw_set_controller_period(mw_sim* s, double period) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    // Model::setControllerPeriod, Model.cpp:589-602 (doubleToSteadyClockDuration truncates)
+    if (!(period > 0.0)) return fail(MW_EINVAL, "The controller period must be greater than zero");
+    const double ns = period * 1e9;
+    s->period_ns = ns >= 9.2e18 ? std::numeric_limits<int64_t>::max() : static_cast<int64_t>(ns);
+    return MW_OK;
+}
+
+int mw_controller_period(const mw_sim* s, double* period) {
+    if (!s || !period) return fail(MW_EINVAL, "null argument");
+    *period = static_cast<double>(s->period_ns) / 1e9;
     return MW_OK;
 }
 
@@ -658,7 +823,19 @@ int mw_device_ptr(mw_sim* s, const char* field, void** dptr, int64_t* stride) {
     if (f == "q") *dptr = s->dev.q;
     else if (f == "qd") *dptr = s->dev.qd;
     else if (f == "qdd") *dptr = s->dev.qdd;
-    else return fail(MW_ENOTFOUND, "unknown field '" + f + "'");
+    else if (f == "position_target") {
+        // the caller drives the targets on the device from now on
+        if ((rc = pull_ptgt(s))) return rc;
+        if (s->ptgt_dirty) {
+            MW_HIP(hipMemcpyAsync(s->d_aux, s->h_ptgt, s->nw * sizeof(float), hipMemcpyHostToDevice, s->stream));
+            s->ptgt_dirty = false;
+        }
+        *dptr = s->dev.ptgt;
+        if (stride) *stride = s->W;
+        s->ptgt_stale = true;
+        s->ptgt_view = true;
+        return MW_OK;
+    } else return fail(MW_ENOTFOUND, "unknown field '" + f + "'");
     if (stride) *stride = s->W;
     s->host_stale = true;  // the caller may write through the view
     return MW_OK;

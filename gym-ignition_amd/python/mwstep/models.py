@@ -9,6 +9,7 @@ MODELS_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.pat
 _FILES = {
     "cartpole": "cartpole.urdf",
     "pendulum": "pendulum.urdf",
+    "panda": "panda.urdf",
     "ground_plane": "ground_plane.sdf",
 }
 

@@ -101,6 +101,10 @@ SIGNATURES = [
     ("mw_reset_joint_velocities", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
     ("mw_set_joint_control_mode", ctypes.c_int, [_P, _I, _I, _IP, _I, _I]),
     ("mw_joint_control_mode", ctypes.c_int, [_P, _I, _I, _IP]),
+    ("mw_set_joint_pid", ctypes.c_int, [_P, _I, _D]),
+    ("mw_joint_pid", ctypes.c_int, [_P, _I, _D]),
+    ("mw_set_controller_period", ctypes.c_int, [_P, ctypes.c_double]),
+    ("mw_controller_period", ctypes.c_int, [_P, _D]),
     ("mw_device_ptr", ctypes.c_int, [_P, _S, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("mw_vecenv_create", ctypes.c_int, [_P, ctypes.POINTER(MwTaskConfig), ctypes.POINTER(_P)]),

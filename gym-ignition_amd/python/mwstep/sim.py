@@ -161,8 +161,27 @@ class Simulator:
         N.check(N.lib().mw_joint_param(self.handle, dof, which, ctypes.byref(v)))
         return v.value
 
+    def set_pid(self, dof: int, gains) -> None:
+        """gains = {p, i, d, cmd_min, cmd_max, cmd_offset, i_min, i_max} (all worlds)."""
+        g = np.ascontiguousarray(gains, dtype=np.float64)
+        assert g.shape == (8,)
+        N.check(N.lib().mw_set_joint_pid(self.handle, dof, N.dptr(g)))
+
+    def pid(self, dof: int) -> np.ndarray:
+        g = np.zeros(8)
+        N.check(N.lib().mw_joint_pid(self.handle, dof, N.dptr(g)))
+        return g
+
+    def set_controller_period(self, period: float) -> None:
+        N.check(N.lib().mw_set_controller_period(self.handle, float(period)))
+
+    def controller_period(self) -> float:
+        v = ctypes.c_double()
+        N.check(N.lib().mw_controller_period(self.handle, ctypes.byref(v)))
+        return v.value
+
     def export_model(self) -> np.ndarray:
-        out = np.zeros(33 * self.dofs + 3)
+        out = np.zeros(34 * self.dofs + 3)
         N.check(N.lib().mw_model_export(self.handle, N.dptr(out), len(out)))
         return out
 

@@ -11,6 +11,8 @@ from __future__ import annotations
 import math
 from typing import Sequence
 
+import numpy as np
+
 # JointType (Joint.h:25-31)
 JointType_invalid = 0
 JointType_fixed = 1
@@ -60,22 +62,35 @@ class Limit:
 
 
 class PID:
-    """PID gains and limits (ignition::math::PID parameters)."""
+    """scenario::core::PID (cpp/scenario/core/include/scenario/core/Joint.h:505-523):
+    gains plus command / integral limits, with the SWIG binding's undercase
+    member names (bindings/core/core.i:69-70).  Defaults leave every limit open."""
 
-    def __init__(self, p: float = 0.0, i: float = 0.0, d: float = 0.0, i_max: float = -1.0,
-                 i_min: float = 0.0, cmd_max: float = -1.0, cmd_min: float = 0.0,
-                 cmd_offset: float = 0.0):
+    _LOWEST = -float(np.finfo(np.float64).max)
+    _MAX = float(np.finfo(np.float64).max)
+
+    def __init__(self, p: float = 0.0, i: float = 0.0, d: float = 0.0):
         self.p, self.i, self.d = float(p), float(i), float(d)
-        self.i_max, self.i_min = float(i_max), float(i_min)
-        self.cmd_max, self.cmd_min = float(cmd_max), float(cmd_min)
-        self.cmd_offset = float(cmd_offset)
+        self.cmd_min, self.cmd_max, self.cmd_offset = self._LOWEST, self._MAX, 0.0
+        self.i_min, self.i_max = self._LOWEST, self._MAX
+
+    def to_list(self):
+        """{p, i, d, cmd_min, cmd_max, cmd_offset, i_min, i_max} (mwstep.h order)."""
+        return [self.p, self.i, self.d, self.cmd_min, self.cmd_max, self.cmd_offset, self.i_min, self.i_max]
+
+    @classmethod
+    def from_list(cls, v) -> "PID":
+        pid = cls(v[0], v[1], v[2])
+        pid.cmd_min, pid.cmd_max, pid.cmd_offset, pid.i_min, pid.i_max = (float(x) for x in v[3:8])
+        return pid
 
     def __repr__(self):
         return f"PID(p={self.p}, i={self.i}, d={self.d})"
 
 
-# Default PID of every joint (Joint.cpp:63)
-DEFAULT_PID = PID(1.0, 0.1, 0.01, -1.0, 0.0, -1.0, 0.0, 0.0)
+# Default PID of every joint: ignition::math::PID(1, 0.1, 0.01, -1, 0, -1, 0, 0)
+# (Joint.cpp:63) as returned by Joint::pid() (fromIgnitionPID)
+DEFAULT_PID = PID.from_list([1.0, 0.1, 0.01, 0.0, -1.0, 0.0, 0.0, -1.0])
 
 
 def __getattr__(name):

@@ -164,6 +164,19 @@ class Joint:
     def set_control_mode(self, mode: int) -> bool:
         return self._model.set_joint_control_mode(mode, [self._name])
 
+    def pid(self) -> core.PID:
+        # Joint::pid (Joint.cpp:470-476)
+        return core.PID.from_list(self._model._sim.pid(self._dof))
+
+    def set_pid(self, pid: core.PID) -> bool:
+        # Joint::setPID (Joint.cpp:479-525)
+        try:
+            self._model._sim.set_pid(self._dof, pid.to_list())
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
     def set_generalized_force_target(self, force: float, dof: int = 0) -> bool:
         if dof != 0:
             _err(f"Joint '{self._name}' does not have DoF#{dof}")
@@ -273,7 +286,6 @@ class Model:
         self._sim = sim
         self._pose = pose
         self._joints = {n: Joint(self, i, n) for i, n in enumerate(sim.joint_names)}
-        self._period = world._simulator.step_size()
         self._history: Optional[collections.deque] = None
 
     # -- identity
@@ -310,14 +322,17 @@ class Model:
         return list(self._pose.orientation)
 
     def controller_period(self) -> float:
-        return self._period
+        # Model::controllerPeriod (Model.cpp:581-587)
+        return self._sim.controller_period()
 
     def set_controller_period(self, period: float) -> bool:
-        if period <= 0:
-            _err("The controller period must be positive")
+        # Model::setControllerPeriod (Model.cpp:589-602)
+        try:
+            self._sim.set_controller_period(float(period))
+            return True
+        except RuntimeError as e:
+            _err(str(e))
             return False
-        self._period = float(period)
-        return True
 
     # -- vectorised joint data (serialised in the requested name order)
     def _dofs(self, names: Sequence[str]):

@@ -112,9 +112,10 @@ int mw_model_name(const mw_sim* sim, char* buf, int32_t buflen);
 int mw_base_frame(const mw_sim* sim, char* buf, int32_t buflen);
 int mw_set_joint_param(mw_sim* sim, int32_t dof, int32_t which, double value);
 int mw_joint_param(const mw_sim* sim, int32_t dof, int32_t which, double* value);
-/* Export the compiled chain (fp64) for cross-checks: per dof
- * {jtype, limited, E[9], r[3], axis[3], mass, com[3], Ic[6], damping,
- *  friction, lower, upper, effort, vel_limit} = 33 doubles, then gravity_base[3]. */
+/* Export the compiled tree (fp64) for cross-checks: per dof, in depth-first
+ * body order, {jtype, limited, E[9], r[3], axis[3], mass, com[3], Ic[6],
+ * damping, friction, lower, upper, effort, vel_limit, parent} = 34 doubles,
+ * then gravity_base[3]. */
 int mw_model_export(const mw_sim* sim, double* out, int32_t len);
 
 /* Copy of the float32 parameter block the kernels read (struct ChainF of
@@ -142,8 +143,25 @@ int mw_reset_joint_velocities(mw_sim* sim, int32_t w0, int32_t nw, const int32_t
 int mw_set_joint_control_mode(mw_sim* sim, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs, int32_t mode);
 int mw_joint_control_mode(const mw_sim* sim, int32_t w, int32_t dof, int32_t* mode);
 
-/* Zero-copy device views of the SoA state, fields "q", "qd", "qdd":
- * float32 [n_dofs][n_worlds] (world index fastest). */
+/* JointController PID of one dof, shared by all worlds of the simulator.
+ * gains = {p, i, d, cmd_min, cmd_max, cmd_offset, i_min, i_max}, the field
+ * order of scenario::core::PID (cpp/scenario/core/include/scenario/core/
+ * Joint.h:505-523).  Replaces Joint::setPID / Joint::pid (Joint.cpp:466-525):
+ * output limits less limiting than +-max generalized force are replaced by
+ * them; the new PID starts from a reset state.  Default: Joint.cpp:63. */
+int mw_set_joint_pid(mw_sim* sim, int32_t dof, const double gains[8]);
+int mw_joint_pid(const mw_sim* sim, int32_t dof, double gains[8]);
+/* Model::setControllerPeriod / controllerPeriod (Model.cpp:589-602, default
+ * the maximum duration, Model.cpp:181-185): the PID force of Position /
+ * Velocity joints is recomputed when at least one period of simulated time
+ * has elapsed (JointController.cpp:130-169), else the last force is reused. */
+int mw_set_controller_period(mw_sim* sim, double period);
+int mw_controller_period(const mw_sim* sim, double* period);
+
+/* Zero-copy device views, float32 [n_dofs][n_worlds] (world index fastest):
+ * the SoA state "q", "qd", "qdd", and "position_target" (the Position-mode
+ * targets; after the view is taken, writes through it drive the next runs
+ * and the host getters/setters re-read the device copy). */
 int mw_device_ptr(mw_sim* sim, const char* field, void** dptr, int64_t* world_stride);
 /* Device-to-device copy of the SoA state ([n_dofs][n_worlds] float32 each) to
  * (to_sim = 0) or from (to_sim = 1) caller buffers, on the sim's stream. */

@@ -186,6 +186,9 @@ typedef struct {
     double Psi[OR_MAXB];     /* (S^T AI S)^-1             */
 } or_impulse_factor;
 
+/* Tree ABA (Featherstone 2008, Table 7.1) with DART's implicit damping.
+ * Bodies are in depth-first order (parent[i] < i), so the outward passes run
+ * i = 0..n-1 and the inward pass i = n-1..0 accumulates into parent[i]. */
 static void aba_full(const or_model* m, const double* q, const double* qd,
                      const double* tau, double dt_implicit, double* qdd,
                      or_impulse_factor* fac)
@@ -194,23 +197,24 @@ static void aba_full(const or_model* m, const double* q, const double* qd,
     double X[OR_MAXB][36], S[OR_MAXB][6], eta[OR_MAXB][6], B[OR_MAXB][6];
     double I[OR_MAXB][36], AIi[OR_MAXB][36], AI[OR_MAXB][36];
     double Ui[OR_MAXB][6], Psii[OR_MAXB], tt[OR_MAXB];
-    double V[6] = {0}, g[3];
-    memcpy(g, m->gravity_base, sizeof g);
+    double V[OR_MAXB][6], g[OR_MAXB][3];
 
     for (int i = 0; i < n; ++i) {
-        double R[9], p[3], Vp[6], Sq[6], IV[6], dd[6], gb[3], Fg[6], ga[6] = {0};
+        double R[9], p[3], Vp[6], Sq[6], IV[6], dd[6], Fg[6], ga[6] = {0};
+        const int pa = m->parent[i];
+        const double zero6[6] = {0}, *Vpar = pa < 0 ? zero6 : V[pa];
+        const double* gpar = pa < 0 ? m->gravity_base : g[pa];
         joint_pose(m, i, q[i], R, p);
         plucker(R, p, X[i]);
         motion_subspace(m, i, S[i]);
-        m6_vec(X[i], V, Vp);
-        for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[k] = Vp[k] + Sq[k]; }
-        for (int r = 0; r < 3; ++r) gb[r] = R[r] * g[0] + R[3 + r] * g[1] + R[6 + r] * g[2];
-        memcpy(g, gb, sizeof g);
-        sp_ad(V, Sq, eta[i]);
+        m6_vec(X[i], Vpar, Vp);
+        for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[i][k] = Vp[k] + Sq[k]; }
+        for (int r = 0; r < 3; ++r) g[i][r] = R[r] * gpar[0] + R[3 + r] * gpar[1] + R[6 + r] * gpar[2];
+        sp_ad(V[i], Sq, eta[i]);
         body_inertia(m, i, I[i]);
-        m6_vec(I[i], V, IV);
-        sp_dad(V, IV, dd);
-        ga[3] = g[0]; ga[4] = g[1]; ga[5] = g[2];
+        m6_vec(I[i], V[i], IV);
+        sp_dad(V[i], IV, dd);
+        ga[3] = g[i][0]; ga[4] = g[i][1]; ga[5] = g[i][2];
         m6_vec(I[i], ga, Fg);
         for (int k = 0; k < 6; ++k) B[i][k] = -dd[k] - Fg[k];
         memcpy(AIi[i], I[i], sizeof(double) * 36);
@@ -219,6 +223,7 @@ static void aba_full(const or_model* m, const double* q, const double* qd,
 
     for (int i = n - 1; i >= 0; --i) {
         double U[6], AIeta[6], tmp[6];
+        const int pa = m->parent[i];
         m6_vec(AIi[i], S[i], Ui[i]);
         Psii[i] = 1.0 / (dot6(S[i], Ui[i]) + dt_implicit * m->damping[i]);
         m6_vec(AI[i], S[i], U);
@@ -227,7 +232,7 @@ static void aba_full(const or_model* m, const double* q, const double* qd,
         m6_vec(AIi[i], eta[i], AIeta);
         for (int k = 0; k < 6; ++k) tmp[k] = AIeta[k] + B[i][k];
         tt[i] = tau[i] - m->damping[i] * qd[i] - dot6(S[i], tmp);
-        if (i > 0) {
+        if (pa >= 0) {
             double Pi[36], Pn[36], beta[6], c[36], bp[6];
             for (int r = 0; r < 6; ++r)
                 for (int k = 0; k < 6; ++k) {
@@ -236,20 +241,22 @@ static void aba_full(const or_model* m, const double* q, const double* qd,
                 }
             for (int k = 0; k < 6; ++k) beta[k] = B[i][k] + AIeta[k] + Ui[i][k] * Psii[i] * tt[i];
             m6_congruence(X[i], Pi, c);
-            for (int k = 0; k < 36; ++k) AIi[i - 1][k] += c[k];
+            for (int k = 0; k < 36; ++k) AIi[pa][k] += c[k];
             m6_congruence(X[i], Pn, c);
-            for (int k = 0; k < 36; ++k) AI[i - 1][k] += c[k];
+            for (int k = 0; k < 36; ++k) AI[pa][k] += c[k];
             m6t_vec(X[i], beta, bp);
-            for (int k = 0; k < 6; ++k) B[i - 1][k] += bp[k];
+            for (int k = 0; k < 6; ++k) B[pa][k] += bp[k];
         }
     }
 
-    double a[6] = {0};
+    double a[OR_MAXB][6];
     for (int i = 0; i < n; ++i) {
         double ap[6];
-        m6_vec(X[i], a, ap);
+        const int pa = m->parent[i];
+        const double zero6[6] = {0};
+        m6_vec(X[i], pa < 0 ? zero6 : a[pa], ap);
         qdd[i] = Psii[i] * (tt[i] - dot6(Ui[i], ap));
-        for (int k = 0; k < 6; ++k) a[k] = ap[k] + eta[i][k] + S[i][k] * qdd[i];
+        for (int k = 0; k < 6; ++k) a[i][k] = ap[k] + eta[i][k] + S[i][k] * qdd[i];
     }
     if (fac) {
         for (int i = 0; i < n; ++i) {
@@ -266,28 +273,33 @@ void or_aba(const or_model* m, const double* q, const double* qd,
 }
 
 /* velocity change of every dof for a unit generalized impulse on dof j
- * (DART computeImpulseForwardDynamics with only joint impulses). */
+ * (DART computeImpulseForwardDynamics with only joint impulses): the bias
+ * impulse is nonzero only on the ancestors of j; the outward pass reaches
+ * every body. */
 static void impulse_column(const or_model* m, const or_impulse_factor* f, int j,
                            double* col)
 {
     const int n = m->n;
-    double u[OR_MAXB];
-    double Bimp[6] = {0};
+    double u[OR_MAXB], Bimp[OR_MAXB][6];
+    memset(Bimp, 0, sizeof(double) * 6 * (size_t)n);
     for (int i = n - 1; i >= 0; --i) {
-        if (i > j) { u[i] = 0.0; continue; }
-        if (i == j) { u[i] = 1.0; memset(Bimp, 0, sizeof Bimp); continue; }
-        double t[6], bp[6];
-        for (int k = 0; k < 6; ++k) t[k] = Bimp[k] + f->U[i + 1][k] * f->Psi[i + 1] * u[i + 1];
-        m6t_vec(f->X[i + 1], t, bp);
-        memcpy(Bimp, bp, sizeof bp);
-        u[i] = -dot6(f->S[i], Bimp);
+        u[i] = (i == j ? 1.0 : 0.0) - dot6(f->S[i], Bimp[i]);
+        const int pa = m->parent[i];
+        if (pa >= 0) {
+            double t[6], bp[6];
+            for (int k = 0; k < 6; ++k) t[k] = Bimp[i][k] + f->U[i][k] * f->Psi[i] * u[i];
+            m6t_vec(f->X[i], t, bp);
+            for (int k = 0; k < 6; ++k) Bimp[pa][k] += bp[k];
+        }
     }
-    double dv[6] = {0};
+    double dv[OR_MAXB][6];
     for (int i = 0; i < n; ++i) {
         double dvp[6];
-        m6_vec(f->X[i], dv, dvp);
+        const int pa = m->parent[i];
+        const double zero6[6] = {0};
+        m6_vec(f->X[i], pa < 0 ? zero6 : dv[pa], dvp);
         col[i] = f->Psi[i] * (u[i] - dot6(f->U[i], dvp));
-        for (int k = 0; k < 6; ++k) dv[k] = dvp[k] + f->S[i][k] * col[i];
+        for (int k = 0; k < 6; ++k) dv[i][k] = dvp[k] + f->S[i][k] * col[i];
     }
 }
 
@@ -302,21 +314,25 @@ void or_crba(const or_model* m, const double* q, double* M)
         motion_subspace(m, i, S[i]);
         body_inertia(m, i, Ic[i]);
     }
-    for (int i = n - 1; i > 0; --i) {
+    for (int i = n - 1; i >= 0; --i) {
+        const int pa = m->parent[i];
+        if (pa < 0) continue;
         double c[36];
         m6_congruence(X[i], Ic[i], c);
-        for (int k = 0; k < 36; ++k) Ic[i - 1][k] += c[k];
+        for (int k = 0; k < 36; ++k) Ic[pa][k] += c[k];
     }
+    for (int i = 0; i < n * n; ++i) M[i] = 0.0;
     for (int i = 0; i < n; ++i) {
         double F[6];
         m6_vec(Ic[i], S[i], F);
         M[i * n + i] = dot6(S[i], F);
-        for (int j = i; j > 0; --j) {
+        for (int j = i; m->parent[j] >= 0;) {
             double Fp[6];
             m6t_vec(X[j], F, Fp);
             memcpy(F, Fp, sizeof F);
-            M[i * n + (j - 1)] = dot6(S[j - 1], F);
-            M[(j - 1) * n + i] = M[i * n + (j - 1)];
+            j = m->parent[j];
+            M[i * n + j] = dot6(S[j], F);
+            M[j * n + i] = M[i * n + j];
         }
     }
 }
@@ -326,30 +342,33 @@ void or_rnea(const or_model* m, const double* q, const double* qd,
 {
     const int n = m->n;
     double X[OR_MAXB][36], S[OR_MAXB][6], f[OR_MAXB][6];
-    double V[6] = {0}, a[6] = {0};
-    a[3] = -m->gravity_base[0]; a[4] = -m->gravity_base[1]; a[5] = -m->gravity_base[2];
+    double V[OR_MAXB][6], a[OR_MAXB][6];
+    const double V0[6] = {0};
+    const double a0[6] = {0, 0, 0, -m->gravity_base[0], -m->gravity_base[1], -m->gravity_base[2]};
     for (int i = 0; i < n; ++i) {
         double R[9], p[3], Vp[6], ap[6], Sq[6], c[6], I[36], Ia[6], IV[6], dd[6];
+        const int pa = m->parent[i];
         joint_pose(m, i, q[i], R, p);
         plucker(R, p, X[i]);
         motion_subspace(m, i, S[i]);
-        m6_vec(X[i], V, Vp);
-        m6_vec(X[i], a, ap);
-        for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[k] = Vp[k] + Sq[k]; }
-        sp_ad(V, Sq, c);
-        for (int k = 0; k < 6; ++k) a[k] = ap[k] + S[i][k] * qdd[i] + c[k];
+        m6_vec(X[i], pa < 0 ? V0 : V[pa], Vp);
+        m6_vec(X[i], pa < 0 ? a0 : a[pa], ap);
+        for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[i][k] = Vp[k] + Sq[k]; }
+        sp_ad(V[i], Sq, c);
+        for (int k = 0; k < 6; ++k) a[i][k] = ap[k] + S[i][k] * qdd[i] + c[k];
         body_inertia(m, i, I);
-        m6_vec(I, a, Ia);
-        m6_vec(I, V, IV);
-        sp_dad(V, IV, dd);
+        m6_vec(I, a[i], Ia);
+        m6_vec(I, V[i], IV);
+        sp_dad(V[i], IV, dd);
         for (int k = 0; k < 6; ++k) f[i][k] = Ia[k] - dd[k];
     }
     for (int i = n - 1; i >= 0; --i) {
         tau[i] = dot6(S[i], f[i]);
-        if (i > 0) {
+        const int pa = m->parent[i];
+        if (pa >= 0) {
             double fp[6];
             m6t_vec(X[i], f[i], fp);
-            for (int k = 0; k < 6; ++k) f[i - 1][k] += fp[k];
+            for (int k = 0; k < 6; ++k) f[pa][k] += fp[k];
         }
     }
 }
@@ -474,6 +493,33 @@ int or_step(const or_model* m, double dt, double* q, double* qd,
     if (force_out)
         for (int i = 0; i < n; ++i) force_out[i] = tau[i] + imp[i] / dt;
     return nr;
+}
+
+/* ---------------- joint PID (ign-math 6 PID, [EXT]) ---------------- */
+
+/* ignition::math::PID::Update restated [EXT: ign-math6 src/PID.cc, not
+ * vendored]: error = current - reference (JointController.cpp), the
+ * integral is clamped to [iMin, iMax] and the command to [cmdMin, cmdMax]
+ * when those ranges are non-empty; a zero dt returns 0 and leaves the state
+ * unchanged.  Reset() zeroes pErrLast / iErr / cmd. */
+double or_pid_update(const or_pid_gains* g, or_pid_state* s, double err, double dt)
+{
+    if (dt == 0.0 || isnan(err) || isinf(err)) return 0.0;
+    const double pterm = g->p * err;
+    s->ierr = s->ierr + g->i * dt * err;
+    if (g->imax >= g->imin) {
+        if (s->ierr > g->imax) s->ierr = g->imax;
+        if (s->ierr < g->imin) s->ierr = g->imin;
+    }
+    const double derr = (err - s->perr_last) / dt;
+    s->perr_last = err;
+    double cmd = -pterm - s->ierr - g->d * derr + g->offset;
+    if (g->cmdmax >= g->cmdmin) {
+        if (cmd > g->cmdmax) cmd = g->cmdmax;
+        if (cmd < g->cmdmin) cmd = g->cmdmin;
+    }
+    s->cmd = cmd;
+    return cmd;
 }
 
 /* ---------------- Philox4x32-10 ---------------- */

@@ -31,11 +31,14 @@ extern "C" {
 
 #define OR_MAXB 48
 
-/* Fixed-base kinematic chain: body i's parent is body i-1 (body -1 = base). */
+/* Fixed-base kinematic tree, one dof per body.  parent[i] < i (bodies in
+ * depth-first order, -1 = the fixed base body); a serial chain has
+ * parent[i] == i - 1. */
 typedef struct {
     int32_t n;                   /* moving bodies == dofs                      */
     int32_t jtype[OR_MAXB];      /* 0 revolute, 1 prismatic                    */
     int32_t limited[OR_MAXB];    /* position limits enforced                   */
+    int32_t parent[OR_MAXB];     /* parent body index, -1 = base               */
     int32_t pad_;
     double gravity_base[3];      /* gravity expressed in the base link frame   */
     double E[OR_MAXB][9];        /* joint origin rotation in parent (row-major) */
@@ -80,6 +83,16 @@ int or_step(const or_model* m, double dt, double* q, double* qd,
 /* Boxed LCP by projected Gauss-Seidel (A row-major n*n). */
 void or_pgs(int n, const double* A, const double* b, const double* lo,
             const double* hi, double* x, int iters);
+
+/* Joint PID of the ScenarI/O JointController (Position / Velocity modes,
+ * cpp/scenario/plugins/JointController/JointController.cpp:129-190). */
+typedef struct {
+    double p, i, d, imax, imin, cmdmax, cmdmin, offset;
+} or_pid_gains;
+typedef struct {
+    double perr_last, ierr, cmd;
+} or_pid_state;
+double or_pid_update(const or_pid_gains* g, or_pid_state* s, double err, double dt);
 
 /* ------------------------------------------------------------------ */
 /* Batched environment (task logic of the reference's CartPole /      */

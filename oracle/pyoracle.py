@@ -40,6 +40,7 @@ class OrModel(ctypes.Structure):
         ("n", ctypes.c_int32),
         ("jtype", ctypes.c_int32 * OR_MAXB),
         ("limited", ctypes.c_int32 * OR_MAXB),
+        ("parent", ctypes.c_int32 * OR_MAXB),
         ("pad_", ctypes.c_int32),
         ("gravity_base", ctypes.c_double * 3),
         ("E", (ctypes.c_double * 9) * OR_MAXB),
@@ -55,6 +56,14 @@ class OrModel(ctypes.Structure):
         ("effort", ctypes.c_double * OR_MAXB),
         ("vel_limit", ctypes.c_double * OR_MAXB),
     ]
+
+
+class OrPidGains(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("p", "i", "d", "imax", "imin", "cmdmax", "cmdmin", "offset")]
+
+
+class OrPidState(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("perr_last", "ierr", "cmd")]
 
 
 class OrTask(ctypes.Structure):
@@ -97,6 +106,9 @@ def lib():
         L.or_step.argtypes = [M, ctypes.c_double, D, D, I32, D, ctypes.c_int, D, D]
         L.or_step.restype = ctypes.c_int
         L.or_pgs.argtypes = [ctypes.c_int, D, D, D, D, D, ctypes.c_int]
+        L.or_pid_update.argtypes = [ctypes.POINTER(OrPidGains), ctypes.POINTER(OrPidState),
+                                    ctypes.c_double, ctypes.c_double]
+        L.or_pid_update.restype = ctypes.c_double
         L.or_philox.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, U32]
         L.or_philox_raw.argtypes = [U32, U32, U32]
         L.or_task_reset_state.argtypes = [T, ctypes.c_uint32, ctypes.c_uint32, D, D]
@@ -279,17 +291,20 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
             changed = True
             break
 
-    # moving joints must form a chain from the base body
+    # moving joints form a tree from the base body, numbered depth-first with
+    # children in declaration order (parent index < child index)
     chain: List[_Joint] = []
-    cur = root_link
-    while True:
-        nxt = [j for j in joints if owner[j.parent] == cur]
-        if not nxt:
-            break
-        assert len(nxt) == 1, "the chain oracle supports serial chains only"
-        chain.append(nxt[0])
-        cur = nxt[0].child
-    assert len(chain) == len(joints)
+    parents: List[int] = []
+
+    def visit(link: str, pidx: int) -> None:
+        for j in [j for j in joints if owner[j.parent] == link]:
+            assert len(chain) < len(joints), "the joints do not form a tree"
+            chain.append(j)
+            parents.append(pidx)
+            visit(j.child, len(chain) - 1)
+
+    visit(root_link, -1)
+    assert len(chain) == len(joints), "moving joints not connected to the base"
 
     M = OrModel()
     M.n = len(chain)
@@ -302,6 +317,7 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
         L = links[j.child]
         M.jtype[i] = 0 if j.jtype in ("revolute", "continuous") else 1
         M.limited[i] = 1 if j.jtype in ("revolute", "prismatic") else 0
+        M.parent[i] = parents[i]
         for k in range(9):
             M.E[i][k] = E.flat[k]
         for k in range(3):
@@ -357,6 +373,121 @@ def step(cm: ChainModel, dt, q, qd, mode, cmd, pgs_iters=50):
     nr = lib().or_step(ctypes.byref(cm.model), dt, _p(q), _p(qd), _p(mode, ctypes.c_int32),
                        _p(cmd), pgs_iters, _p(qdd), _p(f))
     return q, qd, qdd, f, nr
+
+
+# scenario::core::PID defaults (cpp/scenario/core/include/scenario/core/utils/
+# utils.h PID struct): cmd / integral limits open; Joint.cpp:63 DefaultPID is
+# ignition::math::PID(1, 0.1, 0.01, -1, 0, -1, 0, 0) (empty ranges: no clamp).
+_BIG = float(np.finfo(np.float64).max)
+
+
+def pid_gains(p, i, d, imax=_BIG, imin=-_BIG, cmdmax=_BIG, cmdmin=-_BIG, offset=0.0) -> OrPidGains:
+    return OrPidGains(p, i, d, imax, imin, cmdmax, cmdmin, offset)
+
+
+DEFAULT_PID = (1.0, 0.1, 0.01, -1.0, 0.0, -1.0, 0.0, 0.0)
+
+
+def pid_update(g: OrPidGains, s: OrPidState, err: float, dt: float) -> float:
+    return lib().or_pid_update(ctypes.byref(g), ctypes.byref(s), err, dt)
+
+
+IDLE, FORCE_MODE, VELOCITY_FOLLOWER_DART, POSITION, VELOCITY = 1, 2, 4, 5, 3
+
+
+class ScenarioWorld:
+    """fp64 restatement of one world of GazeboSimulator.run() with the
+    ScenarI/O Physics + JointController systems (the checker of the HIP
+    scenario kernel).  Per run, for every substep:
+      JointController::PreUpdate (JointController.cpp:114-287): period gating
+        on the simulated time in integer nanoseconds; Position / Velocity
+        joints run the PID on error = current - target (:308) and write the
+        force target; VelocityFollowerDart re-issues the velocity command;
+      Physics::UpdatePhysics: SetForce (effort clip in the engine) / servo;
+      engine step (or_step); UpdateSim zero-fills the force command
+        (Physics.cpp:2250-2254), so a Force-mode target acts on one substep.
+    Resets apply at the start of the next run (velocity, then position)."""
+
+    def __init__(self, cm: ChainModel, dt: float, steps_per_run: int = 1, pgs_iters: int = 50):
+        n = cm.n
+        self.cm, self.dt, self.spr, self.pgs = cm, dt, steps_per_run, pgs_iters
+        self.dt_ns = int(round(dt * 1e9))
+        self.q, self.qd, self.qdd = np.zeros(n), np.zeros(n), np.zeros(n)
+        self.mode = [IDLE] * n
+        self.force = np.zeros(n)
+        self.ptgt, self.vtgt = np.zeros(n), np.zeros(n)
+        self.gains = [OrPidGains(*DEFAULT_PID) for _ in range(n)]
+        self.state = [OrPidState() for _ in range(n)]
+        self.period_ns = 2 ** 63 - 1          # Model.cpp:181-185: never, after the first update
+        self.prev_ns = 0
+        self.controller = False                # JointController inserted (Joint.cpp:376-404)
+        self.iterations = 0
+        self.reset_q, self.reset_qd = {}, {}
+
+    # -- component writes (Joint.cpp) --
+    def set_mode(self, dof, mode):
+        self.mode[dof] = mode
+        self.force[dof] = 0.0
+        if mode in (POSITION,):
+            self.ptgt[dof] = self.q[dof]
+        if mode in (VELOCITY, VELOCITY_FOLLOWER_DART):
+            self.vtgt[dof] = self.qd[dof]
+        if mode in (POSITION, VELOCITY, VELOCITY_FOLLOWER_DART):
+            self.controller = True
+        self.state[dof] = OrPidState()
+
+    def set_pid(self, dof, p, i, d, imax=_BIG, imin=-_BIG, cmdmax=_BIG, cmdmin=-_BIG, offset=0.0):
+        e = self.cm.model.effort[dof]
+        if cmdmin < -e or cmdmax > e:          # Joint.cpp:504-513
+            cmdmin, cmdmax = -e, e
+        self.gains[dof] = OrPidGains(p, i, d, imax, imin, cmdmax, cmdmin, offset)
+        self.state[dof] = OrPidState()
+
+    def reset_position(self, dof, v):
+        self.reset_q[dof] = v
+        self.state[dof] = OrPidState()
+
+    def reset_velocity(self, dof, v):
+        self.reset_qd[dof] = v
+        self.state[dof] = OrPidState()
+
+    def run(self, paused=False):
+        for d, v in self.reset_qd.items():
+            self.qd[d] = v
+        for d, v in self.reset_q.items():
+            self.q[d] = v
+        self.reset_q, self.reset_qd = {}, {}
+        if paused:
+            self.force[:] = 0.0
+            return
+        n = self.cm.n
+        for s in range(self.spr):
+            sim_ns = (self.iterations + s + 1) * self.dt_ns
+            compute = False
+            if self.controller:
+                elapsed = self.period_ns if self.prev_ns == 0 else sim_ns - self.prev_ns
+                if elapsed >= self.period_ns:
+                    self.prev_ns = sim_ns
+                    compute = True
+            mode = np.zeros(n, dtype=np.int32)
+            cmd = np.zeros(n)
+            for d in range(n):
+                m = self.mode[d]
+                if m in (POSITION, VELOCITY):
+                    if compute:
+                        cur = self.q[d] if m == POSITION else self.qd[d]
+                        tgt = self.ptgt[d] if m == POSITION else self.vtgt[d]
+                        pid_update(self.gains[d], self.state[d], cur - tgt, self.dt)
+                    mode[d], cmd[d] = FORCE, self.state[d].cmd
+                elif m == VELOCITY_FOLLOWER_DART:
+                    mode[d], cmd[d] = SERVO, self.vtgt[d]
+                elif m == FORCE_MODE:
+                    mode[d], cmd[d] = FORCE, (self.force[d] if s == 0 else 0.0)
+                else:
+                    mode[d] = PASSIVE
+            self.q, self.qd, self.qdd, _, _ = step(self.cm, self.dt, self.q, self.qd, mode, cmd, self.pgs)
+        self.force[:] = 0.0
+        self.iterations += self.spr
 
 
 def pgs(A, b, lo, hi, iters=100):

@@ -52,3 +52,8 @@ def pendulum_file():
 def require_gpu():
     if not gpu_available():
         pytest.fail("this test needs a GPU: run it on the MI355X box (pytest -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def panda_file():
+    return os.path.join(MODELS, "panda.urdf")

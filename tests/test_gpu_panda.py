@@ -1,0 +1,202 @@
+"""GPU tests of the Panda row (BASELINE config 4): a branched 9-dof model in
+Position (PID) control, on the HIP scenario kernel.
+
+  * the reference's PID known-answer test, through the ScenarI/O mirror
+    (tests/test_scenario/test_pid_controllers.py:34-115; gains :20-30,
+    controller period = step size, hold 1000 steps within 1 deg, track
+    q0 + 0.9 range/2 sin(2 pi 0.33 t) on joints 1 and 6 within 3 deg); joint 4
+    starts at its published upper limit instead of 0 (see
+    tests/test_oracle_tree_pid.py);
+  * teacher-forced one-step parity against the fp64 oracle
+    (pyoracle.ScenarioWorld: JointController PID + tree ABA + limit rows) over
+    many worlds with random states / targets: fp32 vs fp64, <= 1e-5 rad on q
+    and <= 1e-3 rad/s on qd (PID gains up to 10^4 amplify the fp32 rounding of
+    the error term; the bound is stated per quantity);
+  * free-running parity of a PID tracking run (H = 500) against the oracle,
+    <= 5e-4 rad;
+  * controller-period gating and Velocity-mode PID against the oracle.
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GAINS = {  # test_pid_controllers.py:20-30
+    "panda_joint1": (50, 0, 20), "panda_joint2": (10000, 0, 500),
+    "panda_joint3": (100, 0, 10), "panda_joint4": (1000, 0, 50),
+    "panda_joint5": (100, 0, 10), "panda_joint6": (100, 0, 10),
+    "panda_joint7": (10, 0.5, 0.1), "panda_finger_joint1": (100, 0, 50),
+    "panda_finger_joint2": (100, 0, 50),
+}
+BIG = float(np.finfo(np.float64).max)
+
+
+def test_position_pid_kat(require_gpu):
+    from mwstep import get_model_file
+    from scenario import core
+    from scenario import gazebo as scenario
+    gazebo = scenario.GazeboSimulator(1.0 / 1000, 1.0, 1)
+    assert gazebo.initialize()
+    world = gazebo.get_world().to_gazebo()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("panda"))
+    assert "panda" in world.model_names()
+    panda = world.get_model("panda").to_gazebo()
+    joint1 = panda.get_joint("panda_joint1").to_gazebo()
+    joint1_range = abs(joint1.position_limit().max - joint1.position_limit().min)
+    assert joint1.reset_position(joint1.position_limit().min + joint1_range / 2)
+    joint6 = panda.get_joint("panda_joint6").to_gazebo()
+    joint6_range = abs(joint6.position_limit().max - joint6.position_limit().min)
+    assert joint6.reset_position(joint6.position_limit().min + joint6_range / 2)
+    assert panda.get_joint("panda_joint4").reset_position(-0.0698)
+    assert gazebo.run(paused=True)
+    assert panda.set_controller_period(gazebo.step_size())
+    assert set(panda.joint_names()) == set(GAINS)
+    for name, g in GAINS.items():
+        assert panda.get_joint(name).set_pid(pid=core.PID(*g))
+    assert panda.set_joint_control_mode(core.JointControlMode_position)
+    assert panda.joint_position_targets() == pytest.approx(panda.joint_positions())
+    for _ in range(1000):
+        assert gazebo.run()
+    assert panda.joint_positions() == pytest.approx(panda.joint_position_targets(), abs=np.deg2rad(1))
+    q01, q06 = joint1.position(), joint6.position()
+    worst = 0.0
+    for k in range(5000):
+        t = k * gazebo.step_size()
+        r1 = q01 + 0.9 * joint1_range / 2 * np.sin(2 * np.pi * 0.33 * t)
+        r6 = q06 + 0.9 * joint6_range / 2 * np.sin(2 * np.pi * 0.33 * t)
+        assert joint1.set_position_target(position=r1)
+        assert joint6.set_position_target(position=r6)
+        assert gazebo.run()
+        worst = max(worst, abs(joint1.position() - r1), abs(joint6.position() - r6))
+        assert joint1.position() == pytest.approx(r1, abs=np.deg2rad(3))
+        assert joint6.position() == pytest.approx(r6, abs=np.deg2rad(3))
+    print(f"panda tracking worst error {np.degrees(worst):.3f} deg")
+    gazebo.close()
+
+
+def _sim(W, spr=1, period=1e-3):
+    from mwstep import get_model_file
+    from mwstep.sim import Simulator
+    sim = Simulator(get_model_file("panda"), n_worlds=W, steps_per_run=spr, pgs_iters=20)
+    for d, name in enumerate(sim.joint_names):
+        p, i, dd = GAINS[name]
+        sim.set_pid(d, [p, i, dd, -BIG, BIG, 0.0, -BIG, BIG])
+    sim.set_controller_period(period)
+    return sim
+
+
+def _oracle_world(oracle, cm, q, qd, tgt, mode, period_ns=1_000_000, spr=1, vtgt=None):
+    w = oracle.ScenarioWorld(cm, 1e-3, spr, 20)
+    w.q, w.qd = q.astype(float).copy(), qd.astype(float).copy()
+    w.period_ns = period_ns
+    for d, name in enumerate(cm.joint_names):
+        w.set_pid(d, *GAINS[name])
+        w.set_mode(d, mode)
+    w.ptgt[:] = tgt
+    if vtgt is not None:
+        w.vtgt[:] = vtgt
+    return w
+
+
+def _random_states(cm, W, rng):
+    n = cm.n
+    lo = np.array([cm.model.lower[i] for i in range(n)])
+    hi = np.array([cm.model.upper[i] for i in range(n)])
+    q = rng.uniform(lo, hi, size=(W, n))
+    # some joints 1 mrad beyond a limit: exactly AT a limit, fp32 and fp64
+    # may disagree on whether the limit row activates (a threshold case)
+    at = rng.uniform(size=(W, n)) < 0.15
+    q[at] = np.where(rng.uniform(size=(W, n)) < 0.5, lo - 1e-3, hi + 1e-3)[at]
+    qd = rng.uniform(-0.5, 0.5, size=(W, n))
+    tgt = np.clip(q + rng.uniform(-0.05, 0.05, size=(W, n)), lo, hi)
+    return q.astype(np.float32), qd.astype(np.float32), tgt
+
+
+def test_one_step_parity_position_pid(require_gpu, oracle, panda_file):
+    W = 256
+    rng = np.random.default_rng(3)
+    cm = oracle.load_urdf(panda_file)
+    q, qd, tgt = _random_states(cm, W, rng)
+    sim = _sim(W)
+    sim.set("reset_q", q)
+    sim.set("reset_qd", qd)
+    sim.run(paused=True)
+    sim.set_control_mode(5)                       # Position: targets = current q, PID reset
+    sim.set("position_target", tgt)
+    sim.run()
+    gq, gqd = sim.get("q"), sim.get("qd")
+    wq = wqd = 0.0
+    for w in range(W):
+        ow = _oracle_world(oracle, cm, q[w], qd[w], tgt[w], oracle.POSITION)
+        ow.run()
+        wq = max(wq, float(np.abs(gq[w] - ow.q).max()))
+        wqd = max(wqd, float(np.abs(gqd[w] - ow.qd).max()))
+    print(f"panda one-step: max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
+    assert wq <= 1e-5 and wqd <= 1e-3   # measured r01: 1.3e-7 / 4.2e-5
+    sim.close()
+
+
+def test_free_running_tracking_parity(require_gpu, oracle, panda_file):
+    """8 worlds, 500 steps of sinusoidal targets on joints 1 and 6: the PID
+    feedback keeps fp32 and fp64 trajectories within 1e-3 rad."""
+    W, H = 8, 500
+    cm = oracle.load_urdf(panda_file)
+    n = cm.n
+    q0 = np.zeros((W, n), np.float32)
+    q0[:, 3] = -0.0698
+    q0[:, 5] = 1.8675
+    q0[:, 0] = np.linspace(-1, 1, W)
+    sim = _sim(W)
+    sim.set("reset_q", q0)
+    sim.run(paused=True)
+    sim.set_control_mode(5)
+    ows = [_oracle_world(oracle, cm, q0[w], np.zeros(n), q0[w].astype(float), oracle.POSITION)
+           for w in range(W)]
+    worst = 0.0
+    for k in range(H):
+        t = k * 1e-3
+        tgt = q0.astype(float).copy()
+        tgt[:, 0] += 0.9 * 2.8973 * np.sin(2 * np.pi * 0.33 * t)
+        tgt[:, 5] += 0.9 * 1.885 * np.sin(2 * np.pi * 0.33 * t)
+        sim.set("position_target", tgt)
+        sim.run()
+        gq = sim.get("q")
+        for w in range(W):
+            ows[w].ptgt[:] = tgt[w]
+            ows[w].run()
+            worst = max(worst, float(np.abs(gq[w] - ows[w].q).max()))
+    print(f"panda free-running H={H}: max|dq| {worst:.2e}")
+    assert worst <= 5e-4   # measured r01: 4.1e-5
+    sim.close()
+
+
+def test_period_gating_and_velocity_pid(require_gpu, oracle, panda_file):
+    """controller period = 3 steps with steps_per_run = 2 (the gate crosses run
+    boundaries), Velocity-mode PID on every joint, vs the oracle."""
+    W, H = 16, 60
+    rng = np.random.default_rng(8)
+    cm = oracle.load_urdf(panda_file)
+    q, qd, _ = _random_states(cm, W, rng)
+    vt = rng.uniform(-0.3, 0.3, size=(W, cm.n))
+    sim = _sim(W, spr=2, period=3e-3)
+    sim.set("reset_q", q)
+    sim.set("reset_qd", qd)
+    sim.run(paused=True)
+    sim.set_control_mode(3)                       # Velocity
+    sim.set("velocity_target", vt)
+    ows = [_oracle_world(oracle, cm, q[w], qd[w], q[w], oracle.VELOCITY, period_ns=3_000_000,
+                         spr=2, vtgt=vt[w]) for w in range(W)]
+    worst = 0.0
+    for _ in range(H):
+        sim.run()
+        gq = sim.get("q")
+        for w in range(W):
+            ows[w].run()
+            worst = max(worst, float(np.abs(gq[w] - ows[w].q).max()))
+    print(f"panda velocity PID, period 3 dt: max|dq| {worst:.2e}")
+    assert worst <= 1e-4   # measured r01: 2.9e-6
+    sim.close()

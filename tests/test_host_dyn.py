@@ -57,17 +57,22 @@ def _substep(hd, P, q, qd, tau, act, vc, cons, dual, pgs=20):
     return q.astype(float), qd.astype(float), qdd.astype(float)
 
 
-@pytest.mark.parametrize("model", ["cartpole", "pendulum"])
-def test_unconstrained_substep(hd, oracle, cartpole_file, pendulum_file, model):
-    path = cartpole_file if model == "cartpole" else pendulum_file
+@pytest.mark.parametrize("model", ["cartpole", "pendulum", "panda"])
+def test_unconstrained_substep(hd, oracle, cartpole_file, pendulum_file, panda_file, model):
+    path = {"cartpole": cartpole_file, "pendulum": pendulum_file, "panda": panda_file}[model]
     P = _params(hd, path)
     cm = oracle.load_urdf(path)
     n = cm.n
     rng = np.random.default_rng(5)
+    # strictly inside the position limits: no constraint row may activate
+    lo = np.maximum([cm.model.lower[i] for i in range(n)], -2.0) + 1e-2
+    hi = np.minimum([cm.model.upper[i] for i in range(n)], 2.0) - 1e-2
+    eff = np.array([cm.model.effort[i] for i in range(n)])
     for _ in range(300):
-        q = rng.uniform(-2, 2, n).astype(np.float32)
+        q = rng.uniform(lo, hi).astype(np.float32)
         qd = rng.uniform(-3, 3, n).astype(np.float32)
-        tau = rng.uniform(-40, 40, n).astype(np.float32)
+        # the kernel callers clip to +-effort before the substep; the oracle clips inside
+        tau = np.clip(rng.uniform(-40, 40, n), -eff, eff).astype(np.float32)
         got = _substep(hd, P, q, qd, tau, np.zeros(n), np.zeros(n), cons=False, dual=False)
         ref = oracle.step(cm, 1e-3, q.astype(float), qd.astype(float), [oracle.FORCE] * n,
                           tau.astype(float))
@@ -105,3 +110,28 @@ def test_constraint_rows_and_damping(hd, oracle, pendulum_file, cartpole_file):
         qg, qdg, _ = _substep(hd, P, qg, qdg, [300.0, 0.0], [0, 0], [0, 0], cons=True, dual=False)
         qo, qdo, *_ = oracle.step(cm, 1e-3, qo, qdo, [oracle.FORCE, oracle.PASSIVE], [300.0, 0.0], 20)
     assert qg[0] <= 4.85 and abs(qg[0] - qo[0]) <= 1e-3 and np.abs(qdg - qdo).max() <= 1e-2
+
+
+def test_panda_tree_with_limit_rows(hd, oracle, panda_file):
+    """The branched Panda (fingers on the hand) with joint-limit rows active:
+    impulse columns of the tree, float32 device code vs fp64 oracle."""
+    P = _params(hd, panda_file)
+    cm = oracle.load_urdf(panda_file)
+    n = cm.n
+    lo = np.array([cm.model.lower[i] for i in range(n)])
+    hi = np.array([cm.model.upper[i] for i in range(n)])
+    rng = np.random.default_rng(11)
+    worst = 0.0
+    for _ in range(100):
+        # about half of the joints sit at / beyond a limit
+        q = rng.uniform(lo, hi)
+        at = rng.uniform(size=n) < 0.5
+        q[at] = np.where(rng.uniform(size=n) < 0.5, lo - 1e-3, hi + 1e-3)[at]
+        q = q.astype(np.float32)
+        qd = rng.uniform(-0.5, 0.5, n).astype(np.float32)
+        tau = rng.uniform(-10, 10, n).astype(np.float32)   # within every effort limit
+        got = _substep(hd, P, q, qd, tau, np.zeros(n), np.zeros(n), cons=True, dual=False, pgs=30)
+        ref = oracle.step(cm, 1e-3, q.astype(float), qd.astype(float), [oracle.FORCE] * n,
+                          tau.astype(float), 30)
+        worst = max(worst, float(np.abs(got[1] - ref[1]).max()))
+    assert worst <= 2e-4, worst

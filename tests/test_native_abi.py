@@ -66,7 +66,7 @@ def _export(N, path, pose=(0, 0, 0, 1, 0, 0, 0)):
         N.check(N.lib().mw_load_model(h, path.encode(), N.dptr(p), b""))
         n = ctypes.c_int32()
         N.check(N.lib().mw_dofs(h, ctypes.byref(n)))
-        out = np.zeros(33 * n.value + 3)
+        out = np.zeros(34 * n.value + 3)
         N.check(N.lib().mw_model_export(h, N.dptr(out), len(out)))
         names = []
         buf = ctypes.create_string_buffer(64)
@@ -79,10 +79,10 @@ def _export(N, path, pose=(0, 0, 0, 1, 0, 0, 0)):
         N.lib().mw_destroy(h)
 
 
-@pytest.mark.parametrize("model", ["cartpole", "pendulum"])
+@pytest.mark.parametrize("model", ["cartpole", "pendulum", "panda"])
 @pytest.mark.parametrize("pose", [(0, 0, 0, 1, 0, 0, 0), (0.3, -1, 2, 0.9238795, 0.3826834, 0, 0)])
-def test_model_compiler_matches_oracle_reader(N, oracle, cartpole_file, pendulum_file, model, pose):
-    path = cartpole_file if model == "cartpole" else pendulum_file
+def test_model_compiler_matches_oracle_reader(N, oracle, cartpole_file, pendulum_file, panda_file, model, pose):
+    path = {"cartpole": cartpole_file, "pendulum": pendulum_file, "panda": panda_file}[model]
     n, out, names, base = _export(N, path, pose)
     cm = oracle.load_urdf(path, pose_xyz=pose[:3], pose_wxyz=pose[3:])
     assert names == cm.joint_names and n == cm.n
@@ -90,7 +90,7 @@ def test_model_compiler_matches_oracle_reader(N, oracle, cartpole_file, pendulum
     M = cm.model
     big = lambda v: np.where(v > 1e299, np.inf, np.where(v < -1e299, -np.inf, v))
     for i in range(n):
-        b = out[33 * i: 33 * (i + 1)]
+        b = out[34 * i: 34 * (i + 1)]
         assert b[0] == M.jtype[i] and b[1] == M.limited[i]
         np.testing.assert_allclose(b[2:11], list(M.E[i]), atol=1e-12)
         np.testing.assert_allclose(b[11:14], list(M.r[i]), atol=1e-12)
@@ -100,7 +100,8 @@ def test_model_compiler_matches_oracle_reader(N, oracle, cartpole_file, pendulum
         np.testing.assert_allclose(b[21:27], list(M.Ic[i]), atol=1e-12)
         np.testing.assert_allclose(big(b[27:33]), [M.damping[i], M.friction[i], M.lower[i], M.upper[i],
                                                    M.effort[i], M.vel_limit[i]])
-    np.testing.assert_allclose(out[33 * n:], list(M.gravity_base), atol=1e-12)
+        assert b[33] == M.parent[i]
+    np.testing.assert_allclose(out[34 * n:], list(M.gravity_base), atol=1e-12)
 
 
 def test_fixed_joint_lumping(N, oracle):
@@ -121,8 +122,8 @@ def test_fixed_joint_lumping(N, oracle):
     n, out, names, base = _export(N, urdf)
     cm = oracle.load_urdf(urdf)
     assert names == ["j1", "j2"] == cm.joint_names and base == "a"
-    np.testing.assert_allclose(out[33 + 2:33 + 11], list(cm.model.E[1]), atol=1e-12)
-    np.testing.assert_allclose(out[33 + 11:33 + 14], list(cm.model.r[1]), atol=1e-12)
+    np.testing.assert_allclose(out[34 + 2:34 + 11], list(cm.model.E[1]), atol=1e-12)
+    np.testing.assert_allclose(out[34 + 11:34 + 14], list(cm.model.r[1]), atol=1e-12)
     np.testing.assert_allclose(out[21:27], list(cm.model.Ic[0]), atol=1e-12)
     np.testing.assert_allclose(out[18:21], list(cm.model.com[0]), atol=1e-12)
     assert out[17] == pytest.approx(2.5)
@@ -134,9 +135,11 @@ def test_fixed_joint_lumping(N, oracle):
     ("<robot name='x'><link name='world'/>", "XML"),
     ("<sdf><model name='m'/></sdf>", "URDF"),
     ("<robot name='x'><link name='world'/><link name='a'/><joint name='w' type='fixed'>"
-     "<parent link='world'/><child link='a'/></joint><link name='b'/><link name='c'/>"
+     "<parent link='world'/><child link='a'/></joint>"
+     "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+     "<link name='c'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
      "<joint name='j1' type='revolute'><parent link='a'/><child link='b'/></joint>"
-     "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>", "branched"),
+     "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>", "topology"),
 ])
 def test_unsupported_models_fail_loudly(N, bad, why):
     rc, h = _create(N)
@@ -171,5 +174,37 @@ def test_joint_params_before_first_run(N, pendulum_file):
         N.check(N.lib().mw_joint_param(h, 0, N.PARAM_COULOMB_FRICTION, ctypes.byref(v)))
         assert v.value == 0.01
         assert N.lib().mw_set_joint_param(h, 3, N.PARAM_COULOMB_FRICTION, 0.01) == N.MW_EINVAL
+    finally:
+        N.lib().mw_destroy(h)
+
+
+def test_pid_and_controller_period_semantics(N, panda_file):
+    """Joint::setPID / pid (Joint.cpp:63, :479-525), Model::setControllerPeriod
+    (Model.cpp:589-602) -- host logic, no GPU needed."""
+    rc, h = _create(N)
+    try:
+        p = np.array([0, 0, 0, 1, 0, 0, 0], dtype=np.float64)
+        N.check(N.lib().mw_load_model(h, panda_file.encode(), N.dptr(p), b""))
+        g = np.zeros(8)
+        N.check(N.lib().mw_joint_pid(h, 0, N.dptr(g)))
+        np.testing.assert_array_equal(g, [1.0, 0.1, 0.01, 0.0, -1.0, 0.0, 0.0, -1.0])   # DefaultPID
+        big = float(np.finfo(np.float64).max)
+        # open output limits are less limiting than +-effort (87 Nm): replaced
+        N.check(N.lib().mw_set_joint_pid(h, 0, N.dptr(np.array([50, 0, 20, -big, big, 0, -big, big.real]))))
+        N.check(N.lib().mw_joint_pid(h, 0, N.dptr(g)))
+        np.testing.assert_array_equal(g, [50, 0, 20, -87, 87, 0, -big, big])
+        # tighter limits are kept
+        N.check(N.lib().mw_set_joint_pid(h, 0, N.dptr(np.array([5, 1, 2, -10, 20, 0.5, -1, 1.0]))))
+        N.check(N.lib().mw_joint_pid(h, 0, N.dptr(g)))
+        np.testing.assert_array_equal(g, [5, 1, 2, -10, 20, 0.5, -1, 1])
+        assert N.lib().mw_set_joint_pid(h, 9, N.dptr(g)) == N.MW_EINVAL
+        t = ctypes.c_double()
+        N.check(N.lib().mw_controller_period(h, ctypes.byref(t)))
+        assert t.value == pytest.approx(9.223372036854776e9)        # max duration
+        assert N.lib().mw_set_controller_period(h, 0.0) == N.MW_EINVAL
+        assert "greater than zero" in N.last_error()
+        N.check(N.lib().mw_set_controller_period(h, 1e-3))
+        N.check(N.lib().mw_controller_period(h, ctypes.byref(t)))
+        assert t.value == 1e-3
     finally:
         N.lib().mw_destroy(h)
