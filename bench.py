@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-sweep", action="store_true")
+    p.add_argument("--no-panda", action="store_true", help="skip the config-4 Panda leg")
     return p.parse_args()
 
 
@@ -72,85 +73,35 @@ def main():
     if world_size > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from mwstep.shard import gather_obs
     from mwstep.vecenv import VecEnv
 
     W = args.worlds
     env = VecEnv(args.task, n_worlds=W, device=local_rank, seed=args.seed, world_offset=rank * W)
-    stream = torch.cuda.Stream(device=dev)
-    env.sim.set_stream(stream.cuda_stream)
     K = args.steps
-    G = max(1, min(args.graph_chunk, K))
-    n_full, rem = divmod(K, G)
-    total = args.warmup + K
-    gen = torch.Generator(device=dev).manual_seed(43 + rank)
-    if env.discrete:
-        actions = torch.randint(0, 2, (total, W), generator=gen, device=dev, dtype=torch.int32)
-    else:
-        actions = (torch.rand((total, W), generator=gen, device=dev) * 2 - 1) * 50.0
-    act_buf = torch.empty((G, W), dtype=actions.dtype, device=dev)
-
-    with torch.cuda.stream(stream):
-        env.reset()
-        # warmup (eager), then capture one graph of G step launches
-        for t in range(args.warmup):
-            env.step_raw(actions[t].data_ptr())
-        stream.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            for g in range(G):
-                env.step_raw(act_buf[g].data_ptr())
-        tail = None
-        if rem:
-            tail = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(tail, stream=stream):
-                for g in range(rem):
-                    env.step_raw(act_buf[g].data_ptr())
-        # one untimed replay to settle
-        act_buf.copy_(actions[:G])
-        graph.replay()
-    stream.synchronize()
-
-    # -------------------------------------------------------- timed region
-    if world_size > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(stream):
-        ev_start.record(stream)
-        for c in range(n_full):
-            base = args.warmup + c * G
-            act_buf.copy_(actions[base:base + G])
-            graph.replay()
-        if rem:
-            base = args.warmup + n_full * G
-            act_buf[:rem].copy_(actions[base:base + rem])
-            tail.replay()
-        ev_end.record(stream)
-        if world_size > 1:
-            gathered = gather_obs(env.obs)  # final observation tensor, RCCL over xGMI
-    torch.cuda.synchronize(dev)
-    if world_size > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world_size > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    actions = make_actions(env, args.warmup + K, dev, torch, rank)
+    timed = time_steps(env, actions, args.warmup, K, args.graph_chunk, dev, torch, dist, world_size,
+                       gather=(world_size > 1))
+    elapsed, kernel_us = timed["elapsed"], timed["kernel_us"]
     value = world_size * W * K / elapsed
+    G = timed["G"]
 
-    # ---------------- per-launch time of the step kernel: HIP events recorded on
-    # the launch stream around the timed graph replays (K launches)
-    kernel_us = ev_start.elapsed_time(ev_end) * 1e3 / K
-    bpe = algorithmic_bytes_per_env_step(env.sim.dofs, env.obs_dim)
+    # per-launch time of the step kernel: HIP events recorded on the launch
+    # stream around the timed graph replays (K launches), see time_steps()
+    if env.action_dim:
+        bpe = panda_bytes_per_env_step(env.sim.dofs)
+        kname = "vecenv_pid_step_kernel<9,PandaTopo,false,true>"
+    else:
+        bpe = algorithmic_bytes_per_env_step(env.sim.dofs, env.obs_dim)
+        kname = (f"vecenv_step_kernel<{env.sim.dofs},{env.kind},false,true,false,{env.sim.baked_model()}>"
+                 + (" (model constant-folded)" if env.sim.baked_model() else ""))
     achieved_gbs = bpe * W / (kernel_us * 1e-6) / 1e9
     traffic = pmc_traffic(args.task, W)
 
     # ------------------------------------------- fused open-loop rollout figure
     rollout = None
-    if not args.no_rollout:
+    if not args.no_rollout and not env.action_dim:
         T = 1000
+        stream = timed["stream"]
         with torch.cuda.stream(stream):
             env.rollout(actions[:T].contiguous())   # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -166,13 +117,19 @@ def main():
     # ---------------- world-count sweep (same kernel, graph mode): where the
     # latency regime ends and the HBM / VALU bound takes over
     sweep = None
-    if not args.no_sweep and world_size == 1:
+    if not args.no_sweep and world_size == 1 and not env.action_dim:
         sweep = world_sweep(args, dev, torch)
+
+    # ---------------- BASELINE config 4 (1024 Panda worlds, PID position
+    # tracking) measured in the same run when the headline is config 2
+    panda = None
+    if not args.no_panda and rank == 0 and world_size == 1 and args.task != "PandaPositionTracking":
+        panda = panda_leg(args, dev, torch, dist)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
     parity = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and not env.action_dim:
         cpu, parity = cpu_baseline_and_parity(args, env, actions, np, torch)
 
     if rank == 0:
@@ -191,7 +148,7 @@ def main():
             "data": "synthetic (Philox resets, uniform random actions, seed 42/43)",
             "config": {
                 "workload": f"{args.task}: {W} worlds per GPU, dt=1ms, 1 physics step per env step "
-                            "(BASELINE.json configs[1])",
+                            + ("(BASELINE.json configs[3])" if env.action_dim else "(BASELINE.json configs[1])"),
                 "task": args.task,
                 "worlds_per_gpu": W,
                 "global_worlds": W * world_size,
@@ -206,8 +163,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
-                "kernel": f"vecenv_step_kernel<2,0,false,true,false,{env.sim.baked_model()}>"
-                          + (" (model constant-folded)" if env.sim.baked_model() else ""),
+                "kernel": kname,
                 "kernel_us_per_launch": round(kernel_us, 3),
                 "timing": "HIP events on the launch stream over the K timed launches",
                 "bytes_per_env_step": bpe,
@@ -218,11 +174,123 @@ def main():
             "cpu_baseline": cpu,
             "obs_max_abs_err_vs_oracle": parity,
             "rollout_fused": rollout,
+            "panda_c4": panda,
         }
         print(json.dumps(out))
     env.close()
     if world_size > 1:
         dist.destroy_process_group()
+
+
+def panda_targets(q0, T, dt, torch):
+    """BASELINE config 4 targets: q0 + 0.9 (range/2) sin(2 pi 0.33 t) on joints 1
+    and 6 (tests/test_scenario/test_pid_controllers.py:91-99), the other joints
+    hold q0.  q0 [W, 9] is each world's reset pose; returns [T, W, 9]."""
+    import math
+    t = torch.arange(T, device=q0.device, dtype=torch.float32) * dt
+    s = torch.sin(2 * math.pi * 0.33 * t)[:, None]
+    tg = q0[None].repeat(T, 1, 1)
+    tg[:, :, 0] += 0.9 * (2 * 2.8973) / 2 * s
+    tg[:, :, 5] += 0.9 * (3.7525 + 0.0175) / 2 * s
+    return tg.contiguous()
+
+
+def make_actions(env, total, dev, torch, rank):
+    gen = torch.Generator(device=dev).manual_seed(43 + rank)
+    W = env.n_worlds
+    if env.action_dim:
+        q0 = env.reset()[:, :env.action_dim].clone()
+        return panda_targets(q0, total, 1e-3, torch)
+    if env.discrete:
+        return torch.randint(0, 2, (total, W), generator=gen, device=dev, dtype=torch.int32)
+    return (torch.rand((total, W), generator=gen, device=dev) * 2 - 1) * 50.0
+
+
+def time_steps(env, actions, warmup, K, chunk, dev, torch, dist, world_size, gather=False):
+    """W untimed warmup steps, then EXACTLY K steps replayed from hipGraphs of
+    `chunk` step launches (the action slice of every step is copied into the
+    graph's action buffer before each replay, as a policy would write it),
+    bracketed by barrier + synchronize; max over ranks."""
+    from mwstep.shard import gather_obs
+    stream = torch.cuda.Stream(device=dev)
+    env.sim.set_stream(stream.cuda_stream)
+    G = max(1, min(chunk, K))
+    n_full, rem = divmod(K, G)
+    act_buf = torch.empty((G,) + tuple(actions.shape[1:]), dtype=actions.dtype, device=dev)
+    with torch.cuda.stream(stream):
+        env.reset()
+        for t in range(warmup):
+            env.step_raw(actions[t].data_ptr())
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for g in range(G):
+                env.step_raw(act_buf[g].data_ptr())
+        tail = None
+        if rem:
+            tail = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tail, stream=stream):
+                for g in range(rem):
+                    env.step_raw(act_buf[g].data_ptr())
+        act_buf.copy_(actions[:G])
+        graph.replay()       # one untimed replay to settle
+    stream.synchronize()
+
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        ev_start.record(stream)
+        for c in range(n_full):
+            base = warmup + c * G
+            act_buf.copy_(actions[base:base + G])
+            graph.replay()
+        if rem:
+            base = warmup + n_full * G
+            act_buf[:rem].copy_(actions[base:base + rem])
+            tail.replay()
+        ev_end.record(stream)
+        if gather:
+            gather_obs(env.obs)  # final observation tensor, RCCL over xGMI
+    torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return {"elapsed": elapsed, "kernel_us": ev_start.elapsed_time(ev_end) * 1e3 / K, "G": G,
+            "stream": stream}
+
+
+def panda_bytes_per_env_step(n=9):
+    """Compulsory HBM bytes of one PandaPositionTracking step of one world:
+    read q, qd, targets (4 B x 3n), PID state e/i/u (12n), counters (8 B);
+    write q, qd (8n), PID state (12n), obs 2n floats (8n), reward 4, done 1, steps 4."""
+    return (12 * n + 12 * n + 8) + (8 * n + 12 * n + 8 * n + 9)
+
+
+def panda_leg(args, dev, torch, dist):
+    from mwstep.vecenv import VecEnv
+    W, K, warm = 1024, 1000, 100
+    env = VecEnv("PandaPositionTracking", n_worlds=W, device=dev.index, seed=args.seed,
+                 max_episode_steps=5000)
+    actions = make_actions(env, warm + K, dev, torch, 0)
+    r = time_steps(env, actions, warm, K, args.graph_chunk, dev, torch, dist, 1)
+    bpe = panda_bytes_per_env_step(env.sim.dofs)
+    gbs = bpe * W / (r["kernel_us"] * 1e-6) / 1e9
+    out = {"workload": f"PandaPositionTracking: {W} worlds (9-dof tree), Position-mode PID every 1 ms step, "
+                       "sinusoidal targets on joints 1 and 6 (BASELINE.json configs[3])",
+           "value": round(W * K / r["elapsed"], 1), "unit": "env·steps/s", "steps": K, "warmup": warm,
+           "ms_per_step": round(r["elapsed"] / K * 1e3, 6),
+           "kernel_us_per_launch": round(r["kernel_us"], 3),
+           "bytes_per_env_step": bpe, "achieved_GBs": round(gbs, 3),
+           "hbm_frac": round(gbs / HBM_PEAK_GBS, 6)}
+    env.close()
+    return out
 
 
 def pmc_traffic(task, W):

@@ -36,8 +36,8 @@ __device__ __forceinline__ const ChainF* model_params(const ChainF* P) {
 
 // ------------------------------------------------------------ RNG -------
 __device__ __forceinline__ void philox(uint32_t seed_lo, uint32_t seed_hi, uint32_t world,
-                                       uint32_t episode, uint32_t (&out)[4]) {
-    uint32_t c0 = world, c1 = episode, c2 = 0u, c3 = 0u, k0 = seed_lo, k1 = seed_hi;
+                                       uint32_t episode, uint32_t (&out)[4], uint32_t block = 0u) {
+    uint32_t c0 = world, c1 = episode, c2 = block, c3 = 0u, k0 = seed_lo, k1 = seed_hi;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
@@ -322,6 +322,115 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
     V.steps[w] = steps;
 }
 
+// ------------------------------------------------ position-target task ----
+// kind 4 (BASELINE config 4, Panda): every joint in Position mode, the
+// JointController PID runs every substep (controller period = step size,
+// test_pid_controllers.py:69) on error = q - target (JointController.cpp:308).
+// obs = [q, qd] (2n), reward = -sum (q - target)^2, done = TimeLimit only;
+// reset: home pose + U(-noise, noise) per joint (Philox block k = 4-dof group),
+// clipped into the position limits, qd = 0, PID reset.
+template <int N>
+__device__ __forceinline__ void pid_task_reset(const ChainF* __restrict__ P, const TaskF& T, uint32_t w,
+                                               uint32_t episode, float (&q)[N], float (&qd)[N]) {
+#pragma unroll
+    for (int b = 0; b < (N + 3) / 4; ++b) {
+        uint32_t r[4];
+        philox(T.seed_lo, T.seed_hi, w, episode, r, static_cast<uint32_t>(b));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int d = 4 * b + k;
+            if (d < N) {
+                const float x = T.home[d] + unif(r[k], -T.home_noise, T.home_noise);
+                q[d] = P->b[d].limited ? fminf(fmaxf(x, P->b[d].lower), P->b[d].upper) : x;
+                qd[d] = 0.f;
+            }
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void store_pid_obs(float* __restrict__ dst, const float (&q)[N], const float (&qd)[N]) {
+#pragma unroll
+    for (int d = 0; d < N; ++d) { dst[d] = q[d]; dst[N + d] = qd[d]; }
+}
+
+template <int N, Topo TOPO, bool DUAL, bool CONS>
+__global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __restrict__ P, TaskF T, SimDev S,
+                                                              VecDev V, PidSet pid,
+                                                              const float* __restrict__ targets,
+                                                              float* __restrict__ obs, float* __restrict__ reward,
+                                                              uint8_t* __restrict__ done_out,
+                                                              float* __restrict__ term_obs, int W, float dt,
+                                                              float inv_dt, int substeps, int pgs_iters) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    float q[N], qd[N], tgt[N], pe[N], pi[N], pu[N];
+    load_state<N>(S, W, w, q, qd);
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        tgt[d] = targets[static_cast<size_t>(w) * N + d];
+        pe[d] = S.pid_e[d * W + w];
+        pi[d] = S.pid_i[d * W + w];
+        pu[d] = S.pid_u[d * W + w];
+    }
+    uint8_t act[N];
+    float vc[N];
+#pragma unroll
+    for (int d = 0; d < N; ++d) { act[d] = kActPidPos; vc[d] = 0.f; }
+    float tau[N], qdd[N];
+    for (int s = 0; s < substeps; ++s) {
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            float u = pu[d];
+            if (!pid_update(pid.g[d], q[d] - tgt[d], inv_dt, dt, pe[d], pi[d], u)) u = 0.f;
+            else pu[d] = u;
+            const float e = P->b[d].effort;
+            tau[d] = fminf(fmaxf(u, -e), e);
+        }
+        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
+    }
+    float r = 0.f;
+#pragma unroll
+    for (int d = 0; d < N; ++d) r -= (q[d] - tgt[d]) * (q[d] - tgt[d]);
+    reward[w] = r;
+    const uint32_t episode0 = V.episode[w];
+    uint32_t steps = V.steps[w] + 1u;
+    const bool d_ = (T.max_steps > 0 && steps >= static_cast<uint32_t>(T.max_steps));
+    done_out[w] = d_ ? 1 : 0;
+    if (d_) {
+        store_pid_obs<N>(term_obs + static_cast<size_t>(w) * 2 * N, q, qd);
+        steps = 0u;
+        V.episode[w] = episode0 + 1u;
+        pid_task_reset<N>(P, T, T.world_offset + static_cast<uint32_t>(w), episode0 + 1u, q, qd);
+#pragma unroll
+        for (int d = 0; d < N; ++d) { pe[d] = 0.f; pi[d] = 0.f; pu[d] = 0.f; }
+    }
+    store_pid_obs<N>(obs + static_cast<size_t>(w) * 2 * N, q, qd);
+    store_state<N>(S, W, w, q, qd);
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        S.pid_e[d * W + w] = pe[d];
+        S.pid_i[d * W + w] = pi[d];
+        S.pid_u[d * W + w] = pu[d];
+    }
+    V.steps[w] = steps;
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) vecenv_pid_reset_kernel(const ChainF* __restrict__ P, TaskF T, SimDev S,
+                                                               VecDev V, float* __restrict__ obs, int W) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    float q[N], qd[N];
+    pid_task_reset<N>(P, T, T.world_offset + static_cast<uint32_t>(w), 0u, q, qd);
+    store_pid_obs<N>(obs + static_cast<size_t>(w) * 2 * N, q, qd);
+    store_state<N>(S, W, w, q, qd);
+#pragma unroll
+    for (int d = 0; d < N; ++d) { S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; }
+    V.episode[w] = 0u;
+    V.steps[w] = 0u;
+}
+
 }  // namespace dev
 
 // ------------------------------------------------------- launchers ------
@@ -412,10 +521,12 @@ hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool
     }
 }
 
-hipError_t launch_vecenv_reset(const ChainF* /*P*/, int n, const TaskF& T, const SimDev& S,
+hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
                                const VecDev& V, float* obs, int W, hipStream_t st) {
     const int B = block_for(W);
-    if (T.kind == 3 && n == 1)
+    if (T.kind == 4 && n == 9)
+        hipLaunchKernelGGL((dev::vecenv_pid_reset_kernel<9>), grid_for(W, B), dim3(B), 0, st, P, T, S, V, obs, W);
+    else if (T.kind == 3 && n == 1)
         hipLaunchKernelGGL((dev::vecenv_reset_kernel<1, 3>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
     else if (T.kind == 0 && n == 2)
         hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 0>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
@@ -425,6 +536,28 @@ hipError_t launch_vecenv_reset(const ChainF* /*P*/, int n, const TaskF& T, const
         hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 2>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
     else
         return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, const TaskF& T,
+                                  const SimDev& S, const VecDev& V, const PidSet& pid, const float* targets,
+                                  float* obs, float* reward, uint8_t* done, float* term_obs, int W,
+                                  float dt, int substeps, int pgs_iters, hipStream_t st) {
+    if (n != 9 || topo != 1) return hipErrorInvalidValue;
+    const int B = block_for(W);
+    const float inv_dt = 1.f / dt;
+    if (!cons)
+        hipLaunchKernelGGL((dev::vecenv_pid_step_kernel<9, kPandaTopo, false, false>), grid_for(W, B), dim3(B), 0,
+                           st, P, T, S, V, pid, targets, obs, reward, done, term_obs, W, dt, inv_dt, substeps,
+                           pgs_iters);
+    else if (!dual)
+        hipLaunchKernelGGL((dev::vecenv_pid_step_kernel<9, kPandaTopo, false, true>), grid_for(W, B), dim3(B), 0,
+                           st, P, T, S, V, pid, targets, obs, reward, done, term_obs, W, dt, inv_dt, substeps,
+                           pgs_iters);
+    else
+        hipLaunchKernelGGL((dev::vecenv_pid_step_kernel<9, kPandaTopo, true, true>), grid_for(W, B), dim3(B), 0,
+                           st, P, T, S, V, pid, targets, obs, reward, done, term_obs, W, dt, inv_dt, substeps,
+                           pgs_iters);
     return hipGetLastError();
 }
 

@@ -49,6 +49,9 @@ struct TaskF {
     float force_mag;
     float x_factor;   // reward rail factor (0.9 / 1.0 / 0.8)
     float hi[4];      // float32 bounds of the done-space (reset_space / observation_space)
+    // position-target tasks (kind 4): reset pose and half-width of its uniform noise
+    float home[kMaxKernelDofs];
+    float home_noise;
 };
 
 struct VecDev {
@@ -66,6 +69,13 @@ hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool
 
 hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
                                const VecDev& V, float* obs, int W, hipStream_t st);
+
+// Position-target task (kind 4, Panda): actions float32 [W, n] are the
+// JointController position targets; PID every substep (period = step size).
+hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, const TaskF& T,
+                                  const SimDev& S, const VecDev& V, const PidSet& pid, const float* targets,
+                                  float* obs, float* reward, uint8_t* done, float* term_obs, int W,
+                                  float dt, int substeps, int pgs_iters, hipStream_t st);
 
 // T_steps == 0: one step with the per-step output layout; otherwise a fused
 // open-loop rollout of T_steps steps ([T, W] inputs and outputs).

@@ -866,9 +866,13 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
     *out = nullptr;
     const int n = s->n;
     const bool cart = cfg->kind >= MW_TASK_CARTPOLE_DISCRETE && cfg->kind <= MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP;
+    const bool pidtask = cfg->kind == MW_TASK_PANDA_POSITION_TRACKING;
     if (cart && n != 2) return fail(MW_EINVAL, "CartPole tasks need the 2-dof cartpole model");
     if (cfg->kind == MW_TASK_PENDULUM_SWINGUP && n != 1) return fail(MW_EINVAL, "PendulumSwingUp needs the 1-dof pendulum model");
-    if (!cart && cfg->kind != MW_TASK_PENDULUM_SWINGUP) return fail(MW_EINVAL, "unknown task kind");
+    if (pidtask && (n != 9 || s->topo != 1))
+        return fail(MW_EINVAL, "PandaPositionTracking needs the 9-dof Panda model");
+    if (pidtask && s->cfg.steps_per_run > 64) return fail(MW_EINVAL, "steps_per_run must be <= 64");
+    if (!cart && !pidtask && cfg->kind != MW_TASK_PENDULUM_SWINGUP) return fail(MW_EINVAL, "unknown task kind");
     auto e = std::make_unique<mw_vecenv>();
     e->sim = s;
     e->cfg = *cfg;
@@ -876,7 +880,7 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
     T.kind = cfg->kind;
     T.max_steps = cfg->max_episode_steps;
     T.reward_cart_at_center = cfg->reward_cart_at_center;
-    T.n_obs = (cfg->kind == MW_TASK_PENDULUM_SWINGUP) ? 3 : 4;
+    T.n_obs = (cfg->kind == MW_TASK_PENDULUM_SWINGUP) ? 3 : (pidtask ? 2 * n : 4);
     T.seed_lo = static_cast<uint32_t>(cfg->seed);
     T.seed_hi = static_cast<uint32_t>(cfg->seed >> 32);
     if (cfg->world_offset < 0) return fail(MW_EINVAL, "world_offset must be >= 0");
@@ -901,6 +905,22 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
         T.x_factor = 0.f;
         T.hi[0] = 1.f; T.hi[1] = 1.f; T.hi[2] = 10.f; T.hi[3] = 0.f;
         break;
+    case MW_TASK_PANDA_POSITION_TRACKING: {
+        // start pose of test_pid_controllers.py:49-59 (joints 1 and 6 at mid-range,
+        // the others at 0) with joint 4 at its upper limit (0 violates it), +-0.05 rad
+        for (int d = 0; d < n; ++d) {
+            const mw::ChainBody& b = s->model.bodies[d];
+            double h = 0.0;
+            if (d == 0 || d == 5) h = 0.5 * (b.lower + b.upper);
+            if (d == 3) h = b.upper;
+            T.home[d] = static_cast<float>(h);
+        }
+        T.home_noise = 0.05f;
+        // the JointController runs every physics step (period = step size)
+        s->period_ns = s->dt_ns;
+        s->controller = true;
+        break;
+    }
     }
     MW_HIP(hipSetDevice(s->cfg.device));
     MW_HIP(hipMalloc(&e->d_counters, 2 * static_cast<size_t>(s->W) * sizeof(uint32_t)));
@@ -938,6 +958,17 @@ static int vec_common(mw_vecenv* e, int32_t T, const void* a, float* o, float* r
         ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(to)) & 15u))
         return fail(MW_EINVAL, "obs buffers must be 16-byte aligned");
     mw_sim* s = e->sim;
+    if (e->task.kind == MW_TASK_PANDA_POSITION_TRACKING) {
+        if (T > 0) return fail(MW_EINVAL, "the fused rollout is not available for position-target tasks");
+        MW_HIP(mw::launch_vecenv_pid_step(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), e->task, s->dev,
+                                          e->dev, pid_set(s), static_cast<const float*>(a), o, r, d, to, s->W,
+                                          static_cast<float>(s->cfg.step_size), s->cfg.steps_per_run,
+                                          s->cfg.pgs_iters, s->stream));
+        s->host_stale = true;
+        s->iterations += s->cfg.steps_per_run;
+        s->stepped = true;
+        return MW_OK;
+    }
     MW_HIP(mw::launch_vecenv_step(s->d_params, s->n, needs_cons(s), needs_dual(s), baked_id(s), e->task, s->dev, e->dev,
                                   a, o, r, d, to, s->W, static_cast<float>(s->cfg.step_size),
                                   s->cfg.steps_per_run, s->cfg.pgs_iters, T, s->stream));

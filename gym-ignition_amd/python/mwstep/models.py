@@ -23,3 +23,19 @@ def get_model_file(name: str) -> str:
 
 def get_robot_names():
     return sorted(_FILES)
+
+
+# Panda JointController gains at 1 kHz, as the reference sets them
+# (python/gym_ignition_environments/models/panda.py:48-58,
+#  tests/test_scenario/test_pid_controllers.py:20-30): (P, I, D)
+PANDA_PID_GAINS_1000HZ = {
+    "panda_joint1": (50.0, 0.0, 20.0),
+    "panda_joint2": (10000.0, 0.0, 500.0),
+    "panda_joint3": (100.0, 0.0, 10.0),
+    "panda_joint4": (1000.0, 0.0, 50.0),
+    "panda_joint5": (100.0, 0.0, 10.0),
+    "panda_joint6": (100.0, 0.0, 10.0),
+    "panda_joint7": (10.0, 0.5, 0.1),
+    "panda_finger_joint1": (100.0, 0.0, 50.0),
+    "panda_finger_joint2": (100.0, 0.0, 50.0),
+}

@@ -33,6 +33,7 @@ TASK_CARTPOLE_DISCRETE = 0
 TASK_CARTPOLE_CONTINUOUS_BALANCING = 1
 TASK_CARTPOLE_CONTINUOUS_SWINGUP = 2
 TASK_PENDULUM_SWINGUP = 3
+TASK_PANDA_POSITION_TRACKING = 4
 
 
 class MwConfig(ctypes.Structure):

@@ -18,6 +18,8 @@ from __future__ import annotations
 import ctypes
 from typing import Dict, Optional, Tuple
 
+import numpy as np
+
 from . import native as N
 from .models import get_model_file
 from .sim import Simulator
@@ -27,6 +29,9 @@ TASKS = {
     "CartPoleContinuousBalancing": (N.TASK_CARTPOLE_CONTINUOUS_BALANCING, "cartpole"),
     "CartPoleContinuousSwingup": (N.TASK_CARTPOLE_CONTINUOUS_SWINGUP, "cartpole"),
     "PendulumSwingUp": (N.TASK_PENDULUM_SWINGUP, "pendulum"),
+    # BASELINE config 4: Position-mode PID control of every Panda joint,
+    # actions = position targets [n_worlds, 9]
+    "PandaPositionTracking": (N.TASK_PANDA_POSITION_TRACKING, "panda"),
 }
 
 
@@ -60,6 +65,12 @@ class VecEnv:
                                  step_size=1.0 / physics_rate, steps_per_run=steps_per_run,
                                  device=device, pgs_iters=pgs_iters,
                                  stream=self._stream.cuda_stream)
+        if kind == N.TASK_PANDA_POSITION_TRACKING:
+            from .models import PANDA_PID_GAINS_1000HZ
+            big = float(np.finfo(np.float64).max)
+            for d, name in enumerate(self.sim.joint_names):
+                p, i, dd = PANDA_PID_GAINS_1000HZ[name]
+                self.sim.set_pid(d, [p, i, dd, -big, big, 0.0, -big, big])
         cfg = N.MwTaskConfig(kind, max_episode_steps, 1 if reward_cart_at_center else 0,
                              world_offset, seed & 0xFFFFFFFFFFFFFFFF)
         h = ctypes.c_void_p()
@@ -70,6 +81,7 @@ class VecEnv:
         N.check(N.lib().mw_vecenv_obs_dim(h, ctypes.byref(no)))
         self.obs_dim = no.value
         self.discrete = kind == N.TASK_CARTPOLE_DISCRETE
+        self.action_dim = self.sim.dofs if kind == N.TASK_PANDA_POSITION_TRACKING else 0
         f32 = dict(dtype=torch.float32, device=self.device)
         self.obs = torch.zeros((n_worlds, self.obs_dim), **f32)
         self.reward = torch.zeros((n_worlds,), **f32)
@@ -95,6 +107,8 @@ class VecEnv:
         torch = _torch()
         want = torch.int32 if self.discrete else torch.float32
         shape = (self.n_worlds,) if T == 0 else (T, self.n_worlds)
+        if self.action_dim:
+            shape = shape + (self.action_dim,)
         if not isinstance(actions, torch.Tensor) or actions.device != self.device:
             raise TypeError(f"actions must be a torch tensor on {self.device}")
         if actions.dtype != want or tuple(actions.shape) != shape or not actions.is_contiguous():

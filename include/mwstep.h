@@ -176,6 +176,13 @@ int mw_copy_state(mw_sim* sim, float* q_dev, float* qd_dev, int to_sim);
 #define MW_TASK_CARTPOLE_CONTINUOUS_BALANCING 1
 #define MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP 2
 #define MW_TASK_PENDULUM_SWINGUP 3
+/* Position-target control of the 9-dof Panda (BASELINE config 4): actions
+ * float32 [n_worlds, 9] are the Position-mode targets of every joint, the
+ * JointController PID (gains: mw_set_joint_pid) runs every physics step;
+ * obs = [q, qd] (18), reward = -|q - target|^2, done = TimeLimit only; reset
+ * to the start pose of tests/test_scenario/test_pid_controllers.py:49-59
+ * (joint 4 at its upper limit) + U(-0.05, 0.05) rad per joint. */
+#define MW_TASK_PANDA_POSITION_TRACKING 4
 
 typedef struct {
     int32_t kind;
@@ -192,7 +199,8 @@ int mw_vecenv_obs_dim(const mw_vecenv* env, int32_t* n);
 /* Reset every world (episode 0); obs_dev float32 [n_worlds, obs_dim]. */
 int mw_vecenv_reset(mw_vecenv* env, float* obs_dev);
 /* One env step of every world, asynchronous on the sim's stream.
- *   actions_dev: int32 [n_worlds] (discrete) or float32 [n_worlds]
+ *   actions_dev: int32 [n_worlds] (discrete), float32 [n_worlds], or
+ *                float32 [n_worlds, dofs] (position-target tasks)
  *   obs_dev float32 [n_worlds, obs_dim]  (reset obs where done)
  *   reward_dev float32 [n_worlds], done_dev uint8 [n_worlds]
  *   terminal_obs_dev float32 [n_worlds, obs_dim] (written only where done) */

@@ -200,3 +200,97 @@ def test_period_gating_and_velocity_pid(require_gpu, oracle, panda_file):
     print(f"panda velocity PID, period 3 dt: max|dq| {worst:.2e}")
     assert worst <= 1e-4   # measured r01: 2.9e-6
     sim.close()
+
+
+# --------------------------------------------------------------------------
+# batched position-target env (BASELINE config 4 path): PandaPositionTracking
+# --------------------------------------------------------------------------
+
+def _unif32(x, lo, hi):
+    t = np.float32((x >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0))
+    return np.float32(lo) + (np.float32(hi) - np.float32(lo)) * t
+
+
+def _panda_reset_ref(oracle, cm, seed, world, episode):
+    """Restatement of the kernel's reset: start pose of test_pid_controllers.py
+    (joint 4 at its upper limit) + U(-0.05, 0.05), Philox4x32-10 keyed by the
+    seed, counter (world, episode, block, 0), clipped into the limits."""
+    n = cm.n
+    home = np.zeros(n)
+    home[0] = 0.5 * (cm.model.lower[0] + cm.model.upper[0])
+    home[5] = 0.5 * (cm.model.lower[5] + cm.model.upper[5])
+    home[3] = cm.model.upper[3]
+    q = np.zeros(n, np.float32)
+    for b in range((n + 3) // 4):
+        r = oracle.philox_raw([world, episode, b, 0], [seed & 0xFFFFFFFF, seed >> 32])
+        for k in range(4):
+            d = 4 * b + k
+            if d < n:
+                x = np.float32(home[d]) + _unif32(np.array([r[k]], np.uint32), -0.05, 0.05)[0]
+                q[d] = np.clip(x, np.float32(cm.model.lower[d]), np.float32(cm.model.upper[d]))
+    return q
+
+
+def test_panda_vecenv_reset(require_gpu, oracle, panda_file):
+    from mwstep.vecenv import VecEnv
+    W = 300
+    env = VecEnv("PandaPositionTracking", n_worlds=W, seed=7)
+    obs = env.reset().cpu().numpy()
+    cm = oracle.load_urdf(panda_file)
+    for w in range(0, W, 7):
+        ref = _panda_reset_ref(oracle, cm, 7, w, 0)
+        assert np.abs(obs[w, :9] - ref).max() <= 1e-6
+        assert np.all(obs[w, 9:] == 0)
+    env.close()
+
+
+def test_panda_vecenv_vs_oracle(require_gpu, oracle, panda_file):
+    """Free-running PandaPositionTracking vs per-world oracle ScenarioWorlds
+    (same start state, PID gains, period = dt): obs within 5e-4, reward
+    within 1e-5 relative; TimeLimit auto-reset at step 150."""
+    import torch
+    from mwstep.vecenv import VecEnv
+    W, H, T_LIM = 32, 300, 150
+    env = VecEnv("PandaPositionTracking", n_worlds=W, seed=3, max_episode_steps=T_LIM)
+    cm = oracle.load_urdf(panda_file)
+    # resets clip onto the limits exactly: give the oracle the kernel's float32
+    # limits so that "at the limit" means the same thing to both
+    for i in range(cm.n):
+        cm.model.lower[i] = float(np.float32(cm.model.lower[i]))
+        cm.model.upper[i] = float(np.float32(cm.model.upper[i]))
+    obs0 = env.reset().cpu().numpy()
+    ows = [_oracle_world(oracle, cm, obs0[w, :9], np.zeros(9), obs0[w, :9].astype(float), oracle.POSITION)
+           for w in range(W)]
+    phase = np.linspace(0, np.pi, W)
+    worst_o = worst_r = 0.0
+    for k in range(H):
+        t = k * 1e-3
+        tgt = obs0[:, :9].astype(np.float64).copy()
+        tgt[:, 0] += 0.9 * 2.8973 * np.sin(2 * np.pi * 0.33 * t + phase)
+        tgt[:, 5] += 0.9 * 1.885 * np.sin(2 * np.pi * 0.33 * t + phase)
+        tgt = tgt.astype(np.float32)
+        o, r, d, info = env.step(torch.from_numpy(tgt).cuda())
+        o, r, d = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy().astype(bool)
+        assert d.all() == ((k + 1) % T_LIM == 0) and d.any() == d.all()
+        for w in range(W):
+            ow = ows[w]
+            ow.ptgt[:] = tgt[w]
+            ow.run()
+            ref_obs = np.concatenate([ow.q, ow.qd])
+            ref_r = -float(np.sum((ow.q - tgt[w].astype(np.float64)) ** 2))
+            if d[w]:
+                term = info["terminal_obs"].cpu().numpy()[w]
+                worst_o = max(worst_o, float(np.abs(term - ref_obs).max()))
+                # restart the oracle world from the kernel's reset state
+                ep = (k + 1) // T_LIM
+                qr = _panda_reset_ref(oracle, cm, 3, w, ep)
+                assert np.abs(o[w, :9] - qr).max() <= 1e-6 and np.all(o[w, 9:] == 0)
+                ows[w] = _oracle_world(oracle, cm, o[w, :9], np.zeros(9), o[w, :9].astype(float),
+                                       oracle.POSITION)
+                ows[w].prev_ns = 0
+            else:
+                worst_o = max(worst_o, float(np.abs(o[w] - ref_obs).max()))
+            worst_r = max(worst_r, abs(r[w] - ref_r) / (1.0 + abs(ref_r)))
+    print(f"PandaPositionTracking vs oracle, H={H}: max|obs err| {worst_o:.2e}, reward rel err {worst_r:.2e}")
+    assert worst_o <= 5e-4 and worst_r <= 1e-4
+    env.close()
