@@ -192,9 +192,16 @@ __device__ __forceinline__ SV motion(const BodyF& b, float s) {
     const float sw = rev ? s : 0.f, sv = rev ? 0.f : s;
     return {{b.axis[0] * sw, b.axis[1] * sw, b.axis[2] * sw}, {b.axis[0] * sv, b.axis[1] * sv, b.axis[2] * sv}};
 }
+// S^T x.  Both dots are computed and the VALUES selected: written as
+// `rev ? dot(a, x.w) : dot(a, x.v)`, SimplifyCFG sinks the common dot into a
+// load through a selected address when x is stored, which pins the whole
+// stage in scratch memory.  (dot(motion(b, 1), x) avoids that too but cannot
+// fold its 0 * x terms for the constant-folded models.)
 __device__ __forceinline__ float proj(const BodyF& b, const SV& x) {
     const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
-    return (b.jtype == 0) ? dot(a, x.w) : dot(a, x.v);
+    const float dw = dot(a, x.w);
+    const float dv = dot(a, x.v);
+    return (b.jtype == 0) ? dw : dv;
 }
 
 // AI S for the body's joint: revolute S = [a; 0] -> [A a; B^T a],
@@ -215,17 +222,72 @@ struct BodyState {
     float psi; // (S^T AI S + dt d)^-1
     float tt;  // total joint force
     SV eta;    // velocity-product acceleration
+    float pad_;  // 27 words: an odd record stride keeps LDS lanes conflict-free
 };
 struct ImpulseFactor {  // non-implicit (only when the model has damping)
     SV U;
     float psi;
 };
+struct SV7 {  // padded spatial vector (LDS record)
+    SV v;
+    float pad_;
+};
+
+// Per-body storage of one substep ("stage").  RegStage keeps it in VGPRs
+// (small models: every index folds after unrolling); LdsStage keeps one
+// padded record per (body, lane) in LDS, record stride = 64 lanes, so a
+// wave's accesses to one field hit 64 distinct banks.  The 7..9-dof kernels
+// use LdsStage: in VGPRs their per-body state exceeds the 512-register file
+// and spills to scratch (global memory).
+template <int N, bool DUAL>
+struct RegStage {
+    BodyState bs_[N];
+    ImpulseFactor nf_[DUAL ? N : 1];
+    SV own_[N];
+    float mv_[N][N];  // M^-1 columns of the active constraint rows
+    static constexpr bool kRuntimeColumns = false;
+    __device__ __forceinline__ float& mv(int k, int j) { return mv_[k][j]; }
+    __device__ __forceinline__ void fence() const {}
+    __device__ __forceinline__ BodyState& bs(int i) { return bs_[i]; }
+    __device__ __forceinline__ const BodyState& bs(int i) const { return bs_[i]; }
+    __device__ __forceinline__ ImpulseFactor& nf(int i) { return nf_[i]; }
+    __device__ __forceinline__ const ImpulseFactor& nf(int i) const { return nf_[i]; }
+    __device__ __forceinline__ SV& own(int i) { return own_[i]; }
+};
+
+constexpr int kLdsLanes = 64;  // LdsStage kernels run one wave per workgroup
 
 template <int N, bool DUAL>
-struct Work {
-    BodyState bs[N];
-    ImpulseFactor nf[DUAL ? N : 1];
+struct LdsStage {
+    BodyState* b;       // &records[0][lane]
+    ImpulseFactor* f;
+    SV7* o;
+    float* m;           // M^-1, [N * N][lanes]
+    // unrolled columns measured faster than one runtime-J column body
+    // (scripts/ab_panda.py, 1024 Panda worlds: 27.7 vs 30.3 us per step)
+#ifdef MW_RUNTIME_COLUMNS
+    static constexpr bool kRuntimeColumns = true;
+#else
+    static constexpr bool kRuntimeColumns = false;
+#endif
+    __device__ __forceinline__ float& mv(int k, int j) const { return m[(k * N + j) * kLdsLanes]; }
+    // compiler-only barrier: LDS values are re-read after it instead of being
+    // kept live in VGPRs across the unrolled columns / PGS sweeps
+    __device__ __forceinline__ void fence() const {
+#ifndef MW_HOST_TEST
+        asm volatile("" ::: "memory");
+#endif
+    }
+    __device__ __forceinline__ BodyState& bs(int i) const { return b[i * kLdsLanes]; }
+    __device__ __forceinline__ ImpulseFactor& nf(int i) const { return f[i * kLdsLanes]; }
+    __device__ __forceinline__ SV& own(int i) const { return o[i * kLdsLanes].v; }
 };
+
+// LDS words per lane of an LdsStage<N, DUAL>
+template <int N, bool DUAL>
+constexpr int lds_stage_words() {
+    return N * (27 + 7 + (DUAL ? 7 : 0)) + N * N;
+}
 
 // 1/x: the hardware reciprocal (1 ulp) on the device, IEEE division on the host
 __device__ __forceinline__ float rcp(float x) {
@@ -286,18 +348,17 @@ __device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p
 // Per-body temporaries are arrays indexed by compile-time body numbers (every
 // loop is unrolled and parent_of() folds), so they stay in VGPRs; for a
 // serial chain only one carried articulated inertia is live at a time.
-template <int N, bool DUAL, Topo TOPO>
+template <int N, bool DUAL, Topo TOPO, class WK>
 __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&q)[N],
                                     const float (&qd)[N], const float (&tau)[N], float dt,
-                                    float (&qdd)[N], Work<N, DUAL>& W) {
-    SV Bown[N];
+                                    float (&qdd)[N], WK& W) {
     SV V[N];
     f3 g[N];
     // outward pass: kinematics, velocities, bias forces
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const BodyF& b = P->b[i];
-        BodyState& s = W.bs[i];
+        BodyState& s = W.bs(i);
         const int pa = parent_of(TOPO, i);
         joint_pose(b, q[i], s.R, s.p);
         const SV Sq = motion(b, qd[i]);
@@ -317,8 +378,8 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         const f3 hw = mul(Io, Vi.w) + b.mass * cross(c, Vi.v);
         const f3 hv = b.mass * (Vi.v - cross(c, Vi.w));
         // B = -dad(V, IV) - I [0; g]
-        Bown[i].w = cross(Vi.w, hw) + cross(Vi.v, hv) - b.mass * cross(c, g[i]);
-        Bown[i].v = cross(Vi.w, hv) - b.mass * g[i];
+        W.own(i) = {cross(Vi.w, hw) + cross(Vi.v, hv) - b.mass * cross(c, g[i]),
+                    cross(Vi.w, hv) - b.mass * g[i]};
     }
     // inward pass: articulated inertias / biases accumulate into the parent
     SI carry[N];
@@ -327,11 +388,11 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
         const BodyF& b = P->b[i];
-        BodyState& s = W.bs[i];
+        BodyState& s = W.bs(i);
         const int pa = parent_of(TOPO, i);
         const bool kids = has_child(TOPO, N, i);
         SI AI = rigid(b);
-        SV Bi = Bown[i];
+        SV Bi = W.own(i);
         if (kids) {
             AI += carry[i];
             Bi = Bi + carryB[i];
@@ -345,10 +406,12 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         if constexpr (DUAL) {
             SI AIn = rigid(b);
             if (kids) AIn += carryN[i];
-            W.nf[i].U = ais(AIn, b);
-            W.nf[i].psi = rcp(proj(b, W.nf[i].U));
+            const SV Un = ais(AIn, b);
+            const float psin = rcp(proj(b, Un));
+            W.nf(i).U = Un;
+            W.nf(i).psi = psin;
             if (pa >= 0) {
-                const SI c = to_parent(s.R, s.p, downdate(AIn, W.nf[i].U, W.nf[i].psi));
+                const SI c = to_parent(s.R, s.p, downdate(AIn, Un, psin));
                 if (first_inward(TOPO, N, i)) carryN[pa] = c;
                 else carryN[pa] += c;
             }
@@ -366,7 +429,7 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const BodyF& b = P->b[i];
-        const BodyState& s = W.bs[i];
+        const BodyState& s = W.bs(i);
         const int pa = parent_of(TOPO, i);
         if (pa >= 0) {
             const SV ap = ad_inv(s.R, s.p, a[pa]);
@@ -382,9 +445,8 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
 // column j of M^-1 (velocity change of every dof for a unit impulse on dof j):
 // the bias impulse climbs from J to the root (only J's ancestors are
 // touched), then the outward pass reaches every body.
-template <int N, bool DUAL, Topo TOPO, int J>
-__device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const Work<N, DUAL>& W,
-                                            float (&col)[N]) {
+template <int N, bool DUAL, Topo TOPO, int J, class WK>
+__device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const WK& W, float (&col)[N]) {
     float u[N];
     SV Bimp[N];
 #pragma unroll
@@ -395,10 +457,10 @@ __device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const 
         if (pa >= 0) {
             SV U;
             float psi;
-            if constexpr (DUAL) { U = W.nf[i].U; psi = W.nf[i].psi; }
-            else { U = W.bs[i].U; psi = W.bs[i].psi; }
-            if (i == J) Bimp[pa] = dad_inv(W.bs[i].R, W.bs[i].p, (psi * u[i]) * U);
-            else Bimp[pa] = dad_inv(W.bs[i].R, W.bs[i].p, Bimp[i] + (psi * u[i]) * U);
+            if constexpr (DUAL) { U = W.nf(i).U; psi = W.nf(i).psi; }
+            else { U = W.bs(i).U; psi = W.bs(i).psi; }
+            if (i == J) Bimp[pa] = dad_inv(W.bs(i).R, W.bs(i).p, (psi * u[i]) * U);
+            else Bimp[pa] = dad_inv(W.bs(i).R, W.bs(i).p, Bimp[i] + (psi * u[i]) * U);
         }
     }
     SV dv[N];
@@ -406,11 +468,11 @@ __device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const 
     for (int i = 0; i < N; ++i) {
         SV U;
         float psi;
-        if constexpr (DUAL) { U = W.nf[i].U; psi = W.nf[i].psi; }
-        else { U = W.bs[i].U; psi = W.bs[i].psi; }
+        if constexpr (DUAL) { U = W.nf(i).U; psi = W.nf(i).psi; }
+        else { U = W.bs(i).U; psi = W.bs(i).psi; }
         const int pa = parent_of(TOPO, i);
         if (pa >= 0) {
-            const SV dvp = ad_inv(W.bs[i].R, W.bs[i].p, dv[pa]);
+            const SV dvp = ad_inv(W.bs(i).R, W.bs(i).p, dv[pa]);
             col[i] = psi * (u[i] - dot(U, dvp));
             dv[i] = dvp + motion(P->b[i], col[i]);
         } else {
@@ -420,20 +482,87 @@ __device__ __forceinline__ void minv_column(const ChainF* __restrict__ P, const 
     }
 }
 
-template <int N, bool DUAL, Topo TOPO, int J = 0>
-__device__ __forceinline__ void minv_columns(const ChainF* __restrict__ P, const Work<N, DUAL>& W,
-                                             const bool (&need)[N], float (&Minv)[N][N]) {
-    if constexpr (J < N) {
-        if (need[J]) {
+// bit i set: body i is J or an ancestor of J
+template <int N>
+struct PathMasks {
+    uint32_t m[N];
+};
+template <int N, Topo TOPO>
+constexpr PathMasks<N> path_masks() {
+    PathMasks<N> p{};
+    for (int j = 0; j < N; ++j) {
+        uint32_t bits = 0;
+        for (int k = j; k >= 0; k = parent_of(TOPO, k)) bits |= 1u << k;
+        p.m[j] = bits;
+    }
+    return p;
+}
+
+// column J (uniform, runtime) of M^-1: one copy of the column code for every
+// J (LdsStage models), branches on the path mask are scalar
+template <int N, bool DUAL, Topo TOPO, class WK>
+__device__ __forceinline__ void minv_column_rt(const ChainF* __restrict__ P, const WK& W, int J, uint32_t path,
+                                               float (&col)[N]) {
+    float u[N];
+    SV Bimp[N];
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        u[i] = 0.f;
+        if (!((path >> i) & 1u)) continue;
+        const bool self = (i == J);
+        u[i] = self ? 1.f : -proj(P->b[i], Bimp[i]);
+        const int pa = parent_of(TOPO, i);
+        if (pa >= 0) {
+            SV U;
+            float psi;
+            if constexpr (DUAL) { U = W.nf(i).U; psi = W.nf(i).psi; }
+            else { U = W.bs(i).U; psi = W.bs(i).psi; }
+            if (self) Bimp[pa] = dad_inv(W.bs(i).R, W.bs(i).p, (psi * u[i]) * U);
+            else Bimp[pa] = dad_inv(W.bs(i).R, W.bs(i).p, Bimp[i] + (psi * u[i]) * U);
+        }
+    }
+    SV dv[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        SV U;
+        float psi;
+        if constexpr (DUAL) { U = W.nf(i).U; psi = W.nf(i).psi; }
+        else { U = W.bs(i).U; psi = W.bs(i).psi; }
+        const int pa = parent_of(TOPO, i);
+        if (pa >= 0) {
+            const SV dvp = ad_inv(W.bs(i).R, W.bs(i).p, dv[pa]);
+            col[i] = psi * (u[i] - dot(U, dvp));
+            dv[i] = dvp + motion(P->b[i], col[i]);
+        } else {
+            col[i] = psi * u[i];
+            dv[i] = motion(P->b[i], col[i]);
+        }
+    }
+}
+
+// the M^-1 columns of the dofs with an active row (bit d of `need`)
+template <int N, bool DUAL, Topo TOPO, class WK, int J = 0>
+__device__ __forceinline__ void minv_columns(const ChainF* __restrict__ P, WK& W, uint32_t need) {
+    if constexpr (WK::kRuntimeColumns) {
+        constexpr PathMasks<N> paths = path_masks<N, TOPO>();
+        for (int j = 0; j < N; ++j) {
+            if ((need >> j) & 1u) {
+                float col[N];
+                W.fence();
+                minv_column_rt<N, DUAL, TOPO>(P, W, j, paths.m[j], col);
+#pragma unroll
+                for (int k = 0; k < N; ++k) W.mv(k, j) = col[k];
+            }
+        }
+    } else if constexpr (J < N) {
+        if ((need >> J) & 1u) {
             float col[N];
+            W.fence();
             minv_column<N, DUAL, TOPO, J>(P, W, col);
 #pragma unroll
-            for (int k = 0; k < N; ++k) Minv[k][J] = col[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < N; ++k) Minv[k][J] = 0.f;
+            for (int k = 0; k < N; ++k) W.mv(k, J) = col[k];
         }
-        minv_columns<N, DUAL, TOPO, J + 1>(P, W, need, Minv);
+        minv_columns<N, DUAL, TOPO, WK, J + 1>(P, W, need);
     }
 }
 
@@ -443,72 +572,78 @@ constexpr float kMaxErv = 10.f;
 
 // One engine substep.  act[i]: kActForce (tau[i] is the clipped command) or
 // kActServo (vcmd[i] is the velocity command).  CONS enables the LCP rows.
-template <int N, bool DUAL, bool CONS, Topo TOPO = chain_topo(N)>
+template <int N, bool DUAL, bool CONS, Topo TOPO, class WK>
 __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
                                         const float (&tau)[N], const uint8_t (&act)[N],
                                         const float (&vcmd)[N], float dt, int pgs_iters,
-                                        float (&qdd)[N]) {
-    Work<N, DUAL> W;
+                                        float (&qdd)[N], WK& W) {
     aba<N, DUAL, TOPO>(P, q, qd, tau, dt, qdd, W);
 #pragma unroll
     for (int i = 0; i < N; ++i) qd[i] += dt * qdd[i];
 
     if constexpr (CONS) {
-        // rows per dof: 0 limit, 1 servo, 2 Coulomb friction
-        bool on[N][3];
-        float bb[N][3], lo[N][3], hi[N][3];
-        bool need[N];
-        bool any = false;
+        // rows per dof: 0 limit, 1 servo, 2 Coulomb friction.  Only the
+        // right-hand sides are kept; the boxes are recomputed from the uniform
+        // parameters (limit: [0, inf) at the lower bound, (-inf, 0] at the
+        // upper one; servo +-effort dt; friction +-friction dt).
+        uint32_t on = 0u, at_upper = 0u, need = 0u;
+        float bb[N][3];
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             const BodyF& b = P->b[i];
-            on[i][0] = on[i][1] = on[i][2] = false;
             bb[i][0] = bb[i][1] = bb[i][2] = 0.f;
-            lo[i][0] = lo[i][1] = lo[i][2] = 0.f;
-            hi[i][0] = hi[i][1] = hi[i][2] = 0.f;
             if (b.limited) {
                 float viol = q[i] - b.lower;
+                bool act_lim = false;
                 if (viol <= 0.f) {
-                    on[i][0] = true; lo[i][0] = 0.f; hi[i][0] = INFINITY;
+                    act_lim = true;
                 } else {
                     viol = q[i] - b.upper;
-                    if (viol >= 0.f) { on[i][0] = true; lo[i][0] = -INFINITY; hi[i][0] = 0.f; }
+                    if (viol >= 0.f) { act_lim = true; at_upper |= 1u << i; }
                 }
-                const float bounce = fminf(fmaxf(-viol * kErp * rcp(dt), -kMaxErv), kMaxErv);
-                bb[i][0] = -qd[i] + bounce;
+                if (act_lim) {
+                    on |= 1u << (3 * i);
+                    const float bounce = fminf(fmaxf(-viol * kErp * rcp(dt), -kMaxErv), kMaxErv);
+                    bb[i][0] = -qd[i] + bounce;
+                }
             }
             if (act[i] == kActServo) {
                 const float vc = fminf(fmaxf(vcmd[i], -b.vel_limit), b.vel_limit);
                 const float err = vc - qd[i];
-                if (err != 0.f) {
-                    on[i][1] = true; bb[i][1] = err;
-                    lo[i][1] = -b.effort * dt; hi[i][1] = b.effort * dt;
-                }
+                if (err != 0.f) { on |= 1u << (3 * i + 1); bb[i][1] = err; }
             }
-            if (b.friction != 0.f && qd[i] != 0.f) {
-                on[i][2] = true; bb[i][2] = -qd[i];
-                hi[i][2] = b.friction * dt; lo[i][2] = -hi[i][2];
-            }
-            need[i] = on[i][0] || on[i][1] || on[i][2];
-            any = any || need[i];
+            if (b.friction != 0.f && qd[i] != 0.f) { on |= 1u << (3 * i + 2); bb[i][2] = -qd[i]; }
+            if ((on >> (3 * i)) & 7u) need |= 1u << i;
         }
-        if (any) {
-            float Minv[N][N];
-            minv_columns<N, DUAL, TOPO>(P, W, need, Minv);
+        if (on) {
+            minv_columns<N, DUAL, TOPO, WK>(P, W, need);
             float x[N][3], dq[N];
 #pragma unroll
             for (int i = 0; i < N; ++i) { x[i][0] = x[i][1] = x[i][2] = 0.f; dq[i] = 0.f; }
             for (int it = 0; it < pgs_iters; ++it) {
+                W.fence();
 #pragma unroll
                 for (int d = 0; d < N; ++d) {
+                    if (!((need >> d) & 1u)) continue;
+                    const BodyF& b = P->b[d];
+                    const float inv_diag = rcp(W.mv(d, d));
 #pragma unroll
                     for (int t = 0; t < 3; ++t) {
-                        if (on[d][t]) {
-                            const float xn = fminf(fmaxf(x[d][t] + (bb[d][t] - dq[d]) * rcp(Minv[d][d]), lo[d][t]), hi[d][t]);
+                        if ((on >> (3 * d + t)) & 1u) {
+                            float lo, hi;
+                            if (t == 0) {
+                                const bool up = (at_upper >> d) & 1u;
+                                lo = up ? -INFINITY : 0.f;
+                                hi = up ? 0.f : INFINITY;
+                            } else {
+                                hi = (t == 1 ? b.effort : b.friction) * dt;
+                                lo = -hi;
+                            }
+                            const float xn = fminf(fmaxf(x[d][t] + (bb[d][t] - dq[d]) * inv_diag, lo), hi);
                             const float delta = xn - x[d][t];
                             x[d][t] = xn;
 #pragma unroll
-                            for (int k = 0; k < N; ++k) dq[k] += delta * Minv[k][d];
+                            for (int k = 0; k < N; ++k) dq[k] += delta * W.mv(k, d);
                         }
                     }
                 }
@@ -523,6 +658,16 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) q[i] += dt * qd[i];
+}
+
+// register-staged substep (small models)
+template <int N, bool DUAL, bool CONS, Topo TOPO = chain_topo(N)>
+__device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
+                                        const float (&tau)[N], const uint8_t (&act)[N],
+                                        const float (&vcmd)[N], float dt, int pgs_iters,
+                                        float (&qdd)[N]) {
+    RegStage<N, DUAL> W;
+    substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vcmd, dt, pgs_iters, qdd, W);
 }
 
 }  // namespace dev

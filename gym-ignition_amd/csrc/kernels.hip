@@ -11,6 +11,8 @@
 //                   python/gym_ignition_environments/tasks/*.py fused in
 //                   (obs, reward, done, TimeLimit, auto-reset).
 //  vecenv_reset   : initial reset of every world (Philox4x32-10).
+#include <type_traits>
+
 #include "baked_models.hpp"
 #include "chain_dyn.hpp"
 #include "kernels.hpp"
@@ -26,12 +28,40 @@ namespace dev {
 // when the loaded model's block is bit-identical (sim.cpp: baked_id).
 __constant__ constexpr baked::CartpoleBlock kCartpoleDev = {{MW_BAKED_CARTPOLE_INIT}};
 __constant__ constexpr baked::PendulumBlock kPendulumDev = {{MW_BAKED_PENDULUM_INIT}};
+__constant__ constexpr baked::PandaBlock kPandaDev = {{MW_BAKED_PANDA_INIT}};
 
 template <int BAKED>
 __device__ __forceinline__ const ChainF* model_params(const ChainF* P) {
     if constexpr (BAKED == baked::kCartpoleId) return reinterpret_cast<const ChainF*>(&kCartpoleDev);
     else if constexpr (BAKED == baked::kPendulumId) return reinterpret_cast<const ChainF*>(&kPendulumDev);
+    else if constexpr (BAKED == baked::kPandaId) return reinterpret_cast<const ChainF*>(&kPandaDev);
     else return P;
+}
+
+// ------------------------------------------------------- staging --------
+// Models of >= kLdsMinDofs dofs keep their per-body substep state in LDS
+// (chain_dyn.hpp: LdsStage); their kernels run 64-thread workgroups.
+#ifndef MW_LDS_MIN_DOFS
+#define MW_LDS_MIN_DOFS 7
+#endif
+constexpr int kLdsMinDofs = MW_LDS_MIN_DOFS;
+
+#define MW_DECLARE_STAGE(N, DUAL, NAME)                                                        \
+    __shared__ BodyState sh_bs_[(N >= kLdsMinDofs ? N : 1) * kLdsLanes];                      \
+    __shared__ ImpulseFactor sh_nf_[((N >= kLdsMinDofs && DUAL) ? N : 1) * kLdsLanes];        \
+    __shared__ SV7 sh_own_[(N >= kLdsMinDofs ? N : 1) * kLdsLanes];                           \
+    __shared__ float sh_mv_[(N >= kLdsMinDofs ? N * N : 1) * kLdsLanes];                      \
+    using StageT = std::conditional_t<(N >= kLdsMinDofs), LdsStage<N, DUAL>, RegStage<N, DUAL>>; \
+    StageT NAME = make_stage<N, DUAL>(sh_bs_, sh_nf_, sh_own_, sh_mv_)
+
+template <int N, bool DUAL>
+__device__ __forceinline__ auto make_stage(BodyState* b, ImpulseFactor* f, SV7* o, float* m) {
+    if constexpr (N >= kLdsMinDofs) {
+        return LdsStage<N, DUAL>{b + threadIdx.x, f + threadIdx.x, o + threadIdx.x, m + threadIdx.x};
+    } else {
+        (void)b; (void)f; (void)o; (void)m;
+        return RegStage<N, DUAL>{};
+    }
 }
 
 // ------------------------------------------------------------ RNG -------
@@ -170,11 +200,12 @@ __device__ __forceinline__ bool pid_update(const PidF& g, float err, float inv_d
     return true;
 }
 
-template <int N, bool DUAL, bool CONS, Topo TOPO>
-__global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restrict__ P, SimDev S, PidSet pid,
+template <int N, bool DUAL, bool CONS, Topo TOPO, int BAKED = 0>
+__global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restrict__ Pin, SimDev S, PidSet pid,
                                                            int W, RunArgs A) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
+    const ChainF* __restrict__ P = model_params<BAKED>(Pin);
     float q[N], qd[N];
     load_state<N>(S, W, w, q, qd);
     if (A.first) {
@@ -202,6 +233,7 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
             vc[d] = S.vtgt[d * W + w];
             any_pid = any_pid || act[d] >= kActPidPos;
         }
+        MW_DECLARE_STAGE(N, DUAL, stage);
         for (int s = 0; s < A.substeps; ++s) {
             const bool gate = (A.pid_gate >> s) & 1u;
 #pragma unroll
@@ -235,7 +267,7 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
                     }
                 }
             }
-            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd);
+            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage);
         }
 #pragma unroll
         for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];
@@ -354,8 +386,8 @@ __device__ __forceinline__ void store_pid_obs(float* __restrict__ dst, const flo
     for (int d = 0; d < N; ++d) { dst[d] = q[d]; dst[N + d] = qd[d]; }
 }
 
-template <int N, Topo TOPO, bool DUAL, bool CONS>
-__global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __restrict__ P, TaskF T, SimDev S,
+template <int N, Topo TOPO, bool DUAL, bool CONS, int BAKED = 0>
+__global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __restrict__ Pin, TaskF T, SimDev S,
                                                               VecDev V, PidSet pid,
                                                               const float* __restrict__ targets,
                                                               float* __restrict__ obs, float* __restrict__ reward,
@@ -364,6 +396,7 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
                                                               float inv_dt, int substeps, int pgs_iters) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
+    const ChainF* __restrict__ P = model_params<BAKED>(Pin);
     float q[N], qd[N], tgt[N], pe[N], pi[N], pu[N];
     load_state<N>(S, W, w, q, qd);
 #pragma unroll
@@ -378,6 +411,7 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
 #pragma unroll
     for (int d = 0; d < N; ++d) { act[d] = kActPidPos; vc[d] = 0.f; }
     float tau[N], qdd[N];
+    MW_DECLARE_STAGE(N, DUAL, stage);
     for (int s = 0; s < substeps; ++s) {
 #pragma unroll
         for (int d = 0; d < N; ++d) {
@@ -387,7 +421,7 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
             const float e = P->b[d].effort;
             tau[d] = fminf(fmaxf(u, -e), e);
         }
-        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
+        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd, stage);
     }
     float r = 0.f;
 #pragma unroll
@@ -441,11 +475,21 @@ dim3 grid_for(int W, int block) { return dim3(static_cast<unsigned>((W + block -
 // 64-thread blocks spread a small world count over as many CUs as possible
 // (each wave runs a long dependent chain); 256 once there is work for all.
 int block_for(int W) { return (W <= 64 * 256) ? 64 : 256; }
+// LDS-staged kernels (>= kLdsMinDofs dofs) always run one wave per workgroup
+int block_for(int W, int n) { return (n >= dev::kLdsMinDofs) ? dev::kLdsLanes : block_for(W); }
 
 template <int N, Topo TOPO>
-hipError_t scenario_n(const ChainF* P, bool cons, bool dual, const SimDev& S, const PidSet& pid, int W,
+hipError_t scenario_n(const ChainF* P, bool cons, bool dual, int baked, const SimDev& S, const PidSet& pid, int W,
                       const RunArgs& a, hipStream_t st) {
-    const int B = block_for(W);
+    const int B = block_for(W, N);
+    if constexpr (N == 9 && TOPO == kPandaTopo) {
+        // the shipped Panda, constant-folded (it has limits and no damping)
+        if (baked == baked::kPandaId && cons && !dual) {
+            hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, true, TOPO, baked::kPandaId>), grid_for(W, B),
+                               dim3(B), 0, st, P, S, pid, W, a);
+            return hipGetLastError();
+        }
+    }
     if (!cons)
         hipLaunchKernelGGL((dev::scenario_run_kernel<N, false, false, TOPO>), grid_for(W, B), dim3(B), 0, st, P,
                            S, pid, W, a);
@@ -503,20 +547,20 @@ int kernel_topology(const int* parents, int n) {
     return -1;
 }
 
-hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, const SimDev& S,
+hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const SimDev& S,
                                const PidSet& pid, int W, const RunArgs& a, hipStream_t st) {
-    if (topo == 1) return scenario_n<9, kPandaTopo>(P, cons, dual, S, pid, W, a, st);
+    if (topo == 1) return scenario_n<9, kPandaTopo>(P, cons, dual, baked, S, pid, W, a, st);
     if (topo != 0) return hipErrorInvalidValue;
     switch (n) {
-    case 1: return scenario_n<1, chain_topo(1)>(P, cons, dual, S, pid, W, a, st);
-    case 2: return scenario_n<2, chain_topo(2)>(P, cons, dual, S, pid, W, a, st);
-    case 3: return scenario_n<3, chain_topo(3)>(P, cons, dual, S, pid, W, a, st);
-    case 4: return scenario_n<4, chain_topo(4)>(P, cons, dual, S, pid, W, a, st);
-    case 5: return scenario_n<5, chain_topo(5)>(P, cons, dual, S, pid, W, a, st);
-    case 6: return scenario_n<6, chain_topo(6)>(P, cons, dual, S, pid, W, a, st);
-    case 7: return scenario_n<7, chain_topo(7)>(P, cons, dual, S, pid, W, a, st);
-    case 8: return scenario_n<8, chain_topo(8)>(P, cons, dual, S, pid, W, a, st);
-    case 9: return scenario_n<9, chain_topo(9)>(P, cons, dual, S, pid, W, a, st);
+    case 1: return scenario_n<1, chain_topo(1)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 2: return scenario_n<2, chain_topo(2)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 3: return scenario_n<3, chain_topo(3)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 4: return scenario_n<4, chain_topo(4)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 5: return scenario_n<5, chain_topo(5)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 6: return scenario_n<6, chain_topo(6)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 7: return scenario_n<7, chain_topo(7)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 8: return scenario_n<8, chain_topo(8)>(P, cons, dual, baked, S, pid, W, a, st);
+    case 9: return scenario_n<9, chain_topo(9)>(P, cons, dual, baked, S, pid, W, a, st);
     default: return hipErrorInvalidValue;
     }
 }
@@ -539,14 +583,18 @@ hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const Sim
     return hipGetLastError();
 }
 
-hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, const TaskF& T,
+hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const TaskF& T,
                                   const SimDev& S, const VecDev& V, const PidSet& pid, const float* targets,
                                   float* obs, float* reward, uint8_t* done, float* term_obs, int W,
                                   float dt, int substeps, int pgs_iters, hipStream_t st) {
     if (n != 9 || topo != 1) return hipErrorInvalidValue;
-    const int B = block_for(W);
+    const int B = block_for(W, 9);
     const float inv_dt = 1.f / dt;
-    if (!cons)
+    if (baked == baked::kPandaId && cons && !dual)
+        hipLaunchKernelGGL((dev::vecenv_pid_step_kernel<9, kPandaTopo, false, true, baked::kPandaId>), grid_for(W, B),
+                           dim3(B), 0, st, P, T, S, V, pid, targets, obs, reward, done, term_obs, W, dt, inv_dt,
+                           substeps, pgs_iters);
+    else if (!cons)
         hipLaunchKernelGGL((dev::vecenv_pid_step_kernel<9, kPandaTopo, false, false>), grid_for(W, B), dim3(B), 0,
                            st, P, T, S, V, pid, targets, obs, reward, done, term_obs, W, dt, inv_dt, substeps,
                            pgs_iters);

@@ -64,7 +64,7 @@ struct VecDev {
 // -1 = not compiled into this build
 int kernel_topology(const int* parents, int n);
 
-hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, const SimDev& S,
+hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const SimDev& S,
                                const PidSet& pid, int W, const RunArgs& a, hipStream_t st);
 
 hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
@@ -72,7 +72,7 @@ hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const Sim
 
 // Position-target task (kind 4, Panda): actions float32 [W, n] are the
 // JointController position targets; PID every substep (period = step size).
-hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, const TaskF& T,
+hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const TaskF& T,
                                   const SimDev& S, const VecDev& V, const PidSet& pid, const float* targets,
                                   float* obs, float* reward, uint8_t* done, float* term_obs, int W,
                                   float dt, int substeps, int pgs_iters, hipStream_t st);

@@ -131,13 +131,17 @@ void build_params(mw_sim* s) {
     for (int i = 0; i < s->n; ++i) {
         const mw::ChainBody& b = s->model.bodies[i];
         mw::BodyF& f = P.b[i];
-        for (int k = 0; k < 9; ++k) f.E[k] = static_cast<float>(b.E[k]);
+        // rotation entries below 1e-12 are the residue of cos(pi/2) etc. in the
+        // rpy conversion: exact zeros let the constant-folded kernels drop them
+        // (a 6e-17 change, far below float32 resolution of the unit entries)
+        auto snap = [](double v) { return std::fabs(v) < 1e-12 ? 0.0 : v; };
+        for (int k = 0; k < 9; ++k) f.E[k] = static_cast<float>(snap(b.E[k]));
         for (int k = 0; k < 3; ++k) {
             f.r[k] = static_cast<float>(b.r[k]);
             f.axis[k] = static_cast<float>(b.axis[k]);
             f.com[k] = static_cast<float>(b.com[k]);
-            f.Ea[k] = static_cast<float>(b.E[k * 3] * b.axis[0] + b.E[k * 3 + 1] * b.axis[1] +
-                                         b.E[k * 3 + 2] * b.axis[2]);
+            f.Ea[k] = static_cast<float>(snap(b.E[k * 3] * b.axis[0] + b.E[k * 3 + 1] * b.axis[1] +
+                                              b.E[k * 3 + 2] * b.axis[2]));
         }
         f.jtype = (b.type == mw::JType::Prismatic) ? 1 : 0;
         f.mass = static_cast<float>(b.mass);
@@ -192,6 +196,9 @@ int baked_id(const mw_sim* s) {
     if (words * 4 == sizeof(mw::baked::kPendulumHost) &&
         std::memcmp(&s->h_params, &mw::baked::kPendulumHost, words * 4) == 0)
         return mw::baked::kPendulumId;
+    if (words * 4 == sizeof(mw::baked::kPandaHost) &&
+        std::memcmp(&s->h_params, &mw::baked::kPandaHost, words * 4) == 0)
+        return mw::baked::kPandaId;
     return 0;
 }
 
@@ -469,7 +476,7 @@ int mw_run(mw_sim* s, int paused) {
                 a.pid_gate |= (uint64_t{1} << k);
             }
         }
-        MW_HIP(mw::launch_scenario_run(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), s->dev, pid,
+        MW_HIP(mw::launch_scenario_run(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), baked_id(s), s->dev, pid,
                                        s->W, a, s->stream));
         a.first = 0;
         done += chunk;
@@ -906,13 +913,15 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
         T.hi[0] = 1.f; T.hi[1] = 1.f; T.hi[2] = 10.f; T.hi[3] = 0.f;
         break;
     case MW_TASK_PANDA_POSITION_TRACKING: {
-        // start pose of test_pid_controllers.py:49-59 (joints 1 and 6 at mid-range,
-        // the others at 0) with joint 4 at its upper limit (0 violates it), +-0.05 rad
+        // the Panda wrapper's initial configuration (models/panda.py:41-44) with
+        // joints 1 and 6 at mid-range as test_pid_controllers.py:49-59 sets them
+        // (so the config-4 sinusoids stay inside the limits) and the fingers
+        // half open: no joint starts on a position limit
+        const double wrapper[7] = {0.0, -0.785, 0.0, -2.356, 0.0, 1.571, 0.785};
         for (int d = 0; d < n; ++d) {
             const mw::ChainBody& b = s->model.bodies[d];
-            double h = 0.0;
+            double h = (d < 7) ? wrapper[d] : 0.5 * (b.lower + b.upper);
             if (d == 0 || d == 5) h = 0.5 * (b.lower + b.upper);
-            if (d == 3) h = b.upper;
             T.home[d] = static_cast<float>(h);
         }
         T.home_noise = 0.05f;
@@ -960,7 +969,7 @@ static int vec_common(mw_vecenv* e, int32_t T, const void* a, float* o, float* r
     mw_sim* s = e->sim;
     if (e->task.kind == MW_TASK_PANDA_POSITION_TRACKING) {
         if (T > 0) return fail(MW_EINVAL, "the fused rollout is not available for position-target tasks");
-        MW_HIP(mw::launch_vecenv_pid_step(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), e->task, s->dev,
+        MW_HIP(mw::launch_vecenv_pid_step(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), baked_id(s), e->task, s->dev,
                                           e->dev, pid_set(s), static_cast<const float*>(a), o, r, d, to, s->W,
                                           static_cast<float>(s->cfg.step_size), s->cfg.steps_per_run,
                                           s->cfg.pgs_iters, s->stream));

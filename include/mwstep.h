@@ -180,8 +180,9 @@ int mw_copy_state(mw_sim* sim, float* q_dev, float* qd_dev, int to_sim);
  * float32 [n_worlds, 9] are the Position-mode targets of every joint, the
  * JointController PID (gains: mw_set_joint_pid) runs every physics step;
  * obs = [q, qd] (18), reward = -|q - target|^2, done = TimeLimit only; reset
- * to the start pose of tests/test_scenario/test_pid_controllers.py:49-59
- * (joint 4 at its upper limit) + U(-0.05, 0.05) rad per joint. */
+ * to the Panda wrapper's pose (python/gym_ignition_environments/models/
+ * panda.py:41-44) with joints 1 and 6 at mid-range (test_pid_controllers.py:
+ * 49-59) and the fingers half open, + U(-0.05, 0.05) per joint. */
 #define MW_TASK_PANDA_POSITION_TRACKING 4
 
 typedef struct {
