@@ -566,6 +566,8 @@ __device__ __forceinline__ void minv_columns(const ChainF* __restrict__ P, WK& W
     }
 }
 
+constexpr float kBig = 3.402823466e38f;  // FLT_MAX: "no bound" on the device
+
 // DART constants [EXT]: ERP 0.01, max error-reduction velocity 10
 constexpr float kErp = 0.01f;
 constexpr float kMaxErv = 10.f;
@@ -633,8 +635,10 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
                             float lo, hi;
                             if (t == 0) {
                                 const bool up = (at_upper >> d) & 1u;
-                                lo = up ? -INFINITY : 0.f;
-                                hi = up ? 0.f : INFINITY;
+                                // unbounded side: FLT_MAX (the kernels are built
+                                // finite-math-only, see the Makefile)
+                                lo = up ? -kBig : 0.f;
+                                hi = up ? 0.f : kBig;
                             } else {
                                 hi = (t == 1 ? b.effort : b.friction) * dt;
                                 lo = -hi;

@@ -188,7 +188,9 @@ __device__ __forceinline__ void store_obs(float* __restrict__ dst, const float (
 // or_pid_update]; returns false (and leaves the state) for a non-finite error
 __device__ __forceinline__ bool pid_update(const PidF& g, float err, float inv_dt, float dt, float& e_last,
                                            float& ierr, float& cmd) {
-    if (!isfinite(err)) return false;
+    // exponent-bits test: the kernels are built finite-math-only, where
+    // isfinite() folds to true
+    if ((__float_as_uint(err) & 0x7f800000u) == 0x7f800000u) return false;
     const float pterm = g.p * err;
     ierr = ierr + g.i * dt * err;
     if (g.imax >= g.imin) ierr = fminf(fmaxf(ierr, g.imin), g.imax);

@@ -157,7 +157,8 @@ void build_params(mw_sim* s) {
         f.friction = static_cast<float>(b.friction);
         auto clampf = [](double v) {
             const double big = static_cast<double>(std::numeric_limits<float>::max());
-            return static_cast<float>(v > big ? INFINITY : (v < -big ? -INFINITY : v));
+            // "unlimited" is FLT_MAX on the device (finite-math-only kernels)
+            return static_cast<float>(v > big ? big : (v < -big ? -big : v));
         };
         f.lower = clampf(b.lower);
         f.upper = clampf(b.upper);
@@ -222,7 +223,7 @@ int pull_ptgt(mw_sim* s) {
 
 float to_f32(double v) {
     const double big = static_cast<double>(std::numeric_limits<float>::max());
-    return static_cast<float>(v > big ? INFINITY : (v < -big ? -INFINITY : v));
+    return static_cast<float>(v > big ? big : (v < -big ? -big : v));
 }
 
 mw::PidSet pid_set(const mw_sim* s) {

@@ -24,7 +24,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "gym-ignition_amd", "python"))
 
 METRIC = "env·steps/sec (whole node) at N parallel worlds; obs max-abs-err vs DART"
@@ -54,8 +54,6 @@ def parse():
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-panda", action="store_true", help="skip the config-4 Panda leg")
-    p.add_argument("--groups", type=int, default=1,
-                   help="world groups per GPU, each on its own stream / hardware queue")
     return p.parse_args()
 
 
@@ -78,11 +76,10 @@ def main():
     from mwstep.vecenv import VecEnv
 
     W = args.worlds
-    envs = make_groups(args.task, W, args.groups, dev, args.seed, rank * W)
-    env = envs[0]
+    env = VecEnv(args.task, n_worlds=W, device=local_rank, seed=args.seed, world_offset=rank * W)
     K = args.steps
-    actions = make_actions(envs, args.warmup + K, dev, torch, rank)
-    timed = time_steps(envs, actions, args.warmup, K, args.graph_chunk, dev, torch, dist, world_size,
+    actions = make_actions(env, args.warmup + K, dev, torch, rank)
+    timed = time_steps(env, actions, args.warmup, K, args.graph_chunk, dev, torch, dist, world_size,
                        gather=(world_size > 1))
     elapsed, kernel_us = timed["elapsed"], timed["kernel_us"]
     value = world_size * W * K / elapsed
@@ -106,16 +103,15 @@ def main():
         T = 1000
         stream = timed["stream"]
         with torch.cuda.stream(stream):
-            env.rollout(actions[:T, :env.n_worlds].contiguous())   # warm
+            env.rollout(actions[:T].contiguous())   # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            env.rollout(actions[:T, :env.n_worlds].contiguous())
+            env.rollout(actions[:T].contiguous())
             e1.record(stream)
         stream.synchronize()
         r_ms = e0.elapsed_time(e1)
-        Wr = env.n_worlds
-        rollout = {"steps_per_launch": T, "worlds": Wr, "ms_per_launch": round(r_ms, 4),
-                   "env_steps_per_s_per_gpu": round(Wr * T / (r_ms * 1e-3), 1),
+        rollout = {"steps_per_launch": T, "ms_per_launch": round(r_ms, 4),
+                   "env_steps_per_s_per_gpu": round(W * T / (r_ms * 1e-3), 1),
                    "note": "open-loop (actions known ahead); not the headline value"}
 
     # ---------------- world-count sweep (same kernel, graph mode): where the
@@ -157,9 +153,7 @@ def main():
                 "worlds_per_gpu": W,
                 "global_worlds": W * world_size,
                 "dt": 1e-3,
-                "launch": (f"hipGraph of {G} per-step kernels" if args.groups == 1 else
-                           f"{args.groups} world groups of {W // args.groups}, each on its own stream "
-                           f"(hardware queue) replaying a hipGraph of {G} per-step kernels"),
+                "launch": f"hipGraph of {G} per-step kernels",
                 "parallelism": f"worlds sharded over {world_size} GPU(s)",
             },
             "roofline": {
@@ -183,8 +177,7 @@ def main():
             "panda_c4": panda,
         }
         print(json.dumps(out))
-    for e in envs:
-        e.close()
+    env.close()
     if world_size > 1:
         dist.destroy_process_group()
 
@@ -202,102 +195,65 @@ def panda_targets(q0, T, dt, torch):
     return tg.contiguous()
 
 
-def make_actions(envs, total, dev, torch, rank):
+def make_actions(env, total, dev, torch, rank):
     gen = torch.Generator(device=dev).manual_seed(43 + rank)
-    env = envs[0]
-    W = sum(e.n_worlds for e in envs)
+    W = env.n_worlds
     if env.action_dim:
-        q0 = torch.cat([e.reset()[:, :e.action_dim].clone() for e in envs])
+        q0 = env.reset()[:, :env.action_dim].clone()
         return panda_targets(q0, total, 1e-3, torch)
     if env.discrete:
         return torch.randint(0, 2, (total, W), generator=gen, device=dev, dtype=torch.int32)
     return (torch.rand((total, W), generator=gen, device=dev) * 2 - 1) * 50.0
 
 
-def make_groups(task, W, S, dev, seed, offset, **kw):
-    """S VecEnvs covering worlds [offset, offset + W) in contiguous slices.
-    Resets are keyed by the global world index (world_offset), so a grouped
-    run is bit-identical to one VecEnv of W worlds (tests/test_gpu_groups.py)."""
-    from mwstep.vecenv import VecEnv
-    if W % S:
-        raise SystemExit(f"--worlds {W} is not divisible by --groups {S}")
-    Wg = W // S
-    return [VecEnv(task, n_worlds=Wg, device=dev.index, seed=seed, world_offset=offset + g * Wg, **kw)
-            for g in range(S)]
-
-
-def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, gather=False):
+def time_steps(env, actions, warmup, K, chunk, dev, torch, dist, world_size, gather=False):
     """W untimed warmup steps, then EXACTLY K steps replayed from hipGraphs of
     `chunk` step launches (the action slice of every step is copied into the
     graph's action buffer before each replay, as a policy would write it),
-    bracketed by barrier + synchronize; max over ranks.
-
-    With several world groups (envs), each group has its own stream (its own
-    hardware queue) and graph; a step = every group advanced once.  The
-    groups' kernels overlap each other's launch gaps."""
+    bracketed by barrier + synchronize; max over ranks."""
     from mwstep.shard import gather_obs
-    S = len(envs)
-    Wg = envs[0].n_worlds
+    stream = torch.cuda.Stream(device=dev)
+    env.sim.set_stream(stream.cuda_stream)
     G = max(1, min(chunk, K))
     n_full, rem = divmod(K, G)
-    groups = []
-    for g, env in enumerate(envs):
-        st = torch.cuda.Stream(device=dev)
-        env.sim.set_stream(st.cuda_stream)
-        acts = actions[:, g * Wg:(g + 1) * Wg].contiguous()
-        buf = torch.empty((G,) + tuple(acts.shape[1:]), dtype=actions.dtype, device=dev)
-        with torch.cuda.stream(st):
-            env.reset()
-            for t in range(warmup):
-                env.step_raw(acts[t].data_ptr())
-            st.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=st):
-                for i in range(G):
-                    env.step_raw(buf[i].data_ptr())
-            tail = None
-            if rem:
-                tail = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(tail, stream=st):
-                    for i in range(rem):
-                        env.step_raw(buf[i].data_ptr())
-            buf.copy_(acts[:G])
-            graph.replay()       # one untimed replay to settle
-        st.synchronize()
-        groups.append((env, st, acts, buf, graph, tail))
+    act_buf = torch.empty((G,) + tuple(actions.shape[1:]), dtype=actions.dtype, device=dev)
+    with torch.cuda.stream(stream):
+        env.reset()
+        for t in range(warmup):
+            env.step_raw(actions[t].data_ptr())
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for g in range(G):
+                env.step_raw(act_buf[g].data_ptr())
+        tail = None
+        if rem:
+            tail = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tail, stream=stream):
+                for g in range(rem):
+                    env.step_raw(act_buf[g].data_ptr())
+        act_buf.copy_(actions[:G])
+        graph.replay()       # one untimed replay to settle
+    stream.synchronize()
 
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    # HIP events on group 0's launch stream bracket the timed region; the other
-    # groups join it through one event wait at the start and one at the end
-    st0 = groups[0][1]
     ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev_start.record(st0)
-    for env, st, acts, buf, graph, tail in groups[1:]:
-        st.wait_event(ev_start)
-    for c in range(n_full):
-        base = warmup + c * G
-        for env, st, acts, buf, graph, tail in groups:
-            with torch.cuda.stream(st):
-                buf.copy_(acts[base:base + G])
-                graph.replay()
-    if rem:
-        base = warmup + n_full * G
-        for env, st, acts, buf, graph, tail in groups:
-            with torch.cuda.stream(st):
-                buf[:rem].copy_(acts[base:base + rem])
-                tail.replay()
-    for env, st, acts, buf, graph, tail in groups[1:]:
-        e = torch.cuda.Event()
-        e.record(st)
-        st0.wait_event(e)
-    ev_end.record(st0)
-    if gather:
-        with torch.cuda.stream(st0):
-            obs = torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs
-            gather_obs(obs)  # final observation tensor, RCCL over xGMI
+    with torch.cuda.stream(stream):
+        ev_start.record(stream)
+        for c in range(n_full):
+            base = warmup + c * G
+            act_buf.copy_(actions[base:base + G])
+            graph.replay()
+        if rem:
+            base = warmup + n_full * G
+            act_buf[:rem].copy_(actions[base:base + rem])
+            tail.replay()
+        ev_end.record(stream)
+        if gather:
+            gather_obs(env.obs)  # final observation tensor, RCCL over xGMI
     torch.cuda.synchronize(dev)
     if world_size > 1:
         dist.barrier()
@@ -307,7 +263,7 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     return {"elapsed": elapsed, "kernel_us": ev_start.elapsed_time(ev_end) * 1e3 / K, "G": G,
-            "stream": groups[0][1], "groups": S}
+            "stream": stream}
 
 
 def panda_bytes_per_env_step(n=9):
@@ -320,10 +276,10 @@ def panda_bytes_per_env_step(n=9):
 def panda_leg(args, dev, torch, dist):
     from mwstep.vecenv import VecEnv
     W, K, warm = 1024, 1000, 100
-    envs = make_groups("PandaPositionTracking", W, args.groups, dev, args.seed, 0, max_episode_steps=5000)
-    env = envs[0]
-    actions = make_actions(envs, warm + K, dev, torch, 0)
-    r = time_steps(envs, actions, warm, K, args.graph_chunk, dev, torch, dist, 1)
+    env = VecEnv("PandaPositionTracking", n_worlds=W, device=dev.index, seed=args.seed,
+                 max_episode_steps=5000)
+    actions = make_actions(env, warm + K, dev, torch, 0)
+    r = time_steps(env, actions, warm, K, args.graph_chunk, dev, torch, dist, 1)
     bpe = panda_bytes_per_env_step(env.sim.dofs)
     gbs = bpe * W / (r["kernel_us"] * 1e-6) / 1e9
     out = {"workload": f"PandaPositionTracking: {W} worlds (9-dof tree), Position-mode PID every 1 ms step, "
@@ -332,9 +288,8 @@ def panda_leg(args, dev, torch, dist):
            "ms_per_step": round(r["elapsed"] / K * 1e3, 6),
            "kernel_us_per_launch": round(r["kernel_us"], 3),
            "bytes_per_env_step": bpe, "achieved_GBs": round(gbs, 3),
-           "hbm_frac": round(gbs / HBM_PEAK_GBS, 6), "groups": args.groups}
-    for e in envs:
-        e.close()
+           "hbm_frac": round(gbs / HBM_PEAK_GBS, 6)}
+    env.close()
     return out
 
 
@@ -400,7 +355,7 @@ def cpu_baseline_and_parity(args, env, actions, np, torch):
     kind, model = TASKS[args.task]
     cm = pyoracle.load_urdf(get_model_file(model))
     Wc = 4096
-    acts = actions[:, :Wc].cpu().numpy() if actions.shape[1] >= Wc else None
+    acts = actions[:, :Wc].cpu().numpy() if env.n_worlds >= Wc else None
     if acts is None:
         return None, None
     acts = acts if kind == 0 else acts.astype(np.float64)

@@ -6,7 +6,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-flags = ["-O3", "-std=c++17", "-fno-slp-vectorize", "-DMW_FAST_MATH"]
+flags = ["-O3", "-std=c++17", "-fno-slp-vectorize", "-DMW_FAST_MATH", "-ffinite-math-only", "-fno-signed-zeros"]
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *flags, f"-I{ROOT}/include",
        f"-I{ROOT}/gym-ignition_amd/csrc", "-c", f"{ROOT}/gym-ignition_amd/csrc/kernels.hip",
        "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"]
