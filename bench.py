@@ -333,6 +333,9 @@ def panda_leg(args, dev, torch, dist):
            "kernel_us_per_launch": round(r["kernel_us"], 3),
            "bytes_per_env_step": bpe, "achieved_GBs": round(gbs, 3),
            "hbm_frac": round(gbs / HBM_PEAK_GBS, 6), "groups": args.groups}
+    tr = pmc_traffic("PandaPositionTracking", W)
+    out["traffic"] = tr["bytes_per_launch"] if tr else None
+    out["algorithmic_bytes_per_launch"] = bpe * W
     for e in envs:
         e.close()
     return out
@@ -340,9 +343,11 @@ def panda_leg(args, dev, torch, dist):
 
 def pmc_traffic(task, W):
     """HBM bytes per launch of the step kernel from the committed PMC summary
-    (profiles/pmc_summary.json, produced by scripts/pmc_summary.py from
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of scripts/profile_step.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    (profiles/pmc_summary.json, or pmc_summary_panda.json for config 4;
+    produced by scripts/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of scripts/profile_step.py / profile_panda.py)."""
+    name = "pmc_summary_panda.json" if task == "PandaPositionTracking" else "pmc_summary.json"
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             d = json.load(f)

@@ -39,4 +39,17 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pmc $ctr rc=$rc" | tee -a "$OUT/session.log"
   stop_if_fatal $rc pmc
 done
+# config 4 (Panda): kernel trace + HBM counters of the position-target env kernel
+echo "== panda kernel trace" | tee -a "$OUT/session.log"
+timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$OUT/prof_panda_$tag" -o run --output-format csv -- \
+  python3 scripts/profile_panda.py > "$OUT/prof_panda_$tag.log" 2>&1
+rc=$?; echo "panda trace rc=$rc" | tee -a "$OUT/session.log"
+stop_if_fatal $rc panda_trace
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  echo "== panda pmc $ctr" | tee -a "$OUT/session.log"
+  timeout -k 10 180 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/pmc_panda_${ctr}_$tag" -o run -- \
+    python3 scripts/profile_panda.py > "$OUT/pmc_panda_${ctr}_$tag.log" 2>&1
+  rc=$?; echo "panda pmc $ctr rc=$rc" | tee -a "$OUT/session.log"
+  stop_if_fatal $rc panda_pmc
+done
 exit 0

@@ -2,6 +2,8 @@
 profiles/pmc_summary.json (per-launch HBM bytes of the step kernel).
 
     python scripts/pmc_summary.py gpurun_out/pmc_FETCH_SIZE_rNN gpurun_out/pmc_WRITE_SIZE_rNN out.json
+    python scripts/pmc_summary.py FETCH_DIR WRITE_DIR out.json --kernel vecenv_pid_step_kernel \
+        --task PandaPositionTracking --worlds 1024        (config-4 Panda env)
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 derived counters
 from TCC_EA0_RDREQ/WRREQ).  MI355X_MICROARCH.md: FETCH_SIZE reads exactly half
@@ -16,18 +18,27 @@ import statistics
 import sys
 
 
-def median_counter(d, name):
+def median_counter(d, name, kernel):
     path = os.path.join(d, "run_counter_collection.csv")
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Counter_Name"] == name and "vecenv_step_kernel" in r["Kernel_Name"]]
+            if r["Counter_Name"] == name and kernel in r["Kernel_Name"]]
     return statistics.median(vals), len(vals)
 
 
 def main():
-    fdir, wdir, out = sys.argv[1:4]
-    fetch, nf = median_counter(fdir, "FETCH_SIZE")
-    write, nw = median_counter(wdir, "WRITE_SIZE")
-    d = {"task": "CartPoleDiscreteBalancing", "worlds": 4096, "dispatches": [nf, nw],
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("out")
+    ap.add_argument("--kernel", default="vecenv_step_kernel")
+    ap.add_argument("--task", default="CartPoleDiscreteBalancing")
+    ap.add_argument("--worlds", type=int, default=4096)
+    a = ap.parse_args()
+    fdir, wdir, out = a.fetch_dir, a.write_dir, a.out
+    fetch, nf = median_counter(fdir, "FETCH_SIZE", a.kernel)
+    write, nw = median_counter(wdir, "WRITE_SIZE", a.kernel)
+    d = {"task": a.task, "worlds": a.worlds, "kernel": a.kernel, "dispatches": [nf, nw],
          "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
          "bytes_per_launch": int(round((fetch + write) * 1024)),
          "note": "raw FETCH_SIZE + WRITE_SIZE (KiB x 1024) per dispatch, median over dispatches; "
