@@ -171,11 +171,39 @@ __device__ __forceinline__ SI downdate(const SI& I, const SV& U, float psi) {
     return o;
 }
 
+// Per-world dynamic parameters: body masses and gravity in the base frame.
+// Nominal values come from the shared block; per-world randomisation
+// (kernels.hip: vecenv kernels with RAND) overrides them.  A mass change keeps
+// the COM and the rotational inertia about the COM (an SDF <mass> edit).
+template <int N>
+struct Dyn {
+    float m[N];
+    f3 g;
+};
+template <int N>
+__device__ __forceinline__ Dyn<N> nominal_dyn(const ChainF* __restrict__ P) {
+    Dyn<N> D;
+#pragma unroll
+    for (int i = 0; i < N; ++i) D.m[i] = P->b[i].mass;
+    D.g = {P->g[0], P->g[1], P->g[2]};
+    return D;
+}
+
+// rotational inertia about the body origin for mass m: the stored Io (for
+// b.mass) + (m - b.mass)(|c|^2 1 - c c^T); the correction folds away when
+// m is the nominal mass of a constant-folded model
+__device__ __forceinline__ Sy inertia_origin(const BodyF& b, float m) {
+    const float dm = m - b.mass, cx = b.com[0], cy = b.com[1], cz = b.com[2];
+    return {b.Io[0] + dm * (cy * cy + cz * cz), b.Io[1] + dm * (cx * cx + cz * cz),
+            b.Io[2] + dm * (cx * cx + cy * cy), b.Io[3] - dm * cx * cy, b.Io[4] - dm * cx * cz,
+            b.Io[5] - dm * cy * cz};
+}
+
 // rigid-body spatial inertia about the body origin
-__device__ __forceinline__ SI rigid(const BodyF& b) {
+__device__ __forceinline__ SI rigid(const BodyF& b, float m) {
     SI I;
-    I.A = {b.Io[0], b.Io[1], b.Io[2], b.Io[3], b.Io[4], b.Io[5]};
-    const float m = b.mass, cx = b.com[0], cy = b.com[1], cz = b.com[2];
+    I.A = inertia_origin(b, m);
+    const float cx = b.com[0], cy = b.com[1], cz = b.com[2];
     // B = m [c]x
     I.B.m[0] = 0.f;     I.B.m[1] = -m * cz; I.B.m[2] = m * cy;
     I.B.m[3] = m * cz;  I.B.m[4] = 0.f;     I.B.m[5] = -m * cx;
@@ -351,7 +379,7 @@ __device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p
 template <int N, bool DUAL, Topo TOPO, class WK>
 __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&q)[N],
                                     const float (&qd)[N], const float (&tau)[N], float dt,
-                                    float (&qdd)[N], WK& W) {
+                                    float (&qdd)[N], WK& W, const Dyn<N>& D) {
     SV V[N];
     f3 g[N];
     // outward pass: kinematics, velocities, bias forces
@@ -367,19 +395,20 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
             g[i] = mulT(s.R, g[pa]);
         } else {
             V[i] = Sq;
-            g[i] = mulT(s.R, mk(P->g[0], P->g[1], P->g[2]));
+            g[i] = mulT(s.R, D.g);
         }
         const SV& Vi = V[i];
         // eta = ad(V, S qd)
         s.eta = {cross(Vi.w, Sq.w), cross(Vi.w, Sq.v) + cross(Vi.v, Sq.w)};
         // h = I V (rigid)
         const f3 c = {b.com[0], b.com[1], b.com[2]};
-        const Sy Io = {b.Io[0], b.Io[1], b.Io[2], b.Io[3], b.Io[4], b.Io[5]};
-        const f3 hw = mul(Io, Vi.w) + b.mass * cross(c, Vi.v);
-        const f3 hv = b.mass * (Vi.v - cross(c, Vi.w));
+        const float m = D.m[i];
+        const Sy Io = inertia_origin(b, m);
+        const f3 hw = mul(Io, Vi.w) + m * cross(c, Vi.v);
+        const f3 hv = m * (Vi.v - cross(c, Vi.w));
         // B = -dad(V, IV) - I [0; g]
-        W.own(i) = {cross(Vi.w, hw) + cross(Vi.v, hv) - b.mass * cross(c, g[i]),
-                    cross(Vi.w, hv) - b.mass * g[i]};
+        W.own(i) = {cross(Vi.w, hw) + cross(Vi.v, hv) - m * cross(c, g[i]),
+                    cross(Vi.w, hv) - m * g[i]};
     }
     // inward pass: articulated inertias / biases accumulate into the parent
     SI carry[N];
@@ -391,7 +420,7 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         BodyState& s = W.bs(i);
         const int pa = parent_of(TOPO, i);
         const bool kids = has_child(TOPO, N, i);
-        SI AI = rigid(b);
+        SI AI = rigid(b, D.m[i]);
         SV Bi = W.own(i);
         if (kids) {
             AI += carry[i];
@@ -399,12 +428,12 @@ __device__ __forceinline__ void aba(const ChainF* __restrict__ P, const float (&
         }
         // U = AI S
         s.U = ais(AI, b);
-        const float D = proj(b, s.U);
-        s.psi = rcp(D + dt * b.damping);
+        const float Dss = proj(b, s.U);
+        s.psi = rcp(Dss + dt * b.damping);
         const SV AIeta = mul(AI, s.eta);
         s.tt = tau[i] - b.damping * qd[i] - proj(b, AIeta + Bi);
         if constexpr (DUAL) {
-            SI AIn = rigid(b);
+            SI AIn = rigid(b, D.m[i]);
             if (kids) AIn += carryN[i];
             const SV Un = ais(AIn, b);
             const float psin = rcp(proj(b, Un));
@@ -578,8 +607,8 @@ template <int N, bool DUAL, bool CONS, Topo TOPO, class WK>
 __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
                                         const float (&tau)[N], const uint8_t (&act)[N],
                                         const float (&vcmd)[N], float dt, int pgs_iters,
-                                        float (&qdd)[N], WK& W) {
-    aba<N, DUAL, TOPO>(P, q, qd, tau, dt, qdd, W);
+                                        float (&qdd)[N], WK& W, const Dyn<N>& D) {
+    aba<N, DUAL, TOPO>(P, q, qd, tau, dt, qdd, W, D);
 #pragma unroll
     for (int i = 0; i < N; ++i) qd[i] += dt * qdd[i];
 
@@ -671,7 +700,17 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
                                         const float (&vcmd)[N], float dt, int pgs_iters,
                                         float (&qdd)[N]) {
     RegStage<N, DUAL> W;
-    substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vcmd, dt, pgs_iters, qdd, W);
+    substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vcmd, dt, pgs_iters, qdd, W, nominal_dyn<N>(P));
+}
+
+// register-staged substep with per-world dynamic parameters
+template <int N, bool DUAL, bool CONS, Topo TOPO = chain_topo(N)>
+__device__ __forceinline__ void substep_dyn(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
+                                            const float (&tau)[N], const uint8_t (&act)[N],
+                                            const float (&vcmd)[N], float dt, int pgs_iters,
+                                            float (&qdd)[N], const Dyn<N>& D) {
+    RegStage<N, DUAL> W;
+    substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vcmd, dt, pgs_iters, qdd, W, D);
 }
 
 }  // namespace dev

@@ -153,6 +153,63 @@ __device__ __forceinline__ float task_reward(const TaskF& T, const float (&q)[N]
     }
 }
 
+// Per-world physics sample of (world, episode): masses from Philox blocks
+// 1.., gravity from block 8 by Box-Muller (SDFRandomizer.sample,
+// randomizers/model/sdf.py:264-315: force_positive clips the SAMPLE at 0, so
+// an additive mass change is max(U(lo, hi), 0); cartpole.py:51-56 gravity).
+template <int N>
+__device__ __forceinline__ Dyn<N> sample_dyn(const ChainF* __restrict__ P, const TaskF& T, uint32_t w,
+                                             uint32_t episode, float& gz_out) {
+    Dyn<N> D = nominal_dyn<N>(P);
+    gz_out = 0.f;
+    if (T.randomize & kRandMass) {
+#pragma unroll
+        for (int b = 0; b < (N + 3) / 4; ++b) {
+            uint32_t r[4];
+            philox(T.seed_lo, T.seed_hi, w, episode, r, 1u + static_cast<uint32_t>(b));
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * b + k < N) D.m[4 * b + k] += fmaxf(unif(r[k], T.mass_lo, T.mass_hi), 0.f);
+        }
+    }
+    if (T.randomize & kRandGravity) {
+        uint32_t r[4];
+        philox(T.seed_lo, T.seed_hi, w, episode, r, 8u);
+        const float u1 = static_cast<float>((r[0] >> 8) + 1u) * (1.f / 16777216.f);  // (0, 1]
+        const float u2 = static_cast<float>(r[1] >> 8) * (1.f / 16777216.f);
+        const float z = sqrtf(-2.f * logf(u1)) * cosf(2.f * kPi * u2);
+        const float gz = T.g_mean + T.g_std * z;
+        D.g = {gz * T.gdir[0], gz * T.gdir[1], gz * T.gdir[2]};
+        gz_out = gz;
+    }
+    return D;
+}
+
+template <int N>
+__device__ __forceinline__ Dyn<N> load_dyn(const ChainF* __restrict__ P, const TaskF& T, const VecDev& V, int W,
+                                           int w) {
+    Dyn<N> D = nominal_dyn<N>(P);
+    if (T.randomize & kRandMass) {
+#pragma unroll
+        for (int d = 0; d < N; ++d) D.m[d] = V.rmass[d * W + w];
+    }
+    if (T.randomize & kRandGravity) {
+        const float gz = V.rgz[w];
+        D.g = {gz * T.gdir[0], gz * T.gdir[1], gz * T.gdir[2]};
+    }
+    return D;
+}
+
+template <int N>
+__device__ __forceinline__ void store_dyn(const TaskF& T, const VecDev& V, int W, int w, const Dyn<N>& D,
+                                          float gz) {
+    if (T.randomize & kRandMass) {
+#pragma unroll
+        for (int d = 0; d < N; ++d) V.rmass[d * W + w] = D.m[d];
+    }
+    if (T.randomize & kRandGravity) V.rgz[w] = gz;
+}
+
 template <int N>
 __device__ __forceinline__ void load_state(const SimDev& S, int W, int w, float (&q)[N], float (&qd)[N]) {
 #pragma unroll
@@ -269,7 +326,7 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
                     }
                 }
             }
-            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage);
+            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, nominal_dyn<N>(P));
         }
 #pragma unroll
         for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];
@@ -280,11 +337,17 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
 }
 
 template <int N, int KIND>
-__global__ void __launch_bounds__(256) vecenv_reset_kernel(TaskF T, SimDev S, VecDev V, float* __restrict__ obs,
-                                                           int W) {
+__global__ void __launch_bounds__(256) vecenv_reset_kernel(const ChainF* __restrict__ P, TaskF T, SimDev S,
+                                                           VecDev V, float* __restrict__ obs, int W) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     float q[N], qd[N], o[4];
+    if (T.randomize) {
+        const uint32_t gw = T.world_offset + static_cast<uint32_t>(w);
+        float gz;
+        const Dyn<N> D = sample_dyn<N>(P, T, gw, 0u, gz);
+        store_dyn<N>(T, V, W, w, D, gz);
+    }
     task_reset<N, KIND>(T, T.world_offset + static_cast<uint32_t>(w), 0u, q, qd);
     task_obs<N, KIND>(q, qd, o);
     constexpr int NO = (KIND == 3) ? 3 : 4;
@@ -295,7 +358,7 @@ __global__ void __launch_bounds__(256) vecenv_reset_kernel(TaskF T, SimDev S, Ve
 }
 
 // STEPS == 0: single step; otherwise loop over T_steps with [t, w] layouts.
-template <int N, int KIND, bool DUAL, bool CONS, bool ROLLOUT, int BAKED>
+template <int N, int KIND, bool DUAL, bool CONS, bool ROLLOUT, int BAKED, bool RAND = false>
 __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restrict__ Pin, TaskF T, SimDev S,
                                                           VecDev V, const void* __restrict__ actions,
                                                           float* __restrict__ obs, float* __restrict__ reward,
@@ -315,6 +378,8 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
     float vc[N];
 #pragma unroll
     for (int d = 0; d < N; ++d) { act[d] = kActForce; vc[d] = 0.f; }
+    Dyn<N> D;
+    if constexpr (RAND) D = load_dyn<N>(P, T, V, W, w);
     const int nsteps = ROLLOUT ? T_steps : 1;
     for (int t = 0; t < nsteps; ++t) {
         const size_t idx = static_cast<size_t>(t) * W + w;
@@ -333,7 +398,8 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
 #pragma unroll
             for (int d = 0; d < N; ++d) tau[d] = 0.f;
             tau[0] = (s == 0) ? force : 0.f;
-            substep<N, DUAL, CONS>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
+            if constexpr (RAND) substep_dyn<N, DUAL, CONS>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd, D);
+            else substep<N, DUAL, CONS>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd);
         }
         float o[4];
         task_obs<N, KIND>(q, qd, o);
@@ -346,6 +412,12 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
             store_obs<NO>(term_obs + idx * NO, o);
             episode += 1u;
             steps = 0u;
+            if constexpr (RAND) {
+                // GazeboEnvRandomizer.reset: new physics and model sample per episode
+                float gz;
+                D = sample_dyn<N>(P, T, T.world_offset + static_cast<uint32_t>(w), episode, gz);
+                store_dyn<N>(T, V, W, w, D, gz);
+            }
             task_reset<N, KIND>(T, T.world_offset + static_cast<uint32_t>(w), episode, q, qd);
             task_obs<N, KIND>(q, qd, o);
         }
@@ -423,7 +495,7 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
             const float e = P->b[d].effort;
             tau[d] = fminf(fmaxf(u, -e), e);
         }
-        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd, stage);
+        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd, stage, nominal_dyn<N>(P));
     }
     float r = 0.f;
 #pragma unroll
@@ -504,7 +576,7 @@ hipError_t scenario_n(const ChainF* P, bool cons, bool dual, int baked, const Si
     return hipGetLastError();
 }
 
-template <int N, int KIND, bool ROLLOUT>
+template <int N, int KIND, bool ROLLOUT, bool RAND>
 hipError_t vec_nk(const ChainF* P, bool cons, bool dual, int baked, const TaskF& T, const SimDev& S,
                   const VecDev& V, const void* a, float* o, float* r, uint8_t* d, float* to, int W,
                   float dt, int substeps, int pgs, int Ts, hipStream_t st) {
@@ -512,26 +584,26 @@ hipError_t vec_nk(const ChainF* P, bool cons, bool dual, int baked, const TaskF&
     // constant-folded instantiations for the shipped models (their flags fix cons/dual)
     if constexpr (N == 2 && KIND <= 2) {
         if (baked == baked::kCartpoleId && cons && !dual) {
-            hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, true, ROLLOUT, baked::kCartpoleId>),
+            hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, true, ROLLOUT, baked::kCartpoleId, RAND>),
                                grid_for(W, B), dim3(B), 0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
             return hipGetLastError();
         }
     }
     if constexpr (N == 1 && KIND == 3) {
         if (baked == baked::kPendulumId && !cons) {
-            hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, false, ROLLOUT, baked::kPendulumId>),
+            hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, false, ROLLOUT, baked::kPendulumId, RAND>),
                                grid_for(W, B), dim3(B), 0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
             return hipGetLastError();
         }
     }
     if (!cons)
-        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, false, ROLLOUT, 0>), grid_for(W, B), dim3(B),
+        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, false, ROLLOUT, 0, RAND>), grid_for(W, B), dim3(B),
                            0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
     else if (!dual)
-        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, true, ROLLOUT, 0>), grid_for(W, B), dim3(B),
+        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, false, true, ROLLOUT, 0, RAND>), grid_for(W, B), dim3(B),
                            0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
     else
-        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, true, true, ROLLOUT, 0>), grid_for(W, B), dim3(B),
+        hipLaunchKernelGGL((dev::vecenv_step_kernel<N, KIND, true, true, ROLLOUT, 0, RAND>), grid_for(W, B), dim3(B),
                            0, st, P, T, S, V, a, o, r, d, to, W, dt, substeps, pgs, Ts);
     return hipGetLastError();
 }
@@ -573,13 +645,13 @@ hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const Sim
     if (T.kind == 4 && n == 9)
         hipLaunchKernelGGL((dev::vecenv_pid_reset_kernel<9>), grid_for(W, B), dim3(B), 0, st, P, T, S, V, obs, W);
     else if (T.kind == 3 && n == 1)
-        hipLaunchKernelGGL((dev::vecenv_reset_kernel<1, 3>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<1, 3>), grid_for(W, B), dim3(B), 0, st, P, T, S, V, obs, W);
     else if (T.kind == 0 && n == 2)
-        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 0>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 0>), grid_for(W, B), dim3(B), 0, st, P, T, S, V, obs, W);
     else if (T.kind == 1 && n == 2)
-        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 1>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 1>), grid_for(W, B), dim3(B), 0, st, P, T, S, V, obs, W);
     else if (T.kind == 2 && n == 2)
-        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 2>), grid_for(W, B), dim3(B), 0, st, T, S, V, obs, W);
+        hipLaunchKernelGGL((dev::vecenv_reset_kernel<2, 2>), grid_for(W, B), dim3(B), 0, st, P, T, S, V, obs, W);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -615,17 +687,21 @@ hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, int 
                               const SimDev& S, const VecDev& V, const void* actions, float* obs,
                               float* reward, uint8_t* done, float* term_obs, int W, float dt,
                               int substeps, int pgs_iters, int T_steps, hipStream_t st) {
-#define MW_VEC(NN, KK)                                                                                      \
-    return (T_steps > 0)                                                                                    \
-               ? vec_nk<NN, KK, true>(P, cons, dual, baked, T, S, V, actions, obs, reward, done, term_obs, W, \
-                                      dt, substeps, pgs_iters, T_steps, st)                                 \
-               : vec_nk<NN, KK, false>(P, cons, dual, baked, T, S, V, actions, obs, reward, done, term_obs, W, \
-                                       dt, substeps, pgs_iters, 1, st)
+#define MW_VEC_R(NN, KK, RR)                                                                                 \
+    return (T_steps > 0)                                                                                     \
+               ? vec_nk<NN, KK, true, RR>(P, cons, dual, baked, T, S, V, actions, obs, reward, done, term_obs, W, \
+                                          dt, substeps, pgs_iters, T_steps, st)                              \
+               : vec_nk<NN, KK, false, RR>(P, cons, dual, baked, T, S, V, actions, obs, reward, done, term_obs,   \
+                                           W, dt, substeps, pgs_iters, 1, st)
+#define MW_VEC(NN, KK)              \
+    if (T.randomize) MW_VEC_R(NN, KK, true); \
+    MW_VEC_R(NN, KK, false)
     if (T.kind == 3 && n == 1) { MW_VEC(1, 3); }
     if (T.kind == 0 && n == 2) { MW_VEC(2, 0); }
     if (T.kind == 1 && n == 2) { MW_VEC(2, 1); }
     if (T.kind == 2 && n == 2) { MW_VEC(2, 2); }
 #undef MW_VEC
+#undef MW_VEC_R
     return hipErrorInvalidValue;
 }
 

@@ -52,11 +52,20 @@ struct TaskF {
     // position-target tasks (kind 4): reset pose and half-width of its uniform noise
     float home[kMaxKernelDofs];
     float home_noise;
+    // per-world physics randomisation, resampled at every reset
+    // (gym_ignition_environments/randomizers/cartpole.py:51-56, 100-135)
+    int32_t randomize;     // bit 0: body masses, bit 1: gravity
+    float mass_lo, mass_hi;  // additive mass sample U(lo, hi), clipped at 0 (force_positive)
+    float g_mean, g_std;     // world gravity z ~ N(mean, std)
+    float gdir[3];           // the world z axis in the base frame (gravity = gz * gdir)
 };
+enum : int32_t { kRandMass = 1, kRandGravity = 2 };
 
 struct VecDev {
     uint32_t* episode = nullptr;
     uint32_t* steps = nullptr;
+    float* rmass = nullptr;  // [n_dofs][W] per-world body masses (randomised tasks)
+    float* rgz = nullptr;    // [W] per-world gravity z
 };
 
 // Returns hipSuccess or the launch error.

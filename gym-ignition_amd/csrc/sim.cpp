@@ -109,6 +109,7 @@ struct mw_vecenv {
     mw::TaskF task{};
     mw::VecDev dev{};
     void* d_counters = nullptr;
+    void* d_physics = nullptr;  // per-world randomised masses + gravity
 };
 
 namespace {
@@ -932,7 +933,30 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
         break;
     }
     }
+    if (cfg->randomize & ~(MW_RAND_MASS | MW_RAND_GRAVITY)) return fail(MW_EINVAL, "unknown randomisation bits");
+    if (cfg->randomize && pidtask) return fail(MW_EINVAL, "randomisation is available for the CartPole / Pendulum tasks");
+    if ((cfg->randomize & MW_RAND_MASS) && !(cfg->mass_high >= cfg->mass_low))
+        return fail(MW_EINVAL, "mass_high must be >= mass_low");
+    if ((cfg->randomize & MW_RAND_GRAVITY) && !(cfg->gravity_std >= 0.f))
+        return fail(MW_EINVAL, "gravity_std must be >= 0");
+    T.randomize = cfg->randomize;
+    T.mass_lo = cfg->mass_low;
+    T.mass_hi = cfg->mass_high;
+    T.g_mean = cfg->gravity_mean;
+    T.g_std = cfg->gravity_std;
+    {
+        // the world z axis in the base frame: R_base^T e_z
+        const auto& R = s->model.base_R;
+        for (int k = 0; k < 3; ++k) T.gdir[k] = static_cast<float>(R[6 + k]);
+    }
     MW_HIP(hipSetDevice(s->cfg.device));
+    if (cfg->randomize) {
+        const size_t bytes = (static_cast<size_t>(n) + 1) * s->W * sizeof(float);
+        MW_HIP(hipMalloc(&e->d_physics, bytes));
+        MW_HIP(hipMemsetAsync(e->d_physics, 0, bytes, s->stream));
+        e->dev.rmass = static_cast<float*>(e->d_physics);
+        e->dev.rgz = e->dev.rmass + static_cast<size_t>(n) * s->W;
+    }
     MW_HIP(hipMalloc(&e->d_counters, 2 * static_cast<size_t>(s->W) * sizeof(uint32_t)));
     MW_HIP(hipMemsetAsync(e->d_counters, 0, 2 * static_cast<size_t>(s->W) * sizeof(uint32_t), s->stream));
     e->dev.episode = static_cast<uint32_t*>(e->d_counters);
@@ -945,6 +969,7 @@ void mw_vecenv_destroy(mw_vecenv* e) {
     if (!e) return;
     if (e->sim && e->sim->stream) (void)hipStreamSynchronize(e->sim->stream);
     (void)hipFree(e->d_counters);
+    (void)hipFree(e->d_physics);
     delete e;
 }
 
@@ -995,6 +1020,15 @@ int mw_vecenv_step(mw_vecenv* e, const void* a, float* o, float* r, uint8_t* d, 
 int mw_vecenv_rollout(mw_vecenv* e, int32_t T, const void* a, float* o, float* r, uint8_t* d, float* to) {
     if (T <= 0) return fail(MW_EINVAL, "T must be positive");
     return vec_common(e, T, a, o, r, d, to);
+}
+
+int mw_vecenv_physics(mw_vecenv* e, float* mass, float* gz) {
+    if (!e || !mass || !gz) return fail(MW_EINVAL, "null argument");
+    if (!e->d_physics) return fail(MW_ESTATE, "the env was created without physics randomisation");
+    const size_t nw = static_cast<size_t>(e->sim->n) * e->sim->W;
+    MW_HIP(hipMemcpyAsync(mass, e->dev.rmass, nw * sizeof(float), hipMemcpyDeviceToDevice, e->sim->stream));
+    MW_HIP(hipMemcpyAsync(gz, e->dev.rgz, e->sim->W * sizeof(float), hipMemcpyDeviceToDevice, e->sim->stream));
+    return MW_OK;
 }
 
 int mw_vecenv_counters(mw_vecenv* e, uint32_t* episode, uint32_t* steps) {

@@ -34,6 +34,8 @@ TASK_CARTPOLE_CONTINUOUS_BALANCING = 1
 TASK_CARTPOLE_CONTINUOUS_SWINGUP = 2
 TASK_PENDULUM_SWINGUP = 3
 TASK_PANDA_POSITION_TRACKING = 4
+RAND_MASS = 1
+RAND_GRAVITY = 2
 
 
 class MwConfig(ctypes.Structure):
@@ -54,6 +56,12 @@ class MwTaskConfig(ctypes.Structure):
         ("reward_cart_at_center", ctypes.c_int32),
         ("world_offset", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("randomize", ctypes.c_int32),
+        ("mass_low", ctypes.c_float),
+        ("mass_high", ctypes.c_float),
+        ("gravity_mean", ctypes.c_float),
+        ("gravity_std", ctypes.c_float),
+        ("pad_", ctypes.c_int32),
     ]
 
 
@@ -115,6 +123,7 @@ SIGNATURES = [
     ("mw_vecenv_step", ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     ("mw_vecenv_rollout", ctypes.c_int, [_P, _I, _P, _P, _P, _P, _P]),
     ("mw_vecenv_counters", ctypes.c_int, [_P, _P, _P]),
+    ("mw_vecenv_physics", ctypes.c_int, [_P, _P, _P]),
 ]
 
 _lib: Optional[ctypes.CDLL] = None

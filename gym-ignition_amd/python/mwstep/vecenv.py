@@ -47,7 +47,13 @@ class VecEnv:
                  device: int = 0, seed: int = 42, agent_rate: float = 1000.0,
                  physics_rate: float = 1000.0, max_episode_steps: int = 5000,
                  reward_cart_at_center: bool = True, model_file: Optional[str] = None,
-                 pgs_iters: int = 20, world_offset: int = 0):
+                 pgs_iters: int = 20, world_offset: int = 0, randomize: bool = False,
+                 mass_range: Tuple[float, float] = (-0.2, 0.2),
+                 gravity_normal: Tuple[float, float] = (-9.8, 0.2)):
+        """``randomize=True`` resamples every world's physics at each reset as the
+        reference's CartPole randomizer does (randomizers/cartpole.py:51-56,
+        100-135): body masses + max(U(*mass_range), 0), gravity z ~
+        N(*gravity_normal)."""
         torch = _torch()
         if task not in TASKS:
             raise ValueError(f"unknown task {task!r}; known: {sorted(TASKS)}")
@@ -72,7 +78,10 @@ class VecEnv:
                 p, i, dd = PANDA_PID_GAINS_1000HZ[name]
                 self.sim.set_pid(d, [p, i, dd, -big, big, 0.0, -big, big])
         cfg = N.MwTaskConfig(kind, max_episode_steps, 1 if reward_cart_at_center else 0,
-                             world_offset, seed & 0xFFFFFFFFFFFFFFFF)
+                             world_offset, seed & 0xFFFFFFFFFFFFFFFF,
+                             (N.RAND_MASS | N.RAND_GRAVITY) if randomize else 0,
+                             mass_range[0], mass_range[1], gravity_normal[0], gravity_normal[1], 0)
+        self.randomize = randomize
         h = ctypes.c_void_p()
         N.check(N.lib().mw_vecenv_create(self.sim.handle, ctypes.byref(cfg), ctypes.byref(h)),
                 "mw_vecenv_create")
@@ -161,6 +170,15 @@ class VecEnv:
         N.check(N.lib().mw_vecenv_counters(self._h, ctypes.c_void_p(ep.data_ptr()),
                                            ctypes.c_void_p(st.data_ptr())), "counters")
         return ep, st
+
+    def physics(self):
+        """(masses [dofs, n_worlds], gravity z [n_worlds]) of a randomised env."""
+        torch = _torch()
+        m = torch.empty((self.sim.dofs, self.n_worlds), dtype=torch.float32, device=self.device)
+        gz = torch.empty((self.n_worlds,), dtype=torch.float32, device=self.device)
+        N.check(N.lib().mw_vecenv_physics(self._h, ctypes.c_void_p(m.data_ptr()),
+                                          ctypes.c_void_p(gz.data_ptr())), "physics")
+        return m, gz
 
     def state(self):
         """(q, qd) float32 [dofs, n_worlds] copies of the device SoA state."""

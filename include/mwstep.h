@@ -192,7 +192,20 @@ typedef struct {
     int32_t world_offset;            /* global index of world 0 (sharding):  */
                                      /* reset streams do not depend on P     */
     uint64_t seed;
+    /* Per-world physics randomisation, resampled at every (auto-)reset like
+     * GazeboEnvRandomizer.reset (python/gym_ignition/randomizers/
+     * gazebo_env_randomizer.py): MW_RAND_MASS adds max(U(mass_low, mass_high), 0)
+     * to every moving body's mass (randomizers/cartpole.py:100-135 with
+     * SDFRandomizer's force_positive, randomizers/model/sdf.py:294-295; COM and
+     * rotational inertia unchanged), MW_RAND_GRAVITY sets the world gravity to
+     * (0, 0, N(gravity_mean, gravity_std)) (randomizers/cartpole.py:51-56). */
+    int32_t randomize;
+    float mass_low, mass_high;
+    float gravity_mean, gravity_std;
+    int32_t pad_;
 } mw_task_config;
+#define MW_RAND_MASS 1
+#define MW_RAND_GRAVITY 2
 
 int mw_vecenv_create(mw_sim* sim, const mw_task_config* cfg, mw_vecenv** out);
 void mw_vecenv_destroy(mw_vecenv* env);
@@ -214,6 +227,10 @@ int mw_vecenv_rollout(mw_vecenv* env, int32_t T, const void* actions_dev, float*
 /* Copy the per-world episode / step counters (uint32 [n_worlds]) into caller
  * device buffers (async, on the sim's stream). */
 int mw_vecenv_counters(mw_vecenv* env, uint32_t* episode_dev, uint32_t* steps_dev);
+/* Copy the per-world randomised physics (body masses float32 [n_dofs][n_worlds],
+ * gravity z float32 [n_worlds]) into caller device buffers; MW_ESTATE when the
+ * env was created without randomisation. */
+int mw_vecenv_physics(mw_vecenv* env, float* mass_dev, float* gravity_z_dev);
 
 #ifdef __cplusplus
 }

@@ -556,6 +556,58 @@ static double f32(double v) { return (double)(float)v; }
 #define OR_PI 3.14159265358979323846
 static double deg2rad(double d) { return d * OR_PI / 180.0; }
 
+/* Philox4x32-10 with the third counter word set (block index) */
+static void philox_block(uint64_t seed, uint32_t world, uint32_t episode, uint32_t block, uint32_t out[4])
+{
+    const uint32_t ctr[4] = {world, episode, block, 0u};
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    or_philox_raw(ctr, key, out);
+}
+
+/* SDFRandomizer.sample (randomizers/model/sdf.py:264-315): an Additive
+ * Uniform randomisation with force_positive clips the SAMPLE at 0, so every
+ * moving body's mass becomes m + max(U(low, high), 0) (cartpole.py:100-135;
+ * Philox blocks 1.., four bodies per block); the physics randomizer sets the
+ * gravity to (0, 0, N(mean, std)) (cartpole.py:51-56; Box-Muller on block 8). */
+void or_task_sample_physics(const or_model* m, const or_task* t, uint32_t world,
+                            uint32_t episode, double* masses, double* gz)
+{
+    for (int i = 0; i < m->n; ++i) masses[i] = m->mass[i];
+    *gz = 0.0;
+    if (t->randomize & 1) {
+        for (int b = 0; b < (m->n + 3) / 4; ++b) {
+            uint32_t r[4];
+            philox_block(t->seed, world, episode, 1u + (uint32_t)b, r);
+            for (int k = 0; k < 4 && 4 * b + k < m->n; ++k) {
+                double u = t->mass_low + (t->mass_high - t->mass_low) * ((double)(r[k] >> 8) * (1.0 / 16777216.0));
+                masses[4 * b + k] += (u > 0.0) ? u : 0.0;
+            }
+        }
+    }
+    if (t->randomize & 2) {
+        uint32_t r[4];
+        philox_block(t->seed, world, episode, 8u, r);
+        const double u1 = (double)((r[0] >> 8) + 1u) * (1.0 / 16777216.0);
+        const double u2 = (double)(r[1] >> 8) * (1.0 / 16777216.0);
+        *gz = t->gravity_mean + t->gravity_std * sqrt(-2.0 * log(u1)) * cos(2.0 * 3.14159265358979323846 * u2);
+    }
+}
+
+/* the model one world steps with: the shared one, or a copy carrying the
+ * world's randomised masses / gravity */
+static const or_model* world_model(const or_model* m, const or_task* t, uint32_t w, uint32_t ep,
+                                   or_model* scratch)
+{
+    if (!t->randomize) return m;
+    double masses[OR_MAXB], gz;
+    or_task_sample_physics(m, t, w, ep, masses, &gz);
+    memcpy(scratch, m, sizeof(or_model));
+    for (int i = 0; i < m->n; ++i) scratch->mass[i] = masses[i];
+    if (t->randomize & 2)
+        for (int k = 0; k < 3; ++k) scratch->gravity_base[k] = gz * t->gdir[k];
+    return scratch;
+}
+
 void or_task_reset_state(const or_task* t, uint32_t world, uint32_t episode,
                          double* q, double* qd)
 {
@@ -671,7 +723,8 @@ static void vec_step_one(const or_model* m, const or_task* t, int W, int w,
     const int n = m->n;
     double qw[OR_MAXB], qdw[OR_MAXB], o[4];
     for (int d = 0; d < n; ++d) { qw[d] = q[d * W + w]; qdw[d] = qd[d * W + w]; }
-    world_step(m, t, qw, qdw, action, pgs_iters);
+    or_model scratch;
+    world_step(world_model(m, t, (uint32_t)w, episode[w], &scratch), t, qw, qdw, action, pgs_iters);
     const int no = or_task_obs(t, qw, qdw, o);
     const int tdone = task_done(t, o);
     reward[w] = task_reward(t, qw, qdw, o, tdone);

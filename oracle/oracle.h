@@ -112,7 +112,18 @@ typedef struct {
     int32_t reward_cart_at_center;
     double dt;
     uint64_t seed;
+    /* per-world physics randomisation (bit 0 masses, bit 1 gravity), sampled
+     * from (world, episode): randomizers/cartpole.py:51-56, 100-135 */
+    int32_t randomize;
+    int32_t pad_;
+    double mass_low, mass_high;     /* additive mass sample, clipped at 0     */
+    double gravity_mean, gravity_std;
+    double gdir[3];                 /* world z axis in the base frame          */
 } or_task;
+
+/* Per-world physics of (world, episode): masses[n] and gravity z. */
+void or_task_sample_physics(const or_model* m, const or_task* t, uint32_t world,
+                            uint32_t episode, double* masses, double* gz);
 
 /* Philox4x32-10 (Salmon et al. 2011), key = seed, counter = (world, episode, 0, 0). */
 void or_philox(uint64_t seed, uint32_t world, uint32_t episode, uint32_t out[4]);

@@ -74,6 +74,13 @@ class OrTask(ctypes.Structure):
         ("reward_cart_at_center", ctypes.c_int32),
         ("dt", ctypes.c_double),
         ("seed", ctypes.c_uint64),
+        ("randomize", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("mass_low", ctypes.c_double),
+        ("mass_high", ctypes.c_double),
+        ("gravity_mean", ctypes.c_double),
+        ("gravity_std", ctypes.c_double),
+        ("gdir", ctypes.c_double * 3),
     ]
 
 
@@ -112,6 +119,7 @@ def lib():
         L.or_philox.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, U32]
         L.or_philox_raw.argtypes = [U32, U32, U32]
         L.or_task_reset_state.argtypes = [T, ctypes.c_uint32, ctypes.c_uint32, D, D]
+        L.or_task_sample_physics.argtypes = [M, T, ctypes.c_uint32, ctypes.c_uint32, D, D]
         L.or_vec_step.argtypes = [M, T, ctypes.c_int, D, D, ctypes.c_void_p, U32, U32, D, D,
                                   U8, D, ctypes.c_int]
         L.or_vec_reset.argtypes = [M, T, ctypes.c_int, D, D, U32, U32, D]
@@ -513,8 +521,14 @@ def philox_raw(ctr, key) -> np.ndarray:
 
 
 def make_task(kind: int, dt: float = 1e-3, steps_per_run: int = 1, max_episode_steps: int = 5000,
-              reward_cart_at_center: bool = True, seed: int = 42) -> OrTask:
+              reward_cart_at_center: bool = True, seed: int = 42, randomize: int = 0,
+              mass_range=(-0.2, 0.2), gravity_normal=(-9.8, 0.2), gdir=(0.0, 0.0, 1.0)) -> OrTask:
     t = OrTask()
+    t.randomize = randomize
+    t.mass_low, t.mass_high = mass_range
+    t.gravity_mean, t.gravity_std = gravity_normal
+    for k in range(3):
+        t.gdir[k] = gdir[k]
     t.kind = kind
     t.dt = dt
     t.steps_per_run = steps_per_run
@@ -522,6 +536,15 @@ def make_task(kind: int, dt: float = 1e-3, steps_per_run: int = 1, max_episode_s
     t.reward_cart_at_center = 1 if reward_cart_at_center else 0
     t.seed = seed
     return t
+
+
+def sample_physics(cm: ChainModel, task: OrTask, world: int, episode: int):
+    """(masses [n], gravity z) of one world's episode."""
+    m = np.zeros(cm.n)
+    gz = ctypes.c_double()
+    lib().or_task_sample_physics(ctypes.byref(cm.model), ctypes.byref(task), world, episode, _p(m),
+                                 ctypes.byref(gz))
+    return m, gz.value
 
 
 def n_obs(kind: int) -> int:
