@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-panda", action="store_true", help="skip the config-4 Panda leg")
+    p.add_argument("--no-rand-leg", action="store_true", help="skip the randomised-physics leg")
     p.add_argument("--groups", type=int, default=1,
                    help="world groups per GPU, each on its own stream / hardware queue")
     return p.parse_args()
@@ -124,6 +125,20 @@ def main():
     if not args.no_sweep and world_size == 1 and not env.action_dim:
         sweep = world_sweep(args, dev, torch)
 
+    # ---------------- the same workload with per-world physics randomisation
+    # (masses + gravity resampled at every reset, randomizers/cartpole.py)
+    rand = None
+    if not args.no_rand_leg and rank == 0 and world_size == 1 and not env.action_dim:
+        renvs = make_groups(args.task, W, 1, dev, args.seed, 0, randomize=True)
+        r = time_steps(renvs, actions, args.warmup, K, args.graph_chunk, dev, torch, dist, 1)
+        rand = {"value": round(W * K / r["elapsed"], 1), "unit": "env·steps/s",
+                "ms_per_step": round(r["elapsed"] / K * 1e3, 6),
+                "kernel_us_per_launch": round(r["kernel_us"], 3),
+                "extra_bytes_per_env_step": 4 * (env.sim.dofs + 1),
+                "note": "per-world masses + gravity read every step, resampled at every reset"}
+        for e in renvs:
+            e.close()
+
     # ---------------- BASELINE config 4 (1024 Panda worlds, PID position
     # tracking) measured in the same run when the headline is config 2
     panda = None
@@ -181,6 +196,7 @@ def main():
             "obs_max_abs_err_vs_oracle": parity,
             "rollout_fused": rollout,
             "panda_c4": panda,
+            "randomized": rand,
         }
         print(json.dumps(out))
     for e in envs:

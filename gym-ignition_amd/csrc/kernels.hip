@@ -15,6 +15,7 @@
 
 #include "baked_models.hpp"
 #include "chain_dyn.hpp"
+#include "free_body.hpp"
 #include "kernels.hpp"
 
 namespace mw {
@@ -428,6 +429,66 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
     V.steps[w] = steps;
 }
 
+// ------------------------------------------------- floating free body ----
+// GazeboSimulator::run() for a floating single-body model: pending base pose /
+// velocity resets (WorldPoseCmd / WorldVelocityCmd, Model.cpp:256-360 ->
+// Physics.cpp:1535-1590), the substeps, and the contacts of the last substep
+// (Physics.cpp:2351-2540: point, force on the body = impulse / dt, depth).
+__global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__ F, FreeDev D, int W, RunArgs A,
+                                                       int want_contacts) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    auto at = [&](int f) -> float& { return D.base[f * W + w]; };
+    FreeState S;
+    S.p = {at(0), at(1), at(2)};
+    S.qw = at(3); S.qx = at(4); S.qy = at(5); S.qz = at(6);
+    S.V = {{at(7), at(8), at(9)}, {at(10), at(11), at(12)}};
+    if (A.first) {
+        const uint8_t fl = D.rflag[w];
+        if (fl & 1u) {
+            S.p = {D.rpose[0 * W + w], D.rpose[1 * W + w], D.rpose[2 * W + w]};
+            float qw = D.rpose[3 * W + w], qx = D.rpose[4 * W + w], qy = D.rpose[5 * W + w], qz = D.rpose[6 * W + w];
+            const float inv = 1.f / sqrtf(qw * qw + qx * qx + qy * qy + qz * qz);
+            S.qw = qw * inv; S.qx = qx * inv; S.qy = qy * inv; S.qz = qz * inv;
+        }
+        if (fl & 2u) {
+            // world velocities of the base origin -> body-frame twist
+            const M3 R = quat_to_R(S.qw, S.qx, S.qy, S.qz);
+            const f3 lin = {D.rvel[0 * W + w], D.rvel[1 * W + w], D.rvel[2 * W + w]};
+            const f3 ang = {D.rvel[3 * W + w], D.rvel[4 * W + w], D.rvel[5 * W + w]};
+            S.V = {mulT(R, ang), mulT(R, lin)};
+        }
+        if (fl) D.rflag[w] = 0;
+    }
+    __shared__ SlotRec slots[kMaxFreeSlots * kFreeLanes];
+    Contacts C;
+    C.active = 0u;
+    C.rec = slots + threadIdx.x;
+    if (!A.paused) {
+        for (int s = 0; s < A.substeps; ++s) free_step(F, A.dt, A.pgs_iters, S, C);
+    }
+    at(0) = S.p.x; at(1) = S.p.y; at(2) = S.p.z;
+    at(3) = S.qw; at(4) = S.qx; at(5) = S.qy; at(6) = S.qz;
+    at(7) = S.V.w.x; at(8) = S.V.w.y; at(9) = S.V.w.z;
+    at(10) = S.V.v.x; at(11) = S.V.v.y; at(12) = S.V.v.z;
+    if (want_contacts && !A.paused) {
+        D.cmask[w] = C.active;
+        const float inv_dt = 1.f / A.dt;
+        // force on the body, world frame: (n x_n + t1 x_t1 + t2 x_t2) / dt
+        for (uint32_t m = C.active; m; m &= m - 1u) {
+            const int slot = __builtin_ctz(m);
+            const SlotRec& r = C.at(slot);
+            float* o = D.cdata + static_cast<size_t>(slot) * 7 * W + w;
+            // t1 = (0, -1, 0), t2 = (1, 0, 0), n = (0, 0, 1)
+            o[0 * W] = r.xw.x; o[1 * W] = r.xw.y; o[2 * W] = r.xw.z;
+            o[3 * W] = r.x[2] * inv_dt;
+            o[4 * W] = -r.x[1] * inv_dt;
+            o[5 * W] = r.x[0] * inv_dt;
+            o[6 * W] = r.depth;
+        }
+    }
+}
+
 // ------------------------------------------------ position-target task ----
 // kind 4 (BASELINE config 4, Panda): every joint in Position mode, the
 // JointController PID runs every substep (controller period = step size,
@@ -637,6 +698,13 @@ hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool
     case 9: return scenario_n<9, chain_topo(9)>(P, cons, dual, baked, S, pid, W, a, st);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_free_run(const FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts,
+                           hipStream_t st) {
+    const int B = dev::kFreeLanes;  // the contact slot records in LDS assume 64-thread blocks
+    hipLaunchKernelGGL(dev::free_run_kernel, grid_for(W, B), dim3(B), 0, st, F, D, W, a, contacts);
+    return hipGetLastError();
 }
 
 hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,

@@ -27,6 +27,16 @@ struct SimDev {
     float* pid_u = nullptr;
 };
 
+// Device arrays of a floating single-body model (free_body.hpp).
+struct FreeDev {
+    float* base = nullptr;     // [13][W]: p xyz, q wxyz, twist (body frame) w xyz, v xyz
+    float* rpose = nullptr;    // [7][W] pending base pose reset (p, q wxyz)
+    float* rvel = nullptr;     // [6][W] pending base velocity reset (world linear, world angular)
+    uint8_t* rflag = nullptr;  // [W] bit0 pose reset, bit1 velocity reset
+    float* cdata = nullptr;    // [kMaxFreeSlots][7][W] contact point xyz, force xyz, depth
+    uint32_t* cmask = nullptr; // [W] active contact slots
+};
+
 // One launch of the scenario kernel covers up to 64 substeps of a run.
 struct RunArgs {
     float dt, inv_dt;
@@ -75,6 +85,10 @@ int kernel_topology(const int* parents, int n);
 
 hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const SimDev& S,
                                const PidSet& pid, int W, const RunArgs& a, hipStream_t st);
+
+// F: the model's FreeF block in device memory (free_body.hpp)
+hipError_t launch_free_run(const struct FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts,
+                           hipStream_t st);
 
 hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
                                const VecDev& V, float* obs, int W, hipStream_t st);

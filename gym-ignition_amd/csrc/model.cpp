@@ -208,6 +208,8 @@ struct Link {
     double mass = 0.0;
     V3 com{};
     M3 I{};  // about COM, link frame
+    std::vector<Shape> shapes;  // collision shapes, link frame
+    int unsupported = 0;
 };
 
 struct Joint {
@@ -236,6 +238,20 @@ Link merge(const Link& a, const Link& b, const M3& R, const V3& p) {
     const M3 Ia = shift(a.I, a.mass, sub(a.com, out.com));
     const M3 Ib2 = shift(Ib, b.mass, sub(cb, out.com));
     for (int k = 0; k < 9; ++k) out.I[k] = Ia[k] + Ib2[k];
+    return out;
+}
+
+// lump b (pose R, p in a) into a: inertia (merge) and collision shapes
+Link lump(const Link& a, const Link& b, const M3& R, const V3& p) {
+    Link out = (a.mass + b.mass > 0.0) ? merge(a, b, R, p) : Link{};
+    out.shapes = a.shapes;
+    for (const Shape& sh : b.shapes) {
+        Shape t = sh;
+        t.R = mul(R, sh.R);
+        t.p = add(mul(R, sh.p), p);
+        out.shapes.push_back(t);
+    }
+    out.unsupported = a.unsupported + b.unsupported;
     return out;
 }
 
@@ -283,6 +299,26 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
                 Iin = {ixx, ixy, ixz, ixy, iyy, iyz, ixz, iyz, izz};
             }
             L.I = mul(Ro, mul(Iin, transpose(Ro)));
+        }
+        for (const XNode* ce : le->children("collision")) {
+            const XNode* o = ce->child("origin");
+            const XNode* ge = ce->child("geometry");
+            const XNode* box = ge ? ge->child("box") : nullptr;
+            const XNode* sph = ge ? ge->child("sphere") : nullptr;
+            Shape sh;
+            sh.R = rpy(vec_attr(o, "rpy", {0, 0, 0}));
+            sh.p = vec_attr(o, "xyz", {0, 0, 0});
+            if (box) {
+                sh.type = Shape::Box;
+                sh.size = scale(vec_attr(box, "size", {0, 0, 0}), 0.5);
+            } else if (sph) {
+                sh.type = Shape::Sphere;
+                sh.size = {num_attr(sph, "radius", 0.0), 0.0, 0.0};
+            } else {
+                ++L.unsupported;
+                continue;
+            }
+            L.shapes.push_back(sh);
         }
         links[*nm] = L;
         link_order.push_back(*nm);
@@ -353,9 +389,9 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
         base = joints[found].child;
         joints.erase(joints.begin() + found);
     } else {
-        throw std::runtime_error(
-            "floating-base models are not supported yet (root link '" + base +
-            "' is not attached to 'world')");
+        // floating base: the root link moves with a free joint; its world pose is
+        // the insertion pose (World::insertModel, World.cpp:70-180)
+        out.floating = true;
     }
 
     // lump fixed joints into their parent body
@@ -371,7 +407,7 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
             const std::string po = owner[j.parent];
             const M3 R = mul(offR[j.parent], j.R);
             const V3 p = add(mul(offR[j.parent], j.p), offP[j.parent]);
-            links[po] = merge(links[po], links[j.child], R, p);
+            links[po] = lump(links[po], links[j.child], R, p);
             for (auto& n : link_order)
                 if (owner[n] == j.child) {
                     owner[n] = po;
@@ -441,7 +477,17 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
         if (b.mass <= 0.0) throw std::runtime_error("moving link '" + j.child + "' has no mass");
         out.bodies.push_back(b);
     }
-    if (out.bodies.empty()) throw std::runtime_error("the model has no moving joints");
+    if (out.floating) {
+        const Link& B = links[base];
+        if (B.mass <= 0.0) throw std::runtime_error("the floating base link '" + base + "' has no mass");
+        out.base_mass = B.mass;
+        out.base_com = B.com;
+        out.base_Ic = {B.I[0], B.I[4], B.I[8], B.I[1], B.I[2], B.I[5]};
+        out.base_shapes = B.shapes;
+    }
+    for (auto& kv : links)
+        if (owner[kv.first] == kv.first) out.unsupported_shapes += kv.second.unsupported;
+    if (out.bodies.empty() && !out.floating) throw std::runtime_error("the model has no moving joints");
     return out;
 }
 

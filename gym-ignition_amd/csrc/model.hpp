@@ -39,9 +39,26 @@ struct ChainBody {
     double effort = 1e300, vel_limit = 1e300;
 };
 
+// A collision shape in its body's frame: box (size = half extents) or sphere
+// (size[0] = radius).  Other URDF geometries are counted, not modelled.
+struct Shape {
+    enum Type : int { Box = 0, Sphere = 1 } type = Box;
+    std::array<double, 3> size{};
+    std::array<double, 9> R{};
+    std::array<double, 3> p{};
+};
+
 struct ChainModel {
     std::string name;              // robot name
     std::string base_link;         // canonical (base) link
+    // floating base: the root link is not attached to "world"; it moves with a
+    // 6-dof free joint (DART FreeJoint) and carries the lumped inertia below
+    bool floating = false;
+    double base_mass = 0.0;
+    std::array<double, 3> base_com{};
+    std::array<double, 6> base_Ic{};   // about the COM: xx yy zz xy xz yz
+    std::vector<Shape> base_shapes;    // collision shapes of the base body
+    int unsupported_shapes = 0;        // collision geometries other than box / sphere
     std::array<double, 9> base_R{};  // base pose in world
     std::array<double, 3> base_p{};
     std::vector<ChainBody> bodies; // depth-first: bodies[i].parent < i (-1 = base)

@@ -22,6 +22,7 @@
 
 #include "baked_models.hpp"
 #include "chain_params.hpp"
+#include "free_body.hpp"
 #include "kernels.hpp"
 #include "model.hpp"
 
@@ -85,6 +86,21 @@ struct mw_sim {
     // [ptgt | pid_e | pid_i | pid_u] on the device; h_ptgt mirrors ptgt
     float* d_aux = nullptr;
     float* h_ptgt = nullptr;
+    // floating single-body models (free_body.hpp)
+    bool floating = false;
+    bool ground = false;          // a ground plane z = 0 is in the world
+    double ground_mu = 1.0;       // SDF <surface><friction><ode><mu> default
+    bool contacts = false;        // Model::enableContacts
+    mw::FreeF h_free{};
+    mw::FreeF* d_free = nullptr;
+    mw::FreeDev fdev{};
+    void* d_fblock = nullptr;     // [base 13 | rpose 7 | rvel 6 | contacts 7*slots][W] f32 + rflag u8 + cmask u32
+    float* h_base = nullptr;      // [13][W] host mirror (pinned)
+    float* h_cdata = nullptr;     // [slots][7][W]
+    uint32_t* h_cmask = nullptr;  // [W]
+    std::vector<float> h_rpose, h_rvel;
+    std::vector<uint8_t> h_rflag;
+    bool free_dirty = false;
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -174,7 +190,67 @@ void build_params(mw_sim* s) {
     P.flags = flags;
 }
 
+// FreeF of a floating single-body model: inertia about the body origin, its
+// 6x6 spatial inverse (fp64 Gauss-Jordan, stored float32), shapes, gravity
+void build_free(mw_sim* s) {
+    mw::FreeF& F = s->h_free;
+    std::memset(&F, 0, sizeof(F));
+    const auto& M = s->model;
+    const double m = M.base_mass, *c = M.base_com.data(), *ic = M.base_Ic.data();
+    F.mass = static_cast<float>(m);
+    for (int k = 0; k < 3; ++k) F.com[k] = static_cast<float>(c[k]);
+    const double c2 = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    const double Io[6] = {ic[0] + m * (c2 - c[0] * c[0]), ic[1] + m * (c2 - c[1] * c[1]), ic[2] + m * (c2 - c[2] * c[2]),
+                          ic[3] - m * c[0] * c[1], ic[4] - m * c[0] * c[2], ic[5] - m * c[1] * c[2]};
+    for (int k = 0; k < 6; ++k) F.Io[k] = static_cast<float>(Io[k]);
+    // spatial inertia [[Io, m[c]x], [m[c]x^T, m 1]] and its inverse
+    double A[6][12] = {};
+    const double Sy[9] = {Io[0], Io[3], Io[4], Io[3], Io[1], Io[5], Io[4], Io[5], Io[2]};
+    const double C[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) {
+            A[r][q] = Sy[r * 3 + q];
+            A[r][q + 3] = m * C[r * 3 + q];
+            A[r + 3][q] = m * C[q * 3 + r];
+            A[r + 3][q + 3] = (r == q) ? m : 0.0;
+        }
+    for (int r = 0; r < 6; ++r) A[r][6 + r] = 1.0;
+    for (int col = 0; col < 6; ++col) {
+        int piv = col;
+        for (int r = col + 1; r < 6; ++r)
+            if (std::fabs(A[r][col]) > std::fabs(A[piv][col])) piv = r;
+        for (int k = 0; k < 12; ++k) std::swap(A[col][k], A[piv][k]);
+        const double d = A[col][col];
+        for (int k = 0; k < 12; ++k) A[col][k] /= d;
+        for (int r = 0; r < 6; ++r)
+            if (r != col) {
+                const double f = A[r][col];
+                for (int k = 0; k < 12; ++k) A[r][k] -= f * A[col][k];
+            }
+    }
+    for (int r = 0; r < 6; ++r)
+        for (int q = 0; q < 6; ++q) F.Minv[r * 6 + q] = static_cast<float>(A[r][6 + q]);
+    for (int k = 0; k < 3; ++k) F.g[k] = static_cast<float>(s->gravity[k]);
+    F.mu = static_cast<float>(s->ground_mu);
+    F.ground = s->ground ? 1 : 0;
+    F.n_shapes = static_cast<int32_t>(M.base_shapes.size());
+    for (size_t i = 0; i < M.base_shapes.size(); ++i) {
+        const mw::Shape& sh = M.base_shapes[i];
+        F.shape_type[i] = sh.type;
+        for (int k = 0; k < 3; ++k) {
+            F.shape_size[i][k] = static_cast<float>(sh.size[k]);
+            F.shape_p[i][k] = static_cast<float>(sh.p[k]);
+        }
+        for (int k = 0; k < 9; ++k) F.shape_R[i][k] = static_cast<float>(sh.R[k]);
+    }
+}
+
 int upload_params(mw_sim* s) {
+    if (s->floating) {
+        build_free(s);
+        MW_HIP(hipMemcpyAsync(s->d_free, &s->h_free, sizeof(mw::FreeF), hipMemcpyHostToDevice, s->stream));
+        return MW_OK;
+    }
     build_params(s);
     MW_HIP(hipMemcpyAsync(s->d_params, &s->h_params, sizeof(mw::ChainF), hipMemcpyHostToDevice, s->stream));
     return MW_OK;
@@ -206,6 +282,13 @@ int baked_id(const mw_sim* s) {
 
 int pull_state(mw_sim* s) {
     if (!s->host_stale) return MW_OK;
+    if (s->floating) {
+        MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * static_cast<size_t>(s->W) * sizeof(float),
+                              hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipStreamSynchronize(s->stream));
+        s->host_stale = false;
+        return MW_OK;
+    }
     MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
     MW_HIP(hipStreamSynchronize(s->stream));
     s->host_stale = false;
@@ -330,6 +413,11 @@ void mw_destroy(mw_sim* s) {
         (void)hipFree(s->d_aux);
         (void)hipHostFree(s->h_block);
         (void)hipHostFree(s->h_ptgt);
+        (void)hipFree(s->d_fblock);
+        (void)hipFree(s->d_free);
+        (void)hipHostFree(s->h_base);
+        (void)hipHostFree(s->h_cdata);
+        (void)hipHostFree(s->h_cmask);
         if (s->own_stream) (void)hipStreamDestroy(s->stream);
     }
     delete s;
@@ -346,6 +434,21 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     }
     if (s->model.dofs() > mw::kMaxKernelDofs || s->model.dofs() > 9)
         return fail(MW_EPARSE, "models with more than 9 dofs are not supported by this build");
+    s->floating = s->model.floating;
+    if (s->floating) {
+        if (s->model.dofs() > 0)
+            return fail(MW_EPARSE, "floating-base models with joints are not compiled into this build yet "
+                                   "(single floating bodies are)");
+        if (s->model.base_shapes.size() > static_cast<size_t>(mw::kMaxFreeShapes))
+            return fail(MW_EPARSE, "a floating body may have at most " + std::to_string(mw::kMaxFreeShapes) +
+                                       " box / sphere collision shapes in this build");
+        s->model_name = (name && *name) ? name : s->model.name;
+        s->loaded = true;
+        s->n = 0;
+        s->pid.clear();
+        build_free(s);
+        return MW_OK;
+    }
     {
         std::vector<int> parents;
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
@@ -390,6 +493,57 @@ int mw_initialize(mw_sim* s) {
         s->stream_set = true;
     }
     s->n = s->model.dofs();
+    if (s->floating) {
+        const size_t W = static_cast<size_t>(s->W);
+        const size_t nf = (13 + 7 + 6 + 7 * mw::kMaxFreeSlots) * W;
+        MW_HIP(hipMalloc(&s->d_fblock, nf * sizeof(float) + W * (1 + sizeof(uint32_t)) + 64));
+        MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_free), sizeof(mw::FreeF)));
+        float* f = static_cast<float*>(s->d_fblock);
+        s->fdev.base = f;
+        s->fdev.rpose = f + 13 * W;
+        s->fdev.rvel = f + 20 * W;
+        s->fdev.cdata = f + 26 * W;
+        s->fdev.cmask = reinterpret_cast<uint32_t*>(f + nf);
+        s->fdev.rflag = reinterpret_cast<uint8_t*>(s->fdev.cmask + W);
+        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_base), 13 * W * sizeof(float), hipHostMallocDefault));
+        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_cdata), 7 * mw::kMaxFreeSlots * W * sizeof(float),
+                             hipHostMallocDefault));
+        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_cmask), W * sizeof(uint32_t), hipHostMallocDefault));
+        std::memset(s->h_cmask, 0, W * sizeof(uint32_t));
+        // the insertion pose; at rest
+        const auto& R = s->model.base_R;
+        double qw, qx, qy, qz;
+        {
+            const double tr = R[0] + R[4] + R[8];
+            if (tr > 0) {
+                const double k = 0.5 / std::sqrt(tr + 1.0);
+                qw = 0.25 / k; qx = (R[7] - R[5]) * k; qy = (R[2] - R[6]) * k; qz = (R[3] - R[1]) * k;
+            } else if (R[0] > R[4] && R[0] > R[8]) {
+                const double k = 2.0 * std::sqrt(1.0 + R[0] - R[4] - R[8]);
+                qw = (R[7] - R[5]) / k; qx = 0.25 * k; qy = (R[1] + R[3]) / k; qz = (R[2] + R[6]) / k;
+            } else if (R[4] > R[8]) {
+                const double k = 2.0 * std::sqrt(1.0 + R[4] - R[0] - R[8]);
+                qw = (R[2] - R[6]) / k; qx = (R[1] + R[3]) / k; qy = 0.25 * k; qz = (R[5] + R[7]) / k;
+            } else {
+                const double k = 2.0 * std::sqrt(1.0 + R[8] - R[0] - R[4]);
+                qw = (R[3] - R[1]) / k; qx = (R[2] + R[6]) / k; qy = (R[5] + R[7]) / k; qz = 0.25 * k;
+            }
+        }
+        const double init[13] = {s->model.base_p[0], s->model.base_p[1], s->model.base_p[2], qw, qx, qy, qz,
+                                 0, 0, 0, 0, 0, 0};
+        for (int f2 = 0; f2 < 13; ++f2)
+            for (size_t w = 0; w < W; ++w) s->h_base[f2 * W + w] = static_cast<float>(init[f2]);
+        MW_HIP(hipMemcpyAsync(s->fdev.base, s->h_base, 13 * W * sizeof(float), hipMemcpyHostToDevice, s->stream));
+        MW_HIP(hipMemsetAsync(s->fdev.cmask, 0, W * (1 + sizeof(uint32_t)), s->stream));
+        s->h_rpose.assign(7 * W, 0.f);
+        s->h_rvel.assign(6 * W, 0.f);
+        s->h_rflag.assign(W, 0);
+        s->initialized = true;
+        int rc = upload_params(s);
+        if (rc) return rc;
+        MW_HIP(hipStreamSynchronize(s->stream));
+        return MW_OK;
+    }
     s->nw = static_cast<size_t>(s->n) * s->W;
     s->state_bytes = 3 * s->nw * sizeof(float);
     s->cmd_off = s->state_bytes;
@@ -441,10 +595,46 @@ int mw_set_stream(mw_sim* s, void* stream) {
     return MW_OK;
 }
 
+static int run_free(mw_sim* s, int paused) {
+    const size_t W = static_cast<size_t>(s->W);
+    if (s->free_dirty) {
+        // pending base resets: one H2D copy of [rpose | rvel] and the flags
+        MW_HIP(hipMemcpyAsync(s->fdev.rpose, s->h_rpose.data(), 7 * W * sizeof(float), hipMemcpyHostToDevice,
+                              s->stream));
+        MW_HIP(hipMemcpyAsync(s->fdev.rvel, s->h_rvel.data(), 6 * W * sizeof(float), hipMemcpyHostToDevice,
+                              s->stream));
+        MW_HIP(hipMemcpyAsync(s->fdev.rflag, s->h_rflag.data(), W, hipMemcpyHostToDevice, s->stream));
+        MW_HIP(hipStreamSynchronize(s->stream));  // the host vectors are reused below
+        std::fill(s->h_rflag.begin(), s->h_rflag.end(), 0);
+        s->free_dirty = false;
+    }
+    mw::RunArgs a{};
+    a.dt = static_cast<float>(s->cfg.step_size);
+    a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
+    a.paused = paused ? 1 : 0;
+    a.pgs_iters = s->cfg.pgs_iters;
+    a.first = 1;
+    a.substeps = paused ? 0 : s->cfg.steps_per_run;
+    MW_HIP(mw::launch_free_run(s->d_free, s->fdev, s->W, a, s->contacts ? 1 : 0, s->stream));
+    MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * W * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    if (s->contacts && !paused) {
+        MW_HIP(hipMemcpyAsync(s->h_cmask, s->fdev.cmask, W * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipMemcpyAsync(s->h_cdata, s->fdev.cdata, 7 * mw::kMaxFreeSlots * W * sizeof(float),
+                              hipMemcpyDeviceToHost, s->stream));
+    }
+    MW_HIP(hipStreamSynchronize(s->stream));
+    if (!paused) {
+        s->iterations += s->cfg.steps_per_run;
+        s->stepped = true;
+    }
+    return MW_OK;
+}
+
 int mw_run(mw_sim* s, int paused) {
     int rc = check_sim(s);
     if (rc) return rc;
     if ((rc = pull_state(s))) return rc;
+    if (s->floating) return run_free(s, paused);
     if (s->cmd_dirty) {
         MW_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_block) + s->cmd_off, s->h_block + s->cmd_off,
                               s->cmd_bytes, hipMemcpyHostToDevice, s->stream));
@@ -821,6 +1011,145 @@ int mw_joint_control_mode(const mw_sim* s, int32_t w, int32_t dof, int32_t* mode
     if (!mode) return fail(MW_EINVAL, "null argument");
     if (w < 0 || w >= s->W || dof < 0 || dof >= s->n) return fail(MW_EINVAL, "index out of range");
     *mode = s->mode[s->idx(dof, w)];
+    return MW_OK;
+}
+
+// ------------------------------------------------- floating bodies ----
+
+static int check_free(const mw_sim* s) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!s->floating) return fail(MW_ESTATE, "the model has a fixed base");
+    return MW_OK;
+}
+
+int mw_is_floating(const mw_sim* s, int32_t* floating) {
+    if (!s || !floating) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    *floating = s->floating ? 1 : 0;
+    return MW_OK;
+}
+
+static float* base_at(const mw_sim* s, int f, int w) { return s->h_base + static_cast<size_t>(f) * s->W + w; }
+
+int mw_get_base_pose(const mw_sim* cs, int32_t w0, int32_t nw, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    int rc = check_free(s);
+    if (rc) return rc;
+    if (!out || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null output");
+    if ((rc = pull_state(s))) return rc;
+    // Model::basePosition / baseOrientation (Model.cpp:976-994): x y z, qw qx qy qz
+    for (int32_t k = 0; k < nw; ++k)
+        for (int f = 0; f < 7; ++f) out[7 * k + f] = *base_at(s, f, w0 + k);
+    return MW_OK;
+}
+
+int mw_get_base_velocity(const mw_sim* cs, int32_t w0, int32_t nw, double* out) {
+    mw_sim* s = const_cast<mw_sim*>(cs);
+    int rc = check_free(s);
+    if (rc) return rc;
+    if (!out || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null output");
+    if ((rc = pull_state(s))) return rc;
+    // Model::baseWorldLinearVelocity / baseWorldAngularVelocity (Model.cpp:1024-1075):
+    // the body-frame twist rotated into the world frame
+    for (int32_t k = 0; k < nw; ++k) {
+        const int w = w0 + k;
+        const double qw = *base_at(s, 3, w), qx = *base_at(s, 4, w), qy = *base_at(s, 5, w), qz = *base_at(s, 6, w);
+        const double R[9] = {1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy - qw * qz), 2 * (qx * qz + qw * qy),
+                             2 * (qx * qy + qw * qz), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz - qw * qx),
+                             2 * (qx * qz - qw * qy), 2 * (qy * qz + qw * qx), 1 - 2 * (qx * qx + qy * qy)};
+        const double wb[3] = {*base_at(s, 7, w), *base_at(s, 8, w), *base_at(s, 9, w)};
+        const double vb[3] = {*base_at(s, 10, w), *base_at(s, 11, w), *base_at(s, 12, w)};
+        for (int r = 0; r < 3; ++r) {
+            out[6 * k + r] = R[r * 3] * vb[0] + R[r * 3 + 1] * vb[1] + R[r * 3 + 2] * vb[2];
+            out[6 * k + 3 + r] = R[r * 3] * wb[0] + R[r * 3 + 1] * wb[1] + R[r * 3 + 2] * wb[2];
+        }
+    }
+    return MW_OK;
+}
+
+int mw_reset_base_pose(mw_sim* s, int32_t w0, int32_t nw, const double* in) {
+    int rc = check_free(s);
+    if (rc) return rc;
+    if (!in || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null input");
+    // Model::resetBasePose (Model.cpp:256-289): WorldPoseCmd, applied by the next run
+    for (int32_t k = 0; k < nw; ++k) {
+        const double* v = in + 7 * k;
+        const double qn = std::sqrt(v[3] * v[3] + v[4] * v[4] + v[5] * v[5] + v[6] * v[6]);
+        if (!(qn > 0.0)) return fail(MW_EINVAL, "the base orientation quaternion is zero");
+    }
+    const size_t W = static_cast<size_t>(s->W);
+    for (int32_t k = 0; k < nw; ++k) {
+        for (int f = 0; f < 7; ++f) s->h_rpose[f * W + w0 + k] = static_cast<float>(in[7 * k + f]);
+        s->h_rflag[w0 + k] |= 1u;
+    }
+    s->free_dirty = true;
+    return MW_OK;
+}
+
+int mw_reset_base_velocity(mw_sim* s, int32_t w0, int32_t nw, const double* in) {
+    int rc = check_free(s);
+    if (rc) return rc;
+    if (!in || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null input");
+    // Model::resetBaseWorldVelocity (Model.cpp:343-400): WorldVelocityCmd
+    const size_t W = static_cast<size_t>(s->W);
+    for (int32_t k = 0; k < nw; ++k) {
+        for (int f = 0; f < 6; ++f) s->h_rvel[f * W + w0 + k] = static_cast<float>(in[6 * k + f]);
+        s->h_rflag[w0 + k] |= 2u;
+    }
+    s->free_dirty = true;
+    return MW_OK;
+}
+
+int mw_set_ground_plane(mw_sim* s, int32_t enabled, double mu) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    if (!(mu >= 0.0)) return fail(MW_EINVAL, "the friction coefficient must be >= 0");
+    s->ground = enabled != 0;
+    s->ground_mu = mu;
+    if (s->floating && s->initialized) return upload_params(s);
+    if (s->floating && s->loaded) build_free(s);
+    return MW_OK;
+}
+
+int mw_enable_contacts(mw_sim* s, int32_t enable) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    // Model::enableContacts (Model.cpp:686-700)
+    s->contacts = enable != 0;
+    if (!s->contacts && s->h_cmask) std::memset(s->h_cmask, 0, static_cast<size_t>(s->W) * sizeof(uint32_t));
+    return MW_OK;
+}
+
+int mw_contacts_enabled(const mw_sim* s, int32_t* enabled) {
+    if (!s || !enabled) return fail(MW_EINVAL, "null argument");
+    *enabled = s->contacts ? 1 : 0;
+    return MW_OK;
+}
+
+int mw_get_contacts(const mw_sim* s, int32_t w, double* out, int32_t cap, int32_t* n) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!n || (cap > 0 && !out)) return fail(MW_EINVAL, "null argument");
+    if (w < 0 || w >= s->W) return fail(MW_EINVAL, "world index out of range");
+    *n = 0;
+    if (!s->floating || !s->contacts) return MW_OK;
+    // contacts of the last substep of the last run (Physics.cpp:2351-2540): per
+    // point x y z, normal (into the body), force on the body (N), depth
+    const size_t W = static_cast<size_t>(s->W);
+    const uint32_t mask = s->h_cmask[w];
+    int32_t k = 0;
+    for (int slot = 0; slot < mw::kMaxFreeSlots; ++slot) {
+        if (!((mask >> slot) & 1u)) continue;
+        if (k < cap) {
+            const float* c = s->h_cdata + static_cast<size_t>(slot) * 7 * W + w;
+            double* o = out + 10 * k;
+            o[0] = c[0]; o[1] = c[W]; o[2] = c[2 * W];
+            o[3] = 0.0; o[4] = 0.0; o[5] = 1.0;
+            o[6] = c[3 * W]; o[7] = c[4 * W]; o[8] = c[5 * W];
+            o[9] = c[6 * W];
+        }
+        ++k;
+    }
+    *n = k;
     return MW_OK;
 }
 

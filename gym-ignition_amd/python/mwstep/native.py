@@ -114,6 +114,15 @@ SIGNATURES = [
     ("mw_joint_pid", ctypes.c_int, [_P, _I, _D]),
     ("mw_set_controller_period", ctypes.c_int, [_P, ctypes.c_double]),
     ("mw_controller_period", ctypes.c_int, [_P, _D]),
+    ("mw_is_floating", ctypes.c_int, [_P, _IP]),
+    ("mw_get_base_pose", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_get_base_velocity", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_reset_base_pose", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_reset_base_velocity", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_set_ground_plane", ctypes.c_int, [_P, _I, ctypes.c_double]),
+    ("mw_enable_contacts", ctypes.c_int, [_P, _I]),
+    ("mw_contacts_enabled", ctypes.c_int, [_P, _IP]),
+    ("mw_get_contacts", ctypes.c_int, [_P, _I, _D, _I, _IP]),
     ("mw_device_ptr", ctypes.c_int, [_P, _S, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("mw_vecenv_create", ctypes.c_int, [_P, ctypes.POINTER(MwTaskConfig), ctypes.POINTER(_P)]),

@@ -180,6 +180,56 @@ class Simulator:
         N.check(N.lib().mw_controller_period(self.handle, ctypes.byref(v)))
         return v.value
 
+    # -- floating single bodies (mwstep.h: floating bases)
+    @property
+    def floating(self) -> bool:
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_is_floating(self.handle, ctypes.byref(v)))
+        return bool(v.value)
+
+    def base_pose(self, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        """[nw, 7]: x y z qw qx qy qz."""
+        nw = self.n_worlds - w0 if nw is None else nw
+        out = np.zeros((nw, 7))
+        N.check(N.lib().mw_get_base_pose(self.handle, w0, nw, N.dptr(out)), "base_pose")
+        return out
+
+    def base_velocity(self, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        """[nw, 6]: world linear xyz (base origin), world angular xyz."""
+        nw = self.n_worlds - w0 if nw is None else nw
+        out = np.zeros((nw, 6))
+        N.check(N.lib().mw_get_base_velocity(self.handle, w0, nw, N.dptr(out)), "base_velocity")
+        return out
+
+    def reset_base_pose(self, pose, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(pose, dtype=np.float64), (nw, 7)))
+        N.check(N.lib().mw_reset_base_pose(self.handle, w0, nw, N.dptr(v)), "reset_base_pose")
+
+    def reset_base_velocity(self, lin_ang, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(lin_ang, dtype=np.float64), (nw, 6)))
+        N.check(N.lib().mw_reset_base_velocity(self.handle, w0, nw, N.dptr(v)), "reset_base_velocity")
+
+    def set_ground_plane(self, enabled: bool, mu: float = 1.0) -> None:
+        N.check(N.lib().mw_set_ground_plane(self.handle, 1 if enabled else 0, float(mu)), "set_ground_plane")
+
+    def enable_contacts(self, enable: bool = True) -> None:
+        N.check(N.lib().mw_enable_contacts(self.handle, 1 if enable else 0))
+
+    def contacts_enabled(self) -> bool:
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_contacts_enabled(self.handle, ctypes.byref(v)))
+        return bool(v.value)
+
+    def contacts(self, w: int = 0) -> np.ndarray:
+        """[n, 10]: point xyz, normal xyz, force on the body xyz, depth."""
+        cap = 64
+        out = np.zeros((cap, 10))
+        n = ctypes.c_int32()
+        N.check(N.lib().mw_get_contacts(self.handle, w, N.dptr(out), cap, ctypes.byref(n)), "contacts")
+        return out[:min(n.value, cap)].copy()
+
     def export_model(self) -> np.ndarray:
         out = np.zeros(34 * self.dofs + 3)
         N.check(N.lib().mw_model_export(self.handle, N.dptr(out), len(out)))

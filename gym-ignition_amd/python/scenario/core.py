@@ -93,6 +93,28 @@ class PID:
 DEFAULT_PID = PID.from_list([1.0, 0.1, 0.01, 0.0, -1.0, 0.0, 0.0, -1.0])
 
 
+class ContactPoint:
+    """scenario::core::ContactPoint (Link.h / utils.h): world-frame point,
+    normal, force and torque on the body, penetration depth."""
+
+    def __init__(self, position=(0.0, 0.0, 0.0), normal=(0.0, 0.0, 0.0), force=(0.0, 0.0, 0.0),
+                 torque=(0.0, 0.0, 0.0), depth: float = 0.0):
+        self.position = [float(x) for x in position]
+        self.normal = [float(x) for x in normal]
+        self.force = [float(x) for x in force]
+        self.torque = [float(x) for x in torque]
+        self.depth = float(depth)
+
+
+class Contact:
+    """scenario::core::Contact: the points between two bodies (scoped link names)."""
+
+    def __init__(self, body_a: str = "", body_b: str = "", points=()):
+        self.body_a = body_a
+        self.body_b = body_b
+        self.points = list(points)
+
+
 def __getattr__(name):
     # The abstract core interfaces are the gazebo classes themselves in this
     # build; `to_gazebo()` on any of them returns the same object.

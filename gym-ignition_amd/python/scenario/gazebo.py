@@ -286,6 +286,7 @@ class Model:
         self._sim = sim
         self._pose = pose
         self._joints = {n: Joint(self, i, n) for i, n in enumerate(sim.joint_names)}
+        self._pending_vel = None
         self._history: Optional[collections.deque] = None
 
     # -- identity
@@ -316,10 +317,109 @@ class Model:
         return self._sim.base_frame
 
     def base_position(self) -> List[float]:
+        # Model::basePosition (Model.cpp:976-984); a fixed base stays at its insertion pose
+        if self._sim.floating:
+            return self._sim.base_pose()[0, :3].tolist()
         return list(self._pose.position)
 
     def base_orientation(self) -> List[float]:
+        # Model::baseOrientation (Model.cpp:986-994), wxyz
+        if self._sim.floating:
+            return self._sim.base_pose()[0, 3:].tolist()
         return list(self._pose.orientation)
+
+    def base_world_linear_velocity(self) -> List[float]:
+        return self._sim.base_velocity()[0, :3].tolist() if self._sim.floating else [0.0, 0.0, 0.0]
+
+    def base_world_angular_velocity(self) -> List[float]:
+        return self._sim.base_velocity()[0, 3:].tolist() if self._sim.floating else [0.0, 0.0, 0.0]
+
+    def _base_R(self) -> np.ndarray:
+        w, x, y, z = self.base_orientation()
+        return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                         [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                         [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+    def base_body_linear_velocity(self) -> List[float]:
+        # Model::baseBodyLinearVelocity (Model.cpp:996-1008)
+        return (self._base_R().T @ np.array(self.base_world_linear_velocity())).tolist()
+
+    def base_body_angular_velocity(self) -> List[float]:
+        return (self._base_R().T @ np.array(self.base_world_angular_velocity())).tolist()
+
+    def _floating_only(self, what: str) -> bool:
+        if not self._sim.floating:
+            _err(f"{what}: the model '{self._name}' has a fixed base")
+            return False
+        return True
+
+    def reset_base_pose(self, position: Sequence[float], orientation: Sequence[float]) -> bool:
+        # Model::resetBasePose (Model.cpp:256-289): applied by the next run
+        if not self._floating_only("reset_base_pose"):
+            return False
+        if len(position) != 3 or len(orientation) != 4:
+            _err("Wrong size of the base pose")
+            return False
+        try:
+            self._sim.reset_base_pose(list(position) + list(orientation))
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
+    def reset_base_position(self, position: Sequence[float]) -> bool:
+        # Model.cpp:291-294: with the CURRENT orientation
+        return self.reset_base_pose(position, self.base_orientation())
+
+    def reset_base_orientation(self, orientation: Sequence[float]) -> bool:
+        # Model.cpp:296-299: with the CURRENT position
+        return self.reset_base_pose(self.base_position(), orientation)
+
+    def reset_base_world_velocity(self, linear: Sequence[float], angular: Sequence[float]) -> bool:
+        # Model::resetBaseWorldVelocity (Model.cpp:343-400)
+        if not self._floating_only("reset_base_world_velocity"):
+            return False
+        try:
+            self._sim.reset_base_velocity(list(linear) + list(angular))
+            self._pending_vel = (list(linear), list(angular))
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
+    def reset_base_world_linear_velocity(self, linear: Sequence[float]) -> bool:
+        # Model.cpp:301-320: keeps an angular velocity already reset in this run
+        angular = self._pending_vel[1] if self._pending_vel else self.base_world_angular_velocity()
+        return self.reset_base_world_velocity(linear, angular)
+
+    def reset_base_world_angular_velocity(self, angular: Sequence[float]) -> bool:
+        linear = self._pending_vel[0] if self._pending_vel else self.base_world_linear_velocity()
+        return self.reset_base_world_velocity(linear, angular)
+
+    # -- links and contacts (the floating base link; Link.cpp)
+    def link_names(self, scoped: bool = False) -> List[str]:
+        base = self._sim.base_frame
+        return [f"{self._name}::{base}" if scoped else base]
+
+    def get_link(self, link_name: str) -> "Link":
+        if link_name != self._sim.base_frame:
+            raise RuntimeError(f"Link '{link_name}' not available in model '{self._name}' "
+                               "(this build exposes the base link)")
+        return Link(self, link_name)
+
+    def links(self, link_names: Sequence[str] = ()) -> List["Link"]:
+        return [self.get_link(n) for n in (link_names or self.link_names())]
+
+    def contacts_enabled(self) -> bool:
+        return self._sim.contacts_enabled()
+
+    def enable_contacts(self, enable: bool = True) -> bool:
+        # Model::enableContacts (Model.cpp:686-700)
+        self._sim.enable_contacts(enable)
+        return True
+
+    def contacts(self) -> List[core.Contact]:
+        return Link(self, self._sim.base_frame).contacts()
 
     def controller_period(self) -> float:
         # Model::controllerPeriod (Model.cpp:581-587)
@@ -427,11 +527,72 @@ class Model:
         if self._history is not None and not paused:
             self._history.extend(self._get("force_target", None).tolist())
         self._sim.run(paused)
+        self._pending_vel = None
 
     def _close(self) -> None:
         if self._sim is not None:
             self._sim.close()
             self._sim = None
+
+
+class Link:
+    """The base link of a model (Link.cpp): pose, velocity and contacts."""
+
+    def __init__(self, model: "Model", name: str):
+        self._model = model
+        self._name = name
+
+    def to_gazebo(self) -> "Link":
+        return self
+
+    def name(self, scoped: bool = False) -> str:
+        return f"{self._model.name()}::{self._name}" if scoped else self._name
+
+    def position(self) -> List[float]:
+        return self._model.base_position()
+
+    def orientation(self) -> List[float]:
+        return self._model.base_orientation()
+
+    def world_linear_velocity(self) -> List[float]:
+        return self._model.base_world_linear_velocity()
+
+    def world_angular_velocity(self) -> List[float]:
+        return self._model.base_world_angular_velocity()
+
+    def contacts_enabled(self) -> bool:
+        return self._model.contacts_enabled()
+
+    def enable_contact_detection(self, enable: bool) -> bool:
+        return self._model.enable_contacts(enable)
+
+    def contacts(self) -> List[core.Contact]:
+        # Link::contacts (Link.cpp:365-434): the points of one body pair are
+        # merged into one Contact; the ground plane is the only other body here
+        sim = self._model._sim
+        if not sim.contacts_enabled():
+            return []
+        rows = sim.contacts(0)
+        if len(rows) == 0:
+            return []
+        ground = self._model._world._ground_name or "ground_plane::link"
+        pts = [core.ContactPoint(r[0:3], r[3:6], r[6:9], (0.0, 0.0, 0.0), r[9]) for r in rows]
+        return [core.Contact(self.name(scoped=True), ground, pts)]
+
+    def in_contact(self) -> bool:
+        return len(self.contacts()) > 0
+
+    def contact_wrench(self) -> List[float]:
+        # Link::contactWrench (Link.cpp:436-482): sum of forces and of (p - o_L) x f
+        o = np.array(self.position())
+        f = np.zeros(3)
+        t = np.zeros(3)
+        for c in self.contacts():
+            for p in c.points:
+                fp = np.array(p.force)
+                f += fp
+                t += np.cross(np.array(p.position) - o, fp)
+        return np.concatenate([f, t]).tolist()
 
 
 class StaticModel:
@@ -478,6 +639,8 @@ class World:
         self._physics = False
         self._time_ns = 0
         self._gravity = [0.0, 0.0, -9.8]
+        self._ground_mu = None     # a static model with a plane collision is in the world
+        self._ground_name = None
 
     def to_gazebo(self) -> "World":
         return self
@@ -565,6 +728,16 @@ class World:
                 _err("only static SDF models and URDF robots are supported by this build")
                 return False
             self._models[name] = StaticModel(name, pose)
+            plane = root.find("model/link/collision/geometry/plane")
+            if plane is not None:
+                # the ground plane of the world: floating bodies collide with it
+                mu_el = root.find("model/link/collision/surface/friction/ode/mu")
+                self._ground_mu = float(mu_el.text) if mu_el is not None else 1.0
+                link = root.find("model/link")
+                self._ground_name = f"{name}::{link.get('name', 'link')}"
+                for m in self._models.values():
+                    if isinstance(m, Model):
+                        m._sim.set_ground_plane(True, self._ground_mu)
             return True
         from mwstep.sim import Simulator
         sim_cfg = self._simulator
@@ -576,6 +749,8 @@ class World:
         except RuntimeError as e:
             _err(f"Failed to insert model '{name}': {e}")
             return False
+        if self._ground_mu is not None:
+            sim.set_ground_plane(True, self._ground_mu)
         self._models[name] = Model(self, name, sim, pose)
         return True
 
@@ -583,7 +758,13 @@ class World:
         if model_name not in self._models:
             _err(f"Model '{model_name}' not found in world '{self._name}'")
             return False
-        self._models.pop(model_name)._close()
+        removed = self._models.pop(model_name)
+        removed._close()
+        if self._ground_name is not None and self._ground_name.split("::")[0] == model_name:
+            self._ground_mu = self._ground_name = None
+            for m in self._models.values():
+                if isinstance(m, Model):
+                    m._sim.set_ground_plane(False)
         return True
 
     # called by GazeboSimulator.run

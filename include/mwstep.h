@@ -158,6 +158,29 @@ int mw_joint_pid(const mw_sim* sim, int32_t dof, double gains[8]);
 int mw_set_controller_period(mw_sim* sim, double period);
 int mw_controller_period(const mw_sim* sim, double* period);
 
+/* ---- floating bases (root link not attached to "world"; this build steps
+ * single floating bodies: DART FreeJoint dynamics, box / sphere collision
+ * shapes against a ground plane z = 0, contact LCP with friction) ---- */
+int mw_is_floating(const mw_sim* sim, int32_t* floating);
+/* Model::basePosition / baseOrientation: out [nw][7] = x y z qw qx qy qz. */
+int mw_get_base_pose(const mw_sim* sim, int32_t w0, int32_t nw, double* out);
+/* Model::baseWorldLinearVelocity / baseWorldAngularVelocity: out [nw][6] =
+ * linear xyz (base origin), angular xyz, world frame. */
+int mw_get_base_velocity(const mw_sim* sim, int32_t w0, int32_t nw, double* out);
+/* Model::resetBasePose / resetBaseWorldVelocity (Model.cpp:256-400): applied by
+ * the next run (pose first, then the velocity). */
+int mw_reset_base_pose(mw_sim* sim, int32_t w0, int32_t nw, const double* pose);
+int mw_reset_base_velocity(mw_sim* sim, int32_t w0, int32_t nw, const double* lin_ang);
+/* The world's ground plane (z = 0, normal +z) and its friction coefficient. */
+int mw_set_ground_plane(mw_sim* sim, int32_t enabled, double mu);
+/* Model::enableContacts / contactsEnabled (Model.cpp:674-700). */
+int mw_enable_contacts(mw_sim* sim, int32_t enable);
+int mw_contacts_enabled(const mw_sim* sim, int32_t* enabled);
+/* Contacts of world w after the last run (Physics.cpp:2351-2540): up to cap
+ * rows of 10 doubles = point xyz, normal xyz (into the body), force on the
+ * body xyz (N), penetration depth; *n = number of contact points. */
+int mw_get_contacts(const mw_sim* sim, int32_t w, double* out, int32_t cap, int32_t* n);
+
 /* Zero-copy device views, float32 [n_dofs][n_worlds] (world index fastest):
  * the SoA state "q", "qd", "qdd", and "position_target" (the Position-mode
  * targets; after the view is taken, writes through it drive the next runs

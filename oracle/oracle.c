@@ -495,6 +495,231 @@ int or_step(const or_model* m, double dt, double* q, double* qd,
     return nr;
 }
 
+/* ---------------- free body + ground contacts ---------------- */
+
+/* DART 6 ContactConstraint defaults [EXT, restated, parity unpinned]:
+ * error-reduction parameter 0.01, max error-reduction velocity 1e-3,
+ * constraint force mixing 1e-5, error allowance 0, restitution 0; friction
+ * is a pyramid over the two ODE plane-space tangents (dPlaneSpace), each
+ * bounded by mu times the normal impulse ("findex"). */
+#define OR_C_ERP 0.01
+#define OR_C_MAX_ERV 1e-3
+#define OR_C_CFM 1e-5
+
+/* exp of se(3) (DART math::expMap): R = Rodrigues(phi), t = V(phi) u with
+ * V = 1 + (1 - cos th)/th^2 [phi]x + (th - sin th)/th^3 [phi]x^2 */
+static void se3_exp(const double phi[3], const double u[3], double R[9], double t[3])
+{
+    const double th2 = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+    const double th = sqrt(th2);
+    double a, b, c; /* R = 1 + a K + b K^2,  V = 1 + b K + c K^2 */
+    if (th < 1e-8) {
+        a = 1.0 - th2 / 6.0;
+        b = 0.5 - th2 / 24.0;
+        c = 1.0 / 6.0 - th2 / 120.0;
+    } else {
+        a = sin(th) / th;
+        b = (1.0 - cos(th)) / th2;
+        c = (th - sin(th)) / (th2 * th);
+    }
+    const double K[9] = {0, -phi[2], phi[1], phi[2], 0, -phi[0], -phi[1], phi[0], 0};
+    double K2[9];
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) {
+            double acc = 0.0;
+            for (int k = 0; k < 3; ++k) acc += K[r * 3 + k] * K[k * 3 + q];
+            K2[r * 3 + q] = acc;
+        }
+    for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * K[k] + b * K2[k];
+    for (int r = 0; r < 3; ++r) {
+        double acc = u[r];
+        for (int k = 0; k < 3; ++k) acc += (b * K[r * 3 + k] + c * K2[r * 3 + k]) * u[k];
+        t[r] = acc;
+    }
+}
+
+/* ODE dPlaneSpace: two unit vectors spanning the plane orthogonal to n */
+static void plane_space(const double n[3], double p[3], double q[3])
+{
+    if (fabs(n[2]) > 0.7071067811865476) {
+        const double a = n[1] * n[1] + n[2] * n[2], k = 1.0 / sqrt(a);
+        p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
+        q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
+    } else {
+        const double a = n[0] * n[0] + n[1] * n[1], k = 1.0 / sqrt(a);
+        p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
+        q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
+    }
+}
+
+/* solve the 6x6 SPD system A x = b (Gaussian elimination, partial pivoting) */
+static void solve6(const double* A_in, const double* b, double* x)
+{
+    double A[36], y[6];
+    memcpy(A, A_in, sizeof A);
+    memcpy(y, b, sizeof y);
+    for (int c = 0; c < 6; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < 6; ++r)
+            if (fabs(A[r * 6 + c]) > fabs(A[piv * 6 + c])) piv = r;
+        if (piv != c) {
+            for (int k = 0; k < 6; ++k) { double t = A[c * 6 + k]; A[c * 6 + k] = A[piv * 6 + k]; A[piv * 6 + k] = t; }
+            double t = y[c]; y[c] = y[piv]; y[piv] = t;
+        }
+        for (int r = c + 1; r < 6; ++r) {
+            const double f = A[r * 6 + c] / A[c * 6 + c];
+            for (int k = c; k < 6; ++k) A[r * 6 + k] -= f * A[c * 6 + k];
+            y[r] -= f * y[c];
+        }
+    }
+    for (int r = 5; r >= 0; --r) {
+        double acc = y[r];
+        for (int k = r + 1; k < 6; ++k) acc -= A[r * 6 + k] * x[k];
+        x[r] = acc / A[r * 6 + r];
+    }
+}
+
+int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_iters,
+                 double* c_pos, double* c_normal, double* c_force, double* c_depth)
+{
+    /* spatial inertia about the body origin, [angular; linear] */
+    double I[36];
+    {
+        const double ms = m->mass, *c = m->com, *ic = m->Ic;
+        const double Icm[9] = {ic[0], ic[3], ic[4], ic[3], ic[1], ic[5], ic[4], ic[5], ic[2]};
+        const double C[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+        m6_zero(I);
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) {
+                double cc = 0.0;
+                for (int j = 0; j < 3; ++j) cc -= C[r * 3 + j] * C[j * 3 + k];
+                I[r * 6 + k] = Icm[r * 3 + k] + ms * cc;
+                I[r * 6 + k + 3] = ms * C[r * 3 + k];
+                I[(r + 3) * 6 + k] = -ms * C[r * 3 + k];
+                I[(r + 3) * 6 + k + 3] = (r == k) ? ms : 0.0;
+            }
+    }
+    const double* R = s->R;
+    double V[6] = {s->w[0], s->w[1], s->w[2], s->v[0], s->v[1], s->v[2]};
+    /* forward dynamics (FreeJoint = ABA on one body): I a = dad(V, I V) + I [0; g_b] */
+    double gb[3], IV[6], dd[6], ga[6] = {0}, Ig[6], f[6], a[6];
+    for (int r = 0; r < 3; ++r) gb[r] = R[r] * m->gravity[0] + R[3 + r] * m->gravity[1] + R[6 + r] * m->gravity[2];
+    m6_vec(I, V, IV);
+    sp_dad(V, IV, dd);
+    ga[3] = gb[0]; ga[4] = gb[1]; ga[5] = gb[2];
+    m6_vec(I, ga, Ig);
+    for (int k = 0; k < 6; ++k) f[k] = dd[k] + Ig[k];
+    solve6(I, f, a);
+    for (int k = 0; k < 6; ++k) V[k] += dt * a[k];
+
+    /* collision detection against the ground plane z = 0 (positions of the
+     * start of the step, velocities after integrateVelocities) */
+    int nc = 0;
+    double cb[OR_MAXCONTACTS][3], depth[OR_MAXCONTACTS], cw[OR_MAXCONTACTS][3];
+    if (m->ground) {
+        for (int k = 0; k < m->n_shapes; ++k) {
+            const double* h = m->shape_size[k];
+            const double* SR = m->shape_R[k];
+            const double* sp = m->shape_p[k];
+            if (m->shape_type[k] == 0) {
+                for (int corner = 0; corner < 8; ++corner) {
+                    const double l[3] = {(corner & 4) ? h[0] : -h[0], (corner & 2) ? h[1] : -h[1],
+                                         (corner & 1) ? h[2] : -h[2]};
+                    double b[3], x[3];
+                    for (int r = 0; r < 3; ++r) b[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
+                    for (int r = 0; r < 3; ++r) x[r] = s->p[r] + R[r * 3] * b[0] + R[r * 3 + 1] * b[1] + R[r * 3 + 2] * b[2];
+                    if (x[2] < 0.0) {
+                        memcpy(cb[nc], b, sizeof b);
+                        memcpy(cw[nc], x, sizeof x);
+                        depth[nc] = -x[2];
+                        ++nc;
+                    }
+                }
+            } else {
+                double x[3];
+                for (int r = 0; r < 3; ++r) x[r] = s->p[r] + R[r * 3] * sp[0] + R[r * 3 + 1] * sp[1] + R[r * 3 + 2] * sp[2];
+                if (x[2] - h[0] < 0.0) {
+                    /* lowest point of the sphere */
+                    double xw[3] = {x[0], x[1], x[2] - h[0]}, d[3], bb[3];
+                    for (int r = 0; r < 3; ++r) d[r] = xw[r] - s->p[r];
+                    for (int r = 0; r < 3; ++r) bb[r] = R[r] * d[0] + R[3 + r] * d[1] + R[6 + r] * d[2];
+                    memcpy(cb[nc], bb, sizeof bb);
+                    memcpy(cw[nc], xw, sizeof xw);
+                    depth[nc] = h[0] - x[2];
+                    ++nc;
+                }
+            }
+        }
+    }
+
+    double x[3 * OR_MAXCONTACTS];
+    const double n[3] = {0, 0, 1};
+    double t1[3], t2[3];
+    plane_space(n, t1, t2);
+    if (nc > 0) {
+        /* rows: (normal, t1, t2) per contact; J = [c x d_b; d_b] in the body frame */
+        const int nr = 3 * nc;
+        double J[3 * OR_MAXCONTACTS][6], MJ[3 * OR_MAXCONTACTS][6], b[3 * OR_MAXCONTACTS];
+        for (int i = 0; i < nc; ++i)
+            for (int d = 0; d < 3; ++d) {
+                const double* dw = (d == 0) ? n : (d == 1 ? t1 : t2);
+                double db[3];
+                for (int r = 0; r < 3; ++r) db[r] = R[r] * dw[0] + R[3 + r] * dw[1] + R[6 + r] * dw[2];
+                double* Jr = J[3 * i + d];
+                cross3(cb[i], db, Jr);
+                Jr[3] = db[0]; Jr[4] = db[1]; Jr[5] = db[2];
+                solve6(I, Jr, MJ[3 * i + d]);
+                const double vrel = dot6(Jr, V);
+                double bounce = 0.0;
+                if (d == 0) {
+                    bounce = OR_C_ERP * depth[i] / dt;
+                    if (bounce > OR_C_MAX_ERV) bounce = OR_C_MAX_ERV;
+                }
+                b[3 * i + d] = -vrel + bounce;
+            }
+        double A[3 * OR_MAXCONTACTS][3 * OR_MAXCONTACTS];
+        for (int r = 0; r < nr; ++r)
+            for (int c = 0; c < nr; ++c) A[r][c] = dot6(J[r], MJ[c]);
+        for (int r = 0; r < nr; ++r) { A[r][r] *= (1.0 + OR_C_CFM); x[r] = 0.0; }
+        for (int it = 0; it < pgs_iters; ++it)
+            for (int r = 0; r < nr; ++r) {
+                double acc = b[r];
+                for (int c = 0; c < nr; ++c) acc -= A[r][c] * x[c];
+                double v = x[r] + acc / A[r][r];
+                double lo, hi;
+                if (r % 3 == 0) { lo = 0.0; hi = INFINITY; }
+                else { hi = m->mu * x[r - r % 3]; lo = -hi; }
+                if (v < lo) v = lo;
+                if (v > hi) v = hi;
+                x[r] = v;
+            }
+        for (int r = 0; r < nr; ++r)
+            for (int k = 0; k < 6; ++k) V[k] += MJ[r][k] * x[r];
+    }
+
+    /* integratePositions: T <- T exp(dt V) */
+    double phi[3] = {dt * V[0], dt * V[1], dt * V[2]}, u[3] = {dt * V[3], dt * V[4], dt * V[5]};
+    double dR[9], dp[3], Rn[9];
+    se3_exp(phi, u, dR, dp);
+    for (int r = 0; r < 3; ++r) {
+        s->p[r] += R[r * 3] * dp[0] + R[r * 3 + 1] * dp[1] + R[r * 3 + 2] * dp[2];
+        for (int q = 0; q < 3; ++q)
+            Rn[r * 3 + q] = R[r * 3] * dR[q] + R[r * 3 + 1] * dR[3 + q] + R[r * 3 + 2] * dR[6 + q];
+    }
+    memcpy(s->R, Rn, sizeof Rn);
+    for (int k = 0; k < 3; ++k) { s->w[k] = V[k]; s->v[k] = V[3 + k]; }
+
+    for (int i = 0; i < nc; ++i) {
+        for (int r = 0; r < 3; ++r) {
+            if (c_pos) c_pos[3 * i + r] = cw[i][r];
+            if (c_normal) c_normal[3 * i + r] = n[r];
+            if (c_force) c_force[3 * i + r] = (n[r] * x[3 * i] + t1[r] * x[3 * i + 1] + t2[r] * x[3 * i + 2]) / dt;
+        }
+        if (c_depth) c_depth[i] = depth[i];
+    }
+    return nc;
+}
+
 /* ---------------- joint PID (ign-math 6 PID, [EXT]) ---------------- */
 
 /* ignition::math::PID::Update restated [EXT: ign-math6 src/PID.cc, not

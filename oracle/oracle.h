@@ -95,6 +95,40 @@ typedef struct {
 double or_pid_update(const or_pid_gains* g, or_pid_state* s, double err, double dt);
 
 /* ------------------------------------------------------------------ */
+/* Floating rigid body with ground-plane contacts (DART FreeJoint +     */
+/* ContactConstraint [EXT], Physics.cpp:2351-2540 contact readback).    */
+/* ------------------------------------------------------------------ */
+#define OR_MAXSHAPES 8
+#define OR_MAXCONTACTS (8 * OR_MAXSHAPES)
+
+typedef struct {
+    double mass;
+    double com[3];              /* body frame                                */
+    double Ic[6];               /* about the COM: xx yy zz xy xz yz          */
+    int32_t n_shapes;
+    int32_t ground;             /* 1: ground plane z = 0, normal +z           */
+    int32_t shape_type[OR_MAXSHAPES];   /* 0 box (size = half extents), 1 sphere */
+    double shape_size[OR_MAXSHAPES][3];
+    double shape_R[OR_MAXSHAPES][9];    /* shape pose in the body frame          */
+    double shape_p[OR_MAXSHAPES][3];
+    double gravity[3];          /* world frame                                */
+    double mu;                  /* Coulomb friction with the ground           */
+} or_free_model;
+
+typedef struct {
+    double p[3];                /* body origin, world frame                   */
+    double R[9];                /* body orientation (row-major)               */
+    double w[3];                /* angular velocity, BODY frame (FreeJoint)   */
+    double v[3];                /* linear velocity of the origin, BODY frame  */
+} or_free_state;
+
+/* One engine step of a free body.  Contacts (world frame, force acting on
+ * the body, impulse / dt) are written to c_* (capacity OR_MAXCONTACTS);
+ * returns their number. */
+int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_iters,
+                 double* c_pos, double* c_normal, double* c_force, double* c_depth);
+
+/* ------------------------------------------------------------------ */
 /* Batched environment (task logic of the reference's CartPole /      */
 /* Pendulum tasks + gym TimeLimit + auto-reset with Philox4x32-10).   */
 /* ------------------------------------------------------------------ */

@@ -66,6 +66,31 @@ class OrPidState(ctypes.Structure):
     _fields_ = [(k, ctypes.c_double) for k in ("perr_last", "ierr", "cmd")]
 
 
+OR_MAXSHAPES = 8
+OR_MAXCONTACTS = 8 * OR_MAXSHAPES
+
+
+class OrFreeModel(ctypes.Structure):
+    _fields_ = [
+        ("mass", ctypes.c_double),
+        ("com", ctypes.c_double * 3),
+        ("Ic", ctypes.c_double * 6),
+        ("n_shapes", ctypes.c_int32),
+        ("ground", ctypes.c_int32),
+        ("shape_type", ctypes.c_int32 * OR_MAXSHAPES),
+        ("shape_size", (ctypes.c_double * 3) * OR_MAXSHAPES),
+        ("shape_R", (ctypes.c_double * 9) * OR_MAXSHAPES),
+        ("shape_p", (ctypes.c_double * 3) * OR_MAXSHAPES),
+        ("gravity", ctypes.c_double * 3),
+        ("mu", ctypes.c_double),
+    ]
+
+
+class OrFreeState(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_double * 3), ("R", ctypes.c_double * 9),
+                ("w", ctypes.c_double * 3), ("v", ctypes.c_double * 3)]
+
+
 class OrTask(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
@@ -113,6 +138,9 @@ def lib():
         L.or_step.argtypes = [M, ctypes.c_double, D, D, I32, D, ctypes.c_int, D, D]
         L.or_step.restype = ctypes.c_int
         L.or_pgs.argtypes = [ctypes.c_int, D, D, D, D, D, ctypes.c_int]
+        L.or_free_step.argtypes = [ctypes.POINTER(OrFreeModel), ctypes.c_double, ctypes.POINTER(OrFreeState),
+                                   ctypes.c_int, D, D, D, D]
+        L.or_free_step.restype = ctypes.c_int
         L.or_pid_update.argtypes = [ctypes.POINTER(OrPidGains), ctypes.POINTER(OrPidState),
                                     ctypes.c_double, ctypes.c_double]
         L.or_pid_update.restype = ctypes.c_double
@@ -168,6 +196,8 @@ class _Link:
     mass: float = 0.0
     com: np.ndarray = field(default_factory=lambda: np.zeros(3))
     I: np.ndarray = field(default_factory=lambda: np.zeros((3, 3)))  # about COM, link frame
+    # collision shapes in the link frame: (type 0 box / 1 sphere, size (half extents / radius), R, p)
+    shapes: list = field(default_factory=list)
 
 
 @dataclass
@@ -189,6 +219,13 @@ class _Joint:
 
 def _merge(parent: _Link, child: _Link, R: np.ndarray, p: np.ndarray) -> _Link:
     """Rigidly merge `child` (pose R, p in parent) into `parent`."""
+    shapes = list(parent.shapes) + [(t, sz, R @ SR, R @ sp + p) for (t, sz, SR, sp) in child.shapes]
+    out = _merge_inertia(parent, child, R, p)
+    out.shapes = shapes
+    return out
+
+
+def _merge_inertia(parent: _Link, child: _Link, R: np.ndarray, p: np.ndarray) -> _Link:
     m = parent.mass + child.mass
     if m <= 0.0:
         return _Link()
@@ -210,6 +247,8 @@ class ChainModel:
     model: OrModel
     base_R: np.ndarray
     base_p: np.ndarray
+    floating: bool = False
+    free: Optional[OrFreeModel] = None
 
     @property
     def n(self) -> int:
@@ -238,6 +277,16 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
                             [g("ixy"), g("iyy"), g("iyz")],
                             [g("ixz"), g("iyz"), g("izz")]])
             L.I = Ro @ Iin @ Ro.T
+        for ce in le.findall("collision"):
+            o = ce.find("origin")
+            geo = ce.find("geometry")
+            box = geo.find("box") if geo is not None else None
+            sph = geo.find("sphere") if geo is not None else None
+            SR, sp = _rpy(_vec(o, "rpy", [0, 0, 0])), _vec(o, "xyz", [0, 0, 0])
+            if box is not None:
+                L.shapes.append((0, 0.5 * _vec(box, "size", [0, 0, 0]), SR, sp))
+            elif sph is not None:
+                L.shapes.append((1, np.array([float(sph.get("radius")), 0.0, 0.0]), SR, sp))
         links[le.get("name")] = L
     joints: List[_Joint] = []
     for je in root.findall("joint"):
@@ -266,15 +315,14 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
     root_link = roots[0]
     base_R = _quat_wxyz(pose_wxyz)
     base_p = np.array(pose_xyz, dtype=float)
-    if root_link == "world":
+    floating = root_link != "world"
+    if not floating:
         wj = [j for j in joints if j.parent == "world"]
         assert len(wj) == 1 and wj[0].jtype == "fixed", "only a fixed world joint is supported"
         base_p = base_p + base_R @ wj[0].p
         base_R = base_R @ wj[0].R
         root_link = wj[0].child
         joints = [j for j in joints if j is not wj[0]]
-    else:
-        raise ValueError("floating-base URDFs are not supported by the chain oracle")
 
     # lump fixed joints into their parent (sdformat URDF import behaviour)
     owner = {n: n for n in links}            # link -> body it was lumped into
@@ -342,7 +390,28 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
         M.upper[i] = j.upper
         M.effort[i] = j.effort
         M.vel_limit[i] = j.velocity
-    return ChainModel([j.name for j in chain], root_link, M, base_R, base_p)
+    cm = ChainModel([j.name for j in chain], root_link, M, base_R, base_p)
+    cm.floating = floating
+    if floating:
+        B = links[root_link]
+        F = OrFreeModel()
+        F.mass = B.mass
+        for k in range(3):
+            F.com[k] = B.com[k]
+            F.gravity[k] = gravity[k]
+        for k, v in enumerate([B.I[0, 0], B.I[1, 1], B.I[2, 2], B.I[0, 1], B.I[0, 2], B.I[1, 2]]):
+            F.Ic[k] = v
+        F.n_shapes = len(B.shapes)
+        for i, (t, sz, SR, sp) in enumerate(B.shapes):
+            F.shape_type[i] = t
+            for k in range(3):
+                F.shape_size[i][k] = sz[k]
+                F.shape_p[i][k] = sp[k]
+            for k in range(9):
+                F.shape_R[i][k] = SR.flat[k]
+        F.mu = 1.0
+        cm.free = F
+    return cm
 
 
 # --------------------------------------------------------------------------
@@ -496,6 +565,56 @@ class ScenarioWorld:
             self.q, self.qd, self.qdd, _, _ = step(self.cm, self.dt, self.q, self.qd, mode, cmd, self.pgs)
         self.force[:] = 0.0
         self.iterations += self.spr
+
+
+class FreeWorld:
+    """fp64 floating rigid body on the ground plane (or_free_step): DART
+    FreeJoint dynamics + ContactConstraint rows, the checker of the HIP
+    free-body kernel.  Pose (p, R); twist in the body frame (w, v)."""
+
+    def __init__(self, cm: ChainModel, dt: float = 1e-3, ground: bool = True, mu: float = 1.0,
+                 pgs_iters: int = 100):
+        assert cm.floating and cm.n == 0
+        self.m = OrFreeModel()
+        ctypes.pointer(self.m)[0] = cm.free
+        self.m.ground = 1 if ground else 0
+        self.m.mu = mu
+        self.dt, self.pgs = dt, pgs_iters
+        self.s = OrFreeState()
+        self.set_pose(cm.base_p, cm.base_R)
+        self.contacts = []
+
+    def set_pose(self, p, R):
+        for k in range(3):
+            self.s.p[k] = p[k]
+        for k in range(9):
+            self.s.R[k] = np.asarray(R).flat[k]
+
+    def set_twist(self, w_body, v_body):
+        for k in range(3):
+            self.s.w[k] = w_body[k]
+            self.s.v[k] = v_body[k]
+
+    @property
+    def p(self):
+        return np.array(self.s.p[:])
+
+    @property
+    def R(self):
+        return np.array(self.s.R[:]).reshape(3, 3)
+
+    @property
+    def twist(self):
+        return np.array(self.s.w[:]), np.array(self.s.v[:])
+
+    def step(self):
+        cp, cn, cf, cd = (np.zeros(3 * OR_MAXCONTACTS), np.zeros(3 * OR_MAXCONTACTS),
+                          np.zeros(3 * OR_MAXCONTACTS), np.zeros(OR_MAXCONTACTS))
+        nc = lib().or_free_step(ctypes.byref(self.m), self.dt, ctypes.byref(self.s), self.pgs,
+                                _p(cp), _p(cn), _p(cf), _p(cd))
+        self.contacts = [(cp[3 * i:3 * i + 3].copy(), cn[3 * i:3 * i + 3].copy(), cf[3 * i:3 * i + 3].copy(),
+                          float(cd[i])) for i in range(nc)]
+        return nc
 
 
 def pgs(A, b, lo, hi, iters=100):

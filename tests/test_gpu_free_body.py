@@ -1,0 +1,152 @@
+"""GPU tests of floating bodies with ground contacts (SURVEY.md §8f row 1,
+first slice: single floating bodies).
+
+  * the reference's contact KAT through the ScenarI/O mirror
+    (tests/test_scenario/test_contacts.py:57-122; single and double-collision
+    cube): no contact before falling, one contact (cube::cube vs
+    ground_plane::link) after 150 ms, normals +z, the vertical forces sum to
+    the weight within 0.1 N, Link::contactWrench = [0, 0, sum Fz, 0, 0, 0];
+  * teacher-forced one-step parity of the HIP free-body kernel against the fp64
+    oracle (or_free_step) on random poses / twists near the ground: pose and
+    twist within 1e-5 (fp32 vs fp64), contact forces within 1e-3 relative;
+  * free fall and torque-free spin over 1000 steps against the oracle;
+  * base reset semantics (visible after the next run).
+"""
+
+import numpy as np
+import pytest
+
+from test_free_body_oracle import cube_urdf, sphere_urdf
+
+pytestmark = pytest.mark.gpu
+G = 9.8
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_cube_contact_kat(require_gpu, double):
+    from mwstep import get_model_file
+    from scenario import core
+    from scenario import gazebo as scenario
+    gazebo = scenario.GazeboSimulator(0.001, 1.0, 1)
+    assert gazebo.initialize()
+    world = gazebo.get_world().to_gazebo()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("ground_plane"))
+    assert len(world.model_names()) == 1
+    assert world.insert_model_from_string(cube_urdf(double), core.Pose([0, 0, 0.15], [1., 0, 0, 0]), "cube")
+    assert len(world.model_names()) == 2
+    cube = world.get_model("cube")
+    assert not cube.contacts_enabled()
+    assert cube.enable_contacts(enable=True)
+    assert cube.contacts_enabled()
+    gazebo.run(paused=True)
+    assert not cube.get_link("cube").in_contact()
+    assert len(cube.contacts()) == 0
+    for _ in range(150):
+        gazebo.run()
+    assert cube.get_link("cube").in_contact()
+    assert len(cube.contacts()) == 1
+    c = cube.contacts()[0]
+    assert c.body_a == "cube::cube" and c.body_b == "ground_plane::link"
+    for point in c.points:
+        assert point.normal == pytest.approx([0, 0, 1])
+    z_forces = [point.force[2] for point in c.points]
+    assert np.sum(z_forces) == pytest.approx(-5 * world.gravity()[2], abs=0.1)
+    assert cube.get_link("cube").contact_wrench() == pytest.approx([0, 0, np.sum(z_forces), 0, 0, 0], abs=1e-4)
+    gazebo.close()
+
+
+def _quat_to_R(q):
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+@pytest.mark.parametrize("urdf", ["cube", "double", "sphere"])
+def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
+    from mwstep.sim import Simulator
+    text = {"cube": cube_urdf(), "double": cube_urdf(True), "sphere": sphere_urdf()}[urdf]
+    W, pgs = 256, 50
+    rng = np.random.default_rng(5)
+    sim = Simulator(text, n_worlds=W, pgs_iters=pgs)
+    sim.set_ground_plane(True, 0.8)
+    sim.enable_contacts(True)
+    q = rng.normal(size=(W, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    pos = np.column_stack([rng.uniform(-1, 1, W), rng.uniform(-1, 1, W), rng.uniform(0.05, 0.2, W)])
+    lin = rng.uniform(-0.5, 0.5, (W, 3))
+    ang = rng.uniform(-2, 2, (W, 3))
+    sim.reset_base_pose(np.column_stack([pos, q]).astype(np.float32).astype(np.float64))
+    sim.reset_base_velocity(np.column_stack([lin, ang]).astype(np.float32).astype(np.float64))
+    sim.run(paused=True)
+    p0, v0 = sim.base_pose(), sim.base_velocity()
+    sim.run()
+    p1, v1 = sim.base_pose(), sim.base_velocity()
+    cm = oracle.load_urdf(text)
+    worst_p = worst_v = worst_f = 0.0
+    n_contact = 0
+    for w in range(W):
+        R0 = _quat_to_R(p0[w, 3:])
+        ow = oracle.FreeWorld(cm, ground=True, mu=0.8, pgs_iters=pgs)
+        ow.set_pose(p0[w, :3], R0)
+        ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
+        ow.step()
+        worst_p = max(worst_p, float(np.abs(p1[w, :3] - ow.p).max()),
+                      float(np.abs(_quat_to_R(p1[w, 3:]) - ow.R).max()))
+        wv = np.concatenate([ow.R @ ow.twist[1], ow.R @ ow.twist[0]])
+        worst_v = max(worst_v, float(np.abs(v1[w] - wv).max()))
+        gc = sim.contacts(w)
+        assert len(gc) == len(ow.contacts)
+        n_contact += len(gc) > 0
+        for row, (p, n, f, d) in zip(gc, ow.contacts):
+            assert np.abs(row[0:3] - p).max() <= 1e-5
+            worst_f = max(worst_f, float(np.abs(row[6:9] - f).max()) / (1.0 + float(np.abs(f).max())))
+    print(f"free body {urdf}: one-step max|pose err| {worst_p:.2e}, max|vel err| {worst_v:.2e}, "
+          f"force rel err {worst_f:.2e}, {n_contact}/{W} worlds in contact")
+    assert n_contact > W // 4
+    assert worst_p <= 1e-5 and worst_v <= 1e-4 and worst_f <= 1e-3
+    sim.close()
+
+
+def test_free_fall_and_spin_parity(require_gpu, oracle):
+    from mwstep.sim import Simulator
+    text = cube_urdf()
+    sim = Simulator(text, n_worlds=2, pose=(0, 0, 10.0, 1, 0, 0, 0), gravity=(0, 0, -G))
+    sim.reset_base_velocity([[0.3, -0.2, 1.0, 0.5, -1.0, 2.0], [0, 0, 0, 0, 0, 0]])
+    sim.run(paused=True)
+    cm = oracle.load_urdf(text, pose_xyz=(0, 0, 10.0))
+    ow = oracle.FreeWorld(cm, ground=False)
+    ow.set_twist([0.5, -1.0, 2.0], [0.3, -0.2, 1.0])
+    for _ in range(1000):
+        sim.run()
+        ow.step()
+    p = sim.base_pose()[0]
+    assert np.abs(p[:3] - ow.p).max() <= 1e-4
+    assert np.abs(_quat_to_R(p[3:]) - ow.R).max() <= 1e-4
+    sim.close()
+
+
+def test_base_reset_semantics(require_gpu):
+    from mwstep import get_model_file
+    from scenario import core
+    from scenario import gazebo as scenario
+    gazebo = scenario.GazeboSimulator(0.001, 1.0, 1)
+    assert gazebo.initialize()
+    world = gazebo.get_world().to_gazebo()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model_from_string(cube_urdf(), core.Pose([0, 0, 1.0], [1., 0, 0, 0]), "cube")
+    cube = world.get_model("cube")
+    assert cube.base_position() == pytest.approx([0, 0, 1.0])
+    assert cube.reset_base_pose([1, 2, 3], [0, 0, 0, 1])
+    assert cube.base_position() == pytest.approx([0, 0, 1.0])      # applied by the next run
+    assert cube.reset_base_world_linear_velocity([0.1, 0, 0])
+    assert cube.reset_base_world_angular_velocity([0, 0, 0.5])     # keeps the linear part
+    gazebo.run(paused=True)
+    assert cube.base_position() == pytest.approx([1, 2, 3])
+    assert cube.base_orientation() == pytest.approx([0, 0, 0, 1])
+    assert cube.base_world_linear_velocity() == pytest.approx([0.1, 0, 0], abs=1e-6)
+    assert cube.base_world_angular_velocity() == pytest.approx([0, 0, 0.5], abs=1e-6)
+    # the world-frame velocity of a body rotated by pi about z, seen in its frame
+    assert cube.base_body_linear_velocity() == pytest.approx([-0.1, 0, 0], abs=1e-6)
+    gazebo.close()

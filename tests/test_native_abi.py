@@ -130,8 +130,11 @@ def test_fixed_joint_lumping(N, oracle):
 
 
 @pytest.mark.parametrize("bad, why", [
-    ("<robot name='x'><link name='a'/><link name='b'/>"
-     "<joint name='j' type='revolute'><parent link='a'/><child link='b'/></joint></robot>", "floating"),
+    ("<robot name='x'><link name='a'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+     "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+     "<joint name='j' type='revolute'><parent link='a'/><child link='b'/></joint></robot>",
+     "floating-base models with joints"),
+    ("<robot name='x'><link name='a'/></robot>", "has no mass"),
     ("<robot name='x'><link name='world'/>", "XML"),
     ("<sdf><model name='m'/></sdf>", "URDF"),
     ("<robot name='x'><link name='world'/><link name='a'/><joint name='w' type='fixed'>"
@@ -208,3 +211,39 @@ def test_pid_and_controller_period_semantics(N, panda_file):
         assert t.value == 1e-3
     finally:
         N.lib().mw_destroy(h)
+
+
+CUBE = """<robot name="cube_robot"><link name="cube"><inertial><origin rpy="0 0 0" xyz="0 0 0"/>
+  <mass value="5.0"/><inertia ixx="0.0333333" ixy="0" ixz="0" iyy="0.0333333" iyz="0" izz="0.0333333"/></inertial>
+  <collision><geometry><box size="0.2 0.1 0.2"/></geometry><origin rpy="0 0 0" xyz="0 -0.05 0"/></collision>
+  <collision><geometry><box size="0.2 0.1 0.2"/></geometry><origin rpy="0 0 0" xyz="0 0.05 0"/></collision>
+</link></robot>"""
+
+
+def test_floating_body_model(N, oracle):
+    """A floating single body (the reference's double-collision test cube,
+    tests/test_scenario/test_contacts.py:22-54) compiles with its two box
+    shapes; base / contact calls need an initialised simulator."""
+    rc, h = _create(N)
+    try:
+        p = np.array([0, 0, 0.15, 1, 0, 0, 0], dtype=np.float64)
+        N.check(N.lib().mw_load_model(h, CUBE.encode(), N.dptr(p), b"cube"))
+        f = ctypes.c_int32()
+        N.check(N.lib().mw_is_floating(h, ctypes.byref(f)))
+        assert f.value == 1
+        n = ctypes.c_int32()
+        N.check(N.lib().mw_dofs(h, ctypes.byref(n)))
+        assert n.value == 0
+        out = np.zeros(7)
+        assert N.lib().mw_get_base_pose(h, 0, 1, N.dptr(out)) == N.MW_ESTATE
+        N.check(N.lib().mw_set_ground_plane(h, 1, 1.0))
+        assert N.lib().mw_set_ground_plane(h, 1, -1.0) == N.MW_EINVAL
+        N.check(N.lib().mw_enable_contacts(h, 1))
+        N.check(N.lib().mw_contacts_enabled(h, ctypes.byref(f)))
+        assert f.value == 1
+    finally:
+        N.lib().mw_destroy(h)
+    cm = oracle.load_urdf(CUBE, pose_xyz=(0, 0, 0.15))
+    assert cm.floating and cm.n == 0 and cm.free.n_shapes == 2
+    np.testing.assert_allclose(list(cm.free.shape_p[1]), [0, 0.05, 0])
+    np.testing.assert_allclose(list(cm.free.shape_size[0]), [0.1, 0.05, 0.1])
