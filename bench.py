@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-panda", action="store_true", help="skip the config-4 Panda leg")
     p.add_argument("--no-rand-leg", action="store_true", help="skip the randomised-physics leg")
+    p.add_argument("--no-contact-leg", action="store_true", help="skip the floating-body contact leg")
     p.add_argument("--groups", type=int, default=1,
                    help="world groups per GPU, each on its own stream / hardware queue")
     return p.parse_args()
@@ -144,6 +145,9 @@ def main():
     panda = None
     if not args.no_panda and rank == 0 and world_size == 1 and args.task != "PandaPositionTracking":
         panda = panda_leg(args, dev, torch, dist)
+    contacts = None
+    if not args.no_contact_leg and rank == 0 and world_size == 1:
+        contacts = contact_leg(args, dev, torch)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
@@ -197,6 +201,7 @@ def main():
             "rollout_fused": rollout,
             "panda_c4": panda,
             "randomized": rand,
+            "contacts_floating": contacts,
         }
         print(json.dumps(out))
     for e in envs:
@@ -354,6 +359,58 @@ def panda_leg(args, dev, torch, dist):
     out["algorithmic_bytes_per_launch"] = bpe * W
     for e in envs:
         e.close()
+    return out
+
+
+def contact_leg(args, dev, torch):
+    """Floating bodies with ground contacts (SURVEY §8f row 1 slice): 4096 cubes
+    (the reference's contact-test cube) dropped from random poses onto the
+    ground plane, contacts enabled (read back on the device), one physics step
+    per run, replayed from hipGraphs of device-resident runs (mw_run_device)."""
+    import numpy as np
+    from mwstep import get_model_file
+    from mwstep.sim import Simulator
+    W, K, warm, G = 4096, 1000, 200, 100
+    stream = torch.cuda.Stream(device=dev)
+    sim = Simulator(get_model_file("cube"), n_worlds=W, device=dev.index, pgs_iters=20,
+                    stream=stream.cuda_stream)
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    rng = np.random.default_rng(args.seed)
+    q = rng.normal(size=(W, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), rng.uniform(0.2, 0.6, W), q])
+    sim.reset_base_pose(pose)
+    sim.reset_base_velocity(np.column_stack([rng.uniform(-1, 1, (W, 3)), rng.uniform(-3, 3, (W, 3))]))
+    sim.run(paused=True)
+    with torch.cuda.stream(stream):
+        sim.run_device(warm)
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            sim.run_device(G)
+        graph.replay()
+    stream.synchronize()
+    n_rep = K // G
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        for _ in range(n_rep):
+            graph.replay()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    steps = n_rep * G
+    in_contact = int(sum(len(sim.contacts(w)) > 0 for w in range(0, W, 16)))
+    out = {"workload": f"{W} floating cubes (5 kg, 0.2 m) on a ground plane, box-plane contacts, "
+                       "normal + 2 friction rows per point, PGS 20 iterations, dt = 1 ms",
+           "value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
+           "ms_per_step": round(elapsed / steps * 1e3, 6),
+           "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
+           "worlds_in_contact_sampled": f"{in_contact}/{W // 16}"}
+    sim.close()
     return out
 
 

@@ -87,16 +87,20 @@ __device__ __forceinline__ f3 slot_point(const FreeF& F, int s, int k) {
             F.shape_p[s][2] + R[6] * ax + R[7] * ay + R[8] * az};
 }
 
-// Contact slot record in LDS (11 words: odd, so a wave's accesses to one
+// Contact slot record in LDS (31 words: odd, so a wave's accesses to one
 // field hit distinct banks); slot records of a lane are kFreeLanes apart.
+// Per row the step caches M^-1 J and the diagonal, so a PGS sweep is two
+// 6-dots and a 6-axpy per row.
 constexpr int kFreeLanes = 64;
 struct SlotRec {
     f3 b;          // contact point, body frame
     f3 xw;         // contact point, world frame (start of the step)
     float depth;
     float x[3];    // impulses: normal, t1, t2
-    float pad_;
+    float mj[3][6];  // M^-1 J per row
+    float arr[3];    // J M^-1 J^T per row (without CFM)
 };
+static_assert(sizeof(SlotRec) == 31 * 4, "SlotRec layout: an odd word count");
 
 struct Contacts {
     uint32_t active;   // bit per slot
@@ -157,6 +161,19 @@ __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt
         // directions in the body frame: n = +z, t1, t2 = ODE dPlaneSpace(n)
         const f3 db[3] = {mulT(R, mk(0.f, 0.f, 1.f)), mulT(R, mk(0.f, -1.f, 0.f)), mulT(R, mk(1.f, 0.f, 0.f))};
         const float inv_dt = rcp(dt);
+        // rows of this step: M^-1 J and the diagonal, once
+        for (uint32_t m = C.active; m; m &= m - 1u) {
+            SlotRec& r = C.at(__builtin_ctz(m));
+            const f3 b = r.b;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const SV J = {cross(b, db[d]), db[d]};
+                const SV MJ = minv_mul(F, J);
+                r.mj[d][0] = MJ.w.x; r.mj[d][1] = MJ.w.y; r.mj[d][2] = MJ.w.z;
+                r.mj[d][3] = MJ.v.x; r.mj[d][4] = MJ.v.y; r.mj[d][5] = MJ.v.z;
+                r.arr[d] = dot(J, MJ);
+            }
+        }
         for (int it = 0; it < pgs_iters; ++it) {
             for (uint32_t m = C.active; m; m &= m - 1u) {
                 SlotRec& r = C.at(__builtin_ctz(m));
@@ -166,8 +183,8 @@ __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt
 #pragma unroll
                 for (int d = 0; d < 3; ++d) {
                     const SV J = {cross(b, db[d]), db[d]};
-                    const SV MJ = minv_mul(F, J);
-                    const float Arr = dot(J, MJ);
+                    const SV MJ = {{r.mj[d][0], r.mj[d][1], r.mj[d][2]}, {r.mj[d][3], r.mj[d][4], r.mj[d][5]}};
+                    const float Arr = r.arr[d];
                     // x += (b - sum_c A_rc x_c) / A_rr  with  sum_c A_rc x_c = J (V - V1) + cfm A_rr x
                     const float target = (d == 0) ? bounce : 0.f;
                     const float xo = xs[d];

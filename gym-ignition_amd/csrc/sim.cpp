@@ -101,6 +101,7 @@ struct mw_sim {
     std::vector<float> h_rpose, h_rvel;
     std::vector<uint8_t> h_rflag;
     bool free_dirty = false;
+    bool contacts_stale = false;  // contacts written on the device by mw_run_device
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -595,7 +596,7 @@ int mw_set_stream(mw_sim* s, void* stream) {
     return MW_OK;
 }
 
-static int run_free(mw_sim* s, int paused) {
+static int run_free(mw_sim* s, int paused, bool readback = true) {
     const size_t W = static_cast<size_t>(s->W);
     if (s->free_dirty) {
         // pending base resets: one H2D copy of [rpose | rvel] and the flags
@@ -616,6 +617,15 @@ static int run_free(mw_sim* s, int paused) {
     a.first = 1;
     a.substeps = paused ? 0 : s->cfg.steps_per_run;
     MW_HIP(mw::launch_free_run(s->d_free, s->fdev, s->W, a, s->contacts ? 1 : 0, s->stream));
+    if (!paused) {
+        s->iterations += s->cfg.steps_per_run;
+        s->stepped = true;
+    }
+    if (!readback) {
+        s->host_stale = true;
+        s->contacts_stale = s->contacts;
+        return MW_OK;
+    }
     MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * W * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     if (s->contacts && !paused) {
         MW_HIP(hipMemcpyAsync(s->h_cmask, s->fdev.cmask, W * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
@@ -623,18 +633,17 @@ static int run_free(mw_sim* s, int paused) {
                               hipMemcpyDeviceToHost, s->stream));
     }
     MW_HIP(hipStreamSynchronize(s->stream));
-    if (!paused) {
-        s->iterations += s->cfg.steps_per_run;
-        s->stepped = true;
-    }
+    s->contacts_stale = false;
     return MW_OK;
 }
 
-int mw_run(mw_sim* s, int paused) {
+static int run_impl(mw_sim* s, int paused, bool readback) {
     int rc = check_sim(s);
     if (rc) return rc;
-    if ((rc = pull_state(s))) return rc;
-    if (s->floating) return run_free(s, paused);
+    // a device-resident run never needs the host mirror (and must not
+    // synchronise: it may be captured into a graph)
+    if (readback && (rc = pull_state(s))) return rc;
+    if (s->floating) return run_free(s, paused, readback);
     if (s->cmd_dirty) {
         MW_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_block) + s->cmd_off, s->h_block + s->cmd_off,
                               s->cmd_bytes, hipMemcpyHostToDevice, s->stream));
@@ -673,8 +682,12 @@ int mw_run(mw_sim* s, int paused) {
         a.first = 0;
         done += chunk;
     } while (!paused && done < spr);
-    MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
-    MW_HIP(hipStreamSynchronize(s->stream));
+    if (readback) {
+        MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipStreamSynchronize(s->stream));
+    } else {
+        s->host_stale = true;
+    }
     // mirror the kernel's component semantics on the host copy
     std::memset(s->hcmd(), 0, s->nw * sizeof(float));
     std::memset(s->hrflag(), 0, s->nw);
@@ -682,6 +695,17 @@ int mw_run(mw_sim* s, int paused) {
     if (!paused) {
         s->iterations += s->cfg.steps_per_run;
         s->stepped = true;
+    }
+    return MW_OK;
+}
+
+int mw_run(mw_sim* s, int paused) { return run_impl(s, paused, true); }
+
+int mw_run_device(mw_sim* s, int32_t runs) {
+    if (runs < 0) return fail(MW_EINVAL, "runs must be >= 0");
+    for (int32_t k = 0; k < runs; ++k) {
+        int rc = run_impl(s, 0, false);
+        if (rc) return rc;
     }
     return MW_OK;
 }
@@ -1132,6 +1156,15 @@ int mw_get_contacts(const mw_sim* s, int32_t w, double* out, int32_t cap, int32_
     if (w < 0 || w >= s->W) return fail(MW_EINVAL, "world index out of range");
     *n = 0;
     if (!s->floating || !s->contacts) return MW_OK;
+    if (s->contacts_stale) {
+        mw_sim* m = const_cast<mw_sim*>(s);
+        const size_t Wc = static_cast<size_t>(s->W);
+        MW_HIP(hipMemcpyAsync(m->h_cmask, s->fdev.cmask, Wc * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipMemcpyAsync(m->h_cdata, s->fdev.cdata, 7 * mw::kMaxFreeSlots * Wc * sizeof(float),
+                              hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipStreamSynchronize(s->stream));
+        m->contacts_stale = false;
+    }
     // contacts of the last substep of the last run (Physics.cpp:2351-2540): per
     // point x y z, normal (into the body), force on the body (N), depth
     const size_t W = static_cast<size_t>(s->W);

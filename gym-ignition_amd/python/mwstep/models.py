@@ -10,6 +10,7 @@ _FILES = {
     "cartpole": "cartpole.urdf",
     "pendulum": "pendulum.urdf",
     "panda": "panda.urdf",
+    "cube": "cube.urdf",
     "ground_plane": "ground_plane.sdf",
 }
 

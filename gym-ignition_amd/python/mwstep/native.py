@@ -81,6 +81,7 @@ SIGNATURES = [
     ("mw_initialized", ctypes.c_int, [_P]),
     ("mw_set_stream", ctypes.c_int, [_P, _P]),
     ("mw_run", ctypes.c_int, [_P, ctypes.c_int]),
+    ("mw_run_device", ctypes.c_int, [_P, _I]),
     ("mw_time", ctypes.c_int, [_P, _D]),
     ("mw_set_gravity", ctypes.c_int, [_P, _D]),
     ("mw_gravity", ctypes.c_int, [_P, _D]),

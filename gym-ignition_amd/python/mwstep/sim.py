@@ -82,6 +82,10 @@ class Simulator:
     def run(self, paused: bool = False) -> None:
         N.check(N.lib().mw_run(self.handle, 1 if paused else 0), "run")
 
+    def run_device(self, runs: int = 1) -> None:
+        """`runs` runs with the state kept on the device (graph-capturable)."""
+        N.check(N.lib().mw_run_device(self.handle, runs), "run_device")
+
     def time(self) -> float:
         t = ctypes.c_double()
         N.check(N.lib().mw_time(self.handle, ctypes.byref(t)))

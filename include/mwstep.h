@@ -97,6 +97,9 @@ int mw_set_stream(mw_sim* sim, void* hip_stream);
 /* Applies pending resets and commands, executes steps_per_run substeps unless
  * paused, refreshes the host-side readback, and blocks until done. */
 int mw_run(mw_sim* sim, int paused);
+/* `runs` x mw_run(sim, 0) with the state kept on the device: no readback and
+ * no host synchronisation (graph-capturable; the getters read back lazily). */
+int mw_run_device(mw_sim* sim, int32_t runs);
 /* Simulated time in seconds after the last run (World::time, World.cpp:326-332). */
 int mw_time(const mw_sim* sim, double* seconds);
 int mw_set_gravity(mw_sim* sim, const double g[3]);

@@ -150,3 +150,24 @@ def test_base_reset_semantics(require_gpu):
     # the world-frame velocity of a body rotated by pi about z, seen in its frame
     assert cube.base_body_linear_velocity() == pytest.approx([-0.1, 0, 0], abs=1e-6)
     gazebo.close()
+
+
+def test_run_device_equals_run(require_gpu):
+    """mw_run_device (no readback, graph-capturable) == repeated mw_run."""
+    from mwstep import get_model_file
+    from mwstep.sim import Simulator
+    sims = [Simulator(get_model_file("cube"), n_worlds=64, pose=(0, 0, 0.3, 0.9, 0.3, 0.2, 0.1)) for _ in range(2)]
+    for s in sims:
+        s.set_ground_plane(True, 0.7)
+        s.enable_contacts(True)
+        s.reset_base_velocity([0.2, 0.1, -0.5, 1.0, -2.0, 0.5])
+        s.run(paused=True)
+    for _ in range(300):
+        sims[0].run()
+    sims[1].run_device(300)
+    assert np.array_equal(sims[0].base_pose(), sims[1].base_pose())
+    assert np.array_equal(sims[0].base_velocity(), sims[1].base_velocity())
+    assert np.array_equal(sims[0].contacts(5), sims[1].contacts(5))
+    assert len(sims[0].contacts(5)) > 0
+    for s in sims:
+        s.close()
