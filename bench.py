@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-panda", action="store_true", help="skip the config-4 Panda leg")
     p.add_argument("--no-rand-leg", action="store_true", help="skip the randomised-physics leg")
+    p.add_argument("--no-pendulum", action="store_true", help="skip the config-3 Pendulum leg")
     p.add_argument("--no-contact-leg", action="store_true", help="skip the floating-body contact leg")
     p.add_argument("--groups", type=int, default=1,
                    help="world groups per GPU, each on its own stream / hardware queue")
@@ -72,8 +73,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; the modulo only matters when rehearsing several
+    # ranks on fewer GPUs (the driver launches one rank per GPU)
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank % ndev)
+    dev = torch.device("cuda", local_rank % ndev)
     if world_size > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -125,6 +129,21 @@ def main():
     sweep = None
     if not args.no_sweep and world_size == 1 and not env.action_dim:
         sweep = world_sweep(args, dev, torch)
+
+    # ---------------- BASELINE config 3: 2048 Pendulum worlds (continuous torque)
+    pend = None
+    if not args.no_pendulum and rank == 0 and world_size == 1 and args.task == "CartPoleDiscreteBalancing":
+        penvs = make_groups("PendulumSwingUp", 2048, 1, dev, args.seed, 0)
+        pacts = make_actions(penvs, args.warmup + K, dev, torch, 0)
+        r = time_steps(penvs, pacts, args.warmup, K, args.graph_chunk, dev, torch, dist, 1)
+        pb = algorithmic_bytes_per_env_step(1, 3)
+        pend = {"workload": "PendulumSwingUp: 2048 worlds, tau ~ U(-50, 50), dt = 1 ms (BASELINE.json configs[2])",
+                "value": round(2048 * K / r["elapsed"], 1), "unit": "env·steps/s",
+                "ms_per_step": round(r["elapsed"] / K * 1e3, 6),
+                "kernel_us_per_launch": round(r["kernel_us"], 3), "bytes_per_env_step": pb,
+                "kernel": f"vecenv_step_kernel<1,3,false,false,false,{penvs[0].sim.baked_model()}>"}
+        for e in penvs:
+            e.close()
 
     # ---------------- the same workload with per-world physics randomisation
     # (masses + gravity resampled at every reset, randomizers/cartpole.py)
@@ -200,6 +219,7 @@ def main():
             "obs_max_abs_err_vs_oracle": parity,
             "rollout_fused": rollout,
             "panda_c4": panda,
+            "pendulum_c3": pend,
             "randomized": rand,
             "contacts_floating": contacts,
         }
