@@ -89,5 +89,9 @@ constexpr bool on_path(Topo t, int i, int j) {
 }
 // the Franka Panda: joints 1..7 in a chain, both fingers hang off the hand
 constexpr Topo kPandaTopo = chain_topo(7) | (static_cast<Topo>(7) << 28) | (static_cast<Topo>(7) << 32);
+// four 2-dof legs hanging off a floating base (models/quadruped.urdf):
+// parents [-1, 0, -1, 2, -1, 4, -1, 6]
+constexpr Topo kQuadrupedTopo = (static_cast<Topo>(1) << 4) | (static_cast<Topo>(3) << 12) |
+                                (static_cast<Topo>(5) << 20) | (static_cast<Topo>(7) << 28);
 
 }  // namespace mw

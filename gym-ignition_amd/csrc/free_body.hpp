@@ -63,6 +63,39 @@ __device__ __forceinline__ M3 quat_to_R(float w, float x, float y, float z) {
     return R;
 }
 
+// DART FreeJoint::integratePositions: T <- T exp(dt V) (SE(3) exponential,
+// V = [w; v] in the body frame); R is the rotation of S's quaternion.
+__device__ __forceinline__ void integrate_pose(const M3& R, const SV& V, float dt, FreeState& S) {
+    const f3 phi = dt * V.w, u = dt * V.v;
+    const float th2 = dot(phi, phi);
+    float b, cc;  // V(phi) = 1 + b K + cc K^2
+    if (th2 < 1e-8f) {
+        b = 0.5f - th2 * (1.f / 24.f);
+        cc = (1.f / 6.f) - th2 * (1.f / 120.f);
+    } else {
+        const float th = sqrtf(th2);
+        float sn, cs;
+        sincos_joint(th, &sn, &cs);
+        b = (1.f - cs) / th2;
+        cc = (th - sn) / (th2 * th);
+    }
+    const f3 Ku = cross(phi, u);
+    const f3 dp = u + b * Ku + cc * cross(phi, Ku);
+    S.p = S.p + mul(R, dp);
+    // q <- q (x) [cos(th/2), sin(th/2) phi/th]
+    float hs, hc;
+    const float th = sqrtf(th2);
+    sincos_joint(0.5f * th, &hs, &hc);
+    const float k = (th2 < 1e-12f) ? 0.5f : hs / th;
+    const float dw = hc, dx = k * phi.x, dy = k * phi.y, dz = k * phi.z;
+    const float nw = S.qw * dw - S.qx * dx - S.qy * dy - S.qz * dz;
+    const float nx = S.qw * dx + S.qx * dw + S.qy * dz - S.qz * dy;
+    const float ny = S.qw * dy - S.qx * dz + S.qy * dw + S.qz * dx;
+    const float nz = S.qw * dz + S.qx * dy - S.qy * dx + S.qz * dw;
+    const float inv = 1.f / sqrtf(nw * nw + nx * nx + ny * ny + nz * nz);
+    S.qw = nw * inv; S.qx = nx * inv; S.qy = ny * inv; S.qz = nz * inv;
+}
+
 __device__ __forceinline__ SV minv_mul(const FreeF& __restrict__ F, const SV& x) {
     const float in[6] = {x.w.x, x.w.y, x.w.z, x.v.x, x.v.y, x.v.z};
     float o[6];
@@ -204,34 +237,7 @@ __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt
     }
 
     // integratePositions: T <- T exp(dt V)
-    const f3 phi = dt * V.w, u = dt * V.v;
-    const float th2 = dot(phi, phi);
-    float b, cc;  // V(phi) = 1 + b K + cc K^2
-    if (th2 < 1e-8f) {
-        b = 0.5f - th2 * (1.f / 24.f);
-        cc = (1.f / 6.f) - th2 * (1.f / 120.f);
-    } else {
-        const float th = sqrtf(th2);
-        float sn, cs;
-        sincos_joint(th, &sn, &cs);
-        b = (1.f - cs) / th2;
-        cc = (th - sn) / (th2 * th);
-    }
-    const f3 Ku = cross(phi, u);
-    const f3 dp = u + b * Ku + cc * cross(phi, Ku);
-    S.p = S.p + mul(R, dp);
-    // q <- q (x) [cos(th/2), sin(th/2) phi/th]
-    float hs, hc;
-    const float th = sqrtf(th2);
-    sincos_joint(0.5f * th, &hs, &hc);
-    const float k = (th2 < 1e-12f) ? 0.5f : hs / th;
-    const float dw = hc, dx = k * phi.x, dy = k * phi.y, dz = k * phi.z;
-    const float nw = S.qw * dw - S.qx * dx - S.qy * dy - S.qz * dz;
-    const float nx = S.qw * dx + S.qx * dw + S.qy * dz - S.qz * dy;
-    const float ny = S.qw * dy - S.qx * dz + S.qy * dw + S.qz * dx;
-    const float nz = S.qw * dz + S.qx * dy - S.qy * dx + S.qz * dw;
-    const float inv = 1.f / sqrtf(nw * nw + nx * nx + ny * ny + nz * nz);
-    S.qw = nw * inv; S.qx = nx * inv; S.qy = ny * inv; S.qz = nz * inv;
+    integrate_pose(R, V, dt, S);
     S.V = V;
 }
 

@@ -15,6 +15,7 @@
 
 #include "baked_models.hpp"
 #include "chain_dyn.hpp"
+#include "float_tree.hpp"
 #include "free_body.hpp"
 #include "kernels.hpp"
 
@@ -260,6 +261,63 @@ __device__ __forceinline__ bool pid_update(const PidF& g, float err, float inv_d
     return true;
 }
 
+// Joint forces of substep s of a run: a Force-mode command (SetForce ->
+// GenericJoint::setCommand clips to +-effort) acts on the first substep only
+// (UpdateSim zero-fills it); Position / Velocity joints take the
+// JointController PID force (JointController::PreUpdate,
+// JointController.cpp:195-262), recomputed when the period gate opens,
+// otherwise the last command (pid.Cmd()); error = current - target (:308).
+template <int N>
+__device__ __forceinline__ void joint_forces(const ChainF* __restrict__ P, const SimDev& S, const PidSet& pid, int W,
+                                             int w, const RunArgs& A, int s, const uint8_t (&act)[N],
+                                             const float (&cmd)[N], const float (&vc)[N], const float (&q)[N],
+                                             const float (&qd)[N], bool any_pid, float (&tau)[N]) {
+    const bool gate = (A.pid_gate >> s) & 1u;
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        const float e = P->b[d].effort;
+        tau[d] = (act[d] == kActForce && s == 0) ? fminf(fmaxf(cmd[d], -e), e) : 0.f;
+    }
+    if (any_pid) {
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            if (act[d] >= kActPidPos) {
+                const size_t k = static_cast<size_t>(d) * W + w;
+                float u = S.pid_u[k];
+                if (gate) {
+                    const bool pos = (act[d] == kActPidPos);
+                    const float err = pos ? (q[d] - S.ptgt[k]) : (qd[d] - vc[d]);
+                    float el = S.pid_e[k], ie = S.pid_i[k];
+                    if (pid_update(pid.g[d], err, A.inv_dt, A.dt, el, ie, u)) {
+                        S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
+                    } else {
+                        u = 0.f;
+                    }
+                }
+                const float e = P->b[d].effort;
+                tau[d] = fminf(fmaxf(u, -e), e);
+            }
+        }
+    }
+}
+
+// Joint resets of a run's first launch: velocity reset, then position reset
+// (UpdatePhysics, Physics.cpp:1330-1375); Joint::reset*/setControlMode/setPID
+// also reset the joint PID (Joint.cpp:148-151).
+template <int N>
+__device__ __forceinline__ void joint_resets(const SimDev& S, int W, int w, float (&q)[N], float (&qd)[N]) {
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
+        const uint8_t f = S.rflag[d * W + w];
+        if (f) {
+            if (f & 2u) qd[d] = S.rqd[d * W + w];
+            if (f & 1u) q[d] = S.rq[d * W + w];
+            if (f & 4u) { S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; }
+            S.rflag[d * W + w] = 0;
+        }
+    }
+}
+
 template <int N, bool DUAL, bool CONS, Topo TOPO, int BAKED = 0>
 __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restrict__ Pin, SimDev S, PidSet pid,
                                                            int W, RunArgs A) {
@@ -268,20 +326,7 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
     const ChainF* __restrict__ P = model_params<BAKED>(Pin);
     float q[N], qd[N];
     load_state<N>(S, W, w, q, qd);
-    if (A.first) {
-        // UpdatePhysics: velocity reset, then position reset (Physics.cpp:1330-1375);
-        // Joint::reset*/setControlMode/setPID also reset the joint PID (Joint.cpp:148-151)
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-            const uint8_t f = S.rflag[d * W + w];
-            if (f) {
-                if (f & 2u) qd[d] = S.rqd[d * W + w];
-                if (f & 1u) q[d] = S.rq[d * W + w];
-                if (f & 4u) { S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; }
-                S.rflag[d * W + w] = 0;
-            }
-        }
-    }
+    if (A.first) joint_resets<N>(S, W, w, q, qd);
     if (!A.paused) {
         float cmd[N], vc[N], tau[N], qdd[N];
         uint8_t act[N];
@@ -295,38 +340,7 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
         }
         MW_DECLARE_STAGE(N, DUAL, stage);
         for (int s = 0; s < A.substeps; ++s) {
-            const bool gate = (A.pid_gate >> s) & 1u;
-#pragma unroll
-            for (int d = 0; d < N; ++d) {
-                // SetForce -> GenericJoint::setCommand clips to +-effort; a Force-mode
-                // command only acts on the first substep (UpdateSim zero-fills it)
-                const float e = P->b[d].effort;
-                tau[d] = (act[d] == kActForce && s == 0) ? fminf(fmaxf(cmd[d], -e), e) : 0.f;
-            }
-            if (any_pid) {
-                // JointController::PreUpdate (JointController.cpp:195-262): PID force of
-                // Position / Velocity joints, recomputed when the period gate opens,
-                // otherwise the last command (pid.Cmd()); error = current - target (:308)
-#pragma unroll
-                for (int d = 0; d < N; ++d) {
-                    if (act[d] >= kActPidPos) {
-                        const size_t k = static_cast<size_t>(d) * W + w;
-                        float u = S.pid_u[k];
-                        if (gate) {
-                            const bool pos = (act[d] == kActPidPos);
-                            const float err = pos ? (q[d] - S.ptgt[k]) : (qd[d] - vc[d]);
-                            float el = S.pid_e[k], ie = S.pid_i[k];
-                            if (pid_update(pid.g[d], err, A.inv_dt, A.dt, el, ie, u)) {
-                                S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
-                            } else {
-                                u = 0.f;
-                            }
-                        }
-                        const float e = P->b[d].effort;
-                        tau[d] = fminf(fmaxf(u, -e), e);
-                    }
-                }
-            }
+            joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, q, qd, any_pid, tau);
             substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, nominal_dyn<N>(P));
         }
 #pragma unroll
@@ -430,20 +444,16 @@ __global__ void __launch_bounds__(256) vecenv_step_kernel(const ChainF* __restri
 }
 
 // ------------------------------------------------- floating free body ----
-// GazeboSimulator::run() for a floating single-body model: pending base pose /
-// velocity resets (WorldPoseCmd / WorldVelocityCmd, Model.cpp:256-360 ->
-// Physics.cpp:1535-1590), the substeps, and the contacts of the last substep
-// (Physics.cpp:2351-2540: point, force on the body = impulse / dt, depth).
-__global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__ F, FreeDev D, int W, RunArgs A,
-                                                       int want_contacts) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
-    auto at = [&](int f) -> float& { return D.base[f * W + w]; };
+// Base pose / twist of world w, with the pending resets of a run's first
+// launch applied (UpdatePhysics: World pose / velocity resets of the model's
+// base link, Physics.cpp:1330-1375).
+__device__ __forceinline__ FreeState load_base(const FreeDev& D, int W, int w, bool first) {
+    auto at = [&](int f) -> float { return D.base[f * W + w]; };
     FreeState S;
     S.p = {at(0), at(1), at(2)};
     S.qw = at(3); S.qx = at(4); S.qy = at(5); S.qz = at(6);
     S.V = {{at(7), at(8), at(9)}, {at(10), at(11), at(12)}};
-    if (A.first) {
+    if (first) {
         const uint8_t fl = D.rflag[w];
         if (fl & 1u) {
             S.p = {D.rpose[0 * W + w], D.rpose[1 * W + w], D.rpose[2 * W + w]};
@@ -460,6 +470,38 @@ __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__
         }
         if (fl) D.rflag[w] = 0;
     }
+    return S;
+}
+
+__device__ __forceinline__ void store_base(const FreeDev& D, int W, int w, const FreeState& S) {
+    auto at = [&](int f) -> float& { return D.base[f * W + w]; };
+    at(0) = S.p.x; at(1) = S.p.y; at(2) = S.p.z;
+    at(3) = S.qw; at(4) = S.qx; at(5) = S.qy; at(6) = S.qz;
+    at(7) = S.V.w.x; at(8) = S.V.w.y; at(9) = S.V.w.z;
+    at(10) = S.V.v.x; at(11) = S.V.v.y; at(12) = S.V.v.z;
+}
+
+// contact force on the body, world frame: (n x_n + t1 x_t1 + t2 x_t2) / dt
+// with n = (0, 0, 1), t1 = (0, -1, 0), t2 = (1, 0, 0)
+__device__ __forceinline__ void store_contact(const FreeDev& D, int W, int w, int slot, f3 xw, float xn, float x1,
+                                              float x2, float depth, float inv_dt) {
+    float* o = D.cdata + static_cast<size_t>(slot) * 7 * W + w;
+    o[0 * W] = xw.x; o[1 * W] = xw.y; o[2 * W] = xw.z;
+    o[3 * W] = x2 * inv_dt;
+    o[4 * W] = -x1 * inv_dt;
+    o[5 * W] = xn * inv_dt;
+    o[6 * W] = depth;
+}
+
+// GazeboSimulator::run() for a floating single-body model: pending base pose /
+// velocity resets (WorldPoseCmd / WorldVelocityCmd, Model.cpp:256-360 ->
+// Physics.cpp:1535-1590), the substeps, and the contacts of the last substep
+// (Physics.cpp:2351-2540: point, force on the body = impulse / dt, depth).
+__global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__ F, FreeDev D, int W, RunArgs A,
+                                                       int want_contacts) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    FreeState S = load_base(D, W, w, A.first);
     __shared__ SlotRec slots[kMaxFreeSlots * kFreeLanes];
     Contacts C;
     C.active = 0u;
@@ -467,24 +509,68 @@ __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) free_step(F, A.dt, A.pgs_iters, S, C);
     }
-    at(0) = S.p.x; at(1) = S.p.y; at(2) = S.p.z;
-    at(3) = S.qw; at(4) = S.qx; at(5) = S.qy; at(6) = S.qz;
-    at(7) = S.V.w.x; at(8) = S.V.w.y; at(9) = S.V.w.z;
-    at(10) = S.V.v.x; at(11) = S.V.v.y; at(12) = S.V.v.z;
+    store_base(D, W, w, S);
     if (want_contacts && !A.paused) {
         D.cmask[w] = C.active;
         const float inv_dt = 1.f / A.dt;
-        // force on the body, world frame: (n x_n + t1 x_t1 + t2 x_t2) / dt
         for (uint32_t m = C.active; m; m &= m - 1u) {
             const int slot = __builtin_ctz(m);
             const SlotRec& r = C.at(slot);
-            float* o = D.cdata + static_cast<size_t>(slot) * 7 * W + w;
-            // t1 = (0, -1, 0), t2 = (1, 0, 0), n = (0, 0, 1)
-            o[0 * W] = r.xw.x; o[1 * W] = r.xw.y; o[2 * W] = r.xw.z;
-            o[3 * W] = r.x[2] * inv_dt;
-            o[4 * W] = -r.x[1] * inv_dt;
-            o[5 * W] = r.x[0] * inv_dt;
-            o[6 * W] = r.depth;
+            store_contact(D, W, w, slot, r.xw, r.x[0], r.x[1], r.x[2], r.depth, inv_dt);
+        }
+    }
+}
+
+// Articulated model on a floating base (float_tree.hpp): the scenario run of
+// scenario_run_kernel (joint resets, commands, PID) plus the base state of
+// free_run_kernel.  ws: the per-world row workspace, FloatWs<N>::words(n_slots)
+// floats per world, [word][W].
+template <int N, Topo TOPO, bool CONS>
+__global__ void __launch_bounds__(64) float_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
+                                                       SimDev S, FreeDev D, PidSet pid, float* __restrict__ ws,
+                                                       int W, RunArgs A, int want_contacts) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    FloatBody<N> X;
+    X.base = load_base(D, W, w, A.first);
+    load_state<N>(S, W, w, X.q, X.qd);
+    if (A.first) joint_resets<N>(S, W, w, X.q, X.qd);
+    uint32_t active = 0u;
+    const WsRef wr = {ws + w, W};
+    if (!A.paused) {
+        float cmd[N], vc[N], tau[N], qdd[N];
+        uint8_t act[N];
+        bool any_pid = false;
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            cmd[d] = A.first ? S.cmd[d * W + w] : 0.f;
+            act[d] = S.act[d * W + w];
+            vc[d] = S.vtgt[d * W + w];
+            any_pid = any_pid || act[d] >= kActPidPos;
+        }
+        __shared__ BodyState sh_bs[N * kLdsLanes];
+        __shared__ SV7 sh_own[N * kLdsLanes];
+        LdsStage<N, false> stage{sh_bs + threadIdx.x, nullptr, sh_own + threadIdx.x, nullptr};
+        for (int s = 0; s < A.substeps; ++s) {
+            joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, X.q, X.qd, any_pid, tau);
+            active = float_step<N, TOPO, CONS>(P, F, X, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, wr);
+        }
+#pragma unroll
+        for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];
+    }
+#pragma unroll
+    for (int d = 0; d < N; ++d) S.cmd[d * W + w] = 0.f;
+    store_state<N>(S, W, w, X.q, X.qd);
+    store_base(D, W, w, X.base);
+    if (want_contacts && !A.paused) {
+        D.cmask[w] = active;
+        const float inv_dt = 1.f / A.dt;
+        using L = FloatWs<N>;
+        for (uint32_t m = active; m; m &= m - 1u) {
+            const int slot = __builtin_ctz(m);
+            const int o = slot * L::kSlotWords;
+            store_contact(D, W, w, slot, mk(wr.at(o + 3), wr.at(o + 4), wr.at(o + 5)), wr.at(o + 16), wr.at(o + 17),
+                          wr.at(o + 18), wr.at(o + 6), inv_dt);
         }
     }
 }
@@ -672,14 +758,54 @@ hipError_t vec_nk(const ChainF* P, bool cons, bool dual, int baked, const TaskF&
 }  // namespace
 
 int kernel_topology(const int* parents, int n) {
-    bool chain = true, panda = (n == 9);
+    bool chain = true, panda = (n == 9), quad = (n == 8);
     for (int i = 0; i < n; ++i) {
         chain = chain && parents[i] == i - 1;
         panda = panda && parents[i] == parent_of(kPandaTopo, i);
+        quad = quad && parents[i] == parent_of(kQuadrupedTopo, i);
     }
     if (chain && n >= 1 && n <= 9) return 0;
     if (panda) return 1;
+    if (quad) return 2;
     return -1;
+}
+
+int float_workspace_words(int n, int n_slots) {
+    switch (n) {
+    case 1: return dev::FloatWs<1>::words(n_slots);
+    case 2: return dev::FloatWs<2>::words(n_slots);
+    case 3: return dev::FloatWs<3>::words(n_slots);
+    case 8: return dev::FloatWs<8>::words(n_slots);
+    default: return -1;
+    }
+}
+
+namespace {
+template <int N, Topo TOPO>
+hipError_t float_n(const ChainF* P, bool cons, const FloatF* F, const SimDev& S, const FreeDev& D, const PidSet& pid,
+                   float* ws, int W, const RunArgs& a, int contacts, hipStream_t st) {
+    const int B = dev::kLdsLanes;  // LDS stage: one wave per workgroup
+    if (cons)
+        hipLaunchKernelGGL((dev::float_run_kernel<N, TOPO, true>), grid_for(W, B), dim3(B), 0, st, P, F, S, D, pid, ws,
+                           W, a, contacts);
+    else
+        hipLaunchKernelGGL((dev::float_run_kernel<N, TOPO, false>), grid_for(W, B), dim3(B), 0, st, P, F, S, D, pid,
+                           ws, W, a, contacts);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_float_run(const ChainF* P, int n, int topo, bool cons, const FloatF* F, const SimDev& S,
+                            const FreeDev& D, const PidSet& pid, float* ws, int W, const RunArgs& a, int contacts,
+                            hipStream_t st) {
+    if (topo == 2 && n == 8) return float_n<8, kQuadrupedTopo>(P, cons, F, S, D, pid, ws, W, a, contacts, st);
+    if (topo != 0) return hipErrorInvalidValue;
+    switch (n) {
+    case 1: return float_n<1, chain_topo(1)>(P, cons, F, S, D, pid, ws, W, a, contacts, st);
+    case 2: return float_n<2, chain_topo(2)>(P, cons, F, S, D, pid, ws, W, a, contacts, st);
+    case 3: return float_n<3, chain_topo(3)>(P, cons, F, S, D, pid, ws, W, a, contacts, st);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const SimDev& S,

@@ -80,7 +80,7 @@ struct VecDev {
 
 // Returns hipSuccess or the launch error.
 // topology id of a model's parent list: 0 = serial chain, 1 = Panda tree,
-// -1 = not compiled into this build
+// 2 = quadruped (floating base), -1 = not compiled into this build
 int kernel_topology(const int* parents, int n);
 
 hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const SimDev& S,
@@ -89,6 +89,14 @@ hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool
 // F: the model's FreeF block in device memory (free_body.hpp)
 hipError_t launch_free_run(const struct FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts,
                            hipStream_t st);
+
+// Articulated model on a floating base (float_tree.hpp); F: its FloatF block
+// in device memory, ws: FloatWs words per world x W floats (device).
+hipError_t launch_float_run(const ChainF* P, int n, int topo, bool cons, const struct FloatF* F, const SimDev& S,
+                            const FreeDev& D, const PidSet& pid, float* ws, int W, const RunArgs& a, int contacts,
+                            hipStream_t st);
+// workspace words per world of a floating-tree model, -1 if n is not compiled in
+int float_workspace_words(int n, int n_slots);
 
 hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const SimDev& S,
                                const VecDev& V, float* obs, int W, hipStream_t st);

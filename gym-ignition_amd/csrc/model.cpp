@@ -474,6 +474,7 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
         b.upper = j.upper;
         b.effort = j.effort;
         b.vel_limit = j.velocity;
+        b.shapes = L.shapes;
         if (b.mass <= 0.0) throw std::runtime_error("moving link '" + j.child + "' has no mass");
         out.bodies.push_back(b);
     }

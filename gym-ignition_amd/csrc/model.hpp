@@ -37,6 +37,7 @@ struct ChainBody {
     double damping = 0.0, friction = 0.0;
     double lower = -1e300, upper = 1e300;
     double effort = 1e300, vel_limit = 1e300;
+    std::vector<struct Shape> shapes;  // collision shapes of the (lumped) link, body frame
 };
 
 // A collision shape in its body's frame: box (size = half extents) or sphere

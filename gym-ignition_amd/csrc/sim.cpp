@@ -22,6 +22,7 @@
 
 #include "baked_models.hpp"
 #include "chain_params.hpp"
+#include "float_tree.hpp"
 #include "free_body.hpp"
 #include "kernels.hpp"
 #include "model.hpp"
@@ -102,6 +103,14 @@ struct mw_sim {
     std::vector<uint8_t> h_rflag;
     bool free_dirty = false;
     bool contacts_stale = false;  // contacts written on the device by mw_run_device
+    // articulated models on a floating base (float_tree.hpp): the joint state
+    // of a fixed-base model plus the base block above
+    bool float_tree = false;
+    mw::FloatF h_float{};
+    mw::FloatF* d_float = nullptr;
+    float* d_ws = nullptr;        // constraint-row workspace [words][W]
+    int n_slots = mw::kMaxFreeSlots;
+    std::vector<int32_t> slot_body;  // body of every contact slot (-1 = base)
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -246,7 +255,59 @@ void build_free(mw_sim* s) {
     }
 }
 
+// FloatF of an articulated floating model: base inertia about its origin,
+// shapes in the oracle's order (base first, then by body), their contact
+// slots and the bodies on each shape's path to the base.
+void build_float(mw_sim* s) {
+    mw::FloatF& F = s->h_float;
+    std::memset(&F, 0, sizeof(F));
+    const auto& M = s->model;
+    const double m = M.base_mass, *c = M.base_com.data(), *ic = M.base_Ic.data();
+    F.mass = static_cast<float>(m);
+    for (int k = 0; k < 3; ++k) F.com[k] = static_cast<float>(c[k]);
+    const double c2 = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    const double Io[6] = {ic[0] + m * (c2 - c[0] * c[0]), ic[1] + m * (c2 - c[1] * c[1]), ic[2] + m * (c2 - c[2] * c[2]),
+                          ic[3] - m * c[0] * c[1], ic[4] - m * c[0] * c[2], ic[5] - m * c[1] * c[2]};
+    for (int k = 0; k < 6; ++k) F.Io[k] = static_cast<float>(Io[k]);
+    for (int k = 0; k < 3; ++k) F.g[k] = static_cast<float>(s->gravity[k]);
+    F.mu = static_cast<float>(s->ground_mu);
+    F.ground = s->ground ? 1 : 0;
+    std::vector<std::pair<int, const mw::Shape*>> shapes;
+    for (const auto& sh : M.base_shapes) shapes.push_back({-1, &sh});
+    for (int b = 0; b < M.dofs(); ++b)
+        for (const auto& sh : M.bodies[b].shapes) shapes.push_back({b, &sh});
+    int slot = 0;
+    s->slot_body.clear();
+    for (size_t i = 0; i < shapes.size() && i < static_cast<size_t>(mw::kMaxFloatShapes); ++i) {
+        const int b = shapes[i].first;
+        const mw::Shape& sh = *shapes[i].second;
+        F.shape_body[i] = b;
+        F.shape_type[i] = sh.type;
+        F.shape_slot0[i] = slot;
+        uint32_t path = 0;
+        for (int k = b; k >= 0; k = M.bodies[k].parent) path |= 1u << k;
+        F.shape_path[i] = path;
+        for (int k = 0; k < 3; ++k) {
+            F.shape_size[i][k] = static_cast<float>(sh.size[k]);
+            F.shape_p[i][k] = static_cast<float>(sh.p[k]);
+        }
+        for (int k = 0; k < 9; ++k) F.shape_R[i][k] = static_cast<float>(sh.R[k]);
+        const int ns = (sh.type == mw::Shape::Sphere) ? 1 : 8;
+        for (int k = 0; k < ns; ++k) s->slot_body.push_back(b);
+        slot += ns;
+    }
+    F.n_shapes = static_cast<int32_t>(std::min(shapes.size(), static_cast<size_t>(mw::kMaxFloatShapes)));
+    F.n_slots = slot;
+}
+
 int upload_params(mw_sim* s) {
+    if (s->float_tree) {
+        build_params(s);
+        build_float(s);
+        MW_HIP(hipMemcpyAsync(s->d_params, &s->h_params, sizeof(mw::ChainF), hipMemcpyHostToDevice, s->stream));
+        MW_HIP(hipMemcpyAsync(s->d_float, &s->h_float, sizeof(mw::FloatF), hipMemcpyHostToDevice, s->stream));
+        return MW_OK;
+    }
     if (s->floating) {
         build_free(s);
         MW_HIP(hipMemcpyAsync(s->d_free, &s->h_free, sizeof(mw::FreeF), hipMemcpyHostToDevice, s->stream));
@@ -286,9 +347,11 @@ int pull_state(mw_sim* s) {
     if (s->floating) {
         MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * static_cast<size_t>(s->W) * sizeof(float),
                               hipMemcpyDeviceToHost, s->stream));
-        MW_HIP(hipStreamSynchronize(s->stream));
-        s->host_stale = false;
-        return MW_OK;
+        if (!s->float_tree) {
+            MW_HIP(hipStreamSynchronize(s->stream));
+            s->host_stale = false;
+            return MW_OK;
+        }
     }
     MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
     MW_HIP(hipStreamSynchronize(s->stream));
@@ -416,6 +479,8 @@ void mw_destroy(mw_sim* s) {
         (void)hipHostFree(s->h_ptgt);
         (void)hipFree(s->d_fblock);
         (void)hipFree(s->d_free);
+        (void)hipFree(s->d_float);
+        (void)hipFree(s->d_ws);
         (void)hipHostFree(s->h_base);
         (void)hipHostFree(s->h_cdata);
         (void)hipHostFree(s->h_cmask);
@@ -436,10 +501,38 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     if (s->model.dofs() > mw::kMaxKernelDofs || s->model.dofs() > 9)
         return fail(MW_EPARSE, "models with more than 9 dofs are not supported by this build");
     s->floating = s->model.floating;
+    s->float_tree = s->floating && s->model.dofs() > 0;
+    if (s->float_tree) {
+        std::vector<int> parents;
+        for (const auto& b : s->model.bodies) parents.push_back(b.parent);
+        s->topo = mw::kernel_topology(parents.data(), s->model.dofs());
+        size_t n_shapes = s->model.base_shapes.size();
+        for (const auto& b : s->model.bodies) {
+            n_shapes += b.shapes.size();
+            if (b.damping != 0.0)
+                return fail(MW_EPARSE, "joint damping on floating-base models is not compiled into this build "
+                                       "(joint '" + b.joint_name + "')");
+        }
+        if (n_shapes > static_cast<size_t>(mw::kMaxFloatShapes))
+            return fail(MW_EPARSE, "a floating-base model may have at most " +
+                                       std::to_string(mw::kMaxFloatShapes) + " box / sphere collision shapes");
+        s->n = s->model.dofs();
+        build_float(s);
+        if (s->h_float.n_slots > mw::kMaxFloatSlots)
+            return fail(MW_EPARSE, "a floating-base model may have at most " + std::to_string(mw::kMaxFloatSlots) +
+                                       " contact slots (8 per box, 1 per sphere)");
+        const bool compiled = (s->topo == 0 && s->n <= 3) || s->topo == 2;
+        if (!compiled || mw::float_workspace_words(s->n, s->h_float.n_slots) < 0)
+            return fail(MW_EPARSE, "the topology of this floating-base model is not compiled into this build "
+                                   "(supported: serial chains of 1..3 dofs and the quadruped tree)");
+        s->n_slots = s->h_float.n_slots;
+        s->pid.assign(s->model.dofs(), kDefaultPid);
+        s->model_name = (name && *name) ? name : s->model.name;
+        s->loaded = true;
+        build_params(s);
+        return MW_OK;
+    }
     if (s->floating) {
-        if (s->model.dofs() > 0)
-            return fail(MW_EPARSE, "floating-base models with joints are not compiled into this build yet "
-                                   "(single floating bodies are)");
         if (s->model.base_shapes.size() > static_cast<size_t>(mw::kMaxFreeShapes))
             return fail(MW_EPARSE, "a floating body may have at most " + std::to_string(mw::kMaxFreeShapes) +
                                        " box / sphere collision shapes in this build");
@@ -483,6 +576,17 @@ int mw_device_params(const mw_sim* s, void* out, int32_t bytes) {
     return MW_OK;
 }
 
+int mw_device_float_params(const mw_sim* s, void* out, int32_t bytes) {
+    if (!s || !out) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (!s->float_tree) return fail(MW_ESTATE, "not an articulated floating-base model");
+    if (bytes < static_cast<int32_t>(sizeof(mw::FloatF))) return fail(MW_EINVAL, "buffer too small");
+    mw_sim* m = const_cast<mw_sim*>(s);
+    build_float(m);
+    std::memcpy(out, &m->h_float, sizeof(mw::FloatF));
+    return MW_OK;
+}
+
 int mw_initialize(mw_sim* s) {
     if (!s) return fail(MW_EINVAL, "null simulator handle");
     if (s->initialized) return MW_OK;
@@ -496,9 +600,16 @@ int mw_initialize(mw_sim* s) {
     s->n = s->model.dofs();
     if (s->floating) {
         const size_t W = static_cast<size_t>(s->W);
-        const size_t nf = (13 + 7 + 6 + 7 * mw::kMaxFreeSlots) * W;
+        const size_t ns = static_cast<size_t>(s->n_slots);
+        const size_t nf = (13 + 7 + 6 + 7 * ns) * W;
         MW_HIP(hipMalloc(&s->d_fblock, nf * sizeof(float) + W * (1 + sizeof(uint32_t)) + 64));
-        MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_free), sizeof(mw::FreeF)));
+        if (s->float_tree) {
+            MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_float), sizeof(mw::FloatF)));
+            const size_t words = static_cast<size_t>(mw::float_workspace_words(s->n, s->n_slots));
+            MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ws), words * W * sizeof(float)));
+        } else {
+            MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_free), sizeof(mw::FreeF)));
+        }
         float* f = static_cast<float*>(s->d_fblock);
         s->fdev.base = f;
         s->fdev.rpose = f + 13 * W;
@@ -507,7 +618,7 @@ int mw_initialize(mw_sim* s) {
         s->fdev.cmask = reinterpret_cast<uint32_t*>(f + nf);
         s->fdev.rflag = reinterpret_cast<uint8_t*>(s->fdev.cmask + W);
         MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_base), 13 * W * sizeof(float), hipHostMallocDefault));
-        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_cdata), 7 * mw::kMaxFreeSlots * W * sizeof(float),
+        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_cdata), 7 * ns * W * sizeof(float),
                              hipHostMallocDefault));
         MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_cmask), W * sizeof(uint32_t), hipHostMallocDefault));
         std::memset(s->h_cmask, 0, W * sizeof(uint32_t));
@@ -539,11 +650,13 @@ int mw_initialize(mw_sim* s) {
         s->h_rpose.assign(7 * W, 0.f);
         s->h_rvel.assign(6 * W, 0.f);
         s->h_rflag.assign(W, 0);
-        s->initialized = true;
-        int rc = upload_params(s);
-        if (rc) return rc;
-        MW_HIP(hipStreamSynchronize(s->stream));
-        return MW_OK;
+        if (!s->float_tree) {
+            s->initialized = true;
+            int rc = upload_params(s);
+            if (rc) return rc;
+            MW_HIP(hipStreamSynchronize(s->stream));
+            return MW_OK;
+        }
     }
     s->nw = static_cast<size_t>(s->n) * s->W;
     s->state_bytes = 3 * s->nw * sizeof(float);
@@ -596,7 +709,8 @@ int mw_set_stream(mw_sim* s, void* stream) {
     return MW_OK;
 }
 
-static int run_free(mw_sim* s, int paused, bool readback = true) {
+// pending base resets: one H2D copy of [rpose | rvel] and the flags
+static int upload_base_resets(mw_sim* s) {
     const size_t W = static_cast<size_t>(s->W);
     if (s->free_dirty) {
         // pending base resets: one H2D copy of [rpose | rvel] and the flags
@@ -609,6 +723,24 @@ static int run_free(mw_sim* s, int paused, bool readback = true) {
         std::fill(s->h_rflag.begin(), s->h_rflag.end(), 0);
         s->free_dirty = false;
     }
+    return MW_OK;
+}
+
+// contacts + base of the last run -> host mirrors (queued on the stream)
+static int read_base(mw_sim* s, int paused) {
+    const size_t W = static_cast<size_t>(s->W);
+    MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * W * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    if (s->contacts && !paused) {
+        MW_HIP(hipMemcpyAsync(s->h_cmask, s->fdev.cmask, W * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipMemcpyAsync(s->h_cdata, s->fdev.cdata, 7 * static_cast<size_t>(s->n_slots) * W * sizeof(float),
+                              hipMemcpyDeviceToHost, s->stream));
+    }
+    return MW_OK;
+}
+
+static int run_free(mw_sim* s, int paused, bool readback = true) {
+    int rc = upload_base_resets(s);
+    if (rc) return rc;
     mw::RunArgs a{};
     a.dt = static_cast<float>(s->cfg.step_size);
     a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
@@ -626,12 +758,7 @@ static int run_free(mw_sim* s, int paused, bool readback = true) {
         s->contacts_stale = s->contacts;
         return MW_OK;
     }
-    MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * W * sizeof(float), hipMemcpyDeviceToHost, s->stream));
-    if (s->contacts && !paused) {
-        MW_HIP(hipMemcpyAsync(s->h_cmask, s->fdev.cmask, W * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-        MW_HIP(hipMemcpyAsync(s->h_cdata, s->fdev.cdata, 7 * mw::kMaxFreeSlots * W * sizeof(float),
-                              hipMemcpyDeviceToHost, s->stream));
-    }
+    if ((rc = read_base(s, paused))) return rc;
     MW_HIP(hipStreamSynchronize(s->stream));
     s->contacts_stale = false;
     return MW_OK;
@@ -643,7 +770,8 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     // a device-resident run never needs the host mirror (and must not
     // synchronise: it may be captured into a graph)
     if (readback && (rc = pull_state(s))) return rc;
-    if (s->floating) return run_free(s, paused, readback);
+    if (s->floating && !s->float_tree) return run_free(s, paused, readback);
+    if (s->float_tree && (rc = upload_base_resets(s))) return rc;
     if (s->cmd_dirty) {
         MW_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_block) + s->cmd_off, s->h_block + s->cmd_off,
                               s->cmd_bytes, hipMemcpyHostToDevice, s->stream));
@@ -677,16 +805,23 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
                 a.pid_gate |= (uint64_t{1} << k);
             }
         }
-        MW_HIP(mw::launch_scenario_run(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), baked_id(s), s->dev, pid,
-                                       s->W, a, s->stream));
+        if (s->float_tree)
+            MW_HIP(mw::launch_float_run(s->d_params, s->n, s->topo, needs_cons(s), s->d_float, s->dev, s->fdev, pid,
+                                        s->d_ws, s->W, a, s->contacts ? 1 : 0, s->stream));
+        else
+            MW_HIP(mw::launch_scenario_run(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), baked_id(s),
+                                           s->dev, pid, s->W, a, s->stream));
         a.first = 0;
         done += chunk;
     } while (!paused && done < spr);
     if (readback) {
         MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
+        if (s->float_tree && (rc = read_base(s, paused))) return rc;
         MW_HIP(hipStreamSynchronize(s->stream));
+        s->contacts_stale = false;
     } else {
         s->host_stale = true;
+        s->contacts_stale = s->float_tree && s->contacts;
     }
     // mirror the kernel's component semantics on the host copy
     std::memset(s->hcmd(), 0, s->nw * sizeof(float));
@@ -748,6 +883,12 @@ int mw_joint_name(const mw_sim* s, int32_t dof, char* buf, int32_t len) {
     if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
     if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
     return copy_str(s->model.bodies[dof].joint_name, buf, len);
+}
+
+int mw_link_name(const mw_sim* s, int32_t dof, char* buf, int32_t len) {
+    if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
+    return copy_str(s->model.bodies[dof].link_name, buf, len);
 }
 
 int mw_joint_index(const mw_sim* s, const char* name, int32_t* dof) {
@@ -1131,7 +1272,8 @@ int mw_set_ground_plane(mw_sim* s, int32_t enabled, double mu) {
     s->ground = enabled != 0;
     s->ground_mu = mu;
     if (s->floating && s->initialized) return upload_params(s);
-    if (s->floating && s->loaded) build_free(s);
+    if (s->float_tree && s->loaded) build_float(s);
+    else if (s->floating && s->loaded) build_free(s);
     return MW_OK;
 }
 
@@ -1160,7 +1302,7 @@ int mw_get_contacts(const mw_sim* s, int32_t w, double* out, int32_t cap, int32_
         mw_sim* m = const_cast<mw_sim*>(s);
         const size_t Wc = static_cast<size_t>(s->W);
         MW_HIP(hipMemcpyAsync(m->h_cmask, s->fdev.cmask, Wc * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-        MW_HIP(hipMemcpyAsync(m->h_cdata, s->fdev.cdata, 7 * mw::kMaxFreeSlots * Wc * sizeof(float),
+        MW_HIP(hipMemcpyAsync(m->h_cdata, s->fdev.cdata, 7 * static_cast<size_t>(s->n_slots) * Wc * sizeof(float),
                               hipMemcpyDeviceToHost, s->stream));
         MW_HIP(hipStreamSynchronize(s->stream));
         m->contacts_stale = false;
@@ -1170,7 +1312,7 @@ int mw_get_contacts(const mw_sim* s, int32_t w, double* out, int32_t cap, int32_
     const size_t W = static_cast<size_t>(s->W);
     const uint32_t mask = s->h_cmask[w];
     int32_t k = 0;
-    for (int slot = 0; slot < mw::kMaxFreeSlots; ++slot) {
+    for (int slot = 0; slot < s->n_slots; ++slot) {
         if (!((mask >> slot) & 1u)) continue;
         if (k < cap) {
             const float* c = s->h_cdata + static_cast<size_t>(slot) * 7 * W + w;
@@ -1180,6 +1322,26 @@ int mw_get_contacts(const mw_sim* s, int32_t w, double* out, int32_t cap, int32_
             o[6] = c[3 * W]; o[7] = c[4 * W]; o[8] = c[5 * W];
             o[9] = c[6 * W];
         }
+        ++k;
+    }
+    *n = k;
+    return MW_OK;
+}
+
+int mw_get_contact_bodies(const mw_sim* s, int32_t w, int32_t* out, int32_t cap, int32_t* n) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!n || (cap > 0 && !out)) return fail(MW_EINVAL, "null argument");
+    if (w < 0 || w >= s->W) return fail(MW_EINVAL, "world index out of range");
+    double scratch[10];
+    int32_t total = 0;
+    // the same slot walk as mw_get_contacts (fills the host mirror if stale)
+    if ((rc = mw_get_contacts(s, w, scratch, 0, &total))) return rc;
+    const uint32_t mask = (s->floating && s->contacts) ? s->h_cmask[w] : 0u;
+    int32_t k = 0;
+    for (int slot = 0; slot < s->n_slots; ++slot) {
+        if (!((mask >> slot) & 1u)) continue;
+        if (k < cap) out[k] = s->float_tree ? s->slot_body[slot] : -1;
         ++k;
     }
     *n = k;

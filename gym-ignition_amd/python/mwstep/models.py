@@ -11,6 +11,7 @@ _FILES = {
     "pendulum": "pendulum.urdf",
     "panda": "panda.urdf",
     "cube": "cube.urdf",
+    "quadruped": "quadruped.urdf",
     "ground_plane": "ground_plane.sdf",
 }
 

@@ -88,6 +88,7 @@ SIGNATURES = [
     ("mw_n_worlds", ctypes.c_int, [_P, _IP]),
     ("mw_dofs", ctypes.c_int, [_P, _IP]),
     ("mw_joint_name", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
+    ("mw_link_name", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
     ("mw_joint_index", ctypes.c_int, [_P, _S, _IP]),
     ("mw_joint_type", ctypes.c_int, [_P, _I, _IP]),
     ("mw_model_name", ctypes.c_int, [_P, ctypes.c_char_p, _I]),
@@ -96,6 +97,7 @@ SIGNATURES = [
     ("mw_joint_param", ctypes.c_int, [_P, _I, _I, _D]),
     ("mw_model_export", ctypes.c_int, [_P, _D, _I]),
     ("mw_device_params", ctypes.c_int, [_P, _P, _I]),
+    ("mw_device_float_params", ctypes.c_int, [_P, _P, _I]),
     ("mw_baked_model", ctypes.c_int, [_P, _IP]),
     ("mw_get_joint_positions", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
     ("mw_get_joint_velocities", ctypes.c_int, [_P, _I, _I, _IP, _I, _D]),
@@ -124,6 +126,7 @@ SIGNATURES = [
     ("mw_enable_contacts", ctypes.c_int, [_P, _I]),
     ("mw_contacts_enabled", ctypes.c_int, [_P, _IP]),
     ("mw_get_contacts", ctypes.c_int, [_P, _I, _D, _I, _IP]),
+    ("mw_get_contact_bodies", ctypes.c_int, [_P, _I, _IP, _I, _IP]),
     ("mw_device_ptr", ctypes.c_int, [_P, _S, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("mw_vecenv_create", ctypes.c_int, [_P, ctypes.POINTER(MwTaskConfig), ctypes.POINTER(_P)]),

@@ -59,6 +59,11 @@ class Simulator:
         self.model_name = buf.value.decode()
         N.check(L.mw_base_frame(h, buf, 256))
         self.base_frame = buf.value.decode()
+        # links moved by the joints, in dof order (the base link is not among them)
+        self.link_names: List[str] = []
+        for d in range(self.dofs):
+            N.check(L.mw_link_name(h, d, buf, 256))
+            self.link_names.append(buf.value.decode())
         self._index = {n_: i for i, n_ in enumerate(self.joint_names)}
 
     # ------------------------------------------------------------------
@@ -232,6 +237,15 @@ class Simulator:
         out = np.zeros((cap, 10))
         n = ctypes.c_int32()
         N.check(N.lib().mw_get_contacts(self.handle, w, N.dptr(out), cap, ctypes.byref(n)), "contacts")
+        return out[:min(n.value, cap)].copy()
+
+    def contact_bodies(self, w: int = 0) -> np.ndarray:
+        """Body of every row of contacts(w): -1 = base link, i = the link of joint i."""
+        cap = 64
+        out = np.zeros(cap, dtype=np.int32)
+        n = ctypes.c_int32()
+        N.check(N.lib().mw_get_contact_bodies(self.handle, w, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                              cap, ctypes.byref(n)), "contact_bodies")
         return out[:min(n.value, cap)].copy()
 
     def export_model(self) -> np.ndarray:

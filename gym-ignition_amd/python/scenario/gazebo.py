@@ -287,6 +287,7 @@ class Model:
         self._pose = pose
         self._joints = {n: Joint(self, i, n) for i, n in enumerate(sim.joint_names)}
         self._pending_vel = None
+        self._export = None  # exported model rows (link forward kinematics)
         self._history: Optional[collections.deque] = None
 
     # -- identity
@@ -396,19 +397,61 @@ class Model:
         linear = self._pending_vel[0] if self._pending_vel else self.base_world_linear_velocity()
         return self.reset_base_world_velocity(linear, angular)
 
-    # -- links and contacts (the floating base link; Link.cpp)
+    # -- links and contacts (Link.cpp): the base link and the link of every joint
     def link_names(self, scoped: bool = False) -> List[str]:
-        base = self._sim.base_frame
-        return [f"{self._name}::{base}" if scoped else base]
+        # Model::linkNames (Model.cpp:479-520); links lumped by fixed joints do not exist
+        names = [self._sim.base_frame] + list(self._sim.link_names)
+        return [f"{self._name}::{n}" for n in names] if scoped else names
 
     def get_link(self, link_name: str) -> "Link":
-        if link_name != self._sim.base_frame:
-            raise RuntimeError(f"Link '{link_name}' not available in model '{self._name}' "
-                               "(this build exposes the base link)")
-        return Link(self, link_name)
+        if link_name == self._sim.base_frame:
+            return Link(self, link_name, -1)
+        if link_name in self._sim.link_names:
+            return Link(self, link_name, self._sim.link_names.index(link_name))
+        raise RuntimeError(f"Link '{link_name}' not found in model '{self._name}'")
 
     def links(self, link_names: Sequence[str] = ()) -> List["Link"]:
         return [self.get_link(n) for n in (link_names or self.link_names())]
+
+    def _link_state(self, body: int):
+        """World pose (R, p) and world velocity (linear of the link origin,
+        angular) of `body` (-1 = base) by forward kinematics of the exported
+        model (joint origin E, r, axis per body) from the base state."""
+        R = self._base_R()
+        p = np.array(self.base_position(), dtype=float)
+        v = np.array(self.base_world_linear_velocity(), dtype=float)
+        w = np.array(self.base_world_angular_velocity(), dtype=float)
+        if body < 0:
+            return R, p, v, w
+        if self._export is None:
+            n = self._sim.dofs
+            self._export = self._sim.export_model()[:34 * n].reshape(n, 34)
+        rows = self._export
+        path = []
+        k = body
+        while k >= 0:
+            path.append(k)
+            k = int(rows[k, 33])
+        q = self._sim.get("q")[0]
+        qd = self._sim.get("qd")[0]
+        for j in reversed(path):
+            row = rows[j]
+            E, r, a = row[2:11].reshape(3, 3), row[11:14], row[14:17]
+            if row[0] == 0:  # revolute: Rodrigues about the child-frame axis
+                c, sn = np.cos(q[j]), np.sin(q[j])
+                K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+                Rr, pr = E @ (np.eye(3) + sn * K + (1 - c) * K @ K), r
+            else:
+                Rr, pr = E, r + q[j] * (E @ a)
+            pn = p + R @ pr
+            v = v + np.cross(w, pn - p)
+            R = R @ Rr
+            if row[0] == 0:
+                w = w + R @ a * qd[j]
+            else:
+                v = v + R @ a * qd[j]
+            p = pn
+        return R, p, v, w
 
     def contacts_enabled(self) -> bool:
         return self._sim.contacts_enabled()
@@ -418,8 +461,12 @@ class Model:
         self._sim.enable_contacts(enable)
         return True
 
-    def contacts(self) -> List[core.Contact]:
-        return Link(self, self._sim.base_frame).contacts()
+    def contacts(self, link_names: Sequence[str] = ()) -> List[core.Contact]:
+        # Model::contacts (Model.cpp:739-755): the contacts of every (selected) link
+        out: List[core.Contact] = []
+        for ln in (link_names or self.link_names()):
+            out.extend(self.get_link(ln).contacts())
+        return out
 
     def controller_period(self) -> float:
         # Model::controllerPeriod (Model.cpp:581-587)
@@ -536,11 +583,12 @@ class Model:
 
 
 class Link:
-    """The base link of a model (Link.cpp): pose, velocity and contacts."""
+    """A link of a model (Link.cpp): pose, velocity and contacts."""
 
-    def __init__(self, model: "Model", name: str):
+    def __init__(self, model: "Model", name: str, body: int = -1):
         self._model = model
         self._name = name
+        self._body = body  # -1 = the base link, i = the link moved by joint i
 
     def to_gazebo(self) -> "Link":
         return self
@@ -549,16 +597,18 @@ class Link:
         return f"{self._model.name()}::{self._name}" if scoped else self._name
 
     def position(self) -> List[float]:
-        return self._model.base_position()
+        return self._model._link_state(self._body)[1].tolist()
 
     def orientation(self) -> List[float]:
-        return self._model.base_orientation()
+        # wxyz of the link rotation
+        R = self._model._link_state(self._body)[0]
+        return _quat_from_R(R)
 
     def world_linear_velocity(self) -> List[float]:
-        return self._model.base_world_linear_velocity()
+        return self._model._link_state(self._body)[2].tolist()
 
     def world_angular_velocity(self) -> List[float]:
-        return self._model.base_world_angular_velocity()
+        return self._model._link_state(self._body)[3].tolist()
 
     def contacts_enabled(self) -> bool:
         return self._model.contacts_enabled()
@@ -570,10 +620,14 @@ class Link:
         # Link::contacts (Link.cpp:365-434): the points of one body pair are
         # merged into one Contact; the ground plane is the only other body here
         sim = self._model._sim
-        if not sim.contacts_enabled():
+        if not sim.floating or not sim.contacts_enabled():
             return []
         rows = sim.contacts(0)
         if len(rows) == 0:
+            return []
+        bodies = sim.contact_bodies(0)
+        rows = [r for r, b in zip(rows, bodies) if b == self._body]
+        if not rows:
             return []
         ground = self._model._world._ground_name or "ground_plane::link"
         pts = [core.ContactPoint(r[0:3], r[3:6], r[6:9], (0.0, 0.0, 0.0), r[9]) for r in rows]
@@ -593,6 +647,23 @@ class Link:
                 f += fp
                 t += np.cross(np.array(p.position) - o, fp)
         return np.concatenate([f, t]).tolist()
+
+
+def _quat_from_R(R: np.ndarray) -> List[float]:
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    if tr > 0:
+        k = 0.5 / np.sqrt(tr + 1.0)
+        q = [0.25 / k, (R[2, 1] - R[1, 2]) * k, (R[0, 2] - R[2, 0]) * k, (R[1, 0] - R[0, 1]) * k]
+    elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        k = 2.0 * np.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2])
+        q = [(R[2, 1] - R[1, 2]) / k, 0.25 * k, (R[0, 1] + R[1, 0]) / k, (R[0, 2] + R[2, 0]) / k]
+    elif R[1, 1] > R[2, 2]:
+        k = 2.0 * np.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2])
+        q = [(R[0, 2] - R[2, 0]) / k, (R[0, 1] + R[1, 0]) / k, 0.25 * k, (R[1, 2] + R[2, 1]) / k]
+    else:
+        k = 2.0 * np.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1])
+        q = [(R[1, 0] - R[0, 1]) / k, (R[0, 2] + R[2, 0]) / k, (R[1, 2] + R[2, 1]) / k, 0.25 * k]
+    return [float(x) for x in q]
 
 
 class StaticModel:

@@ -1015,3 +1015,383 @@ void or_vec_rollout(const or_model* m, const or_task* t, int W, int T, double* q
                     pgs_iters);
     }
 }
+
+/* ---------------- articulated floating base + ground contacts ---------------- */
+
+/* Generalized velocity nu = [V0 (base twist, base frame, [w; v]); qd], the
+ * coordinates of a DART skeleton whose root joint is a FreeJoint [EXT: DART
+ * 6 FreeJoint, relative-twist parameterisation].  Restated densely:
+ *   M(q) nu' + h(q, nu) = [0; tau]      (CRBA for M, RNEA for h; Featherstone
+ *                                        2008 ch. 6 / 5 with a floating root)
+ * DART's implicit joint damping solves (M + dt D) nu' = tau - h - D qd (the
+ * recursive ABA of DART applies the same dt*d term to each joint's
+ * articulated inertia); constraint impulses use the non-implicit M, as DART's
+ * impulse propagation does.  The device kernel runs the recursive form
+ * (float_tree.hpp); this dense path is deliberately independent. */
+
+typedef struct {
+    double X[OR_MAXB][36];        /* parent -> body (Plucker)             */
+    double S[OR_MAXB][6];
+    double Rw[OR_MAXB][9], pw[OR_MAXB][3];  /* body pose in the world     */
+} or_fkin;
+
+static void float_kin(const or_float_model* m, const or_float_state* s, or_fkin* k)
+{
+    const or_model* t = &m->tree;
+    for (int i = 0; i < t->n; ++i) {
+        double R[9], p[3];
+        joint_pose(t, i, s->q[i], R, p);
+        plucker(R, p, k->X[i]);
+        motion_subspace(t, i, k->S[i]);
+        const int pa = t->parent[i];
+        const double* Rp = pa < 0 ? s->R : k->Rw[pa];
+        const double* pp = pa < 0 ? s->p : k->pw[pa];
+        for (int r = 0; r < 3; ++r) {
+            k->pw[i][r] = pp[r] + Rp[r * 3] * p[0] + Rp[r * 3 + 1] * p[1] + Rp[r * 3 + 2] * p[2];
+            for (int c = 0; c < 3; ++c)
+                k->Rw[i][r * 3 + c] = Rp[r * 3] * R[c] + Rp[r * 3 + 1] * R[3 + c] + Rp[r * 3 + 2] * R[6 + c];
+        }
+    }
+}
+
+static void base_inertia(const or_float_model* m, double I[36])
+{
+    or_model one;
+    memset(&one, 0, sizeof one);
+    one.n = 1;
+    one.mass[0] = m->base_mass;
+    memcpy(one.com[0], m->base_com, sizeof m->base_com);
+    memcpy(one.Ic[0], m->base_Ic, sizeof m->base_Ic);
+    body_inertia(&one, 0, I);
+}
+
+void or_float_dynamics(const or_float_model* m, const or_float_state* s, double* M, double* h)
+{
+    const or_model* t = &m->tree;
+    const int n = t->n, nv = 6 + n;
+    or_fkin k;
+    float_kin(m, s, &k);
+
+    /* CRBA: composite inertias accumulate towards the base */
+    double Ic[OR_MAXB][36], I0[36];
+    for (int i = 0; i < n; ++i) body_inertia(t, i, Ic[i]);
+    base_inertia(m, I0);
+    for (int i = n - 1; i >= 0; --i) {
+        double c[36];
+        m6_congruence(k.X[i], Ic[i], c);
+        double* dst = t->parent[i] < 0 ? I0 : Ic[t->parent[i]];
+        for (int e = 0; e < 36; ++e) dst[e] += c[e];
+    }
+    for (int e = 0; e < nv * nv; ++e) M[e] = 0.0;
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c) M[r * nv + c] = I0[r * 6 + c];
+    for (int i = 0; i < n; ++i) {
+        double F[6];
+        m6_vec(Ic[i], k.S[i], F);
+        M[(6 + i) * nv + 6 + i] = dot6(k.S[i], F);
+        int j = i;
+        for (;;) {
+            double Fp[6];
+            m6t_vec(k.X[j], F, Fp);
+            memcpy(F, Fp, sizeof F);
+            j = t->parent[j];
+            if (j < 0) break;
+            M[(6 + i) * nv + 6 + j] = M[(6 + j) * nv + 6 + i] = dot6(k.S[j], F);
+        }
+        for (int r = 0; r < 6; ++r) M[(6 + i) * nv + r] = M[r * nv + 6 + i] = F[r];
+    }
+
+    /* RNEA with nu' = 0; gravity as the base "acceleration" -g0 */
+    double g0[3];
+    for (int r = 0; r < 3; ++r)
+        g0[r] = s->R[r] * m->gravity[0] + s->R[3 + r] * m->gravity[1] + s->R[6 + r] * m->gravity[2];
+    const double a0[6] = {0, 0, 0, -g0[0], -g0[1], -g0[2]};
+    double V[OR_MAXB][6], a[OR_MAXB][6], f[OR_MAXB][6], f0[6];
+    {
+        double dd[6], Ib[36], Ia[6], IbV[6];  /* the base's own inertia (I0 is composite) */
+        base_inertia(m, Ib);
+        m6_vec(Ib, a0, Ia);
+        m6_vec(Ib, s->V, IbV);
+        sp_dad(s->V, IbV, dd);
+        for (int e = 0; e < 6; ++e) f0[e] = Ia[e] - dd[e];
+    }
+    for (int i = 0; i < n; ++i) {
+        const int pa = t->parent[i];
+        double Vp[6], ap[6], Sq[6], c[6], I[36], Ia[6], IV[6], dd[6];
+        m6_vec(k.X[i], pa < 0 ? s->V : V[pa], Vp);
+        m6_vec(k.X[i], pa < 0 ? a0 : a[pa], ap);
+        for (int e = 0; e < 6; ++e) { Sq[e] = k.S[i][e] * s->qd[i]; V[i][e] = Vp[e] + Sq[e]; }
+        sp_ad(V[i], Sq, c);
+        for (int e = 0; e < 6; ++e) a[i][e] = ap[e] + c[e];
+        body_inertia(t, i, I);
+        m6_vec(I, a[i], Ia);
+        m6_vec(I, V[i], IV);
+        sp_dad(V[i], IV, dd);
+        for (int e = 0; e < 6; ++e) f[i][e] = Ia[e] - dd[e];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        h[6 + i] = dot6(k.S[i], f[i]);
+        double fp[6];
+        m6t_vec(k.X[i], f[i], fp);
+        double* dst = t->parent[i] < 0 ? f0 : f[t->parent[i]];
+        for (int e = 0; e < 6; ++e) dst[e] += fp[e];
+    }
+    for (int e = 0; e < 6; ++e) h[e] = f0[e];
+}
+
+/* dense solve A x = b (n <= 6 + OR_MAXB), partial pivoting */
+static void solve_dense(int n, const double* A_in, const double* b, double* x)
+{
+    double A[(6 + OR_MAXB) * (6 + OR_MAXB)], y[6 + OR_MAXB];
+    memcpy(A, A_in, (size_t)n * n * sizeof(double));
+    memcpy(y, b, (size_t)n * sizeof(double));
+    for (int c = 0; c < n; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < n; ++r)
+            if (fabs(A[r * n + c]) > fabs(A[piv * n + c])) piv = r;
+        if (piv != c) {
+            for (int e = 0; e < n; ++e) { double tt = A[c * n + e]; A[c * n + e] = A[piv * n + e]; A[piv * n + e] = tt; }
+            double tt = y[c]; y[c] = y[piv]; y[piv] = tt;
+        }
+        for (int r = c + 1; r < n; ++r) {
+            const double fr = A[r * n + c] / A[c * n + c];
+            for (int e = c; e < n; ++e) A[r * n + e] -= fr * A[c * n + e];
+            y[r] -= fr * y[c];
+        }
+    }
+    for (int r = n - 1; r >= 0; --r) {
+        double acc = y[r];
+        for (int e = r + 1; e < n; ++e) acc -= A[r * n + e] * x[e];
+        x[r] = acc / A[r * n + r];
+    }
+}
+
+/* generalized row of a spatial "direction" f (body-k frame, force-like):
+ * J . nu = f . V_k.  f climbs to the base through X^T. */
+static void float_row(const or_float_model* m, const or_fkin* k, int body, const double f_in[6], double* J)
+{
+    const or_model* t = &m->tree;
+    const int nv = 6 + t->n;
+    double f[6];
+    memcpy(f, f_in, sizeof f);
+    for (int e = 0; e < nv; ++e) J[e] = 0.0;
+    for (int i = body; i >= 0; i = t->parent[i]) {
+        J[6 + i] = dot6(k->S[i], f);
+        double fp[6];
+        m6t_vec(k->X[i], f, fp);
+        memcpy(f, fp, sizeof f);
+    }
+    for (int e = 0; e < 6; ++e) J[e] = f[e];
+}
+
+int or_float_step(const or_float_model* m, double dt, or_float_state* s, const int32_t* mode,
+                  const double* cmd, int pgs_iters, double* c_pos, double* c_force, double* c_depth,
+                  int32_t* c_body)
+{
+    const or_model* t = &m->tree;
+    const int n = t->n, nv = 6 + n;
+    or_fkin k;
+    float_kin(m, s, &k);
+
+    static double M[(6 + OR_MAXB) * (6 + OR_MAXB)];
+    double h[6 + OR_MAXB], rhs[6 + OR_MAXB], acc[6 + OR_MAXB], nu[6 + OR_MAXB];
+    or_float_dynamics(m, s, M, h);
+    double Mi[(6 + OR_MAXB) * (6 + OR_MAXB)];
+    memcpy(Mi, M, (size_t)nv * nv * sizeof(double));
+    for (int e = 0; e < 6; ++e) { rhs[e] = -h[e]; nu[e] = s->V[e]; }
+    for (int i = 0; i < n; ++i) {
+        double tau = 0.0;
+        if (mode[i] == OR_FORCE) {
+            tau = cmd[i];
+            if (tau < -t->effort[i]) tau = -t->effort[i];
+            if (tau > t->effort[i]) tau = t->effort[i];
+        }
+        rhs[6 + i] = tau - h[6 + i] - t->damping[i] * s->qd[i];
+        Mi[(6 + i) * nv + 6 + i] += dt * t->damping[i];
+        nu[6 + i] = s->qd[i];
+    }
+    solve_dense(nv, Mi, rhs, acc);
+    for (int e = 0; e < nv; ++e) nu[e] += dt * acc[e];
+
+    /* ground contacts (positions of the start of the step), then joint rows
+     * -- the order of DART ConstraintSolver::updateConstraints [EXT] */
+    int nc = 0;
+    double cw[OR_MAXFC][3], depth[OR_MAXFC], cb[OR_MAXFC][3];
+    int cbody[OR_MAXFC];
+    if (m->ground) {
+        for (int sh = 0; sh < m->n_shapes; ++sh) {
+            const int bi = m->shape_body[sh];
+            const double* Rb = bi < 0 ? s->R : k.Rw[bi];
+            const double* pb = bi < 0 ? s->p : k.pw[bi];
+            const double* hh = m->shape_size[sh];
+            const double* SR = m->shape_R[sh];
+            const double* sp = m->shape_p[sh];
+            const int corners = (m->shape_type[sh] == 0) ? 8 : 1;
+            for (int corner = 0; corner < corners; ++corner) {
+                double l[3] = {0, 0, 0};
+                if (m->shape_type[sh] == 0) {
+                    l[0] = (corner & 4) ? hh[0] : -hh[0];
+                    l[1] = (corner & 2) ? hh[1] : -hh[1];
+                    l[2] = (corner & 1) ? hh[2] : -hh[2];
+                }
+                double b[3], x[3];
+                for (int r = 0; r < 3; ++r) b[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
+                for (int r = 0; r < 3; ++r) x[r] = pb[r] + Rb[r * 3] * b[0] + Rb[r * 3 + 1] * b[1] + Rb[r * 3 + 2] * b[2];
+                double dep = -x[2];
+                if (m->shape_type[sh] == 1) {
+                    dep = hh[0] - x[2];
+                    x[2] -= hh[0];
+                    double d[3] = {x[0] - pb[0], x[1] - pb[1], x[2] - pb[2]};
+                    for (int r = 0; r < 3; ++r) b[r] = Rb[r] * d[0] + Rb[3 + r] * d[1] + Rb[6 + r] * d[2];
+                }
+                if (dep > 0.0 && nc < OR_MAXFC) {
+                    memcpy(cw[nc], x, sizeof x);
+                    memcpy(cb[nc], b, sizeof b);
+                    depth[nc] = dep;
+                    cbody[nc] = bi;
+                    ++nc;
+                }
+            }
+        }
+    }
+
+    /* rows: J, rhs, bounds kind */
+    enum { K_NORMAL, K_FRIC, K_BOX };
+    static double J[3 * OR_MAXFC + 3 * OR_MAXB][6 + OR_MAXB];
+    static double MJ[3 * OR_MAXFC + 3 * OR_MAXB][6 + OR_MAXB];
+    static double A[(3 * OR_MAXFC + 3 * OR_MAXB) * (3 * OR_MAXFC + 3 * OR_MAXB)];
+    double bb[3 * OR_MAXFC + 3 * OR_MAXB], lo[3 * OR_MAXFC + 3 * OR_MAXB], hi[3 * OR_MAXFC + 3 * OR_MAXB];
+    double cfm[3 * OR_MAXFC + 3 * OR_MAXB], x[3 * OR_MAXFC + 3 * OR_MAXB];
+    int kind[3 * OR_MAXFC + 3 * OR_MAXB];
+    int nr = 0;
+    const double nrm[3] = {0, 0, 1};
+    double t1[3], t2[3];
+    plane_space(nrm, t1, t2);
+    for (int c = 0; c < nc; ++c) {
+        const int bi = cbody[c];
+        const double* Rb = bi < 0 ? s->R : k.Rw[bi];
+        for (int d = 0; d < 3; ++d) {
+            const double* dw = d == 0 ? nrm : (d == 1 ? t1 : t2);
+            double f[6];
+            for (int r = 0; r < 3; ++r) f[3 + r] = Rb[r] * dw[0] + Rb[3 + r] * dw[1] + Rb[6 + r] * dw[2];
+            cross3(cb[c], f + 3, f);
+            if (bi < 0) {
+                for (int e = 0; e < nv; ++e) J[nr][e] = 0.0;
+                for (int e = 0; e < 6; ++e) J[nr][e] = f[e];
+            } else {
+                float_row(m, &k, bi, f, J[nr]);
+            }
+            double vrel = 0.0;
+            for (int e = 0; e < nv; ++e) vrel += J[nr][e] * nu[e];
+            double bounce = 0.0;
+            if (d == 0) {
+                bounce = OR_C_ERP * depth[c] / dt;
+                if (bounce > OR_C_MAX_ERV) bounce = OR_C_MAX_ERV;
+            }
+            bb[nr] = -vrel + bounce;
+            kind[nr] = d == 0 ? K_NORMAL : K_FRIC;
+            cfm[nr] = OR_C_CFM;
+            ++nr;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        const double qdi = nu[6 + i];
+        int rows_i[3], nri = 0;
+        if (t->limited[i]) {
+            double viol = s->q[i] - t->lower[i];
+            int active = 0;
+            if (viol <= 0.0) { lo[nr] = 0.0; hi[nr] = INFINITY; active = 1; }
+            else {
+                viol = s->q[i] - t->upper[i];
+                if (viol >= 0.0) { lo[nr] = -INFINITY; hi[nr] = 0.0; active = 1; }
+            }
+            if (active) {
+                double bounce = -viol * OR_ERP / dt;
+                if (bounce > OR_MAX_ERV) bounce = OR_MAX_ERV;
+                if (bounce < -OR_MAX_ERV) bounce = -OR_MAX_ERV;
+                bb[nr] = -qdi + bounce;
+                rows_i[nri++] = nr++;
+            }
+        }
+        if (mode[i] == OR_SERVO) {
+            double vc = cmd[i];
+            if (vc < -t->vel_limit[i]) vc = -t->vel_limit[i];
+            if (vc > t->vel_limit[i]) vc = t->vel_limit[i];
+            if (vc - qdi != 0.0) {
+                bb[nr] = vc - qdi;
+                lo[nr] = -t->effort[i] * dt;
+                hi[nr] = t->effort[i] * dt;
+                rows_i[nri++] = nr++;
+            }
+        }
+        if (t->friction[i] != 0.0 && qdi != 0.0) {
+            bb[nr] = -qdi;
+            hi[nr] = t->friction[i] * dt;
+            lo[nr] = -hi[nr];
+            rows_i[nri++] = nr++;
+        }
+        for (int r = 0; r < nri; ++r) {
+            const int row = rows_i[r];
+            for (int e = 0; e < nv; ++e) J[row][e] = 0.0;
+            J[row][6 + i] = 1.0;
+            kind[row] = K_BOX;
+            cfm[row] = OR_CFM;
+        }
+    }
+    if (nr > 0) {
+        for (int r = 0; r < nr; ++r) solve_dense(nv, M, J[r], MJ[r]);
+        for (int r = 0; r < nr; ++r) {
+            for (int c = 0; c < nr; ++c) {
+                double a = 0.0;
+                for (int e = 0; e < nv; ++e) a += J[r][e] * MJ[c][e];
+                A[r * nr + c] = a;
+            }
+            A[r * nr + r] *= 1.0 + cfm[r];
+            x[r] = 0.0;
+        }
+        for (int it = 0; it < pgs_iters; ++it)
+            for (int r = 0; r < nr; ++r) {
+                double acc_r = bb[r];
+                for (int c = 0; c < nr; ++c) acc_r -= A[r * nr + c] * x[c];
+                double v = x[r] + acc_r / A[r * nr + r];
+                double l = lo[r], u = hi[r];
+                if (kind[r] == K_NORMAL) { l = 0.0; u = INFINITY; }
+                else if (kind[r] == K_FRIC) {
+                    const int nrow = r - (r % 3);
+                    u = m->mu * x[nrow];
+                    l = -u;
+                }
+                if (v < l) v = l;
+                if (v > u) v = u;
+                x[r] = v;
+            }
+        for (int r = 0; r < nr; ++r)
+            for (int e = 0; e < nv; ++e) nu[e] += MJ[r][e] * x[r];
+    }
+
+    /* integratePositions: q += dt qd; T0 <- T0 exp(dt V0) */
+    for (int i = 0; i < n; ++i) {
+        s->qd[i] = nu[6 + i];
+        s->q[i] += dt * nu[6 + i];
+    }
+    double phi[3] = {dt * nu[0], dt * nu[1], dt * nu[2]}, u[3] = {dt * nu[3], dt * nu[4], dt * nu[5]};
+    double dR[9], dp[3], Rn[9];
+    se3_exp(phi, u, dR, dp);
+    for (int r = 0; r < 3; ++r) {
+        s->p[r] += s->R[r * 3] * dp[0] + s->R[r * 3 + 1] * dp[1] + s->R[r * 3 + 2] * dp[2];
+        for (int q = 0; q < 3; ++q)
+            Rn[r * 3 + q] = s->R[r * 3] * dR[q] + s->R[r * 3 + 1] * dR[3 + q] + s->R[r * 3 + 2] * dR[6 + q];
+    }
+    memcpy(s->R, Rn, sizeof Rn);
+    for (int e = 0; e < 6; ++e) s->V[e] = nu[e];
+
+    for (int c = 0; c < nc; ++c) {
+        for (int r = 0; r < 3; ++r) {
+            if (c_pos) c_pos[3 * c + r] = cw[c][r];
+            if (c_force) c_force[3 * c + r] = (nrm[r] * x[3 * c] + t1[r] * x[3 * c + 1] + t2[r] * x[3 * c + 2]) / dt;
+        }
+        if (c_depth) c_depth[c] = depth[c];
+        if (c_body) c_body[c] = cbody[c];
+    }
+    return nc;
+}

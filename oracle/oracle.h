@@ -129,6 +129,49 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
                  double* c_pos, double* c_normal, double* c_force, double* c_depth);
 
 /* ------------------------------------------------------------------ */
+/* Articulated floating base (DART FreeJoint root + tree) with ground   */
+/* contacts: dense formulation (CRBA + RNEA + dense LCP), independent   */
+/* of the device's recursive one.                                       */
+/* ------------------------------------------------------------------ */
+#define OR_MAXFS 16
+#define OR_MAXFC (8 * OR_MAXFS)
+
+typedef struct {
+    or_model tree;               /* moving bodies; parent -1 = the base body  */
+    double base_mass;
+    double base_com[3];
+    double base_Ic[6];
+    int32_t n_shapes;
+    int32_t ground;
+    int32_t shape_body[OR_MAXFS];        /* -1 = base                        */
+    int32_t shape_type[OR_MAXFS];        /* 0 box (half extents), 1 sphere   */
+    double shape_size[OR_MAXFS][3];
+    double shape_R[OR_MAXFS][9];
+    double shape_p[OR_MAXFS][3];
+    double gravity[3];           /* world frame                               */
+    double mu;
+} or_float_model;
+
+typedef struct {
+    double p[3];
+    double R[9];
+    double V[6];                 /* base twist, body frame [w; v]             */
+    double q[OR_MAXB];
+    double qd[OR_MAXB];
+} or_float_state;
+
+/* One engine step; mode / cmd as or_step (joint actuation).  Contacts as
+ * or_free_step (point, normal +z, force on the body, depth) plus the body
+ * index (-1 = base) in c_body.  Returns the number of contact points. */
+int or_float_step(const or_float_model* m, double dt, or_float_state* s, const int32_t* mode,
+                  const double* cmd, int pgs_iters, double* c_pos, double* c_force, double* c_depth,
+                  int32_t* c_body);
+
+/* Floating-base mass matrix ((6+n)^2, row-major) and bias h (gravity +
+ * velocity products) at a state (test cross-checks). */
+void or_float_dynamics(const or_float_model* m, const or_float_state* s, double* M, double* h);
+
+/* ------------------------------------------------------------------ */
 /* Batched environment (task logic of the reference's CartPole /      */
 /* Pendulum tasks + gym TimeLimit + auto-reset with Philox4x32-10).   */
 /* ------------------------------------------------------------------ */

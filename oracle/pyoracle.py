@@ -91,6 +91,33 @@ class OrFreeState(ctypes.Structure):
                 ("w", ctypes.c_double * 3), ("v", ctypes.c_double * 3)]
 
 
+OR_MAXFS = 16
+OR_MAXFC = 8 * OR_MAXFS
+
+
+class OrFloatModel(ctypes.Structure):
+    _fields_ = [
+        ("tree", OrModel),
+        ("base_mass", ctypes.c_double),
+        ("base_com", ctypes.c_double * 3),
+        ("base_Ic", ctypes.c_double * 6),
+        ("n_shapes", ctypes.c_int32),
+        ("ground", ctypes.c_int32),
+        ("shape_body", ctypes.c_int32 * OR_MAXFS),
+        ("shape_type", ctypes.c_int32 * OR_MAXFS),
+        ("shape_size", (ctypes.c_double * 3) * OR_MAXFS),
+        ("shape_R", (ctypes.c_double * 9) * OR_MAXFS),
+        ("shape_p", (ctypes.c_double * 3) * OR_MAXFS),
+        ("gravity", ctypes.c_double * 3),
+        ("mu", ctypes.c_double),
+    ]
+
+
+class OrFloatState(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_double * 3), ("R", ctypes.c_double * 9), ("V", ctypes.c_double * 6),
+                ("q", ctypes.c_double * OR_MAXB), ("qd", ctypes.c_double * OR_MAXB)]
+
+
 class OrTask(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
@@ -141,6 +168,10 @@ def lib():
         L.or_free_step.argtypes = [ctypes.POINTER(OrFreeModel), ctypes.c_double, ctypes.POINTER(OrFreeState),
                                    ctypes.c_int, D, D, D, D]
         L.or_free_step.restype = ctypes.c_int
+        FM, FS = ctypes.POINTER(OrFloatModel), ctypes.POINTER(OrFloatState)
+        L.or_float_step.argtypes = [FM, ctypes.c_double, FS, I32, D, ctypes.c_int, D, D, D, I32]
+        L.or_float_step.restype = ctypes.c_int
+        L.or_float_dynamics.argtypes = [FM, FS, D, D]
         L.or_pid_update.argtypes = [ctypes.POINTER(OrPidGains), ctypes.POINTER(OrPidState),
                                     ctypes.c_double, ctypes.c_double]
         L.or_pid_update.restype = ctypes.c_double
@@ -249,6 +280,8 @@ class ChainModel:
     base_p: np.ndarray
     floating: bool = False
     free: Optional[OrFreeModel] = None
+    # collision shapes of the moving bodies: (body, type, size, R, p) in the body frame
+    body_shapes: list = field(default_factory=list)
 
     @property
     def n(self) -> int:
@@ -392,6 +425,9 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
         M.vel_limit[i] = j.velocity
     cm = ChainModel([j.name for j in chain], root_link, M, base_R, base_p)
     cm.floating = floating
+    for i, j in enumerate(chain):
+        for (t, sz, SR, sp) in links[j.child].shapes:
+            cm.body_shapes.append((i, t, sz, SR, sp))
     if floating:
         B = links[root_link]
         F = OrFreeModel()
@@ -614,6 +650,100 @@ class FreeWorld:
                                 _p(cp), _p(cn), _p(cf), _p(cd))
         self.contacts = [(cp[3 * i:3 * i + 3].copy(), cn[3 * i:3 * i + 3].copy(), cf[3 * i:3 * i + 3].copy(),
                           float(cd[i])) for i in range(nc)]
+        return nc
+
+
+class FloatWorld:
+    """fp64 articulated floating-base model on the ground plane (or_float_step):
+    DART FreeJoint root + the joint tree, dense CRBA/RNEA dynamics, contact
+    rows on any body and joint rows -- the checker of the HIP floating-tree
+    kernel.  Base pose (p, R), base twist V = [w; v] in the base frame."""
+
+    def __init__(self, cm: ChainModel, dt: float = 1e-3, ground: bool = True, mu: float = 1.0,
+                 pgs_iters: int = 100):
+        assert cm.floating
+        m = OrFloatModel()
+        ctypes.pointer(m.tree)[0] = cm.model
+        F = cm.free
+        m.base_mass = F.mass
+        for k in range(3):
+            m.base_com[k] = F.com[k]
+            m.gravity[k] = F.gravity[k]
+        for k in range(6):
+            m.base_Ic[k] = F.Ic[k]
+        shapes = [(-1, F.shape_type[i], np.array(F.shape_size[i][:]), np.array(F.shape_R[i][:]).reshape(3, 3),
+                   np.array(F.shape_p[i][:])) for i in range(F.n_shapes)] + list(cm.body_shapes)
+        assert len(shapes) <= OR_MAXFS
+        m.n_shapes = len(shapes)
+        for i, (b, t, sz, SR, sp) in enumerate(shapes):
+            m.shape_body[i] = b
+            m.shape_type[i] = t
+            for k in range(3):
+                m.shape_size[i][k] = sz[k]
+                m.shape_p[i][k] = sp[k]
+            for k in range(9):
+                m.shape_R[i][k] = np.asarray(SR).flat[k]
+        m.ground = 1 if ground else 0
+        m.mu = mu
+        self.m, self.cm = m, cm
+        self.dt, self.pgs = dt, pgs_iters
+        self.s = OrFloatState()
+        self.set_pose(cm.base_p, cm.base_R)
+        self.mode = np.zeros(cm.n, dtype=np.int32)
+        self.cmd = np.zeros(cm.n)
+        self.contacts = []
+
+    def set_pose(self, p, R):
+        for k in range(3):
+            self.s.p[k] = p[k]
+        for k in range(9):
+            self.s.R[k] = np.asarray(R).flat[k]
+
+    def set_twist(self, w_body, v_body):
+        for k in range(3):
+            self.s.V[k] = w_body[k]
+            self.s.V[3 + k] = v_body[k]
+
+    def set_joints(self, q, qd):
+        for i in range(self.cm.n):
+            self.s.q[i] = q[i]
+            self.s.qd[i] = qd[i]
+
+    @property
+    def p(self):
+        return np.array(self.s.p[:])
+
+    @property
+    def R(self):
+        return np.array(self.s.R[:]).reshape(3, 3)
+
+    @property
+    def V(self):
+        return np.array(self.s.V[:])
+
+    @property
+    def q(self):
+        return np.array(self.s.q[:self.cm.n])
+
+    @property
+    def qd(self):
+        return np.array(self.s.qd[:self.cm.n])
+
+    def dynamics(self):
+        nv = 6 + self.cm.n
+        M, h = np.zeros(nv * nv), np.zeros(nv)
+        lib().or_float_dynamics(ctypes.byref(self.m), ctypes.byref(self.s), _p(M), _p(h))
+        return M.reshape(nv, nv), h
+
+    def step(self, mode=None, cmd=None):
+        mode = self.mode if mode is None else np.ascontiguousarray(mode, dtype=np.int32)
+        cmd = self.cmd if cmd is None else np.ascontiguousarray(cmd, dtype=float)
+        cp, cf, cd = np.zeros(3 * OR_MAXFC), np.zeros(3 * OR_MAXFC), np.zeros(OR_MAXFC)
+        cb = np.zeros(OR_MAXFC, dtype=np.int32)
+        nc = lib().or_float_step(ctypes.byref(self.m), self.dt, ctypes.byref(self.s), _p(mode, ctypes.c_int32),
+                                 _p(cmd), self.pgs, _p(cp), _p(cf), _p(cd), _p(cb, ctypes.c_int32))
+        self.contacts = [(cp[3 * i:3 * i + 3].copy(), cf[3 * i:3 * i + 3].copy(), float(cd[i]), int(cb[i]))
+                         for i in range(nc)]
         return nc
 
 

@@ -1,0 +1,234 @@
+"""GPU tests of articulated models on a floating base (SURVEY.md §8f row 1:
+floating base + contacts; BASELINE config 5 machinery on the authored
+quadruped, models/quadruped.urdf, and floating serial chains of 1..3 joints).
+
+  * teacher-forced one-step parity of the HIP floating-tree kernel against the
+    fp64 dense oracle (or_float_step) on random states near the ground
+    (feet and trunk corners in contact, joints beyond their limits, random
+    torques): pose and joint positions within 1e-5, velocities within 2e-3,
+    contact points within 1e-5 and forces within 5e-3 relative.  A world
+    whose contact LCP is ill-conditioned (a violent impact saturating the
+    friction pyramid: the oracle's own result moves by O(1) under a 3e-7
+    perturbation of its inputs) is accepted only when that measured
+    sensitivity explains the difference, and such worlds stay under 5%;
+  * closed-loop standing: the JointController PID (Position mode, period =
+    step size) holds the quadruped on its feet for 1 s; the fp32 trajectory
+    stays within 1e-3 of the fp64 oracle's and the four foot contacts carry
+    the weight within 0.5 N;
+  * the reference's contact semantics through the ScenarI/O mirror: contacts
+    are reported per link (the four shanks), Model::contacts collects them;
+  * mw_run_device (no readback, graph-capturable) equals repeated mw_run.
+"""
+
+import numpy as np
+import pytest
+
+from test_float_tree_oracle import STAND, chain_urdf
+
+pytestmark = pytest.mark.gpu
+G = 9.8
+# fp32 kernel vs fp64 oracle, one engine step
+TOL = dict(pose=1e-5, q=1e-5, point=1e-5, vel=2e-3, qd=2e-3, force=5e-3)
+
+
+def _quat_to_R(q):
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def _model(name):
+    from mwstep import get_model_file
+    if name == "quadruped":
+        return get_model_file("quadruped")
+    return chain_urdf(int(name[-1]))
+
+
+def _random_states(cm, W, rng):
+    n = cm.n
+    lo = np.array(cm.model.lower[:n])
+    hi = np.array(cm.model.upper[:n])
+    q = rng.uniform(lo, hi, size=(W, n))
+    beyond = rng.uniform(size=(W, n)) < 0.1
+    q[beyond] = np.where(rng.uniform(size=(W, n)) < 0.5, lo - 1e-3, hi + 1e-3)[beyond]
+    qd = rng.uniform(-2, 2, size=(W, n))
+    # base: half the worlds near standing height, half low and tilted
+    axis = rng.normal(size=(W, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    ang = rng.uniform(0, 0.5, W)
+    quat = np.column_stack([np.cos(ang / 2), axis * np.sin(ang / 2)[:, None]])
+    z = np.where(np.arange(W) % 2 == 0, rng.uniform(0.30, 0.48, W), rng.uniform(0.02, 0.25, W))
+    pos = np.column_stack([rng.uniform(-1, 1, W), rng.uniform(-1, 1, W), z])
+    lin = rng.uniform(-0.5, 0.5, (W, 3))
+    angv = rng.uniform(-1, 1, (W, 3))
+    tau = rng.uniform(-20, 20, size=(W, n))
+    f32 = lambda a: a.astype(np.float32).astype(np.float64)
+    return f32(q), f32(qd), f32(np.column_stack([pos, quat])), f32(np.column_stack([lin, angv])), f32(tau)
+
+
+@pytest.mark.parametrize("name", ["quadruped", "chain1", "chain2", "chain3"])
+def test_one_step_parity_with_contacts(require_gpu, oracle, name):
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    text = _model(name)
+    W, pgs, mu = 256, 50, 0.8
+    rng = np.random.default_rng(11)
+    cm = oracle.load_urdf(text)
+    q, qd, pose, vel, tau = _random_states(cm, W, rng)
+    sim = Simulator(text, n_worlds=W, pgs_iters=pgs)
+    sim.set_ground_plane(True, mu)
+    sim.enable_contacts(True)
+    sim.set("reset_q", q)
+    sim.set("reset_qd", qd)
+    sim.reset_base_pose(pose)
+    sim.reset_base_velocity(vel)
+    sim.run(paused=True)
+    p0, v0 = sim.base_pose(), sim.base_velocity()
+    gq0, gqd0 = sim.get("q"), sim.get("qd")
+    sim.set_control_mode(N.MODE_FORCE)
+    sim.set("force_target", tau)
+    sim.run()
+    p1, v1 = sim.base_pose(), sim.base_velocity()
+    gq1, gqd1 = sim.get("q"), sim.get("qd")
+    mode = np.full(cm.n, oracle.FORCE, np.int32)
+
+    def oracle_step(w, eps=0.0, seed=0):
+        # eps > 0: inputs perturbed at fp32 resolution (the conditioning probe)
+        r = np.random.default_rng(seed)
+        jig = (lambda a: a * (1.0 + eps * r.uniform(-1, 1, np.shape(a)))) if eps else (lambda a: a)
+        R0 = _quat_to_R(p0[w, 3:])
+        ow = oracle.FloatWorld(cm, ground=True, mu=mu, pgs_iters=pgs)
+        ow.set_pose(jig(p0[w, :3]), R0)
+        ow.set_twist(jig(R0.T @ v0[w, 3:]), jig(R0.T @ v0[w, :3]))
+        ow.set_joints(jig(gq0[w]), jig(gqd0[w]))
+        ow.step(mode, tau[w])
+        return ow
+
+    worst = dict(pose=0.0, q=0.0, vel=0.0, qd=0.0, force=0.0, point=0.0)
+    n_contact, ill = 0, []
+    for w in range(W):
+        ow = oracle_step(w)
+        e = dict(pose=max(float(np.abs(p1[w, :3] - ow.p).max()), float(np.abs(_quat_to_R(p1[w, 3:]) - ow.R).max())),
+                 q=float(np.abs(gq1[w] - ow.q).max()),
+                 vel=float(np.abs(v1[w] - np.concatenate([ow.R @ ow.V[3:], ow.R @ ow.V[:3]])).max()),
+                 qd=float(np.abs(gqd1[w] - ow.qd).max()), force=0.0, point=0.0)
+        gc, gb = sim.contacts(w), sim.contact_bodies(w)
+        assert len(gc) == len(ow.contacts)
+        n_contact += len(gc) > 0
+        for row, body, (p, f, d, ob) in zip(gc, gb, ow.contacts):
+            assert body == ob
+            e["point"] = max(e["point"], float(np.abs(row[0:3] - p).max()))
+            e["force"] = max(e["force"], float(np.abs(row[6:9] - f).max()) / (1.0 + float(np.abs(f).max())))
+        if e["vel"] > TOL["vel"] or e["qd"] > TOL["qd"] or e["force"] > TOL["force"]:
+            # an ill-conditioned contact LCP (violent impacts saturating the
+            # friction pyramid, PGS far from converged) amplifies rounding:
+            # accept the world only if the oracle itself moves as much when its
+            # inputs are perturbed at fp32 resolution
+            sens = max(float(np.abs(oracle_step(w, 3e-7, k).qd - ow.qd).max()) for k in range(4))
+            ill.append((w, e["qd"], sens))
+            assert sens >= 0.05 * e["qd"], f"world {w}: GPU-oracle |dqd| {e['qd']:.2e}, oracle sensitivity {sens:.2e}"
+            # the positions integrate these velocities: dt * |dqd| at most
+            assert e["q"] <= 2e-3 * e["qd"] + TOL["q"] and e["pose"] <= 2e-3 * e["vel"] + TOL["pose"]
+            e.update(pose=0.0, q=0.0, vel=0.0, qd=0.0, force=0.0)
+        for k in worst:
+            worst[k] = max(worst[k], e[k])
+    print(f"float tree {name}: one-step " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
+          f", {n_contact}/{W} worlds in contact, ill-conditioned: {[(w, f'{a:.1e}', f'{b:.1e}') for w, a, b in ill]}")
+    assert n_contact > W // 4
+    assert len(ill) <= W // 20
+    assert worst["pose"] <= TOL["pose"] and worst["q"] <= TOL["q"] and worst["point"] <= TOL["point"]
+    assert worst["vel"] <= TOL["vel"] and worst["qd"] <= TOL["qd"] and worst["force"] <= TOL["force"]
+    sim.close()
+
+
+def _stand_sim(W, pgs=50):
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    sim = Simulator(get_model_file("quadruped"), n_worlds=W, pgs_iters=pgs, pose=(0, 0, 0.45, 1, 0, 0, 0))
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    sim.set("reset_q", np.tile(STAND, (W, 1)))
+    sim.run(paused=True)
+    sim.set_controller_period(1e-3)
+    for d in range(8):
+        sim.set_pid(d, [400.0, 0.0, 10.0, -60.0, 60.0, 0.0, 0.0, -1.0])
+    sim.set_control_mode(N.MODE_POSITION)
+    sim.set("position_target", np.tile(STAND, (W, 1)))
+    return sim
+
+
+def test_standing_closed_loop_parity(require_gpu, oracle):
+    from mwstep import get_model_file
+    W, H = 4, 1000
+    sim = _stand_sim(W)
+    cm = oracle.load_urdf(get_model_file("quadruped"), pose_xyz=(0, 0, 0.45))
+    ow = oracle.FloatWorld(cm, pgs_iters=50)
+    ow.set_joints(STAND, np.zeros(8))
+    gains = oracle.pid_gains(400.0, 0.0, 10.0, cmdmax=60.0, cmdmin=-60.0)
+    states = [oracle.OrPidState() for _ in range(8)]
+    mode = np.full(8, oracle.FORCE, np.int32)
+    worst_q = worst_z = 0.0
+    for k in range(H):
+        tau = np.array([oracle.pid_update(gains, states[d], ow.q[d] - STAND[d], 1e-3) for d in range(8)])
+        ow.step(mode, tau)
+        sim.run()
+        if k % 50 == 49 or k == H - 1:
+            gq = sim.get("q")
+            worst_q = max(worst_q, float(np.abs(gq - ow.q).max()))
+            worst_z = max(worst_z, float(np.abs(sim.base_pose()[:, 2] - ow.p[2]).max()))
+    fz = [sum(r[8] for r in sim.contacts(w)) for w in range(W)]
+    print(f"quadruped standing H={H}: max|dq| {worst_q:.2e}, max|dz| {worst_z:.2e}, sum Fz {fz}")
+    assert worst_q <= 1e-3 and worst_z <= 1e-4
+    for w in range(W):
+        assert len(sim.contacts(w)) == 4
+        assert sorted(sim.contact_bodies(w).tolist()) == [1, 3, 5, 7]
+        assert fz[w] == pytest.approx(16.0 * G, abs=0.5)
+    sim.close()
+
+
+def test_link_contacts_through_scenario(require_gpu):
+    from mwstep import get_model_file
+    from scenario import core
+    from scenario import gazebo as scenario
+    gazebo = scenario.GazeboSimulator(0.001, 1.0, 1)
+    assert gazebo.initialize()
+    world = gazebo.get_world().to_gazebo()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("ground_plane"))
+    assert world.insert_model(get_model_file("quadruped"), core.Pose([0, 0, 0.45], [1., 0, 0, 0]), "quad")
+    quad = world.get_model("quad")
+    assert quad.link_names() == ["trunk", "thigh_fl", "shank_fl", "thigh_fr", "shank_fr",
+                                 "thigh_hl", "shank_hl", "thigh_hr", "shank_hr"]
+    assert quad.enable_contacts(True)
+    assert quad.reset_joint_positions(list(STAND))
+    assert quad.set_controller_period(0.001)
+    for j in quad.joints():
+        assert j.set_pid(core.PID(400.0, 0.0, 10.0))
+        assert j.set_control_mode(core.JointControlMode_position)
+    assert quad.set_joint_position_targets(list(STAND))
+    for _ in range(1000):
+        gazebo.run()
+    contacts = quad.contacts()
+    assert sorted(c.body_a for c in contacts) == sorted(f"quad::shank_{l}" for l in ("fl", "fr", "hl", "hr"))
+    fz = sum(p.force[2] for c in contacts for p in c.points)
+    assert fz == pytest.approx(16.0 * G, abs=0.5)
+    foot = quad.get_link("shank_fl")
+    assert foot.in_contact() and not quad.get_link("trunk").in_contact()
+    # the shank frame sits at the knee: 0.25 m above the foot sphere's centre
+    assert foot.position()[2] == pytest.approx(0.25 * np.cos(0.6) + 0.03, abs=5e-3)
+    gazebo.close()
+
+
+def test_run_device_equals_run(require_gpu):
+    sims = [_stand_sim(64) for _ in range(2)]
+    for _ in range(200):
+        sims[0].run()
+    sims[1].run_device(200)
+    assert np.array_equal(sims[0].base_pose(), sims[1].base_pose())
+    assert np.array_equal(sims[0].get("q"), sims[1].get("q"))
+    assert np.array_equal(sims[0].contacts(5), sims[1].contacts(5))
+    assert len(sims[0].contacts(5)) == 4
+    for s in sims:
+        s.close()

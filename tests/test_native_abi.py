@@ -130,10 +130,17 @@ def test_fixed_joint_lumping(N, oracle):
 
 
 @pytest.mark.parametrize("bad, why", [
+    # a floating base with two branches: not a compiled floating topology
     ("<robot name='x'><link name='a'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
      "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<joint name='j' type='revolute'><parent link='a'/><child link='b'/></joint></robot>",
-     "floating-base models with joints"),
+     "<link name='c'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+     "<joint name='j1' type='revolute'><parent link='a'/><child link='b'/></joint>"
+     "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>",
+     "topology of this floating-base model"),
+    ("<robot name='x'><link name='a'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+     "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+     "<joint name='j' type='revolute'><parent link='a'/><child link='b'/><dynamics damping='0.1'/></joint></robot>",
+     "joint damping on floating-base models"),
     ("<robot name='x'><link name='a'/></robot>", "has no mass"),
     ("<robot name='x'><link name='world'/>", "XML"),
     ("<sdf><model name='m'/></sdf>", "URDF"),
