@@ -164,9 +164,10 @@ def main():
     panda = None
     if not args.no_panda and rank == 0 and world_size == 1 and args.task != "PandaPositionTracking":
         panda = panda_leg(args, dev, torch, dist)
-    contacts = None
+    contacts = quadruped = None
     if not args.no_contact_leg and rank == 0 and world_size == 1:
         contacts = contact_leg(args, dev, torch)
+        quadruped = quadruped_leg(args, dev, torch)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
@@ -222,6 +223,7 @@ def main():
             "pendulum_c3": pend,
             "randomized": rand,
             "contacts_floating": contacts,
+            "quadruped_floating": quadruped,
         }
         print(json.dumps(out))
     for e in envs:
@@ -379,6 +381,65 @@ def panda_leg(args, dev, torch, dist):
     out["algorithmic_bytes_per_launch"] = bpe * W
     for e in envs:
         e.close()
+    return out
+
+
+def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
+    """Articulated floating base with contacts (BASELINE
+    config 5's machinery on the authored 8-dof quadruped): W quadrupeds
+    standing on the ground plane under the JointController PID (Position
+    mode, period = dt), foot / trunk contacts enabled, PGS 20 iterations,
+    one physics step per run, replayed from hipGraphs of mw_run_device."""
+    import numpy as np
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    K, warm, G = 500, 100, 50
+    stand = np.array([0.6, -1.2] * 4)
+    stream = torch.cuda.Stream(device=dev)
+    sim = Simulator(get_model_file("quadruped"), n_worlds=W, device=dev.index, pgs_iters=pgs,
+                    stream=stream.cuda_stream, pose=(0, 0, 0.45, 1, 0, 0, 0))
+    sim.set_ground_plane(ground, 1.0)
+    sim.enable_contacts(True)
+    rng = np.random.default_rng(args.seed)
+    q0 = stand + rng.uniform(-0.1, 0.1, (W, 8))
+    sim.set("reset_q", q0)
+    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), np.full(W, 0.45), np.ones(W), np.zeros((W, 3))])
+    sim.reset_base_pose(pose)
+    sim.run(paused=True)
+    sim.set_controller_period(1e-3)
+    for d in range(8):
+        sim.set_pid(d, [400.0, 0.0, 10.0, -60.0, 60.0, 0.0, 0.0, -1.0])
+    sim.set_control_mode(N.MODE_POSITION)
+    sim.set("position_target", np.tile(stand, (W, 1)))
+    with torch.cuda.stream(stream):
+        sim.run_device(warm)
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            sim.run_device(G)
+        graph.replay()
+    stream.synchronize()
+    n_rep = K // G
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        for _ in range(n_rep):
+            graph.replay()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    steps = n_rep * G
+    feet = [len(sim.contacts(w)) for w in range(0, W, W // 64)]
+    out = {"workload": f"{W} quadrupeds (16 kg, 8 dofs, floating base) standing on a ground plane under "
+                       "JointController PID hold, sphere-foot / box-trunk contacts, PGS 20 iterations, dt = 1 ms",
+           "value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
+           "ms_per_step": round(elapsed / steps * 1e3, 6),
+           "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
+           "contact_points_sampled": f"{sum(feet)} in {len(feet)} worlds"}
+    sim.close()
     return out
 
 

@@ -13,8 +13,9 @@
 //                         tangents per point, ERP 0.01 / max 1e-3 m/s, CFM
 //                         1e-5) first, then the joint rows (limit, servo,
 //                         Coulomb friction), the order of DART's
-//                         ConstraintSolver; projected Gauss-Seidel in
-//                         sequential-impulse form on nu
+//                         ConstraintSolver; projected Gauss-Seidel on the
+//                         impulses x with the Delassus matrix J M^-1 J^T
+//                         (the oracle's form)
 //   integratePositions    q += dt qd;  T0 <- T0 exp(dt V0)
 //
 // Layout for CDNA4:
@@ -26,7 +27,12 @@
 //     bytes): per contact slot its point, depth, body rotation, the three
 //     rows' J, M^-1 J^T and J M^-1 J^T, and per dof a column M^-1 e_j.
 //     Rows live in the workspace, not LDS, so a model's slot count is not
-//     capped by the 160 KB of LDS per CU; the rows a wave touches stay in L2.
+//     capped by the 160 KB of LDS per CU.
+//   - the PGS itself runs on a compacted table of the active rows in LDS
+//     (RowsLds: A, b, bounds, x for up to kLdsRows rows), assembled once per
+//     step; every sweep is then LDS-only.  A step with more active rows falls
+//     back to sequential impulses on nu over the workspace rows (the same
+//     iteration; each row then costs dependent global round trips).
 //   - contact slots are fixed per model (8 corners of a box, 1 per sphere),
 //     an active bitmask selects them; the loops over slots and their bodies
 //     are uniform (model data), only the active test diverges.
@@ -39,6 +45,7 @@ namespace mw {
 
 constexpr int kMaxFloatShapes = 16;
 constexpr int kMaxFloatSlots = 32;  // active-slot bitmask
+constexpr float kJointCfm = 1e-9f;  // DART JointConstraint CFM [EXT] (oracle OR_CFM)
 
 // Floating base + collision shapes of an articulated floating model; the
 // joints are the ChainF bodies (their parent -1 is this base).
@@ -80,6 +87,26 @@ struct WsRef {
     float* base;  // &ws[0 * W + w]
     int W;
     __device__ __forceinline__ float& at(int word) const { return base[static_cast<size_t>(word) * W]; }
+};
+
+// Compacted active rows of one world in LDS for the x-space PGS (the
+// oracle's form): the Delassus matrix A = J M^-1 J^T with the CFM on its
+// diagonal, right-hand sides, bounds, impulses and each row's source (a
+// contact row 3 slot + d, or a joint row kJointRow + 3 dof + type).  Word k
+// of lane l at [k * 64 + l].  A PGS sweep then touches LDS only.
+constexpr int kLdsRows = 16;
+constexpr int kJointRow = 128;
+constexpr int kRowsLdsWords = kLdsRows * kLdsRows + 5 * kLdsRows;
+struct RowsLds {
+    float* base;  // &words[0][lane]
+    __device__ __forceinline__ float& A(int r, int c) const { return base[(r * kLdsRows + c) * kLdsLanes]; }
+    __device__ __forceinline__ float& b(int r) const { return base[(kLdsRows * kLdsRows + r) * kLdsLanes]; }
+    __device__ __forceinline__ float& x(int r) const { return base[(kLdsRows * (kLdsRows + 1) + r) * kLdsLanes]; }
+    __device__ __forceinline__ float& lo(int r) const { return base[(kLdsRows * (kLdsRows + 2) + r) * kLdsLanes]; }
+    __device__ __forceinline__ float& hi(int r) const { return base[(kLdsRows * (kLdsRows + 3) + r) * kLdsLanes]; }
+    __device__ __forceinline__ int32_t& src(int r) const {
+        return reinterpret_cast<int32_t*>(base)[(kLdsRows * (kLdsRows + 4) + r) * kLdsLanes];
+    }
 };
 
 // 6x6 SPD factorisation (Cholesky, lower, packed row-major) of a root
@@ -281,7 +308,7 @@ template <int N, Topo TOPO, bool CONS, class WK>
 __device__ __forceinline__ uint32_t float_step(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
                                                FloatBody<N>& X, const float (&tau)[N], const uint8_t (&act)[N],
                                                const float (&vcmd)[N], float dt, int pgs_iters, float (&qdd)[N],
-                                               WK& W, const WsRef& ws) {
+                                               WK& W, const WsRef& ws, const RowsLds& RL) {
     using L = FloatWs<N>;
     constexpr int NV = L::kNv;
     const M3 R0 = quat_to_R(X.base.qw, X.base.qx, X.base.qy, X.base.qz);
@@ -436,8 +463,107 @@ __device__ __forceinline__ uint32_t float_step(const ChainF* __restrict__ P, con
         }
     }
 
-    // ---- projected Gauss-Seidel (sequential impulses on nu) ---------------
-    if (active || on) {
+    // ---- projected Gauss-Seidel ---------------------------------------------
+    const int n_rows = 3 * __builtin_popcount(active) + __builtin_popcount(on);
+    const float inv_dt_c = rcp(dt);
+    if (n_rows > 0 && n_rows <= kLdsRows) {
+        // x-space PGS on the compacted rows, A in LDS (the oracle's order:
+        // contacts by slot, then joint rows by dof: limit, servo, friction)
+        int R = 0;
+        for (uint32_t m = active; m; m &= m - 1u) {
+            const int slot = __builtin_ctz(m);
+            const int o = slot * L::kSlotWords;
+            const float bounce = fminf(kContactErp * ws.at(o + 6) * inv_dt_c, kContactMaxErv);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const int ro = o + L::kSlotHead + d * 2 * NV;
+                float jv = 0.f;
+#pragma unroll
+                for (int e = 0; e < NV; ++e) jv += ws.at(ro + e) * nu[e];
+                RL.src(R) = 3 * slot + d;
+                RL.b(R) = ((d == 0) ? bounce : 0.f) - jv;
+                RL.lo(R) = 0.f;
+                RL.hi(R) = kBig;
+                ++R;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                if (!((on >> (3 * i + t)) & 1u)) continue;
+                const BodyF& b = P->b[i];
+                float lo, hi;
+                if (t == 0) {
+                    const bool up = (at_upper >> i) & 1u;
+                    lo = up ? -kBig : 0.f;
+                    hi = up ? 0.f : kBig;
+                } else {
+                    hi = (t == 1 ? b.effort : b.friction) * dt;
+                    lo = -hi;
+                }
+                RL.src(R) = kJointRow + 3 * i + t;
+                RL.b(R) = bb[i][t] - nu[6 + i];
+                RL.lo(R) = lo;
+                RL.hi(R) = hi;
+                ++R;
+            }
+        }
+        // word offset of a row's M^-1 J^T in the workspace
+        auto mj_off = [&](int src) -> int {
+            if (src >= kJointRow) return F->n_slots * L::kSlotWords + ((src - kJointRow) / 3) * L::kColWords;
+            return (src / 3) * L::kSlotWords + L::kSlotHead + (src % 3) * 2 * NV + NV;
+        };
+        // Delassus matrix (symmetric): A_rc = J_r . M^-1 J_c^T
+        for (int c = 0; c < R; ++c) {
+            const int sc = RL.src(c);
+            const int mo = mj_off(sc);
+            float Mc[NV];
+#pragma unroll
+            for (int e = 0; e < NV; ++e) Mc[e] = ws.at(mo + e);
+            for (int r = 0; r <= c; ++r) {
+                const int sr = RL.src(r);
+                float a;
+                if (sr >= kJointRow) {
+                    a = ws.at(mo + 6 + (sr - kJointRow) / 3);  // J = e_dof
+                } else {
+                    const int jo = mj_off(sr) - NV;
+                    a = 0.f;
+#pragma unroll
+                    for (int e = 0; e < NV; ++e) a += ws.at(jo + e) * Mc[e];
+                }
+                RL.A(r, c) = a;
+                RL.A(c, r) = a;
+            }
+            RL.A(c, c) *= 1.f + ((sc >= kJointRow) ? kJointCfm : kContactCfm);
+            RL.x(c) = 0.f;
+        }
+        for (int it = 0; it < pgs_iters; ++it) {
+            for (int r = 0; r < R; ++r) {
+                float acc = RL.b(r);
+                for (int c = 0; c < R; ++c) acc -= RL.A(r, c) * RL.x(c);
+                const float v = RL.x(r) + acc * rcp(RL.A(r, r));
+                const int sr = RL.src(r);
+                float lo = RL.lo(r), hi = RL.hi(r);
+                if (sr < kJointRow && (sr % 3) != 0) {  // friction: |x| <= mu x_normal
+                    hi = F->mu * RL.x(r - sr % 3);
+                    lo = -hi;
+                }
+                RL.x(r) = fminf(fmaxf(v, lo), hi);
+            }
+        }
+        for (int r = 0; r < R; ++r) {
+            const float xr = RL.x(r);
+            const int sr = RL.src(r);
+            if (sr < kJointRow) ws.at((sr / 3) * L::kSlotWords + 16 + sr % 3) = xr;
+            if (xr == 0.f) continue;
+            const int mo = mj_off(sr);
+#pragma unroll
+            for (int e = 0; e < NV; ++e) nu[e] += xr * ws.at(mo + e);
+        }
+    } else if (active || on) {
+        // more rows than the LDS table holds: sequential impulses on nu over
+        // the workspace rows (mathematically the same iteration)
         float xj[N][3];
 #pragma unroll
         for (int i = 0; i < N; ++i) xj[i][0] = xj[i][1] = xj[i][2] = 0.f;

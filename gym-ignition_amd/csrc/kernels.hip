@@ -550,10 +550,12 @@ __global__ void __launch_bounds__(64) float_run_kernel(const ChainF* __restrict_
         }
         __shared__ BodyState sh_bs[N * kLdsLanes];
         __shared__ SV7 sh_own[N * kLdsLanes];
+        __shared__ float sh_rows[kRowsLdsWords * kLdsLanes];
         LdsStage<N, false> stage{sh_bs + threadIdx.x, nullptr, sh_own + threadIdx.x, nullptr};
+        const RowsLds rows{sh_rows + threadIdx.x};
         for (int s = 0; s < A.substeps; ++s) {
             joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, X.q, X.qd, any_pid, tau);
-            active = float_step<N, TOPO, CONS>(P, F, X, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, wr);
+            active = float_step<N, TOPO, CONS>(P, F, X, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, wr, rows);
         }
 #pragma unroll
         for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];

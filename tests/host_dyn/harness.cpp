@@ -61,8 +61,10 @@ static int frun(const ChainF* P, const FloatF* F, float* base, float* q, float* 
     uint8_t act[N];
     for (int i = 0; i < N; ++i) { X.q[i] = q[i]; X.qd[i] = qd[i]; t[i] = tau[i]; vc[i] = 0.f; act[i] = kActForce; }
     const dev::WsRef wr = {ws, 1};
-    if (cons) *active = dev::float_step<N, TOPO, true>(P, F, X, t, act, vc, dt, pgs, qdd, st, wr);
-    else *active = dev::float_step<N, TOPO, false>(P, F, X, t, act, vc, dt, pgs, qdd, st, wr);
+    static float rows[dev::kRowsLdsWords * dev::kLdsLanes];
+    const dev::RowsLds rl{rows};
+    if (cons) *active = dev::float_step<N, TOPO, true>(P, F, X, t, act, vc, dt, pgs, qdd, st, wr, rl);
+    else *active = dev::float_step<N, TOPO, false>(P, F, X, t, act, vc, dt, pgs, qdd, st, wr, rl);
     base[0] = X.base.p.x; base[1] = X.base.p.y; base[2] = X.base.p.z;
     base[3] = X.base.qw; base[4] = X.base.qx; base[5] = X.base.qy; base[6] = X.base.qz;
     base[7] = X.base.V.w.x; base[8] = X.base.V.w.y; base[9] = X.base.V.w.z;

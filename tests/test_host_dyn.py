@@ -25,6 +25,8 @@ def hd(tmp_path_factory):
     L = ctypes.CDLL(out)
     L.hd_substep.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                                       ctypes.c_int, ctypes.c_void_p]
+    L.hd_float_step.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                                         ctypes.c_void_p, ctypes.c_void_p]
     return L
 
 
@@ -135,3 +137,60 @@ def test_panda_tree_with_limit_rows(hd, oracle, panda_file):
                           tau.astype(float), 30)
         worst = max(worst, float(np.abs(got[1] - ref[1]).max()))
     assert worst <= 2e-4, worst
+
+
+def _float_blocks(hd, text, mu):
+    from mwstep import native as N
+    cfg = N.MwConfig(1e-3, 1.0, 1, 1, 0, 0)
+    h = ctypes.c_void_p()
+    N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
+    try:
+        p = np.array([0, 0, 0, 1, 0, 0, 0.0])
+        N.check(N.lib().mw_load_model(h, text.encode(), N.dptr(p), b""))
+        N.check(N.lib().mw_set_ground_plane(h, 1, mu))
+        P = ctypes.create_string_buffer(hd.hd_sizeof_chain())
+        N.check(N.lib().mw_device_params(h, P, len(P)))
+        F = ctypes.create_string_buffer(hd.hd_sizeof_float())
+        N.check(N.lib().mw_device_float_params(h, F, len(F)))
+        return P, F
+    finally:
+        N.lib().mw_destroy(h)
+
+
+@pytest.mark.parametrize("name", ["quadruped", "chain2"])
+def test_floating_tree_step(hd, oracle, name):
+    """float_tree.hpp on the host (float32) vs or_float_step (fp64): random
+    well-conditioned states (gentle velocities, joints inside their limits,
+    feet / corners touching the ground)."""
+    import os
+    from test_float_tree_oracle import STAND, chain_urdf
+    text = (open(os.path.join(ROOT, "gym-ignition_amd", "models", "quadruped.urdf")).read()
+            if name == "quadruped" else chain_urdf(2))
+    P, F = _float_blocks(hd, text, 0.8)
+    cm = oracle.load_urdf(text)
+    n = cm.n
+    rng = np.random.default_rng(2)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    worst_qd = worst_v = 0.0
+    n_contact = 0
+    for k in range(60):
+        q0 = (STAND if name == "quadruped" else np.zeros(n)) + rng.uniform(-0.2, 0.2, n)
+        z = (0.44 if name == "quadruped" else 0.33) + rng.uniform(-0.01, 0.01)
+        base = np.array([0.0, 0.0, z, 1, 0, 0, 0, *rng.uniform(-0.2, 0.2, 6)], np.float32)
+        q, qd = q0.astype(np.float32), rng.uniform(-0.3, 0.3, n).astype(np.float32)
+        tau = rng.uniform(-5, 5, n).astype(np.float32)
+        ow = oracle.FloatWorld(cm, ground=True, mu=0.8, pgs_iters=50)
+        ow.set_pose(base[:3].astype(float), np.eye(3))
+        ow.set_twist(base[7:10].astype(float), base[10:13].astype(float))
+        ow.set_joints(q.astype(float), qd.astype(float))
+        ow.step(np.full(n, oracle.FORCE, np.int32), tau.astype(float))
+        ws = np.zeros(4096, np.float32)
+        active = ctypes.c_uint()
+        assert hd.hd_float_step(P, F, ptr(base), ptr(q), ptr(qd), ptr(tau), 1e-3, 50, 1, ptr(ws),
+                                ctypes.byref(active)) == 0
+        assert bin(active.value).count("1") == len(ow.contacts)
+        n_contact += len(ow.contacts) > 0
+        worst_qd = max(worst_qd, float(np.abs(qd - ow.qd).max()))
+        worst_v = max(worst_v, float(np.abs(base[7:] - ow.V).max()))
+    assert n_contact >= 30
+    assert worst_qd <= 1e-3 and worst_v <= 1e-3, (worst_qd, worst_v)
