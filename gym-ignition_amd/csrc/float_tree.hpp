@@ -63,7 +63,7 @@ struct FloatF {
     int32_t shape_body[kMaxFloatShapes];   // -1 = base
     int32_t shape_type[kMaxFloatShapes];   // 0 box (half extents), 1 sphere (radius)
     int32_t shape_slot0[kMaxFloatShapes];  // first contact slot of the shape
-    uint32_t shape_path[kMaxFloatShapes];  // bit i: body i is the shape's body or one of its ancestors
+    uint64_t shape_path[kMaxFloatShapes];  // bit i: body i is the shape's body or one of its ancestors
     float shape_size[kMaxFloatShapes][3];
     float shape_R[kMaxFloatShapes][9];
     float shape_p[kMaxFloatShapes][3];
@@ -387,7 +387,7 @@ __device__ __forceinline__ uint32_t float_step(const ChainF* __restrict__ P, con
     if (active) {
         for (int sh = 0; sh < F->n_shapes; ++sh) {
             const int k = F->shape_body[sh];
-            const uint32_t path = F->shape_path[sh];
+            const uint32_t path = static_cast<uint32_t>(F->shape_path[sh]);  // N <= 32 here
             const int corners = (F->shape_type[sh] == 1) ? 1 : 8;
             for (int c = 0; c < corners; ++c) {
                 const int slot = F->shape_slot0[sh] + c;

@@ -16,6 +16,7 @@
 #include "baked_models.hpp"
 #include "chain_dyn.hpp"
 #include "float_tree.hpp"
+#include "wave_tree.hpp"
 #include "free_body.hpp"
 #include "kernels.hpp"
 
@@ -577,6 +578,91 @@ __global__ void __launch_bounds__(64) float_run_kernel(const ChainF* __restrict_
     }
 }
 
+// Large articulated models on a floating base, one world per wavefront
+// (wave_tree.hpp).  Same run semantics as float_run_kernel; the PID gains
+// come from a device array (any dof count).  blockIdx.x = world.
+__device__ __forceinline__ float dof_force(const ChainF* __restrict__ P, const SimDev& S, const PidF* __restrict__ pid,
+                                           int W, int w, const RunArgs& A, int s, int d, uint32_t act, float cmd,
+                                           float vc, float q, float qd) {
+    const float e = P->b[d].effort;
+    float tau = (act == kActForce && s == 0) ? fminf(fmaxf(cmd, -e), e) : 0.f;
+    if (act >= kActPidPos) {
+        const size_t k = static_cast<size_t>(d) * W + w;
+        float u = S.pid_u[k];
+        if ((A.pid_gate >> s) & 1u) {
+            const float err = (act == kActPidPos) ? (q - S.ptgt[k]) : (qd - vc);
+            float el = S.pid_e[k], ie = S.pid_i[k];
+            if (pid_update(pid[d], err, A.inv_dt, A.dt, el, ie, u)) {
+                S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
+            } else {
+                u = 0.f;
+            }
+        }
+        tau = fminf(fmaxf(u, -e), e);
+    }
+    return tau;
+}
+
+template <int MAXN, bool CONS>
+__global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
+                                                      int N, SimDev S, FreeDev D, const PidF* __restrict__ pid,
+                                                      int W, RunArgs A, int want_contacts, int* __restrict__ overflow) {
+    const int w = blockIdx.x;
+    const int lane = lane_id();
+    __shared__ WaveWorld<MAXN> L;
+    FreeState base = load_base(D, W, w, A.first);
+    uint32_t act = 0u;
+    float cmd = 0.f, vc = 0.f;
+    if (lane < N) {
+        const size_t k = static_cast<size_t>(lane) * W + w;
+        float q = S.q[k], qd = S.qd[k];
+        if (A.first) {
+            const uint8_t f = S.rflag[k];
+            if (f) {
+                if (f & 2u) qd = S.rqd[k];
+                if (f & 1u) q = S.rq[k];
+                if (f & 4u) { S.pid_e[k] = 0.f; S.pid_i[k] = 0.f; S.pid_u[k] = 0.f; }
+                S.rflag[k] = 0;
+            }
+        }
+        act = S.act[k];
+        vc = S.vtgt[k];
+        cmd = A.first ? S.cmd[k] : 0.f;
+        L.q[lane] = q;
+        L.qd[lane] = qd;
+        L.act[lane] = act;
+        L.vc[lane] = vc;
+    }
+    uint32_t active = 0u;
+    int ovf = 0;
+    if (!A.paused) {
+        for (int s = 0; s < A.substeps; ++s) {
+            if (lane < N)
+                L.tau[lane] = dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
+            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, L.qdd, &ovf);
+        }
+    }
+    if (lane < N) {
+        const size_t k = static_cast<size_t>(lane) * W + w;
+        S.q[k] = L.q[lane];
+        S.qd[k] = L.qd[lane];
+        if (!A.paused) S.qdd[k] = L.qdd[lane];
+        S.cmd[k] = 0.f;
+    }
+    if (lane == 0) {
+        store_base(D, W, w, base);
+        if (ovf) atomicAdd(overflow, ovf);
+    }
+    if (want_contacts && !A.paused) {
+        if (lane == 0) D.cmask[w] = active;
+        if (lane < 32 && ((active >> lane) & 1u)) {
+            const float inv_dt = 1.f / A.dt;
+            store_contact(D, W, w, lane, mk(L.s_xw[lane][0], L.s_xw[lane][1], L.s_xw[lane][2]), L.s_x[lane][0],
+                          L.s_x[lane][1], L.s_x[lane][2], L.s_depth[lane], inv_dt);
+        }
+    }
+}
+
 // ------------------------------------------------ position-target task ----
 // kind 4 (BASELINE config 4, Panda): every joint in Position mode, the
 // JointController PID runs every substep (controller period = step size,
@@ -796,6 +882,29 @@ hipError_t float_n(const ChainF* P, bool cons, const FloatF* F, const SimDev& S,
     return hipGetLastError();
 }
 }  // namespace
+
+hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const FloatF* F, const SimDev& S, const FreeDev& D,
+                           const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(W)), block(dev::kWaveLanes);
+    if (n <= 16) {
+        if (cons)
+            hipLaunchKernelGGL((dev::wave_run_kernel<16, true>), grid, block, 0, st, P, F, n, S, D, pid, W, a,
+                               contacts, overflow);
+        else
+            hipLaunchKernelGGL((dev::wave_run_kernel<16, false>), grid, block, 0, st, P, F, n, S, D, pid, W, a,
+                               contacts, overflow);
+    } else if (n <= kMaxBodies) {
+        if (cons)
+            hipLaunchKernelGGL((dev::wave_run_kernel<kMaxBodies, true>), grid, block, 0, st, P, F, n, S, D, pid, W,
+                               a, contacts, overflow);
+        else
+            hipLaunchKernelGGL((dev::wave_run_kernel<kMaxBodies, false>), grid, block, 0, st, P, F, n, S, D, pid, W,
+                               a, contacts, overflow);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_float_run(const ChainF* P, int n, int topo, bool cons, const FloatF* F, const SimDev& S,
                             const FreeDev& D, const PidSet& pid, float* ws, int W, const RunArgs& a, int contacts,

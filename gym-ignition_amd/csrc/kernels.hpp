@@ -95,6 +95,13 @@ hipError_t launch_free_run(const struct FreeF* F, const FreeDev& D, int W, const
 hipError_t launch_float_run(const ChainF* P, int n, int topo, bool cons, const struct FloatF* F, const SimDev& S,
                             const FreeDev& D, const PidSet& pid, float* ws, int W, const RunArgs& a, int contacts,
                             hipStream_t st);
+// Large floating-base trees, one world per wavefront (wave_tree.hpp): any
+// topology of <= kMaxBodies bodies and depth <= 12; pid: n PidF in device
+// memory; overflow: device counter of constraint rows dropped (> 64 per step).
+hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const struct FloatF* F, const SimDev& S,
+                           const FreeDev& D, const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow,
+                           hipStream_t st);
+constexpr int kWaveMaxDepthHost = 12;
 // workspace words per world of a floating-tree model, -1 if n is not compiled in
 int float_workspace_words(int n, int n_slots);
 

@@ -111,6 +111,12 @@ struct mw_sim {
     float* d_ws = nullptr;        // constraint-row workspace [words][W]
     int n_slots = mw::kMaxFreeSlots;
     std::vector<int32_t> slot_body;  // body of every contact slot (-1 = base)
+    // large trees (or MWSTEP_WAVE_TREE=1): one world per wavefront (wave_tree.hpp)
+    bool wave = false;
+    mw::PidF* d_pid = nullptr;    // PID gains of every dof (device)
+    mw::PidF* h_pid = nullptr;    // pinned staging copy
+    bool pid_dirty = true;        // gains changed since the last upload
+    int* d_overflow = nullptr;    // constraint rows dropped by the wave kernel
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -284,8 +290,8 @@ void build_float(mw_sim* s) {
         F.shape_body[i] = b;
         F.shape_type[i] = sh.type;
         F.shape_slot0[i] = slot;
-        uint32_t path = 0;
-        for (int k = b; k >= 0; k = M.bodies[k].parent) path |= 1u << k;
+        uint64_t path = 0;
+        for (int k = b; k >= 0; k = M.bodies[k].parent) path |= uint64_t{1} << k;
         F.shape_path[i] = path;
         for (int k = 0; k < 3; ++k) {
             F.shape_size[i][k] = static_cast<float>(sh.size[k]);
@@ -481,6 +487,9 @@ void mw_destroy(mw_sim* s) {
         (void)hipFree(s->d_free);
         (void)hipFree(s->d_float);
         (void)hipFree(s->d_ws);
+        (void)hipFree(s->d_pid);
+        (void)hipHostFree(s->h_pid);
+        (void)hipFree(s->d_overflow);
         (void)hipHostFree(s->h_base);
         (void)hipHostFree(s->h_cdata);
         (void)hipHostFree(s->h_cmask);
@@ -498,8 +507,8 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     } catch (const std::exception& e) {
         return fail(MW_EPARSE, e.what());
     }
-    if (s->model.dofs() > mw::kMaxKernelDofs || s->model.dofs() > 9)
-        return fail(MW_EPARSE, "models with more than 9 dofs are not supported by this build");
+    if (s->model.dofs() > 9 && !(s->model.floating && s->model.dofs() <= mw::kMaxBodies))
+        return fail(MW_EPARSE, "fixed-base models with more than 9 dofs are not supported by this build");
     s->floating = s->model.floating;
     s->float_tree = s->floating && s->model.dofs() > 0;
     if (s->float_tree) {
@@ -521,10 +530,24 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         if (s->h_float.n_slots > mw::kMaxFloatSlots)
             return fail(MW_EPARSE, "a floating-base model may have at most " + std::to_string(mw::kMaxFloatSlots) +
                                        " contact slots (8 per box, 1 per sphere)");
-        const bool compiled = (s->topo == 0 && s->n <= 3) || s->topo == 2;
-        if (!compiled || mw::float_workspace_words(s->n, s->h_float.n_slots) < 0)
-            return fail(MW_EPARSE, "the topology of this floating-base model is not compiled into this build "
-                                   "(supported: serial chains of 1..3 dofs and the quadruped tree)");
+        // small compiled topologies: one world per lane (float_tree.hpp); any
+        // other tree: one world per wavefront (wave_tree.hpp)
+        const bool compiled = ((s->topo == 0 && s->n <= 3) || s->topo == 2) &&
+                              mw::float_workspace_words(s->n, s->h_float.n_slots) >= 0;
+        const char* force_wave = std::getenv("MWSTEP_WAVE_TREE");
+        s->wave = !compiled || (force_wave && *force_wave && *force_wave != '0');
+        if (s->wave) {
+            std::vector<int> depth(s->n, 0);
+            int max_depth = 0;
+            for (int i = 0; i < s->n; ++i) {
+                const int pa = s->model.bodies[i].parent;
+                depth[i] = (pa >= 0) ? depth[pa] + 1 : 0;
+                max_depth = std::max(max_depth, depth[i] + 1);
+            }
+            if (max_depth > mw::kWaveMaxDepthHost)
+                return fail(MW_EPARSE, "the kinematic tree of this floating-base model is deeper than " +
+                                           std::to_string(mw::kWaveMaxDepthHost) + " joints");
+        }
         s->n_slots = s->h_float.n_slots;
         s->pid.assign(s->model.dofs(), kDefaultPid);
         s->model_name = (name && *name) ? name : s->model.name;
@@ -576,6 +599,26 @@ int mw_device_params(const mw_sim* s, void* out, int32_t bytes) {
     return MW_OK;
 }
 
+int mw_constraint_overflow(const mw_sim* s, int64_t* rows) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!rows) return fail(MW_EINVAL, "null argument");
+    *rows = 0;
+    if (!s->d_overflow) return MW_OK;
+    int v = 0;
+    MW_HIP(hipMemcpyAsync(&v, s->d_overflow, sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    *rows = v;
+    return MW_OK;
+}
+
+int mw_float_kernel(const mw_sim* s, int32_t* kind) {
+    if (!s || !kind) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    *kind = !s->float_tree ? 0 : (s->wave ? 2 : 1);
+    return MW_OK;
+}
+
 int mw_device_float_params(const mw_sim* s, void* out, int32_t bytes) {
     if (!s || !out) return fail(MW_EINVAL, "null argument");
     if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
@@ -605,8 +648,16 @@ int mw_initialize(mw_sim* s) {
         MW_HIP(hipMalloc(&s->d_fblock, nf * sizeof(float) + W * (1 + sizeof(uint32_t)) + 64));
         if (s->float_tree) {
             MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_float), sizeof(mw::FloatF)));
-            const size_t words = static_cast<size_t>(mw::float_workspace_words(s->n, s->n_slots));
-            MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ws), words * W * sizeof(float)));
+            if (s->wave) {
+                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), mw::kMaxBodies * sizeof(mw::PidF)));
+                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), mw::kMaxBodies * sizeof(mw::PidF),
+                                     hipHostMallocDefault));
+                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), sizeof(int)));
+                MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
+            } else {
+                const size_t words = static_cast<size_t>(mw::float_workspace_words(s->n, s->n_slots));
+                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ws), words * W * sizeof(float)));
+            }
         } else {
             MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_free), sizeof(mw::FreeF)));
         }
@@ -782,6 +833,19 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
         s->ptgt_dirty = false;
     }
     const mw::PidSet pid = pid_set(s);
+    if (s->wave && s->pid_dirty) {
+        // the wave kernel reads every dof's gains from device memory; the pinned
+        // staging buffer is only rewritten after the stream has drained it (gains
+        // change between runs, never inside a captured device-resident run)
+        MW_HIP(hipStreamSynchronize(s->stream));
+        s->pid_dirty = false;
+        for (int d = 0; d < s->n; ++d) {
+            const auto& g = s->pid[d];
+            s->h_pid[d] = {to_f32(g[0]), to_f32(g[1]), to_f32(g[2]), to_f32(g[7]), to_f32(g[6]),
+                           to_f32(g[4]), to_f32(g[3]), to_f32(g[5])};
+        }
+        MW_HIP(hipMemcpyAsync(s->d_pid, s->h_pid, s->n * sizeof(mw::PidF), hipMemcpyHostToDevice, s->stream));
+    }
     mw::RunArgs a{};
     a.dt = static_cast<float>(s->cfg.step_size);
     a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
@@ -805,7 +869,10 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
                 a.pid_gate |= (uint64_t{1} << k);
             }
         }
-        if (s->float_tree)
+        if (s->wave)
+            MW_HIP(mw::launch_wave_run(s->d_params, s->n, needs_cons(s), s->d_float, s->dev, s->fdev, s->d_pid, s->W,
+                                       a, s->contacts ? 1 : 0, s->d_overflow, s->stream));
+        else if (s->float_tree)
             MW_HIP(mw::launch_float_run(s->d_params, s->n, s->topo, needs_cons(s), s->d_float, s->dev, s->fdev, pid,
                                         s->d_ws, s->W, a, s->contacts ? 1 : 0, s->stream));
         else
@@ -1138,6 +1205,7 @@ int mw_set_joint_pid(mw_sim* s, int32_t dof, const double gains[8]) {
         g[4] = maxf;
     }
     s->pid[dof] = g;
+    s->pid_dirty = true;
     // a new ignition::math::PID starts from a reset state (before mw_initialize
     // the device state is zero-initialised anyway)
     if (s->initialized) {

@@ -1,0 +1,491 @@
+// wave_tree.hpp -- one engine step of an articulated model on a floating
+// base, ONE WORLD PER WAVEFRONT (large trees: the iCub-class models of
+// BASELINE config 5).  Same physics as float_tree.hpp / oracle.c
+// or_float_step (DART 6 World::step restated [EXT]); different mapping:
+//
+//   uniform phases   the ABA over the tree (runtime topology, bodies in
+//                    depth-first order) is executed by the whole wave with
+//                    identical values (no broadcast needed: every lane holds
+//                    the result); per-body records live in LDS, written by
+//                    lane 0 and read as LDS broadcasts.
+//   lane phases      joint commands / PID (lane = dof), contact detection
+//                    (lane = slot), row responses M^-1 J^T (lane = row; each
+//                    walks its body's path to the base, then the outward pass
+//                    with a per-lane stack indexed by body depth), Delassus
+//                    columns (lane = column), the nu update (lane = component).
+//   PGS              rows in order (the oracle's order); row r's
+//                    sum_c A_rc x_c has lane c multiply its own x_c and a DPP
+//                    wave reduction add the 64 products.
+//
+// Capacities (checked on the host): bodies <= MAXN, tree depth <= kWaveMaxDepth,
+// contact slots <= 32, active rows <= 64 per step (beyond: the step's extra
+// rows are dropped and counted in the world's overflow counter).
+#pragma once
+
+#include "float_tree.hpp"
+
+namespace mw {
+namespace dev {
+
+constexpr int kWaveLanes = 64;
+constexpr int kWaveMaxRows = 64;
+constexpr int kWaveMaxDepth = 12;
+
+// per-body record (uniform), 75 words
+struct WaveBody {
+    M3 R;        // joint transform (parent -> body)
+    f3 p;
+    SV U;        // AI S
+    float psi;   // (S^T AI S)^-1
+    float tt;    // total joint force (ABA u)
+    SV eta;      // velocity-product acceleration
+    SV B;        // bias force, then articulated bias accumulated from the children
+    SI IA;       // articulated inertia accumulated from the children
+    SV V;        // body velocity, then acceleration
+    M3 Rw;       // world pose (contact detection)
+    f3 pw;
+    int32_t depth;
+    float pad_[3];
+};
+static_assert(sizeof(WaveBody) == 75 * 4, "WaveBody layout");
+
+template <int MAXN>
+struct WaveWorld {
+    static constexpr int kNv = 6 + MAXN;
+    static constexpr int kRowStride = kNv | 1;  // odd: lane-strided row access is conflict-free
+    WaveBody body[MAXN];
+    float q[MAXN], qd[MAXN], qdd[MAXN], tau[MAXN], vc[MAXN];
+    uint32_t act[MAXN];
+    float nu[kNv];
+    float J[kWaveMaxRows][kRowStride];
+    float MJ[kWaveMaxRows][kRowStride];
+    float A[kWaveMaxRows][kWaveMaxRows + 1];
+    float b[kWaveMaxRows], lo[kWaveMaxRows], hi[kWaveMaxRows];
+    int32_t src[kWaveMaxRows];   // 3 slot + d, or kJointRow + 3 dof + type
+    // contact slots
+    float s_b[kMaxFloatSlots][3];   // body-frame point
+    float s_xw[kMaxFloatSlots][3];  // world point
+    float s_depth[kMaxFloatSlots];
+    float s_R[kMaxFloatSlots][9];   // body rotation
+    float s_x[kMaxFloatSlots][3];   // impulses (output)
+    // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
+    float stack[kWaveMaxDepth][7][kWaveLanes];
+};
+
+__device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63u); }
+
+// sum over the 64 lanes (DPP: quad perms, half-row / row mirrors, row
+// broadcasts 15 and 31), the total read from lane 63; a fixed order, so the
+// result is deterministic
+__device__ __forceinline__ float wave_sum(float x) {
+#ifdef MW_HOST_TEST
+    return x;
+#else
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x142, 0xA, 0xF, false));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x143, 0xC, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+#endif
+}
+
+__device__ __forceinline__ float read_lane(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+
+// the whole wave runs these with identical values; lane 0 stores
+#define MW_LANE0 if (lane_id() == 0)
+
+// Floating-base ABA, uniform (runtime topology).  Returns a0 and leaves
+// qdd_i in qdd_out (L.qdd, LDS).
+template <int MAXN>
+__device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
+                                       const M3& R0, const f3& p0, const SV& V0, WaveWorld<MAXN>& L, Chol6& L0,
+                                       float* qdd_out) {
+    const f3 g0 = mulT(R0, mk(F->g[0], F->g[1], F->g[2]));
+    // outward: kinematics, velocities, bias forces, world poses, depths
+    for (int i = 0; i < N; ++i) {
+        const BodyF& b = P->b[i];
+        const int pa = b.parent;
+        M3 R;
+        f3 p;
+        joint_pose(b, L.q[i], R, p);
+        const SV Sq = motion(b, L.qd[i]);
+        const SV Vp = (pa >= 0) ? L.body[pa].V : V0;
+        const SV Vi = ad_inv(R, p, Vp) + Sq;
+        // gravity in the body frame: R_w^T g_world
+        const M3& Rwp = (pa >= 0) ? L.body[pa].Rw : R0;
+        const f3 pwp = (pa >= 0) ? L.body[pa].pw : p0;
+        M3 Rw;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                Rw.m[r * 3 + c] = Rwp.m[r * 3] * R.m[c] + Rwp.m[r * 3 + 1] * R.m[3 + c] + Rwp.m[r * 3 + 2] * R.m[6 + c];
+        const f3 pw = pwp + mul(Rwp, p);
+        const f3 gi = mulT(Rw, mk(F->g[0], F->g[1], F->g[2]));
+        const SV eta = {cross(Vi.w, Sq.w), cross(Vi.w, Sq.v) + cross(Vi.v, Sq.w)};
+        const SV Bi = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), Vi, gi);
+        const int depth = (pa >= 0) ? L.body[pa].depth + 1 : 0;
+        MW_LANE0 {
+            WaveBody& s = L.body[i];
+            s.R = R;
+            s.p = p;
+            s.V = Vi;
+            s.Rw = Rw;
+            s.pw = pw;
+            s.eta = eta;
+            s.B = Bi;
+            s.IA = rigid(b, b.mass);
+            s.depth = depth;
+        }
+    }
+    // inward: articulated inertias and biases accumulate into the parents
+    SI IA0 = rigid_base(*F);
+    SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
+                       Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, g0);
+    for (int i = N - 1; i >= 0; --i) {
+        const BodyF& b = P->b[i];
+        const int pa = b.parent;
+        const WaveBody& s = L.body[i];
+        const SI AI = s.IA;
+        const SV U = ais(AI, b);
+        const float psi = rcp(proj(b, U));
+        const SV AIeta = mul(AI, s.eta);
+        const float tt = L.tau[i] - proj(b, AIeta + s.B);
+        const SI c = to_parent(s.R, s.p, downdate(AI, U, psi));
+        const SV cb = dad_inv(s.R, s.p, s.B + AIeta + (psi * tt) * U);
+        if (pa >= 0) {
+            SI Ip = L.body[pa].IA;
+            Ip += c;
+            const SV Bp = L.body[pa].B + cb;
+            MW_LANE0 {
+                L.body[pa].IA = Ip;
+                L.body[pa].B = Bp;
+            }
+        } else {
+            IA0 += c;
+            B0 = B0 + cb;
+        }
+        MW_LANE0 {
+            L.body[i].U = U;
+            L.body[i].psi = psi;
+            L.body[i].tt = tt;
+        }
+    }
+    L0.factor(IA0);
+    const SV a0 = L0.solve(-1.f * B0);
+    // outward: accelerations (reuse V for a)
+    for (int i = 0; i < N; ++i) {
+        const BodyF& b = P->b[i];
+        const int pa = b.parent;
+        const WaveBody& s = L.body[i];
+        const SV ap = ad_inv(s.R, s.p, (pa >= 0) ? L.body[pa].V : a0);
+        const float qdd = s.psi * (s.tt - dot(s.U, ap));
+        const SV ai = ap + s.eta + motion(b, qdd);
+        MW_LANE0 {
+            L.body[i].V = ai;
+            qdd_out[i] = qdd;
+        }
+    }
+    return a0;
+}
+
+// Per-lane response to a spatial impulse f on body k (k = -1: base) and/or
+// a unit impulse on dof j: J = J_k^T f (generalized row), MJ = M^-1 (J^T + e_j).
+// Writes J (if Jrow) and MJ to the lane's LDS rows.
+template <int MAXN>
+__device__ __forceinline__ void wave_response(const ChainF* __restrict__ P, int N, WaveWorld<MAXN>& L,
+                                              const Chol6& L0, int k, int j, const SV& f, float* Jrow,
+                                              float* MJrow) {
+    const int lane = lane_id();
+    uint64_t path = 0;
+    const int start = (k >= 0) ? k : j;
+    for (int i = start; i >= 0; i = P->b[i].parent) path |= uint64_t{1} << i;
+    for (int e = 0; e < 6 + N; ++e) Jrow[e] = 0.f;
+    // inward along the path: articulated bias impulse Bi and the kinematic
+    // force Fi (for J); u_i parked in the lane's depth stack
+    SV Bi = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Fi = Bi;
+    if (k >= 0 || (k < 0 && j < 0)) { Bi = -1.f * f; Fi = f; }
+    for (int i = start; i >= 0; i = P->b[i].parent) {
+        const BodyF& b = P->b[i];
+        const WaveBody& s = L.body[i];
+        Jrow[6 + i] = proj(b, Fi);
+        const float u = ((i == j) ? 1.f : 0.f) - proj(b, Bi);
+        L.stack[s.depth][6][lane] = u;
+        Bi = dad_inv(s.R, s.p, Bi + (s.psi * u) * s.U);
+        Fi = dad_inv(s.R, s.p, Fi);
+    }
+    Jrow[0] = Fi.w.x; Jrow[1] = Fi.w.y; Jrow[2] = Fi.w.z; Jrow[3] = Fi.v.x; Jrow[4] = Fi.v.y; Jrow[5] = Fi.v.z;
+    const SV dV0 = L0.solve(-1.f * Bi);
+    MJrow[0] = dV0.w.x; MJrow[1] = dV0.w.y; MJrow[2] = dV0.w.z;
+    MJrow[3] = dV0.v.x; MJrow[4] = dV0.v.y; MJrow[5] = dV0.v.z;
+    for (int i = 0; i < N; ++i) {
+        const BodyF& b = P->b[i];
+        const WaveBody& s = L.body[i];
+        const int pa = b.parent;
+        SV dvp_in;
+        if (pa >= 0) {
+            const int dp = L.body[pa].depth;
+            dvp_in = {{L.stack[dp][0][lane], L.stack[dp][1][lane], L.stack[dp][2][lane]},
+                      {L.stack[dp][3][lane], L.stack[dp][4][lane], L.stack[dp][5][lane]}};
+        } else {
+            dvp_in = dV0;
+        }
+        const SV dvp = ad_inv(s.R, s.p, dvp_in);
+        const float u = ((path >> i) & 1u) ? L.stack[s.depth][6][lane] : 0.f;
+        const float m = s.psi * (u - dot(s.U, dvp));
+        MJrow[6 + i] = m;
+        const SV dv = dvp + motion(b, m);
+        float* st = &L.stack[s.depth][0][lane];
+        st[0 * kWaveLanes] = dv.w.x; st[1 * kWaveLanes] = dv.w.y; st[2 * kWaveLanes] = dv.w.z;
+        st[3 * kWaveLanes] = dv.v.x; st[4 * kWaveLanes] = dv.v.y; st[5 * kWaveLanes] = dv.v.z;
+    }
+}
+
+// One engine step of world L (state in L.q / L.qd / base; joint forces in
+// L.tau).  Returns the active slot mask; *overflow += rows dropped.
+template <int MAXN, bool CONS>
+__device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
+                                              FreeState& base, WaveWorld<MAXN>& L, float dt, int pgs_iters,
+                                              float* qdd_out, int* overflow) {
+    const int lane = lane_id();
+    const int NV = 6 + N;
+    const M3 R0 = quat_to_R(base.qw, base.qx, base.qy, base.qz);
+    Chol6 L0;
+    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, qdd_out);
+    // integrateVelocities (lane e: nu component e)
+    if (lane < NV) {
+        float v;
+        if (lane < 6) {
+            const float a[6] = {a0.w.x, a0.w.y, a0.w.z, a0.v.x, a0.v.y, a0.v.z};
+            const float V0[6] = {base.V.w.x, base.V.w.y, base.V.w.z, base.V.v.x, base.V.v.y, base.V.v.z};
+            float ae = 0.f, ve = 0.f;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) {
+                ae = (lane == e) ? a[e] : ae;
+                ve = (lane == e) ? V0[e] : ve;
+            }
+            v = ve + dt * ae;
+        } else {
+            v = L.qd[lane - 6] + dt * qdd_out[lane - 6];
+        }
+        L.nu[lane] = v;
+    }
+
+    // ---- contact detection (lane = slot) -----------------------------------
+    uint32_t active = 0u;
+    if (F->ground) {
+        bool hit = false;
+        if (lane < F->n_slots) {
+            int sh = 0;
+            while (sh + 1 < F->n_shapes && F->shape_slot0[sh + 1] <= lane) ++sh;
+            const int c = lane - F->shape_slot0[sh];
+            const int bi = F->shape_body[sh];
+            M3 Rb;
+            f3 pb;
+            if (bi < 0) { Rb = R0; pb = base.p; }
+            else { Rb = L.body[bi].Rw; pb = L.body[bi].pw; }
+            const bool sphere = (F->shape_type[sh] == 1);
+            const float* h = F->shape_size[sh];
+            const float* SR = F->shape_R[sh];
+            const float lx = sphere ? 0.f : ((c & 4) ? h[0] : -h[0]);
+            const float ly = sphere ? 0.f : ((c & 2) ? h[1] : -h[1]);
+            const float lz = sphere ? 0.f : ((c & 1) ? h[2] : -h[2]);
+            f3 bb = {F->shape_p[sh][0] + SR[0] * lx + SR[1] * ly + SR[2] * lz,
+                     F->shape_p[sh][1] + SR[3] * lx + SR[4] * ly + SR[5] * lz,
+                     F->shape_p[sh][2] + SR[6] * lx + SR[7] * ly + SR[8] * lz};
+            f3 xw = pb + mul(Rb, bb);
+            float depth = -xw.z;
+            if (sphere) {
+                depth = h[0] - xw.z;
+                xw.z -= h[0];
+                bb = mulT(Rb, xw - pb);
+            }
+            if (depth > 0.f) {
+                hit = true;
+                L.s_b[lane][0] = bb.x; L.s_b[lane][1] = bb.y; L.s_b[lane][2] = bb.z;
+                L.s_xw[lane][0] = xw.x; L.s_xw[lane][1] = xw.y; L.s_xw[lane][2] = xw.z;
+                L.s_depth[lane] = depth;
+#pragma unroll
+                for (int e = 0; e < 9; ++e) L.s_R[lane][e] = Rb.m[e];
+                L.s_x[lane][0] = L.s_x[lane][1] = L.s_x[lane][2] = 0.f;
+            }
+        }
+        active = static_cast<uint32_t>(__ballot(hit));
+    }
+
+    // ---- rows: contacts (slot order), then joint rows (dof order) ----------
+    // joint rows of dof `lane`: bit t of jbits = limit / servo / friction
+    uint32_t jbits = 0u;
+    float jb[3] = {0.f, 0.f, 0.f}, jlo[3] = {0.f, 0.f, 0.f}, jhi[3] = {0.f, 0.f, 0.f};
+    if (CONS && lane < N) {
+        const BodyF& b = P->b[lane];
+        const float qdi = L.nu[6 + lane];
+        if (b.limited) {
+            float viol = L.q[lane] - b.lower;
+            bool lim = false, up = false;
+            if (viol <= 0.f) {
+                lim = true;
+            } else {
+                viol = L.q[lane] - b.upper;
+                if (viol >= 0.f) { lim = true; up = true; }
+            }
+            if (lim) {
+                jbits |= 1u;
+                jb[0] = fminf(fmaxf(-viol * kErp * rcp(dt), -kMaxErv), kMaxErv) - qdi;
+                jlo[0] = up ? -kBig : 0.f;
+                jhi[0] = up ? 0.f : kBig;
+            }
+        }
+        if (L.act[lane] == kActServo) {
+            const float vc = fminf(fmaxf(L.vc[lane], -b.vel_limit), b.vel_limit);
+            if (vc - qdi != 0.f) {
+                jbits |= 2u;
+                jb[1] = vc - qdi;
+                jhi[1] = b.effort * dt;
+                jlo[1] = -jhi[1];
+            }
+        }
+        if (b.friction != 0.f && qdi != 0.f) {
+            jbits |= 4u;
+            jb[2] = -qdi;
+            jhi[2] = b.friction * dt;
+            jlo[2] = -jhi[2];
+        }
+    }
+    const int n_contact_rows = 3 * __builtin_popcount(active);
+    // prefix count of the joint rows in dof order
+    const int my_j = __builtin_popcount(jbits);
+    int before = 0, total_j = 0;
+    for (int d = 0; d < N; ++d) {
+        const int cnt = __builtin_amdgcn_readlane(my_j, d);
+        before += (d < lane) ? cnt : 0;
+        total_j += cnt;
+    }
+    int R = n_contact_rows + total_j;
+    if (R > kWaveMaxRows) {
+        MW_LANE0 { *overflow += R - kWaveMaxRows; }
+        R = kWaveMaxRows;
+    }
+    // contact rows: lane = slot -> rows 3 rank + d
+    if (lane < 32 && ((active >> lane) & 1u)) {
+        const int rank = __builtin_popcount(active & ((1u << lane) - 1u));
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int r = 3 * rank + d;
+            if (r < R) {
+                L.src[r] = 3 * lane + d;
+                L.lo[r] = 0.f;
+                L.hi[r] = kBig;
+            }
+        }
+    }
+    if (CONS && lane < N) {
+        int r = n_contact_rows + before;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            if (((jbits >> t) & 1u) && r < R) {
+                L.src[r] = kJointRow + 3 * lane + t;
+                L.b[r] = jb[t];
+                L.lo[r] = jlo[t];
+                L.hi[r] = jhi[t];
+                ++r;
+            }
+        }
+    }
+
+    if (R > 0) {
+        // ---- responses (lane = row) ------------------------------------------
+        for (int r0 = 0; r0 < R; r0 += kWaveLanes) {
+            const int r = r0 + lane;
+            if (r < R) {
+                const int src = L.src[r];
+                if (src < kJointRow) {
+                    const int slot = src / 3, d = src % 3;
+                    int sh = 0;
+                    while (sh + 1 < F->n_shapes && F->shape_slot0[sh + 1] <= slot) ++sh;
+                    const int k = F->shape_body[sh];
+                    const f3 bpt = {L.s_b[slot][0], L.s_b[slot][1], L.s_b[slot][2]};
+                    // body-frame direction R_k^T d: n -> row 2, t1 -> -row 1, t2 -> row 0
+                    const int row = (d == 0) ? 2 : ((d == 1) ? 1 : 0);
+                    const float sg = (d == 1) ? -1.f : 1.f;
+                    const f3 dir = {sg * L.s_R[slot][row * 3], sg * L.s_R[slot][row * 3 + 1],
+                                    sg * L.s_R[slot][row * 3 + 2]};
+                    const SV f = {cross(bpt, dir), dir};
+                    wave_response<MAXN>(P, N, L, L0, k, -1, f, L.J[r], L.MJ[r]);
+                    float jv = 0.f;
+                    for (int e = 0; e < NV; ++e) jv += L.J[r][e] * L.nu[e];
+                    const float bounce =
+                        (d == 0) ? fminf(kContactErp * L.s_depth[slot] * rcp(dt), kContactMaxErv) : 0.f;
+                    L.b[r] = bounce - jv;
+                } else {
+                    const int dof = (src - kJointRow) / 3;
+                    const SV zero = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+                    wave_response<MAXN>(P, N, L, L0, -2, dof, zero, L.J[r], L.MJ[r]);
+                    for (int e = 0; e < NV; ++e) L.J[r][e] = (e == 6 + dof) ? 1.f : 0.f;
+                }
+            }
+        }
+        // ---- Delassus matrix (lane = column) ------------------------------------
+        for (int c0 = 0; c0 < R; c0 += kWaveLanes) {
+            const int c = c0 + lane;
+            if (c < R) {
+                for (int r = 0; r < R; ++r) {
+                    float a = 0.f;
+                    for (int e = 0; e < NV; ++e) a += L.J[r][e] * L.MJ[c][e];
+                    L.A[r][c] = a;
+                }
+                L.A[c][c] *= 1.f + ((L.src[c] >= kJointRow) ? kJointCfm : kContactCfm);
+            }
+        }
+        // ---- PGS: x_c in lane c ----------------------------------------------------
+        float x = 0.f;
+        for (int it = 0; it < pgs_iters; ++it) {
+            for (int r = 0; r < R; ++r) {
+                const float prod = (lane < R) ? L.A[r][lane] * x : 0.f;
+                const float s = wave_sum(prod);
+                const float xr = read_lane(x, r);
+                float v = xr + (L.b[r] - s) * rcp(L.A[r][r]);
+                const int src = L.src[r];
+                float lo = L.lo[r], hi = L.hi[r];
+                if (src < kJointRow && (src % 3) != 0) {
+                    hi = F->mu * read_lane(x, r - src % 3);
+                    lo = -hi;
+                }
+                v = fminf(fmaxf(v, lo), hi);
+                if (lane == r) x = v;
+            }
+        }
+        // ---- nu += MJ^T x (lane = component); impulses to the slots ----------------
+        if (lane < R) {
+            const int src = L.src[lane];
+            if (src < kJointRow) L.s_x[src / 3][src % 3] = x;
+        }
+        float dnu = 0.f;
+        for (int r = 0; r < R; ++r) {
+            const float xr = read_lane(x, r);
+            if (lane < NV) dnu += xr * L.MJ[r][lane];
+        }
+        if (lane < NV) L.nu[lane] += dnu;
+    }
+
+    // ---- integratePositions ---------------------------------------------------
+    if (lane < N) {
+        const float qd_new = L.nu[6 + lane];
+        qdd_out[lane] = (qd_new - L.qd[lane]) * rcp(dt);
+        L.qd[lane] = qd_new;
+        L.q[lane] += dt * qd_new;
+    }
+    const SV V = {{L.nu[0], L.nu[1], L.nu[2]}, {L.nu[3], L.nu[4], L.nu[5]}};
+    integrate_pose(R0, V, dt, base);
+    base.V = V;
+    return active;
+}
+
+#undef MW_LANE0
+
+}  // namespace dev
+}  // namespace mw

@@ -12,6 +12,7 @@ _FILES = {
     "panda": "panda.urdf",
     "cube": "cube.urdf",
     "quadruped": "quadruped.urdf",
+    "humanoid32": "humanoid32.urdf",
     "ground_plane": "ground_plane.sdf",
 }
 

@@ -127,6 +127,8 @@ SIGNATURES = [
     ("mw_contacts_enabled", ctypes.c_int, [_P, _IP]),
     ("mw_get_contacts", ctypes.c_int, [_P, _I, _D, _I, _IP]),
     ("mw_get_contact_bodies", ctypes.c_int, [_P, _I, _IP, _I, _IP]),
+    ("mw_float_kernel", ctypes.c_int, [_P, _IP]),
+    ("mw_constraint_overflow", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     ("mw_device_ptr", ctypes.c_int, [_P, _S, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("mw_vecenv_create", ctypes.c_int, [_P, ctypes.POINTER(MwTaskConfig), ctypes.POINTER(_P)]),

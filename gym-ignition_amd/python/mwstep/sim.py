@@ -248,6 +248,17 @@ class Simulator:
                                               cap, ctypes.byref(n)), "contact_bodies")
         return out[:min(n.value, cap)].copy()
 
+    def float_kernel(self) -> int:
+        """0: not an articulated floating model, 1: world-per-lane kernel, 2: world-per-wavefront kernel."""
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_float_kernel(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def constraint_overflow(self) -> int:
+        v = ctypes.c_int64()
+        N.check(N.lib().mw_constraint_overflow(self.handle, ctypes.byref(v)))
+        return v.value
+
     def export_model(self) -> np.ndarray:
         out = np.zeros(34 * self.dofs + 3)
         N.check(N.lib().mw_model_export(self.handle, N.dptr(out), len(out)))

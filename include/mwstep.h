@@ -194,6 +194,13 @@ int mw_get_contacts(const mw_sim* sim, int32_t w, double* out, int32_t cap, int3
  * base link, i >= 0 = the link moved by joint i (Link::contacts,
  * Link.cpp:365-440, collects the contacts of one link). */
 int mw_get_contact_bodies(const mw_sim* sim, int32_t w, int32_t* bodies, int32_t cap, int32_t* n);
+/* Articulated floating-base models: which kernel steps them -- 0 none (not
+ * such a model), 1 one world per lane (small compiled trees), 2 one world per
+ * wavefront (any tree of <= 48 bodies; MWSTEP_WAVE_TREE=1 forces it) -- and the
+ * number of constraint rows the wave kernel dropped so far (its per-step
+ * capacity is 64 active rows; 0 in every test and bench configuration). */
+int mw_float_kernel(const mw_sim* sim, int32_t* kind);
+int mw_constraint_overflow(const mw_sim* sim, int64_t* rows);
 
 /* Zero-copy device views, float32 [n_dofs][n_worlds] (world index fastest):
  * the SoA state "q", "qd", "qdd", and "position_target" (the Position-mode

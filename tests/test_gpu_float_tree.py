@@ -40,8 +40,8 @@ def _quat_to_R(q):
 
 def _model(name):
     from mwstep import get_model_file
-    if name == "quadruped":
-        return get_model_file("quadruped")
+    if name in ("quadruped", "humanoid32"):
+        return get_model_file(name)
     return chain_urdf(int(name[-1]))
 
 
@@ -67,16 +67,21 @@ def _random_states(cm, W, rng):
     return f32(q), f32(qd), f32(np.column_stack([pos, quat])), f32(np.column_stack([lin, angv])), f32(tau)
 
 
-@pytest.mark.parametrize("name", ["quadruped", "chain1", "chain2", "chain3"])
-def test_one_step_parity_with_contacts(require_gpu, oracle, name):
+@pytest.mark.parametrize("name, kernel", [("quadruped", "lane"), ("chain1", "lane"), ("chain2", "lane"),
+                                          ("chain3", "lane"), ("quadruped", "wave"), ("chain2", "wave"),
+                                          ("humanoid32", "wave")])
+def test_one_step_parity_with_contacts(require_gpu, oracle, monkeypatch, name, kernel):
     from mwstep import native as N
     from mwstep.sim import Simulator
     text = _model(name)
+    if kernel == "wave":
+        monkeypatch.setenv("MWSTEP_WAVE_TREE", "1")
     W, pgs, mu = 256, 50, 0.8
     rng = np.random.default_rng(11)
     cm = oracle.load_urdf(text)
     q, qd, pose, vel, tau = _random_states(cm, W, rng)
     sim = Simulator(text, n_worlds=W, pgs_iters=pgs)
+    assert sim.float_kernel() == (2 if kernel == "wave" else 1)
     sim.set_ground_plane(True, mu)
     sim.enable_contacts(True)
     sim.set("reset_q", q)
@@ -133,7 +138,8 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, name):
             e.update(pose=0.0, q=0.0, vel=0.0, qd=0.0, force=0.0)
         for k in worst:
             worst[k] = max(worst[k], e[k])
-    print(f"float tree {name}: one-step " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
+    assert sim.constraint_overflow() == 0
+    print(f"float tree {name} ({kernel}): one-step " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
           f", {n_contact}/{W} worlds in contact, ill-conditioned: {[(w, f'{a:.1e}', f'{b:.1e}') for w, a, b in ill]}")
     assert n_contact > W // 4
     assert len(ill) <= W // 20
@@ -230,5 +236,81 @@ def test_run_device_equals_run(require_gpu):
     assert np.array_equal(sims[0].get("q"), sims[1].get("q"))
     assert np.array_equal(sims[0].contacts(5), sims[1].contacts(5))
     assert len(sims[0].contacts(5)) == 4
+    for s in sims:
+        s.close()
+
+
+HUMANOID_Z = 0.535
+
+
+def _humanoid_gains(names):
+    # stiff legs / torso, soft arms / neck (explicit PD: D dt / I_eff < 2)
+    stiff = lambda n: "leg" in n or "torso" in n
+    return [(500.0, 5.0) if stiff(n) else (50.0, 0.5) for n in names]
+
+
+def test_humanoid_standing_closed_loop_parity(require_gpu, oracle):
+    """BASELINE config 5's workload shape on the iCub-class humanoid (32 dofs,
+    floating base, box feet): JointController PID hold for 1 s on the wave
+    kernel vs the fp64 oracle; the 8 foot corners carry the weight."""
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    W, H = 4, 1000
+    sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=50, pose=(0, 0, HUMANOID_Z, 1, 0, 0, 0))
+    assert sim.float_kernel() == 2
+    n = sim.dofs
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    sim.set_controller_period(1e-3)
+    gains = _humanoid_gains(sim.joint_names)
+    for d, (p, dd) in enumerate(gains):
+        sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
+    sim.set_control_mode(N.MODE_POSITION)
+    sim.set("position_target", np.zeros((W, n)))
+    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, HUMANOID_Z))
+    ow = oracle.FloatWorld(cm, pgs_iters=50)
+    og = [oracle.pid_gains(p, 0.0, dd, cmdmax=80.0, cmdmin=-80.0) for p, dd in gains]
+    st = [oracle.OrPidState() for _ in range(n)]
+    mode = np.full(n, oracle.FORCE, np.int32)
+    worst_q = worst_z = 0.0
+    for k in range(H):
+        tau = np.array([oracle.pid_update(og[d], st[d], ow.q[d], 1e-3) for d in range(n)])
+        ow.step(mode, tau)
+        sim.run()
+        if k % 100 == 99:
+            worst_q = max(worst_q, float(np.abs(sim.get("q") - ow.q).max()))
+            worst_z = max(worst_z, float(np.abs(sim.base_pose()[:, 2] - ow.p[2]).max()))
+    fz = [sum(r[8] for r in sim.contacts(w)) for w in range(W)]
+    print(f"humanoid32 standing H={H}: max|dq| {worst_q:.2e}, max|dz| {worst_z:.2e}, sum Fz {fz}")
+    assert worst_q <= 1e-3 and worst_z <= 1e-4
+    for w in range(W):
+        assert len(sim.contacts(w)) == 8
+        assert fz[w] == pytest.approx(36.4 * G, abs=0.5)
+    assert sim.constraint_overflow() == 0
+    sim.close()
+
+
+def test_wave_run_device_equals_run(require_gpu):
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    sims = []
+    for _ in range(2):
+        s = Simulator(get_model_file("humanoid32"), n_worlds=8, pose=(0, 0, HUMANOID_Z, 1, 0, 0, 0))
+        s.set_ground_plane(True, 1.0)
+        s.enable_contacts(True)
+        s.set_controller_period(1e-3)
+        for d, (p, dd) in enumerate(_humanoid_gains(s.joint_names)):
+            s.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
+        s.set_control_mode(N.MODE_POSITION)
+        s.set("position_target", np.zeros((8, s.dofs)))
+        sims.append(s)
+    for _ in range(100):
+        sims[0].run()
+    sims[1].run_device(100)
+    assert np.array_equal(sims[0].base_pose(), sims[1].base_pose())
+    assert np.array_equal(sims[0].get("q"), sims[1].get("q"))
+    assert np.array_equal(sims[0].contacts(3), sims[1].contacts(3))
     for s in sims:
         s.close()

@@ -130,13 +130,13 @@ def test_fixed_joint_lumping(N, oracle):
 
 
 @pytest.mark.parametrize("bad, why", [
-    # a floating base with two branches: not a compiled floating topology
-    ("<robot name='x'><link name='a'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<link name='c'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<joint name='j1' type='revolute'><parent link='a'/><child link='b'/></joint>"
-     "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>",
-     "topology of this floating-base model"),
+    # a floating chain of 13 joints: deeper than the wave kernel's stack
+    ("<robot name='x'>" + "".join(
+        f"<link name='l{i}'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+        for i in range(14)) + "".join(
+        f"<joint name='j{i}' type='revolute'><parent link='l{i}'/><child link='l{i + 1}'/></joint>"
+        for i in range(13)) + "</robot>",
+     "deeper than 12"),
     ("<robot name='x'><link name='a'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
      "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
      "<joint name='j' type='revolute'><parent link='a'/><child link='b'/><dynamics damping='0.1'/></joint></robot>",
