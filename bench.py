@@ -164,10 +164,11 @@ def main():
     panda = None
     if not args.no_panda and rank == 0 and world_size == 1 and args.task != "PandaPositionTracking":
         panda = panda_leg(args, dev, torch, dist)
-    contacts = quadruped = None
+    contacts = quadruped = humanoid = None
     if not args.no_contact_leg and rank == 0 and world_size == 1:
         contacts = contact_leg(args, dev, torch)
         quadruped = quadruped_leg(args, dev, torch)
+        humanoid = humanoid_leg(args, dev, torch)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
@@ -224,6 +225,7 @@ def main():
             "randomized": rand,
             "contacts_floating": contacts,
             "quadruped_floating": quadruped,
+            "humanoid_c5": humanoid,
         }
         print(json.dumps(out))
     for e in envs:
@@ -391,27 +393,59 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
     mode, period = dt), foot / trunk contacts enabled, PGS 20 iterations,
     one physics step per run, replayed from hipGraphs of mw_run_device."""
     import numpy as np
+    stand = np.array([0.6, -1.2] * 4)
+    rng = np.random.default_rng(args.seed)
+    out = float_tree_leg(args, dev, torch, "quadruped", W, pgs, 0.45, [(400.0, 10.0, 60.0)] * 8,
+                         stand + rng.uniform(-0.1, 0.1, (W, 8)), np.tile(stand, (W, 1)), rng)
+    out["workload"] = (f"{W} quadrupeds (16 kg, 8 dofs, floating base) standing on a ground plane under "
+                       f"JointController PID hold, sphere-foot / box-trunk contacts, PGS {pgs} iterations, dt = 1 ms")
+    return out
+
+
+def humanoid_leg(args, dev, torch, W=512, pgs=50):
+    """BASELINE config 5 on one GPU: 512 iCub-class humanoids (models/humanoid32.urdf:
+    32 dofs, 36.4 kg, floating base, box feet) standing on the ground plane
+    under the JointController PID hold (stiff legs / torso, soft arms),
+    contacts enabled, PGS 50 iterations, one physics step per run; the
+    one-world-per-wavefront kernel (wave_tree.hpp)."""
+    import numpy as np
+    from mwstep import get_model_file
+    from mwstep.sim import Simulator
+    probe = Simulator(get_model_file("humanoid32"), n_worlds=1)
+    names = probe.joint_names
+    probe.close()
+    gains = [(500.0, 5.0, 80.0) if ("leg" in n or "torso" in n) else (50.0, 0.5, 80.0) for n in names]
+    n = len(names)
+    rng = np.random.default_rng(args.seed)
+    out = float_tree_leg(args, dev, torch, "humanoid32", W, pgs, 0.535, gains,
+                         rng.uniform(-0.02, 0.02, (W, n)), np.zeros((W, n)), rng, K=200, G=20, warm=40)
+    out["workload"] = (f"{W} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) standing on a "
+                       f"ground plane under JointController PID hold, PGS {pgs} iterations, dt = 1 ms "
+                       "(BASELINE.json configs[4] on one GPU)")
+    return out
+
+
+def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, rng, K=500, G=50, warm=100):
+    """Time W floating-base worlds of `model` under a PID hold, one physics
+    step per run, replayed from hipGraphs of mw_run_device."""
+    import numpy as np
     from mwstep import get_model_file
     from mwstep import native as N
     from mwstep.sim import Simulator
-    K, warm, G = 500, 100, 50
-    stand = np.array([0.6, -1.2] * 4)
     stream = torch.cuda.Stream(device=dev)
-    sim = Simulator(get_model_file("quadruped"), n_worlds=W, device=dev.index, pgs_iters=pgs,
-                    stream=stream.cuda_stream, pose=(0, 0, 0.45, 1, 0, 0, 0))
-    sim.set_ground_plane(ground, 1.0)
+    sim = Simulator(get_model_file(model), n_worlds=W, device=dev.index, pgs_iters=pgs,
+                    stream=stream.cuda_stream, pose=(0, 0, z0, 1, 0, 0, 0))
+    sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
-    rng = np.random.default_rng(args.seed)
-    q0 = stand + rng.uniform(-0.1, 0.1, (W, 8))
     sim.set("reset_q", q0)
-    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), np.full(W, 0.45), np.ones(W), np.zeros((W, 3))])
+    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), np.full(W, z0), np.ones(W), np.zeros((W, 3))])
     sim.reset_base_pose(pose)
     sim.run(paused=True)
     sim.set_controller_period(1e-3)
-    for d in range(8):
-        sim.set_pid(d, [400.0, 0.0, 10.0, -60.0, 60.0, 0.0, 0.0, -1.0])
+    for d, (p, dd, lim) in enumerate(gains):
+        sim.set_pid(d, [p, 0.0, dd, -lim, lim, 0.0, 0.0, -1.0])
     sim.set_control_mode(N.MODE_POSITION)
-    sim.set("position_target", np.tile(stand, (W, 1)))
+    sim.set("position_target", targets)
     with torch.cuda.stream(stream):
         sim.run_device(warm)
         stream.synchronize()
@@ -432,13 +466,16 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     steps = n_rep * G
-    feet = [len(sim.contacts(w)) for w in range(0, W, W // 64)]
-    out = {"workload": f"{W} quadrupeds (16 kg, 8 dofs, floating base) standing on a ground plane under "
-                       "JointController PID hold, sphere-foot / box-trunk contacts, PGS 20 iterations, dt = 1 ms",
-           "value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
+    sample = range(0, W, max(1, W // 64))
+    pts = [len(sim.contacts(w)) for w in sample]
+    z = sim.base_pose()[:, 2]
+    out = {"value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
            "ms_per_step": round(elapsed / steps * 1e3, 6),
            "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
-           "contact_points_sampled": f"{sum(feet)} in {len(feet)} worlds"}
+           "float_kernel": {1: "world per lane (float_tree.hpp)", 2: "world per wavefront (wave_tree.hpp)"}.get(sim.float_kernel()),
+           "contact_points_sampled": f"{sum(pts)} in {len(pts)} worlds",
+           "base_z_range_after": [round(float(z.min()), 4), round(float(z.max()), 4)],
+           "constraint_overflow": int(sim.constraint_overflow())}
     sim.close()
     return out
 
