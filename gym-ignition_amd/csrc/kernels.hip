@@ -635,13 +635,25 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     }
     uint32_t active = 0u;
     int ovf = 0;
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
+            MW_PROF_T(ta);
             if (lane < N)
                 L.tau[lane] = dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
-            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, L.qdd, &ovf);
+            MW_PROF_T(tb);
+            MW_PROF_ACC(0, ta, tb);
+            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, L.qdd, &ovf, prof);
+            MW_PROF_T(tc);
+            MW_PROF_ACC(7, ta, tc);
         }
     }
+#ifdef MW_WAVE_PROF
+    if (lane == 0)
+        for (int k = 0; k < kWaveProfPhases; ++k) atomicAdd(&g_wave_prof[k], prof[k]);
+#else
+    (void)prof;
+#endif
     if (lane < N) {
         const size_t k = static_cast<size_t>(lane) * W + w;
         S.q[k] = L.q[lane];
@@ -883,6 +895,15 @@ hipError_t float_n(const ChainF* P, bool cons, const FloatF* F, const SimDev& S,
 }
 }  // namespace
 
+#ifdef MW_WAVE_PROF
+// debug builds only: read and clear the wave kernel's phase counters
+extern "C" int mw_debug_wave_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_wave_prof), sizeof(dev::g_wave_prof)) != hipSuccess) return 1;
+    const unsigned long long z[dev::kWaveProfPhases] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(dev::g_wave_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const FloatF* F, const SimDev& S, const FreeDev& D,
                            const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(W)), block(dev::kWaveLanes);
@@ -892,6 +913,13 @@ hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const FloatF* F, c
                                contacts, overflow);
         else
             hipLaunchKernelGGL((dev::wave_run_kernel<16, false>), grid, block, 0, st, P, F, n, S, D, pid, W, a,
+                               contacts, overflow);
+    } else if (n <= 32) {
+        if (cons)
+            hipLaunchKernelGGL((dev::wave_run_kernel<32, true>), grid, block, 0, st, P, F, n, S, D, pid, W, a,
+                               contacts, overflow);
+        else
+            hipLaunchKernelGGL((dev::wave_run_kernel<32, false>), grid, block, 0, st, P, F, n, S, D, pid, W, a,
                                contacts, overflow);
     } else if (n <= kMaxBodies) {
         if (cons)

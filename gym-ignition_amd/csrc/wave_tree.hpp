@@ -31,6 +31,10 @@ constexpr int kWaveLanes = 64;
 constexpr int kWaveMaxRows = 64;
 constexpr int kWaveMaxDepth = 12;
 
+struct alignas(16) F4 {
+    float x, y, z, w;
+};
+
 // per-body record (uniform), 75 words
 struct WaveBody {
     M3 R;        // joint transform (parent -> body)
@@ -57,10 +61,11 @@ struct WaveWorld {
     float q[MAXN], qd[MAXN], qdd[MAXN], tau[MAXN], vc[MAXN];
     uint32_t act[MAXN];
     float nu[kNv];
-    float J[kWaveMaxRows][kRowStride];
+    static constexpr int kJStride = (kNv + 3) & ~3;  // float4 rows: read as uniform broadcasts
+    alignas(16) float J[kWaveMaxRows][kJStride];
     float MJ[kWaveMaxRows][kRowStride];
-    float A[kWaveMaxRows][kWaveMaxRows + 1];
     float b[kWaveMaxRows], lo[kWaveMaxRows], hi[kWaveMaxRows];
+    F4 rc[kWaveMaxRows];         // PGS row constants {b, 1/A_rr, lo, hi}
     int32_t src[kWaveMaxRows];   // 3 slot + d, or kJointRow + 3 dof + type
     // contact slots
     float s_b[kMaxFloatSlots][3];   // body-frame point
@@ -73,6 +78,18 @@ struct WaveWorld {
 };
 
 __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63u); }
+
+// Phase timing (debug builds only: EXTRA=-DMW_WAVE_PROF, scripts/wave_prof.py):
+// shader-clock cycles per phase, summed over the worlds of a launch.
+#ifdef MW_WAVE_PROF
+constexpr int kWaveProfPhases = 8;
+__device__ unsigned long long g_wave_prof[kWaveProfPhases];
+#define MW_PROF_T(var) const long long var = clock64()
+#define MW_PROF_ACC(k, a, b) (prof[k] += static_cast<unsigned long long>((b) - (a)))
+#else
+#define MW_PROF_T(var)
+#define MW_PROF_ACC(k, a, b)
+#endif
 
 // sum over the 64 lanes (DPP: quad perms, half-row / row mirrors, row
 // broadcasts 15 and 31), the total read from lane 63; a fixed order, so the
@@ -204,7 +221,7 @@ __device__ __forceinline__ void wave_response(const ChainF* __restrict__ P, int 
     uint64_t path = 0;
     const int start = (k >= 0) ? k : j;
     for (int i = start; i >= 0; i = P->b[i].parent) path |= uint64_t{1} << i;
-    for (int e = 0; e < 6 + N; ++e) Jrow[e] = 0.f;
+    for (int e = 0; e < WaveWorld<MAXN>::kJStride; ++e) Jrow[e] = 0.f;
     // inward along the path: articulated bias impulse Bi and the kinematic
     // force Fi (for J); u_i parked in the lane's depth stack
     SV Bi = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Fi = Bi;
@@ -250,12 +267,15 @@ __device__ __forceinline__ void wave_response(const ChainF* __restrict__ P, int 
 template <int MAXN, bool CONS>
 __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                               FreeState& base, WaveWorld<MAXN>& L, float dt, int pgs_iters,
-                                              float* qdd_out, int* overflow) {
+                                              float* qdd_out, int* overflow, unsigned long long* prof) {
     const int lane = lane_id();
     const int NV = 6 + N;
+    MW_PROF_T(t0);
     const M3 R0 = quat_to_R(base.qw, base.qx, base.qy, base.qz);
     Chol6 L0;
     const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, qdd_out);
+    MW_PROF_T(t1);
+    MW_PROF_ACC(1, t0, t1);
     // integrateVelocities (lane e: nu component e)
     if (lane < NV) {
         float v;
@@ -397,6 +417,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         }
     }
 
+    MW_PROF_T(t2);
+    MW_PROF_ACC(2, t1, t2);
     if (R > 0) {
         // ---- responses (lane = row) ------------------------------------------
         for (int r0 = 0; r0 < R; r0 += kWaveLanes) {
@@ -429,45 +451,110 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                 }
             }
         }
-        // ---- Delassus matrix (lane = column) ------------------------------------
-        for (int c0 = 0; c0 < R; c0 += kWaveLanes) {
-            const int c = c0 + lane;
-            if (c < R) {
-                for (int r = 0; r < R; ++r) {
-                    float a = 0.f;
-                    for (int e = 0; e < NV; ++e) a += L.J[r][e] * L.MJ[c][e];
-                    L.A[r][c] = a;
+        MW_PROF_T(t3);
+        MW_PROF_ACC(3, t2, t3);
+        // ---- Delassus matrix: lane = column c, kept in registers a[r] = A[r][c] --
+        // (A is symmetric, so a[] is also row c).  J rows are read as uniform
+        // float4 broadcasts; the column's M^-1 J^T row sits in registers.
+        constexpr int kJS = WaveWorld<MAXN>::kJStride;
+        const int ncr = (n_contact_rows < R) ? n_contact_rows : R;
+        float mjc[kJS];
+#pragma unroll
+        for (int e = 0; e < kJS; ++e) mjc[e] = (lane < R && e < NV) ? L.MJ[lane][e] : 0.f;
+        float a[kWaveMaxRows];
+        float dg = 1.f;
+#pragma unroll
+        for (int r = 0; r < kWaveMaxRows; ++r) {
+            a[r] = 0.f;
+            if (r < R) {
+                const F4* jr = reinterpret_cast<const F4*>(L.J[r]);
+                float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                for (int e4 = 0; e4 < kJS / 4; ++e4) {
+                    const F4 j = jr[e4];
+                    s0 += j.x * mjc[4 * e4] + j.z * mjc[4 * e4 + 2];
+                    s1 += j.y * mjc[4 * e4 + 1] + j.w * mjc[4 * e4 + 3];
                 }
-                L.A[c][c] *= 1.f + ((L.src[c] >= kJointRow) ? kJointCfm : kContactCfm);
+                a[r] = s0 + s1;
+                if (lane == r) {
+                    a[r] *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
+                    dg = a[r];
+                }
             }
         }
-        // ---- PGS: x_c in lane c ----------------------------------------------------
-        float x = 0.f;
+        MW_PROF_T(t4);
+        MW_PROF_ACC(4, t3, t4);
+        // ---- PGS: impulses x[r] uniform (registers), residual w_c = sum_r A[c][r] x_r
+        // in lane c.  Rows in order (the oracle's Gauss-Seidel order), padded
+        // to blocks of 8 with inert rows (zero column, b = 0, bounds [0, 0]) so
+        // the sweep is branch-free inside a block.  The residual is rebuilt at
+        // the start of every sweep and updated by column r (= a[r], symmetry)
+        // after row r moves, so a row costs one lane read of w, one uniform
+        // LDS broadcast of its constants {b, 1/A_rr, lo, hi} (off the chain)
+        // and a handful of dependent VALU ops.  Friction rows store the
+        // bounds (-1, 1), scaled by mu x_normal of the same contact.
+        const int Rpad = (R + 7) & ~7;
+        if (lane < Rpad) {
+            F4 c = {0.f, 0.f, 0.f, 0.f};
+            if (lane < R) {
+                c.x = L.b[lane];
+                c.y = rcp(dg);
+                if (lane < ncr) {
+                    const bool normal = (lane % 3) == 0;
+                    c.z = normal ? 0.f : -1.f;
+                    c.w = normal ? kBig : 1.f;
+                } else {
+                    c.z = L.lo[lane];
+                    c.w = L.hi[lane];
+                }
+            }
+            L.rc[lane] = c;
+        }
+        const float mu = F->mu;
+        float x[kWaveMaxRows];
+#pragma unroll
+        for (int r = 0; r < kWaveMaxRows; ++r) x[r] = 0.f;
         for (int it = 0; it < pgs_iters; ++it) {
-            for (int r = 0; r < R; ++r) {
-                const float prod = (lane < R) ? L.A[r][lane] * x : 0.f;
-                const float s = wave_sum(prod);
-                const float xr = read_lane(x, r);
-                float v = xr + (L.b[r] - s) * rcp(L.A[r][r]);
-                const int src = L.src[r];
-                float lo = L.lo[r], hi = L.hi[r];
-                if (src < kJointRow && (src % 3) != 0) {
-                    hi = F->mu * read_lane(x, r - src % 3);
-                    lo = -hi;
+            float w = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
+                if (rb >= Rpad) break;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) w += a[rb + k] * x[rb + k];
+            }
+#pragma unroll
+            for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
+                if (rb >= Rpad) break;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int r = rb + k;
+                    const F4 c = L.rc[r];
+                    float v = x[r] + (c.x - read_lane(w, r)) * c.y;
+                    float sc = 1.f;
+                    if (r % 3 != 0) sc = (r < ncr) ? mu * x[r - r % 3] : 1.f;
+                    v = fminf(fmaxf(v, c.z * sc), c.w * sc);
+                    w += a[r] * (v - x[r]);
+                    x[r] = v;
                 }
-                v = fminf(fmaxf(v, lo), hi);
-                if (lane == r) x = v;
             }
         }
+        MW_PROF_T(t5);
+        MW_PROF_ACC(5, t4, t5);
         // ---- nu += MJ^T x (lane = component); impulses to the slots ----------------
+        float xl = 0.f, dnu = 0.f;
+#pragma unroll
+        for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
+            if (rb >= Rpad) break;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = rb + k;
+                xl = (lane == r) ? x[r] : xl;
+                if (r < R && lane < NV) dnu += x[r] * L.MJ[r][lane];
+            }
+        }
         if (lane < R) {
             const int src = L.src[lane];
-            if (src < kJointRow) L.s_x[src / 3][src % 3] = x;
-        }
-        float dnu = 0.f;
-        for (int r = 0; r < R; ++r) {
-            const float xr = read_lane(x, r);
-            if (lane < NV) dnu += xr * L.MJ[r][lane];
+            if (src < kJointRow) L.s_x[src / 3][src % 3] = xl;
         }
         if (lane < NV) L.nu[lane] += dnu;
     }
@@ -482,6 +569,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
     const SV V = {{L.nu[0], L.nu[1], L.nu[2]}, {L.nu[3], L.nu[4], L.nu[5]}};
     integrate_pose(R0, V, dt, base);
     base.V = V;
+    MW_PROF_T(t6);
+    MW_PROF_ACC(6, t2, t6);
     return active;
 }
 

@@ -1,0 +1,50 @@
+"""Phase breakdown of the one-world-per-wavefront kernel (wave_tree.hpp) on
+BASELINE config 5's workload (512 humanoid32 worlds standing, PGS 50).
+
+Needs the debug build with shader-clock phase counters:
+    make -C gym-ignition_amd BUILD=build_prof LIB=libmwstep_prof.so EXTRA=-DMW_WAVE_PROF
+    MWSTEP_LIB=gym-ignition_amd/libmwstep_prof.so python scripts/wave_prof.py [W] [pgs]
+Prints shader-clock cycles per world-step of every phase (sum over worlds / worlds / steps)."""
+import ctypes
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-ignition_amd", "python"))
+import numpy as np  # noqa: E402
+
+from mwstep import get_model_file  # noqa: E402
+from mwstep import native as N  # noqa: E402
+from mwstep.sim import Simulator  # noqa: E402
+
+W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+PGS = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+T = 20
+PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
+          "Delassus (lane = column)", "PGS", "rows total (responses .. integrate)", "whole substep"]
+
+sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=PGS, pose=(0, 0, 0.535, 1, 0, 0, 0))
+names = sim.joint_names
+sim.set_ground_plane(True, 1.0)
+sim.enable_contacts(True)
+sim.set_controller_period(1e-3)
+for d, n in enumerate(names):
+    p, dd = (500.0, 5.0) if ("leg" in n or "torso" in n) else (50.0, 0.5)
+    sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
+sim.set_control_mode(N.MODE_POSITION)
+sim.set("position_target", np.zeros((W, sim.dofs)))
+sim.run_device(50)
+L = N.lib()
+fn = L.mw_debug_wave_prof
+fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+buf = (ctypes.c_ulonglong * 8)()
+fn(buf)  # clear
+t0 = time.perf_counter()
+sim.run_device(T)
+sim.get("q")
+dt = time.perf_counter() - t0
+fn(buf)
+print(f"{W} worlds, PGS {PGS}, {T} steps: {dt / T * 1e6:.1f} us/step wall; contacts in world 0: {len(sim.contacts(0))}")
+for k, name in enumerate(PHASES):
+    print(f"  {name:40s} {buf[k] / W / T:12.0f} cycles/world-step")
+sim.close()
