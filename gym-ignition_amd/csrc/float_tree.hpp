@@ -67,6 +67,15 @@ struct FloatF {
     float shape_size[kMaxFloatShapes][3];
     float shape_R[kMaxFloatShapes][9];
     float shape_p[kMaxFloatShapes][3];
+    // tree levels for the level-parallel ABA of the wave kernel (wave_tree.hpp):
+    // depth of every body (0 = child of the base), its rank among the
+    // children of its parent counted from the highest index (the order the
+    // serial inward pass adds them in), the number of levels and the largest
+    // number of children of one body (or of the base)
+    int32_t levels;
+    int32_t fanout;
+    int8_t body_depth[kMaxBodies];
+    int8_t body_srank[kMaxBodies];
 };
 
 namespace dev {

@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -304,6 +305,19 @@ void build_float(mw_sim* s) {
     }
     F.n_shapes = static_cast<int32_t>(std::min(shapes.size(), static_cast<size_t>(mw::kMaxFloatShapes)));
     F.n_slots = slot;
+    const int n = std::min(M.dofs(), mw::kMaxBodies);
+    std::vector<int> children(n + 1, 0);  // [n] = the base
+    F.levels = 0;
+    for (int i = n - 1; i >= 0; --i) {
+        const int pa = M.bodies[i].parent;
+        F.body_srank[i] = static_cast<int8_t>(children[pa >= 0 ? pa : n]++);
+    }
+    for (int i = 0; i < n; ++i) {
+        const int pa = M.bodies[i].parent;
+        F.body_depth[i] = static_cast<int8_t>(pa >= 0 ? F.body_depth[pa] + 1 : 0);
+        F.levels = std::max<int32_t>(F.levels, F.body_depth[i] + 1);
+    }
+    F.fanout = *std::max_element(children.begin(), children.end());
 }
 
 int upload_params(mw_sim* s) {

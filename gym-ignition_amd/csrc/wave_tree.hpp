@@ -53,11 +53,20 @@ struct WaveBody {
 };
 static_assert(sizeof(WaveBody) == 75 * 4, "WaveBody layout");
 
+// child -> parent accumulator of the inward pass (28 words, float4-aligned)
+struct alignas(16) WaveAcc {
+    SI I;
+    SV B;
+    float pad_;
+};
+static_assert(sizeof(WaveAcc) == 28 * 4, "WaveAcc layout");
+
 template <int MAXN>
 struct WaveWorld {
     static constexpr int kNv = 6 + MAXN;
     static constexpr int kRowStride = kNv | 1;  // odd: lane-strided row access is conflict-free
     WaveBody body[MAXN];
+    WaveAcc acc[MAXN + 1];       // [MAXN] = the base
     float q[MAXN], qd[MAXN], qdd[MAXN], tau[MAXN], vc[MAXN];
     uint32_t act[MAXN];
     float nu[kNv];
@@ -115,97 +124,115 @@ __device__ __forceinline__ float read_lane(float x, int l) {
 // the whole wave runs these with identical values; lane 0 stores
 #define MW_LANE0 if (lane_id() == 0)
 
-// Floating-base ABA, uniform (runtime topology).  Returns a0 and leaves
-// qdd_i in qdd_out (L.qdd, LDS).
+// Floating-base ABA, level-parallel (runtime topology): lane i owns body i
+// and keeps its quantities in registers; the passes walk the tree by depth
+// level (all bodies of one level at once), so a step costs `levels` body
+// updates instead of N.  Parent -> child data (velocity, world pose,
+// acceleration) goes through the body records in LDS; child -> parent
+// articulated inertias and biases are added into the parent's accumulator
+// one sibling rank at a time, highest body index first (the order of the
+// serial inward pass), so the sums are deterministic.  Every lane then has
+// IA0 and B0 of the base (broadcast reads) and solves a0 itself.  Returns a0
+// and leaves qdd_i in qdd_out (L.qdd, LDS) and the per-body records that the
+// later phases read (R, p, U, psi, depth, Rw, pw) in L.body.
 template <int MAXN>
 __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                        const M3& R0, const f3& p0, const SV& V0, WaveWorld<MAXN>& L, Chol6& L0,
                                        float* qdd_out) {
-    const f3 g0 = mulT(R0, mk(F->g[0], F->g[1], F->g[2]));
-    // outward: kinematics, velocities, bias forces, world poses, depths
-    for (int i = 0; i < N; ++i) {
-        const BodyF& b = P->b[i];
-        const int pa = b.parent;
-        M3 R;
-        f3 p;
-        joint_pose(b, L.q[i], R, p);
-        const SV Sq = motion(b, L.qd[i]);
-        const SV Vp = (pa >= 0) ? L.body[pa].V : V0;
-        const SV Vi = ad_inv(R, p, Vp) + Sq;
-        // gravity in the body frame: R_w^T g_world
-        const M3& Rwp = (pa >= 0) ? L.body[pa].Rw : R0;
-        const f3 pwp = (pa >= 0) ? L.body[pa].pw : p0;
-        M3 Rw;
+    const int lane = lane_id();
+    const bool own = lane < N;
+    const int i = own ? lane : 0;
+    const BodyF& b = P->b[i];
+    const int pa = b.parent;
+    const int depth = own ? F->body_depth[i] : -1;
+    const int srank = F->body_srank[i];
+    const int levels = F->levels, fanout = F->fanout;
+    const f3 gw = mk(F->g[0], F->g[1], F->g[2]);
+    const int slot = (pa >= 0) ? pa : MAXN;  // accumulator of the parent (MAXN = the base)
+    // accumulators start empty
+    if (lane <= MAXN) L.acc[lane] = WaveAcc{};
+    // outward: kinematics, velocities, bias forces, world poses
+    M3 R, Rw;
+    f3 p, pw;
+    SV V, eta, B;
+    float tau = 0.f;
+    for (int d = 0; d < levels; ++d) {
+        if (depth == d) {
+            joint_pose(b, L.q[i], R, p);
+            const SV Sq = motion(b, L.qd[i]);
+            const SV Vp = (pa >= 0) ? L.body[pa].V : V0;
+            const M3 Rwp = (pa >= 0) ? L.body[pa].Rw : R0;
+            const f3 pwp = (pa >= 0) ? L.body[pa].pw : p0;
+            V = ad_inv(R, p, Vp) + Sq;
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+            for (int r = 0; r < 3; ++r)
 #pragma unroll
-            for (int c = 0; c < 3; ++c)
-                Rw.m[r * 3 + c] = Rwp.m[r * 3] * R.m[c] + Rwp.m[r * 3 + 1] * R.m[3 + c] + Rwp.m[r * 3 + 2] * R.m[6 + c];
-        const f3 pw = pwp + mul(Rwp, p);
-        const f3 gi = mulT(Rw, mk(F->g[0], F->g[1], F->g[2]));
-        const SV eta = {cross(Vi.w, Sq.w), cross(Vi.w, Sq.v) + cross(Vi.v, Sq.w)};
-        const SV Bi = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), Vi, gi);
-        const int depth = (pa >= 0) ? L.body[pa].depth + 1 : 0;
-        MW_LANE0 {
-            WaveBody& s = L.body[i];
-            s.R = R;
-            s.p = p;
-            s.V = Vi;
-            s.Rw = Rw;
-            s.pw = pw;
-            s.eta = eta;
-            s.B = Bi;
-            s.IA = rigid(b, b.mass);
-            s.depth = depth;
+                for (int c = 0; c < 3; ++c)
+                    Rw.m[r * 3 + c] =
+                        Rwp.m[r * 3] * R.m[c] + Rwp.m[r * 3 + 1] * R.m[3 + c] + Rwp.m[r * 3 + 2] * R.m[6 + c];
+            pw = pwp + mul(Rwp, p);
+            eta = {cross(V.w, Sq.w), cross(V.w, Sq.v) + cross(V.v, Sq.w)};
+            B = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), V,
+                           mulT(Rw, gw));
+            L.body[i].V = V;
+            L.body[i].Rw = Rw;
+            L.body[i].pw = pw;
         }
     }
-    // inward: articulated inertias and biases accumulate into the parents
-    SI IA0 = rigid_base(*F);
-    SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
-                       Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, g0);
-    for (int i = N - 1; i >= 0; --i) {
-        const BodyF& b = P->b[i];
-        const int pa = b.parent;
-        const WaveBody& s = L.body[i];
-        const SI AI = s.IA;
-        const SV U = ais(AI, b);
-        const float psi = rcp(proj(b, U));
-        const SV AIeta = mul(AI, s.eta);
-        const float tt = L.tau[i] - proj(b, AIeta + s.B);
-        const SI c = to_parent(s.R, s.p, downdate(AI, U, psi));
-        const SV cb = dad_inv(s.R, s.p, s.B + AIeta + (psi * tt) * U);
-        if (pa >= 0) {
-            SI Ip = L.body[pa].IA;
-            Ip += c;
-            const SV Bp = L.body[pa].B + cb;
-            MW_LANE0 {
-                L.body[pa].IA = Ip;
-                L.body[pa].B = Bp;
+    if (own) tau = L.tau[i];
+    // inward, deepest level first
+    SV U;
+    float psi = 0.f, tt = 0.f;
+    for (int d = levels - 1; d >= 0; --d) {
+        const bool mine = (depth == d);
+        SI c;
+        SV cb;
+        if (mine) {
+            const WaveAcc in = L.acc[i];
+            SI AI = rigid(b, b.mass);
+            AI += in.I;
+            const SV Bt = B + in.B;
+            U = ais(AI, b);
+            psi = rcp(proj(b, U));
+            const SV AIeta = mul(AI, eta);
+            tt = tau - proj(b, AIeta + Bt);
+            c = to_parent(R, p, downdate(AI, U, psi));
+            cb = dad_inv(R, p, Bt + AIeta + (psi * tt) * U);
+        }
+        for (int k = 0; k < fanout; ++k) {
+            if (mine && srank == k) {
+                WaveAcc acc = L.acc[slot];
+                acc.I += c;
+                acc.B = acc.B + cb;
+                L.acc[slot] = acc;
             }
-        } else {
-            IA0 += c;
-            B0 = B0 + cb;
-        }
-        MW_LANE0 {
-            L.body[i].U = U;
-            L.body[i].psi = psi;
-            L.body[i].tt = tt;
         }
     }
+    const WaveAcc base = L.acc[MAXN];
+    SI IA0 = rigid_base(*F);
+    IA0 += base.I;
+    const SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
+                             Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
+                  base.B;
     L0.factor(IA0);
     const SV a0 = L0.solve(-1.f * B0);
-    // outward: accelerations (reuse V for a)
-    for (int i = 0; i < N; ++i) {
-        const BodyF& b = P->b[i];
-        const int pa = b.parent;
-        const WaveBody& s = L.body[i];
-        const SV ap = ad_inv(s.R, s.p, (pa >= 0) ? L.body[pa].V : a0);
-        const float qdd = s.psi * (s.tt - dot(s.U, ap));
-        const SV ai = ap + s.eta + motion(b, qdd);
-        MW_LANE0 {
-            L.body[i].V = ai;
+    // outward: accelerations (the V record now carries a)
+    for (int d = 0; d < levels; ++d) {
+        if (depth == d) {
+            const SV ap = ad_inv(R, p, (pa >= 0) ? L.body[pa].V : a0);
+            const float qdd = psi * (tt - dot(U, ap));
+            L.body[i].V = ap + eta + motion(b, qdd);
             qdd_out[i] = qdd;
         }
+    }
+    if (own) {
+        WaveBody& s = L.body[i];
+        s.R = R;
+        s.p = p;
+        s.U = U;
+        s.psi = psi;
+        s.tt = tt;
+        s.depth = depth;
     }
     return a0;
 }
