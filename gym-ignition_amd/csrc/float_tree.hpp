@@ -76,6 +76,7 @@ struct FloatF {
     int32_t fanout;
     int8_t body_depth[kMaxBodies];
     int8_t body_srank[kMaxBodies];
+    uint64_t body_path[kMaxBodies];  // bit k: body k is body i or one of its ancestors
 };
 
 namespace dev {

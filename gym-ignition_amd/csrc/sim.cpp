@@ -316,6 +316,7 @@ void build_float(mw_sim* s) {
         const int pa = M.bodies[i].parent;
         F.body_depth[i] = static_cast<int8_t>(pa >= 0 ? F.body_depth[pa] + 1 : 0);
         F.levels = std::max<int32_t>(F.levels, F.body_depth[i] + 1);
+        F.body_path[i] = (uint64_t{1} << i) | (pa >= 0 ? F.body_path[pa] : uint64_t{0});
     }
     F.fanout = *std::max_element(children.begin(), children.end());
 }

@@ -117,6 +117,16 @@ __device__ __forceinline__ float wave_sum(float x) {
 #endif
 }
 
+// min(max(v, lo), hi) for lo <= hi (every PGS bound pair is ordered): one
+// v_med3_f32 on the device
+__device__ __forceinline__ float clamp_ordered(float v, float lo, float hi) {
+#ifdef MW_HOST_TEST
+    return fminf(fmaxf(v, lo), hi);
+#else
+    return __builtin_amdgcn_fmed3f(v, lo, hi);
+#endif
+}
+
 __device__ __forceinline__ float read_lane(float x, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
@@ -239,39 +249,52 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
 
 // Per-lane response to a spatial impulse f on body k (k = -1: base) and/or
 // a unit impulse on dof j: J = J_k^T f (generalized row), MJ = M^-1 (J^T + e_j).
-// Writes J (if Jrow) and MJ to the lane's LDS rows.
+// Writes J (if Jrow) and MJ to the lane's LDS rows and returns J nu.
+// The path to the base comes from the model's ancestor masks (no dependent
+// parent loads); on the outward pass a body whose parent is the previous
+// body takes the parent's response from registers, so only branch points
+// wait on the lane's LDS stack.
 template <int MAXN>
-__device__ __forceinline__ void wave_response(const ChainF* __restrict__ P, int N, WaveWorld<MAXN>& L,
-                                              const Chol6& L0, int k, int j, const SV& f, float* Jrow,
-                                              float* MJrow) {
+__device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
+                                               WaveWorld<MAXN>& L, const Chol6& L0, int k, int j, const SV& f,
+                                               float* Jrow, float* MJrow) {
     const int lane = lane_id();
-    uint64_t path = 0;
     const int start = (k >= 0) ? k : j;
-    for (int i = start; i >= 0; i = P->b[i].parent) path |= uint64_t{1} << i;
+    const uint64_t path = (start >= 0) ? F->body_path[start] : uint64_t{0};
     for (int e = 0; e < WaveWorld<MAXN>::kJStride; ++e) Jrow[e] = 0.f;
     // inward along the path: articulated bias impulse Bi and the kinematic
     // force Fi (for J); u_i parked in the lane's depth stack
     SV Bi = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Fi = Bi;
     if (k >= 0 || (k < 0 && j < 0)) { Bi = -1.f * f; Fi = f; }
-    for (int i = start; i >= 0; i = P->b[i].parent) {
+    float jv = 0.f;
+    for (uint64_t m = path; m != 0;) {
+        const int i = 63 - __builtin_clzll(m);
+        m &= ~(uint64_t{1} << i);
         const BodyF& b = P->b[i];
         const WaveBody& s = L.body[i];
-        Jrow[6 + i] = proj(b, Fi);
+        const float ji = proj(b, Fi);
+        Jrow[6 + i] = ji;
+        jv += ji * L.nu[6 + i];
         const float u = ((i == j) ? 1.f : 0.f) - proj(b, Bi);
         L.stack[s.depth][6][lane] = u;
         Bi = dad_inv(s.R, s.p, Bi + (s.psi * u) * s.U);
         Fi = dad_inv(s.R, s.p, Fi);
     }
     Jrow[0] = Fi.w.x; Jrow[1] = Fi.w.y; Jrow[2] = Fi.w.z; Jrow[3] = Fi.v.x; Jrow[4] = Fi.v.y; Jrow[5] = Fi.v.z;
+    jv += Fi.w.x * L.nu[0] + Fi.w.y * L.nu[1] + Fi.w.z * L.nu[2] + Fi.v.x * L.nu[3] + Fi.v.y * L.nu[4] +
+          Fi.v.z * L.nu[5];
     const SV dV0 = L0.solve(-1.f * Bi);
     MJrow[0] = dV0.w.x; MJrow[1] = dV0.w.y; MJrow[2] = dV0.w.z;
     MJrow[3] = dV0.v.x; MJrow[4] = dV0.v.y; MJrow[5] = dV0.v.z;
+    SV dv_prev = dV0;
     for (int i = 0; i < N; ++i) {
         const BodyF& b = P->b[i];
         const WaveBody& s = L.body[i];
         const int pa = b.parent;
         SV dvp_in;
-        if (pa >= 0) {
+        if (pa == i - 1) {
+            dvp_in = dv_prev;  // the previous body (or the base for i = 0)
+        } else if (pa >= 0) {
             const int dp = L.body[pa].depth;
             dvp_in = {{L.stack[dp][0][lane], L.stack[dp][1][lane], L.stack[dp][2][lane]},
                       {L.stack[dp][3][lane], L.stack[dp][4][lane], L.stack[dp][5][lane]}};
@@ -280,13 +303,15 @@ __device__ __forceinline__ void wave_response(const ChainF* __restrict__ P, int 
         }
         const SV dvp = ad_inv(s.R, s.p, dvp_in);
         const float u = ((path >> i) & 1u) ? L.stack[s.depth][6][lane] : 0.f;
-        const float m = s.psi * (u - dot(s.U, dvp));
-        MJrow[6 + i] = m;
-        const SV dv = dvp + motion(b, m);
+        const float mm = s.psi * (u - dot(s.U, dvp));
+        MJrow[6 + i] = mm;
+        const SV dv = dvp + motion(b, mm);
+        dv_prev = dv;
         float* st = &L.stack[s.depth][0][lane];
         st[0 * kWaveLanes] = dv.w.x; st[1 * kWaveLanes] = dv.w.y; st[2 * kWaveLanes] = dv.w.z;
         st[3 * kWaveLanes] = dv.v.x; st[4 * kWaveLanes] = dv.v.y; st[5 * kWaveLanes] = dv.v.z;
     }
+    return jv;
 }
 
 // One engine step of world L (state in L.q / L.qd / base; joint forces in
@@ -464,16 +489,14 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                     const f3 dir = {sg * L.s_R[slot][row * 3], sg * L.s_R[slot][row * 3 + 1],
                                     sg * L.s_R[slot][row * 3 + 2]};
                     const SV f = {cross(bpt, dir), dir};
-                    wave_response<MAXN>(P, N, L, L0, k, -1, f, L.J[r], L.MJ[r]);
-                    float jv = 0.f;
-                    for (int e = 0; e < NV; ++e) jv += L.J[r][e] * L.nu[e];
+                    const float jv = wave_response<MAXN>(P, F, N, L, L0, k, -1, f, L.J[r], L.MJ[r]);
                     const float bounce =
                         (d == 0) ? fminf(kContactErp * L.s_depth[slot] * rcp(dt), kContactMaxErv) : 0.f;
                     L.b[r] = bounce - jv;
                 } else {
                     const int dof = (src - kJointRow) / 3;
                     const SV zero = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-                    wave_response<MAXN>(P, N, L, L0, -2, dof, zero, L.J[r], L.MJ[r]);
+                    wave_response<MAXN>(P, F, N, L, L0, -2, dof, zero, L.J[r], L.MJ[r]);
                     for (int e = 0; e < NV; ++e) L.J[r][e] = (e == 6 + dof) ? 1.f : 0.f;
                 }
             }
@@ -559,7 +582,7 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                     float v = x[r] + (c.x - read_lane(w, r)) * c.y;
                     float sc = 1.f;
                     if (r % 3 != 0) sc = (r < ncr) ? mu * x[r - r % 3] : 1.f;
-                    v = fminf(fmaxf(v, c.z * sc), c.w * sc);
+                    v = clamp_ordered(v, c.z * sc, c.w * sc);
                     w += a[r] * (v - x[r]);
                     x[r] = v;
                 }
