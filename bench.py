@@ -105,6 +105,7 @@ def main():
                  + (" (model constant-folded)" if env.sim.baked_model() else ""))
     achieved_gbs = bpe * W / (kernel_us * 1e-6) / 1e9
     traffic = pmc_traffic(args.task, W)
+    floor_us = launch_floor(dev, torch) if rank == 0 else None
 
     # ------------------------------------------- fused open-loop rollout figure
     rollout = None
@@ -215,6 +216,9 @@ def main():
                 "bytes_per_env_step": bpe,
                 "algorithmic_bytes_per_launch": bpe * W,
                 "traffic_source": traffic["source"] if traffic else None,
+                "launch_floor_us": round(floor_us, 3) if floor_us else None,
+                "launch_floor_note": "per-node time of a hipGraph of 1-element kernels, same replay pattern: "
+                                     "the dispatch floor of a one-kernel-per-step closed loop",
             },
             "world_sweep": sweep,
             "cpu_baseline": cpu,
@@ -353,6 +357,32 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
         elapsed = float(tt.item())
     return {"elapsed": elapsed, "kernel_us": ev_start.elapsed_time(ev_end) * 1e3 / K, "G": G,
             "stream": groups[0][1], "groups": S}
+
+
+def launch_floor(dev, torch, K=2000, G=100):
+    """Per-node time of a hipGraph of G back-to-back 1-element kernels (a
+    torch add on one float), replayed like the step graphs: the dispatch /
+    completion floor any one-kernel-per-step closed loop pays on this GPU."""
+    st = torch.cuda.Stream(device=dev)
+    x = torch.zeros(1, device=dev)
+    with torch.cuda.stream(st):
+        for _ in range(10):
+            x.add_(1.0)
+        st.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=st):
+            for _ in range(G):
+                x.add_(1.0)
+        graph.replay()
+    st.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):
+        e0.record(st)
+        for _ in range(K // G):
+            graph.replay()
+        e1.record(st)
+    st.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (K // G * G)
 
 
 def panda_bytes_per_env_step(n=9):

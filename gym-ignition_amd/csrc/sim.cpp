@@ -550,7 +550,16 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         const bool compiled = ((s->topo == 0 && s->n <= 3) || s->topo == 2) &&
                               mw::float_workspace_words(s->n, s->h_float.n_slots) >= 0;
         const char* force_wave = std::getenv("MWSTEP_WAVE_TREE");
-        s->wave = !compiled || (force_wave && *force_wave && *force_wave != '0');
+        // small compiled topologies at large world counts take the lane kernel;
+        // up to kWaveWorldsMax worlds the wave kernel is faster (quadruped,
+        // profiles/r01f/quadruped_*_sweep.log: 1024 worlds 62 us/step wave vs
+        // 365 lane, 16384 worlds 638 wave vs 394 lane).  MWSTEP_WAVE_TREE=1 / =0
+        // forces the wave / lane kernel.
+        constexpr int kWaveWorldsMax = 4096;
+        if (force_wave && *force_wave)
+            s->wave = !compiled || *force_wave != '0';
+        else
+            s->wave = !compiled || s->W <= kWaveWorldsMax;
         if (s->wave) {
             std::vector<int> depth(s->n, 0);
             int max_depth = 0;

@@ -476,28 +476,37 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         for (int r0 = 0; r0 < R; r0 += kWaveLanes) {
             const int r = r0 + lane;
             if (r < R) {
+                // contact rows (impulse f on body k) and joint rows (unit
+                // impulse on dof j) share one response pass: the lanes of a
+                // mixed row set do not diverge into two serial passes
                 const int src = L.src[r];
-                if (src < kJointRow) {
-                    const int slot = src / 3, d = src % 3;
+                const bool contact = src < kJointRow;
+                int k = -2, j = -1;
+                SV f = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+                int slot = 0, d = 0;
+                if (contact) {
+                    slot = src / 3;
+                    d = src % 3;
                     int sh = 0;
                     while (sh + 1 < F->n_shapes && F->shape_slot0[sh + 1] <= slot) ++sh;
-                    const int k = F->shape_body[sh];
+                    k = F->shape_body[sh];
                     const f3 bpt = {L.s_b[slot][0], L.s_b[slot][1], L.s_b[slot][2]};
                     // body-frame direction R_k^T d: n -> row 2, t1 -> -row 1, t2 -> row 0
                     const int row = (d == 0) ? 2 : ((d == 1) ? 1 : 0);
                     const float sg = (d == 1) ? -1.f : 1.f;
                     const f3 dir = {sg * L.s_R[slot][row * 3], sg * L.s_R[slot][row * 3 + 1],
                                     sg * L.s_R[slot][row * 3 + 2]};
-                    const SV f = {cross(bpt, dir), dir};
-                    const float jv = wave_response<MAXN>(P, F, N, L, L0, k, -1, f, L.J[r], L.MJ[r]);
+                    f = {cross(bpt, dir), dir};
+                } else {
+                    j = (src - kJointRow) / 3;
+                }
+                const float jv = wave_response<MAXN>(P, F, N, L, L0, k, j, f, L.J[r], L.MJ[r]);
+                if (contact) {
                     const float bounce =
                         (d == 0) ? fminf(kContactErp * L.s_depth[slot] * rcp(dt), kContactMaxErv) : 0.f;
                     L.b[r] = bounce - jv;
                 } else {
-                    const int dof = (src - kJointRow) / 3;
-                    const SV zero = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-                    wave_response<MAXN>(P, F, N, L, L0, -2, dof, zero, L.J[r], L.MJ[r]);
-                    for (int e = 0; e < NV; ++e) L.J[r][e] = (e == 6 + dof) ? 1.f : 0.f;
+                    L.J[r][6 + j] = 1.f;  // the response pass left the joint row's J zero
                 }
             }
         }

@@ -74,8 +74,7 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, monkeypatch, name, k
     from mwstep import native as N
     from mwstep.sim import Simulator
     text = _model(name)
-    if kernel == "wave":
-        monkeypatch.setenv("MWSTEP_WAVE_TREE", "1")
+    monkeypatch.setenv("MWSTEP_WAVE_TREE", "1" if kernel == "wave" else "0")
     W, pgs, mu = 256, 50, 0.8
     rng = np.random.default_rng(11)
     cm = oracle.load_urdf(text)
