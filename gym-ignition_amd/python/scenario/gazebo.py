@@ -453,6 +453,59 @@ class Model:
             p = pn
         return R, p, v, w
 
+    def _link_acc(self, body: int):
+        """World linear acceleration of the link origin and world angular
+        acceleration of `body` from the joint accelerations of the last run
+        (Physics.cpp:1948-2079 reads them from DART's link frames).  The base
+        of a fixed-base model does not accelerate; a floating base's
+        acceleration is not read back by this backend."""
+        if self._sim.floating:
+            raise RuntimeError("link accelerations of floating-base models are not available in this backend")
+        R = self._base_R()
+        p = np.array(self.base_position(), dtype=float)
+        v = np.zeros(3)
+        w = np.zeros(3)
+        a = np.zeros(3)
+        al = np.zeros(3)
+        if body < 0:
+            return a, al
+        if self._export is None:
+            n = self._sim.dofs
+            self._export = self._sim.export_model()[:34 * n].reshape(n, 34)
+        rows = self._export
+        path = []
+        k = body
+        while k >= 0:
+            path.append(k)
+            k = int(rows[k, 33])
+        q = self._sim.get("q")[0]
+        qd = self._sim.get("qd")[0]
+        qdd = self._sim.get("qdd")[0]
+        for j in reversed(path):
+            row = rows[j]
+            E, r, ax = row[2:11].reshape(3, 3), row[11:14], row[14:17]
+            if row[0] == 0:
+                c, sn = np.cos(q[j]), np.sin(q[j])
+                K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+                Rr, pr = E @ (np.eye(3) + sn * K + (1 - c) * K @ K), r
+            else:
+                Rr, pr = E, r + q[j] * (E @ ax)
+            pn = p + R @ pr
+            d = pn - p
+            # rigid transport from the parent origin, then the joint's own terms
+            a = a + np.cross(al, d) + np.cross(w, np.cross(w, d))
+            v = v + np.cross(w, d)
+            R = R @ Rr
+            u = R @ ax  # joint axis in the world (fixed in parent and child)
+            if row[0] == 0:
+                al = al + u * qdd[j] + np.cross(w, u * qd[j])
+                w = w + u * qd[j]
+            else:
+                a = a + u * qdd[j] + 2.0 * np.cross(w, u * qd[j])
+                v = v + u * qd[j]
+            p = pn
+        return a, al
+
     def contacts_enabled(self) -> bool:
         return self._sim.contacts_enabled()
 
@@ -609,6 +662,30 @@ class Link:
 
     def world_angular_velocity(self) -> List[float]:
         return self._model._link_state(self._body)[3].tolist()
+
+    # body-fixed (link frame) velocities and accelerations: W_R_L^T times the
+    # world ones (Link.cpp bodyLinearVelocity & co., ign-gazebo issue 87 note)
+    def body_linear_velocity(self) -> List[float]:
+        R, _, v, _ = self._model._link_state(self._body)
+        return (R.T @ v).tolist()
+
+    def body_angular_velocity(self) -> List[float]:
+        R, _, _, w = self._model._link_state(self._body)
+        return (R.T @ w).tolist()
+
+    def world_linear_acceleration(self) -> List[float]:
+        return self._model._link_acc(self._body)[0].tolist()
+
+    def world_angular_acceleration(self) -> List[float]:
+        return self._model._link_acc(self._body)[1].tolist()
+
+    def body_linear_acceleration(self) -> List[float]:
+        R = self._model._link_state(self._body)[0]
+        return (R.T @ self._model._link_acc(self._body)[0]).tolist()
+
+    def body_angular_acceleration(self) -> List[float]:
+        R = self._model._link_state(self._body)[0]
+        return (R.T @ self._model._link_acc(self._body)[1]).tolist()
 
     def contacts_enabled(self) -> bool:
         return self._model.contacts_enabled()
