@@ -38,10 +38,48 @@ def _quat_to_R(q):
                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
 
 
+# a branched tree exercising the wave kernel's level-parallel passes: three
+# children at the base and at body 8, branch points at depths 0..2, a prismatic
+# joint every fifth body, random joint axes and frames (DFS order as listed)
+TREE_PARENTS = [-1, 0, 1, 1, 3, 3, 0, 6, -1, 8, 8, 8, 11, 2, -1, 14]
+
+
+def tree_urdf(parents=TREE_PARENTS, seed=5):
+    """A floating box base with a random branched tree: revolute / prismatic
+    joints about random unit axes, random origins and masses, a sphere on
+    every leaf."""
+    rng = np.random.default_rng(seed)
+    parts = ['<link name="base"><inertial><mass value="4.0"/>'
+             '<inertia ixx="0.05" iyy="0.06" izz="0.07" ixy="0.002" ixz="0" iyz="0"/></inertial>'
+             '<collision><geometry><box size="0.4 0.3 0.12"/></geometry></collision></link>']
+    leaves = set(range(len(parents))) - {p for p in parents if p >= 0}
+    for i, pa in enumerate(parents):
+        axis = rng.normal(size=3)
+        axis /= np.linalg.norm(axis)
+        prismatic = i % 5 == 4
+        lim = ('<limit lower="-0.2" upper="0.2" effort="80" velocity="10"/>' if prismatic else
+               '<limit lower="-1.5" upper="1.5" effort="50" velocity="30"/>')
+        xyz = " ".join(f"{v:.3f}" for v in rng.uniform(-0.15, 0.15, 3))
+        rpy = " ".join(f"{v:.3f}" for v in rng.uniform(-0.5, 0.5, 3))
+        tip = ('<collision><origin xyz="0 0 -0.1"/><geometry><sphere radius="0.03"/></geometry></collision>'
+               if i in leaves else "")
+        m = rng.uniform(0.2, 1.0)
+        parent = "base" if pa < 0 else f"l{pa}"
+        parts.append(f'<joint name="j{i}" type="{"prismatic" if prismatic else "revolute"}">'
+                     f'<parent link="{parent}"/><child link="l{i}"/><origin xyz="{xyz}" rpy="{rpy}"/>'
+                     f'<axis xyz="{axis[0]:.4f} {axis[1]:.4f} {axis[2]:.4f}"/>{lim}</joint>'
+                     f'<link name="l{i}"><inertial><origin xyz="0 0.01 -0.05"/><mass value="{m:.3f}"/>'
+                     f'<inertia ixx="{0.004 * m:.5f}" iyy="{0.005 * m:.5f}" izz="{0.002 * m:.5f}" ixy="0.0001" '
+                     f'ixz="0" iyz="0"/></inertial>{tip}</link>')
+    return '<robot name="ftree">' + "".join(parts) + "</robot>"
+
+
 def _model(name):
     from mwstep import get_model_file
     if name in ("quadruped", "humanoid32"):
         return get_model_file(name)
+    if name == "tree16":
+        return tree_urdf()
     return chain_urdf(int(name[-1]))
 
 
@@ -69,7 +107,7 @@ def _random_states(cm, W, rng):
 
 @pytest.mark.parametrize("name, kernel", [("quadruped", "lane"), ("chain1", "lane"), ("chain2", "lane"),
                                           ("chain3", "lane"), ("quadruped", "wave"), ("chain2", "wave"),
-                                          ("humanoid32", "wave")])
+                                          ("humanoid32", "wave"), ("tree16", "wave")])
 def test_one_step_parity_with_contacts(require_gpu, oracle, monkeypatch, name, kernel):
     from mwstep import native as N
     from mwstep.sim import Simulator
