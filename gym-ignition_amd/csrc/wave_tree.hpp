@@ -31,6 +31,8 @@ constexpr int kWaveLanes = 64;
 constexpr int kWaveMaxRows = 64;
 constexpr int kWaveMaxDepth = 12;
 
+typedef float v16f __attribute__((ext_vector_type(16)));
+
 struct alignas(16) F4 {
     float x, y, z, w;
 };
@@ -512,33 +514,50 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         }
         MW_PROF_T(t3);
         MW_PROF_ACC(3, t2, t3);
-        // ---- Delassus matrix: lane = column c, kept in registers a[r] = A[r][c] --
-        // (A is symmetric, so a[] is also row c).  J rows are read as uniform
-        // float4 broadcasts; the column's M^-1 J^T row sits in registers.
-        constexpr int kJS = WaveWorld<MAXN>::kJStride;
+        // ---- Delassus matrix A = J (M^-1 J^T)^T on the matrix cores ------------
+        // v_mfma_f32_32x32x2_f32 tiles (fp32 operands, fp32 accumulate): in
+        // k-step k, lane l supplies J[m0 + l%32][2k + l/32] and
+        // MJ[n0 + l%32][2k + l/32]; the 32x32 result holds column n0 + l%32 in
+        // lane l, rows 8(i/4) + 4(l/32) + i%4 in accumulator i.  One exchange
+        // of the two 32-lane halves then gives lane c all of column c (= row
+        // c: A is symmetric), a[r] = A[r][c], the layout the PGS keeps in
+        // registers.  Rows / columns >= R (stale LDS) are masked to zero.
         const int ncr = (n_contact_rows < R) ? n_contact_rows : R;
-        float mjc[kJS];
-#pragma unroll
-        for (int e = 0; e < kJS; ++e) mjc[e] = (lane < R && e < NV) ? L.MJ[lane][e] : 0.f;
+        const int lr = lane & 31, lh = lane >> 5;
+        const bool two = R > 32;
+        v16f t00 = {}, t01 = {}, t10 = {}, t11 = {};
+        for (int k = 0; 2 * k < NV; ++k) {
+            const int e = 2 * k + lh;
+            const bool ev = e < NV;
+            const float j0 = L.J[lr][e];
+            const float m0 = ev ? L.MJ[lr][e] : 0.f;
+            t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m0, t00, 0, 0, 0);
+            if (two) {
+                const float j1 = L.J[32 + lr][e];
+                const float m1 = ev ? L.MJ[32 + lr][e] : 0.f;
+                t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m1, t01, 0, 0, 0);
+                t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m0, t10, 0, 0, 0);
+                t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m1, t11, 0, 0, 0);
+            }
+        }
         float a[kWaveMaxRows];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int r0 = 8 * (i / 4) + (i % 4);  // this half's row; the other half holds r0 + 4
+            const float g0 = __shfl_xor(lh ? t00[i] : t01[i], 32);
+            a[r0] = lh ? g0 : t00[i];
+            a[r0 + 4] = lh ? t01[i] : g0;
+            const float g1 = __shfl_xor(lh ? t10[i] : t11[i], 32);
+            a[32 + r0] = lh ? g1 : t10[i];
+            a[32 + r0 + 4] = lh ? t11[i] : g1;
+        }
         float dg = 1.f;
 #pragma unroll
         for (int r = 0; r < kWaveMaxRows; ++r) {
-            a[r] = 0.f;
-            if (r < R) {
-                const F4* jr = reinterpret_cast<const F4*>(L.J[r]);
-                float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-                for (int e4 = 0; e4 < kJS / 4; ++e4) {
-                    const F4 j = jr[e4];
-                    s0 += j.x * mjc[4 * e4] + j.z * mjc[4 * e4 + 2];
-                    s1 += j.y * mjc[4 * e4 + 1] + j.w * mjc[4 * e4 + 3];
-                }
-                a[r] = s0 + s1;
-                if (lane == r) {
-                    a[r] *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
-                    dg = a[r];
-                }
+            a[r] = (r < R && lane < R) ? a[r] : 0.f;
+            if (lane == r && r < R) {
+                a[r] *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
+                dg = a[r];
             }
         }
         MW_PROF_T(t4);
@@ -587,12 +606,17 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const int r = rb + k;
+                    // dependent chain per row: lane read of w_r, one fma, the
+                    // clamp, one fma into w (x + b/A_rr and w - A[.][r] x_r
+                    // are formed off the chain)
                     const F4 c = L.rc[r];
-                    float v = x[r] + (c.x - read_lane(w, r)) * c.y;
+                    const float xb = fmaf(c.x, c.y, x[r]);
+                    const float wpre = fmaf(-a[r], x[r], w);
+                    float v = fmaf(-read_lane(w, r), c.y, xb);
                     float sc = 1.f;
                     if (r % 3 != 0) sc = (r < ncr) ? mu * x[r - r % 3] : 1.f;
                     v = clamp_ordered(v, c.z * sc, c.w * sc);
-                    w += a[r] * (v - x[r]);
+                    w = fmaf(a[r], v, wpre);
                     x[r] = v;
                 }
             }
