@@ -641,9 +641,31 @@ def cpu_baseline_and_parity(args, env, actions, np, torch):
     t0 = time.perf_counter()
     ref.rollout(acts[:T])
     cpu_s = time.perf_counter() - t0
-    cpu = {"value": round(Wc * T / cpu_s, 1), "unit": "env·steps/s", "cores": 1, "kind": "port",
-           "sample": f"{Wc} worlds x {T} env steps of {args.task}, fp64 C oracle, 1 thread "
-                     f"({cpu_s:.1f} s); the reference's ign-gazebo+DART path is not buildable here"}
+    single = Wc * T / cpu_s
+    # the same sample on every host core this process may use (at most 16,
+    # the box's CPU share): one oracle VecEnv of Wc worlds per thread, the C
+    # rollout releases the GIL (ctypes), worlds are independent
+    from concurrent.futures import ThreadPoolExecutor
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    envs = [pyoracle.VecEnv(cm, pyoracle.make_task(kind, seed=args.seed + k), Wc) for k in range(threads)]
+    for e in envs:
+        e.reset()
+    a_T = np.ascontiguousarray(acts[:T])
+    with ThreadPoolExecutor(threads) as pool:
+        t0 = time.perf_counter()
+        list(pool.map(lambda e: e.rollout(a_T), envs))
+        mt_s = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    cpu = {"value": round(threads * Wc * T / mt_s, 1), "unit": "env·steps/s", "cores": threads, "kind": "port",
+           "sample": f"{threads} threads x {Wc} worlds x {T} env steps of {args.task}, fp64 C oracle "
+                     f"({mt_s:.1f} s wall; {cpu_model}); the reference's ign-gazebo+DART path is not buildable here",
+           "single_thread_value": round(single, 1),
+           "single_thread_sample": f"{Wc} worlds x {T} env steps, 1 thread ({cpu_s:.1f} s)"}
 
     # teacher-forced one-step parity on 256 worlds x 100 steps
     from mwstep.vecenv import VecEnv

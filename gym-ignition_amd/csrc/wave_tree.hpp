@@ -3,19 +3,23 @@
 // BASELINE config 5).  Same physics as float_tree.hpp / oracle.c
 // or_float_step (DART 6 World::step restated [EXT]); different mapping:
 //
-//   uniform phases   the ABA over the tree (runtime topology, bodies in
-//                    depth-first order) is executed by the whole wave with
-//                    identical values (no broadcast needed: every lane holds
-//                    the result); per-body records live in LDS, written by
-//                    lane 0 and read as LDS broadcasts.
+//   ABA              level-parallel (runtime topology, bodies in depth-first
+//                    order): lane = body, the passes walk the tree by depth
+//                    level; child -> parent sums go through per-parent LDS
+//                    accumulators one sibling rank at a time (deterministic).
+//                    Per-body records (R, p, U, psi, depth, world pose) are
+//                    left in LDS for the later phases (uniform broadcasts).
 //   lane phases      joint commands / PID (lane = dof), contact detection
-//                    (lane = slot), row responses M^-1 J^T (lane = row; each
-//                    walks its body's path to the base, then the outward pass
-//                    with a per-lane stack indexed by body depth), Delassus
-//                    columns (lane = column), the nu update (lane = component).
-//   PGS              rows in order (the oracle's order); row r's
-//                    sum_c A_rc x_c has lane c multiply its own x_c and a DPP
-//                    wave reduction add the 64 products.
+//                    (lane = slot), row responses M^-1 J^T (lane = row, contact
+//                    and joint rows in one pass; each walks its body's
+//                    ancestor mask to the base, then the outward pass with a
+//                    per-lane stack indexed by body depth), the nu update
+//                    (lane = component).
+//   Delassus         J (M^-1 J^T)^T on the matrix cores (32x32x2 f32 MFMA
+//                    tiles), rearranged so lane c holds column c in registers.
+//   PGS              rows in order (the oracle's order); impulses uniform in
+//                    registers, the residual sum_c A_rc x_c distributed over
+//                    the lanes and updated by one column per row.
 //
 // Capacities (checked on the host): bodies <= MAXN, tree depth <= kWaveMaxDepth,
 // contact slots <= 32, active rows <= 64 per step (beyond: the step's extra
