@@ -573,8 +573,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         // the start of every sweep and updated by column r (= a[r], symmetry)
         // after row r moves, so a row costs one lane read of w, one uniform
         // LDS broadcast of its constants {b, 1/A_rr, lo, hi} (off the chain)
-        // and a handful of dependent VALU ops.  Friction rows store the
-        // bounds (-1, 1), scaled by mu x_normal of the same contact.
+        // and a handful of dependent VALU ops.  A contact's normal row sets
+        // the bound mu x_normal its two friction rows clamp to.
         const int Rpad = (R + 7) & ~7;
         if (lane < Rpad) {
             F4 c = {0.f, 0.f, 0.f, 0.f};
@@ -604,6 +604,7 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #pragma unroll
                 for (int k = 0; k < 8; ++k) w += a[rb + k] * x[rb + k];
             }
+            float h = 0.f;  // mu x_normal of the current contact (set by its normal row)
 #pragma unroll
             for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
                 if (rb >= Rpad) break;
@@ -617,9 +618,13 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                     const float xb = fmaf(c.x, c.y, x[r]);
                     const float wpre = fmaf(-a[r], x[r], w);
                     float v = fmaf(-read_lane(w, r), c.y, xb);
-                    float sc = 1.f;
-                    if (r % 3 != 0) sc = (r < ncr) ? mu * x[r - r % 3] : 1.f;
-                    v = clamp_ordered(v, c.z * sc, c.w * sc);
+                    if (r % 3 == 0) {
+                        v = clamp_ordered(v, c.z, c.w);  // normal row (0, inf) or joint row
+                        h = mu * v;                      // friction bound of this contact
+                    } else {  // friction row |x| <= mu x_normal, or joint row
+                        const bool fr = r < ncr;
+                        v = clamp_ordered(v, fr ? -h : c.z, fr ? h : c.w);
+                    }
                     w = fmaf(a[r], v, wpre);
                     x[r] = v;
                 }
