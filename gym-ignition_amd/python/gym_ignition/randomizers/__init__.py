@@ -1,1 +1,1 @@
-from . import abc, gazebo_env_randomizer, physics  # noqa: F401
+from . import abc, gazebo_env_randomizer, model, physics  # noqa: F401

@@ -9,5 +9,8 @@ class DART(PhysicsRandomizer):
     def __init__(self):
         super().__init__(randomize_after_rollouts_num=0)
 
+    def randomize_physics(self, task, **kwargs) -> None:
+        return None
+
     def get_engine(self):
         return scenario_gazebo.PhysicsEngine_dart

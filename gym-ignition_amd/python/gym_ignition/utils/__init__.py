@@ -1,1 +1,1 @@
-from . import logger, scenario, typing  # noqa: F401
+from . import logger, misc, scenario, typing  # noqa: F401

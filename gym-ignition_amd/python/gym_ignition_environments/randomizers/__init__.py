@@ -1,1 +1,1 @@
-from . import cartpole_no_rand, pendulum_no_rand  # noqa: F401
+from . import cartpole, cartpole_no_rand, pendulum_no_rand  # noqa: F401

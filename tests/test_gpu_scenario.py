@@ -196,6 +196,47 @@ def test_reproducibility(require_gpu):
     e2.close()
 
 
+def test_cartpole_env_randomizer(require_gpu):
+    """randomizers/cartpole.py: every reset inserts a cartpole whose link
+    masses are the nominal ones + max(U(-0.2, 0.2), 0) drawn from the task
+    RNG; the same seed reproduces the same masses and rollouts."""
+    import gym_ignition_environments  # noqa: F401
+    from gym_ignition_environments import randomizers
+    from mwstep import gym_module
+    gym = gym_module()
+    make = lambda: randomizers.cartpole.CartpoleEnvRandomizer(
+        env=lambda **kw: gym.make("CartPoleDiscreteBalancing-Gazebo-v0", **kw))
+
+    def masses(env):
+        task = env.env.task if hasattr(env.env, "task") else env.unwrapped.task
+        model = task.world.get_model(task.model_name)
+        n = model.dofs()
+        return model._sim.export_model()[:34 * n].reshape(n, 34)[:, 17].copy()
+
+    e1, e2 = make(), make()
+    e1.seed(42)
+    e2.seed(42)
+    nominal = np.array([1.0, 0.1])  # cart, pole (models/cartpole.urdf)
+    seen = []
+    for _ in range(4):
+        o1, o2 = e1.reset(), e2.reset()
+        m1, m2 = masses(e1), masses(e2)
+        assert np.array_equal(m1, m2)
+        assert np.all(m1 >= nominal - 1e-12) and np.all(m1 <= nominal + 0.2 + 1e-12)
+        seen.append(m1)
+        assert o1 == pytest.approx(o2)
+        for _ in range(30):
+            a = e1.action_space.sample()
+            assert a == e2.action_space.sample()
+            s1, s2 = e1.step(a), e2.step(a)
+            assert s1[0] == pytest.approx(s2[0]) and s1[2] == s2[2]
+            if s1[2]:
+                break
+    assert len({tuple(m) for m in seen}) > 1
+    e1.close()
+    e2.close()
+
+
 def test_joint_limit_matches_oracle(require_gpu, oracle):
     from mwstep import get_model_file
     from scenario import core
