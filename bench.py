@@ -57,6 +57,7 @@ def parse():
     p.add_argument("--no-rand-leg", action="store_true", help="skip the randomised-physics leg")
     p.add_argument("--no-pendulum", action="store_true", help="skip the config-3 Pendulum leg")
     p.add_argument("--no-contact-leg", action="store_true", help="skip the floating-body contact leg")
+    p.add_argument("--no-runtime-leg", action="store_true", help="skip the config-1 GazeboRuntime leg")
     p.add_argument("--groups", type=int, default=1,
                    help="world groups per GPU, each on its own stream / hardware queue")
     return p.parse_args()
@@ -170,6 +171,9 @@ def main():
         contacts = contact_leg(args, dev, torch)
         quadruped = quadruped_leg(args, dev, torch)
         humanoid = humanoid_leg(args, dev, torch)
+    runtime = None
+    if rank == 0 and world_size == 1 and not args.no_runtime_leg:
+        runtime = runtime_leg(args, dev)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
@@ -230,6 +234,7 @@ def main():
             "contacts_floating": contacts,
             "quadruped_floating": quadruped,
             "humanoid_c5": humanoid,
+            "runtime_c1": runtime,
         }
         print(json.dumps(out))
     for e in envs:
@@ -508,6 +513,39 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, rng,
            "constraint_overflow": int(sim.constraint_overflow())}
     sim.close()
     return out
+
+
+def runtime_leg(args, dev, steps=3000):
+    """BASELINE config 1's shape on the GPU backend: ONE CartPoleDiscreteBalancing
+    world through the unchanged-surface gym stack (gym.make -> GazeboRuntime ->
+    Task -> ScenarI/O mirror -> C-ABI mw_run, one kernel + one H2D / D2H copy
+    per env step), random actions, seed 42, episodes reset as they end.  This
+    is the drop-in plumbing path (per-env Python and getters), not the
+    throughput path."""
+    import gym_ignition_environments  # noqa: F401
+    from gym_ignition_environments import randomizers
+    from mwstep import gym_module
+    gym = gym_module()
+    os.environ.setdefault("MWSTEP_DEVICE", str(dev.index))
+    env = randomizers.cartpole_no_rand.CartpoleEnvNoRandomizations(
+        env=lambda **kw: gym.make("CartPoleDiscreteBalancing-Gazebo-v0", **kw))
+    env.seed(args.seed)
+    env.reset()
+    for _ in range(200):
+        if env.step(env.action_space.sample())[2]:
+            env.reset()
+    resets = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if env.step(env.action_space.sample())[2]:
+            env.reset()
+            resets += 1
+    elapsed = time.perf_counter() - t0
+    env.close()
+    return {"workload": "1 CartPoleDiscreteBalancing world through gym.make / GazeboRuntime / ScenarI/O "
+                        "(BASELINE.json configs[0] shape, GPU backend), random actions, seed 42",
+            "value": round(steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "episode_resets": resets}
 
 
 def contact_leg(args, dev, torch):
