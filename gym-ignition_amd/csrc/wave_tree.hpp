@@ -41,23 +41,21 @@ struct alignas(16) F4 {
     float x, y, z, w;
 };
 
-// per-body record (uniform), 75 words
+// per-body record, 41 words (odd: lane-strided gathers of parent records are
+// conflict-free); the articulated inertias live in the accumulators below
 struct WaveBody {
     M3 R;        // joint transform (parent -> body)
     f3 p;
     SV U;        // AI S
     float psi;   // (S^T AI S)^-1
     float tt;    // total joint force (ABA u)
-    SV eta;      // velocity-product acceleration
-    SV B;        // bias force, then articulated bias accumulated from the children
-    SI IA;       // articulated inertia accumulated from the children
     SV V;        // body velocity, then acceleration
     M3 Rw;       // world pose (contact detection)
     f3 pw;
     int32_t depth;
-    float pad_[3];
+    float pad_[2];
 };
-static_assert(sizeof(WaveBody) == 75 * 4, "WaveBody layout");
+static_assert(sizeof(WaveBody) == 41 * 4, "WaveBody layout");
 
 // child -> parent accumulator of the inward pass (28 words, float4-aligned)
 struct alignas(16) WaveAcc {
@@ -105,23 +103,6 @@ __device__ unsigned long long g_wave_prof[kWaveProfPhases];
 #define MW_PROF_T(var)
 #define MW_PROF_ACC(k, a, b)
 #endif
-
-// sum over the 64 lanes (DPP: quad perms, half-row / row mirrors, row
-// broadcasts 15 and 31), the total read from lane 63; a fixed order, so the
-// result is deterministic
-__device__ __forceinline__ float wave_sum(float x) {
-#ifdef MW_HOST_TEST
-    return x;
-#else
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x142, 0xA, 0xF, false));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x143, 0xC, 0xF, false));
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
-#endif
-}
 
 // min(max(v, lo), hi) for lo <= hi (every PGS bound pair is ordered): one
 // v_med3_f32 on the device
