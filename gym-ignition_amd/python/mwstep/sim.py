@@ -23,7 +23,8 @@ class Simulator:
                  steps_per_run: int = 1, rtf: float = 1.0, device: int = 0,
                  pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "",
                  pgs_iters: int = 20, gravity: Optional[Sequence[float]] = None,
-                 stream: Optional[int] = None, joint_params: Optional[dict] = None):
+                 stream: Optional[int] = None, joint_params: Optional[dict] = None,
+                 cache_reads: bool = False):
         L = N.lib()
         cfg = N.MwConfig(step_size, rtf, steps_per_run, n_worlds, device, pgs_iters)
         h = ctypes.c_void_p()
@@ -32,6 +33,12 @@ class Simulator:
         self.n_worlds = n_worlds
         self.step_size = step_size
         self.steps_per_run = steps_per_run
+        # cache_reads: joint positions / velocities / accelerations are read
+        # back once per run and sliced for every later getter call (the
+        # ScenarI/O mirror asks for them several times per env step); any
+        # call that can change state drops the cache
+        self._cache_reads = cache_reads
+        self._cache: dict = {}
         try:
             p = np.ascontiguousarray(pose, dtype=np.float64)
             N.check(L.mw_load_model(h, model.encode(), N.dptr(p), name.encode()), "mw_load_model")
@@ -85,10 +92,12 @@ class Simulator:
             pass
 
     def run(self, paused: bool = False) -> None:
+        self._cache.clear()
         N.check(N.lib().mw_run(self.handle, 1 if paused else 0), "run")
 
     def run_device(self, runs: int = 1) -> None:
         """`runs` runs with the state kept on the device (graph-capturable)."""
+        self._cache.clear()
         N.check(N.lib().mw_run_device(self.handle, runs), "run_device")
 
     def time(self) -> float:
@@ -102,6 +111,7 @@ class Simulator:
         return g.tolist()
 
     def set_gravity(self, g: Sequence[float]) -> None:
+        self._cache.clear()
         a = np.ascontiguousarray(g, dtype=np.float64)
         N.check(N.lib().mw_set_gravity(self.handle, N.dptr(a)), "set_gravity")
 
@@ -135,9 +145,19 @@ class Simulator:
             "velocity_target": N.lib().mw_get_joint_velocity_targets,
             "position_target": N.lib().mw_get_joint_position_targets,
         }[what]
-        return self._get(fn, w0, self.n_worlds - w0 if nw is None else nw, dofs)
+        nw = self.n_worlds - w0 if nw is None else nw
+        if self._cache_reads and what in ("q", "qd", "qdd"):
+            full = self._cache.get(what)
+            if full is None:
+                full = self._cache[what] = self._get(fn, 0, self.n_worlds, None)
+            out = full[w0:w0 + nw]
+            if dofs is not None:
+                out = out[:, dofs]
+            return out.copy()
+        return self._get(fn, w0, nw, dofs)
 
     def set(self, what: str, values, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
+        self._cache.clear()
         fn = {
             "force_target": N.lib().mw_set_joint_force_targets,
             "velocity_target": N.lib().mw_set_joint_velocity_targets,
@@ -148,6 +168,7 @@ class Simulator:
         self._set(fn, w0, self.n_worlds - w0 if nw is None else nw, dofs, values)
 
     def set_control_mode(self, mode: int, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
+        self._cache.clear()
         nw = self.n_worlds - w0 if nw is None else nw
         N.check(N.lib().mw_set_joint_control_mode(self.handle, w0, nw, N.iptr(dofs),
                                                   0 if dofs is None else len(dofs), mode))
@@ -163,6 +184,7 @@ class Simulator:
         return t.value
 
     def set_joint_param(self, dof: int, which: int, value: float) -> None:
+        self._cache.clear()
         N.check(N.lib().mw_set_joint_param(self.handle, dof, which, float(value)))
 
     def joint_param(self, dof: int, which: int) -> float:
@@ -172,6 +194,7 @@ class Simulator:
 
     def set_pid(self, dof: int, gains) -> None:
         """gains = {p, i, d, cmd_min, cmd_max, cmd_offset, i_min, i_max} (all worlds)."""
+        self._cache.clear()
         g = np.ascontiguousarray(gains, dtype=np.float64)
         assert g.shape == (8,)
         N.check(N.lib().mw_set_joint_pid(self.handle, dof, N.dptr(g)))
@@ -182,6 +205,7 @@ class Simulator:
         return g
 
     def set_controller_period(self, period: float) -> None:
+        self._cache.clear()
         N.check(N.lib().mw_set_controller_period(self.handle, float(period)))
 
     def controller_period(self) -> float:
@@ -211,19 +235,23 @@ class Simulator:
         return out
 
     def reset_base_pose(self, pose, w0: int = 0, nw: Optional[int] = None) -> None:
+        self._cache.clear()
         nw = self.n_worlds - w0 if nw is None else nw
         v = np.ascontiguousarray(np.broadcast_to(np.asarray(pose, dtype=np.float64), (nw, 7)))
         N.check(N.lib().mw_reset_base_pose(self.handle, w0, nw, N.dptr(v)), "reset_base_pose")
 
     def reset_base_velocity(self, lin_ang, w0: int = 0, nw: Optional[int] = None) -> None:
+        self._cache.clear()
         nw = self.n_worlds - w0 if nw is None else nw
         v = np.ascontiguousarray(np.broadcast_to(np.asarray(lin_ang, dtype=np.float64), (nw, 6)))
         N.check(N.lib().mw_reset_base_velocity(self.handle, w0, nw, N.dptr(v)), "reset_base_velocity")
 
     def set_ground_plane(self, enabled: bool, mu: float = 1.0) -> None:
+        self._cache.clear()
         N.check(N.lib().mw_set_ground_plane(self.handle, 1 if enabled else 0, float(mu)), "set_ground_plane")
 
     def enable_contacts(self, enable: bool = True) -> None:
+        self._cache.clear()
         N.check(N.lib().mw_enable_contacts(self.handle, 1 if enable else 0))
 
     def contacts_enabled(self) -> bool:
@@ -271,10 +299,12 @@ class Simulator:
         return v.value
 
     def device_ptr(self, field: str):
+        self._cache.clear()
         p = ctypes.c_void_p()
         stride = ctypes.c_int64()
         N.check(N.lib().mw_device_ptr(self.handle, field.encode(), ctypes.byref(p), ctypes.byref(stride)))
         return p.value, stride.value
 
     def set_stream(self, stream: int) -> None:
+        self._cache.clear()
         N.check(N.lib().mw_set_stream(self.handle, ctypes.c_void_p(stream)))

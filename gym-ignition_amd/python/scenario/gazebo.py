@@ -893,7 +893,7 @@ class World:
             sim = Simulator(model_string, n_worlds=1, step_size=sim_cfg.step_size(),
                             steps_per_run=sim_cfg.steps_per_run(), rtf=sim_cfg.real_time_factor(),
                             device=_device(), pose=list(pose.position) + list(pose.orientation),
-                            name=name, gravity=self._gravity)
+                            name=name, gravity=self._gravity, cache_reads=True)
         except RuntimeError as e:
             _err(f"Failed to insert model '{name}': {e}")
             return False
