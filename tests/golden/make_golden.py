@@ -1,0 +1,105 @@
+"""Generate the golden fixtures of tests/golden/ (fp64, CPU).
+
+The reference cannot run here (ign-gazebo / DART / SWIG absent,
+no golden trajectories in the reference), so the fixtures are produced by this
+repository's fp64 oracle (oracle/, pinned by the reference's known-answer
+tests: tests/test_oracle_kat.py, test_oracle_tree_pid.py,
+test_float_tree_oracle.py) on the shipped models, with every input stored next
+to the outputs:
+
+  cartpole_discrete.npz  CartPoleDiscreteBalancing, 16 worlds x 300 env steps:
+                         Philox resets (seed 42), Bernoulli actions
+                         (numpy PCG64 seed 43), obs / reward / done per step
+  pendulum_swingup.npz   PendulumSwingUp, 16 worlds x 300 steps, torques
+                         U(-50, 50) (PCG64 seed 43)
+  humanoid_stand.npz     humanoid32 (floating base, ground contacts, PGS 50)
+                         under the JointController PID hold for 300 steps:
+                         joint positions and base position every 10 steps,
+                         final contact forces
+
+    python tests/golden/make_golden.py        (rewrites the .npz files)
+"""
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "gym-ignition_amd", "python"))
+
+W, T = 16, 300
+HUMANOID_Z = 0.535
+HUMANOID_STEPS, HUMANOID_EVERY = 300, 10
+
+
+def humanoid_gains(names):
+    stiff = lambda n: "leg" in n or "torso" in n
+    return [(500.0, 5.0) if stiff(n) else (50.0, 0.5) for n in names]
+
+
+def vec_rollout(kind, model, actions):
+    import pyoracle
+    from mwstep import get_model_file
+    cm = pyoracle.load_urdf(get_model_file(model))
+    env = pyoracle.VecEnv(cm, pyoracle.make_task(kind, seed=42), W)
+    obs0 = env.reset()
+    obs, rew, done = [], [], []
+    for t in range(T):
+        o, r, d, _ = env.step(actions[t])
+        obs.append(o)
+        rew.append(r)
+        done.append(d)
+    return obs0, np.array(obs), np.array(rew), np.array(done)
+
+
+def cartpole():
+    import pyoracle
+    actions = np.random.default_rng(43).integers(0, 2, size=(T, W)).astype(np.int32)
+    obs0, obs, rew, done = vec_rollout(pyoracle.TASK_CARTPOLE_DISCRETE, "cartpole", actions)
+    return dict(actions=actions, obs0=obs0, obs=obs, reward=rew, done=done)
+
+
+def pendulum():
+    import pyoracle
+    actions = np.random.default_rng(43).uniform(-50.0, 50.0, size=(T, W))
+    obs0, obs, rew, done = vec_rollout(pyoracle.TASK_PENDULUM_SWINGUP, "pendulum", actions)
+    return dict(actions=actions, obs0=obs0, obs=obs, reward=rew, done=done)
+
+
+def humanoid():
+    import pyoracle
+    from mwstep import get_model_file
+    cm = pyoracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, HUMANOID_Z))
+    names = list(cm.joint_names)
+    ow = pyoracle.FloatWorld(cm, pgs_iters=50)
+    n = cm.n
+    gains = humanoid_gains(names)
+    og = [pyoracle.pid_gains(p, 0.0, d, cmdmax=80.0, cmdmin=-80.0) for p, d in gains]
+    st = [pyoracle.OrPidState() for _ in range(n)]
+    mode = np.full(n, pyoracle.FORCE, np.int32)
+    qs, ps = [], []
+    for k in range(HUMANOID_STEPS):
+        tau = np.array([pyoracle.pid_update(og[d], st[d], ow.q[d], 1e-3) for d in range(n)])
+        ow.step(mode, tau)
+        if k % HUMANOID_EVERY == HUMANOID_EVERY - 1:
+            qs.append(ow.q.copy())
+            ps.append(ow.p.copy())
+    fz = np.array([c[1][2] for c in ow.contacts])
+    return dict(q=np.array(qs), p=np.array(ps), contact_fz=fz, joint_names=np.array(names))
+
+
+FIXTURES = {"cartpole_discrete": cartpole, "pendulum_swingup": pendulum, "humanoid_stand": humanoid}
+
+
+def main():
+    for name, fn in FIXTURES.items():
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **fn())
+        print(f"wrote {path} ({os.path.getsize(path)} bytes)")
+
+
+if __name__ == "__main__":
+    main()
