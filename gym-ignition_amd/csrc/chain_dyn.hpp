@@ -653,6 +653,10 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
             for (int i = 0; i < N; ++i) { x[i][0] = x[i][1] = x[i][2] = 0.f; dq[i] = 0.f; }
             for (int it = 0; it < pgs_iters; ++it) {
                 W.fence();
+                // a sweep that moves no impulse is a fixed point: every later
+                // sweep would repeat it exactly, so stopping there returns the
+                // same bits as running all pgs_iters sweeps
+                bool moved = false;
 #pragma unroll
                 for (int d = 0; d < N; ++d) {
                     if (!((need >> d) & 1u)) continue;
@@ -674,12 +678,14 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
                             }
                             const float xn = fminf(fmaxf(x[d][t] + (bb[d][t] - dq[d]) * inv_diag, lo), hi);
                             const float delta = xn - x[d][t];
+                            moved |= delta != 0.f;
                             x[d][t] = xn;
 #pragma unroll
                             for (int k = 0; k < N; ++k) dq[k] += delta * W.mv(k, d);
                         }
                     }
                 }
+                if (!moved) break;
             }
             const float inv_dt = rcp(dt);
 #pragma unroll
