@@ -80,7 +80,13 @@ def main():
     torch.cuda.set_device(local_rank % ndev)
     dev = torch.device("cuda", local_rank % ndev)
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl") is the product path; MWSTEP_DIST_BACKEND=gloo rehearses
+        # several ranks on one GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("MWSTEP_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from mwstep.vecenv import VecEnv
 
@@ -320,6 +326,14 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
         st.synchronize()
         groups.append((env, st, acts, buf, graph, tail))
 
+    if gather:
+        # the first RCCL collective sets up its channels (milliseconds): do it
+        # once here so the timed region holds only the steady-state all-gather
+        st0 = groups[0][1]
+        with torch.cuda.stream(st0):
+            obs = torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs
+            gather_obs(obs)
+        torch.cuda.synchronize(dev)
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -26,6 +26,9 @@ def gather_obs(obs, group=None):
     import torch
     import torch.distributed as dist
     ws = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo" and obs.is_cuda:
+        # gloo (CPU rehearsal of a multi-rank run) gathers host copies
+        return gather_obs(obs.cpu(), group).to(obs.device)
     out = torch.empty((ws * obs.shape[0],) + tuple(obs.shape[1:]), dtype=obs.dtype, device=obs.device)
     dist.all_gather_into_tensor(out, obs.contiguous(), group=group)
     return out
