@@ -114,6 +114,7 @@ struct mw_sim {
     std::vector<int32_t> slot_body;  // body of every contact slot (-1 = base)
     // large trees (or MWSTEP_WAVE_TREE=1): one world per wavefront (wave_tree.hpp)
     bool wave = false;
+    bool wave_depth_ok = false;   // the tree fits the wave kernel's depth stack
     mw::PidF* d_pid = nullptr;    // PID gains of every dof (device)
     mw::PidF* h_pid = nullptr;    // pinned staging copy
     bool pid_dirty = true;        // gains changed since the last upload
@@ -319,6 +320,9 @@ void build_float(mw_sim* s) {
         F.body_path[i] = (uint64_t{1} << i) | (pa >= 0 ? F.body_path[pa] : uint64_t{0});
     }
     F.fanout = *std::max_element(children.begin(), children.end());
+    F.dual = 0;
+    for (int i = 0; i < n; ++i)
+        if (M.bodies[i].damping != 0.0) F.dual = 1;
 }
 
 int upload_params(mw_sim* s) {
@@ -531,11 +535,10 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
         s->topo = mw::kernel_topology(parents.data(), s->model.dofs());
         size_t n_shapes = s->model.base_shapes.size();
+        bool damped = false;  // joint damping: the wave kernel (its dual recursion) only
         for (const auto& b : s->model.bodies) {
             n_shapes += b.shapes.size();
-            if (b.damping != 0.0)
-                return fail(MW_EPARSE, "joint damping on floating-base models is not compiled into this build "
-                                       "(joint '" + b.joint_name + "')");
+            damped = damped || b.damping != 0.0;
         }
         if (n_shapes > static_cast<size_t>(mw::kMaxFloatShapes))
             return fail(MW_EPARSE, "a floating-base model may have at most " +
@@ -557,10 +560,10 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         // forces the wave / lane kernel.
         constexpr int kWaveWorldsMax = 4096;
         if (force_wave && *force_wave)
-            s->wave = !compiled || *force_wave != '0';
+            s->wave = !compiled || *force_wave != '0' || damped;
         else
-            s->wave = !compiled || s->W <= kWaveWorldsMax;
-        if (s->wave) {
+            s->wave = !compiled || s->W <= kWaveWorldsMax || damped;
+        {
             std::vector<int> depth(s->n, 0);
             int max_depth = 0;
             for (int i = 0; i < s->n; ++i) {
@@ -568,7 +571,8 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
                 depth[i] = (pa >= 0) ? depth[pa] + 1 : 0;
                 max_depth = std::max(max_depth, depth[i] + 1);
             }
-            if (max_depth > mw::kWaveMaxDepthHost)
+            s->wave_depth_ok = max_depth <= mw::kWaveMaxDepthHost;
+            if (s->wave && !s->wave_depth_ok)
                 return fail(MW_EPARSE, "the kinematic tree of this floating-base model is deeper than " +
                                            std::to_string(mw::kWaveMaxDepthHost) + " joints");
         }
@@ -1019,7 +1023,25 @@ int mw_set_joint_param(mw_sim* s, int32_t dof, int32_t which, double value) {
     mw::ChainBody& b = s->model.bodies[dof];
     switch (which) {
     case MW_PARAM_COULOMB_FRICTION: b.friction = value; break;
-    case MW_PARAM_VISCOUS_FRICTION: b.damping = value; break;
+    case MW_PARAM_VISCOUS_FRICTION:
+        // a damped floating tree runs on the wave kernel (dual recursion);
+        // before the first step a lane-kernel model can still switch
+        if (s->float_tree && value != 0.0 && !s->wave) {
+            if (!s->wave_depth_ok)
+                return fail(MW_EPARSE, "joint damping on this floating-base model needs the world-per-wavefront "
+                                       "kernel, whose depth limit the tree exceeds");
+            if (s->initialized && !s->d_pid) {
+                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), mw::kMaxBodies * sizeof(mw::PidF)));
+                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), mw::kMaxBodies * sizeof(mw::PidF),
+                                     hipHostMallocDefault));
+                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), sizeof(int)));
+                MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
+                s->pid_dirty = true;
+            }
+            s->wave = true;
+        }
+        b.damping = value;
+        break;
     case MW_PARAM_MAX_GENERALIZED_FORCE: b.effort = value; break;
     case MW_PARAM_POSITION_LIMIT_MIN: b.lower = value; break;
     case MW_PARAM_POSITION_LIMIT_MAX: b.upper = value; break;

@@ -57,13 +57,16 @@ struct WaveBody {
 };
 static_assert(sizeof(WaveBody) == 41 * 4, "WaveBody layout");
 
-// child -> parent accumulator of the inward pass (28 words, float4-aligned)
+// child -> parent accumulator of the inward pass (48 words, float4-aligned):
+// articulated inertia with DART's implicit joint damping, bias, and the
+// non-implicit articulated inertia (models with damping: impulses propagate
+// through it)
 struct alignas(16) WaveAcc {
     SI I;
     SV B;
-    float pad_;
+    SI In;
 };
-static_assert(sizeof(WaveAcc) == 28 * 4, "WaveAcc layout");
+static_assert(sizeof(WaveAcc) == 48 * 4, "WaveAcc layout");
 
 template <int MAXN>
 struct WaveWorld {
@@ -135,7 +138,7 @@ __device__ __forceinline__ float read_lane(float x, int l) {
 template <int MAXN>
 __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                        const M3& R0, const f3& p0, const SV& V0, WaveWorld<MAXN>& L, Chol6& L0,
-                                       float* qdd_out) {
+                                       Chol6& L0n, float dt, float* qdd_out) {
     const int lane = lane_id();
     const bool own = lane < N;
     const int i = own ? lane : 0;
@@ -176,43 +179,67 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
             L.body[i].pw = pw;
         }
     }
-    if (own) tau = L.tau[i];
+    float qdi = 0.f;
+    if (own) {
+        tau = L.tau[i];
+        qdi = L.qd[i];
+    }
+    // DART's implicit joint damping (Psi = (S^T AI S + dt d)^-1, force
+    // tau - d qd) for the free motion; with damping the impulses use the
+    // non-implicit articulated inertias, a second recursion (F->dual)
+    const bool dual = F->dual != 0;
     // inward, deepest level first
-    SV U;
-    float psi = 0.f, tt = 0.f;
+    SV U, Un;
+    float psi = 0.f, tt = 0.f, psin = 0.f;
     for (int d = levels - 1; d >= 0; --d) {
         const bool mine = (depth == d);
-        SI c;
+        SI c, cn;
         SV cb;
         if (mine) {
-            const WaveAcc in = L.acc[i];
             SI AI = rigid(b, b.mass);
-            AI += in.I;
-            const SV Bt = B + in.B;
+            AI += L.acc[i].I;
+            const SV Bt = B + L.acc[i].B;
             U = ais(AI, b);
-            psi = rcp(proj(b, U));
+            psi = rcp(proj(b, U) + dt * b.damping);
             const SV AIeta = mul(AI, eta);
-            tt = tau - proj(b, AIeta + Bt);
+            tt = tau - b.damping * qdi - proj(b, AIeta + Bt);
             c = to_parent(R, p, downdate(AI, U, psi));
             cb = dad_inv(R, p, Bt + AIeta + (psi * tt) * U);
+            if (dual) {
+                SI AIn = rigid(b, b.mass);
+                AIn += L.acc[i].In;
+                Un = ais(AIn, b);
+                psin = rcp(proj(b, Un));
+                cn = to_parent(R, p, downdate(AIn, Un, psin));
+            }
         }
         for (int k = 0; k < fanout; ++k) {
             if (mine && srank == k) {
-                WaveAcc acc = L.acc[slot];
-                acc.I += c;
+                WaveAcc& acc = L.acc[slot];
+                SI I = acc.I;
+                I += c;
+                acc.I = I;
                 acc.B = acc.B + cb;
-                L.acc[slot] = acc;
+                if (dual) {
+                    SI In = acc.In;
+                    In += cn;
+                    acc.In = In;
+                }
             }
         }
     }
-    const WaveAcc base = L.acc[MAXN];
     SI IA0 = rigid_base(*F);
-    IA0 += base.I;
+    IA0 += L.acc[MAXN].I;
     const SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
                              Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
-                  base.B;
+                  L.acc[MAXN].B;
     L0.factor(IA0);
     const SV a0 = L0.solve(-1.f * B0);
+    if (dual) {
+        SI IA0n = rigid_base(*F);
+        IA0n += L.acc[MAXN].In;
+        L0n.factor(IA0n);
+    }
     // outward: accelerations (the V record now carries a)
     for (int d = 0; d < levels; ++d) {
         if (depth == d) {
@@ -226,8 +253,8 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         WaveBody& s = L.body[i];
         s.R = R;
         s.p = p;
-        s.U = U;
-        s.psi = psi;
+        s.U = dual ? Un : U;        // the responses are impulse dynamics
+        s.psi = dual ? psin : psi;
         s.tt = tt;
         s.depth = depth;
     }
@@ -311,8 +338,9 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
     const int NV = 6 + N;
     MW_PROF_T(t0);
     const M3 R0 = quat_to_R(base.qw, base.qx, base.qy, base.qz);
-    Chol6 L0;
-    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, qdd_out);
+    Chol6 L0, L0n;
+    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, L0n, dt, qdd_out);
+    const Chol6& Lr = F->dual ? L0n : L0;  // impulses: the non-implicit base inertia
     MW_PROF_T(t1);
     MW_PROF_ACC(1, t0, t1);
     // integrateVelocities (lane e: nu component e)
@@ -487,7 +515,7 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                 } else {
                     j = (src - kJointRow) / 3;
                 }
-                const float jv = wave_response<MAXN>(P, F, N, L, L0, k, j, f, L.J[r], L.MJ[r]);
+                const float jv = wave_response<MAXN>(P, F, N, L, Lr, k, j, f, L.J[r], L.MJ[r]);
                 if (contact) {
                     const float bounce =
                         (d == 0) ? fminf(kContactErp * L.s_depth[slot] * rcp(dt), kContactMaxErv) : 0.f;

@@ -44,10 +44,11 @@ def _quat_to_R(q):
 TREE_PARENTS = [-1, 0, 1, 1, 3, 3, 0, 6, -1, 8, 8, 8, 11, 2, -1, 14]
 
 
-def tree_urdf(parents=TREE_PARENTS, seed=5):
+def tree_urdf(parents=TREE_PARENTS, seed=5, damping=0.0):
     """A floating box base with a random branched tree: revolute / prismatic
     joints about random unit axes, random origins and masses, a sphere on
-    every leaf."""
+    every leaf; `damping` > 0 adds viscous joint damping of that size times a
+    random factor in [0.5, 1.5] to every joint."""
     rng = np.random.default_rng(seed)
     parts = ['<link name="base"><inertial><mass value="4.0"/>'
              '<inertia ixx="0.05" iyy="0.06" izz="0.07" ixy="0.002" ixz="0" iyz="0"/></inertial>'
@@ -64,10 +65,11 @@ def tree_urdf(parents=TREE_PARENTS, seed=5):
         tip = ('<collision><origin xyz="0 0 -0.1"/><geometry><sphere radius="0.03"/></geometry></collision>'
                if i in leaves else "")
         m = rng.uniform(0.2, 1.0)
+        dyn = f'<dynamics damping="{damping * rng.uniform(0.5, 1.5):.4f}"/>' if damping > 0 else ""
         parent = "base" if pa < 0 else f"l{pa}"
         parts.append(f'<joint name="j{i}" type="{"prismatic" if prismatic else "revolute"}">'
                      f'<parent link="{parent}"/><child link="l{i}"/><origin xyz="{xyz}" rpy="{rpy}"/>'
-                     f'<axis xyz="{axis[0]:.4f} {axis[1]:.4f} {axis[2]:.4f}"/>{lim}</joint>'
+                     f'<axis xyz="{axis[0]:.4f} {axis[1]:.4f} {axis[2]:.4f}"/>{lim}{dyn}</joint>'
                      f'<link name="l{i}"><inertial><origin xyz="0 0.01 -0.05"/><mass value="{m:.3f}"/>'
                      f'<inertia ixx="{0.004 * m:.5f}" iyy="{0.005 * m:.5f}" izz="{0.002 * m:.5f}" ixy="0.0001" '
                      f'ixz="0" iyz="0"/></inertial>{tip}</link>')
@@ -80,6 +82,8 @@ def _model(name):
         return get_model_file(name)
     if name == "tree16":
         return tree_urdf()
+    if name == "tree16d":  # joint damping: DART's implicit damping + the dual (impulse) recursion
+        return tree_urdf(damping=2.0)
     return chain_urdf(int(name[-1]))
 
 
@@ -107,7 +111,7 @@ def _random_states(cm, W, rng):
 
 @pytest.mark.parametrize("name, kernel", [("quadruped", "lane"), ("chain1", "lane"), ("chain2", "lane"),
                                           ("chain3", "lane"), ("quadruped", "wave"), ("chain2", "wave"),
-                                          ("humanoid32", "wave"), ("tree16", "wave")])
+                                          ("humanoid32", "wave"), ("tree16", "wave"), ("tree16d", "wave")])
 def test_one_step_parity_with_contacts(require_gpu, oracle, monkeypatch, name, kernel):
     from mwstep import native as N
     from mwstep.sim import Simulator

@@ -137,10 +137,6 @@ def test_fixed_joint_lumping(N, oracle):
         f"<joint name='j{i}' type='revolute'><parent link='l{i}'/><child link='l{i + 1}'/></joint>"
         for i in range(13)) + "</robot>",
      "deeper than 12"),
-    ("<robot name='x'><link name='a'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<joint name='j' type='revolute'><parent link='a'/><child link='b'/><dynamics damping='0.1'/></joint></robot>",
-     "joint damping on floating-base models"),
     ("<robot name='x'><link name='a'/></robot>", "has no mass"),
     ("<robot name='x'><link name='world'/>", "XML"),
     ("<sdf><model name='m'/></sdf>", "URDF"),
