@@ -264,9 +264,10 @@ struct SV7 {  // padded spatial vector (LDS record)
 // Per-body storage of one substep ("stage").  RegStage keeps it in VGPRs
 // (small models: every index folds after unrolling); LdsStage keeps one
 // padded record per (body, lane) in LDS, record stride = 64 lanes, so a
-// wave's accesses to one field hit 64 distinct banks.  The 7..9-dof kernels
-// use LdsStage: in VGPRs their per-body state exceeds the 512-register file
-// and spills to scratch (global memory).
+// wave's accesses to one field hit 64 distinct banks.  The generic 7..9-dof
+// kernels use LdsStage: in VGPRs their per-body state exceeds the
+// 512-register file and spills to scratch (global memory); the constant-folded
+// ones fit (kernels.hip: lds_staged).
 template <int N, bool DUAL>
 struct RegStage {
     BodyState bs_[N];

@@ -42,24 +42,33 @@ __device__ __forceinline__ const ChainF* model_params(const ChainF* P) {
 }
 
 // ------------------------------------------------------- staging --------
-// Models of >= kLdsMinDofs dofs keep their per-body substep state in LDS
-// (chain_dyn.hpp: LdsStage); their kernels run 64-thread workgroups.
+// Generic models of >= kLdsMinDofs dofs keep their per-body substep state in
+// LDS (chain_dyn.hpp: LdsStage): in registers it spills to scratch.  The
+// constant-folded (baked) models need far fewer live values and keep it in
+// VGPRs + AGPRs without scratch (the baked Panda: 256 + 136 registers);
+// measured on the config-4 Panda env (scripts/ab_panda.py, graph replay):
+// LDS 15.9 -> registers 9.3 us per step at 1024 worlds, 15.1 -> 9.0 at 128.
+// Both kinds run 64-thread workgroups.
 #ifndef MW_LDS_MIN_DOFS
 #define MW_LDS_MIN_DOFS 7
 #endif
 constexpr int kLdsMinDofs = MW_LDS_MIN_DOFS;
 
-#define MW_DECLARE_STAGE(N, DUAL, NAME)                                                        \
-    __shared__ BodyState sh_bs_[(N >= kLdsMinDofs ? N : 1) * kLdsLanes];                      \
-    __shared__ ImpulseFactor sh_nf_[((N >= kLdsMinDofs && DUAL) ? N : 1) * kLdsLanes];        \
-    __shared__ SV7 sh_own_[(N >= kLdsMinDofs ? N : 1) * kLdsLanes];                           \
-    __shared__ float sh_mv_[(N >= kLdsMinDofs ? N * N : 1) * kLdsLanes];                      \
-    using StageT = std::conditional_t<(N >= kLdsMinDofs), LdsStage<N, DUAL>, RegStage<N, DUAL>>; \
-    StageT NAME = make_stage<N, DUAL>(sh_bs_, sh_nf_, sh_own_, sh_mv_)
+template <int N, int BAKED>
+constexpr bool lds_staged() { return N >= kLdsMinDofs && BAKED == 0; }
 
-template <int N, bool DUAL>
+#define MW_DECLARE_STAGE(N, DUAL, BAKED, NAME)                                                       \
+    constexpr bool kLds_##NAME = lds_staged<N, BAKED>();                                             \
+    __shared__ BodyState sh_bs_[(kLds_##NAME ? N : 1) * kLdsLanes];                                  \
+    __shared__ ImpulseFactor sh_nf_[((kLds_##NAME && DUAL) ? N : 1) * kLdsLanes];                    \
+    __shared__ SV7 sh_own_[(kLds_##NAME ? N : 1) * kLdsLanes];                                       \
+    __shared__ float sh_mv_[(kLds_##NAME ? N * N : 1) * kLdsLanes];                                  \
+    using StageT = std::conditional_t<kLds_##NAME, LdsStage<N, DUAL>, RegStage<N, DUAL>>;           \
+    StageT NAME = make_stage<N, DUAL, kLds_##NAME>(sh_bs_, sh_nf_, sh_own_, sh_mv_)
+
+template <int N, bool DUAL, bool LDS>
 __device__ __forceinline__ auto make_stage(BodyState* b, ImpulseFactor* f, SV7* o, float* m) {
-    if constexpr (N >= kLdsMinDofs) {
+    if constexpr (LDS) {
         return LdsStage<N, DUAL>{b + threadIdx.x, f + threadIdx.x, o + threadIdx.x, m + threadIdx.x};
     } else {
         (void)b; (void)f; (void)o; (void)m;
@@ -339,7 +348,7 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
             vc[d] = S.vtgt[d * W + w];
             any_pid = any_pid || act[d] >= kActPidPos;
         }
-        MW_DECLARE_STAGE(N, DUAL, stage);
+        MW_DECLARE_STAGE(N, DUAL, BAKED, stage);
         for (int s = 0; s < A.substeps; ++s) {
             joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, q, qd, any_pid, tau);
             substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, nominal_dyn<N>(P));
@@ -732,7 +741,7 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
 #pragma unroll
     for (int d = 0; d < N; ++d) { act[d] = kActPidPos; vc[d] = 0.f; }
     float tau[N], qdd[N];
-    MW_DECLARE_STAGE(N, DUAL, stage);
+    MW_DECLARE_STAGE(N, DUAL, BAKED, stage);
     for (int s = 0; s < substeps; ++s) {
 #pragma unroll
         for (int d = 0; d < N; ++d) {
