@@ -138,7 +138,7 @@ __device__ __forceinline__ float read_lane(float x, int l) {
 template <int MAXN>
 __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                        const M3& R0, const f3& p0, const SV& V0, WaveWorld<MAXN>& L, Chol6& L0,
-                                       Chol6& L0n, float dt, float* qdd_out) {
+                                       float dt, float* qdd_out) {
     const int lane = lane_id();
     const bool own = lane < N;
     const int i = own ? lane : 0;
@@ -238,7 +238,7 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     if (dual) {
         SI IA0n = rigid_base(*F);
         IA0n += L.acc[MAXN].In;
-        L0n.factor(IA0n);
+        L0.factor(IA0n);  // L0 leaves with the impulses' (non-implicit) base inertia
     }
     // outward: accelerations (the V record now carries a)
     for (int d = 0; d < levels; ++d) {
@@ -253,7 +253,10 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         WaveBody& s = L.body[i];
         s.R = R;
         s.p = p;
-        s.U = dual ? Un : U;        // the responses are impulse dynamics
+        // the responses are impulse dynamics; component selects (a select
+        // between two SV objects is lowered to a scratch round trip)
+        s.U = {{dual ? Un.w.x : U.w.x, dual ? Un.w.y : U.w.y, dual ? Un.w.z : U.w.z},
+               {dual ? Un.v.x : U.v.x, dual ? Un.v.y : U.v.y, dual ? Un.v.z : U.v.z}};
         s.psi = dual ? psin : psi;
         s.tt = tt;
         s.depth = depth;
@@ -338,9 +341,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
     const int NV = 6 + N;
     MW_PROF_T(t0);
     const M3 R0 = quat_to_R(base.qw, base.qx, base.qy, base.qz);
-    Chol6 L0, L0n;
-    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, L0n, dt, qdd_out);
-    const Chol6& Lr = F->dual ? L0n : L0;  // impulses: the non-implicit base inertia
+    Chol6 L0;  // on return: the factorisation the impulses use
+    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, dt, qdd_out);
     MW_PROF_T(t1);
     MW_PROF_ACC(1, t0, t1);
     // integrateVelocities (lane e: nu component e)
@@ -515,7 +517,7 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                 } else {
                     j = (src - kJointRow) / 3;
                 }
-                const float jv = wave_response<MAXN>(P, F, N, L, Lr, k, j, f, L.J[r], L.MJ[r]);
+                const float jv = wave_response<MAXN>(P, F, N, L, L0, k, j, f, L.J[r], L.MJ[r]);
                 if (contact) {
                     const float bounce =
                         (d == 0) ? fminf(kContactErp * L.s_depth[slot] * rcp(dt), kContactMaxErv) : 0.f;
