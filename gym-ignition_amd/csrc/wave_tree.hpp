@@ -142,7 +142,7 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     const int lane = lane_id();
     const bool own = lane < N;
     const int i = own ? lane : 0;
-    const BodyF& b = P->b[i];
+    const BodyF b = P->b[i];  // by value: one load up front, not one per level
     const int pa = b.parent;
     const int depth = own ? F->body_depth[i] : -1;
     const int srank = F->body_srank[i];
