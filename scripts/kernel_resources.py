@@ -11,10 +11,6 @@ cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *flags, f"-I{ROOT}/includ
        f"-I{ROOT}/gym-ignition_amd/csrc", "-c", f"{ROOT}/gym-ignition_amd/csrc/kernels.hip",
        "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
-# the Panda env translation unit (Makefile: kernels_panda.o)
-panda = ["-DMW_PANDA_ENV_TU", "-mllvm", "--amdgpu-sched-strategy=gcn-max-ilp"]
-out += subprocess.run(cmd[:-3] + panda + ["-o", "/tmp/_krp.o", "-Rpass-analysis=kernel-resource-usage"],
-                      capture_output=True, text=True).stderr
 rows, cur = [], {}
 for line in out.splitlines():
     m = re.search(r"Function Name: (\S+)", line)
