@@ -507,7 +507,6 @@ __device__ __forceinline__ void store_contact(const FreeDev& D, int W, int w, in
 // velocity resets (WorldPoseCmd / WorldVelocityCmd, Model.cpp:256-360 ->
 // Physics.cpp:1535-1590), the substeps, and the contacts of the last substep
 // (Physics.cpp:2351-2540: point, force on the body = impulse / dt, depth).
-#ifndef MW_PANDA_ENV_TU  // non-template: emitted by one translation unit only
 __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__ F, FreeDev D, int W, RunArgs A,
                                                        int want_contacts) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -531,7 +530,6 @@ __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__
         }
     }
 }
-#endif
 
 // Articulated model on a floating base (float_tree.hpp): the scenario run of
 // scenario_run_kernel (joint resets, commands, PID) plus the base state of
@@ -810,17 +808,6 @@ int block_for(int W) { return (W <= 64 * 256) ? 64 : 256; }
 // LDS-staged kernels (>= kLdsMinDofs dofs) always run one wave per workgroup
 int block_for(int W, int n) { return (n >= dev::kLdsMinDofs) ? dev::kLdsLanes : block_for(W); }
 
-}  // namespace
-
-// The config-4 Panda env kernels are compiled in a translation unit of their
-// own (this file with MW_PANDA_ENV_TU, Makefile: kernels_panda.o) under the
-// max-ILP scheduler: a lone wave per SIMD running a long dependent chain gains
-// from latency-oriented scheduling there (A/B, scripts/ab_panda.py, 1,024
-// worlds: 10.5 -> 9.2 us per step), while the CartPole and humanoid kernels
-// do not (3.11 vs 3.08 us, 91.3 vs 92.2 us).
-#ifndef MW_PANDA_ENV_TU
-namespace {
-
 template <int N, Topo TOPO>
 hipError_t scenario_n(const ChainF* P, bool cons, bool dual, int baked, const SimDev& S, const PidSet& pid, int W,
                       const RunArgs& a, hipStream_t st) {
@@ -1012,8 +999,6 @@ hipError_t launch_vecenv_reset(const ChainF* P, int n, const TaskF& T, const Sim
     return hipGetLastError();
 }
 
-#else  // MW_PANDA_ENV_TU
-
 hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, bool dual, int baked, const TaskF& T,
                                   const SimDev& S, const VecDev& V, const PidSet& pid, const float* targets,
                                   float* obs, float* reward, uint8_t* done, float* term_obs, int W,
@@ -1040,9 +1025,6 @@ hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, b
     return hipGetLastError();
 }
 
-#endif  // MW_PANDA_ENV_TU
-#ifndef MW_PANDA_ENV_TU
-
 hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, int baked, const TaskF& T,
                               const SimDev& S, const VecDev& V, const void* actions, float* obs,
                               float* reward, uint8_t* done, float* term_obs, int W, float dt,
@@ -1064,7 +1046,5 @@ hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, int 
 #undef MW_VEC_R
     return hipErrorInvalidValue;
 }
-
-#endif  // MW_PANDA_ENV_TU
 
 }  // namespace mw
