@@ -1,0 +1,6 @@
+# SQ counters of the config-4 Panda env kernel (register-staged build)
+set -u
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out/probe
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD \
+  --kernel-trace --output-format csv -d gpurun_out/probe/panda_sq2 -o run -- python3 scripts/profile_panda.py > gpurun_out/probe/panda_sq2.log 2>&1 || { echo "rc=$?"; exit 1; }
+echo ok
