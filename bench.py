@@ -117,17 +117,20 @@ def main():
     # ------------------------------------------- fused open-loop rollout figure
     rollout = None
     if not args.no_rollout and not env.action_dim:
+        # its own T-step action tensor: independent of --steps / --warmup
         T = 1000
+        ractions = make_actions(envs, T, dev, torch, rank + 1000)[:, :env.n_worlds].contiguous()
         stream = timed["stream"]
         with torch.cuda.stream(stream):
-            env.rollout(actions[:T, :env.n_worlds].contiguous())   # warm
+            env.rollout(ractions)   # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            env.rollout(actions[:T, :env.n_worlds].contiguous())
+            env.rollout(ractions)
             e1.record(stream)
         stream.synchronize()
         r_ms = e0.elapsed_time(e1)
         Wr = env.n_worlds
+        assert ractions.shape[0] == T
         rollout = {"steps_per_launch": T, "worlds": Wr, "ms_per_launch": round(r_ms, 4),
                    "env_steps_per_s_per_gpu": round(Wr * T / (r_ms * 1e-3), 1),
                    "note": "open-loop (actions known ahead); not the headline value"}
@@ -169,14 +172,18 @@ def main():
 
     # ---------------- BASELINE config 4 (1024 Panda worlds, PID position
     # tracking) measured in the same run when the headline is config 2
+    # every rank takes part (strong split of the 1024 global worlds, barrier +
+    # max over ranks like the headline)
     panda = None
-    if not args.no_panda and rank == 0 and world_size == 1 and args.task != "PandaPositionTracking":
-        panda = panda_leg(args, dev, torch, dist)
+    if not args.no_panda and args.task != "PandaPositionTracking":
+        panda = panda_leg(args, dev, torch, dist, world_size, rank)
     contacts = quadruped = humanoid = None
-    if not args.no_contact_leg and rank == 0 and world_size == 1:
-        contacts = contact_leg(args, dev, torch)
-        quadruped = quadruped_leg(args, dev, torch)
-        humanoid = humanoid_leg(args, dev, torch)
+    if not args.no_contact_leg:
+        if rank == 0 and world_size == 1:
+            contacts = contact_leg(args, dev, torch)
+            quadruped = quadruped_leg(args, dev, torch)
+        # BASELINE config 5: 512 global humanoid worlds split over the ranks
+        humanoid = humanoid_leg(args, dev, torch, dist, world_size, rank)
     runtime = None
     if rank == 0 and world_size == 1 and not args.no_runtime_leg:
         runtime = runtime_leg(args, dev)
@@ -185,7 +192,7 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline and not env.action_dim:
-        cpu, parity = cpu_baseline_and_parity(args, env, actions, np, torch)
+        cpu, parity = cpu_baseline_and_parity(args, env, np, torch)
 
     if rank == 0:
         out = {
@@ -277,7 +284,7 @@ def make_actions(envs, total, dev, torch, rank):
 def make_groups(task, W, S, dev, seed, offset, **kw):
     """S VecEnvs covering worlds [offset, offset + W) in contiguous slices.
     Resets are keyed by the global world index (world_offset), so a grouped
-    run is bit-identical to one VecEnv of W worlds (tests/test_gpu_groups.py)."""
+    run is bit-identical to one VecEnv of W worlds (tests/test_gpu_shard.py)."""
     from mwstep.vecenv import VecEnv
     if W % S:
         raise SystemExit(f"--worlds {W} is not divisible by --groups {S}")
@@ -411,27 +418,36 @@ def panda_bytes_per_env_step(n=9):
     return (12 * n + 12 * n + 8) + (8 * n + 12 * n + 8 * n + 9)
 
 
-def panda_leg(args, dev, torch, dist):
-    from mwstep.vecenv import VecEnv
-    W, K, warm = 1024, 1000, 100
-    envs = make_groups("PandaPositionTracking", W, args.groups, dev, args.seed, 0, max_episode_steps=5000)
+def panda_leg(args, dev, torch, dist, world_size=1, rank=0, W_global=1024):
+    """BASELINE config 4: 1024 Panda worlds in total, split over the ranks in
+    contiguous blocks (strong scaling, "1->8 MI355X shard"); resets are keyed
+    by the global world index, so every world's trajectory is the same at any
+    rank count (tests/test_gpu_shard.py)."""
+    from mwstep.shard import shard_range
+    b, e = shard_range(W_global, rank, world_size)
+    W = e - b
+    K, warm = 1000, 100
+    envs = make_groups("PandaPositionTracking", W, args.groups, dev, args.seed, b, max_episode_steps=5000)
     env = envs[0]
     actions = make_actions(envs, warm + K, dev, torch, 0)
-    r = time_steps(envs, actions, warm, K, args.graph_chunk, dev, torch, dist, 1)
+    r = time_steps(envs, actions, warm, K, args.graph_chunk, dev, torch, dist, world_size)
     bpe = panda_bytes_per_env_step(env.sim.dofs)
     gbs = bpe * W / (r["kernel_us"] * 1e-6) / 1e9
-    out = {"workload": f"PandaPositionTracking: {W} worlds (9-dof tree), Position-mode PID every 1 ms step, "
-                       "sinusoidal targets on joints 1 and 6 (BASELINE.json configs[3])",
-           "value": round(W * K / r["elapsed"], 1), "unit": "env·steps/s", "steps": K, "warmup": warm,
+    out = {"workload": f"PandaPositionTracking: {W_global} worlds (9-dof tree) split over {world_size} GPU(s) "
+                       f"({W} per GPU), Position-mode PID every 1 ms step, sinusoidal targets on joints 1 "
+                       "and 6 (BASELINE.json configs[3])",
+           "value": round(W_global * K / r["elapsed"], 1), "unit": "env·steps/s", "steps": K, "warmup": warm,
+           "scaling": "strong", "worlds_per_gpu": W,
            "ms_per_step": round(r["elapsed"] / K * 1e3, 6),
            "kernel_us_per_launch": round(r["kernel_us"], 3),
            "bytes_per_env_step": bpe, "achieved_GBs": round(gbs, 3),
-           "hbm_frac": round(gbs / HBM_PEAK_GBS, 6), "groups": args.groups}
+           "hbm_frac": round(gbs / HBM_PEAK_GBS, 6), "groups": args.groups,
+           "kernel": "vecenv_pid_step_kernel<9,PandaTopo,false,true>"}
     tr = pmc_traffic("PandaPositionTracking", W)
     out["traffic"] = tr["bytes_per_launch"] if tr else None
     out["algorithmic_bytes_per_launch"] = bpe * W
-    for e in envs:
-        e.close()
+    for e_ in envs:
+        e_.close()
     return out
 
 
@@ -444,39 +460,51 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
     import numpy as np
     stand = np.array([0.6, -1.2] * 4)
     rng = np.random.default_rng(args.seed)
+    q0 = stand + rng.uniform(-0.1, 0.1, (W, 8))
     out = float_tree_leg(args, dev, torch, "quadruped", W, pgs, 0.45, [(400.0, 10.0, 60.0)] * 8,
-                         stand + rng.uniform(-0.1, 0.1, (W, 8)), np.tile(stand, (W, 1)), rng)
+                         q0, np.tile(stand, (W, 1)), rng.uniform(-5, 5, (W, 2)))
     out["workload"] = (f"{W} quadrupeds (16 kg, 8 dofs, floating base) standing on a ground plane under "
                        f"JointController PID hold, sphere-foot / box-trunk contacts, PGS {pgs} iterations, dt = 1 ms")
     return out
 
 
-def humanoid_leg(args, dev, torch, W=512, pgs=50):
-    """BASELINE config 5 on one GPU: 512 iCub-class humanoids (models/humanoid32.urdf:
-    32 dofs, 36.4 kg, floating base, box feet) standing on the ground plane
-    under the JointController PID hold (stiff legs / torso, soft arms),
-    contacts enabled, PGS 50 iterations, one physics step per run; the
-    one-world-per-wavefront kernel (wave_tree.hpp)."""
+def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512, pgs=50):
+    """BASELINE config 5: 512 iCub-class humanoids in total (models/humanoid32.urdf:
+    32 dofs, 36.4 kg, floating base, box feet) split over the ranks, standing on
+    the ground plane under the JointController PID hold (stiff legs / torso,
+    soft arms), contacts enabled, PGS 50 iterations, one physics step per run;
+    the one-world-per-wavefront kernel (wave_tree.hpp).  Initial states are
+    drawn for all 512 worlds and sliced per rank (independent of the rank count)."""
     import numpy as np
     from mwstep import get_model_file
+    from mwstep.shard import shard_range
     from mwstep.sim import Simulator
     probe = Simulator(get_model_file("humanoid32"), n_worlds=1)
     names = probe.joint_names
     probe.close()
     gains = [(500.0, 5.0, 80.0) if ("leg" in n or "torso" in n) else (50.0, 0.5, 80.0) for n in names]
     n = len(names)
+    b, e = shard_range(W_global, rank, world_size)
     rng = np.random.default_rng(args.seed)
-    out = float_tree_leg(args, dev, torch, "humanoid32", W, pgs, 0.535, gains,
-                         rng.uniform(-0.02, 0.02, (W, n)), np.zeros((W, n)), rng, K=200, G=20, warm=40)
-    out["workload"] = (f"{W} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) standing on a "
-                       f"ground plane under JointController PID hold, PGS {pgs} iterations, dt = 1 ms "
-                       "(BASELINE.json configs[4] on one GPU)")
+    q0 = rng.uniform(-0.02, 0.02, (W_global, n))
+    xy = rng.uniform(-5, 5, (W_global, 2))
+    out = float_tree_leg(args, dev, torch, "humanoid32", e - b, pgs, 0.535, gains,
+                         q0[b:e], np.zeros((e - b, n)), xy[b:e], K=200, G=20, warm=40,
+                         dist=dist, world_size=world_size)
+    out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
+    out["scaling"] = "strong"
+    out["worlds_per_gpu"] = e - b
+    out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
+                       f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "
+                       f"PGS {pgs} iterations, dt = 1 ms (BASELINE.json configs[4])")
     return out
 
 
-def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, rng, K=500, G=50, warm=100):
+def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, K=500, G=50, warm=100,
+                   dist=None, world_size=1):
     """Time W floating-base worlds of `model` under a PID hold, one physics
-    step per run, replayed from hipGraphs of mw_run_device."""
+    step per run, replayed from hipGraphs of mw_run_device; with several ranks
+    the timed region is bracketed by barriers and the max over ranks is kept."""
     import numpy as np
     from mwstep import get_model_file
     from mwstep import native as N
@@ -487,7 +515,7 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, rng,
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
     sim.set("reset_q", q0)
-    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), np.full(W, z0), np.ones(W), np.zeros((W, 3))])
+    pose = np.column_stack([xy, np.full(W, z0), np.ones(W), np.zeros((W, 3))])
     sim.reset_base_pose(pose)
     sim.run(paused=True)
     sim.set_controller_period(1e-3)
@@ -505,6 +533,9 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, rng,
     stream.synchronize()
     n_rep = K // G
     torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(stream):
@@ -513,12 +544,19 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, rng,
             graph.replay()
         e1.record(stream)
     torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
     steps = n_rep * G
     sample = range(0, W, max(1, W // 64))
     pts = [len(sim.contacts(w)) for w in sample]
     z = sim.base_pose()[:, 2]
     out = {"value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
+           "elapsed_s": elapsed,
            "ms_per_step": round(elapsed / steps * 1e3, 6),
            "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
            "float_kernel": {1: "world per lane (float_tree.hpp)", 2: "world per wavefront (wave_tree.hpp)"}.get(sim.float_kernel()),
@@ -666,10 +704,27 @@ def world_sweep(args, dev, torch):
     return out
 
 
-def cpu_baseline_and_parity(args, env, actions, np, torch):
+def dart_probe():
+    """is a DART (the reference's physics engine) runtime on
+    this host?  `ldconfig -p` lines naming dart; nothing is installed or run."""
+    import subprocess
+    try:
+        out = subprocess.run(["ldconfig", "-p"], capture_output=True, text=True, timeout=20).stdout
+    except (OSError, subprocess.SubprocessError) as e:
+        return {"found": False, "probe": f"ldconfig -p failed: {e}"}
+    libs = sorted({ln.split()[0] for ln in out.splitlines() if "dart" in ln.lower() and ln.strip()})
+    return {"found": bool(libs), "libs": libs[:8],
+            "probe": "ldconfig -p | grep -i dart",
+            "note": ("DART libraries present, but not ign-gazebo/ign-physics: the reference path is still "
+                     "not runnable" if libs else "no DART on this host: the reference CPU path cannot run")}
+
+
+def cpu_baseline_and_parity(args, env, np, torch):
     """fp64 C oracle (oracle/, test infrastructure) on a bounded sample of the
-    same workload, single thread; plus a teacher-forced one-step parity check
-    of the GPU kernel against it on the same sample."""
+    same workload (its own actions: PCG64(43) Bernoulli(0.5) for the discrete
+    task, U(-50, 50) otherwise -- SURVEY §8d), on every host core this process
+    may use; plus a teacher-forced one-step parity check of the GPU kernel
+    against it on 256 worlds x 100 steps.  Nothing here depends on --steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from mwstep import get_model_file
@@ -677,18 +732,18 @@ def cpu_baseline_and_parity(args, env, actions, np, torch):
 
     kind, model = TASKS[args.task]
     cm = pyoracle.load_urdf(get_model_file(model))
-    Wc = 4096
-    acts = actions[:, :Wc].cpu().numpy() if actions.shape[1] >= Wc else None
-    if acts is None:
-        return None, None
-    acts = acts if kind == 0 else acts.astype(np.float64)
+    Wc, T_max = 4096, 4000
+    rng = np.random.default_rng(43)
+    if kind == 0:
+        acts = rng.integers(0, 2, (T_max, Wc)).astype(np.int32)
+    else:
+        acts = rng.uniform(-50.0, 50.0, (T_max, Wc))
     ref = pyoracle.VecEnv(cm, pyoracle.make_task(kind, seed=args.seed), Wc)
     ref.reset()
     t0 = time.perf_counter()
     ref.rollout(acts[:20])
     probe = time.perf_counter() - t0
-    T = int(max(20, min(acts.shape[0], args.cpu_seconds / max(probe / 20, 1e-9))))
-    T = min(T, acts.shape[0])
+    T = int(max(20, min(T_max, args.cpu_seconds / max(probe / 20, 1e-9))))
     ref.reset()
     t0 = time.perf_counter()
     ref.rollout(acts[:T])
@@ -713,11 +768,13 @@ def cpu_baseline_and_parity(args, env, actions, np, torch):
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
+    dart = dart_probe()
     cpu = {"value": round(threads * Wc * T / mt_s, 1), "unit": "env·steps/s", "cores": threads, "kind": "port",
            "sample": f"{threads} threads x {Wc} worlds x {T} env steps of {args.task}, fp64 C oracle "
                      f"({mt_s:.1f} s wall; {cpu_model}); the reference's ign-gazebo+DART path is not buildable here",
            "single_thread_value": round(single, 1),
-           "single_thread_sample": f"{Wc} worlds x {T} env steps, 1 thread ({cpu_s:.1f} s)"}
+           "single_thread_sample": f"{Wc} worlds x {T} env steps, 1 thread ({cpu_s:.1f} s)",
+           "dart_probe": dart}
 
     # teacher-forced one-step parity on 256 worlds x 100 steps
     from mwstep.vecenv import VecEnv
@@ -739,7 +796,7 @@ def cpu_baseline_and_parity(args, env, actions, np, torch):
         if m.any():
             worst = max(worst, float(np.abs(o[m] - orf[m]).max()))
     gpu.close()
-    return cpu, {"value": worst, "mode": "one-step teacher-forced, 256 worlds x 100 steps",
+    return cpu, {"value": worst, "mode": f"one-step teacher-forced, {Wp} worlds x {Tp} steps",
                  "vs": "fp64 DART-semantics oracle (DART itself absent: parity unpinned)"}
 
 

@@ -88,6 +88,12 @@ struct mw_sim {
     // [ptgt | pid_e | pid_i | pid_u] on the device; h_ptgt mirrors ptgt
     float* d_aux = nullptr;
     float* h_ptgt = nullptr;
+    // pinned staging copy of [command slab | position targets]: the H2D copies
+    // of a run read it, so the host mirror can be cleared / rewritten right
+    // after the launch; stage_ev marks when the last copy out of it finished
+    uint8_t* h_stage = nullptr;
+    hipEvent_t stage_ev = nullptr;
+    bool stage_pending = false;
     // floating single-body models (free_body.hpp)
     bool floating = false;
     bool ground = false;          // a ground plane z = 0 is in the world
@@ -502,6 +508,8 @@ void mw_destroy(mw_sim* s) {
         (void)hipFree(s->d_aux);
         (void)hipHostFree(s->h_block);
         (void)hipHostFree(s->h_ptgt);
+        (void)hipHostFree(s->h_stage);
+        if (s->stage_ev) (void)hipEventDestroy(s->stage_ev);
         (void)hipFree(s->d_fblock);
         (void)hipFree(s->d_free);
         (void)hipFree(s->d_float);
@@ -750,6 +758,9 @@ int mw_initialize(mw_sim* s) {
     std::memset(s->h_ptgt, 0, s->nw * sizeof(float));
     MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_block), s->block_bytes, hipHostMallocDefault));
     std::memset(s->h_block, 0, s->block_bytes);
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_stage), s->cmd_bytes + s->nw * sizeof(float),
+                         hipHostMallocDefault));
+    MW_HIP(hipEventCreateWithFlags(&s->stage_ev, hipEventDisableTiming));
     float* base = reinterpret_cast<float*>(s->d_block);
     s->dev.q = base;
     s->dev.qd = base + s->nw;
@@ -851,14 +862,35 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     if (readback && (rc = pull_state(s))) return rc;
     if (s->floating && !s->float_tree) return run_free(s, paused, readback);
     if (s->float_tree && (rc = upload_base_resets(s))) return rc;
-    if (s->cmd_dirty) {
-        MW_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_block) + s->cmd_off, s->h_block + s->cmd_off,
-                              s->cmd_bytes, hipMemcpyHostToDevice, s->stream));
-        s->cmd_dirty = false;
-    }
-    if (s->ptgt_dirty) {
-        MW_HIP(hipMemcpyAsync(s->d_aux, s->h_ptgt, s->nw * sizeof(float), hipMemcpyHostToDevice, s->stream));
-        s->ptgt_dirty = false;
+    if (s->cmd_dirty || s->ptgt_dirty) {
+        // pending commands / resets / targets go through the staging buffer:
+        // the host mirror is cleared below while the copy may still be queued
+        // (a device-resident run does not synchronise).  A graph would replay
+        // a host-memory copy with whatever the buffer holds at replay time, so
+        // pending commands cannot be captured.
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        MW_HIP(hipStreamIsCapturing(s->stream, &cap));
+        if (cap != hipStreamCaptureStatusNone)
+            return fail(MW_ESTATE, "pending joint commands, resets or targets cannot be captured into a graph: "
+                                   "apply them with a run before capturing");
+        if (s->stage_pending) {
+            MW_HIP(hipEventSynchronize(s->stage_ev));  // the previous copy out of the stage is done
+            s->stage_pending = false;
+        }
+        if (s->cmd_dirty) {
+            std::memcpy(s->h_stage, s->h_block + s->cmd_off, s->cmd_bytes);
+            MW_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_block) + s->cmd_off, s->h_stage, s->cmd_bytes,
+                                  hipMemcpyHostToDevice, s->stream));
+            s->cmd_dirty = false;
+        }
+        if (s->ptgt_dirty) {
+            std::memcpy(s->h_stage + s->cmd_bytes, s->h_ptgt, s->nw * sizeof(float));
+            MW_HIP(hipMemcpyAsync(s->d_aux, s->h_stage + s->cmd_bytes, s->nw * sizeof(float),
+                                  hipMemcpyHostToDevice, s->stream));
+            s->ptgt_dirty = false;
+        }
+        MW_HIP(hipEventRecord(s->stage_ev, s->stream));
+        s->stage_pending = true;
     }
     const mw::PidSet pid = pid_set(s);
     if (s->wave && s->pid_dirty) {
@@ -1512,6 +1544,9 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
     if (!cfg || !out) return fail(MW_EINVAL, "null argument");
     *out = nullptr;
     const int n = s->n;
+    // the batched env kernels step fixed-base chains only: a floating model
+    // with a matching dof count would have its base and contacts ignored
+    if (s->floating) return fail(MW_EINVAL, "the batched env tasks need a fixed-base model");
     const bool cart = cfg->kind >= MW_TASK_CARTPOLE_DISCRETE && cfg->kind <= MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP;
     const bool pidtask = cfg->kind == MW_TASK_PANDA_POSITION_TRACKING;
     if (cart && n != 2) return fail(MW_EINVAL, "CartPole tasks need the 2-dof cartpole model");

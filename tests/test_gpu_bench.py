@@ -1,0 +1,40 @@
+"""The driver's exact bench command (`python bench.py --gpus 1 --steps 20
+--warmup 5`) in a fresh process: one JSON line with the contract's fields,
+`roofline`, `cpu_baseline` and the parity figure (the r01 bench
+crashed on exactly this command because a leg was sized from --steps)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(600)
+def test_driver_bench_command(require_gpu):
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "20", "--warmup", "5"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=560, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in out, k
+    assert out["steps"] == 20 and out["warmup"] == 5 and out["n_gpus"] == 1
+    assert out["value"] > 1e6
+    assert "configs[1]" in out["config"]["workload"]
+    rl = out["roofline"]
+    assert rl["bound"] == "hbm" and 0 < rl["frac"] < 1 and rl["peak"] == 8000.0
+    cpu = out["cpu_baseline"]
+    assert cpu["kind"] == "port" and cpu["cores"] >= 1 and cpu["value"] > 0 and "dart_probe" in cpu
+    assert out["obs_max_abs_err_vs_oracle"]["value"] <= 1e-4
+    assert out["rollout_fused"]["steps_per_launch"] == 1000
+    assert out["panda_c4"]["worlds_per_gpu"] == 1024
+    assert out["humanoid_c5"]["worlds_per_gpu"] == 512

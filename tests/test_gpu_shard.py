@@ -1,0 +1,136 @@
+"""GPU tests of the world sharding and of the device-resident run.
+
+  * a VecEnv of W worlds equals two VecEnvs of W/2 worlds with world_offset
+    0 / W/2 (a rank's shard, and bench.py's world groups) BIT FOR BIT over 200
+    closed-loop steps including TimeLimit / termination auto-resets, for the
+    headline CartPole task (BASELINE configs[1]) and the Panda PID task
+    (configs[3], the 1 -> 8 GPU strong split): resets are keyed by the global
+    world index, so a world's trajectory does not depend on the rank count;
+  * mw_run_device with a pending joint reset and a force command equals mw_run
+    (the command slab is copied out of a staging buffer, so clearing the host
+    mirror right after the asynchronous launch cannot drop it);
+  * pending commands cannot be captured into a graph (loud error).
+"""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_split(task, W, T, max_steps, make_actions):
+    import torch
+    from mwstep.vecenv import VecEnv
+    full = VecEnv(task, n_worlds=W, device=0, seed=7, max_episode_steps=max_steps)
+    half = [VecEnv(task, n_worlds=W // 2, device=0, seed=7, world_offset=k * (W // 2),
+                   max_episode_steps=max_steps) for k in range(2)]
+    o_full = full.reset().clone()
+    o_half = torch.cat([h.reset().clone() for h in half])
+    assert torch.equal(o_full, o_half)
+    n_done = 0
+    for t in range(T):
+        a = make_actions(t, o_full)
+        o, r, d, info = full.step(a)
+        parts = [h.step(a[k * (W // 2):(k + 1) * (W // 2)].contiguous()) for k, h in enumerate(half)]
+        torch.cuda.synchronize()
+        assert torch.equal(o, torch.cat([p[0] for p in parts])), t
+        assert torch.equal(r, torch.cat([p[1] for p in parts])), t
+        assert torch.equal(d, torch.cat([p[2] for p in parts])), t
+        n_done += int(d.sum())
+        o_full = o
+    q, qd = full.state()
+    qs = [h.state() for h in half]
+    assert torch.equal(q, torch.cat([x[0] for x in qs], dim=1))
+    assert torch.equal(qd, torch.cat([x[1] for x in qs], dim=1))
+    for e in [full] + half:
+        e.close()
+    return n_done
+
+
+def test_cartpole_shards_bit_identical(require_gpu):
+    import torch
+    gen = torch.Generator(device="cuda").manual_seed(43)
+    acts = torch.randint(0, 2, (200, 4096), generator=gen, device="cuda", dtype=torch.int32)
+    n_done = _run_split("CartPoleDiscreteBalancing", 4096, 200, 50, lambda t, o: acts[t].contiguous())
+    assert n_done > 4096  # TimeLimit (50 steps) and pole-angle resets happened inside the window
+
+
+def test_panda_shards_bit_identical(require_gpu):
+    import torch
+    T, W = 200, 1024
+    state = {}
+
+    def targets(t, obs):
+        if "q0" not in state:
+            state["q0"] = obs[:, :9].clone()
+        tg = state["q0"].clone()
+        s = float(np.sin(2 * np.pi * 0.33 * t * 1e-3))
+        tg[:, 0] += 0.9 * 2.8973 * s
+        tg[:, 5] += 0.9 * (3.7525 + 0.0175) / 2 * s
+        return tg.contiguous()
+
+    n_done = _run_split("PandaPositionTracking", W, T, 80, targets)
+    assert n_done >= W  # every world hit the 80-step TimeLimit at least once
+    del torch
+
+
+@pytest.mark.parametrize("model", ["cartpole", "pendulum"])
+def test_run_device_applies_pending_commands(require_gpu, model):
+    """run_impl cleared the host command slab right after queueing
+    its asynchronous H2D copy; a device-resident run could lose the force
+    command and the reset."""
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    W = 257
+    sims = [Simulator(get_model_file(model), n_worlds=W) for _ in range(2)]
+    rng = np.random.default_rng(3)
+    q0 = rng.uniform(-0.3, 0.3, (W, sims[0].dofs))
+    qd0 = rng.uniform(-1, 1, (W, sims[0].dofs))
+    tau = rng.uniform(-5, 5, (W, sims[0].dofs))
+    for s in sims:
+        s.set_control_mode(N.MODE_FORCE)
+        s.run(paused=True)
+        s.set("reset_q", q0)
+        s.set("reset_qd", qd0)
+        s.set("force_target", tau)
+    sims[0].run()
+    sims[1].run_device(1)
+    assert np.array_equal(sims[0].get("q"), sims[1].get("q"))
+    assert np.array_equal(sims[0].get("qd"), sims[1].get("qd"))
+    # the reset took effect (not the zero state) and the force acted
+    assert np.abs(sims[1].get("q") - q0).max() < 0.01
+    # a second round: new commands while the first copy may still be queued
+    for s in sims:
+        s.set("force_target", -tau)
+    sims[0].run()
+    sims[1].run_device(1)
+    assert np.array_equal(sims[0].get("qd"), sims[1].get("qd"))
+    for s in sims:
+        s.close()
+
+
+def test_pending_commands_refuse_graph_capture(require_gpu):
+    import torch
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    stream = torch.cuda.Stream()
+    sim = Simulator(get_model_file("cartpole"), n_worlds=64, stream=stream.cuda_stream)
+    sim.set_control_mode(N.MODE_FORCE)
+    sim.run()
+    sim.set("force_target", np.ones((64, 2)))
+    graph = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="captured"):
+        with torch.cuda.stream(stream):
+            with torch.cuda.graph(graph, stream=stream):
+                sim.run_device(1)
+    sim.run_device(1)  # applied outside capture: fine
+    with torch.cuda.stream(stream):
+        stream.synchronize()
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2, stream=stream):
+            sim.run_device(2)
+        g2.replay()
+    stream.synchronize()
+    sim.close()
