@@ -15,7 +15,7 @@ stop_if_fatal() {  # $1 = exit code, $2 = step name
   fi
 }
 echo "== pytest -m gpu" | tee "$OUT/session.log"
-timeout -k 10 420 python -m pytest tests -m gpu -x -q -s > "$OUT/pytest_gpu_$tag.log" 2>&1
+timeout -k 10 720 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$tag.log" 2>&1
 rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -5 "$OUT/pytest_gpu_$tag.log"
 stop_if_fatal $rc pytest
 echo "== smoke" | tee -a "$OUT/session.log"
@@ -23,7 +23,7 @@ timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/smoke_$tag.log"
 stop_if_fatal $rc smoke
 echo "== bench" | tee -a "$OUT/session.log"
-timeout -k 10 240 python bench.py > "$OUT/bench_$tag.json" 2> "$OUT/bench_$tag.err"
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_$tag.json" 2> "$OUT/bench_$tag.err"
 rc=$?; echo "bench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_$tag.json"; tail -3 "$OUT/bench_$tag.err"
 stop_if_fatal $rc bench
 echo "== rocprofv3" | tee -a "$OUT/session.log"
