@@ -413,9 +413,10 @@ def launch_floor(dev, torch, K=2000, G=100):
 
 def panda_bytes_per_env_step(n=9):
     """Compulsory HBM bytes of one PandaPositionTracking step of one world:
-    read q, qd, targets (4 B x 3n), PID state e/i/u (12n), counters (8 B);
-    write q, qd (8n), PID state (12n), obs 2n floats (8n), reward 4, done 1, steps 4."""
-    return (12 * n + 12 * n + 8) + (8 * n + 12 * n + 8 * n + 9)
+    read q, qlo, qd, targets (4 B x 4n), PID state e/i/u (12n), counters (8 B);
+    write q, qlo, qd (12n), PID state (12n), obs 2n floats (8n), reward 4, done 1,
+    steps 4.  qlo: low word of the compensated joint positions (kernels.hpp)."""
+    return (16 * n + 12 * n + 8) + (12 * n + 12 * n + 8 * n + 9)
 
 
 def panda_leg(args, dev, torch, dist, world_size=1, rank=0, W_global=1024):

@@ -608,7 +608,8 @@ template <int N, bool DUAL, bool CONS, Topo TOPO, class WK>
 __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)[N], float (&qd)[N],
                                         const float (&tau)[N], const uint8_t (&act)[N],
                                         const float (&vcmd)[N], float dt, int pgs_iters,
-                                        float (&qdd)[N], WK& W, const Dyn<N>& D) {
+                                        float (&qdd)[N], WK& W, const Dyn<N>& D,
+                                        float* __restrict__ qlo = nullptr) {
     aba<N, DUAL, TOPO>(P, q, qd, tau, dt, qdd, W, D);
 #pragma unroll
     for (int i = 0; i < N; ++i) qd[i] += dt * qdd[i];
@@ -696,8 +697,24 @@ __device__ __forceinline__ void substep(const ChainF* __restrict__ P, float (&q)
             }
         }
     }
+    if (qlo) {
+        // compensated q += dt qd: (q, qlo) is an unevaluated sum; TwoSum
+        // keeps the rounding error of every step in qlo, Fast2Sum renormalises
 #pragma unroll
-    for (int i = 0; i < N; ++i) q[i] += dt * qd[i];
+        for (int i = 0; i < N; ++i) {
+            const float h = dt * qd[i];
+            const float s = q[i] + h;
+            const float bv = s - q[i];
+            const float err = (q[i] - (s - bv)) + (h - bv);
+            const float lo = qlo[i] + err;
+            const float hi = s + lo;
+            qlo[i] = lo - (hi - s);
+            q[i] = hi;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) q[i] += dt * qd[i];
+    }
 }
 
 // register-staged substep (small models)

@@ -281,7 +281,8 @@ template <int N>
 __device__ __forceinline__ void joint_forces(const ChainF* __restrict__ P, const SimDev& S, const PidSet& pid, int W,
                                              int w, const RunArgs& A, int s, const uint8_t (&act)[N],
                                              const float (&cmd)[N], const float (&vc)[N], const float (&q)[N],
-                                             const float (&qd)[N], bool any_pid, float (&tau)[N]) {
+                                             const float (&qd)[N], const float (&qlo)[N], bool any_pid,
+                                             float (&tau)[N]) {
     const bool gate = (A.pid_gate >> s) & 1u;
 #pragma unroll
     for (int d = 0; d < N; ++d) {
@@ -296,7 +297,7 @@ __device__ __forceinline__ void joint_forces(const ChainF* __restrict__ P, const
                 float u = S.pid_u[k];
                 if (gate) {
                     const bool pos = (act[d] == kActPidPos);
-                    const float err = pos ? (q[d] - S.ptgt[k]) : (qd[d] - vc[d]);
+                    const float err = pos ? ((q[d] - S.ptgt[k]) + qlo[d]) : (qd[d] - vc[d]);
                     float el = S.pid_e[k], ie = S.pid_i[k];
                     if (pid_update(pid.g[d], err, A.inv_dt, A.dt, el, ie, u)) {
                         S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
@@ -321,7 +322,7 @@ __device__ __forceinline__ void joint_resets(const SimDev& S, int W, int w, floa
         const uint8_t f = S.rflag[d * W + w];
         if (f) {
             if (f & 2u) qd[d] = S.rqd[d * W + w];
-            if (f & 1u) q[d] = S.rq[d * W + w];
+            if (f & 1u) { q[d] = S.rq[d * W + w]; S.qlo[d * W + w] = 0.f; }
             if (f & 4u) { S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; }
             S.rflag[d * W + w] = 0;
         }
@@ -334,9 +335,11 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     const ChainF* __restrict__ P = model_params<BAKED>(Pin);
-    float q[N], qd[N];
+    float q[N], qd[N], qlo[N];
     load_state<N>(S, W, w, q, qd);
     if (A.first) joint_resets<N>(S, W, w, q, qd);
+#pragma unroll
+    for (int d = 0; d < N; ++d) qlo[d] = S.qlo[d * W + w];
     if (!A.paused) {
         float cmd[N], vc[N], tau[N], qdd[N];
         uint8_t act[N];
@@ -350,11 +353,14 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
         }
         MW_DECLARE_STAGE(N, DUAL, BAKED, stage);
         for (int s = 0; s < A.substeps; ++s) {
-            joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, q, qd, any_pid, tau);
-            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, nominal_dyn<N>(P));
+            joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, q, qd, qlo, any_pid, tau);
+            substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, nominal_dyn<N>(P),
+                                         qlo);
         }
 #pragma unroll
         for (int d = 0; d < N; ++d) S.qdd[d * W + w] = qdd[d];
+#pragma unroll
+        for (int d = 0; d < N; ++d) S.qlo[d * W + w] = qlo[d];
     }
 #pragma unroll
     for (int d = 0; d < N; ++d) S.cmd[d * W + w] = 0.f;  // JointForceCmd zero-fill (paused too)
@@ -563,8 +569,9 @@ __global__ void __launch_bounds__(64) float_run_kernel(const ChainF* __restrict_
         __shared__ float sh_rows[kRowsLdsWords * kLdsLanes];
         LdsStage<N, false> stage{sh_bs + threadIdx.x, nullptr, sh_own + threadIdx.x, nullptr};
         const RowsLds rows{sh_rows + threadIdx.x};
+        const float no_lo[N] = {};  // the floating-tree kernel integrates q uncompensated
         for (int s = 0; s < A.substeps; ++s) {
-            joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, X.q, X.qd, any_pid, tau);
+            joint_forces<N>(P, S, pid, W, w, A, s, act, cmd, vc, X.q, X.qd, no_lo, any_pid, tau);
             active = float_step<N, TOPO, CONS>(P, F, X, tau, act, vc, A.dt, A.pgs_iters, qdd, stage, wr, rows);
         }
 #pragma unroll
@@ -727,10 +734,11 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     const ChainF* __restrict__ P = model_params<BAKED>(Pin);
-    float q[N], qd[N], tgt[N], pe[N], pi[N], pu[N];
+    float q[N], qd[N], qlo[N], tgt[N], pe[N], pi[N], pu[N];
     load_state<N>(S, W, w, q, qd);
 #pragma unroll
     for (int d = 0; d < N; ++d) {
+        qlo[d] = S.qlo[d * W + w];
         tgt[d] = targets[static_cast<size_t>(w) * N + d];
         pe[d] = S.pid_e[d * W + w];
         pi[d] = S.pid_i[d * W + w];
@@ -746,12 +754,12 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
 #pragma unroll
         for (int d = 0; d < N; ++d) {
             float u = pu[d];
-            if (!pid_update(pid.g[d], q[d] - tgt[d], inv_dt, dt, pe[d], pi[d], u)) u = 0.f;
+            if (!pid_update(pid.g[d], (q[d] - tgt[d]) + qlo[d], inv_dt, dt, pe[d], pi[d], u)) u = 0.f;
             else pu[d] = u;
             const float e = P->b[d].effort;
             tau[d] = fminf(fmaxf(u, -e), e);
         }
-        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd, stage, nominal_dyn<N>(P));
+        substep<N, DUAL, CONS, TOPO>(P, q, qd, tau, act, vc, dt, pgs_iters, qdd, stage, nominal_dyn<N>(P), qlo);
     }
     float r = 0.f;
 #pragma unroll
@@ -767,12 +775,13 @@ __global__ void __launch_bounds__(256) vecenv_pid_step_kernel(const ChainF* __re
         V.episode[w] = episode0 + 1u;
         pid_task_reset<N>(P, T, T.world_offset + static_cast<uint32_t>(w), episode0 + 1u, q, qd);
 #pragma unroll
-        for (int d = 0; d < N; ++d) { pe[d] = 0.f; pi[d] = 0.f; pu[d] = 0.f; }
+        for (int d = 0; d < N; ++d) { pe[d] = 0.f; pi[d] = 0.f; pu[d] = 0.f; qlo[d] = 0.f; }
     }
     store_pid_obs<N>(obs + static_cast<size_t>(w) * 2 * N, q, qd);
     store_state<N>(S, W, w, q, qd);
 #pragma unroll
     for (int d = 0; d < N; ++d) {
+        S.qlo[d * W + w] = qlo[d];
         S.pid_e[d * W + w] = pe[d];
         S.pid_i[d * W + w] = pi[d];
         S.pid_u[d * W + w] = pu[d];
@@ -790,7 +799,9 @@ __global__ void __launch_bounds__(256) vecenv_pid_reset_kernel(const ChainF* __r
     store_pid_obs<N>(obs + static_cast<size_t>(w) * 2 * N, q, qd);
     store_state<N>(S, W, w, q, qd);
 #pragma unroll
-    for (int d = 0; d < N; ++d) { S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; }
+    for (int d = 0; d < N; ++d) {
+        S.pid_e[d * W + w] = 0.f; S.pid_i[d * W + w] = 0.f; S.pid_u[d * W + w] = 0.f; S.qlo[d * W + w] = 0.f;
+    }
     V.episode[w] = 0u;
     V.steps[w] = 0u;
 }

@@ -25,6 +25,11 @@ struct SimDev {
     float* pid_e = nullptr;
     float* pid_i = nullptr;
     float* pid_u = nullptr;
+    // low word of the joint positions (q = q_hi + qlo, compensated position
+    // integration): the PID error q - target is formed from both, so its
+    // derivative term (gain d / dt on the position error) does not amplify
+    // the float32 rounding of q += dt qd (kernels with a JointController)
+    float* qlo = nullptr;
 };
 
 // Device arrays of a floating single-body model (free_body.hpp).

@@ -85,7 +85,7 @@ struct mw_sim {
     size_t block_bytes = 0, cmd_off = 0, cmd_bytes = 0, state_bytes = 0;
     mw::ChainF* d_params = nullptr;
     mw::ChainF h_params{};
-    // [ptgt | pid_e | pid_i | pid_u] on the device; h_ptgt mirrors ptgt
+    // [ptgt | pid_e | pid_i | pid_u | qlo] on the device; h_ptgt mirrors ptgt
     float* d_aux = nullptr;
     float* h_ptgt = nullptr;
     // pinned staging copy of [command slab | position targets]: the H2D copies
@@ -752,8 +752,8 @@ int mw_initialize(mw_sim* s) {
     s->block_bytes = s->state_bytes + s->cmd_bytes;
     MW_HIP(hipMalloc(&s->d_block, s->block_bytes));
     MW_HIP(hipMalloc(&s->d_params, sizeof(mw::ChainF)));
-    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_aux), 4 * s->nw * sizeof(float)));
-    MW_HIP(hipMemsetAsync(s->d_aux, 0, 4 * s->nw * sizeof(float), s->stream));
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_aux), 5 * s->nw * sizeof(float)));
+    MW_HIP(hipMemsetAsync(s->d_aux, 0, 5 * s->nw * sizeof(float), s->stream));
     MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ptgt), s->nw * sizeof(float), hipHostMallocDefault));
     std::memset(s->h_ptgt, 0, s->nw * sizeof(float));
     MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_block), s->block_bytes, hipHostMallocDefault));
@@ -775,6 +775,7 @@ int mw_initialize(mw_sim* s) {
     s->dev.pid_e = s->d_aux + s->nw;
     s->dev.pid_i = s->d_aux + 2 * s->nw;
     s->dev.pid_u = s->d_aux + 3 * s->nw;
+    s->dev.qlo = s->d_aux + 4 * s->nw;
     s->mode.assign(s->nw, MW_MODE_IDLE);
     s->ptgt.assign(s->nw, 0.0);
     s->cmd64.assign(s->nw, 0.0);
@@ -1528,6 +1529,7 @@ int mw_copy_state(mw_sim* s, float* q, float* qd, int to_sim) {
     if (to_sim) {
         MW_HIP(hipMemcpyAsync(s->dev.q, q, bytes, hipMemcpyDeviceToDevice, s->stream));
         MW_HIP(hipMemcpyAsync(s->dev.qd, qd, bytes, hipMemcpyDeviceToDevice, s->stream));
+        MW_HIP(hipMemsetAsync(s->dev.qlo, 0, bytes, s->stream));
         s->host_stale = true;
     } else {
         MW_HIP(hipMemcpyAsync(q, s->dev.q, bytes, hipMemcpyDeviceToDevice, s->stream));

@@ -375,10 +375,222 @@ void or_rnea(const or_model* m, const double* q, const double* qd,
 
 /* ---------------- boxed LCP ---------------- */
 
+/* Sweep budget: iters >= 0 runs exactly that many Gauss-Seidel sweeps (the
+ * GPU kernels' fixed count).  iters < 0 (OR_PGS_CONVERGED) solves the boxed
+ * LCP exactly: OR_PGS_WARM sweeps give an active-set guess, then lcp_refine()
+ * solves the linear system of that active set and repairs it until the
+ * complementarity conditions hold to round-off (friction rows bounded by
+ * mu x_normal).  That is the problem DART's primary solver, the Dantzig
+ * pivoting LCP of BoxedLcpConstraintSolver [EXT], solves exactly -- the
+ * converged reference for the truncated sweeps of the kernels.  (Plain PGS
+ * would need ~1e5+ sweeps: with CFM 1e-5 the redundant contact corners leave
+ * A conditioned ~1e5.)  or_pgs_stats(): sweeps and active-set rounds of the
+ * latest solve, and its final complementarity residual. */
+#define OR_PGS_WARM 300
+#define OR_LCP_MAXN (3 * OR_MAXFC + 3 * OR_MAXB > 3 * OR_MAXCONTACTS ? 3 * OR_MAXFC + 3 * OR_MAXB : 3 * OR_MAXCONTACTS)
+static int g_pgs_sweeps = 0;
+static double g_pgs_delta = 0.0;
+
+void or_pgs_stats(int* sweeps, double* last_delta)
+{
+    if (sweeps) *sweeps = g_pgs_sweeps;
+    if (last_delta) *last_delta = g_pgs_delta;
+}
+
+static int pgs_budget(int iters) { return iters >= 0 ? iters : OR_PGS_WARM; }
+
+static void pgs_count(int it) { g_pgs_sweeps = it + 1; g_pgs_delta = 0.0; }
+
+/* bounds of row r at impulses x: findex[r] >= 0 marks a friction row whose
+ * box is [-mu x_f, mu x_f] (x_f: its contact's normal impulse) */
+static void row_bounds(int r, const double* lo, const double* hi, const int* findex, double mu,
+                       const double* x, double* L, double* U)
+{
+    if (findex[r] >= 0) {
+        const double u = mu * x[findex[r]];
+        *L = -u;
+        *U = u;
+    } else {
+        *L = lo[r];
+        *U = hi[r];
+    }
+}
+
+/* dense Gaussian elimination with partial pivoting, n <= OR_LCP_MAXN; 0 if singular */
+static int lcp_gauss(int n, double* K, double* c, double* y)
+{
+    for (int col = 0; col < n; ++col) {
+        int piv = col;
+        for (int r = col + 1; r < n; ++r)
+            if (fabs(K[r * n + col]) > fabs(K[piv * n + col])) piv = r;
+        if (K[piv * n + col] == 0.0) return 0;
+        if (piv != col) {
+            for (int e = 0; e < n; ++e) { double t = K[col * n + e]; K[col * n + e] = K[piv * n + e]; K[piv * n + e] = t; }
+            double t = c[col]; c[col] = c[piv]; c[piv] = t;
+        }
+        for (int r = col + 1; r < n; ++r) {
+            const double f = K[r * n + col] / K[col * n + col];
+            if (f == 0.0) continue;
+            for (int e = col; e < n; ++e) K[r * n + e] -= f * K[col * n + e];
+            c[r] -= f * c[col];
+        }
+    }
+    for (int r = n - 1; r >= 0; --r) {
+        double acc = c[r];
+        for (int e = r + 1; e < n; ++e) acc -= K[r * n + e] * y[e];
+        y[r] = acc / K[r * n + r];
+    }
+    return 1;
+}
+
+/* Complementarity residual of x in velocity units (0 at an exact solution):
+ * free rows |s|, rows at the lower bound max(s, 0), at the upper bound
+ * max(-s, 0), plus any bound violation scaled by A_rr; s = b - A x. */
+static double lcp_residual(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
+                           const int* findex, double mu, const double* x, double tol_x)
+{
+    double res = 0.0;
+    for (int r = 0; r < n; ++r) {
+        double s = b[r];
+        for (int c = 0; c < n; ++c) s -= A[r * lda + c] * x[c];
+        double l, u, e;
+        row_bounds(r, lo, hi, findex, mu, x, &l, &u);
+        if (x[r] < l - tol_x || x[r] > u + tol_x)
+            e = (x[r] < l ? l - x[r] : x[r] - u) * A[r * lda + r];
+        else if (u - l <= tol_x)
+            e = 0.0;  /* a pinned row (friction of a contact without normal impulse) */
+        else if (x[r] <= l + tol_x)
+            e = s > 0.0 ? s : 0.0;
+        else if (x[r] >= u - tol_x)
+            e = s < 0.0 ? -s : 0.0;
+        else
+            e = fabs(s);
+        res = e > res ? e : res;
+    }
+    return res;
+}
+
+/* Exact solve of the box QP  min 1/2 x'Ax - b'x,  L <= x <= U  (A symmetric
+ * positive definite: the CFM makes it so) by the primal active-set method,
+ * warm-started from x (clamped).  Finite for a strictly convex QP: every
+ * step either reaches the minimiser on the working set (then the bound with
+ * the most wrongly signed multiplier is released) or stops at the first
+ * blocking bound, which joins the working set.  Returns the iterations
+ * used, or -1 when the budget ran out. */
+static int boxqp_solve(int n, const double* A, int lda, const double* b, const double* L, const double* U,
+                       double* x)
+{
+    static double K[OR_LCP_MAXN * OR_LCP_MAXN];
+    double g[OR_LCP_MAXN], c[OR_LCP_MAXN], d[OR_LCP_MAXN];
+    int fidx[OR_LCP_MAXN], ws[OR_LCP_MAXN]; /* ws: 0 free, 1 held at L, 2 held at U */
+    for (int r = 0; r < n; ++r) {
+        if (x[r] <= L[r]) { x[r] = L[r]; ws[r] = 1; }
+        else if (x[r] >= U[r]) { x[r] = U[r]; ws[r] = 2; }
+        else ws[r] = 0;
+        if (L[r] == U[r]) ws[r] = 1;
+    }
+    int at_min = 0;  /* the last step was a full Newton step: x minimises the working set */
+    for (int it = 0; it < 4 * n + 50; ++it) {
+        for (int r = 0; r < n; ++r) {
+            double acc = -b[r];
+            for (int e = 0; e < n; ++e) acc += A[r * lda + e] * x[e];
+            g[r] = acc;
+        }
+        int nf = 0;
+        for (int r = 0; r < n; ++r)
+            if (ws[r] == 0) fidx[nf++] = r;
+        /* Newton step on the free rows: A_FF d_F = -g_F */
+        for (int i = 0; i < nf; ++i) {
+            for (int j = 0; j < nf; ++j) K[i * nf + j] = A[fidx[i] * lda + fidx[j]];
+            c[i] = -g[fidx[i]];
+        }
+        double dn = 0.0;
+        if (nf > 0 && !at_min) {
+            if (!lcp_gauss(nf, K, c, d)) return -1;
+            for (int i = 0; i < nf; ++i) dn = fabs(d[i]) > dn ? fabs(d[i]) : dn;
+        }
+        double xm = 0.0;
+        for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
+        if (at_min || dn <= 1e-15 * (1.0 + xm)) {
+            at_min = 0;
+            /* minimiser on the working set: release the worst multiplier */
+            int worst = -1;
+            double wv = 0.0;
+            double gm = 0.0;
+            for (int r = 0; r < n; ++r) gm = fabs(g[r]) > gm ? fabs(g[r]) : gm;
+            const double tol = 1e-13 * (1.0 + gm);
+            for (int r = 0; r < n; ++r) {
+                if (L[r] == U[r]) continue;
+                const double v = (ws[r] == 1) ? -g[r] : ((ws[r] == 2) ? g[r] : 0.0);
+                if (v > tol && v > wv) { wv = v; worst = r; }
+            }
+            if (worst < 0) return it;
+            ws[worst] = 0;
+            continue;
+        }
+        /* longest feasible step along d (at most 1) */
+        double alpha = 1.0;
+        int block = -1, bside = 0;
+        for (int i = 0; i < nf; ++i) {
+            const int r = fidx[i];
+            if (d[i] < 0.0 && x[r] + d[i] < L[r]) {
+                const double a = (L[r] - x[r]) / d[i];
+                if (a < alpha) { alpha = a; block = r; bside = 1; }
+            } else if (d[i] > 0.0 && x[r] + d[i] > U[r]) {
+                const double a = (U[r] - x[r]) / d[i];
+                if (a < alpha) { alpha = a; block = r; bside = 2; }
+            }
+        }
+        if (alpha < 0.0) alpha = 0.0;
+        for (int i = 0; i < nf; ++i) x[fidx[i]] += alpha * d[i];
+        if (block >= 0) {
+            x[block] = (bside == 1) ? L[block] : U[block];
+            ws[block] = bside;
+        } else {
+            at_min = 1;
+        }
+    }
+    return -1;
+}
+
+/* Converged mode: staggered fixed point of the friction bounds.  With the
+ * boxes [-mu x_n, mu x_n] frozen at the current normal impulses the LCP is a
+ * strictly convex box QP (boxqp_solve, exact); the bounds are then updated
+ * from its normals until they stop moving.  At the fixed point x satisfies
+ * the complementarity conditions of the coupled boxed LCP (the fixed point
+ * PGS approaches).  Stats: sweeps + 1e6 x outer rounds; the final
+ * complementarity residual (velocity units). */
+static void lcp_refine(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
+                       const int* findex, double mu, double* x)
+{
+    double L[OR_LCP_MAXN], U[OR_LCP_MAXN], prev[OR_LCP_MAXN];
+    int round = 0, failed = 0;
+    for (; round < 100; ++round) {
+        for (int r = 0; r < n; ++r) row_bounds(r, lo, hi, findex, mu, x, &L[r], &U[r]);
+        for (int r = 0; r < n; ++r) {  /* a negative normal cannot occur: x_n >= 0 */
+            if (L[r] > U[r]) { const double t = L[r]; L[r] = U[r]; U[r] = t; }
+            prev[r] = x[r];
+        }
+        if (boxqp_solve(n, A, lda, b, L, U, x) < 0) { failed = 1; break; }
+        double dmax = 0.0, xm = 0.0;
+        for (int r = 0; r < n; ++r) {
+            dmax = fabs(x[r] - prev[r]) > dmax ? fabs(x[r] - prev[r]) : dmax;
+            xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
+        }
+        if (dmax <= 1e-14 * (1.0 + xm)) { ++round; break; }
+    }
+    double xm = 0.0;
+    for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
+    g_pgs_delta = lcp_residual(n, A, lda, b, lo, hi, findex, mu, x, 1e-12 * (1.0 + xm));
+    if (failed) g_pgs_delta = -1.0 - g_pgs_delta;
+    g_pgs_sweeps += 1000000 * round;
+}
+
 void or_pgs(int n, const double* A, const double* b, const double* lo,
             const double* hi, double* x, int iters)
 {
-    for (int it = 0; it < iters; ++it) {
+    g_pgs_sweeps = 0;
+    for (int it = 0; it < pgs_budget(iters); ++it) {
         for (int r = 0; r < n; ++r) {
             double s = b[r];
             for (int c = 0; c < n; ++c) s -= A[r * n + c] * x[c];
@@ -387,6 +599,12 @@ void or_pgs(int n, const double* A, const double* b, const double* lo,
             if (v > hi[r]) v = hi[r];
             x[r] = v;
         }
+        pgs_count(it);
+    }
+    if (iters < 0 && n <= OR_LCP_MAXN) {
+        int findex[OR_LCP_MAXN];
+        for (int r = 0; r < n; ++r) findex[r] = -1;
+        lcp_refine(n, A, n, b, lo, hi, findex, 0.0, x);
     }
 }
 
@@ -681,7 +899,8 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
         for (int r = 0; r < nr; ++r)
             for (int c = 0; c < nr; ++c) A[r][c] = dot6(J[r], MJ[c]);
         for (int r = 0; r < nr; ++r) { A[r][r] *= (1.0 + OR_C_CFM); x[r] = 0.0; }
-        for (int it = 0; it < pgs_iters; ++it)
+        g_pgs_sweeps = 0;
+        for (int it = 0; it < pgs_budget(pgs_iters); ++it) {
             for (int r = 0; r < nr; ++r) {
                 double acc = b[r];
                 for (int c = 0; c < nr; ++c) acc -= A[r][c] * x[c];
@@ -693,6 +912,18 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
                 if (v > hi) v = hi;
                 x[r] = v;
             }
+            pgs_count(it);
+        }
+        if (pgs_iters < 0) {
+            double lo[3 * OR_MAXCONTACTS], hi[3 * OR_MAXCONTACTS];
+            int findex[3 * OR_MAXCONTACTS];
+            for (int r = 0; r < nr; ++r) {
+                lo[r] = 0.0;
+                hi[r] = INFINITY;
+                findex[r] = (r % 3 == 0) ? -1 : r - r % 3;
+            }
+            lcp_refine(nr, &A[0][0], 3 * OR_MAXCONTACTS, b, lo, hi, findex, m->mu, x);
+        }
         for (int r = 0; r < nr; ++r)
             for (int k = 0; k < 6; ++k) V[k] += MJ[r][k] * x[r];
     }
@@ -1349,7 +1580,8 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
             A[r * nr + r] *= 1.0 + cfm[r];
             x[r] = 0.0;
         }
-        for (int it = 0; it < pgs_iters; ++it)
+        g_pgs_sweeps = 0;
+        for (int it = 0; it < pgs_budget(pgs_iters); ++it) {
             for (int r = 0; r < nr; ++r) {
                 double acc_r = bb[r];
                 for (int c = 0; c < nr; ++c) acc_r -= A[r * nr + c] * x[c];
@@ -1365,6 +1597,16 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                 if (v > u) v = u;
                 x[r] = v;
             }
+            pgs_count(it);
+        }
+        if (pgs_iters < 0) {
+            int findex[3 * OR_MAXFC + 3 * OR_MAXB];
+            for (int r = 0; r < nr; ++r) {
+                findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
+                if (kind[r] == K_NORMAL) { lo[r] = 0.0; hi[r] = INFINITY; }
+            }
+            lcp_refine(nr, A, nr, bb, lo, hi, findex, m->mu, x);
+        }
         for (int r = 0; r < nr; ++r)
             for (int e = 0; e < nv; ++e) nu[e] += MJ[r][e] * x[r];
     }

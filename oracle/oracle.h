@@ -80,9 +80,15 @@ int or_step(const or_model* m, double dt, double* q, double* qd,
             const int32_t* mode, const double* cmd, int pgs_iters,
             double* qdd_out, double* force_out);
 
-/* Boxed LCP by projected Gauss-Seidel (A row-major n*n). */
+/* Boxed LCP by projected Gauss-Seidel (A row-major n*n).  Every solver of
+ * this oracle takes a sweep budget: iters >= 0 runs exactly that many sweeps
+ * (the GPU kernels' count); iters < 0 (OR_PGS_CONVERGED) sweeps to the fixed
+ * point (largest change of a sweep <= 1e-13 (1 + max|x|)).  or_pgs_stats():
+ * sweeps and last change of the latest solve. */
+#define OR_PGS_CONVERGED (-1)
 void or_pgs(int n, const double* A, const double* b, const double* lo,
             const double* hi, double* x, int iters);
+void or_pgs_stats(int* sweeps, double* last_delta);
 
 /* Joint PID of the ScenarI/O JointController (Position / Velocity modes,
  * cpp/scenario/plugins/JointController/JointController.cpp:129-190). */

@@ -747,6 +747,16 @@ class FloatWorld:
         return nc
 
 
+PGS_CONVERGED = -1   # sweep budget: run the boxed LCP to its fixed point (oracle.h)
+
+
+def pgs_stats():
+    """(sweeps, last sweep's largest impulse change) of the latest LCP solve."""
+    n, d = ctypes.c_int(0), ctypes.c_double(0.0)
+    lib().or_pgs_stats(ctypes.byref(n), ctypes.byref(d))
+    return n.value, d.value
+
+
 def pgs(A, b, lo, hi, iters=100):
     A = np.ascontiguousarray(A, dtype=np.float64)
     b, lo, hi = (np.ascontiguousarray(x, dtype=np.float64) for x in (b, lo, hi))

@@ -332,6 +332,117 @@ def test_humanoid_standing_closed_loop_parity(require_gpu, oracle):
     sim.close()
 
 
+def test_humanoid_512_impacts_vs_converged_lcp(require_gpu, oracle):
+    """BASELINE config 5 at its full size (512 humanoid worlds, PGS 50, one
+    physics step per run) with varied starts: drops from up to 9 cm (impacts),
+    sliding base velocities, tilted bodies, joint offsets.  Joint torques come
+    from a host PD law on the GPU state (Force mode), so every step is
+    teacher-forced: a subset of worlds is restarted in the fp64 oracle from
+    the GPU state and stepped twice, with the kernel's truncated PGS (50
+    sweeps) and with the boxed LCP solved exactly (pyoracle.PGS_CONVERGED:
+    the solution DART's Dantzig solver returns [EXT]).  Stated bounds, per
+    quantity: the GPU against the same-algorithm oracle is fp32 round-off
+    (velocities 2e-3, positions 1e-5); against the exact LCP the GPU's error
+    must be the PGS-50 truncation (oracle PGS-50 vs exact on the same inputs)
+    plus that round-off, and the truncation stays within the contact
+    tolerance: positions 2e-4, velocities 0.15 at impacts."""
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    W, H, pgs = 512, 200, 50
+    rng = np.random.default_rng(21)
+    sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=pgs, pose=(0, 0, HUMANOID_Z, 1, 0, 0, 0))
+    assert sim.float_kernel() == 2
+    n = sim.dofs
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, HUMANOID_Z))
+    lo = np.array(cm.model.lower[:n])
+    hi = np.array(cm.model.upper[:n])
+    q0 = np.clip(rng.uniform(-0.1, 0.1, (W, n)), lo, hi)
+    axis = rng.normal(size=(W, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    ang = rng.uniform(0, 0.08, W)
+    quat = np.column_stack([np.cos(ang / 2), axis * np.sin(ang / 2)[:, None]])
+    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), rng.uniform(HUMANOID_Z, HUMANOID_Z + 0.09, W), quat])
+    vel = np.column_stack([rng.uniform(-0.8, 0.8, (W, 2)), rng.uniform(-0.5, 0.0, W), rng.uniform(-0.3, 0.3, (W, 3))])
+    sim.set("reset_q", q0)
+    sim.set("reset_qd", rng.uniform(-0.5, 0.5, (W, n)))
+    sim.reset_base_pose(pose)
+    sim.reset_base_velocity(vel)
+    sim.run(paused=True)
+    sim.set_control_mode(N.MODE_FORCE)
+    gains = np.array(_humanoid_gains(sim.joint_names))
+    mode = np.full(n, oracle.FORCE, np.int32)
+    subset = list(range(0, W, W // 16))
+    keys = ("pose", "q", "vel", "qd")
+    e50 = dict.fromkeys(keys, 0.0)
+    econv = dict.fromkeys(keys, 0.0)
+    trunc = dict.fromkeys(keys, 0.0)
+    in_contact = np.zeros(W, bool)
+    rounds, worst_res = 0, 0.0
+
+    def errs(p1, v1, q1, qd1, ow):
+        return dict(pose=max(float(np.abs(p1[:3] - ow.p).max()), float(np.abs(_quat_to_R(p1[3:]) - ow.R).max())),
+                    q=float(np.abs(q1 - ow.q).max()),
+                    vel=float(np.abs(v1 - np.concatenate([ow.R @ ow.V[3:], ow.R @ ow.V[:3]])).max()),
+                    qd=float(np.abs(qd1 - ow.qd).max()))
+
+    for k in range(H):
+        p0, v0, gq, gqd = sim.base_pose(), sim.base_velocity(), sim.get("q"), sim.get("qd")
+        tau = np.clip(-gains[:, 0] * gq - gains[:, 1] * gqd, -80.0, 80.0).astype(np.float32).astype(np.float64)
+        sim.set("force_target", tau)
+        refs = {}
+        for w in subset:
+            R0 = _quat_to_R(p0[w, 3:])
+            pair = []
+            for it in (pgs, oracle.PGS_CONVERGED):
+                ow = oracle.FloatWorld(cm, ground=True, mu=1.0, pgs_iters=it)
+                ow.set_pose(p0[w, :3], R0)
+                ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
+                ow.set_joints(gq[w], gqd[w])
+                ow.step(mode, tau[w])
+                if it < 0:
+                    # complementarity residual of the exact solve (m/s): round-off
+                    # level, far below the PGS-truncation figures compared here
+                    sweeps, res = oracle.pgs_stats()
+                    assert 0.0 <= res <= 1e-6, f"exact LCP not reached (world {w}, step {k}): residual {res}"
+                    rounds = max(rounds, sweeps // 1000000)
+                    worst_res = max(worst_res, res)
+                pair.append(ow)
+            refs[w] = pair
+        sim.run()
+        p1, v1, q1, qd1 = sim.base_pose(), sim.base_velocity(), sim.get("q"), sim.get("qd")
+        for w in subset:
+            in_contact[w] |= len(sim.contacts(w)) > 0
+        for w, (o50, oex) in refs.items():
+            a, b = errs(p1[w], v1[w], q1[w], qd1[w], o50), errs(p1[w], v1[w], q1[w], qd1[w], oex)
+            c = errs(np.concatenate([o50.p, [1, 0, 0, 0]]), np.concatenate([o50.R @ o50.V[3:], o50.R @ o50.V[:3]]),
+                     o50.q, o50.qd, oex)
+            c["pose"] = max(float(np.abs(o50.p - oex.p).max()), float(np.abs(o50.R - oex.R).max()))
+            for key in keys:
+                e50[key] = max(e50[key], a[key])
+                econv[key] = max(econv[key], b[key])
+                trunc[key] = max(trunc[key], c[key])
+    z = sim.base_pose()[:, 2]
+    fmt = lambda d: ", ".join(f"{k} {v:.2e}" for k, v in d.items())
+    print(f"humanoid32 x{W}, {H} teacher-forced steps, PGS {pgs}: GPU vs oracle PGS-{pgs}: {fmt(e50)}; "
+          f"GPU vs exact LCP: {fmt(econv)}; oracle PGS-{pgs} vs exact: {fmt(trunc)}; "
+          f"base z [{z.min():.3f}, {z.max():.3f}], exact LCP: max rounds {rounds}, max residual {worst_res:.1e}")
+    assert np.isfinite(sim.get("q")).all() and np.isfinite(sim.base_pose()).all()
+    assert z.min() > 0.3 and sim.constraint_overflow() == 0
+    assert in_contact[subset].all()
+    assert e50["pose"] <= 1e-5 and e50["q"] <= 1e-5 and e50["vel"] <= 2e-3 and e50["qd"] <= 2e-3
+    # the GPU's distance to the exact LCP is the PGS truncation (oracle PGS-50
+    # vs exact, same inputs) plus fp32 round-off -- nothing else
+    for key in keys:
+        assert econv[key] <= trunc[key] + 2 * e50[key] + 1e-7, key
+    # and the truncation itself stays within the stated contact tolerance
+    # (measured r02: pose 1.5e-5, q 7.0e-5, vel 1.5e-2, qd 7.0e-2)
+    assert econv["pose"] <= 5e-5 and econv["q"] <= 2e-4 and econv["vel"] <= 5e-2 and econv["qd"] <= 0.15
+    sim.close()
+
+
 def test_wave_run_device_equals_run(require_gpu):
     from mwstep import get_model_file
     from mwstep import native as N

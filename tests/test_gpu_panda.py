@@ -10,10 +10,10 @@ Position (PID) control, on the HIP scenario kernel.
   * teacher-forced one-step parity against the fp64 oracle
     (pyoracle.ScenarioWorld: JointController PID + tree ABA + limit rows) over
     many worlds with random states / targets: fp32 vs fp64, <= 1e-5 rad on q
-    and <= 1e-3 rad/s on qd (PID gains up to 10^4 amplify the fp32 rounding of
-    the error term; the bound is stated per quantity);
+    and <= 1e-4 rad/s on qd (the north star's observation bound);
   * free-running parity of a PID tracking run (H = 500) against the oracle,
-    <= 5e-4 rad;
+    <= 1e-4 rad (the joint positions are integrated compensated, q = q_hi +
+    qlo, so the PID's d/dt gain does not amplify the float32 rounding of q);
   * controller-period gating and Velocity-mode PID against the oracle.
 """
 
@@ -166,13 +166,13 @@ def test_one_step_parity_position_pid(require_gpu, oracle, panda_file):
         wq = max(wq, float(np.abs(gq[w] - ow.q).max()))
         wqd = max(wqd, float(np.abs(gqd[w] - ow.qd).max()))
     print(f"panda one-step: max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
-    assert wq <= 1e-5 and wqd <= 1e-3   # measured r01: 1.3e-7 / 4.2e-5
+    assert wq <= 1e-5 and wqd <= 1e-4   # measured r01: 1.3e-7 / 4.2e-5
     sim.close()
 
 
 def test_free_running_tracking_parity(require_gpu, oracle, panda_file):
     """8 worlds, 500 steps of sinusoidal targets on joints 1 and 6: the PID
-    feedback keeps fp32 and fp64 trajectories within 1e-3 rad."""
+    feedback keeps fp32 and fp64 trajectories within 1e-4 rad."""
     W, H = 8, 500
     cm = oracle.load_urdf(panda_file)
     n = cm.n
@@ -200,7 +200,7 @@ def test_free_running_tracking_parity(require_gpu, oracle, panda_file):
             ows[w].run()
             worst = max(worst, float(np.abs(gq[w] - ows[w].q).max()))
     print(f"panda free-running H={H}: max|dq| {worst:.2e}")
-    assert worst <= 5e-4   # measured r01: 4.1e-5
+    assert worst <= 1e-4   # measured r01: 4.1e-5
     sim.close()
 
 
@@ -277,7 +277,7 @@ def test_panda_vecenv_reset(require_gpu, oracle, panda_file):
 
 def test_panda_vecenv_vs_oracle(require_gpu, oracle, panda_file):
     """Free-running PandaPositionTracking vs per-world oracle ScenarioWorlds
-    (same start state, PID gains, period = dt): obs within 5e-4, reward
+    (same start state, PID gains, period = dt): obs within 1e-4, reward
     within 1e-5 relative; TimeLimit auto-reset at step 150."""
     import torch
     from mwstep.vecenv import VecEnv
@@ -323,14 +323,16 @@ def test_panda_vecenv_vs_oracle(require_gpu, oracle, panda_file):
                 worst_o = max(worst_o, float(np.abs(o[w] - ref_obs).max()))
             worst_r = max(worst_r, abs(r[w] - ref_r) / (1.0 + abs(ref_r)))
     print(f"PandaPositionTracking vs oracle, H={H}: max|obs err| {worst_o:.2e}, reward rel err {worst_r:.2e}")
-    assert worst_o <= 5e-4 and worst_r <= 1e-4
+    # measured r01 1.5e-4 (joint 6 qd: the d/dt gain on the float32 rounding of
+    # q); r02, compensated q: 2.9e-5
+    assert worst_o <= 1e-4 and worst_r <= 1e-4
     env.close()
 
 
 def test_panda_baked_matches_generic(require_gpu, monkeypatch):
     """The constant-folded Panda kernel against the generic one on the same
     inputs (rounding differs; the high-gain PID feedback carries it): obs within
-    5e-4 after 300 tracking steps (measured r01: 1.5e-4, the same size as the
+    1e-4 after 300 tracking steps (measured r01: 1.5e-4, the same size as the
     fp32-vs-fp64 drift of test_panda_vecenv_vs_oracle)."""
     import torch
     from mwstep.vecenv import VecEnv
@@ -352,6 +354,6 @@ def test_panda_baked_matches_generic(require_gpu, monkeypatch):
         worst = max(worst, float((oa - ob).abs().max()))
     monkeypatch.delenv("MWSTEP_DISABLE_BAKED", raising=False)
     print(f"panda baked vs generic, H={H}: max|obs diff| {worst:.2e}")
-    assert worst <= 5e-4
+    assert worst <= 1e-4
     a.close()
     b.close()

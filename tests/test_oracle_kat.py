@@ -181,3 +181,32 @@ def test_pgs_matches_exact_boxed_lcp(oracle):
         lo[rng.uniform(size=n) < 0.3] = 0.0
         x = oracle.pgs(A, b, lo, hi, iters=400)
         np.testing.assert_allclose(x, _lcp_exact(A, b, lo, hi), atol=1e-8)
+
+
+def test_converged_lcp_mode_is_exact(oracle):
+    """The oracle's converged mode (sweep budget PGS_CONVERGED, the reference
+    for the kernels' truncated PGS): box LCPs against exhaustive enumeration,
+    and the friction-coupled contact LCP of a humanoid drop reaches the
+    complementarity conditions to round-off at every step."""
+    from mwstep import get_model_file
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        n = rng.integers(1, 6)
+        B = rng.normal(size=(n, n))
+        A = B @ B.T + 0.05 * np.eye(n)
+        b = rng.normal(size=n)
+        lo = -rng.uniform(0.05, 1.0, size=n)
+        hi = rng.uniform(0.05, 1.0, size=n)
+        lo[rng.uniform(size=n) < 0.3] = 0.0
+        x = oracle.pgs(A, b, lo, hi, iters=oracle.PGS_CONVERGED)
+        np.testing.assert_allclose(x, _lcp_exact(A, b, lo, hi), atol=1e-9)
+    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.6))
+    ow = oracle.FloatWorld(cm, pgs_iters=oracle.PGS_CONVERGED)
+    ow.set_twist([0.3, 0.0, 0.2], [0.5, -0.3, -0.5])
+    mode = np.full(cm.n, oracle.FORCE, np.int32)
+    n_contact = 0
+    for _ in range(150):
+        n_contact = max(n_contact, ow.step(mode, np.clip(-500 * ow.q - 5 * ow.qd, -80, 80)))
+        sweeps, res = oracle.pgs_stats()
+        assert 0.0 <= res <= 1e-9
+    assert n_contact >= 4
