@@ -1,0 +1,1032 @@
+// scene_kernel.hip -- one engine step of a SCENE (several models in one world:
+// World::insertModel, cpp/scenario/gazebo/src/World.cpp:394-420), ONE WORLD
+// PER WAVEFRONT.  Same physics as oracle.c or_scene_step (DART 6 World::step
+// restated [EXT]: ABA with implicit damping, v-integration, one boxed LCP over
+// every contact and joint row, impulse velocities, p-integration), the
+// mapping of wave_tree.hpp generalised from one floating tree to a forest:
+//
+//   nodes            lane = node: the model bases (fixed or floating) and
+//                    every body; the level-parallel ABA walks the forest by
+//                    depth (bases are level 0), child -> parent sums through
+//                    per-node LDS accumulators one sibling rank at a time
+//                    (deterministic); a floating base solves its 6x6
+//                    articulated inertia on its own lane (Cholesky, kept in
+//                    LDS for the impulse responses); a welded base does not
+//                    move.
+//   wrenches         Link::applyWorldWrench (Link.cpp:484-560) records with an
+//                    expiry iteration (Physics.cpp:1446-1525): the active
+//                    ones enter the node's bias force, body frame.
+//   contacts         lane = ground slot (box corners, sphere bottoms under
+//                    z = 0), then lane = shape pair of two models (box-box
+//                    SAT + face clipping / edge-edge, box-sphere,
+//                    sphere-sphere: the restatement of oracle.c or_collide);
+//                    points compacted in (slot, pair, point) order.
+//   rows             contact rows (normal + 2 friction directions, ODE
+//                    dPlaneSpace) then joint rows (limit / servo / Coulomb);
+//                    lane = row responses M^-1 J^T: the two bodies of a
+//                    contact each walk their path to their base, floating
+//                    bases solve through the stored factor, then the outward
+//                    pass over that model's bodies.
+//   Delassus / PGS   A = J (M^-1 J^T)^T in LDS (lane = column); projected
+//                    Gauss-Seidel in row order (the oracle's), lane c owning
+//                    rows c and c + 64: residual w_c, impulse x_c; one row
+//                    update = two lane reads, a clamp and one FMA per lane.
+#include <hip/hip_runtime.h>
+
+#include "free_body.hpp"
+#include "kernels.hpp"
+#include "pid.hpp"
+#include "scene_params.hpp"
+#include "wave_tree.hpp"
+
+namespace mw {
+namespace dev {
+
+// per-node record (41 words, odd: lane-strided parent gathers are conflict-free)
+struct ScNode {
+    M3 R;        // joint transform parent -> node (bases: unused)
+    f3 p;
+    SV U;        // AI S (impulse inertia)
+    float psi;
+    float tt;
+    SV V;        // velocity, then acceleration
+    M3 Rw;       // world pose
+    f3 pw;
+    int32_t depth;
+    float pad_[2];
+};
+static_assert(sizeof(ScNode) == 41 * 4, "ScNode layout");
+
+template <int MAXNV>
+struct ScWorld {
+    static constexpr int kStride = MAXNV + 1;     // odd: lane-strided rows are conflict-free
+    static constexpr int kAStride = kScMaxRows + 1;
+    ScNode node[kScMaxNodes];
+    WaveAcc acc[kScMaxNodes];
+    float l0[kScMaxModels][28];   // Chol6 (l[21], id[6]) of every floating base
+    float q[kScMaxBodies], qd[kScMaxBodies], qdd[kScMaxBodies], tau[kScMaxBodies], vc[kScMaxBodies];
+    uint32_t act[kScMaxBodies];
+    float nu[MAXNV];
+    float J[kScMaxRows][kStride];
+    float MJ[kScMaxRows][kStride];
+    float A[kScMaxRows][kAStride];
+    F4 rc[kScMaxRows];            // {b, 1/A_rr, lo, hi}
+    int32_t src[kScMaxRows];      // contact rows 3 c + d; joint rows kJointRow + 3 body + type
+    float rb[kScMaxRows], rlo[kScMaxRows], rhi[kScMaxRows];
+    float c_p[kScMaxContacts][3], c_n[kScMaxContacts][3], c_t1[kScMaxContacts][3], c_t2[kScMaxContacts][3];
+    float c_d[kScMaxContacts];
+    int32_t c_na[kScMaxContacts], c_nb[kScMaxContacts];
+    float c_x[kScMaxContacts][3];
+    float stack[kScMaxDepth][7][kWaveLanes];
+};
+
+// ODE dPlaneSpace (oracle.c plane_space), float32
+__device__ __forceinline__ void plane_space_f(f3 n, f3& p, f3& q) {
+    if (fabsf(n.z) > 0.70710678f) {
+        const float a = n.y * n.y + n.z * n.z, k = rsqrtf(a);
+        p = {0.f, -n.z * k, n.y * k};
+        q = {a * k, -n.x * p.z, n.x * p.y};
+    } else {
+        const float a = n.x * n.x + n.y * n.y, k = rsqrtf(a);
+        p = {-n.y * k, n.x * k, 0.f};
+        q = {-n.z * p.y, n.z * p.x, a * k};
+    }
+}
+
+__device__ __forceinline__ f3 col(const M3& R, int k) { return {R.m[k], R.m[3 + k], R.m[6 + k]}; }
+__device__ __forceinline__ M3 mul3(const M3& A, const M3& B) {
+    M3 C;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) C.m[r * 3 + c] = A.m[r * 3] * B.m[c] + A.m[r * 3 + 1] * B.m[3 + c] + A.m[r * 3 + 2] * B.m[6 + c];
+    return C;
+}
+
+// ---------------------------------------------------------------- narrow phase
+// Restatement of oracle.c box_box / box_sphere / or_collide in float32 (same
+// axis order, tie rules, clipping order and point reduction).
+
+__device__ __forceinline__ int sc_reduce(int n, f3* p, float* d) {
+    if (n <= 4) return n;
+    int a = 0;
+    for (int i = 1; i < n; ++i) if (d[i] > d[a]) a = i;
+    uint32_t used = 1u << a;
+    int b = -1;
+    float best = -1.f;
+    for (int i = 0; i < n; ++i) {
+        if ((used >> i) & 1u) continue;
+        const f3 e = p[i] - p[a];
+        const float v = dot(e, e);
+        if (v > best) { best = v; b = i; }
+    }
+    used |= 1u << b;
+    int c = -1;
+    best = -1.f;
+    const f3 ab = p[b] - p[a];
+    for (int i = 0; i < n; ++i) {
+        if ((used >> i) & 1u) continue;
+        const f3 x = cross(ab, p[i] - p[a]);
+        const float v = dot(x, x);
+        if (v > best) { best = v; c = i; }
+    }
+    used |= 1u << c;
+    const f3 g = (1.f / 3.f) * (p[a] + p[b] + p[c]);
+    int e4 = -1;
+    best = -1.f;
+    for (int i = 0; i < n; ++i) {
+        if ((used >> i) & 1u) continue;
+        const f3 e = p[i] - g;
+        const float v = dot(e, e);
+        if (v > best) { best = v; e4 = i; }
+    }
+    used |= 1u << e4;
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        if ((used >> i) & 1u) { p[m] = p[i]; d[m] = d[i]; ++m; }
+    return 4;
+}
+
+__device__ __forceinline__ int sc_box_box(f3 hA, f3 cA, const M3& RA, f3 hB, f3 cB, const M3& RB, f3& n, f3* pts,
+                                          float* deps) {
+    f3 a[3] = {col(RA, 0), col(RA, 1), col(RA, 2)};
+    f3 b[3] = {col(RB, 0), col(RB, 1), col(RB, 2)};
+    const float ha[3] = {hA.x, hA.y, hA.z}, hb[3] = {hB.x, hB.y, hB.z};
+    const f3 T = cB - cA;
+    float best_face = 3.0e38f, best_edge = 3.0e38f;
+    int face = -1, ei = -1, ej = -1;
+    f3 eaxis = {0.f, 0.f, 0.f};
+    for (int k = 0; k < 6; ++k) {
+        const f3 L = k < 3 ? a[k] : b[k - 3];
+        float rA = 0.f, rB = 0.f;
+        for (int i = 0; i < 3; ++i) { rA += ha[i] * fabsf(dot(a[i], L)); rB += hb[i] * fabsf(dot(b[i], L)); }
+        const float pen = rA + rB - fabsf(dot(T, L));
+        if (pen < 0.f) return 0;
+        if (pen < best_face) { best_face = pen; face = k; }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            f3 L = cross(a[i], b[j]);
+            const float len = sqrtf(dot(L, L));
+            if (len < 1e-6f) continue;
+            L = (1.f / len) * L;
+            float rA = 0.f, rB = 0.f;
+            for (int k = 0; k < 3; ++k) { rA += ha[k] * fabsf(dot(a[k], L)); rB += hb[k] * fabsf(dot(b[k], L)); }
+            const float pen = rA + rB - fabsf(dot(T, L));
+            if (pen < 0.f) return 0;
+            if (pen < best_edge) { best_edge = pen; ei = i; ej = j; eaxis = L; }
+        }
+    if (ei >= 0 && best_edge < 0.95f * best_face - 1e-5f) {
+        f3 L = eaxis;
+        if (dot(L, T) > 0.f) L = -L;
+        n = L;
+        f3 pa = cA, pb = cB;
+        for (int k = 0; k < 3; ++k) {
+            if (k != ei) pa = pa + ((dot(a[k], n) > 0.f ? -1.f : 1.f) * ha[k]) * a[k];
+            if (k != ej) pb = pb + ((dot(b[k], n) > 0.f ? 1.f : -1.f) * hb[k]) * b[k];
+        }
+        const f3 u = a[ei], v = b[ej];
+        const f3 w0 = pa - pb;
+        const float uv = dot(u, v), uw = dot(u, w0), vw = dot(v, w0);
+        const float den = 1.f - uv * uv;
+        float s = den > 1e-12f ? (uv * vw - uw) / den : 0.f;
+        float t = den > 1e-12f ? (vw - uv * uw) / den : 0.f;
+        s = fminf(fmaxf(s, -ha[ei]), ha[ei]);
+        t = fminf(fmaxf(t, -hb[ej]), hb[ej]);
+        pts[0] = 0.5f * ((pa + s * u) + (pb + t * v));
+        deps[0] = best_edge;
+        return 1;
+    }
+    const bool refA = face < 3;
+    const int fk = refA ? face : face - 3;
+    const f3 cR = refA ? cA : cB, cI = refA ? cB : cA;
+    const float* hR = refA ? ha : hb;
+    const float* hI = refA ? hb : ha;
+    const f3* R = refA ? a : b;
+    const f3* I = refA ? b : a;
+    f3 nr = R[fk];
+    if (dot(nr, cI - cR) < 0.f) nr = -nr;
+    n = refA ? -nr : nr;
+    int ik = 0;
+    float bd = 0.f;
+    for (int k = 0; k < 3; ++k) {
+        const float d = fabsf(dot(I[k], nr));
+        if (d > bd) { bd = d; ik = k; }
+    }
+    const float sg = dot(I[ik], nr) > 0.f ? -1.f : 1.f;
+    const int k1 = (ik + 1) % 3, k2 = (ik + 2) % 3;
+    const int u1 = (fk + 1) % 3, u2 = (fk + 2) % 3;
+    const f3 fc = cR + hR[fk] * nr;
+    // polygon: (u, v, x, y, z) per vertex, clipped in place (at most 8 vertices)
+    float poly[2][8][5];
+    const float sx[4] = {1.f, -1.f, -1.f, 1.f}, sy[4] = {1.f, 1.f, -1.f, -1.f};
+    for (int q = 0; q < 4; ++q) {
+        const f3 x = cI + (sg * hI[ik]) * I[ik] + (sx[q] * hI[k1]) * I[k1] + (sy[q] * hI[k2]) * I[k2];
+        const f3 rel = x - fc;
+        poly[0][q][0] = dot(rel, R[u1]);
+        poly[0][q][1] = dot(rel, R[u2]);
+        poly[0][q][2] = x.x; poly[0][q][3] = x.y; poly[0][q][4] = x.z;
+    }
+    int cnt = 4, cur = 0;
+    for (int plane = 0; plane < 4 && cnt > 0; ++plane) {
+        const int axis = plane >> 1;
+        const float s2 = (plane & 1) ? -1.f : 1.f;
+        const float h = axis ? hR[u2] : hR[u1];
+        int m = 0;
+        for (int i = 0; i < cnt; ++i) {
+            const float* P = poly[cur][i];
+            const float* Q = poly[cur][(i + 1) % cnt];
+            const float dp = s2 * P[axis] - h, dq = s2 * Q[axis] - h;
+            if (dp <= 0.f && m < 8) {
+                for (int k = 0; k < 5; ++k) poly[cur ^ 1][m][k] = P[k];
+                ++m;
+            }
+            if (((dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f)) && m < 8) {
+                const float t = dp / (dp - dq);
+                for (int k = 0; k < 5; ++k) poly[cur ^ 1][m][k] = P[k] + t * (Q[k] - P[k]);
+                ++m;
+            }
+        }
+        cnt = m;
+        cur ^= 1;
+    }
+    f3 P8[8];
+    float D8[8];
+    int np = 0;
+    for (int i = 0; i < cnt; ++i) {
+        const f3 x = {poly[cur][i][2], poly[cur][i][3], poly[cur][i][4]};
+        const float dep = dot(fc - x, nr);
+        if (dep > 0.f && np < 8) { P8[np] = x; D8[np] = dep; ++np; }
+    }
+    np = sc_reduce(np, P8, D8);
+    for (int i = 0; i < np; ++i) { pts[i] = P8[i]; deps[i] = D8[i]; }
+    return np;
+}
+
+__device__ __forceinline__ int sc_box_sphere(f3 h, f3 c, const M3& R, float rad, f3 s, f3& nbs, f3& pt, float& dep) {
+    const f3 l = mulT(R, s - c);
+    const f3 q = {fminf(fmaxf(l.x, -h.x), h.x), fminf(fmaxf(l.y, -h.y), h.y), fminf(fmaxf(l.z, -h.z), h.z)};
+    const bool inside = q.x == l.x && q.y == l.y && q.z == l.z;
+    if (!inside) {
+        f3 e = l - q;
+        const float dist = sqrtf(dot(e, e));
+        if (dist > rad) return 0;
+        e = (1.f / dist) * e;
+        nbs = mul(R, e);
+        pt = c + mul(R, q);
+        dep = rad - dist;
+        return 1;
+    }
+    const float g[3] = {h.x - fabsf(l.x), h.y - fabsf(l.y), h.z - fabsf(l.z)};
+    int kk = 0;
+    if (g[1] < g[kk]) kk = 1;
+    if (g[2] < g[kk]) kk = 2;
+    const float lk = kk == 0 ? l.x : (kk == 1 ? l.y : l.z);
+    const float sg = lk >= 0.f ? 1.f : -1.f;
+    f3 lq = l;
+    if (kk == 0) lq.x = sg * h.x; else if (kk == 1) lq.y = sg * h.y; else lq.z = sg * h.z;
+    nbs = sg * col(R, kk);
+    pt = c + mul(R, lq);
+    dep = rad + g[kk];
+    return 1;
+}
+
+// shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius):
+// normal from B into A, up to 4 points / depths
+__device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, int tb, f3 sb, f3 cb, const M3& Rb,
+                                          f3& n, f3* pts, float* deps) {
+    if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, pts, deps);
+    if (ta == 1 && tb == 1) {
+        const f3 d = ca - cb;
+        const float dist = sqrtf(dot(d, d));
+        const float pen = sa.x + sb.x - dist;
+        if (pen < 0.f || dist < 1e-12f) return 0;
+        n = (1.f / dist) * d;
+        pts[0] = cb + (sb.x - 0.5f * pen) * n;
+        deps[0] = pen;
+        return 1;
+    }
+    f3 nbs;
+    if (ta == 0) {
+        if (!sc_box_sphere(sa, ca, Ra, sb.x, cb, nbs, pts[0], deps[0])) return 0;
+        n = -nbs;
+        return 1;
+    }
+    if (!sc_box_sphere(sb, cb, Rb, sa.x, ca, nbs, pts[0], deps[0])) return 0;
+    n = nbs;
+    return 1;
+}
+
+// exclusive prefix over the wave of per-lane counts in [0, 7]
+__device__ __forceinline__ int wave_prefix7(int v, int& total) {
+    const uint64_t lt = (uint64_t{1} << lane_id()) - 1u;
+    int pre = 0;
+    total = 0;
+#pragma unroll
+    for (int bit = 0; bit < 3; ++bit) {
+        const uint64_t m = __ballot((v >> bit) & 1);
+        pre += (1 << bit) * __popcll(m & lt);
+        total += (1 << bit) * __popcll(m);
+    }
+    return pre;
+}
+
+// ------------------------------------------------------------------ responses
+// Response of the row in MJ / J (accumulated) to a spatial impulse f on node k
+// (k < K: a base) or, with k = -1, to a unit impulse on body j's joint; returns
+// J nu.  Same passes as wave_response, restricted to k's model.
+template <int MAXNV>
+__device__ __forceinline__ float sc_response(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, int k, int j, SV f,
+                                             float* __restrict__ Jrow, float* __restrict__ MJrow) {
+    const int lane = lane_id();
+    const int m = (k >= 0) ? P->node_model[k] : P->body_model[j];
+    const SceneModelF& md = P->model[m];
+    const int start = (k >= 0) ? P->node_body[k] : j;
+    const uint64_t path = (start >= 0) ? P->body_path[start] : uint64_t{0};
+    SV Bi = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Fi = Bi;
+    if (k >= 0) { Bi = -1.f * f; Fi = f; }
+    float jv = 0.f;
+    for (uint64_t mm = path; mm != 0;) {
+        const int i = 63 - __builtin_clzll(mm);
+        mm &= ~(uint64_t{1} << i);
+        const BodyF& b = P->b[i];
+        const ScNode& s = L.node[P->body_node[i]];
+        const int c = P->body_coord[i];
+        const float ji = proj(b, Fi);
+        Jrow[c] += ji;
+        jv += ji * L.nu[c];
+        const float u = ((i == j) ? 1.f : 0.f) - proj(b, Bi);
+        L.stack[s.depth - 1][6][lane] = u;
+        Bi = dad_inv(s.R, s.p, Bi + (s.psi * u) * s.U);
+        Fi = dad_inv(s.R, s.p, Fi);
+    }
+    SV dV0 = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    if (md.floating) {
+        const int o = md.coff;
+        const float fb[6] = {Fi.w.x, Fi.w.y, Fi.w.z, Fi.v.x, Fi.v.y, Fi.v.z};
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+            Jrow[o + e] += fb[e];
+            jv += fb[e] * L.nu[o + e];
+        }
+        Chol6 L0;
+#pragma unroll
+        for (int e = 0; e < 21; ++e) L0.l[e] = L.l0[m][e];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) L0.id[e] = L.l0[m][21 + e];
+        dV0 = L0.solve(-1.f * Bi);
+        const float dv[6] = {dV0.w.x, dV0.w.y, dV0.w.z, dV0.v.x, dV0.v.y, dV0.v.z};
+#pragma unroll
+        for (int e = 0; e < 6; ++e) MJrow[o + e] += dv[e];
+    }
+    SV dv_prev = dV0;
+    const int i0 = md.body0, i1 = md.body0 + md.n_bodies;
+    for (int i = i0; i < i1; ++i) {
+        const BodyF& b = P->b[i];
+        const ScNode& s = L.node[P->body_node[i]];
+        const int pa = b.parent;
+        SV dvp_in;
+        if (pa == i - 1 && i > i0) {
+            dvp_in = dv_prev;
+        } else if (pa >= 0) {
+            const int dp = L.node[P->body_node[pa]].depth - 1;
+            dvp_in = {{L.stack[dp][0][lane], L.stack[dp][1][lane], L.stack[dp][2][lane]},
+                      {L.stack[dp][3][lane], L.stack[dp][4][lane], L.stack[dp][5][lane]}};
+        } else {
+            dvp_in = dV0;
+        }
+        const SV dvp = ad_inv(s.R, s.p, dvp_in);
+        const float u = ((path >> i) & 1u) ? L.stack[s.depth - 1][6][lane] : 0.f;
+        const float mmv = s.psi * (u - dot(s.U, dvp));
+        MJrow[P->body_coord[i]] += mmv;
+        const SV dv = dvp + motion(b, mmv);
+        dv_prev = dv;
+        float* st = &L.stack[s.depth - 1][0][lane];
+        st[0 * kWaveLanes] = dv.w.x; st[1 * kWaveLanes] = dv.w.y; st[2 * kWaveLanes] = dv.w.z;
+        st[3 * kWaveLanes] = dv.v.x; st[4 * kWaveLanes] = dv.v.y; st[5 * kWaveLanes] = dv.v.z;
+    }
+    return jv;
+}
+
+// joint force of body d on substep s (dof_force with the model's PID gate)
+__device__ __forceinline__ float sc_dof_force(const SceneF* __restrict__ P, const SceneDev& S,
+                                              const PidF* __restrict__ pid, const SceneGates& G, int W, int w,
+                                              const SceneArgs& A, int s, int d, uint32_t act, float cmd, float vc,
+                                              float q, float qd) {
+    const float e = P->b[d].effort;
+    float tau = (act == kActForce && s == 0) ? fminf(fmaxf(cmd, -e), e) : 0.f;
+    if (act >= kActPidPos) {
+        const size_t k = static_cast<size_t>(d) * W + w;
+        float u = S.pid_u[k];
+        if ((G.gate[P->body_model[d]] >> s) & 1u) {
+            const float err = (act == kActPidPos) ? (q - S.ptgt[k]) : (qd - vc);
+            float el = S.pid_e[k], ie = S.pid_i[k];
+            if (pid_update(pid[d], err, A.inv_dt, A.dt, el, ie, u)) {
+                S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
+            } else {
+                u = 0.f;
+            }
+        }
+        tau = fminf(fmaxf(u, -e), e);
+    }
+    return tau;
+}
+
+// ------------------------------------------------------------------- step
+template <int MAXNV>
+__device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeState& base, uint32_t present,
+                        const float (&wr)[kScWrenchSlots][6], const int32_t (&wl)[kScWrenchSlots], int iter,
+                        float dt, int pgs_iters, int& nc_out, int& ovf) {
+    const int lane = lane_id();
+    const int NB = P->n_bodies, NV = P->nv;
+    const bool isnode = lane < P->n_nodes;
+    const int nbody = isnode ? P->node_body[lane] : -1;
+    const bool isbase = isnode && nbody < 0;
+    const bool isbody = isnode && nbody >= 0;
+    const int bi = isbody ? nbody : 0;
+    const int m = isnode ? P->node_model[lane] : 0;
+    const bool alive = isnode && ((present >> m) & 1u);
+    const SceneModelF& md = P->model[m];
+    const BodyF b = P->b[bi];
+    const int depth = alive ? P->node_depth[lane] : -1;
+    const int srank = P->node_srank[lane];
+    const int pnode = isbody ? (b.parent >= 0 ? P->body_node[b.parent] : md.node0) : 0;
+    const int levels = P->levels, fanout = P->fanout;
+    const f3 gw = mk(P->g[0], P->g[1], P->g[2]);
+    const bool dual = P->dual != 0;
+    // external wrench of this node at this iteration (world force at the
+    // origin, world torque), summed over the active records
+    f3 Fw = {0.f, 0.f, 0.f}, Tw = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < kScWrenchSlots; ++k)
+        if (wl[k] >= iter) {
+            Fw = Fw + mk(wr[k][0], wr[k][1], wr[k][2]);
+            Tw = Tw + mk(wr[k][3], wr[k][4], wr[k][5]);
+        }
+    if (lane < kScMaxNodes) L.acc[lane] = WaveAcc{};
+    M3 R, Rw;
+    f3 p, pw;
+    SV V, eta, B;
+    const M3 Rb0 = md.floating ? quat_to_R(base.qw, base.qx, base.qy, base.qz)
+                               : M3{{md.R0[0], md.R0[1], md.R0[2], md.R0[3], md.R0[4], md.R0[5], md.R0[6], md.R0[7], md.R0[8]}};
+    // ---- outward: kinematics, velocities, bias forces
+    for (int d = 0; d < levels; ++d) {
+        if (depth == d) {
+            if (isbase) {
+                Rw = Rb0;
+                pw = md.floating ? base.p : mk(md.p0[0], md.p0[1], md.p0[2]);
+                V = md.floating ? base.V : SV{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+                B = rigid_bias(md.mass, mk(md.com[0], md.com[1], md.com[2]),
+                               Sy{md.Io[0], md.Io[1], md.Io[2], md.Io[3], md.Io[4], md.Io[5]}, V, mulT(Rw, gw));
+                R = Rw;
+                p = pw;
+                eta = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+            } else {
+                joint_pose(b, L.q[bi], R, p);
+                const SV Sq = motion(b, L.qd[bi]);
+                const ScNode& pn = L.node[pnode];
+                V = ad_inv(R, p, pn.V) + Sq;
+                Rw = mul3(pn.Rw, R);
+                pw = pn.pw + mul(pn.Rw, p);
+                eta = {cross(V.w, Sq.w), cross(V.w, Sq.v) + cross(V.v, Sq.w)};
+                B = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), V, mulT(Rw, gw));
+            }
+            B = B + (-1.f) * SV{mulT(Rw, Tw), mulT(Rw, Fw)};
+            L.node[lane].V = V;
+            L.node[lane].Rw = Rw;
+            L.node[lane].pw = pw;
+        }
+    }
+    float tau = 0.f, qdi = 0.f;
+    if (isbody && alive) { tau = L.tau[bi]; qdi = L.qd[bi]; }
+    // ---- inward, deepest level first
+    SV U = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Un = U;
+    float psi = 0.f, tt = 0.f, psin = 0.f;
+    for (int d = levels - 1; d >= 1; --d) {
+        const bool mine = (depth == d);
+        SI c, cn;
+        SV cb;
+        if (mine) {
+            SI AI = rigid(b, b.mass);
+            AI += L.acc[lane].I;
+            const SV Bt = B + L.acc[lane].B;
+            U = ais(AI, b);
+            psi = rcp(proj(b, U) + dt * b.damping);
+            const SV AIeta = mul(AI, eta);
+            tt = tau - b.damping * qdi - proj(b, AIeta + Bt);
+            c = to_parent(R, p, downdate(AI, U, psi));
+            cb = dad_inv(R, p, Bt + AIeta + (psi * tt) * U);
+            if (dual) {
+                SI AIn = rigid(b, b.mass);
+                AIn += L.acc[lane].In;
+                Un = ais(AIn, b);
+                psin = rcp(proj(b, Un));
+                cn = to_parent(R, p, downdate(AIn, Un, psin));
+            }
+        }
+        for (int k = 0; k < fanout; ++k) {
+            if (mine && srank == k) {
+                WaveAcc& acc = L.acc[pnode];
+                SI I = acc.I;
+                I += c;
+                acc.I = I;
+                acc.B = acc.B + cb;
+                if (dual) {
+                    SI In = acc.In;
+                    In += cn;
+                    acc.In = In;
+                }
+            }
+        }
+    }
+    // ---- floating bases: a0 = -IA0^-1 B0 on the base's own lane
+    SV a0 = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    if (isbase && alive && md.floating) {
+        SI IA0;
+        IA0.A = {md.Io[0], md.Io[1], md.Io[2], md.Io[3], md.Io[4], md.Io[5]};
+        const float mm = md.mass, cx = md.com[0], cy = md.com[1], cz = md.com[2];
+        IA0.B.m[0] = 0.f;      IA0.B.m[1] = -mm * cz; IA0.B.m[2] = mm * cy;
+        IA0.B.m[3] = mm * cz;  IA0.B.m[4] = 0.f;      IA0.B.m[5] = -mm * cx;
+        IA0.B.m[6] = -mm * cy; IA0.B.m[7] = mm * cx;  IA0.B.m[8] = 0.f;
+        IA0.C = {mm, mm, mm, 0.f, 0.f, 0.f};
+        SI IAn = IA0;
+        IA0 += L.acc[lane].I;
+        Chol6 L0;
+        L0.factor(IA0);
+        a0 = L0.solve(-1.f * (B + L.acc[lane].B));
+        if (dual) {
+            IAn += L.acc[lane].In;
+            L0.factor(IAn);
+        }
+#pragma unroll
+        for (int e = 0; e < 21; ++e) L.l0[m][e] = L0.l[e];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) L.l0[m][21 + e] = L0.id[e];
+    }
+    if (isbase && alive) L.node[lane].V = a0;  // the V record now carries a
+    // ---- outward: accelerations
+    float qddi = 0.f;
+    for (int d = 1; d < levels; ++d) {
+        if (depth == d) {
+            const SV ap = ad_inv(R, p, L.node[pnode].V);
+            qddi = psi * (tt - dot(U, ap));
+            L.node[lane].V = ap + eta + motion(b, qddi);
+        }
+    }
+    if (alive) {
+        ScNode& s = L.node[lane];
+        s.R = R;
+        s.p = p;
+        s.U = {{dual ? Un.w.x : U.w.x, dual ? Un.w.y : U.w.y, dual ? Un.w.z : U.w.z},
+               {dual ? Un.v.x : U.v.x, dual ? Un.v.y : U.v.y, dual ? Un.v.z : U.v.z}};
+        s.psi = dual ? psin : psi;
+        s.tt = tt;
+        s.depth = depth;
+    }
+    // ---- integrateVelocities
+    if (isbody && alive) {
+        L.qdd[bi] = qddi;
+        L.nu[P->body_coord[bi]] = qdi + dt * qddi;
+    }
+    if (isbase && alive && md.floating) {
+        const float a[6] = {a0.w.x, a0.w.y, a0.w.z, a0.v.x, a0.v.y, a0.v.z};
+        const float v0[6] = {base.V.w.x, base.V.w.y, base.V.w.z, base.V.v.x, base.V.v.y, base.V.v.z};
+#pragma unroll
+        for (int e = 0; e < 6; ++e) L.nu[md.coff + e] = v0[e] + dt * a[e];
+    }
+
+    // ---- contacts: ground slots, then shape pairs
+    int nc = 0;
+    if (P->ground) {
+        for (int s0 = 0; s0 < P->n_slots; s0 += kWaveLanes) {
+            const int slot = s0 + lane;
+            bool hit = false;
+            f3 xw = {0.f, 0.f, 0.f};
+            float dep = 0.f;
+            int na = 0;
+            if (slot < P->n_slots) {
+                const int sh = P->slot_shape[slot];
+                const int mo = P->shape_model[sh];
+                if ((present >> mo) & 1u) {
+                    const int c = slot - P->shape_slot0[sh];
+                    na = P->shape_node[sh];
+                    const ScNode& nd = L.node[na];
+                    const bool sphere = (P->shape_type[sh] == 1);
+                    const float* h = P->shape_size[sh];
+                    const float* SR = P->shape_R[sh];
+                    const float lx = sphere ? 0.f : ((c & 4) ? h[0] : -h[0]);
+                    const float ly = sphere ? 0.f : ((c & 2) ? h[1] : -h[1]);
+                    const float lz = sphere ? 0.f : ((c & 1) ? h[2] : -h[2]);
+                    const f3 bb = {P->shape_p[sh][0] + SR[0] * lx + SR[1] * ly + SR[2] * lz,
+                                   P->shape_p[sh][1] + SR[3] * lx + SR[4] * ly + SR[5] * lz,
+                                   P->shape_p[sh][2] + SR[6] * lx + SR[7] * ly + SR[8] * lz};
+                    xw = nd.pw + mul(nd.Rw, bb);
+                    dep = -xw.z;
+                    if (sphere) {
+                        dep = h[0] - xw.z;
+                        xw.z -= h[0];
+                    }
+                    hit = dep > 0.f;
+                }
+            }
+            const uint64_t bal = __ballot(hit);
+            const int rank = __popcll(bal & ((uint64_t{1} << lane) - 1u));
+            if (hit && nc + rank < kScMaxContacts) {
+                const int c = nc + rank;
+                L.c_p[c][0] = xw.x; L.c_p[c][1] = xw.y; L.c_p[c][2] = xw.z;
+                L.c_n[c][0] = 0.f; L.c_n[c][1] = 0.f; L.c_n[c][2] = 1.f;
+                L.c_d[c] = dep;
+                L.c_na[c] = na;
+                L.c_nb[c] = -1;
+            }
+            nc += __popcll(bal);
+        }
+    }
+    for (int p0 = 0; p0 < P->n_pairs; p0 += kWaveLanes) {
+        const int pr = p0 + lane;
+        int np = 0;
+        f3 nrm = {0.f, 0.f, 1.f}, pts[4];
+        float deps[4];
+        int na = 0, nb = 0;
+        if (pr < P->n_pairs) {
+            const int sa = P->pair_a[pr], sb = P->pair_b[pr];
+            if (((present >> P->shape_model[sa]) & 1u) && ((present >> P->shape_model[sb]) & 1u)) {
+                na = P->shape_node[sa];
+                nb = P->shape_node[sb];
+                const ScNode& A_ = L.node[na];
+                const ScNode& B_ = L.node[nb];
+                const M3 SRa = {{P->shape_R[sa][0], P->shape_R[sa][1], P->shape_R[sa][2], P->shape_R[sa][3],
+                                 P->shape_R[sa][4], P->shape_R[sa][5], P->shape_R[sa][6], P->shape_R[sa][7],
+                                 P->shape_R[sa][8]}};
+                const M3 SRb = {{P->shape_R[sb][0], P->shape_R[sb][1], P->shape_R[sb][2], P->shape_R[sb][3],
+                                 P->shape_R[sb][4], P->shape_R[sb][5], P->shape_R[sb][6], P->shape_R[sb][7],
+                                 P->shape_R[sb][8]}};
+                const f3 ca = A_.pw + mul(A_.Rw, mk(P->shape_p[sa][0], P->shape_p[sa][1], P->shape_p[sa][2]));
+                const f3 cb = B_.pw + mul(B_.Rw, mk(P->shape_p[sb][0], P->shape_p[sb][1], P->shape_p[sb][2]));
+                np = sc_collide(P->shape_type[sa], mk(P->shape_size[sa][0], P->shape_size[sa][1], P->shape_size[sa][2]),
+                                ca, mul3(A_.Rw, SRa), P->shape_type[sb],
+                                mk(P->shape_size[sb][0], P->shape_size[sb][1], P->shape_size[sb][2]), cb,
+                                mul3(B_.Rw, SRb), nrm, pts, deps);
+            }
+        }
+        int total = 0;
+        const int pre = wave_prefix7(np, total);
+        for (int i = 0; i < np; ++i) {
+            const int c = nc + pre + i;
+            if (c < kScMaxContacts) {
+                L.c_p[c][0] = pts[i].x; L.c_p[c][1] = pts[i].y; L.c_p[c][2] = pts[i].z;
+                L.c_n[c][0] = nrm.x; L.c_n[c][1] = nrm.y; L.c_n[c][2] = nrm.z;
+                L.c_d[c] = deps[i];
+                L.c_na[c] = na;
+                L.c_nb[c] = nb;
+            }
+        }
+        nc += total;
+    }
+    if (nc > kScMaxContacts) {
+        ovf += nc - kScMaxContacts;
+        nc = kScMaxContacts;
+    }
+    if (lane < nc) {
+        const f3 n = mk(L.c_n[lane][0], L.c_n[lane][1], L.c_n[lane][2]);
+        f3 t1, t2;
+        plane_space_f(n, t1, t2);
+        L.c_t1[lane][0] = t1.x; L.c_t1[lane][1] = t1.y; L.c_t1[lane][2] = t1.z;
+        L.c_t2[lane][0] = t2.x; L.c_t2[lane][1] = t2.y; L.c_t2[lane][2] = t2.z;
+        L.c_x[lane][0] = L.c_x[lane][1] = L.c_x[lane][2] = 0.f;
+    }
+
+    // ---- joint rows of body `lane` (bit t: limit / servo / friction)
+    uint32_t jbits = 0u;
+    float jb[3] = {0.f, 0.f, 0.f}, jlo[3] = {0.f, 0.f, 0.f}, jhi[3] = {0.f, 0.f, 0.f};
+    const bool jlane = lane < NB && ((present >> P->body_model[lane < NB ? lane : 0]) & 1u);
+    if (jlane) {
+        const BodyF& bj = P->b[lane];
+        const float qv = L.nu[P->body_coord[lane]];
+        if (bj.limited) {
+            float viol = L.q[lane] - bj.lower;
+            bool lim = false, up = false;
+            if (viol <= 0.f) {
+                lim = true;
+            } else {
+                viol = L.q[lane] - bj.upper;
+                if (viol >= 0.f) { lim = true; up = true; }
+            }
+            if (lim) {
+                jbits |= 1u;
+                jb[0] = fminf(fmaxf(-viol * kErp * rcp(dt), -kMaxErv), kMaxErv) - qv;
+                jlo[0] = up ? -kBig : 0.f;
+                jhi[0] = up ? 0.f : kBig;
+            }
+        }
+        if (L.act[lane] == kActServo) {
+            const float vcv = fminf(fmaxf(L.vc[lane], -bj.vel_limit), bj.vel_limit);
+            if (vcv - qv != 0.f) {
+                jbits |= 2u;
+                jb[1] = vcv - qv;
+                jhi[1] = bj.effort * dt;
+                jlo[1] = -jhi[1];
+            }
+        }
+        if (bj.friction != 0.f && qv != 0.f) {
+            jbits |= 4u;
+            jb[2] = -qv;
+            jhi[2] = bj.friction * dt;
+            jlo[2] = -jhi[2];
+        }
+    }
+    int tj = 0;
+    const int jbefore = wave_prefix7(__builtin_popcount(jbits), tj);
+    const int ncr = 3 * nc;
+    int NR = ncr + tj;
+    if (NR > kScMaxRows) {
+        ovf += NR - kScMaxRows;
+        NR = kScMaxRows;
+    }
+    if (lane < nc) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            L.src[3 * lane + d] = 3 * lane + d;
+            L.rlo[3 * lane + d] = 0.f;
+            L.rhi[3 * lane + d] = kBig;
+        }
+    }
+    if (jlane) {
+        int r = ncr + jbefore;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            if (((jbits >> t) & 1u) && r < NR) {
+                L.src[r] = kJointRow + 3 * lane + t;
+                L.rb[r] = jb[t];
+                L.rlo[r] = jlo[t];
+                L.rhi[r] = jhi[t];
+                ++r;
+            }
+        }
+    }
+
+    if (NR > 0) {
+        // ---- responses, lane = row
+        for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
+            const int r = r0 + lane;
+            if (r < NR) {
+                float* Jr = L.J[r];
+                float* MJr = L.MJ[r];
+                for (int e = 0; e < MAXNV; ++e) { Jr[e] = 0.f; MJr[e] = 0.f; }
+                const int src = L.src[r];
+                if (src < kJointRow) {
+                    const int c = src / 3, d = src % 3;
+                    const float* dwp = d == 0 ? L.c_n[c] : (d == 1 ? L.c_t1[c] : L.c_t2[c]);
+                    const f3 dw = mk(dwp[0], dwp[1], dwp[2]);
+                    const f3 xp = mk(L.c_p[c][0], L.c_p[c][1], L.c_p[c][2]);
+                    float jv = 0.f;
+#pragma unroll
+                    for (int side = 0; side < 2; ++side) {
+                        const int k = side ? L.c_nb[c] : L.c_na[c];
+                        if (k >= 0) {
+                            const ScNode& nd = L.node[k];
+                            const f3 bpt = mulT(nd.Rw, xp - nd.pw);
+                            const f3 dk = mulT(nd.Rw, dw);
+                            const float sg = side ? -1.f : 1.f;
+                            const SV f = {sg * cross(bpt, dk), sg * dk};
+                            jv += sc_response<MAXNV>(P, L, k, -1, f, Jr, MJr);
+                        }
+                    }
+                    const float bounce = (d == 0) ? fminf(kContactErp * L.c_d[c] * rcp(dt), kContactMaxErv) : 0.f;
+                    L.rb[r] = bounce - jv;
+                } else {
+                    const int j = (src - kJointRow) / 3;
+                    (void)sc_response<MAXNV>(P, L, -1, j, SV{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Jr, MJr);
+                    for (int e = 0; e < MAXNV; ++e) Jr[e] = 0.f;
+                    Jr[P->body_coord[j]] = 1.f;
+                }
+            }
+        }
+        // ---- Delassus A = J MJ^T (lane = column, MJ row in registers)
+        for (int c0 = 0; c0 < NR; c0 += kWaveLanes) {
+            const int c = c0 + lane;
+            float mj[MAXNV];
+#pragma unroll
+            for (int e = 0; e < MAXNV; ++e) mj[e] = (c < NR) ? L.MJ[c][e] : 0.f;
+            for (int r = 0; r < NR; ++r) {
+                float a = 0.f;
+#pragma unroll
+                for (int e = 0; e < MAXNV; ++e) a += L.J[r][e] * mj[e];
+                if (c < NR) {
+                    if (r == c) a *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
+                    L.A[r][c] = a;
+                }
+            }
+        }
+        for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
+            const int r = r0 + lane;
+            if (r < NR) {
+                F4 cst;
+                cst.x = L.rb[r];
+                cst.y = rcp(L.A[r][r]);
+                cst.z = L.rlo[r];
+                cst.w = L.rhi[r];
+                L.rc[r] = cst;
+            }
+        }
+        // ---- PGS (rows in order; lane c owns rows c and c + 64)
+        const float mu = P->mu;
+        float x0 = 0.f, x1 = 0.f, w0 = 0.f, w1 = 0.f;
+        const bool two = NR > kWaveLanes;
+        for (int it = 0; it < pgs_iters; ++it) {
+            float h = 0.f;
+            for (int r = 0; r < NR; ++r) {
+                const F4 cst = L.rc[r];
+                const bool hi = r >= kWaveLanes;
+                const int lr = r & (kWaveLanes - 1);
+                const float xr = read_lane(hi ? x1 : x0, lr);
+                const float wr_ = read_lane(hi ? w1 : w0, lr);
+                float v = fmaf(cst.x - wr_, cst.y, xr);
+                if (r < ncr) {
+                    if (r % 3 == 0) {
+                        v = clamp_ordered(v, 0.f, kBig);
+                        h = mu * v;
+                    } else {
+                        v = clamp_ordered(v, -h, h);
+                    }
+                } else {
+                    v = clamp_ordered(v, cst.z, cst.w);
+                }
+                const float dl = v - xr;
+                w0 = fmaf(L.A[r][lane], dl, w0);
+                if (two && kWaveLanes + lane < NR) w1 = fmaf(L.A[r][kWaveLanes + lane], dl, w1);
+                // branch-free: x stays defined in every lane for the lane reads
+                x0 = (lane == lr && !hi) ? v : x0;
+                x1 = (lane == lr && hi) ? v : x1;
+            }
+        }
+        // ---- nu += MJ^T x (lane = coordinate); impulses of the contacts.
+        // The lane reads of x run with every lane active: inside a branch on
+        // the lane index the compiler may keep x only in the active lanes.
+        {
+            const int lc = lane < NV ? lane : 0;
+            float dnu = 0.f;
+            for (int r = 0; r < NR; ++r) {
+                const float xr = read_lane(r >= kWaveLanes ? x1 : x0, r & (kWaveLanes - 1));
+                dnu += xr * L.MJ[r][lc];
+            }
+            if (lane < NV) L.nu[lane] += dnu;
+        }
+        for (int r0 = 0; r0 < NR && r0 < ncr; r0 += kWaveLanes) {
+            const int r = r0 + lane;
+            if (r < ncr && r < NR) L.c_x[r / 3][r % 3] = r0 ? x1 : x0;
+        }
+    }
+    nc_out = nc;
+
+    // ---- integratePositions
+    if (isbody && alive) {
+        const float qn = L.nu[P->body_coord[bi]];
+        L.qdd[bi] = (qn - L.qd[bi]) * rcp(dt);
+        L.qd[bi] = qn;
+        L.q[bi] += dt * qn;
+    }
+    if (isbase && alive && md.floating) {
+        const int o = md.coff;
+        const SV Vn = {{L.nu[o], L.nu[o + 1], L.nu[o + 2]}, {L.nu[o + 3], L.nu[o + 4], L.nu[o + 5]}};
+        integrate_pose(Rb0, Vn, dt, base);
+        base.V = Vn;
+    }
+}
+
+template <int MAXNV>
+__global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict__ P, SceneDev D,
+                                                       const PidF* __restrict__ pid, SceneGates G, int W,
+                                                       SceneArgs A) {
+    const int w = blockIdx.x;
+    const int lane = lane_id();
+    __shared__ ScWorld<MAXNV> L;
+    const int NB = P->n_bodies, NN = P->n_nodes;
+    const uint32_t present = D.present[w];
+    // the base lanes: node0 of every model (lane m of the base arrays = model)
+    const bool baselane = lane < NN && P->node_body[lane] < 0;
+    const int bm = baselane ? P->node_model[lane] : 0;
+    // ---- joints: resets and commands (lane = body)
+    uint32_t act = 0u;
+    float cmd = 0.f, vc = 0.f;
+    if (lane < NB) {
+        const size_t k = static_cast<size_t>(lane) * W + w;
+        float q = D.q[k], qd = D.qd[k];
+        if (A.first) {
+            const uint8_t f = D.rflag[k];
+            if (f) {
+                if (f & 2u) qd = D.rqd[k];
+                if (f & 1u) q = D.rq[k];
+                if (f & 4u) { D.pid_e[k] = 0.f; D.pid_i[k] = 0.f; D.pid_u[k] = 0.f; }
+                D.rflag[k] = 0;
+            }
+        }
+        act = D.act[k];
+        vc = D.vtgt[k];
+        cmd = A.first ? D.cmd[k] : 0.f;
+        L.q[lane] = q;
+        L.qd[lane] = qd;
+        L.act[lane] = act;
+        L.vc[lane] = vc;
+        L.qdd[lane] = 0.f;
+    }
+    // ---- bases (lane = model): pending pose / velocity resets
+    FreeState base{};
+    if (baselane) {
+        auto at = [&](int f) -> float { return D.base[static_cast<size_t>(13 * bm + f) * W + w]; };
+        base.p = {at(0), at(1), at(2)};
+        base.qw = at(3); base.qx = at(4); base.qy = at(5); base.qz = at(6);
+        base.V = {{at(7), at(8), at(9)}, {at(10), at(11), at(12)}};
+        if (A.first) {
+            const size_t fk = static_cast<size_t>(bm) * W + w;
+            const uint8_t fl = D.bflag[fk];
+            if (fl & 1u) {
+                auto rp = [&](int f) -> float { return D.rpose[static_cast<size_t>(7 * bm + f) * W + w]; };
+                base.p = {rp(0), rp(1), rp(2)};
+                const float qw = rp(3), qx = rp(4), qy = rp(5), qz = rp(6);
+                const float inv = 1.f / sqrtf(qw * qw + qx * qx + qy * qy + qz * qz);
+                base.qw = qw * inv; base.qx = qx * inv; base.qy = qy * inv; base.qz = qz * inv;
+            }
+            if (fl & 2u) {
+                auto rv = [&](int f) -> float { return D.rvel[static_cast<size_t>(6 * bm + f) * W + w]; };
+                const M3 Rq = quat_to_R(base.qw, base.qx, base.qy, base.qz);
+                base.V = {mulT(Rq, mk(rv(3), rv(4), rv(5))), mulT(Rq, mk(rv(0), rv(1), rv(2)))};
+            }
+            if (fl) D.bflag[fk] = 0;
+        }
+    }
+    // ---- wrench records of this node (lane = node)
+    float wr[kScWrenchSlots][6];
+    int32_t wl[kScWrenchSlots];
+#pragma unroll
+    for (int s = 0; s < kScWrenchSlots; ++s) {
+        wl[s] = -1;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) wr[s][e] = 0.f;
+        if (lane < NN) {
+            wl[s] = D.wlast[(static_cast<size_t>(s) * kScMaxNodes + lane) * W + w];
+            if (wl[s] > A.iter0) {
+#pragma unroll
+                for (int e = 0; e < 6; ++e)
+                    wr[s][e] = D.wrench[((static_cast<size_t>(s) * 6 + e) * kScMaxNodes + lane) * W + w];
+            }
+        }
+    }
+    int nc = 0, ovf = 0;
+    if (!A.paused) {
+        for (int s = 0; s < A.substeps; ++s) {
+            if (lane < NB && ((present >> P->body_model[lane]) & 1u))
+                L.tau[lane] = sc_dof_force(P, D, pid, G, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
+            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, nc, ovf);
+        }
+    }
+    if (lane < NB) {
+        const size_t k = static_cast<size_t>(lane) * W + w;
+        D.q[k] = L.q[lane];
+        D.qd[k] = L.qd[lane];
+        if (!A.paused) D.qdd[k] = L.qdd[lane];
+        D.cmd[k] = 0.f;
+    }
+    if (baselane) {
+        auto at = [&](int f) -> float& { return D.base[static_cast<size_t>(13 * bm + f) * W + w]; };
+        at(0) = base.p.x; at(1) = base.p.y; at(2) = base.p.z;
+        at(3) = base.qw; at(4) = base.qx; at(5) = base.qy; at(6) = base.qz;
+        at(7) = base.V.w.x; at(8) = base.V.w.y; at(9) = base.V.w.z;
+        at(10) = base.V.v.x; at(11) = base.V.v.y; at(12) = base.V.v.z;
+    }
+    if (!A.paused) {
+        if (lane == 0) {
+            D.ncontact[w] = nc;
+            if (ovf) atomicAdd(D.overflow, ovf);
+        }
+        if (A.want_contacts && lane < nc) {
+            const float inv_dt = A.inv_dt;
+            float* o = D.contact + static_cast<size_t>(lane) * 12 * W + w;
+            const f3 n = mk(L.c_n[lane][0], L.c_n[lane][1], L.c_n[lane][2]);
+            const f3 t1 = mk(L.c_t1[lane][0], L.c_t1[lane][1], L.c_t1[lane][2]);
+            const f3 t2 = mk(L.c_t2[lane][0], L.c_t2[lane][1], L.c_t2[lane][2]);
+            const f3 f = inv_dt * (L.c_x[lane][0] * n + L.c_x[lane][1] * t1 + L.c_x[lane][2] * t2);
+            o[0 * W] = L.c_p[lane][0]; o[1 * W] = L.c_p[lane][1]; o[2 * W] = L.c_p[lane][2];
+            o[3 * W] = n.x; o[4 * W] = n.y; o[5 * W] = n.z;
+            o[6 * W] = f.x; o[7 * W] = f.y; o[8 * W] = f.z;
+            o[9 * W] = L.c_d[lane];
+            o[10 * W] = __int_as_float(L.c_na[lane]);
+            o[11 * W] = __int_as_float(L.c_nb[lane]);
+        }
+    }
+}
+
+}  // namespace dev
+
+hipError_t launch_scene_run(const SceneF* P, int nv, const SceneDev& D, const PidF* pid, const SceneGates& G, int W,
+                            const SceneArgs& a, hipStream_t st) {
+    if (nv <= 32)
+        hipLaunchKernelGGL((dev::scene_run_kernel<32>), dim3(static_cast<unsigned>(W)), dim3(64), 0, st, P, D, pid,
+                           G, W, a);
+    else
+        hipLaunchKernelGGL((dev::scene_run_kernel<64>), dim3(static_cast<unsigned>(W)), dim3(64), 0, st, P, D, pid,
+                           G, W, a);
+    return hipGetLastError();
+}
+
+}  // namespace mw

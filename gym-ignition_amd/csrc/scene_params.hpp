@@ -1,0 +1,125 @@
+// scene_params.hpp -- device parameter block of a scene: several models in
+// one world (World::insertModel, cpp/scenario/gazebo/src/World.cpp:394-420),
+// each a kinematic tree on a fixed or floating base, with box / sphere
+// collision shapes that touch the ground plane and the shapes of the other
+// models.  Shared by every world of a scene (read-only, uniform per wave).
+//
+// Node numbering of the scene kernel (scene_kernel.hip), one node per lane, model by
+// model in insertion order (stable when models are added): model m owns nodes
+// [node0, node0 + 1 + n_bodies): its base link, then its bodies (the links
+// moved by its joints) depth-first (parent index < own index).  Bodies (=
+// dofs) are numbered globally in the same order.
+// Generalized velocity nu: model by model, [6 base coordinates if floating]
+// then the model's joint coordinates.
+#pragma once
+
+#include <cstdint>
+
+#include "chain_params.hpp"
+
+namespace mw {
+
+constexpr int kScMaxModels = 8;
+constexpr int kScMaxBodies = 48;
+constexpr int kScMaxNodes = kScMaxModels + kScMaxBodies;   // <= 64 lanes
+constexpr int kScMaxNv = 6 * kScMaxModels + kScMaxBodies;   // 96 coordinates
+constexpr int kScMaxShapes = 48;
+constexpr int kScMaxPairs = 128;        // shape pairs of different models (2 lane passes)
+constexpr int kScMaxGroundSlots = 128;  // 8 corners per box, 1 per sphere (2 lane passes)
+constexpr int kScMaxContacts = 32;      // contact points per step (3 rows each)
+constexpr int kScMaxRows = 96;
+constexpr int kScWrenchSlots = 4;       // concurrent wrenches (distinct expiries) per link
+constexpr int kScMaxDepth = 12;         // tree depth of the response passes' stacks
+
+struct SceneModelF {
+    int32_t floating;   // 1: DART FreeJoint root; 0: welded at (p0, R0)
+    int32_t body0;      // first body of the model
+    int32_t n_bodies;
+    int32_t coff;       // first coordinate of the model in nu
+    int32_t node0;      // the base link's node
+    float mass;         // base link inertial
+    float com[3];
+    float Io[6];        // rotational inertia about the base ORIGIN: xx yy zz xy xz yz
+    float p0[3];        // pose of a welded base (world)
+    float R0[9];
+    float pad_[5];
+};
+static_assert(sizeof(SceneModelF) == 32 * 4, "SceneModelF layout");
+
+struct SceneF {
+    int32_t n_models;
+    int32_t n_bodies;
+    int32_t nv;             // coordinates
+    int32_t n_shapes;
+    int32_t n_pairs;
+    int32_t n_slots;        // ground slots
+    int32_t n_nodes;
+    int32_t levels;         // node depth levels (bases are level 0)
+    int32_t fanout;         // most children of one node
+    int32_t dual;           // some joint has damping
+    int32_t ground;         // ground plane z = 0
+    float mu;               // Coulomb friction of every contact
+    float g[3];             // world gravity
+    int32_t pad_;
+    SceneModelF model[kScMaxModels];
+    BodyF b[kScMaxBodies];  // parent: global body index, -1 = the model's base
+    int8_t body_model[kScMaxBodies];
+    int8_t body_node[kScMaxBodies];
+    int8_t node_model[kScMaxNodes];
+    int8_t node_body[kScMaxNodes];      // -1: the node is its model's base link
+    int8_t node_depth[kScMaxNodes];     // bases 0, bodies 1 + depth below the base
+    int8_t node_srank[kScMaxNodes];     // rank among the parent node's children (highest index first)
+    int16_t body_coord[kScMaxBodies];   // coordinate of the body's joint in nu
+    uint64_t body_path[kScMaxBodies];   // bit k: body k is the body or one of its ancestors
+    // collision shapes, model by model (base first, then by body)
+    int32_t shape_node[kScMaxShapes];   // node owning the shape
+    int32_t shape_model[kScMaxShapes];
+    int32_t shape_type[kScMaxShapes];   // 0 box (half extents), 1 sphere (radius)
+    int32_t shape_slot0[kScMaxShapes];  // first ground slot
+    float shape_size[kScMaxShapes][3];
+    float shape_R[kScMaxShapes][9];     // shape pose in the node frame
+    float shape_p[kScMaxShapes][3];
+    int16_t pair_a[kScMaxPairs];        // shape indices, model(a) < model(b)
+    int16_t pair_b[kScMaxPairs];
+    int16_t slot_shape[kScMaxGroundSlots];
+};
+
+// per-model JointController period gates of one launch (bit s: the PID of the
+// model's Position / Velocity joints is recomputed on substep s)
+struct SceneGates {
+    uint64_t gate[kScMaxModels];
+};
+
+// device arrays of a scene, world index fastest
+struct SceneDev {
+    // joints [n_bodies][W] (same meaning as SimDev)
+    float *q, *qd, *qdd, *cmd, *vtgt, *rq, *rqd, *ptgt, *pid_e, *pid_i, *pid_u;
+    uint8_t *act, *rflag;
+    // bases [13 * n_models][W] (p xyz, q wxyz, twist body frame [w; v]); pending
+    // pose / velocity resets [7 * K][W], [6 * K][W] and their flags [K][W]
+    float *base, *rpose, *rvel;
+    uint8_t* bflag;
+    uint32_t* present;   // [W] bit m: model m is in world w
+    // wrenches [slot][6][node][W] (world force at the link origin, world
+    // torque) and the last iteration of each slot [slot][node][W]
+    float* wrench;
+    int32_t* wlast;
+    // contacts of the last step: [c][12][W] (point, normal B->A, force on A,
+    // depth, node A, node B (-1 ground)) and their count [W]
+    float* contact;
+    int32_t* ncontact;
+    int32_t* overflow;   // contact points / rows dropped (capacity)
+};
+
+// per-launch arguments
+struct SceneArgs {
+    float dt, inv_dt;
+    int32_t substeps;
+    int32_t pgs_iters;
+    int32_t first;       // first launch of a run: apply resets and commands
+    int32_t paused;
+    int32_t iter0;       // simulator iterations before this launch (wrench expiry)
+    int32_t want_contacts;
+};
+
+}  // namespace mw

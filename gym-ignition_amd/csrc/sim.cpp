@@ -27,6 +27,7 @@
 #include "free_body.hpp"
 #include "kernels.hpp"
 #include "model.hpp"
+#include "errors.hpp"
 
 namespace {
 
@@ -36,6 +37,13 @@ int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
 }
+
+}  // namespace
+
+// the calling thread's last error (mw_last_error), shared with scene.cpp
+void mw::set_last_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
 
 #define MW_HIP(call)                                                                      \
     do {                                                                                  \

@@ -141,6 +141,50 @@ SIGNATURES = [
     ("mw_vecenv_physics", ctypes.c_int, [_P, _P, _P]),
 ]
 
+# include/mwscene.h
+SC_POSITION, SC_VELOCITY, SC_ACCELERATION, SC_FORCE_TARGET = 0, 1, 2, 3
+SC_VELOCITY_TARGET, SC_POSITION_TARGET, SC_RESET_POSITION, SC_RESET_VELOCITY, SC_FORCE = 4, 5, 6, 7, 8
+SCENE_SIGNATURES = [
+    ("mw_scene_create", ctypes.c_int, [ctypes.POINTER(MwConfig), ctypes.POINTER(_P)]),
+    ("mw_scene_destroy", None, [_P]),
+    ("mw_scene_set_stream", ctypes.c_int, [_P, _P]),
+    ("mw_scene_insert_model", ctypes.c_int, [_P, _S, _D, _S, _I, _I, _IP]),
+    ("mw_scene_set_present", ctypes.c_int, [_P, _I, _I, _I, _I]),
+    ("mw_scene_present", ctypes.c_int, [_P, _I, _I, _IP]),
+    ("mw_scene_n_worlds", ctypes.c_int, [_P, _IP]),
+    ("mw_scene_n_models", ctypes.c_int, [_P, _IP]),
+    ("mw_scene_model_info", ctypes.c_int, [_P, _I, _IP, _IP, _IP]),
+    ("mw_scene_model_name", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
+    ("mw_scene_base_frame", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
+    ("mw_scene_joint_name", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
+    ("mw_scene_link_name", ctypes.c_int, [_P, _I, ctypes.c_char_p, _I]),
+    ("mw_scene_joint_type", ctypes.c_int, [_P, _I, _IP]),
+    ("mw_scene_model_export", ctypes.c_int, [_P, _I, _D, _I]),
+    ("mw_scene_run", ctypes.c_int, [_P, _I]),
+    ("mw_scene_run_device", ctypes.c_int, [_P, _I]),
+    ("mw_scene_time", ctypes.c_int, [_P, _D]),
+    ("mw_scene_set_gravity", ctypes.c_int, [_P, _D]),
+    ("mw_scene_gravity", ctypes.c_int, [_P, _D]),
+    ("mw_scene_set_ground_plane", ctypes.c_int, [_P, _I, ctypes.c_double]),
+    ("mw_scene_get_joints", ctypes.c_int, [_P, _I, _I, _I, _IP, _I, _D]),
+    ("mw_scene_set_joints", ctypes.c_int, [_P, _I, _I, _I, _IP, _I, _D]),
+    ("mw_scene_set_control_mode", ctypes.c_int, [_P, _I, _I, _IP, _I, _I]),
+    ("mw_scene_control_mode", ctypes.c_int, [_P, _I, _I, _IP]),
+    ("mw_scene_set_joint_pid", ctypes.c_int, [_P, _I, _D]),
+    ("mw_scene_joint_pid", ctypes.c_int, [_P, _I, _D]),
+    ("mw_scene_set_joint_param", ctypes.c_int, [_P, _I, _I, ctypes.c_double]),
+    ("mw_scene_joint_param", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_scene_set_controller_period", ctypes.c_int, [_P, _I, ctypes.c_double]),
+    ("mw_scene_controller_period", ctypes.c_int, [_P, _I, _D]),
+    ("mw_scene_get_base_pose", ctypes.c_int, [_P, _I, _I, _I, _D]),
+    ("mw_scene_get_base_velocity", ctypes.c_int, [_P, _I, _I, _I, _D]),
+    ("mw_scene_reset_base_pose", ctypes.c_int, [_P, _I, _I, _I, _D]),
+    ("mw_scene_reset_base_velocity", ctypes.c_int, [_P, _I, _I, _I, _D]),
+    ("mw_scene_get_contacts", ctypes.c_int, [_P, _I, _D, _I, _IP]),
+    ("mw_scene_apply_world_wrench", ctypes.c_int, [_P, _I, _I, _I, _I, _D, ctypes.c_double]),
+    ("mw_scene_overflow", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
+]
+
 _lib: Optional[ctypes.CDLL] = None
 
 
@@ -157,7 +201,7 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} not found: build it with `make -C gym-ignition_amd` "
                 "(hipcc --offload-arch=gfx950); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES:
+        for name, res, args in SIGNATURES + SCENE_SIGNATURES:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -1,0 +1,234 @@
+"""Pythonic handle over one native ``mw_scene``: several models per world,
+many worlds per launch (include/mwscene.h, csrc/scene_kernel.hip).
+
+A scene is what the reference builds with ``World::insertModel`` on every
+world of a ``GazeboSimulator`` (``cpp/scenario/gazebo/src/World.cpp:394-420``,
+``GazeboSimulator.cpp:435-488``): models collide with the ground plane and
+with each other, links take world wrenches (``Link.cpp:484-560``), and one
+``run()`` steps every world in one kernel launch.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import native as N
+
+
+class Scene:
+    def __init__(self, n_worlds: int = 1, step_size: float = 1e-3, steps_per_run: int = 1, rtf: float = 1.0,
+                 device: int = 0, pgs_iters: int = 50):
+        L = N.lib()
+        cfg = N.MwConfig(step_size, rtf, steps_per_run, n_worlds, device, pgs_iters)
+        h = ctypes.c_void_p()
+        N.check(L.mw_scene_create(ctypes.byref(cfg), ctypes.byref(h)), "mw_scene_create")
+        self._h = h
+        self.n_worlds = n_worlds
+        self.step_size = step_size
+        self.steps_per_run = steps_per_run
+        self.models: List[dict] = []
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise RuntimeError("the scene was closed")
+        return self._h
+
+    def close(self) -> None:
+        if self._h is not None:
+            N.lib().mw_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------- models
+    def insert_model(self, urdf: str, pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "",
+                     worlds: Optional[Sequence[int]] = None) -> int:
+        """World::insertModel into worlds [w0, w0 + nw) (default: all); returns the model index."""
+        w0, nw = (0, self.n_worlds) if worlds is None else (worlds[0], worlds[1])
+        p = np.ascontiguousarray(pose, dtype=np.float64)
+        m = ctypes.c_int32()
+        N.check(N.lib().mw_scene_insert_model(self.handle, urdf.encode(), N.dptr(p), name.encode(), w0, nw,
+                                              ctypes.byref(m)), "insert_model")
+        self.models.append(self._info(m.value))
+        return m.value
+
+    def _info(self, m: int) -> dict:
+        L = N.lib()
+        first, n, fl = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        N.check(L.mw_scene_model_info(self.handle, m, ctypes.byref(first), ctypes.byref(n), ctypes.byref(fl)))
+        buf = ctypes.create_string_buffer(256)
+        N.check(L.mw_scene_model_name(self.handle, m, buf, 256))
+        name = buf.value.decode()
+        N.check(L.mw_scene_base_frame(self.handle, m, buf, 256))
+        base = buf.value.decode()
+        joints, links = [], []
+        for d in range(first.value, first.value + n.value):
+            N.check(L.mw_scene_joint_name(self.handle, d, buf, 256))
+            joints.append(buf.value.decode())
+            N.check(L.mw_scene_link_name(self.handle, d, buf, 256))
+            links.append(buf.value.decode())
+        return dict(first=first.value, dofs=n.value, floating=bool(fl.value), name=name, base_frame=base,
+                    joint_names=joints, link_names=links)
+
+    def set_present(self, m: int, present: bool, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_scene_set_present(self.handle, m, w0, nw, 1 if present else 0), "set_present")
+
+    def present(self, m: int, w: int = 0) -> bool:
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_scene_present(self.handle, m, w, ctypes.byref(v)))
+        return bool(v.value)
+
+    def export_model(self, m: int) -> np.ndarray:
+        n = self.models[m]["dofs"]
+        out = np.zeros(34 * n + 3)
+        N.check(N.lib().mw_scene_model_export(self.handle, m, N.dptr(out), out.size))
+        return out
+
+    # ----------------------------------------------------------- stepping
+    def run(self, paused: bool = False) -> None:
+        N.check(N.lib().mw_scene_run(self.handle, 1 if paused else 0), "run")
+
+    def run_device(self, runs: int = 1) -> None:
+        N.check(N.lib().mw_scene_run_device(self.handle, runs), "run_device")
+
+    def set_stream(self, stream: int) -> None:
+        N.check(N.lib().mw_scene_set_stream(self.handle, ctypes.c_void_p(stream)), "set_stream")
+
+    def time(self) -> float:
+        t = ctypes.c_double()
+        N.check(N.lib().mw_scene_time(self.handle, ctypes.byref(t)))
+        return t.value
+
+    def gravity(self) -> List[float]:
+        g = np.zeros(3)
+        N.check(N.lib().mw_scene_gravity(self.handle, N.dptr(g)))
+        return g.tolist()
+
+    def set_gravity(self, g: Sequence[float]) -> None:
+        a = np.ascontiguousarray(g, dtype=np.float64)
+        N.check(N.lib().mw_scene_set_gravity(self.handle, N.dptr(a)), "set_gravity")
+
+    def set_ground_plane(self, enabled: bool = True, mu: float = 1.0) -> None:
+        N.check(N.lib().mw_scene_set_ground_plane(self.handle, 1 if enabled else 0, float(mu)), "set_ground_plane")
+
+    # ------------------------------------------------------------- joints
+    _FIELDS = {"q": N.SC_POSITION, "qd": N.SC_VELOCITY, "qdd": N.SC_ACCELERATION,
+               "force_target": N.SC_FORCE_TARGET, "velocity_target": N.SC_VELOCITY_TARGET,
+               "position_target": N.SC_POSITION_TARGET, "reset_q": N.SC_RESET_POSITION,
+               "reset_qd": N.SC_RESET_VELOCITY, "force": N.SC_FORCE}
+
+    def _sel(self, m: Optional[int], dofs):
+        """global dof indices of model m (local indices `dofs`), or every dof"""
+        if m is None:
+            return None if dofs is None else np.ascontiguousarray(dofs, dtype=np.int32)
+        info = self.models[m]
+        local = range(info["dofs"]) if dofs is None else dofs
+        return np.ascontiguousarray([info["first"] + d for d in local], dtype=np.int32)
+
+    def get(self, what: str, m: Optional[int] = None, w0: int = 0, nw: Optional[int] = None, dofs=None) -> np.ndarray:
+        nw = self.n_worlds - w0 if nw is None else nw
+        sel = self._sel(m, dofs)
+        nd = (sum(i["dofs"] for i in self.models) if sel is None else len(sel))
+        out = np.zeros((nw, nd))
+        if nd:
+            N.check(N.lib().mw_scene_get_joints(self.handle, self._FIELDS[what], w0, nw, N.iptr(sel),
+                                                0 if sel is None else len(sel), N.dptr(out)), f"get {what}")
+        return out
+
+    def set(self, what: str, values, m: Optional[int] = None, w0: int = 0, nw: Optional[int] = None,
+            dofs=None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        sel = self._sel(m, dofs)
+        nd = (sum(i["dofs"] for i in self.models) if sel is None else len(sel))
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.float64), (nw, nd)))
+        N.check(N.lib().mw_scene_set_joints(self.handle, self._FIELDS[what], w0, nw, N.iptr(sel),
+                                            0 if sel is None else len(sel), N.dptr(v)), f"set {what}")
+
+    def set_control_mode(self, mode: int, m: Optional[int] = None, w0: int = 0, nw: Optional[int] = None,
+                         dofs=None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        sel = self._sel(m, dofs)
+        N.check(N.lib().mw_scene_set_control_mode(self.handle, w0, nw, N.iptr(sel),
+                                                  0 if sel is None else len(sel), mode), "set_control_mode")
+
+    def control_mode(self, w: int, dof: int) -> int:
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_scene_control_mode(self.handle, w, dof, ctypes.byref(v)))
+        return v.value
+
+    def set_pid(self, dof: int, gains) -> None:
+        g = np.ascontiguousarray(gains, dtype=np.float64)
+        N.check(N.lib().mw_scene_set_joint_pid(self.handle, dof, N.dptr(g)), "set_pid")
+
+    def pid(self, dof: int) -> np.ndarray:
+        g = np.zeros(8)
+        N.check(N.lib().mw_scene_joint_pid(self.handle, dof, N.dptr(g)))
+        return g
+
+    def set_joint_param(self, dof: int, which: int, value: float) -> None:
+        N.check(N.lib().mw_scene_set_joint_param(self.handle, dof, which, float(value)), "set_joint_param")
+
+    def joint_param(self, dof: int, which: int) -> float:
+        v = ctypes.c_double()
+        N.check(N.lib().mw_scene_joint_param(self.handle, dof, which, ctypes.byref(v)))
+        return v.value
+
+    def set_controller_period(self, m: int, period: float) -> None:
+        N.check(N.lib().mw_scene_set_controller_period(self.handle, m, float(period)), "set_controller_period")
+
+    def controller_period(self, m: int) -> float:
+        v = ctypes.c_double()
+        N.check(N.lib().mw_scene_controller_period(self.handle, m, ctypes.byref(v)))
+        return v.value
+
+    # -------------------------------------------------------------- bases
+    def base_pose(self, m: int, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        nw = self.n_worlds - w0 if nw is None else nw
+        out = np.zeros((nw, 7))
+        N.check(N.lib().mw_scene_get_base_pose(self.handle, m, w0, nw, N.dptr(out)), "base_pose")
+        return out
+
+    def base_velocity(self, m: int, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        nw = self.n_worlds - w0 if nw is None else nw
+        out = np.zeros((nw, 6))
+        N.check(N.lib().mw_scene_get_base_velocity(self.handle, m, w0, nw, N.dptr(out)), "base_velocity")
+        return out
+
+    def reset_base_pose(self, m: int, pose, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        p = np.ascontiguousarray(np.broadcast_to(np.asarray(pose, dtype=np.float64), (nw, 7)))
+        N.check(N.lib().mw_scene_reset_base_pose(self.handle, m, w0, nw, N.dptr(p)), "reset_base_pose")
+
+    def reset_base_velocity(self, m: int, lin_ang, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(lin_ang, dtype=np.float64), (nw, 6)))
+        N.check(N.lib().mw_scene_reset_base_velocity(self.handle, m, w0, nw, N.dptr(v)), "reset_base_velocity")
+
+    # ---------------------------------------------------- contacts, wrenches
+    def contacts(self, w: int = 0) -> np.ndarray:
+        """rows: point(3), normal B->A (3), force on A (3), depth, model A, link A, model B, link B"""
+        out = np.zeros((32, 14))
+        n = ctypes.c_int32()
+        N.check(N.lib().mw_scene_get_contacts(self.handle, w, N.dptr(out), 32, ctypes.byref(n)), "contacts")
+        return out[:n.value]
+
+    def apply_world_wrench(self, m: int, link: int, wrench, duration: float, w0: int = 0,
+                           nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(wrench, dtype=np.float64), (nw, 6)))
+        N.check(N.lib().mw_scene_apply_world_wrench(self.handle, m, link, w0, nw, N.dptr(v), float(duration)),
+                "apply_world_wrench")
+
+    def overflow(self) -> int:
+        v = ctypes.c_int64()
+        N.check(N.lib().mw_scene_overflow(self.handle, ctypes.byref(v)))
+        return v.value

@@ -1637,3 +1637,633 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
     }
     return nc;
 }
+
+/* ====================================================================== */
+/* Scene: several models in one world, shape-pair contacts, wrenches.     */
+/* ====================================================================== */
+
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+/* column k of a row-major rotation (the k-th shape axis in the world) */
+static void col3(const double* R, int k, double out[3])
+{
+    out[0] = R[k]; out[1] = R[3 + k]; out[2] = R[6 + k];
+}
+
+/* reduce n > 4 contact points to 4 (deterministic): the deepest, the one
+ * farthest from it, the one farthest from the line through both, then the
+ * one farthest from the triangle's plane-projected centroid */
+static int reduce_points(int n, double (*p)[3], double* d)
+{
+    if (n <= 4) return n;
+    int keep[4], used[8] = {0};
+    int a = 0;
+    for (int i = 1; i < n; ++i) if (d[i] > d[a]) a = i;
+    keep[0] = a; used[a] = 1;
+    int b = -1; double best = -1.0;
+    for (int i = 0; i < n; ++i) {
+        if (used[i]) continue;
+        double e[3] = {p[i][0] - p[a][0], p[i][1] - p[a][1], p[i][2] - p[a][2]};
+        const double v = dot3(e, e);
+        if (v > best) { best = v; b = i; }
+    }
+    keep[1] = b; used[b] = 1;
+    int c = -1; best = -1.0;
+    const double ab[3] = {p[b][0] - p[a][0], p[b][1] - p[a][1], p[b][2] - p[a][2]};
+    for (int i = 0; i < n; ++i) {
+        if (used[i]) continue;
+        double e[3] = {p[i][0] - p[a][0], p[i][1] - p[a][1], p[i][2] - p[a][2]}, x[3];
+        cross3(ab, e, x);
+        const double v = dot3(x, x);
+        if (v > best) { best = v; c = i; }
+    }
+    keep[2] = c; used[c] = 1;
+    int e4 = -1; best = -1.0;
+    const double g[3] = {(p[a][0] + p[b][0] + p[c][0]) / 3.0, (p[a][1] + p[b][1] + p[c][1]) / 3.0,
+                         (p[a][2] + p[b][2] + p[c][2]) / 3.0};
+    for (int i = 0; i < n; ++i) {
+        if (used[i]) continue;
+        double e[3] = {p[i][0] - g[0], p[i][1] - g[1], p[i][2] - g[2]};
+        const double v = dot3(e, e);
+        if (v > best) { best = v; e4 = i; }
+    }
+    keep[3] = e4;
+    /* keep the original order of the survivors */
+    double tp[4][3], td[4];
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 4; ++k)
+            if (keep[k] == i) { memcpy(tp[m], p[i], sizeof tp[m]); td[m] = d[i]; ++m; }
+    for (int i = 0; i < 4; ++i) { memcpy(p[i], tp[i], sizeof tp[i]); d[i] = td[i]; }
+    return 4;
+}
+
+/* Sutherland-Hodgman clip of a polygon (2D coordinates in (u, v) plus the 3D
+ * point) against |u| <= hu, |v| <= hv */
+static int clip_polygon(int n, double (*poly)[5], double hu, double hv, double (*out)[5])
+{
+    double buf[2][16][5];
+    int cnt = n;
+    memcpy(buf[0], poly, (size_t)n * sizeof(double[5]));
+    int cur = 0;
+    for (int plane = 0; plane < 4; ++plane) {
+        const int axis = plane >> 1;              /* 0: u, 1: v */
+        const double sg = (plane & 1) ? -1.0 : 1.0; /* keep sg * x <= h */
+        const double h = axis ? hv : hu;
+        int m = 0;
+        double (*src)[5] = buf[cur], (*dst)[5] = buf[cur ^ 1];
+        for (int i = 0; i < cnt; ++i) {
+            const double* P = src[i];
+            const double* Q = src[(i + 1) % cnt];
+            const double dp = sg * P[axis] - h, dq = sg * Q[axis] - h;
+            if (dp <= 0.0) { memcpy(dst[m++], P, sizeof(double[5])); }
+            if ((dp < 0.0 && dq > 0.0) || (dp > 0.0 && dq < 0.0)) {
+                const double t = dp / (dp - dq);
+                for (int k = 0; k < 5; ++k) dst[m][k] = P[k] + t * (Q[k] - P[k]);
+                ++m;
+            }
+        }
+        cnt = m;
+        cur ^= 1;
+        if (cnt == 0) return 0;
+    }
+    memcpy(out, buf[cur], (size_t)cnt * sizeof(double[5]));
+    return cnt;
+}
+
+static int box_box(const double* hA, const double* cA, const double* RA, const double* hB, const double* cB,
+                   const double* RB, double n[3], double* pts, double* deps)
+{
+    double a[3][3], b[3][3], T[3] = {cB[0] - cA[0], cB[1] - cA[1], cB[2] - cA[2]};
+    for (int k = 0; k < 3; ++k) { col3(RA, k, a[k]); col3(RB, k, b[k]); }
+    /* face axes: k < 3 of A, 3..5 of B */
+    double best_face = INFINITY, best_edge = INFINITY;
+    int face = -1, ei = -1, ej = -1;
+    double edge_axis[3] = {0, 0, 0};
+    for (int k = 0; k < 6; ++k) {
+        const double* L = k < 3 ? a[k] : b[k - 3];
+        double rA = 0.0, rB = 0.0;
+        for (int i = 0; i < 3; ++i) { rA += hA[i] * fabs(dot3(a[i], L)); rB += hB[i] * fabs(dot3(b[i], L)); }
+        const double pen = rA + rB - fabs(dot3(T, L));
+        if (pen < 0.0) return 0;
+        if (pen < best_face) { best_face = pen; face = k; }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double L[3];
+            cross3(a[i], b[j], L);
+            const double len = sqrt(dot3(L, L));
+            if (len < 1e-6) continue;
+            for (int k = 0; k < 3; ++k) L[k] /= len;
+            double rA = 0.0, rB = 0.0;
+            for (int k = 0; k < 3; ++k) { rA += hA[k] * fabs(dot3(a[k], L)); rB += hB[k] * fabs(dot3(b[k], L)); }
+            const double pen = rA + rB - fabs(dot3(T, L));
+            if (pen < 0.0) return 0;
+            if (pen < best_edge) { best_edge = pen; ei = i; ej = j; memcpy(edge_axis, L, sizeof L); }
+        }
+    /* face contacts unless an edge axis is clearly shallower */
+    if (ei >= 0 && best_edge < 0.95 * best_face - 1e-5) {
+        double L[3] = {edge_axis[0], edge_axis[1], edge_axis[2]};
+        if (dot3(L, T) > 0.0) for (int k = 0; k < 3; ++k) L[k] = -L[k];   /* from B to A */
+        memcpy(n, L, sizeof L);
+        /* the edge of A nearest B (direction -n) and of B nearest A (+n) */
+        double pa[3], pb[3];
+        memcpy(pa, cA, sizeof pa);
+        memcpy(pb, cB, sizeof pb);
+        for (int k = 0; k < 3; ++k) {
+            if (k != ei) {
+                const double sg = dot3(a[k], n) > 0.0 ? -1.0 : 1.0;
+                for (int r = 0; r < 3; ++r) pa[r] += sg * hA[k] * a[k][r];
+            }
+            if (k != ej) {
+                const double sg = dot3(b[k], n) > 0.0 ? 1.0 : -1.0;
+                for (int r = 0; r < 3; ++r) pb[r] += sg * hB[k] * b[k][r];
+            }
+        }
+        /* closest points of the two edge lines, clamped to the edges */
+        const double* u = a[ei];
+        const double* v = b[ej];
+        double w0[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+        const double uv = dot3(u, v), uw = dot3(u, w0), vw = dot3(v, w0);
+        const double den = 1.0 - uv * uv;
+        double s = den > 1e-12 ? (uv * vw - uw) / den : 0.0;
+        double t = den > 1e-12 ? (vw - uv * uw) / den : 0.0;
+        if (s < -hA[ei]) s = -hA[ei];
+        if (s > hA[ei]) s = hA[ei];
+        if (t < -hB[ej]) t = -hB[ej];
+        if (t > hB[ej]) t = hB[ej];
+        for (int r = 0; r < 3; ++r) pts[r] = 0.5 * (pa[r] + s * u[r] + pb[r] + t * v[r]);
+        deps[0] = best_edge;
+        return 1;
+    }
+    /* face case: reference box owns the axis, incident box is the other */
+    const int refA = face < 3;
+    const int fk = refA ? face : face - 3;
+    const double* cR = refA ? cA : cB;
+    const double* cI = refA ? cB : cA;
+    const double* hR = refA ? hA : hB;
+    const double* hI = refA ? hB : hA;
+    double (*R)[3] = refA ? a : b;
+    double (*I)[3] = refA ? b : a;
+    double nr[3];   /* reference face normal, pointing towards the incident box */
+    memcpy(nr, R[fk], sizeof nr);
+    const double tI[3] = {cI[0] - cR[0], cI[1] - cR[1], cI[2] - cR[2]};
+    if (dot3(nr, tI) < 0.0) for (int k = 0; k < 3; ++k) nr[k] = -nr[k];
+    /* n from B to A: the reference normal points from R to I */
+    for (int k = 0; k < 3; ++k) n[k] = refA ? -nr[k] : nr[k];
+    /* incident face: most anti-parallel to nr */
+    int ik = 0;
+    double bd = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double d = fabs(dot3(I[k], nr));
+        if (d > bd) { bd = d; ik = k; }
+    }
+    const double sg = dot3(I[ik], nr) > 0.0 ? -1.0 : 1.0;
+    const int k1 = (ik + 1) % 3, k2 = (ik + 2) % 3;
+    const int u1 = (fk + 1) % 3, u2 = (fk + 2) % 3;
+    double fc[3];   /* reference face centre */
+    for (int r = 0; r < 3; ++r) fc[r] = cR[r] + hR[fk] * nr[r];
+    double poly[4][5];
+    const double sx[4] = {1, -1, -1, 1}, sy[4] = {1, 1, -1, -1};
+    for (int q = 0; q < 4; ++q) {
+        double x[3];
+        for (int r = 0; r < 3; ++r)
+            x[r] = cI[r] + sg * hI[ik] * I[ik][r] + sx[q] * hI[k1] * I[k1][r] + sy[q] * hI[k2] * I[k2][r];
+        const double rel[3] = {x[0] - fc[0], x[1] - fc[1], x[2] - fc[2]};
+        poly[q][0] = dot3(rel, R[u1]);
+        poly[q][1] = dot3(rel, R[u2]);
+        poly[q][2] = x[0]; poly[q][3] = x[1]; poly[q][4] = x[2];
+    }
+    double clipped[16][5];
+    const int m = clip_polygon(4, poly, hR[u1], hR[u2], clipped);
+    double P[16][3], D[16];
+    int cnt = 0;
+    for (int i = 0; i < m; ++i) {
+        const double* x = clipped[i] + 2;
+        const double rel[3] = {fc[0] - x[0], fc[1] - x[1], fc[2] - x[2]};
+        const double dep = dot3(rel, nr);
+        if (dep > 0.0 && cnt < 8) {
+            memcpy(P[cnt], x, sizeof P[cnt]);
+            D[cnt] = dep;
+            ++cnt;
+        }
+    }
+    cnt = reduce_points(cnt, P, D);
+    for (int i = 0; i < cnt; ++i) { memcpy(pts + 3 * i, P[i], sizeof P[i]); deps[i] = D[i]; }
+    return cnt;
+}
+
+/* box (A or B) against a sphere; nbs: unit normal from the box into the
+ * sphere; the point lies on the box surface */
+static int box_sphere(const double* h, const double* c, const double* R, double rad, const double* s,
+                      double nbs[3], double* pt, double* dep)
+{
+    const double d[3] = {s[0] - c[0], s[1] - c[1], s[2] - c[2]};
+    double l[3], q[3];
+    int inside = 1;
+    for (int k = 0; k < 3; ++k) {
+        l[k] = R[k] * d[0] + R[3 + k] * d[1] + R[6 + k] * d[2];
+        q[k] = l[k] < -h[k] ? -h[k] : (l[k] > h[k] ? h[k] : l[k]);
+        if (q[k] != l[k]) inside = 0;
+    }
+    if (!inside) {
+        double e[3] = {l[0] - q[0], l[1] - q[1], l[2] - q[2]};
+        const double dist = sqrt(dot3(e, e));
+        if (dist > rad) return 0;
+        for (int k = 0; k < 3; ++k) e[k] /= dist;
+        for (int r = 0; r < 3; ++r) {
+            nbs[r] = R[r * 3] * e[0] + R[r * 3 + 1] * e[1] + R[r * 3 + 2] * e[2];
+            pt[r] = c[r] + R[r * 3] * q[0] + R[r * 3 + 1] * q[1] + R[r * 3 + 2] * q[2];
+        }
+        *dep = rad - dist;
+        return 1;
+    }
+    int kk = 0;
+    double best = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        const double g = h[k] - fabs(l[k]);
+        if (g < best) { best = g; kk = k; }
+    }
+    const double sg = l[kk] >= 0.0 ? 1.0 : -1.0;
+    double lq[3] = {l[0], l[1], l[2]};
+    lq[kk] = sg * h[kk];
+    for (int r = 0; r < 3; ++r) {
+        nbs[r] = sg * R[r * 3 + kk];
+        pt[r] = c[r] + R[r * 3] * lq[0] + R[r * 3 + 1] * lq[1] + R[r * 3 + 2] * lq[2];
+    }
+    *dep = rad + best;
+    return 1;
+}
+
+int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
+               const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
+               double* depths)
+{
+    if (type_a == 0 && type_b == 0) return box_box(size_a, c_a, R_a, size_b, c_b, R_b, normal, points, depths);
+    if (type_a == 1 && type_b == 1) {
+        double d[3] = {c_a[0] - c_b[0], c_a[1] - c_b[1], c_a[2] - c_b[2]};
+        const double dist = sqrt(dot3(d, d));
+        const double pen = size_a[0] + size_b[0] - dist;
+        if (pen < 0.0 || dist < 1e-12) return 0;
+        for (int k = 0; k < 3; ++k) normal[k] = d[k] / dist;
+        for (int k = 0; k < 3; ++k) points[k] = c_b[k] + normal[k] * (size_b[0] - 0.5 * pen);
+        depths[0] = pen;
+        return 1;
+    }
+    double nbs[3];
+    if (type_a == 0) {   /* box A, sphere B: n from B into A = -(box -> sphere) */
+        if (!box_sphere(size_a, c_a, R_a, size_b[0], c_b, nbs, points, depths)) return 0;
+        for (int k = 0; k < 3; ++k) normal[k] = -nbs[k];
+        return 1;
+    }
+    if (!box_sphere(size_b, c_b, R_b, size_a[0], c_a, nbs, points, depths)) return 0;
+    memcpy(normal, nbs, sizeof nbs);
+    return 1;
+}
+
+/* dense solve with pivoting for the scene (n <= OR_SC_MAXNV) */
+static void scene_solve(int n, const double* A_in, const double* b, double* x)
+{
+    static double A[OR_SC_MAXNV * OR_SC_MAXNV];
+    double y[OR_SC_MAXNV];
+    memcpy(A, A_in, (size_t)n * n * sizeof(double));
+    memcpy(y, b, (size_t)n * sizeof(double));
+    (void)lcp_gauss(n, A, y, x);
+}
+
+/* world pose of link `b` (-1 = base) of model m */
+static void scene_link_pose(const or_float_state* s, const or_fkin* k, int b, const double** R, const double** p)
+{
+    *R = b < 0 ? s->R : k->Rw[b];
+    *p = b < 0 ? s->p : k->pw[b];
+}
+
+int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const int32_t* mode,
+                  const double* cmd, const double* wrench, int pgs_iters, double* c_out, int32_t* c_who)
+{
+    const int K = sm->n_models;
+    static or_fkin kin[OR_SC_MAXM];
+    int off[OR_SC_MAXM], nbase[OR_SC_MAXM];
+    int NV = 0;
+    for (int m = 0; m < K; ++m) {
+        off[m] = NV;
+        nbase[m] = sm->floating[m] ? 6 : 0;
+        NV += nbase[m] + sm->model[m].tree.n;
+        float_kin(&sm->model[m], &st->s[m], &kin[m]);
+    }
+    /* block-diagonal M, h; rhs with damping, commands and wrenches */
+    static double M[OR_SC_MAXNV * OR_SC_MAXNV], Mi[OR_SC_MAXNV * OR_SC_MAXNV];
+    double rhs[OR_SC_MAXNV], acc[OR_SC_MAXNV], nu[OR_SC_MAXNV];
+    for (int e = 0; e < NV * NV; ++e) M[e] = 0.0;
+    for (int m = 0; m < K; ++m) {
+        const or_float_model* fm = &sm->model[m];
+        const or_model* t = &fm->tree;
+        const int n = t->n, nvm = 6 + n, nb = nbase[m], o = off[m];
+        static double Mm[(6 + OR_MAXB) * (6 + OR_MAXB)];
+        double hm[6 + OR_MAXB];
+        or_float_model tmp = *fm;
+        for (int r = 0; r < 3; ++r) tmp.gravity[r] = sm->gravity[r];
+        or_float_state s0 = st->s[m];
+        if (!sm->floating[m]) memset(s0.V, 0, sizeof s0.V);
+        or_float_dynamics(&tmp, &s0, Mm, hm);
+        for (int r = 6 - nb; r < nvm; ++r)
+            for (int c = 6 - nb; c < nvm; ++c) M[(o + r - 6 + nb) * NV + o + c - 6 + nb] = Mm[r * nvm + c];
+        for (int r = 6 - nb; r < nvm; ++r) rhs[o + r - 6 + nb] = -hm[r];
+        for (int e = 0; e < nb; ++e) nu[o + e] = s0.V[e];
+        for (int i = 0; i < n; ++i) {
+            const int j = o + nb + i;
+            double tau = 0.0;
+            if (mode[m * OR_MAXB + i] == OR_FORCE) {
+                tau = cmd[m * OR_MAXB + i];
+                if (tau < -t->effort[i]) tau = -t->effort[i];
+                if (tau > t->effort[i]) tau = t->effort[i];
+            }
+            rhs[j] += tau - t->damping[i] * s0.qd[i];
+            nu[j] = s0.qd[i];
+        }
+        if (wrench) {
+            for (int b = -1; b < n; ++b) {
+                const double* wr = wrench + ((size_t)m * (1 + OR_MAXB) + (size_t)(b + 1)) * 6;
+                if (wr[0] == 0.0 && wr[1] == 0.0 && wr[2] == 0.0 && wr[3] == 0.0 && wr[4] == 0.0 && wr[5] == 0.0)
+                    continue;
+                const double *Rl, *pl;
+                scene_link_pose(&s0, &kin[m], b, &Rl, &pl);
+                /* body-frame spatial force [R^T torque; R^T force] at the link origin */
+                double f[6], J[6 + OR_MAXB];
+                for (int r = 0; r < 3; ++r) {
+                    f[r] = Rl[r] * wr[3] + Rl[3 + r] * wr[4] + Rl[6 + r] * wr[5];
+                    f[3 + r] = Rl[r] * wr[0] + Rl[3 + r] * wr[1] + Rl[6 + r] * wr[2];
+                }
+                if (b < 0) {
+                    for (int e = 0; e < nvm; ++e) J[e] = 0.0;
+                    for (int e = 0; e < 6; ++e) J[e] = f[e];
+                } else {
+                    float_row(fm, &kin[m], b, f, J);
+                }
+                for (int r = 6 - nb; r < nvm; ++r) rhs[o + r - 6 + nb] += J[r];
+            }
+        }
+    }
+    memcpy(Mi, M, (size_t)NV * NV * sizeof(double));
+    for (int m = 0; m < K; ++m)
+        for (int i = 0; i < sm->model[m].tree.n; ++i) {
+            const int j = off[m] + nbase[m] + i;
+            Mi[j * NV + j] += dt * sm->model[m].tree.damping[i];
+        }
+    scene_solve(NV, Mi, rhs, acc);
+    for (int e = 0; e < NV; ++e) nu[e] += dt * acc[e];
+
+    /* ---- contacts ---- */
+    int nc = 0;
+    double cp[OR_SC_MAXC][3], cn[OR_SC_MAXC][3], cd[OR_SC_MAXC];
+    int who[OR_SC_MAXC][4];
+    if (sm->ground) {
+        for (int m = 0; m < K; ++m) {
+            const or_float_model* fm = &sm->model[m];
+            for (int sh = 0; sh < fm->n_shapes; ++sh) {
+                const int bi = fm->shape_body[sh];
+                if (bi < 0 && !sm->floating[m]) continue;   /* a welded base link does not move */
+                const double *Rb, *pb;
+                scene_link_pose(&st->s[m], &kin[m], bi, &Rb, &pb);
+                const double* hh = fm->shape_size[sh];
+                const double* SR = fm->shape_R[sh];
+                const double* sp = fm->shape_p[sh];
+                const int corners = (fm->shape_type[sh] == 0) ? 8 : 1;
+                for (int corner = 0; corner < corners; ++corner) {
+                    double l[3] = {0, 0, 0}, b3[3], x[3];
+                    if (fm->shape_type[sh] == 0) {
+                        l[0] = (corner & 4) ? hh[0] : -hh[0];
+                        l[1] = (corner & 2) ? hh[1] : -hh[1];
+                        l[2] = (corner & 1) ? hh[2] : -hh[2];
+                    }
+                    for (int r = 0; r < 3; ++r) b3[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
+                    for (int r = 0; r < 3; ++r) x[r] = pb[r] + Rb[r * 3] * b3[0] + Rb[r * 3 + 1] * b3[1] + Rb[r * 3 + 2] * b3[2];
+                    double dep = -x[2];
+                    if (fm->shape_type[sh] == 1) {
+                        dep = hh[0] - x[2];
+                        x[2] -= hh[0];
+                    }
+                    if (dep > 0.0 && nc < OR_SC_MAXC) {
+                        memcpy(cp[nc], x, sizeof x);
+                        cn[nc][0] = 0.0; cn[nc][1] = 0.0; cn[nc][2] = 1.0;
+                        cd[nc] = dep;
+                        who[nc][0] = m; who[nc][1] = bi; who[nc][2] = -1; who[nc][3] = -1;
+                        ++nc;
+                    }
+                }
+            }
+        }
+    }
+    for (int ma = 0; ma < K; ++ma)
+        for (int sa = 0; sa < sm->model[ma].n_shapes; ++sa)
+            for (int mb = ma + 1; mb < K; ++mb)
+                for (int sb = 0; sb < sm->model[mb].n_shapes; ++sb) {
+                    double cA[3], RA[9], cB[3], RB[9];
+                    const or_float_model* A = &sm->model[ma];
+                    const or_float_model* B = &sm->model[mb];
+                    const int ba = A->shape_body[sa], bb = B->shape_body[sb];
+                    if (ba < 0 && !sm->floating[ma] && bb < 0 && !sm->floating[mb]) continue;  /* both welded */
+                    for (int side = 0; side < 2; ++side) {
+                        const or_float_model* F = side ? B : A;
+                        const int sh = side ? sb : sa;
+                        const double *Rl, *pl;
+                        scene_link_pose(&st->s[side ? mb : ma], &kin[side ? mb : ma], side ? bb : ba, &Rl, &pl);
+                        double* c = side ? cB : cA;
+                        double* R = side ? RB : RA;
+                        for (int r = 0; r < 3; ++r) {
+                            c[r] = pl[r] + Rl[r * 3] * F->shape_p[sh][0] + Rl[r * 3 + 1] * F->shape_p[sh][1] +
+                                   Rl[r * 3 + 2] * F->shape_p[sh][2];
+                            for (int q = 0; q < 3; ++q)
+                                R[r * 3 + q] = Rl[r * 3] * F->shape_R[sh][q] + Rl[r * 3 + 1] * F->shape_R[sh][3 + q] +
+                                               Rl[r * 3 + 2] * F->shape_R[sh][6 + q];
+                        }
+                    }
+                    double nrm[3], pts[12], deps[4];
+                    const int np = or_collide(A->shape_type[sa], A->shape_size[sa], cA, RA, B->shape_type[sb],
+                                              B->shape_size[sb], cB, RB, nrm, pts, deps);
+                    for (int i = 0; i < np && nc < OR_SC_MAXC; ++i) {
+                        memcpy(cp[nc], pts + 3 * i, sizeof cp[nc]);
+                        memcpy(cn[nc], nrm, sizeof nrm);
+                        cd[nc] = deps[i];
+                        who[nc][0] = ma; who[nc][1] = ba; who[nc][2] = mb; who[nc][3] = bb;
+                        ++nc;
+                    }
+                }
+
+    /* ---- rows: contacts (normal, t1, t2), then joint rows model by model ---- */
+    enum { K_NORMAL, K_FRIC, K_BOX };
+    const int maxr = 3 * OR_SC_MAXC + 3 * OR_MAXB;
+    static double J[3 * OR_SC_MAXC + 3 * OR_MAXB][OR_SC_MAXNV];
+    static double MJ[3 * OR_SC_MAXC + 3 * OR_MAXB][OR_SC_MAXNV];
+    static double A[(3 * OR_SC_MAXC + 3 * OR_MAXB) * (3 * OR_SC_MAXC + 3 * OR_MAXB)];
+    static double bb[3 * OR_SC_MAXC + 3 * OR_MAXB], lo[3 * OR_SC_MAXC + 3 * OR_MAXB],
+        hi[3 * OR_SC_MAXC + 3 * OR_MAXB], cfm[3 * OR_SC_MAXC + 3 * OR_MAXB], x[3 * OR_SC_MAXC + 3 * OR_MAXB];
+    static int kind[3 * OR_SC_MAXC + 3 * OR_MAXB];
+    (void)maxr;
+    int nr = 0;
+    double tb1[OR_SC_MAXC][3], tb2[OR_SC_MAXC][3];
+    for (int c = 0; c < nc; ++c) {
+        plane_space(cn[c], tb1[c], tb2[c]);
+        for (int d = 0; d < 3; ++d) {
+            const double* dw = d == 0 ? cn[c] : (d == 1 ? tb1[c] : tb2[c]);
+            for (int e = 0; e < NV; ++e) J[nr][e] = 0.0;
+            for (int side = 0; side < 2; ++side) {
+                const int m = who[c][2 * side], b = who[c][2 * side + 1];
+                if (m < 0) continue;
+                const double sg = side ? -1.0 : 1.0;
+                const or_float_model* fm = &sm->model[m];
+                const double *Rl, *pl;
+                scene_link_pose(&st->s[m], &kin[m], b, &Rl, &pl);
+                const double rel[3] = {cp[c][0] - pl[0], cp[c][1] - pl[1], cp[c][2] - pl[2]};
+                double f[6], bp[3], Jm[6 + OR_MAXB];
+                for (int r = 0; r < 3; ++r) {
+                    f[3 + r] = Rl[r] * dw[0] + Rl[3 + r] * dw[1] + Rl[6 + r] * dw[2];
+                    bp[r] = Rl[r] * rel[0] + Rl[3 + r] * rel[1] + Rl[6 + r] * rel[2];
+                }
+                cross3(bp, f + 3, f);
+                const int nvm = 6 + fm->tree.n;
+                if (b < 0) {
+                    for (int e = 0; e < nvm; ++e) Jm[e] = 0.0;
+                    for (int e = 0; e < 6; ++e) Jm[e] = f[e];
+                } else {
+                    float_row(fm, &kin[m], b, f, Jm);
+                }
+                const int nb = nbase[m];
+                for (int r = 6 - nb; r < nvm; ++r) J[nr][off[m] + r - 6 + nb] += sg * Jm[r];
+            }
+            double vrel = 0.0;
+            for (int e = 0; e < NV; ++e) vrel += J[nr][e] * nu[e];
+            double bounce = 0.0;
+            if (d == 0) {
+                bounce = OR_C_ERP * cd[c] / dt;
+                if (bounce > OR_C_MAX_ERV) bounce = OR_C_MAX_ERV;
+            }
+            bb[nr] = -vrel + bounce;
+            kind[nr] = d == 0 ? K_NORMAL : K_FRIC;
+            lo[nr] = 0.0;
+            hi[nr] = INFINITY;
+            cfm[nr] = OR_C_CFM;
+            ++nr;
+        }
+    }
+    for (int m = 0; m < K; ++m) {
+        const or_model* t = &sm->model[m].tree;
+        const or_float_state* s = &st->s[m];
+        for (int i = 0; i < t->n; ++i) {
+            const int col = off[m] + nbase[m] + i;
+            const double qdi = nu[col];
+            int rows_i[3], nri = 0;
+            if (t->limited[i]) {
+                double viol = s->q[i] - t->lower[i];
+                int active = 0;
+                if (viol <= 0.0) { lo[nr] = 0.0; hi[nr] = INFINITY; active = 1; }
+                else {
+                    viol = s->q[i] - t->upper[i];
+                    if (viol >= 0.0) { lo[nr] = -INFINITY; hi[nr] = 0.0; active = 1; }
+                }
+                if (active) {
+                    double bounce = -viol * OR_ERP / dt;
+                    if (bounce > OR_MAX_ERV) bounce = OR_MAX_ERV;
+                    if (bounce < -OR_MAX_ERV) bounce = -OR_MAX_ERV;
+                    bb[nr] = -qdi + bounce;
+                    rows_i[nri++] = nr++;
+                }
+            }
+            if (mode[m * OR_MAXB + i] == OR_SERVO) {
+                double vc = cmd[m * OR_MAXB + i];
+                if (vc < -t->vel_limit[i]) vc = -t->vel_limit[i];
+                if (vc > t->vel_limit[i]) vc = t->vel_limit[i];
+                if (vc - qdi != 0.0) {
+                    bb[nr] = vc - qdi;
+                    lo[nr] = -t->effort[i] * dt;
+                    hi[nr] = t->effort[i] * dt;
+                    rows_i[nri++] = nr++;
+                }
+            }
+            if (t->friction[i] != 0.0 && qdi != 0.0) {
+                bb[nr] = -qdi;
+                hi[nr] = t->friction[i] * dt;
+                lo[nr] = -hi[nr];
+                rows_i[nri++] = nr++;
+            }
+            for (int r = 0; r < nri; ++r) {
+                const int row = rows_i[r];
+                for (int e = 0; e < NV; ++e) J[row][e] = 0.0;
+                J[row][col] = 1.0;
+                kind[row] = K_BOX;
+                cfm[row] = OR_CFM;
+            }
+        }
+    }
+    if (nr > 0) {
+        for (int r = 0; r < nr; ++r) scene_solve(NV, M, J[r], MJ[r]);
+        for (int r = 0; r < nr; ++r) {
+            for (int c = 0; c < nr; ++c) {
+                double a = 0.0;
+                for (int e = 0; e < NV; ++e) a += J[r][e] * MJ[c][e];
+                A[r * nr + c] = a;
+            }
+            A[r * nr + r] *= 1.0 + cfm[r];
+            x[r] = 0.0;
+        }
+        g_pgs_sweeps = 0;
+        for (int it = 0; it < pgs_budget(pgs_iters); ++it) {
+            for (int r = 0; r < nr; ++r) {
+                double acc_r = bb[r];
+                for (int c = 0; c < nr; ++c) acc_r -= A[r * nr + c] * x[c];
+                double v = x[r] + acc_r / A[r * nr + r];
+                double l = lo[r], u = hi[r];
+                if (kind[r] == K_FRIC) {
+                    u = sm->mu * x[r - (r % 3)];
+                    l = -u;
+                }
+                if (v < l) v = l;
+                if (v > u) v = u;
+                x[r] = v;
+            }
+            pgs_count(it);
+        }
+        if (pgs_iters < 0) {
+            static int findex[3 * OR_SC_MAXC + 3 * OR_MAXB];
+            for (int r = 0; r < nr; ++r) findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
+            lcp_refine(nr, A, nr, bb, lo, hi, findex, sm->mu, x);
+        }
+        for (int r = 0; r < nr; ++r)
+            for (int e = 0; e < NV; ++e) nu[e] += MJ[r][e] * x[r];
+    }
+
+    /* ---- integratePositions ---- */
+    for (int m = 0; m < K; ++m) {
+        or_float_state* s = &st->s[m];
+        const int o = off[m], nb = nbase[m];
+        for (int i = 0; i < sm->model[m].tree.n; ++i) {
+            s->qd[i] = nu[o + nb + i];
+            s->q[i] += dt * nu[o + nb + i];
+        }
+        if (!nb) continue;
+        double phi[3] = {dt * nu[o], dt * nu[o + 1], dt * nu[o + 2]};
+        double u[3] = {dt * nu[o + 3], dt * nu[o + 4], dt * nu[o + 5]};
+        double dR[9], dp[3], Rn[9];
+        se3_exp(phi, u, dR, dp);
+        for (int r = 0; r < 3; ++r) {
+            s->p[r] += s->R[r * 3] * dp[0] + s->R[r * 3 + 1] * dp[1] + s->R[r * 3 + 2] * dp[2];
+            for (int q = 0; q < 3; ++q)
+                Rn[r * 3 + q] = s->R[r * 3] * dR[q] + s->R[r * 3 + 1] * dR[3 + q] + s->R[r * 3 + 2] * dR[6 + q];
+        }
+        memcpy(s->R, Rn, sizeof Rn);
+        for (int e = 0; e < 6; ++e) s->V[e] = nu[o + e];
+    }
+    for (int c = 0; c < nc; ++c) {
+        if (c_out) {
+            double* o = c_out + 10 * c;
+            for (int r = 0; r < 3; ++r) {
+                o[r] = cp[c][r];
+                o[3 + r] = cn[c][r];
+                o[6 + r] = (cn[c][r] * x[3 * c] + tb1[c][r] * x[3 * c + 1] + tb2[c][r] * x[3 * c + 2]) / dt;
+            }
+            o[9] = cd[c];
+        }
+        if (c_who) memcpy(c_who + 4 * c, who[c], sizeof who[c]);
+    }
+    return nc;
+}

@@ -241,6 +241,60 @@ void or_vec_rollout(const or_model* m, const or_task* t, int W, int T,
                     double* reward, uint8_t* done, double* terminal_obs,
                     int pgs_iters);
 
+/* ------------------------------------------------------------------ */
+/* Scene: several models in one world (World::insertModel,             */
+/* cpp/scenario/gazebo/src/World.cpp:394-420), each a tree on a fixed  */
+/* or floating base, colliding with the ground plane and with each     */
+/* other (box / sphere shapes; DART + ODE collision detector [EXT]),   */
+/* external world wrenches on links (Link::applyWorldWrench,           */
+/* Link.cpp:484-560; Physics.cpp:1446-1525).  Dense formulation: block */
+/* diagonal mass matrix of the models' or_float_dynamics, one boxed    */
+/* LCP over every contact and joint row.                               */
+/* ------------------------------------------------------------------ */
+#define OR_SC_MAXM 8
+#define OR_SC_MAXC 64            /* contact points per step                  */
+#define OR_SC_MAXNV (6 * OR_SC_MAXM + OR_MAXB)
+
+typedef struct {
+    int32_t n_models;
+    int32_t ground;              /* ground plane z = 0, normal +z             */
+    double mu;                   /* Coulomb friction of every contact         */
+    double gravity[3];
+    int32_t floating[OR_SC_MAXM];/* 0: the base link is welded at its pose    */
+    int32_t pad_;
+    or_float_model model[OR_SC_MAXM];  /* trees, base inertias, shapes        */
+} or_scene_model;
+
+typedef struct {
+    or_float_state s[OR_SC_MAXM];      /* fixed models: p, R constant, V = 0  */
+} or_scene_state;
+
+/* One engine step of the scene.
+ *   mode / cmd   [OR_SC_MAXM][OR_MAXB] joint actuation of every model
+ *   wrench       [OR_SC_MAXM][1 + OR_MAXB][6] world force (at the link
+ *                origin) and world torque per link, index 0 = the base link;
+ *                may be NULL
+ * Contacts (capacity OR_SC_MAXC): c_out rows of 10 = point xyz, normal xyz
+ * (from body B into body A), force on A xyz (impulse / dt), depth; c_who
+ * rows of 4 = model A, link A, model B, link B (link -1 = base; model B -1 =
+ * the ground plane).  Order: ground contacts model by model, shape by shape
+ * (box corners, then spheres); then shape pairs of different models in
+ * (model a, shape, model b, shape) order, at most 4 points per pair.  Shapes
+ * on the base link of a welded (fixed-base) model do not touch the ground,
+ * nor each other.
+ * Returns the number of contacts. */
+int or_scene_step(const or_scene_model* m, double dt, or_scene_state* st, const int32_t* mode,
+                  const double* cmd, const double* wrench, int pgs_iters, double* c_out, int32_t* c_who);
+
+/* Narrow phase used by or_scene_step (exposed for tests): box-box (SAT over
+ * the 15 axes, face clipping or edge-edge), box-sphere, sphere-sphere.  Shape
+ * type 0 box (size = half extents), 1 sphere (size[0] = radius); pose (c, R
+ * row-major, columns = shape axes in the world).  Writes up to 4 points and
+ * depths and the unit normal from B into A; returns the point count. */
+int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
+               const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
+               double* depths);
+
 #ifdef __cplusplus
 }
 #endif

@@ -171,6 +171,9 @@ def lib():
         FM, FS = ctypes.POINTER(OrFloatModel), ctypes.POINTER(OrFloatState)
         L.or_float_step.argtypes = [FM, ctypes.c_double, FS, I32, D, ctypes.c_int, D, D, D, I32]
         L.or_float_step.restype = ctypes.c_int
+        L.or_scene_step.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, I32, D, D, ctypes.c_int,
+                                    D, I32]
+        L.or_scene_step.restype = ctypes.c_int
         L.or_float_dynamics.argtypes = [FM, FS, D, D]
         L.or_pid_update.argtypes = [ctypes.POINTER(OrPidGains), ctypes.POINTER(OrPidState),
                                     ctypes.c_double, ctypes.c_double]
@@ -282,6 +285,9 @@ class ChainModel:
     free: Optional[OrFreeModel] = None
     # collision shapes of the moving bodies: (body, type, size, R, p) in the body frame
     body_shapes: list = field(default_factory=list)
+    # the base link's shapes (type, size, R, p) and inertial (mass, com, I about the com)
+    base_shapes: list = field(default_factory=list)
+    base_inertial: tuple = None
 
     @property
     def n(self) -> int:
@@ -425,6 +431,9 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
         M.vel_limit[i] = j.velocity
     cm = ChainModel([j.name for j in chain], root_link, M, base_R, base_p)
     cm.floating = floating
+    B0 = links[root_link]
+    cm.base_shapes = list(B0.shapes)
+    cm.base_inertial = (B0.mass, np.array(B0.com, dtype=float), np.array(B0.I, dtype=float))
     for i, j in enumerate(chain):
         for (t, sz, SR, sp) in links[j.child].shapes:
             cm.body_shapes.append((i, t, sz, SR, sp))
@@ -744,6 +753,128 @@ class FloatWorld:
                                  _p(cmd), self.pgs, _p(cp), _p(cf), _p(cd), _p(cb, ctypes.c_int32))
         self.contacts = [(cp[3 * i:3 * i + 3].copy(), cf[3 * i:3 * i + 3].copy(), float(cd[i]), int(cb[i]))
                          for i in range(nc)]
+        return nc
+
+
+OR_SC_MAXM = 8
+OR_SC_MAXC = 64
+
+
+class OrSceneModel(ctypes.Structure):
+    _fields_ = [("n_models", ctypes.c_int32), ("ground", ctypes.c_int32), ("mu", ctypes.c_double),
+                ("gravity", ctypes.c_double * 3), ("floating", ctypes.c_int32 * OR_SC_MAXM),
+                ("pad_", ctypes.c_int32), ("model", OrFloatModel * OR_SC_MAXM)]
+
+
+class OrSceneState(ctypes.Structure):
+    _fields_ = [("s", OrFloatState * OR_SC_MAXM)]
+
+
+def collide(type_a, size_a, c_a, R_a, type_b, size_b, c_b, R_b):
+    """or_collide: (normal from B into A, points [k][3], depths [k])."""
+    n, pts, dep = np.zeros(3), np.zeros(12), np.zeros(4)
+    f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=float).reshape(-1))
+    k = lib().or_collide(int(type_a), _p(f(list(size_a) + [0] * (3 - len(size_a)))), _p(f(c_a)), _p(f(R_a)),
+                         int(type_b), _p(f(list(size_b) + [0] * (3 - len(size_b)))), _p(f(c_b)), _p(f(R_b)),
+                         _p(n), _p(pts), _p(dep))
+    return n, pts[:3 * k].reshape(k, 3), dep[:k]
+
+
+class SceneWorld:
+    """fp64 scene (or_scene_step): several models in one world, each on a
+    fixed or floating base, ground plane, shape-pair contacts between models,
+    external world wrenches.  models: list of ChainModel (from load_urdf with
+    the insertion pose); a model is floating when its URDF root is not
+    attached to "world"."""
+
+    def __init__(self, models, dt=1e-3, ground=True, mu=1.0, pgs_iters=50, gravity=(0.0, 0.0, -9.8)):
+        assert len(models) <= OR_SC_MAXM
+        sm = OrSceneModel()
+        sm.n_models = len(models)
+        sm.ground = 1 if ground else 0
+        sm.mu = mu
+        for k in range(3):
+            sm.gravity[k] = gravity[k]
+        self.st = OrSceneState()
+        for m, cm in enumerate(models):
+            sm.floating[m] = 1 if cm.floating else 0
+            fm = sm.model[m]
+            ctypes.pointer(fm.tree)[0] = cm.model
+            mass, com, I = cm.base_inertial
+            fm.base_mass = mass
+            for k in range(3):
+                fm.base_com[k] = com[k]
+                fm.gravity[k] = gravity[k]
+            for k, v in enumerate([I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]):
+                fm.base_Ic[k] = v
+            shapes = [(-1, t, sz, SR, sp) for (t, sz, SR, sp) in cm.base_shapes] + list(cm.body_shapes)
+            assert len(shapes) <= OR_MAXFS
+            fm.n_shapes = len(shapes)
+            for i, (b, t, sz, SR, sp) in enumerate(shapes):
+                fm.shape_body[i] = b
+                fm.shape_type[i] = t
+                for k in range(3):
+                    fm.shape_size[i][k] = sz[k]
+                    fm.shape_p[i][k] = sp[k]
+                for k in range(9):
+                    fm.shape_R[i][k] = np.asarray(SR).flat[k]
+            s0 = self.st.s[m]
+            for k in range(3):
+                s0.p[k] = cm.base_p[k]
+            for k in range(9):
+                s0.R[k] = np.asarray(cm.base_R).flat[k]
+        self.sm, self.models = sm, list(models)
+        self.dt, self.pgs = dt, pgs_iters
+        self.mode = np.zeros((OR_SC_MAXM, OR_MAXB), dtype=np.int32)
+        self.cmd = np.zeros((OR_SC_MAXM, OR_MAXB))
+        self.wrench = np.zeros((OR_SC_MAXM, 1 + OR_MAXB, 6))
+        self.contacts = []
+
+    def state(self, m):
+        return self.st.s[m]
+
+    def set_pose(self, m, p, R):
+        s = self.st.s[m]
+        for k in range(3):
+            s.p[k] = p[k]
+        for k in range(9):
+            s.R[k] = np.asarray(R).flat[k]
+
+    def set_twist(self, m, w_body, v_body):
+        s = self.st.s[m]
+        for k in range(3):
+            s.V[k] = w_body[k]
+            s.V[3 + k] = v_body[k]
+
+    def set_joints(self, m, q, qd):
+        s = self.st.s[m]
+        for i in range(self.models[m].n):
+            s.q[i] = q[i]
+            s.qd[i] = qd[i]
+
+    def p(self, m):
+        return np.array(self.st.s[m].p[:])
+
+    def R(self, m):
+        return np.array(self.st.s[m].R[:]).reshape(3, 3)
+
+    def V(self, m):
+        return np.array(self.st.s[m].V[:])
+
+    def q(self, m):
+        return np.array(self.st.s[m].q[:self.models[m].n])
+
+    def qd(self, m):
+        return np.array(self.st.s[m].qd[:self.models[m].n])
+
+    def step(self):
+        c = np.zeros((OR_SC_MAXC, 10))
+        who = np.zeros((OR_SC_MAXC, 4), dtype=np.int32)
+        nc = lib().or_scene_step(ctypes.byref(self.sm), self.dt, ctypes.byref(self.st),
+                                 _p(np.ascontiguousarray(self.mode), ctypes.c_int32),
+                                 _p(np.ascontiguousarray(self.cmd)), _p(np.ascontiguousarray(self.wrench)),
+                                 self.pgs, _p(c), _p(who, ctypes.c_int32))
+        self.contacts = [(c[i].copy(), tuple(int(v) for v in who[i])) for i in range(nc)]
         return nc
 
 

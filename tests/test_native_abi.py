@@ -12,10 +12,11 @@ import pytest
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "mwstep.h")
+SCENE_HEADER = os.path.join(ROOT, "include", "mwscene.h")
 
 
-def _declared_symbols():
-    text = open(HEADER).read()
+def _declared_symbols(header=HEADER):
+    text = open(header).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(mw_[a-z_]+)\s*\(", text)))
 
@@ -35,6 +36,26 @@ def test_every_declared_symbol_is_exported(N):
     assert not missing, missing
     bound = {name for name, _, _ in N.SIGNATURES}
     assert set(declared) == bound, set(declared) ^ bound
+
+
+def test_every_scene_symbol_is_exported(N):
+    """include/mwscene.h (multi-model worlds): every declared entry point is
+    in the library and bound by the ctypes layer."""
+    L = ctypes.CDLL(N.LIB_PATH)
+    declared = _declared_symbols(SCENE_HEADER)
+    assert len(declared) >= 35
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    bound = {name for name, _, _ in N.SCENE_SIGNATURES}
+    assert set(declared) == bound, set(declared) ^ bound
+
+
+def test_scene_create_validates_arguments(N):
+    h = ctypes.c_void_p()
+    for step, rtf, spr, nw in [(0.0, 1.0, 1, 1), (1e-3, 0.0, 1, 1), (1e-3, 1.0, 0, 1), (1e-3, 1.0, 1, 0)]:
+        cfg = N.MwConfig(step, rtf, spr, nw, 0, 0)
+        assert N.lib().mw_scene_create(ctypes.byref(cfg), ctypes.byref(h)) == N.MW_EINVAL
+        assert N.last_error()
 
 
 def test_library_is_gfx950(N):
