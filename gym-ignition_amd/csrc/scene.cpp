@@ -625,9 +625,73 @@ int mw_scene_insert_model(mw_scene* s, const char* urdf, const double pose[7], c
 int mw_scene_set_present(mw_scene* s, int32_t model, int32_t w0, int32_t nw, int32_t present) {
     if (int rc = check_model(s, model)) return rc;
     if (int rc = check_worlds(s, w0, nw)) return rc;
-    if (present) return place_model(s, model, w0, nw);
-    for (int w = w0; w < w0 + nw; ++w) s->h_present[w] &= ~(1u << model);
+    if (present == 1) return place_model(s, model, w0, nw);
+    for (int w = w0; w < w0 + nw; ++w) {
+        if (present == 2) s->h_present[w] |= 1u << model;   // resume: the state is kept
+        else s->h_present[w] &= ~(1u << model);
+    }
     s->present_dirty = true;
+    return MW_OK;
+}
+
+int mw_scene_set_world_ground(mw_scene* s, int32_t w0, int32_t nw, int32_t enabled) {
+    if (int rc = check(s)) return rc;
+    if (int rc = check_worlds(s, w0, nw)) return rc;
+    for (int w = w0; w < w0 + nw; ++w) {
+        if (enabled) s->h_present[w] |= mw::kScGroundBit;
+        else s->h_present[w] &= ~mw::kScGroundBit;
+    }
+    s->present_dirty = true;
+    return MW_OK;
+}
+
+int mw_scene_replace_model(mw_scene* s, int32_t model, const char* urdf, const double pose[7], const char* name) {
+    if (int rc = check_model(s, model)) return rc;
+    if (!urdf) return fail(MW_EINVAL, "null argument");
+    for (int w = 0; w < s->W; ++w)
+        if ((s->h_present[w] >> model) & 1u)
+            return fail(MW_ESTATE, "a model can be replaced only while it is in no world");
+    const double ident[7] = {0, 0, 0, 1, 0, 0, 0};
+    mw::ChainModel cm;
+    try {
+        cm = mw::compile_urdf(urdf, pose ? pose : ident);
+    } catch (const std::exception& e) {
+        return fail(MW_EPARSE, e.what());
+    }
+    SceneModel& old = s->models[model];
+    auto n_shapes = [](const mw::ChainModel& c) {
+        size_t k = c.base_shapes.size();
+        for (const auto& b : c.bodies) k += b.shapes.size();
+        return k;
+    };
+    bool same = cm.dofs() == old.m.dofs() && cm.floating == old.m.floating && n_shapes(cm) == n_shapes(old.m);
+    for (int i = 0; same && i < cm.dofs(); ++i) {
+        same = cm.bodies[i].parent == old.m.bodies[i].parent && cm.bodies[i].shapes.size() == old.m.bodies[i].shapes.size();
+        for (size_t k = 0; same && k < cm.bodies[i].shapes.size(); ++k)
+            same = cm.bodies[i].shapes[k].type == old.m.bodies[i].shapes[k].type;
+    }
+    for (size_t k = 0; same && k < cm.base_shapes.size(); ++k) same = cm.base_shapes[k].type == old.m.base_shapes[k].type;
+    if (!same) return fail(MW_EINVAL, "the replacement model must have the same tree, base and collision shapes");
+    const std::string nm = (name && *name) ? name : cm.name;
+    for (size_t k = 0; k < s->models.size(); ++k)
+        if (static_cast<int>(k) != model && s->models[k].name == nm)
+            return fail(MW_EINVAL, "a model named '" + nm + "' is already in the scene");
+    SceneModel sm = old;
+    sm.m = cm;
+    sm.name = nm;
+    for (int k = 0; k < 7; ++k) sm.pose[k] = (pose ? pose : ident)[k];
+    sm.controller = false;
+    sm.period_ns = std::numeric_limits<int64_t>::max();
+    sm.prev_ns = 0;
+    sm.stepped = false;
+    old = sm;
+    try {
+        build_params(s);
+    } catch (const std::exception& e) {
+        return fail(MW_EPARSE, e.what());
+    }
+    for (int i = 0; i < cm.dofs(); ++i) s->pid[old.body0 + i] = kDefaultPid;
+    s->params_dirty = s->pid_dirty = true;
     return MW_OK;
 }
 
@@ -719,6 +783,10 @@ int mw_scene_model_export(const mw_scene* s, int32_t model, double* out, int32_t
     }
     const auto& R = cm.base_R;
     for (int k = 0; k < 3; ++k) *o++ = R[k] * s->gravity[0] + R[3 + k] * s->gravity[1] + R[6 + k] * s->gravity[2];
+    if (len >= 34 * n + 7) {  // the base link's mass and COM (base frame)
+        *o++ = cm.base_mass;
+        for (int k = 0; k < 3; ++k) *o++ = cm.base_com[k];
+    }
     return MW_OK;
 }
 
@@ -807,11 +875,13 @@ int mw_scene_gravity(const mw_scene* s, double g[3]) {
 int mw_scene_set_ground_plane(mw_scene* s, int32_t enabled, double mu) {
     if (int rc = check(s)) return rc;
     if (!(mu >= 0.0)) return fail(MW_EINVAL, "the friction coefficient must be >= 0");
-    s->ground = enabled != 0;
+    // the plane's friction is scene-wide; its presence is a per-world bit
+    // (mw_scene_set_world_ground), set here for every world
+    s->ground = true;
     s->mu = mu;
     try { build_params(s); } catch (const std::exception& e) { return fail(MW_EPARSE, e.what()); }
     s->params_dirty = true;
-    return MW_OK;
+    return mw_scene_set_world_ground(s, 0, s->W, enabled);
 }
 
 int mw_scene_get_joints(const mw_scene* cs, int32_t field, int32_t w0, int32_t nw, const int32_t* dofs, int32_t nd,

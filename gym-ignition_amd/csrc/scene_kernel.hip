@@ -597,7 +597,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 
     // ---- contacts: ground slots, then shape pairs
     int nc = 0;
-    if (P->ground) {
+    if (P->ground && (present & kScGroundBit)) {
         for (int s0 = 0; s0 < P->n_slots; s0 += kWaveLanes) {
             const int slot = s0 + lane;
             bool hit = false;
@@ -834,6 +834,18 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         float x0 = 0.f, x1 = 0.f, w0 = 0.f, w1 = 0.f;
         const bool two = NR > kWaveLanes;
         for (int it = 0; it < pgs_iters; ++it) {
+            // the residual w = A x is rebuilt at the start of every sweep (as
+            // the oracle forms b - A x exactly per row): no drift of the
+            // incremental updates across sweeps
+            if (it > 0) {
+                w0 = 0.f;
+                w1 = 0.f;
+                for (int r = 0; r < NR; ++r) {
+                    const float xr = read_lane(r >= kWaveLanes ? x1 : x0, r & (kWaveLanes - 1));
+                    w0 = fmaf(L.A[r][lane], xr, w0);
+                    if (two && kWaveLanes + lane < NR) w1 = fmaf(L.A[r][kWaveLanes + lane], xr, w1);
+                }
+            }
             float h = 0.f;
             for (int r = 0; r < NR; ++r) {
                 const F4 cst = L.rc[r];

@@ -30,6 +30,7 @@ constexpr int kScMaxContacts = 32;      // contact points per step (3 rows each)
 constexpr int kScMaxRows = 96;
 constexpr int kScWrenchSlots = 4;       // concurrent wrenches (distinct expiries) per link
 constexpr int kScMaxDepth = 12;         // tree depth of the response passes' stacks
+constexpr uint32_t kScGroundBit = 1u << 31;  // present mask: the world has a ground plane
 
 struct SceneModelF {
     int32_t floating;   // 1: DART FreeJoint root; 0: welded at (p0, R0)

@@ -151,6 +151,8 @@ SCENE_SIGNATURES = [
     ("mw_scene_insert_model", ctypes.c_int, [_P, _S, _D, _S, _I, _I, _IP]),
     ("mw_scene_set_present", ctypes.c_int, [_P, _I, _I, _I, _I]),
     ("mw_scene_present", ctypes.c_int, [_P, _I, _I, _IP]),
+    ("mw_scene_replace_model", ctypes.c_int, [_P, _I, _S, _D, _S]),
+    ("mw_scene_set_world_ground", ctypes.c_int, [_P, _I, _I, _I]),
     ("mw_scene_n_worlds", ctypes.c_int, [_P, _IP]),
     ("mw_scene_n_models", ctypes.c_int, [_P, _IP]),
     ("mw_scene_model_info", ctypes.c_int, [_P, _I, _IP, _IP, _IP]),

@@ -78,9 +78,20 @@ class Scene:
         return dict(first=first.value, dofs=n.value, floating=bool(fl.value), name=name, base_frame=base,
                     joint_names=joints, link_names=links)
 
-    def set_present(self, m: int, present: bool, w0: int = 0, nw: Optional[int] = None) -> None:
+    def set_present(self, m: int, present, w0: int = 0, nw: Optional[int] = None) -> None:
+        """present: False / 0 remove, True / 1 (re-)insert at the insertion pose, 2 resume with the state kept"""
         nw = self.n_worlds - w0 if nw is None else nw
-        N.check(N.lib().mw_scene_set_present(self.handle, m, w0, nw, 1 if present else 0), "set_present")
+        N.check(N.lib().mw_scene_set_present(self.handle, m, w0, nw, int(present)), "set_present")
+
+    def replace_model(self, m: int, urdf: str, pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "") -> None:
+        p = np.ascontiguousarray(pose, dtype=np.float64)
+        N.check(N.lib().mw_scene_replace_model(self.handle, m, urdf.encode(), N.dptr(p), name.encode()),
+                "replace_model")
+        self.models[m] = self._info(m)
+
+    def set_world_ground(self, enabled: bool, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_scene_set_world_ground(self.handle, w0, nw, 1 if enabled else 0), "set_world_ground")
 
     def present(self, m: int, w: int = 0) -> bool:
         v = ctypes.c_int32()
@@ -88,8 +99,9 @@ class Scene:
         return bool(v.value)
 
     def export_model(self, m: int) -> np.ndarray:
+        """34 doubles per body, gravity in the base frame (3), base mass and COM (4)"""
         n = self.models[m]["dofs"]
-        out = np.zeros(34 * n + 3)
+        out = np.zeros(34 * n + 7)
         N.check(N.lib().mw_scene_model_export(self.handle, m, N.dptr(out), out.size))
         return out
 
@@ -232,3 +244,113 @@ class Scene:
         v = ctypes.c_int64()
         N.check(N.lib().mw_scene_overflow(self.handle, ctypes.byref(v)))
         return v.value
+
+
+class SceneView:
+    """One model of one world of a Scene, with the interface of
+    ``mwstep.sim.Simulator`` that the ScenarI/O mirror (``scenario.gazebo``)
+    drives: joint getters / setters over local dof indices, base state,
+    contacts from this model's side, parameters.  Joint parameters, PID gains
+    and the controller period belong to the model slot (shared by the worlds
+    that hold the same model); state, commands, targets, control modes,
+    resets and wrenches are per world."""
+
+    def __init__(self, scene: Scene, m: int, w: int):
+        self.scene, self.m, self.w = scene, m, w
+        self._contacts_enabled = False
+        self._refresh()
+
+    def _refresh(self) -> None:
+        info = self.scene.models[self.m]
+        self.first = info["first"]
+        self.dofs = info["dofs"]
+        self.floating = info["floating"]
+        self.joint_names = list(info["joint_names"])
+        self.link_names = list(info["link_names"])
+        self.base_frame = info["base_frame"]
+        self._index = {n: i for i, n in enumerate(self.joint_names)}
+
+    # ---- identity / parameters
+    def dof_indices(self, names) -> Optional[np.ndarray]:
+        if names is None:
+            return None
+        try:
+            return np.array([self._index[n] for n in names], dtype=np.int32)
+        except KeyError as e:
+            raise RuntimeError(f"Joint {e} not found") from None
+
+    def joint_type(self, dof: int) -> int:
+        v = ctypes.c_int32()
+        N.check(N.lib().mw_scene_joint_type(self.scene.handle, self.first + dof, ctypes.byref(v)))
+        return v.value
+
+    def control_mode(self, w: int, dof: int) -> int:
+        return self.scene.control_mode(self.w, self.first + dof)
+
+    def pid(self, dof: int) -> np.ndarray:
+        return self.scene.pid(self.first + dof)
+
+    def set_pid(self, dof: int, gains) -> None:
+        self.scene.set_pid(self.first + dof, gains)
+
+    def set_joint_param(self, dof: int, which: int, value: float) -> None:
+        self.scene.set_joint_param(self.first + dof, which, value)
+
+    def joint_param(self, dof: int, which: int) -> float:
+        return self.scene.joint_param(self.first + dof, which)
+
+    def controller_period(self) -> float:
+        return self.scene.controller_period(self.m)
+
+    def set_controller_period(self, period: float) -> None:
+        self.scene.set_controller_period(self.m, period)
+
+    def export_model(self) -> np.ndarray:
+        return self.scene.export_model(self.m)
+
+    # ---- joints (local dof indices, this world)
+    def get(self, what: str, w0: int = 0, nw: Optional[int] = None, dofs=None) -> np.ndarray:
+        return self.scene.get(what, self.m, self.w, 1, None if dofs is None else list(np.asarray(dofs)))
+
+    def set(self, what: str, values, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
+        self.scene.set(what, values, self.m, self.w, 1, None if dofs is None else list(np.asarray(dofs)))
+
+    def set_control_mode(self, mode: int, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
+        self.scene.set_control_mode(mode, self.m, self.w, 1, None if dofs is None else list(np.asarray(dofs)))
+
+    # ---- base
+    def base_pose(self, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        return self.scene.base_pose(self.m, self.w, 1)
+
+    def base_velocity(self, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        return self.scene.base_velocity(self.m, self.w, 1)
+
+    def reset_base_pose(self, pose, w0: int = 0, nw: Optional[int] = None) -> None:
+        self.scene.reset_base_pose(self.m, np.asarray(pose, dtype=np.float64).reshape(1, 7), self.w, 1)
+
+    def reset_base_velocity(self, lin_ang, w0: int = 0, nw: Optional[int] = None) -> None:
+        self.scene.reset_base_velocity(self.m, np.asarray(lin_ang, dtype=np.float64).reshape(1, 6), self.w, 1)
+
+    # ---- contacts (reporting only: collisions always act) and wrenches
+    def contacts_enabled(self) -> bool:
+        return self._contacts_enabled
+
+    def enable_contacts(self, enable: bool = True) -> None:
+        self._contacts_enabled = bool(enable)
+
+    def contact_rows(self) -> np.ndarray:
+        """This model's contacts in world w, rows of 13: point, normal into
+        this model's body, force on it, depth, own link, other model (-1:
+        ground), other link (Physics.cpp:2498-2529 flips the second body)."""
+        rows = self.scene.contacts(self.w)
+        out = []
+        for r in rows:
+            if int(r[10]) == self.m:
+                out.append(np.concatenate([r[0:10], [r[11], r[12], r[13]]]))
+            elif int(r[12]) == self.m:
+                out.append(np.concatenate([r[0:3], -r[3:6], -r[6:9], [r[9], r[13], r[10], r[11]]]))
+        return np.array(out).reshape(-1, 13)
+
+    def apply_world_wrench(self, link: int, wrench, duration: float) -> None:
+        self.scene.apply_world_wrench(self.m, link, np.asarray(wrench, dtype=np.float64).reshape(1, 6), duration,
+                                      self.w, 1)

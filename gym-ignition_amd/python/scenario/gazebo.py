@@ -5,10 +5,17 @@ Same names and return conventions as the reference's SWIG module
 return ``bool`` and log the reason of a failure, getters raise
 ``RuntimeError`` (the SWIG mapping of ``scenario::gazebo::exceptions``).
 
-Where the reference keeps entity state in an ign-gazebo ECM and steps it with
-DART on the CPU, every articulated model here owns one native simulator
-(``mwstep.Simulator``) whose state lives in HBM; ``GazeboSimulator.run()``
-steps all of them.  Component semantics that callers can observe are kept:
+Where the reference keeps entity state in one ign-gazebo ECM per world and
+steps each with DART on the CPU, a ``GazeboSimulator`` here owns one native
+scene (``mwstep.scene.Scene``, include/mwscene.h) whose worlds are the
+simulator's worlds: every model of every world lives in HBM, models of one
+world collide with each other and with the world's ground plane, and one
+``run()`` steps all worlds in one kernel launch (GazeboSimulator.cpp:435-488,
+Physics.cpp:1832-1834).  A model inserted with the same name, file and pose
+into several worlds shares one model slot of the scene (its joint parameters,
+PID gains and controller period are the slot's); state, commands, targets,
+control modes, resets and wrenches are per world.  Component semantics that
+callers can observe are kept:
 
   * resets and commands take effect on the next ``run()`` (paused or not),
     and getters return the state refreshed by the last run
@@ -624,14 +631,14 @@ class Model:
 
     # -- stepping (called by GazeboSimulator.run)
     def _run(self, paused: bool) -> None:
+        # bookkeeping before the world's scene runs (GazeboSimulator.run)
         if self._history is not None and not paused:
             self._history.extend(self._get("force_target", None).tolist())
-        self._sim.run(paused)
         self._pending_vel = None
 
     def _close(self) -> None:
         if self._sim is not None:
-            self._sim.close()
+            self._world._simulator._remove_model(self._sim)
             self._sim = None
 
 
@@ -695,23 +702,61 @@ class Link:
 
     def contacts(self) -> List[core.Contact]:
         # Link::contacts (Link.cpp:365-434): the points of one body pair are
-        # merged into one Contact; the ground plane is the only other body here
+        # merged into one Contact, body_a = this link; the other body is a
+        # link of another model of the world or the ground plane
         sim = self._model._sim
-        if not sim.floating or not sim.contacts_enabled():
+        if not sim.contacts_enabled():
             return []
-        rows = sim.contacts(0)
-        if len(rows) == 0:
-            return []
-        bodies = sim.contact_bodies(0)
-        rows = [r for r, b in zip(rows, bodies) if b == self._body]
-        if not rows:
-            return []
-        ground = self._model._world._ground_name or "ground_plane::link"
-        pts = [core.ContactPoint(r[0:3], r[3:6], r[6:9], (0.0, 0.0, 0.0), r[9]) for r in rows]
-        return [core.Contact(self.name(scoped=True), ground, pts)]
+        rows = sim.contact_rows()
+        groups: "collections.OrderedDict[tuple, list]" = collections.OrderedDict()
+        for r in rows:
+            if int(r[10]) != self._body:
+                continue
+            groups.setdefault((int(r[11]), int(r[12])), []).append(r)
+        out = []
+        world = self._model._world
+        for (om, ol), pts in groups.items():
+            if om < 0:
+                other = world._ground_name or "ground_plane::link"
+            else:
+                other = world._link_name_of(om, ol)
+            cps = [core.ContactPoint(r[0:3], r[3:6], r[6:9], (0.0, 0.0, 0.0), r[9]) for r in pts]
+            out.append(core.Contact(self.name(scoped=True), other, cps))
+        return out
 
     def in_contact(self) -> bool:
         return len(self.contacts()) > 0
+
+    # -- external wrenches (Link::applyWorldForce / Torque / Wrench[ToCoM],
+    # Link.cpp:484-560): world force at the link origin and world torque,
+    # applied from the next physics step until simTime >= now + duration
+    def apply_world_wrench(self, force: Sequence[float], torque: Sequence[float], duration: float = 0.0) -> bool:
+        if len(force) != 3 or len(torque) != 3:
+            _err("The force and the torque must have 3 elements")
+            return False
+        try:
+            self._model._sim.apply_world_wrench(self._body, list(force) + list(torque), float(duration))
+            return True
+        except RuntimeError as e:
+            _err(str(e))
+            return False
+
+    def apply_world_force(self, force: Sequence[float], duration: float = 0.0) -> bool:
+        return self.apply_world_wrench(force, [0.0, 0.0, 0.0], duration)
+
+    def apply_world_torque(self, torque: Sequence[float], duration: float = 0.0) -> bool:
+        return self.apply_world_wrench([0.0, 0.0, 0.0], torque, duration)
+
+    def apply_world_wrench_to_com(self, force: Sequence[float], torque: Sequence[float],
+                                  duration: float = 0.0) -> bool:
+        # the force acts at the COM: its moment about the link origin is added
+        # (W_R_L L_o_I) x f (Link.cpp:534-560)
+        ex = self._model._sim.export_model()
+        n = self._model._sim.dofs
+        com = ex[34 * n + 4:34 * n + 7] if self._body < 0 else ex[34 * self._body + 18:34 * self._body + 21]
+        R = self._model._link_state(self._body)[0]
+        t = np.asarray(torque, dtype=float) + np.cross(R @ com, np.asarray(force, dtype=float))
+        return self.apply_world_wrench(force, t.tolist(), duration)
 
     def contact_wrench(self) -> List[float]:
         # Link::contactWrench (Link.cpp:436-482): sum of forces and of (p - o_L) x f
@@ -780,9 +825,12 @@ class StaticModel:
 
 # ---------------------------------------------------------------------- World
 class World:
-    def __init__(self, simulator: "GazeboSimulator", name: str):
+    """One world of the simulator: world index `_index` of the simulator's scene."""
+
+    def __init__(self, simulator: "GazeboSimulator", name: str, index: int):
         self._simulator = simulator
         self._name = name
+        self._index = index
         self._models: "collections.OrderedDict[str, object]" = collections.OrderedDict()
         self._physics = False
         self._time_ns = 0
@@ -809,13 +857,11 @@ class World:
             _err("The gravity must have 3 elements")
             return False
         self._gravity = [float(g) for g in gravity]
-        for m in self._models.values():
-            if isinstance(m, Model):
-                try:
-                    m._sim.set_gravity(self._gravity)
-                except RuntimeError as e:
-                    _err(str(e))
-                    return False
+        try:
+            self._simulator._set_gravity(self._gravity)
+        except RuntimeError as e:
+            _err(str(e))
+            return False
         return True
 
     def model_names(self) -> List[str]:
@@ -829,6 +875,14 @@ class World:
     def models(self, model_names: Sequence[str] = ()) -> list:
         return [self.get_model(n) for n in (model_names or self.model_names())]
 
+    def _link_name_of(self, slot: int, link: int) -> str:
+        """scoped name of link `link` (-1 base) of the model in scene slot `slot`"""
+        for name, m in self._models.items():
+            if isinstance(m, Model) and m._sim is not None and m._sim.m == slot:
+                sim = m._sim
+                return f"{name}::{sim.base_frame if link < 0 else sim.link_names[link]}"
+        return f"model{slot}::link{link}"
+
     def set_physics_engine(self, engine: int = PhysicsEngine_dart) -> bool:
         if engine != PhysicsEngine_dart:
             _err("Physics engine not supported")
@@ -837,6 +891,10 @@ class World:
             _err("The physics engine was already inserted in this world")
             return False
         self._physics = True
+        # the Physics system starts stepping the models already in the world
+        for m in self._models.values():
+            if isinstance(m, Model):
+                self._simulator._scene.set_present(m._sim.m, 2, self._index, 1)
         return True
 
     def insert_model(self, model_file: str, pose: core.Pose = None, override_model_name: str = "") -> bool:
@@ -878,28 +936,20 @@ class World:
             self._models[name] = StaticModel(name, pose)
             plane = root.find("model/link/collision/geometry/plane")
             if plane is not None:
-                # the ground plane of the world: floating bodies collide with it
+                # the ground plane of the world: every model collides with it
                 mu_el = root.find("model/link/collision/surface/friction/ode/mu")
                 self._ground_mu = float(mu_el.text) if mu_el is not None else 1.0
                 link = root.find("model/link")
                 self._ground_name = f"{name}::{link.get('name', 'link')}"
-                for m in self._models.values():
-                    if isinstance(m, Model):
-                        m._sim.set_ground_plane(True, self._ground_mu)
+                self._simulator._set_ground(self, True, self._ground_mu)
             return True
-        from mwstep.sim import Simulator
-        sim_cfg = self._simulator
         try:
-            sim = Simulator(model_string, n_worlds=1, step_size=sim_cfg.step_size(),
-                            steps_per_run=sim_cfg.steps_per_run(), rtf=sim_cfg.real_time_factor(),
-                            device=_device(), pose=list(pose.position) + list(pose.orientation),
-                            name=name, gravity=self._gravity, cache_reads=True)
+            view = self._simulator._place_model(self, model_string,
+                                                list(pose.position) + list(pose.orientation), name)
         except RuntimeError as e:
             _err(f"Failed to insert model '{name}': {e}")
             return False
-        if self._ground_mu is not None:
-            sim.set_ground_plane(True, self._ground_mu)
-        self._models[name] = Model(self, name, sim, pose)
+        self._models[name] = Model(self, name, view, pose)
         return True
 
     def remove_model(self, model_name: str) -> bool:
@@ -910,12 +960,10 @@ class World:
         removed._close()
         if self._ground_name is not None and self._ground_name.split("::")[0] == model_name:
             self._ground_mu = self._ground_name = None
-            for m in self._models.values():
-                if isinstance(m, Model):
-                    m._sim.set_ground_plane(False)
+            self._simulator._set_ground(self, False, 1.0)
         return True
 
-    # called by GazeboSimulator.run
+    # called by GazeboSimulator.run before the scene steps
     def _update(self, paused: bool, sim_time_ns: int) -> None:
         if not self._physics:
             return
@@ -939,7 +987,8 @@ class _NameProxy(str):
 
 # ------------------------------------------------------------ GazeboSimulator
 class GazeboSimulator:
-    """Lifecycle of a set of worlds stepped in lockstep (GazeboSimulator.h)."""
+    """Lifecycle of a set of worlds stepped in lockstep (GazeboSimulator.h):
+    all of them are the worlds of one native scene, stepped by one launch."""
 
     def __init__(self, step_size: float = 0.001, rtf: float = 1.0, steps_per_run: int = 1):
         self._step_size = float(step_size)
@@ -949,6 +998,9 @@ class GazeboSimulator:
         self._worlds: "collections.OrderedDict[str, World]" = collections.OrderedDict()
         self._pending_worlds: List[str] = []
         self._iterations = 0
+        self._scene = None
+        self._slots: List[tuple] = []   # per scene slot: (name, text, pose) of its current model
+        self._ground_mu = 1.0
 
     def step_size(self) -> float:
         return self._step_size
@@ -1009,10 +1061,71 @@ class GazeboSimulator:
             return False
         if not self._pending_worlds:
             self._pending_worlds.append("default")
-        for n in self._pending_worlds:
-            self._worlds[n] = World(self, n)
+        from mwstep.scene import Scene
+        try:
+            self._scene = Scene(n_worlds=len(self._pending_worlds), step_size=self._step_size,
+                                steps_per_run=self._steps_per_run, rtf=self._rtf, device=_device(), pgs_iters=50)
+            self._scene.set_ground_plane(False, 1.0)
+        except RuntimeError as e:
+            _err(f"Failed to create the simulator: {e}")
+            return False
+        for i, n in enumerate(self._pending_worlds):
+            self._worlds[n] = World(self, n, i)
         self._initialized = True
         return True
+
+    # ---- scene slots (internal)
+    def _place_model(self, world: World, text: str, pose: List[float], name: str):
+        """World::insertModel into `world`: reuse the slot holding the same
+        model (name, file, pose) if it is not in that world yet, else a free
+        slot of the same tree (an env randomizer's per-episode model), else a
+        new slot; returns the SceneView of the model in that world."""
+        from mwstep.scene import SceneView
+        sc, w = self._scene, world._index
+        key = (name, text, tuple(round(float(v), 12) for v in pose))
+        slot = None
+        for m, k in enumerate(self._slots):
+            if k == key and not sc.present(m, w):
+                slot = m
+                break
+        if slot is not None:
+            sc.set_present(slot, 1, w, 1)
+        else:
+            for m, k in enumerate(self._slots):
+                if not any(sc.present(m, ww) for ww in range(sc.n_worlds)):
+                    try:
+                        sc.replace_model(m, text, pose, f"{name}#{m}")
+                    except RuntimeError:
+                        continue
+                    self._slots[m] = key
+                    slot = m
+                    sc.set_present(slot, 1, w, 1)
+                    break
+        if slot is None:
+            slot = sc.insert_model(text, pose, f"{name}#{len(self._slots)}", worlds=(w, 1))
+            self._slots.append(key)
+        if not world._physics:
+            sc.set_present(slot, 0, w, 1)   # placed, not stepped until the Physics system is inserted
+        return SceneView(sc, slot, w)
+
+    def _remove_model(self, view) -> None:
+        if self._scene is not None:
+            self._scene.set_present(view.m, 0, view.w, 1)
+
+    def _set_ground(self, world: World, enabled: bool, mu: float) -> None:
+        if enabled and mu != self._ground_mu:
+            # the plane's friction is scene-wide; keep the other worlds' planes
+            self._ground_mu = mu
+            grounds = [ww._ground_name is not None for ww in self._worlds.values()]
+            self._scene.set_ground_plane(True, mu)
+            for ww, g in zip(self._worlds.values(), grounds):
+                self._scene.set_world_ground(g, ww._index, 1)
+        self._scene.set_world_ground(enabled, world._index, 1)
+
+    def _set_gravity(self, g: List[float]) -> None:
+        if len(self._worlds) > 1:
+            _warn("the gravity of a batched simulator is shared by all of its worlds")
+        self._scene.set_gravity(g)
 
     def world_names(self) -> List[str]:
         return list(self._worlds.keys())
@@ -1036,6 +1149,7 @@ class GazeboSimulator:
         try:
             for w in self._worlds.values():
                 w._update(paused, t_ns)
+            self._scene.run(paused)
         except RuntimeError as e:
             _err(f"The server couldn't execute the step: {e}")
             return False
@@ -1055,6 +1169,9 @@ class GazeboSimulator:
         for w in self._worlds.values():
             w._close()
         self._worlds.clear()
+        if self._scene is not None:
+            self._scene.close()
+            self._scene = None
         self._initialized = False
         return True
 

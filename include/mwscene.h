@@ -58,10 +58,19 @@ int mw_scene_set_stream(mw_scene* sc, void* hip_stream);
  * already in the scene is kept.  *model = its index. */
 int mw_scene_insert_model(mw_scene* sc, const char* urdf, const double pose[7], const char* name, int32_t w0,
                           int32_t nw, int32_t* model);
-/* World::removeModel (present = 0) or re-insertion at the insertion pose
- * with zero joint state (present = 1) in worlds [w0, w0 + nw). */
+/* In worlds [w0, w0 + nw): World::removeModel (present = 0), re-insertion at
+ * the insertion pose with zero joint state (present = 1), or resuming a
+ * removed model with its state kept (present = 2; e.g. a world whose physics
+ * system is inserted late). */
 int mw_scene_set_present(mw_scene* sc, int32_t model, int32_t w0, int32_t nw, int32_t present);
 int mw_scene_present(const mw_scene* sc, int32_t model, int32_t w, int32_t* present);
+/* Swap the definition of a model that is in no world for another URDF with
+ * the same tree and collision shapes (inertias, joint parameters, pose and
+ * name may differ): the per-episode model of an env randomizer
+ * (python/gym_ignition/randomizers/gazebo_env_randomizer.py) reuses its slot. */
+int mw_scene_replace_model(mw_scene* sc, int32_t model, const char* urdf, const double pose[7], const char* name);
+/* the ground plane (a static model with a plane collision) of worlds [w0, w0 + nw) */
+int mw_scene_set_world_ground(mw_scene* sc, int32_t w0, int32_t nw, int32_t enabled);
 int mw_scene_n_worlds(const mw_scene* sc, int32_t* n);
 int mw_scene_n_models(const mw_scene* sc, int32_t* n);
 /* first global dof, dof count, floating base (1) or welded (0) */
@@ -72,7 +81,8 @@ int mw_scene_joint_name(const mw_scene* sc, int32_t dof, char* buf, int32_t len)
 int mw_scene_link_name(const mw_scene* sc, int32_t dof, char* buf, int32_t len);
 int mw_scene_joint_type(const mw_scene* sc, int32_t dof, int32_t* type);
 /* per body of the model, 34 doubles (the layout of mw_model_export, parent
- * = model-local index), then gravity in the base frame (3) */
+ * = model-local index), then gravity in the base frame (3); with len >=
+ * 34 n + 7 also the base link's mass and COM (base frame) */
 int mw_scene_model_export(const mw_scene* sc, int32_t model, double* out, int32_t len);
 
 /* GazeboSimulator::run: pending resets and commands, steps_per_run physics
@@ -84,6 +94,7 @@ int mw_scene_run_device(mw_scene* sc, int32_t runs);
 int mw_scene_time(const mw_scene* sc, double* seconds);
 int mw_scene_set_gravity(mw_scene* sc, const double g[3]);
 int mw_scene_gravity(const mw_scene* sc, double g[3]);
+/* the ground plane's friction, and the plane in (enabled) or out of every world */
 int mw_scene_set_ground_plane(mw_scene* sc, int32_t enabled, double mu);
 
 /* joints over worlds [w0, w0 + nw), dofs == NULL: every dof */
