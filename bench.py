@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--no-pendulum", action="store_true", help="skip the config-3 Pendulum leg")
     p.add_argument("--no-contact-leg", action="store_true", help="skip the floating-body contact leg")
     p.add_argument("--no-runtime-leg", action="store_true", help="skip the config-1 GazeboRuntime leg")
+    p.add_argument("--no-scene-leg", action="store_true", help="skip the multi-model scene leg")
     p.add_argument("--groups", type=int, default=1,
                    help="world groups per GPU, each on its own stream / hardware queue")
     return p.parse_args()
@@ -187,6 +188,9 @@ def main():
     runtime = None
     if rank == 0 and world_size == 1 and not args.no_runtime_leg:
         runtime = runtime_leg(args, dev)
+    scene = None
+    if rank == 0 and world_size == 1 and not args.no_scene_leg:
+        scene = scene_leg(args, dev, torch)
 
     # ------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
@@ -248,6 +252,7 @@ def main():
             "quadruped_floating": quadruped,
             "humanoid_c5": humanoid,
             "runtime_c1": runtime,
+            "scene_multi_model": scene,
         }
         print(json.dumps(out))
     for e in envs:
@@ -599,6 +604,59 @@ def runtime_leg(args, dev, steps=3000):
                         "(BASELINE.json configs[0] shape, GPU backend), random actions, seed 42",
             "value": round(steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
             "ms_per_step": round(elapsed / steps * 1e3, 4), "episode_resets": resets}
+
+
+def scene_leg(args, dev, torch, W=4096, K=500, warm=100, G=50):
+    """Multi-model worlds on the scene kernel (include/mwscene.h): every world
+    holds the reference's three-cube contact scene (tests/test_scenario/
+    test_contacts.py:125-236: two cubes on the ground, a third across their
+    gap, box-box + box-plane contacts) with per-world random offsets, PGS 50,
+    one physics step per run, replayed from hipGraphs of mw_scene_run_device."""
+    import numpy as np
+    from mwstep import get_model_file
+    from mwstep.scene import Scene
+    stream = torch.cuda.Stream(device=dev)
+    sc = Scene(n_worlds=W, device=dev.index, pgs_iters=50)
+    sc.set_stream(stream.cuda_stream)
+    sc.set_ground_plane(True, 1.0)
+    rng = np.random.default_rng(args.seed)
+    for k, p in enumerate([(0, -0.15, 0.101), (0, 0.15, 0.101), (0, 0, 0.301)]):
+        sc.insert_model(get_model_file("cube"), tuple(p) + (1, 0, 0, 0), f"cube{k + 1}")
+        pose = np.column_stack([np.full(W, p[0]) + rng.uniform(-0.01, 0.01, W), np.full(W, p[1]),
+                                np.full(W, p[2]) + rng.uniform(0, 0.02, W), np.ones(W), np.zeros((W, 3))])
+        sc.reset_base_pose(k, pose)
+    sc.run(paused=True)
+    with torch.cuda.stream(stream):
+        sc.run_device(warm)
+        stream.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            sc.run_device(G)
+        graph.replay()
+    stream.synchronize()
+    n_rep = K // G
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        for _ in range(n_rep):
+            graph.replay()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    steps = n_rep * G
+    rows = sc.contacts(0)
+    fz3 = float(sum(r[8] for r in rows if int(r[12]) == 2)) * -1.0
+    out = {"workload": f"{W} worlds x 3 cubes (the three-cube contact KAT scene), box-box + box-plane "
+                       "contacts, PGS 50, dt = 1 ms, scene kernel (one world per wavefront)",
+           "value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
+           "ms_per_step": round(elapsed / steps * 1e3, 6),
+           "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
+           "contacts_world0": len(rows), "cube3_support_N_world0": round(fz3, 2),
+           "dropped_rows": sc.overflow()}
+    sc.close()
+    return out
 
 
 def contact_leg(args, dev, torch):

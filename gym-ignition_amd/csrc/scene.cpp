@@ -111,6 +111,8 @@ struct mw_scene {
     bool params_dirty = true;
     bool joints_stale = false, base_stale = false, contacts_stale = false;
     bool ran = false;              // an unpaused run produced contacts
+    bool idle = true;              // nothing of ours is queued on the stream
+    bool clear_cmd = false, clear_base = false;  // consumed mirrors to clear after the next sync
 
     size_t jidx(int d, int w) const { return static_cast<size_t>(d) * W + w; }
     float* hq() { return reinterpret_cast<float*>(h_joint); }
@@ -317,8 +319,30 @@ void build_params(mw_scene* s) {
     s->nv = coff;
 }
 
-// upload pending parameters, commands, resets, presence, wrenches and gains
-int flush(mw_scene* s) {
+int sync(mw_scene* s) {
+    SC_HIP(hipStreamSynchronize(s->stream));
+    s->idle = true;
+    return MW_OK;
+}
+
+// the kernel consumes force commands and resets (UpdateSim zero-fill,
+// Physics.cpp:2226-2254): mirror that on the host copy once the uploads
+// out of it have completed
+void clear_consumed(mw_scene* s) {
+    if (s->clear_cmd) {
+        std::memset(s->hcmd(), 0, s->jrows * sizeof(float));
+        std::memset(s->hrflag(), 0, s->jrows);
+        std::fill(s->cmd64.begin(), s->cmd64.end(), 0.0);
+    }
+    if (s->clear_base) std::memset(s->hbflag(), 0, s->krows());
+    s->clear_cmd = s->clear_base = false;
+}
+
+// Upload pending parameters, commands, resets, presence, wrenches and gains
+// (asynchronous copies out of the pinned mirrors).  defer: the caller
+// synchronises later and then calls clear_consumed(); otherwise this waits
+// for the copies and clears the consumed mirrors itself.
+int flush(mw_scene* s, bool defer) {
     const bool any = s->params_dirty || s->cmd_dirty || s->base_dirty || s->present_dirty || s->wrench_dirty ||
                      s->pid_dirty;
     if (!any) return MW_OK;
@@ -327,9 +351,10 @@ int flush(mw_scene* s) {
     if (cap != hipStreamCaptureStatusNone)
         return fail(MW_ESTATE, "pending commands, resets or model changes cannot be captured into a graph: "
                                "apply them with a run before capturing");
-    // the host mirrors are rewritten right after: the stream must have drained
-    // every earlier copy out of them
-    SC_HIP(hipStreamSynchronize(s->stream));
+    // the mirrors were rewritten by the setters: an earlier copy out of them
+    // must not still be queued
+    if (!s->idle)
+        if (int rc = sync(s)) return rc;
     if (s->params_dirty) {
         SC_HIP(hipMemcpyAsync(s->dp, &s->hp, sizeof(mw::SceneF), hipMemcpyHostToDevice, s->stream));
         s->params_dirty = false;
@@ -337,11 +362,13 @@ int flush(mw_scene* s) {
     if (s->cmd_dirty) {
         SC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_joint) + s->cmd_off(), s->h_joint + s->cmd_off(),
                               s->cmd_bytes(), hipMemcpyHostToDevice, s->stream));
+        s->clear_cmd = true;
     }
     if (s->base_dirty) {
         const size_t off = 13 * s->krows() * sizeof(float);
         SC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_base) + off, s->h_base + off, s->base_bytes() - off,
                               hipMemcpyHostToDevice, s->stream));
+        s->clear_base = true;
     }
     if (s->present_dirty) {
         SC_HIP(hipMemcpyAsync(s->dev.present, s->h_present, s->W * sizeof(uint32_t), hipMemcpyHostToDevice,
@@ -360,41 +387,49 @@ int flush(mw_scene* s) {
         }
         SC_HIP(hipMemcpyAsync(s->d_pid, s->h_pid, NBMAX * sizeof(mw::PidF), hipMemcpyHostToDevice, s->stream));
     }
-    SC_HIP(hipStreamSynchronize(s->stream));
-    // the kernel consumes force commands and resets (UpdateSim zero-fill,
-    // Physics.cpp:2226-2254): mirror that on the host copy
-    if (s->cmd_dirty) {
-        std::memset(s->hcmd(), 0, s->jrows * sizeof(float));
-        std::memset(s->hrflag(), 0, s->jrows);
-        std::fill(s->cmd64.begin(), s->cmd64.end(), 0.0);
-    }
-    if (s->base_dirty) std::memset(s->hbflag(), 0, s->krows());
+    s->idle = false;
     s->cmd_dirty = s->base_dirty = s->present_dirty = s->wrench_dirty = s->pid_dirty = false;
+    if (!defer) {
+        if (int rc = sync(s)) return rc;
+        clear_consumed(s);
+    }
+    return MW_OK;
+}
+
+// queue the D2H copies of the joint state planes (q, qd, qdd: the rows of
+// the scene's bodies) and of the base states
+int queue_readback(mw_scene* s) {
+    const size_t plane = s->jrows * sizeof(float), rows = static_cast<size_t>(s->NB) * s->W * sizeof(float);
+    if (rows && 3 * plane <= (size_t{1} << 20)) {
+        // small scenes: one copy of the three planes beats three copies
+        SC_HIP(hipMemcpyAsync(s->h_joint, s->d_joint, 3 * plane, hipMemcpyDeviceToHost, s->stream));
+    } else if (rows) {
+        for (int f = 0; f < 3; ++f)
+            SC_HIP(hipMemcpyAsync(s->h_joint + f * plane, static_cast<uint8_t*>(s->d_joint) + f * plane, rows,
+                                  hipMemcpyDeviceToHost, s->stream));
+    }
+    const size_t brows = static_cast<size_t>(13 * s->models.size()) * s->W * sizeof(float);
+    if (brows) SC_HIP(hipMemcpyAsync(s->h_base, s->d_base, brows, hipMemcpyDeviceToHost, s->stream));
+    s->idle = false;
     return MW_OK;
 }
 
 int pull_joints(mw_scene* s) {
     if (!s->joints_stale) return MW_OK;
-    SC_HIP(hipMemcpyAsync(s->h_joint, s->d_joint, s->state_bytes(), hipMemcpyDeviceToHost, s->stream));
-    SC_HIP(hipStreamSynchronize(s->stream));
-    s->joints_stale = false;
+    if (int rc = queue_readback(s)) return rc;
+    if (int rc = sync(s)) return rc;
+    s->joints_stale = s->base_stale = false;
     return MW_OK;
 }
 
-int pull_base(mw_scene* s) {
-    if (!s->base_stale) return MW_OK;
-    SC_HIP(hipMemcpyAsync(s->h_base, s->d_base, 13 * s->krows() * sizeof(float), hipMemcpyDeviceToHost, s->stream));
-    SC_HIP(hipStreamSynchronize(s->stream));
-    s->base_stale = false;
-    return MW_OK;
-}
+int pull_base(mw_scene* s) { return pull_joints(s); }
 
 int pull_contacts(mw_scene* s) {
     if (!s->contacts_stale) return MW_OK;
     SC_HIP(hipMemcpyAsync(s->h_ncontact, s->dev.ncontact, s->W * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     SC_HIP(hipMemcpyAsync(s->h_contact, s->d_contact, static_cast<size_t>(CMAX) * 12 * s->W * sizeof(float),
                           hipMemcpyDeviceToHost, s->stream));
-    SC_HIP(hipStreamSynchronize(s->stream));
+    if (int rc = sync(s)) return rc;
     s->contacts_stale = false;
     return MW_OK;
 }
@@ -441,7 +476,6 @@ void quat_of(const std::array<double, 9>& R, double q[4]) {
 // model m enters worlds [w0, w0 + nw) at its insertion pose, joints at rest
 int place_model(mw_scene* s, int m, int32_t w0, int32_t nw) {
     if (int rc = pull_joints(s)) return rc;
-    if (int rc = pull_base(s)) return rc;
     const SceneModel& sm = s->models[m];
     double q[4];
     quat_of(sm.m.base_R, q);
@@ -790,13 +824,13 @@ int mw_scene_model_export(const mw_scene* s, int32_t model, double* out, int32_t
     return MW_OK;
 }
 
-static int scene_run(mw_scene* s, int32_t paused) {
+static int scene_run(mw_scene* s, int32_t paused, bool defer) {
     if (int rc = check(s)) return rc;
     if (s->models.empty()) {
         if (!paused) s->iterations += s->cfg.steps_per_run;
         return MW_OK;
     }
-    if (int rc = flush(s)) return rc;
+    if (int rc = flush(s, defer)) return rc;
     mw::SceneArgs a{};
     a.dt = static_cast<float>(s->cfg.step_size);
     a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
@@ -824,6 +858,7 @@ static int scene_run(mw_scene* s, int32_t paused) {
             }
         }
         SC_HIP(mw::launch_scene_run(s->dp, s->nv, s->dev, s->d_pid, G, s->W, a, s->stream));
+        s->idle = false;
         a.first = 0;
         done += chunk;
     } while (!paused && done < spr);
@@ -837,15 +872,21 @@ static int scene_run(mw_scene* s, int32_t paused) {
 }
 
 int mw_scene_run(mw_scene* s, int32_t paused) {
-    if (int rc = scene_run(s, paused)) return rc;
-    SC_HIP(hipStreamSynchronize(s->stream));
+    // one synchronisation per run: uploads, the launch and the readback of
+    // the joint and base state are queued back to back
+    if (int rc = scene_run(s, paused, true)) return rc;
+    if (s->models.empty()) return MW_OK;
+    if (int rc = queue_readback(s)) return rc;
+    if (int rc = sync(s)) return rc;
+    clear_consumed(s);
+    s->joints_stale = s->base_stale = false;
     return MW_OK;
 }
 
 int mw_scene_run_device(mw_scene* s, int32_t runs) {
     if (runs < 0) return fail(MW_EINVAL, "runs must be >= 0");
     for (int32_t k = 0; k < runs; ++k)
-        if (int rc = scene_run(s, 0)) return rc;
+        if (int rc = scene_run(s, 0, false)) return rc;
     return MW_OK;
 }
 

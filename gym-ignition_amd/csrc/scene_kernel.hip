@@ -833,7 +833,55 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         const float mu = P->mu;
         float x0 = 0.f, x1 = 0.f, w0 = 0.f, w1 = 0.f;
         const bool two = NR > kWaveLanes;
-        for (int it = 0; it < pgs_iters; ++it) {
+        if (NR <= kWaveLanes) {
+            // up to 64 rows: the register form of wave_tree.hpp -- lane c holds
+            // column c of A (= row c) in registers, the impulses are uniform
+            // registers, the residual w_c = sum_r A[c][r] x_r is rebuilt per
+            // sweep and updated by one column per row; rows padded to blocks
+            // of 8 with inert rows (zero column, b = 0, bounds [0, 0])
+            const int Rpad = (NR + 7) & ~7;
+            if (lane >= NR && lane < Rpad) L.rc[lane] = F4{0.f, 0.f, 0.f, 0.f};
+            float a[kWaveLanes], x[kWaveLanes];
+#pragma unroll
+            for (int r = 0; r < kWaveLanes; ++r) {
+                a[r] = (r < NR && lane < NR) ? L.A[r][lane] : 0.f;
+                x[r] = 0.f;
+            }
+            for (int it = 0; it < pgs_iters; ++it) {
+                float w = 0.f;
+#pragma unroll
+                for (int rb = 0; rb < kWaveLanes; rb += 8) {
+                    if (rb >= Rpad) break;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) w += a[rb + k] * x[rb + k];
+                }
+                float h = 0.f;
+#pragma unroll
+                for (int rb = 0; rb < kWaveLanes; rb += 8) {
+                    if (rb >= Rpad) break;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int r = rb + k;
+                        const F4 c = L.rc[r];
+                        const float xb = fmaf(c.x, c.y, x[r]);
+                        const float wpre = fmaf(-a[r], x[r], w);
+                        float v = fmaf(-read_lane(w, r), c.y, xb);
+                        if (r % 3 == 0) {
+                            v = clamp_ordered(v, c.z, c.w);  // normal row [0, inf) or joint row
+                            h = mu * v;
+                        } else {
+                            const bool fr = r < ncr;      // friction |x| <= mu x_normal, or joint row
+                            v = clamp_ordered(v, fr ? -h : c.z, fr ? h : c.w);
+                        }
+                        w = fmaf(a[r], v, wpre);
+                        x[r] = v;
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < kWaveLanes; ++r) x0 = (lane == r) ? x[r] : x0;
+        }
+        for (int it = 0; it < (two ? pgs_iters : 0); ++it) {
             // the residual w = A x is rebuilt at the start of every sweep (as
             // the oracle forms b - A x exactly per row): no drift of the
             // incremental updates across sweeps

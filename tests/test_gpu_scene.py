@@ -301,3 +301,78 @@ def test_partial_presence_and_batch_identity(require_gpu):
     for s1 in solo:
         s1.close()
     sc.close()
+
+
+def _fixed_tree_urdf(n=16, seed=9):
+    """A random branched tree of n revolute / prismatic joints welded to the
+    world (the fixed-base generalisation of test_gpu_float_tree.tree_urdf):
+    models of this shape are refused by the single-model chain kernels
+    (serial chains of <= 9 dofs and the Panda only) and run on the scene kernel."""
+    rng = np.random.default_rng(seed)
+    parents = [-1] + [int(rng.integers(-1, i)) for i in range(1, n)]
+    parts = ['<robot name="ftree"><link name="world"/><joint name="weld" type="fixed"><parent link="world"/>'
+             '<child link="base"/><origin xyz="0 0 1.5"/></joint><link name="base"><inertial><mass value="3"/>'
+             '<inertia ixx="0.1" iyy="0.1" izz="0.1" ixy="0" ixz="0" iyz="0"/></inertial></link>']
+    for i, pa in enumerate(parents):
+        axis = rng.normal(size=3)
+        axis /= np.linalg.norm(axis)
+        prismatic = i % 6 == 5
+        lim = ('<limit lower="-0.2" upper="0.2" effort="80" velocity="10"/>' if prismatic else
+               '<limit lower="-1.2" upper="1.2" effort="50" velocity="30"/>')
+        xyz = " ".join(f"{v:.3f}" for v in rng.uniform(-0.15, 0.15, 3))
+        rpy = " ".join(f"{v:.3f}" for v in rng.uniform(-0.5, 0.5, 3))
+        m = rng.uniform(0.2, 1.0)
+        parent = "base" if pa < 0 else f"l{pa}"
+        parts.append(f'<joint name="j{i}" type="{"prismatic" if prismatic else "revolute"}">'
+                     f'<parent link="{parent}"/><child link="l{i}"/><origin xyz="{xyz}" rpy="{rpy}"/>'
+                     f'<axis xyz="{axis[0]:.4f} {axis[1]:.4f} {axis[2]:.4f}"/>{lim}'
+                     f'<dynamics damping="{0.3 * (i % 3):.2f}" friction="{0.2 if i % 4 == 1 else 0.0}"/></joint>'
+                     f'<link name="l{i}"><inertial><origin xyz="0 0.01 -0.05"/><mass value="{m:.3f}"/>'
+                     f'<inertia ixx="{0.004 * m:.5f}" iyy="{0.005 * m:.5f}" izz="{0.002 * m:.5f}" ixy="0.0001" '
+                     f'ixz="0" iyz="0"/></inertial></link>')
+    return "".join(parts) + "</robot>"
+
+
+def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
+    """A welded random 16-joint branched tree (damping, Coulomb friction,
+    joints beyond their limits, random torques): one step on the scene
+    kernel against the fp64 tree oracle or_step (ABA + joint LCP) for 256
+    worlds of random states: q within 1e-5, qd within 1e-4.  The model is
+    refused by mw_load_model (chain kernels) and runs here instead."""
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    text = _fixed_tree_urdf()
+    with pytest.raises(RuntimeError):
+        Simulator(text, n_worlds=1)
+    W = 256
+    rng = np.random.default_rng(4)
+    cm = oracle.load_urdf(text)
+    n = cm.n
+    assert n == 16 and not cm.floating
+    lo, hi = np.array(cm.model.lower[:n]), np.array(cm.model.upper[:n])
+    q = rng.uniform(lo, hi, (W, n))
+    beyond = rng.uniform(size=(W, n)) < 0.1
+    q[beyond] = np.where(rng.uniform(size=(W, n)) < 0.5, lo - 1e-3, hi + 1e-3)[beyond]
+    qd = rng.uniform(-1, 1, (W, n))
+    tau = rng.uniform(-10, 10, (W, n))
+    f32 = lambda a: a.astype(np.float32).astype(np.float64)
+    q, qd, tau = f32(q), f32(qd), f32(tau)
+    from mwstep.scene import Scene
+    sc = Scene(n_worlds=W, pgs_iters=50)
+    sc.insert_model(text, (0, 0, 0, 1, 0, 0, 0), "ftree")
+    assert sc.models[0]["floating"] is False and sc.models[0]["dofs"] == n
+    sc.set("reset_q", q, m=0)
+    sc.set("reset_qd", qd, m=0)
+    sc.run(paused=True)
+    sc.set_control_mode(N.MODE_FORCE, m=0)
+    sc.set("force_target", tau, m=0)
+    sc.run()
+    gq, gqd = sc.get("q", 0), sc.get("qd", 0)
+    wq = wqd = 0.0
+    for w in range(W):
+        oq, oqd, *_ = oracle.step(cm, 1e-3, q[w], qd[w], np.full(n, oracle.FORCE, np.int32), tau[w], 50)
+        wq = max(wq, float(np.abs(gq[w] - oq).max()))
+        wqd = max(wqd, float(np.abs(gqd[w] - oqd).max()))
+    print(f"fixed 16-joint tree on the scene kernel, one step x{W}: max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
+    assert wq <= 1e-5 and wqd <= 1e-4
+    sc.close()
