@@ -300,43 +300,44 @@ def make_groups(task, W, S, dev, seed, offset, **kw):
 
 def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, gather=False):
     """W untimed warmup steps, then EXACTLY K steps replayed from hipGraphs of
-    `chunk` step launches (the action slice of every step is copied into the
-    graph's action buffer before each replay, as a policy would write it),
-    bracketed by barrier + synchronize; max over ranks.
+    `chunk` step launches, bracketed by barrier + synchronize; max over ranks.
+    Every step reads its action slice where the policy wrote it (the device
+    action tensor [T, W]): each chunk's graph is captured with the pointers of
+    its own steps, so a replay is the K-step closed loop with nothing but the
+    step kernels inside (no per-chunk copy into a staging buffer).
 
     With several world groups (envs), each group has its own stream (its own
-    hardware queue) and graph; a step = every group advanced once.  The
+    hardware queue) and graphs; a step = every group advanced once.  The
     groups' kernels overlap each other's launch gaps."""
     from mwstep.shard import gather_obs
     S = len(envs)
     Wg = envs[0].n_worlds
     G = max(1, min(chunk, K))
-    n_full, rem = divmod(K, G)
+    n_chunks = (K + G - 1) // G
     groups = []
     for g, env in enumerate(envs):
         st = torch.cuda.Stream(device=dev)
         env.sim.set_stream(st.cuda_stream)
         acts = actions[:, g * Wg:(g + 1) * Wg].contiguous()
-        buf = torch.empty((G,) + tuple(acts.shape[1:]), dtype=actions.dtype, device=dev)
+        graphs = []
         with torch.cuda.stream(st):
             env.reset()
             for t in range(warmup):
                 env.step_raw(acts[t].data_ptr())
             st.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=st):
-                for i in range(G):
-                    env.step_raw(buf[i].data_ptr())
-            tail = None
-            if rem:
-                tail = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(tail, stream=st):
-                    for i in range(rem):
-                        env.step_raw(buf[i].data_ptr())
-            buf.copy_(acts[:G])
-            graph.replay()       # one untimed replay to settle
+            for c in range(n_chunks):
+                t0_ = warmup + c * G
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=st):
+                    for t in range(t0_, min(warmup + K, t0_ + G)):
+                        env.step_raw(acts[t].data_ptr())
+                graphs.append(graph)
+            # one untimed replay of every graph: the first launch of an
+            # instantiated graph uploads it (more warmup steps, same actions)
+            for graph in graphs:
+                graph.replay()
         st.synchronize()
-        groups.append((env, st, acts, buf, graph, tail))
+        groups.append((env, st, acts, graphs))
 
     if gather:
         # the first RCCL collective sets up its channels (milliseconds): do it
@@ -355,21 +356,13 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
     st0 = groups[0][1]
     ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev_start.record(st0)
-    for env, st, acts, buf, graph, tail in groups[1:]:
+    for env, st, acts, graphs in groups[1:]:
         st.wait_event(ev_start)
-    for c in range(n_full):
-        base = warmup + c * G
-        for env, st, acts, buf, graph, tail in groups:
+    for c in range(n_chunks):
+        for env, st, acts, graphs in groups:
             with torch.cuda.stream(st):
-                buf.copy_(acts[base:base + G])
-                graph.replay()
-    if rem:
-        base = warmup + n_full * G
-        for env, st, acts, buf, graph, tail in groups:
-            with torch.cuda.stream(st):
-                buf[:rem].copy_(acts[base:base + rem])
-                tail.replay()
-    for env, st, acts, buf, graph, tail in groups[1:]:
+                graphs[c].replay()
+    for env, st, acts, graphs in groups[1:]:
         e = torch.cuda.Event()
         e.record(st)
         st0.wait_event(e)

@@ -13,8 +13,7 @@ rows = [r for r in csv.DictReader(open(trace))
         if "vecenv_step_kernel<2, 0, false, true, false" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == W]
 dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
 warm, steps = b["warmup"], b["steps"]
-G = min(100, steps)
-timed = dur[warm + G: warm + G + steps]          # warmup eager, settle replay, timed replays
+timed = dur[warm + steps: warm + 2 * steps]      # warmup eager, one settle replay of every graph, timed replays
 out = {"kernel": rows[0]["Kernel_Name"].split("(")[0] if rows else None, "worlds": W, "dispatches": len(dur),
        "timed_dispatches": len(timed), "timed_median_ns": statistics.median(timed),
        "timed_mean_ns": round(statistics.mean(timed), 1),
