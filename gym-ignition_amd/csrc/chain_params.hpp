@@ -28,7 +28,14 @@ struct BodyF {
     int32_t limited;   // position limits enforced (LCP row)
     float Ea[3];       // E * axis (prismatic translation direction in the parent)
     int32_t parent;    // parent body (< own index), -1 = base
-    float pad_[3];
+    // row topology for the lane-group kernels (group_tree.hpp), filled by
+    // group_topology_words(): ancestor bit mask, subtree end (bodies are
+    // numbered depth-first, the subtree of i is [i, end)), lane-order chain
+    // segment (bits 0-7: distance to the segment head, 8-15: the head's
+    // parent + 1, 16-23: segment nesting level)
+    uint32_t anc;
+    int32_t end;
+    int32_t seg;
 };
 static_assert(sizeof(BodyF) == 40 * 4, "BodyF layout");
 
@@ -37,7 +44,10 @@ enum : int32_t { kHasDamping = 1, kHasLimits = 2, kHasFriction = 4 };
 struct ChainF {
     int32_t n;
     int32_t flags;     // kHas* bits
-    int32_t pad_[2];
+    // lane-group kernels: bits 0-7 body whose origin is the common frame's,
+    // 8-15 segment nesting levels, 16-23 longest lane-order chain segment
+    int32_t gtopo;
+    int32_t pad_;
     float g[4];        // gravity in the base frame
     BodyF b[kMaxBodies];
 };
@@ -87,6 +97,43 @@ constexpr bool on_path(Topo t, int i, int j) {
         if (k == i) return true;
     return false;
 }
+// Fill the lane-group topology words of a depth-first numbered tree
+// (P.n bodies, P.b[i].parent set).  The common frame's origin is the body
+// half-way up the deepest chain (group_tree.hpp).
+inline void group_topology_words(ChainF& P) {
+    const int n = P.n;
+    int depth[kMaxBodies] = {}, level[kMaxBodies] = {};
+    int deepest = 0, levels = 0, maxh = 0;
+    for (int i = 0; i < n; ++i) {
+        const int pa = P.b[i].parent;
+        depth[i] = (pa >= 0) ? depth[pa] + 1 : 0;
+        if (depth[i] > depth[deepest]) deepest = i;
+        uint32_t anc = 0;
+        for (int k = pa; k >= 0; k = P.b[k].parent) anc |= 1u << (k & 31);
+        P.b[i].anc = anc;
+        int end = i + 1;
+        while (end < n) {
+            bool desc = false;
+            for (int k = P.b[end].parent; k >= 0; k = P.b[k].parent) desc = desc || (k == i);
+            if (!desc) break;
+            ++end;
+        }
+        P.b[i].end = end;
+        int h = 0;  // lanes i-h..i form a parent chain in lane order
+        while (i - h > 0 && P.b[i - h].parent == i - h - 1) ++h;
+        const int head = i - h, hp = P.b[head].parent;
+        level[i] = (hp >= 0) ? level[hp] + 1 : 0;
+        levels = level[i] > levels ? level[i] : levels;
+        maxh = h > maxh ? h : maxh;
+        P.b[i].seg = h | ((hp + 1) << 8) | (level[i] << 16);
+    }
+    int ref = deepest;
+    while (depth[ref] > depth[deepest] / 2) ref = P.b[ref].parent;
+    int steps = 0;  // Hillis-Steele steps of the segmented scans: 2^steps > maxh
+    while ((1 << steps) <= maxh) ++steps;
+    P.gtopo = ref | (levels << 8) | (steps << 16);
+}
+
 // the Franka Panda: joints 1..7 in a chain, both fingers hang off the hand
 constexpr Topo kPandaTopo = chain_topo(7) | (static_cast<Topo>(7) << 28) | (static_cast<Topo>(7) << 32);
 // four 2-dof legs hanging off a floating base (models/quadruped.urdf):

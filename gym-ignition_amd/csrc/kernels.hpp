@@ -120,6 +120,20 @@ hipError_t launch_vecenv_pid_step(const ChainF* P, int n, int topo, bool cons, b
                                   float* obs, float* reward, uint8_t* done, float* term_obs, int W,
                                   float dt, int substeps, int pgs_iters, hipStream_t st);
 
+// The same task with one world per 16-lane row (group_kernel.hip): any
+// fixed-base tree of <= kMaxKernelDofs bodies numbered depth-first, with the
+// row topology words of the parameter block filled (group_topology_words).
+// lt: per-dof PID gains and reset pose in device memory (one record per lane).
+struct GLaneTask {
+    PidF pid;
+    float home;
+    float pad_[3];
+};
+hipError_t launch_vecenv_pid_group(const ChainF* P, int n, bool cons, bool dual, const TaskF& T, const SimDev& S,
+                                   const VecDev& V, const GLaneTask* lt, const float* targets, float* obs,
+                                   float* reward, uint8_t* done, float* term_obs, int W, float dt, int substeps,
+                                   int pgs_iters, hipStream_t st);
+
 // T_steps == 0: one step with the per-step output layout; otherwise a fused
 // open-loop rollout of T_steps steps ([T, W] inputs and outputs).
 // baked: id of a bit-identical shipped model (baked_models.hpp) or 0 (generic)

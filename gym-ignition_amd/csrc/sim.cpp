@@ -158,6 +158,11 @@ struct mw_vecenv {
     mw::VecDev dev{};
     void* d_counters = nullptr;
     void* d_physics = nullptr;  // per-world randomised masses + gravity
+    // lane-group Panda kernel: per-dof PID gains + reset pose (device), and
+    // the host copy last uploaded
+    mw::GLaneTask* d_lane = nullptr;
+    mw::GLaneTask h_lane[mw::kMaxKernelDofs] = {};
+    bool lane_uploaded = false;
 };
 
 namespace {
@@ -220,6 +225,7 @@ void build_params(mw_sim* s) {
         if (b.friction != 0.0) flags |= mw::kHasFriction;
     }
     P.flags = flags;
+    mw::group_topology_words(P);
 }
 
 // FreeF of a floating single-body model: inertia about the body origin, its
@@ -1653,6 +1659,7 @@ void mw_vecenv_destroy(mw_vecenv* e) {
     if (e->sim && e->sim->stream) (void)hipStreamSynchronize(e->sim->stream);
     (void)hipFree(e->d_counters);
     (void)hipFree(e->d_physics);
+    (void)hipFree(e->d_lane);
     delete e;
 }
 
@@ -1678,10 +1685,35 @@ static int vec_common(mw_vecenv* e, int32_t T, const void* a, float* o, float* r
     mw_sim* s = e->sim;
     if (e->task.kind == MW_TASK_PANDA_POSITION_TRACKING) {
         if (T > 0) return fail(MW_EINVAL, "the fused rollout is not available for position-target tasks");
-        MW_HIP(mw::launch_vecenv_pid_step(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), baked_id(s), e->task, s->dev,
-                                          e->dev, pid_set(s), static_cast<const float*>(a), o, r, d, to, s->W,
-                                          static_cast<float>(s->cfg.step_size), s->cfg.steps_per_run,
-                                          s->cfg.pgs_iters, s->stream));
+        // one world per 16-lane row (group_kernel.hip) unless
+        // MWSTEP_PANDA_KERNEL=lane asks for the one-world-per-lane kernel
+        const char* kk = std::getenv("MWSTEP_PANDA_KERNEL");
+        if (kk && std::strcmp(kk, "lane") == 0) {
+            MW_HIP(mw::launch_vecenv_pid_step(s->d_params, s->n, s->topo, needs_cons(s), needs_dual(s), baked_id(s),
+                                              e->task, s->dev, e->dev, pid_set(s), static_cast<const float*>(a), o,
+                                              r, d, to, s->W, static_cast<float>(s->cfg.step_size),
+                                              s->cfg.steps_per_run, s->cfg.pgs_iters, s->stream));
+        } else {
+            // per-dof gains and reset pose: uploaded when they change (a
+            // pageable copy, complete when the call returns; never inside a
+            // captured step, where the gains are fixed)
+            const mw::PidSet ps = pid_set(s);
+            mw::GLaneTask lt[mw::kMaxKernelDofs] = {};
+            for (int k = 0; k < s->n; ++k) {
+                lt[k].pid = ps.g[k];
+                lt[k].home = e->task.home[k];
+            }
+            if (!e->d_lane) MW_HIP(hipMalloc(reinterpret_cast<void**>(&e->d_lane), sizeof(lt)));
+            if (!e->lane_uploaded || std::memcmp(lt, e->h_lane, sizeof(lt)) != 0) {
+                std::memcpy(e->h_lane, lt, sizeof(lt));
+                MW_HIP(hipMemcpyAsync(e->d_lane, e->h_lane, sizeof(lt), hipMemcpyHostToDevice, s->stream));
+                e->lane_uploaded = true;
+            }
+            MW_HIP(mw::launch_vecenv_pid_group(s->d_params, s->n, needs_cons(s), needs_dual(s), e->task, s->dev,
+                                               e->dev, e->d_lane, static_cast<const float*>(a), o, r, d, to, s->W,
+                                               static_cast<float>(s->cfg.step_size), s->cfg.steps_per_run,
+                                               s->cfg.pgs_iters, s->stream));
+        }
         s->host_stale = true;
         s->iterations += s->cfg.steps_per_run;
         s->stepped = true;
