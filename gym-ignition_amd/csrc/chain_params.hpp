@@ -45,9 +45,13 @@ struct ChainF {
     int32_t n;
     int32_t flags;     // kHas* bits
     // lane-group kernels: bits 0-7 body whose origin is the common frame's,
-    // 8-15 segment nesting levels, 16-23 longest lane-order chain segment
+    // 8-15 segment nesting levels, 16-23 Hillis-Steele steps of the segmented
+    // scans; gtopo2: bits 0-7 the head parent of every level-1 segment + 1
+    // when there is exactly one (a DPP broadcast replaces the shuffle), 8-15
+    // the end of every subtree that ends before n + 1 when there is exactly
+    // one, bit 16 set when some subtree ends before n
     int32_t gtopo;
-    int32_t pad_;
+    int32_t gtopo2;
     float g[4];        // gravity in the base frame
     BodyF b[kMaxBodies];
 };
@@ -132,6 +136,19 @@ inline void group_topology_words(ChainF& P) {
     int steps = 0;  // Hillis-Steele steps of the segmented scans: 2^steps > maxh
     while ((1 << steps) <= maxh) ++steps;
     P.gtopo = ref | (levels << 8) | (steps << 16);
+    int fix = -2, dend = -2;  // -2: none yet, -1: more than one
+    bool diff = false;
+    for (int i = 0; i < n; ++i) {
+        const int hp = ((P.b[i].seg >> 8) & 0xff) - 1;
+        if (level[i] == 1) fix = (fix == -2 || fix == hp) ? hp : -1;
+        if (P.b[i].end < n) {
+            diff = true;
+            dend = (dend == -2 || dend == P.b[i].end) ? P.b[i].end : -1;
+        }
+    }
+    const int fixw = (levels == 1 && fix >= 0) ? fix + 1 : 0;
+    const int dendw = dend >= 0 ? dend + 1 : 0;
+    P.gtopo2 = fixw | (dendw << 8) | ((diff ? 1 : 0) << 16);
 }
 
 // the Franka Panda: joints 1..7 in a chain, both fingers hang off the hand

@@ -35,9 +35,7 @@ __global__ void __launch_bounds__(64) vecenv_pid_group_kernel(const ChainF* __re
     const int w = live ? wr : W - 1;
     const bool body = li < n;
     const GBody<N> B = load_gbody<N>(P, li, n);
-    const int gt = P->gtopo;
-    const GTopo TT = {(gt >> 16) & 0xff, (gt >> 8) & 0xff, gt & 0xff};
-    const bool diff = __any(body && B.end < n);
+    const GTopo TT = load_gtopo(P);
     PidF g{};
     float home = 0.f;
     if (body) {
@@ -68,7 +66,7 @@ __global__ void __launch_bounds__(64) vecenv_pid_group_kernel(const ChainF* __re
             else pu = u;
             tau = fminf(fmaxf(u, -B.effort), B.effort);
         }
-        group_substep<N, DUAL, CONS>(B, li, n, TT, diff, grav, q, qd, qlo, tau, dt, inv_dt, pgs_iters,
+        group_substep<N, DUAL, CONS>(B, li, n, TT, grav, q, qd, qlo, tau, dt, inv_dt, pgs_iters,
                                      prof);
     }
     MW_GPROF_T(k2);

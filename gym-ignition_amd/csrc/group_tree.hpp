@@ -179,7 +179,23 @@ __device__ __forceinline__ GBody<N> load_gbody(const ChainF* __restrict__ P, int
 // scans, the number of segment levels, the common frame's body
 struct GTopo {
     int steps, levels, ref;
+    int fix;   // the one head parent of the level-1 segments, or -1
+    int dend;  // the one subtree end before n, or -1
+    bool diff; // some subtree ends before n
 };
+__device__ __forceinline__ GTopo load_gtopo(const ChainF* __restrict__ P) {
+    const int a = P->gtopo, b = P->gtopo2;
+    return {(a >> 16) & 0xff, (a >> 8) & 0xff, a & 0xff, (b & 0xff) - 1, ((b >> 8) & 0xff) - 1, ((b >> 16) & 1) != 0};
+}
+
+// f(std::integral_constant<int, K>) for the uniform runtime lane k: one
+// uniform branch picks the instance, whose broadcasts are DPP row_newbcast:K
+template <class F>
+__device__ __forceinline__ void with_lane(int k, F&& f) {
+    sfor<kGroupLanes>([&](auto K) {
+        if (k == K) f(K);
+    });
+}
 
 // x_i <- sum of x over i and its ancestors
 template <int K, int N>
@@ -194,6 +210,15 @@ __device__ __forceinline__ void tree_prefix(float (&x)[K], const GBody<N>& B, co
     if (T.steps > 1) step(std::integral_constant<int, 2>{});
     if (T.steps > 2) step(std::integral_constant<int, 4>{});
     if (T.steps > 3) step(std::integral_constant<int, 8>{});
+    if (T.fix >= 0) {
+        // one level-1 segment head parent: DPP broadcasts
+        const float fm = (B.level == 1) ? 1.f : 0.f;
+        with_lane(T.fix, [&](auto L) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = fmaf(row_bcast<L>(x[k]), fm, x[k]);
+        });
+        return;
+    }
     for (int r = 1; r <= T.levels; ++r) {
         const bool fix = B.level == r;
         const float fm = fix ? 1.f : 0.f;
@@ -236,6 +261,16 @@ __device__ __forceinline__ void tree_poses(M3& R, f3& p, const GBody<N>& B, cons
     if (T.steps > 1) step(std::integral_constant<int, 2>{});
     if (T.steps > 2) step(std::integral_constant<int, 4>{});
     if (T.steps > 3) step(std::integral_constant<int, 8>{});
+    if (T.fix >= 0) {
+        with_lane(T.fix, [&](auto L) {
+            M3 Ra;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Ra.m[k] = row_bcast<L>(R.m[k]);
+            const f3 pa = {row_bcast<L>(p.x), row_bcast<L>(p.y), row_bcast<L>(p.z)};
+            compose_masked(Ra, pa, (B.level == 1) ? 1.f : 0.f, R, p);
+        });
+        return;
+    }
     for (int r = 1; r <= T.levels; ++r) {
         const bool fix = B.level == r;
         const int src = fix ? B.hp : li;
@@ -251,10 +286,17 @@ __device__ __forceinline__ void tree_poses(M3& R, f3& p, const GBody<N>& B, cons
 // suffix past the subtree's end (exact when the subtree runs to the row's
 // end or the rest is zero; diff: some body's subtree ends before n)
 template <int K>
-__device__ __forceinline__ void subtree_sum(float (&x)[K], int end, int li, bool diff) {
+__device__ __forceinline__ void subtree_sum(float (&x)[K], int end, int li, const GTopo& T) {
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = row_suffix(x[k]);
-    if (diff) {
+    if (T.dend >= 0) {
+        // one subtree end before n: DPP broadcasts
+        const float sm = (end == T.dend) ? 1.f : 0.f;
+        with_lane(T.dend, [&](auto L) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = fmaf(-row_bcast<L>(x[k]), sm, x[k]);
+        });
+    } else if (T.diff) {
         const bool sub = end < kGroupLanes;
         const float sm = sub ? 1.f : 0.f;
         const int src = sub ? end : li;
@@ -329,7 +371,7 @@ __device__ __forceinline__ SV gmul(const GI& I, const SV& V) {
 // Lane li (< n: body li) of a world.  q, qd, qlo: this lane's joint; tau its
 // force.  Returns with q, qd (and qlo) advanced by one substep.
 template <int N, bool DUAL, bool CONS>
-__device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, const GTopo& T, bool diff,
+__device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, const GTopo& T,
                                               f3 grav, float& q, float& qd, float& qlo, float tau, float dt,
                                               float inv_dt, int pgs_iters,
                                               unsigned long long (&prof)[kGroupProfPhases]) {
@@ -361,9 +403,7 @@ __device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, 
     // common frame: origin at body T.ref's origin (uniform: one DPP broadcast)
     {
         f3 pr = {0.f, 0.f, 0.f};
-        sfor<kGroupLanes>([&](auto K) {
-            if (T.ref == K) pr = {row_bcast<K>(p.x), row_bcast<K>(p.y), row_bcast<K>(p.z)};
-        });
+        with_lane(T.ref, [&](auto K) { pr = {row_bcast<K>(p.x), row_bcast<K>(p.y), row_bcast<K>(p.z)}; });
         p = p - pr;
     }
     MW_GPROF_T(t1);
@@ -385,7 +425,7 @@ __device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, 
     }
     // composite inertia of the subtree
     float ci[10] = {I.m, I.h.x, I.h.y, I.h.z, I.J.xx, I.J.yy, I.J.zz, I.J.xy, I.J.xz, I.J.yz};
-    subtree_sum<10>(ci, B.end, li, diff);
+    subtree_sum<10>(ci, B.end, li, T);
     const GI Ic = {ci[0], {ci[1], ci[2], ci[3]}, {ci[4], ci[5], ci[6], ci[7], ci[8], ci[9]}};
     const SV F = gmul(Ic, S);
     // rows of M (implicit: + dt d on the diagonal); padding lanes: unit rows
@@ -431,7 +471,7 @@ __device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, 
             const f3 fv = IA.v + cross(V.w, IV.v);
             f6[0] = fw.x; f6[1] = fw.y; f6[2] = fw.z; f6[3] = fv.x; f6[4] = fv.y; f6[5] = fv.z;
         }
-        subtree_sum<6>(f6, B.end, li, diff);
+        subtree_sum<6>(f6, B.end, li, T);
         hb = dot(S, SV{{f6[0], f6[1], f6[2]}, {f6[3], f6[4], f6[5]}});
     }
     MW_GPROF_T(t3);
@@ -469,27 +509,28 @@ __device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, 
         if (__any(on != 0u)) {
             if constexpr (DUAL) row_factor<N>(Cn, B);
             float mc[N], invd[N], rb0[N], rb2[N], lo0[N], hi0[N], a0m[N], a2m[N], x0[N], x2[N];
-            uint32_t need = 0u, rows0 = 0u, rows2 = 0u;  // dofs with a row in some world of the wave
+            // dofs with a limit / friction row in some world of the wave: the
+            // union of the four 16-lane slices of the ballots (scalar ops)
+            auto rows_of = [](uint64_t m) {
+                return static_cast<uint32_t>((m | (m >> 16) | (m >> 32) | (m >> 48)) & 0xffffu);
+            };
+            const uint32_t rows0 = rows_of(__ballot((on & 1u) != 0u));
+            const uint32_t rows2 = rows_of(__ballot((on & 4u) != 0u));
             const float onf0 = (on & 1u) ? 1.f : 0.f, onf2 = (on & 4u) ? 1.f : 0.f, upf = up ? 1.f : 0.f;
             sfor<N>([&](auto D) {
                 constexpr int d = D;
-                // row constants of dof d, uniform over the world's lanes
-                rb0[d] = row_bcast<d>(b0);
-                rb2[d] = row_bcast<d>(b2);
-                a0m[d] = row_bcast<d>(onf0);
-                a2m[d] = row_bcast<d>(onf2);
-                const float u = row_bcast<d>(upf);
-                lo0[d] = u != 0.f ? -kBig : 0.f;
-                hi0[d] = u != 0.f ? 0.f : kBig;
                 x0[d] = x2[d] = 0.f;
-                mc[d] = 0.f;
-                invd[d] = 0.f;
-                const bool r0 = __any(a0m[d] != 0.f), r2 = __any(a2m[d] != 0.f);
-                rows0 |= r0 ? (1u << d) : 0u;
-                rows2 |= r2 ? (1u << d) : 0u;
-                // M^-1 column d where some world of the wave has a row on dof d
-                if (r0 || r2) {
-                    need |= 1u << d;
+                mc[d] = invd[d] = rb0[d] = rb2[d] = a0m[d] = a2m[d] = lo0[d] = hi0[d] = 0.f;
+                if (((rows0 | rows2) >> d) & 1u) {
+                    // row constants of dof d, uniform over the world's lanes
+                    rb0[d] = row_bcast<d>(b0);
+                    rb2[d] = row_bcast<d>(b2);
+                    a0m[d] = row_bcast<d>(onf0);
+                    a2m[d] = row_bcast<d>(onf2);
+                    const float u = row_bcast<d>(upf);
+                    lo0[d] = u != 0.f ? -kBig : 0.f;
+                    hi0[d] = u != 0.f ? 0.f : kBig;
+                    // M^-1 column d
                     if constexpr (DUAL) mc[d] = row_solve<N, d>(Cn, B.eq[d], B);
                     else mc[d] = row_solve<N, d>(C, B.eq[d], B);
                     invd[d] = rcp(row_bcast<d>(mc[d]));
@@ -523,7 +564,6 @@ __device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, 
                 // fixed point of every one of them (chain_dyn.hpp: substep)
                 if (!__any(moved != 0.f)) break;
             }
-            (void)need;
             qd += dq;
             qdd += dq * inv_dt;
             MW_GPROF_T(t6);

@@ -27,9 +27,9 @@ def targets(q0, T):
     return tg.contiguous()
 
 
-def time_kernel(kind, W, G=100, reps=5):
+def time_kernel(kind, W, G=100, reps=5, **kw):
     os.environ["MWSTEP_PANDA_KERNEL"] = kind
-    env = VecEnv("PandaPositionTracking", n_worlds=W, seed=1, max_episode_steps=5000)
+    env = VecEnv("PandaPositionTracking", n_worlds=W, seed=1, max_episode_steps=5000, **kw)
     st = torch.cuda.Stream()
     env.sim.set_stream(st.cuda_stream)
     with torch.cuda.stream(st):
@@ -80,6 +80,12 @@ def main():
         a = time_kernel("lane", W)
         b = time_kernel("group", W)
         print(f"W={W}: lane {a:.2f} us/step, group {b:.2f} us/step ({a / b:.2f}x)", flush=True)
+    if os.environ.get("PANDA_VARIANTS"):
+        # cost structure of the group kernel at 1024 worlds: PGS sweeps, and
+        # the marginal cost of a second substep per launch
+        for label, kw in (("pgs 0", dict(pgs_iters=0)), ("pgs 1", dict(pgs_iters=1)),
+                          ("2 substeps", dict(physics_rate=2000.0)), ("4 substeps", dict(physics_rate=4000.0))):
+            print(f"  group W=1024 {label}: {time_kernel('group', 1024, **kw):.2f} us/step", flush=True)
 
 
 if __name__ == "__main__":

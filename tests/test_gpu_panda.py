@@ -337,6 +337,8 @@ def test_panda_baked_matches_generic(require_gpu, monkeypatch):
     import torch
     from mwstep.vecenv import VecEnv
     W, H = 512, 300
+    # the constant-folded kernels are the one-world-per-lane ones
+    monkeypatch.setenv("MWSTEP_PANDA_KERNEL", "lane")
     a = VecEnv("PandaPositionTracking", n_worlds=W, seed=4)
     b = VecEnv("PandaPositionTracking", n_worlds=W, seed=4)
     assert a.sim.baked_model() == 3
