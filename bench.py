@@ -106,7 +106,7 @@ def main():
     # stream around the timed graph replays (K launches), see time_steps()
     if env.action_dim:
         bpe = panda_bytes_per_env_step(env.sim.dofs)
-        kname = "vecenv_pid_step_kernel<9,PandaTopo,false,true>"
+        kname = "vecenv_pid_group_kernel<9,false,true> (one world per 16-lane row)"
     else:
         bpe = algorithmic_bytes_per_env_step(env.sim.dofs, env.obs_dim)
         kname = (f"vecenv_step_kernel<{env.sim.dofs},{env.kind},false,true,false,{env.sim.baked_model()}>"
@@ -315,6 +315,8 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
     G = max(1, min(chunk, K))
     n_chunks = (K + G - 1) // G
     groups = []
+    keep = []  # the CUDAGraph objects own the executables launched below
+    hip_runtime()
     for g, env in enumerate(envs):
         st = torch.cuda.Stream(device=dev)
         env.sim.set_stream(st.cuda_stream)
@@ -337,7 +339,8 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
             for graph in graphs:
                 graph.replay()
         st.synchronize()
-        groups.append((env, st, acts, graphs))
+        groups.append((env, st, acts, [g.raw_cuda_graph_exec() for g in graphs]))
+        keep.extend(graphs)
 
     if gather:
         # the first RCCL collective sets up its channels (milliseconds): do it
@@ -347,26 +350,28 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
             obs = torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs
             gather_obs(obs)
         torch.cuda.synchronize(dev)
+    ev_start, ev_end = hip_event(), hip_event()
+    ev_join = [hip_event() for _ in range(S - 1)]
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    # HIP events on group 0's launch stream bracket the timed region; the other
-    # groups join it through one event wait at the start and one at the end
+    # HIP events on group 0's launch stream bracket the timed region (raw
+    # hipEventRecord: torch's Event.record costs several us of host time per
+    # call); the other groups join it through one event wait at the start and
+    # one at the end
     st0 = groups[0][1]
-    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev_start.record(st0)
+    hip = hip_runtime()
+    hip.hipEventRecord(ev_start, st0.cuda_stream)
     for env, st, acts, graphs in groups[1:]:
-        st.wait_event(ev_start)
+        hip.hipStreamWaitEvent(st.cuda_stream, ev_start, 0)
     for c in range(n_chunks):
         for env, st, acts, graphs in groups:
-            with torch.cuda.stream(st):
-                graphs[c].replay()
-    for env, st, acts, graphs in groups[1:]:
-        e = torch.cuda.Event()
-        e.record(st)
-        st0.wait_event(e)
-    ev_end.record(st0)
+            launch_graph(graphs[c], st)
+    for (env, st, acts, graphs), ev in zip(groups[1:], ev_join):
+        hip.hipEventRecord(ev, st.cuda_stream)
+        hip.hipStreamWaitEvent(st0.cuda_stream, ev, 0)
+    hip.hipEventRecord(ev_end, st0.cuda_stream)
     if gather:
         with torch.cuda.stream(st0):
             obs = torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs
@@ -379,8 +384,57 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    return {"elapsed": elapsed, "kernel_us": ev_start.elapsed_time(ev_end) * 1e3 / K, "G": G,
+    del keep
+    kernel_us = hip_elapsed_ms(ev_start, ev_end) * 1e3 / K
+    for ev in [ev_start, ev_end] + ev_join:
+        hip_runtime().hipEventDestroy(ev)
+    return {"elapsed": elapsed, "kernel_us": kernel_us, "G": G,
             "stream": groups[0][1], "groups": S}
+
+
+_HIP = None
+
+
+def hip_runtime():
+    """The HIP runtime library (loaded once, before any timed region)."""
+    global _HIP
+    import ctypes
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipGraphLaunch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        _HIP.hipGraphLaunch.restype = ctypes.c_int
+        _HIP.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        _HIP.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        _HIP.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        _HIP.hipEventDestroy.argtypes = [ctypes.c_void_p]
+    return _HIP
+
+
+def hip_event():
+    """A timing hipEvent_t (raw handle)."""
+    import ctypes
+    ev = ctypes.c_void_p()
+    if hip_runtime().hipEventCreate(ctypes.byref(ev)) != 0:
+        raise RuntimeError("hipEventCreate failed")
+    return ev
+
+
+def hip_elapsed_ms(a, b):
+    import ctypes
+    ms = ctypes.c_float()
+    if hip_runtime().hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+        raise RuntimeError("hipEventElapsedTime failed")
+    return ms.value
+
+
+def launch_graph(exe, stream):
+    """hipGraphLaunch of a captured graph's executable (`raw_cuda_graph_exec()`,
+    fetched before the timed region) on `stream` through the HIP runtime
+    directly: torch's CUDAGraph.replay adds ~8 us of host work per call
+    (scripts/probe_short_run.py: a 20-step region 75.7 -> 67.9 us)."""
+    rc = _HIP.hipGraphLaunch(exe, stream.cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"hipGraphLaunch failed: {rc}")
 
 
 def launch_floor(dev, torch, K=2000, G=100):
@@ -441,7 +495,7 @@ def panda_leg(args, dev, torch, dist, world_size=1, rank=0, W_global=1024):
            "kernel_us_per_launch": round(r["kernel_us"], 3),
            "bytes_per_env_step": bpe, "achieved_GBs": round(gbs, 3),
            "hbm_frac": round(gbs / HBM_PEAK_GBS, 6), "groups": args.groups,
-           "kernel": "vecenv_pid_step_kernel<9,PandaTopo,false,true>"}
+           "kernel": "vecenv_pid_group_kernel<9,false,true> (one world per 16-lane row)"}
     tr = pmc_traffic("PandaPositionTracking", W)
     out["traffic"] = tr["bytes_per_launch"] if tr else None
     out["algorithmic_bytes_per_launch"] = bpe * W

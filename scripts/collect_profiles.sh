@@ -19,5 +19,5 @@ done
 python scripts/trace_summary.py "$G/prof_$tag/run_kernel_trace.csv" "$G/bench_prof_$tag.json" > "$P/trace_summary.json" || true
 python scripts/pmc_summary.py "$G/pmc_FETCH_SIZE_$tag" "$G/pmc_WRITE_SIZE_$tag" profiles/pmc_summary.json
 python scripts/pmc_summary.py "$G/pmc_panda_FETCH_SIZE_$tag" "$G/pmc_panda_WRITE_SIZE_$tag" profiles/pmc_summary_panda.json \
-  --kernel vecenv_pid_step_kernel --task PandaPositionTracking --worlds 1024
+  --kernel vecenv_pid_group_kernel --task PandaPositionTracking --worlds 1024
 ls -la "$P"
