@@ -9,6 +9,7 @@
 #include "group_tree.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
+#include "xcd.hpp"
 
 namespace mw {
 namespace dev {
@@ -28,13 +29,10 @@ __global__ void __launch_bounds__(64) vecenv_pid_group_kernel(const ChainF* __re
     unsigned long long prof[kGroupProfPhases] = {};
     MW_GPROF_T(k0);
     const int li = static_cast<int>(threadIdx.x) & (kGroupLanes - 1);
-    // XCD-aware world blocks: workgroups go round-robin to the 8 XCDs, each
-    // with its own L2; a 128-B line of a [dof][world] array holds 32 worlds =
-    // 8 workgroups, so consecutive world blocks are given to one XCD (else
-    // every XCD fetches and partially writes every line: 4.5x FETCH_SIZE)
-    const int nb = static_cast<int>(gridDim.x), bx = static_cast<int>(blockIdx.x);
-    const int xq = nb >> 3, xr = nb & 7, xcd = bx & 7;
-    const int wb = xcd * xq + (xcd < xr ? xcd : xr) + (bx >> 3);
+    // XCD-aware world blocks (xcd.hpp): a 128-B line of a [dof][world] array
+    // holds 32 worlds = 8 workgroups, which then share one XCD's L2 (else
+    // every XCD fetches and partially writes every line: 2.5x the traffic)
+    const int wb = xcd_block();
     // rows past the last world run on a copy of it (every lane of the wave
     // takes part in the row exchanges) and store nothing
     const int wr = static_cast<int>((wb * blockDim.x + threadIdx.x) / kGroupLanes);

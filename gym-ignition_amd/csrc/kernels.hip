@@ -21,6 +21,7 @@
 #include "kernels.hpp"
 #include "pid.hpp"
 #include "rng.hpp"
+#include "xcd.hpp"
 
 namespace mw {
 namespace dev {
@@ -589,7 +590,7 @@ template <int MAXN, bool CONS>
 __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
                                                       int N, SimDev S, FreeDev D, const PidF* __restrict__ pid,
                                                       int W, RunArgs A, int want_contacts, int* __restrict__ overflow) {
-    const int w = blockIdx.x;
+    const int w = xcd_block();  // XCD-aware (xcd.hpp): neighbouring worlds share state lines
     const int lane = lane_id();
     __shared__ WaveWorld<MAXN> L;
     FreeState base = load_base(D, W, w, A.first);

@@ -33,6 +33,7 @@
 //                    update = two lane reads, a clamp and one FMA per lane.
 #include <hip/hip_runtime.h>
 
+#include "xcd.hpp"
 #include "free_body.hpp"
 #include "kernels.hpp"
 #include "pid.hpp"
@@ -958,7 +959,7 @@ template <int MAXNV>
 __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict__ P, SceneDev D,
                                                        const PidF* __restrict__ pid, SceneGates G, int W,
                                                        SceneArgs A) {
-    const int w = blockIdx.x;
+    const int w = xcd_block();  // XCD-aware (xcd.hpp): neighbouring worlds share state lines
     const int lane = lane_id();
     __shared__ ScWorld<MAXNV> L;
     const int NB = P->n_bodies, NN = P->n_nodes;
