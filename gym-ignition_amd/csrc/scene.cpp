@@ -100,6 +100,8 @@ struct mw_scene {
     float* h_wrench = nullptr;
     float* h_contact = nullptr;
     int32_t* h_ncontact = nullptr;
+    int32_t* h_overflow = nullptr;  // pinned copy of the device drop counter
+    int64_t overflow_seen = 0;      // drops already reported
     mw::PidF* h_pid = nullptr;
     size_t jrows = 0;              // NBMAX * W
     // host-only component data
@@ -557,6 +559,10 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
                          hipHostMallocDefault));
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ncontact), W * sizeof(int32_t), hipHostMallocDefault));
     std::memset(s->h_ncontact, 0, W * sizeof(int32_t));
+    if (!s->h_overflow) {
+        SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int32_t), hipHostMallocDefault));
+        *s->h_overflow = 0;
+    }
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), NBMAX * sizeof(mw::PidF), hipHostMallocDefault));
     // device views
     float* j = static_cast<float*>(s->d_joint);
@@ -606,6 +612,7 @@ void mw_scene_destroy(mw_scene* s) {
     (void)hipHostFree(s->h_wrench);
     (void)hipHostFree(s->h_contact);
     (void)hipHostFree(s->h_ncontact);
+    (void)hipHostFree(s->h_overflow);
     (void)hipHostFree(s->h_pid);
     if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -877,9 +884,22 @@ int mw_scene_run(mw_scene* s, int32_t paused) {
     if (int rc = scene_run(s, paused, true)) return rc;
     if (s->models.empty()) return MW_OK;
     if (int rc = queue_readback(s)) return rc;
+    // the drop counter rides on the same synchronisation
+    SC_HIP(hipMemcpyAsync(s->h_overflow, s->dev.overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     if (int rc = sync(s)) return rc;
     clear_consumed(s);
     s->joints_stale = s->base_stale = false;
+    const int64_t dropped = *s->h_overflow;
+    if (dropped > s->overflow_seen) {
+        const int64_t d = dropped - s->overflow_seen;
+        s->overflow_seen = dropped;
+        char msg[256];
+        std::snprintf(msg, sizeof msg,
+                      "this run dropped %lld contact points / constraint rows: a world exceeded the per-step "
+                      "capacity (%d contact points, %d constraint rows)",
+                      static_cast<long long>(d), CMAX, mw::kScMaxRows);
+        return fail(MW_ECAPACITY, msg);
+    }
     return MW_OK;
 }
 

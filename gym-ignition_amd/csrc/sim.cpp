@@ -133,6 +133,8 @@ struct mw_sim {
     mw::PidF* h_pid = nullptr;    // pinned staging copy
     bool pid_dirty = true;        // gains changed since the last upload
     int* d_overflow = nullptr;    // constraint rows dropped by the wave kernel
+    int* h_overflow = nullptr;    // pinned copy read back with each synchronous run
+    int64_t overflow_seen = 0;    // drops already reported
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -531,6 +533,7 @@ void mw_destroy(mw_sim* s) {
         (void)hipFree(s->d_pid);
         (void)hipHostFree(s->h_pid);
         (void)hipFree(s->d_overflow);
+        (void)hipHostFree(s->h_overflow);
         (void)hipHostFree(s->h_base);
         (void)hipHostFree(s->h_cdata);
         (void)hipHostFree(s->h_cmask);
@@ -704,6 +707,8 @@ int mw_initialize(mw_sim* s) {
                                      hipHostMallocDefault));
                 MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), sizeof(int)));
                 MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
+                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int), hipHostMallocDefault));
+                *s->h_overflow = 0;
             } else {
                 const size_t words = static_cast<size_t>(mw::float_workspace_words(s->n, s->n_slots));
                 MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ws), words * W * sizeof(float)));
@@ -959,6 +964,8 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     if (readback) {
         MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
         if (s->float_tree && (rc = read_base(s, paused))) return rc;
+        if (s->h_overflow)
+            MW_HIP(hipMemcpyAsync(s->h_overflow, s->d_overflow, sizeof(int), hipMemcpyDeviceToHost, s->stream));
         MW_HIP(hipStreamSynchronize(s->stream));
         s->contacts_stale = false;
     } else {
@@ -972,6 +979,15 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     if (!paused) {
         s->iterations += s->cfg.steps_per_run;
         s->stepped = true;
+    }
+    if (readback && s->h_overflow && *s->h_overflow > s->overflow_seen) {
+        // DART keeps every contact: a run that dropped constraint rows fails
+        // loudly (the state has advanced without them)
+        const int64_t d = *s->h_overflow - s->overflow_seen;
+        s->overflow_seen = *s->h_overflow;
+        return fail(MW_ECAPACITY, "this run dropped " + std::to_string(d) +
+                                      " constraint rows: a world exceeded the per-step capacity of the "
+                                      "world-per-wavefront kernel (64 rows)");
     }
     return MW_OK;
 }
@@ -1083,6 +1099,8 @@ int mw_set_joint_param(mw_sim* s, int32_t dof, int32_t which, double value) {
                                      hipHostMallocDefault));
                 MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), sizeof(int)));
                 MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
+                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int), hipHostMallocDefault));
+                *s->h_overflow = 0;
                 s->pid_dirty = true;
             }
             s->wave = true;

@@ -16,7 +16,7 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__fi
 LIB_PATH = os.environ.get("MWSTEP_LIB", os.path.join(_PKG_ROOT, "libmwstep.so"))
 
 MW_OK = 0
-MW_EINVAL, MW_ESTATE, MW_EPARSE, MW_EHIP, MW_ENOTFOUND = 1, 2, 3, 4, 5
+MW_EINVAL, MW_ESTATE, MW_EPARSE, MW_EHIP, MW_ENOTFOUND, MW_ECAPACITY = 1, 2, 3, 4, 5, 6
 
 MODE_INVALID, MODE_IDLE, MODE_FORCE, MODE_VELOCITY = 0, 1, 2, 3
 MODE_VELOCITY_FOLLOWER_DART, MODE_POSITION, MODE_POSITION_INTERPOLATED = 4, 5, 6

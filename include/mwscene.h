@@ -127,7 +127,10 @@ int mw_scene_get_contacts(const mw_scene* sc, int32_t w, double* out, int32_t ca
  * max(1, ceil(duration / step_size)) physics steps from the next one. */
 int mw_scene_apply_world_wrench(mw_scene* sc, int32_t model, int32_t link, int32_t w0, int32_t nw,
                                 const double* wrench, double duration);
-/* contact points / constraint rows dropped so far (per-step capacity) */
+/* contact points / constraint rows dropped so far (per-step capacity).
+ * mw_scene_run returns MW_ECAPACITY when its run dropped any (the state has
+ * advanced; the error says how many were dropped); mw_scene_run_device, which
+ * does not synchronise, leaves the check to this counter. */
 int mw_scene_overflow(const mw_scene* sc, int64_t* dropped);
 
 #ifdef __cplusplus

@@ -37,6 +37,9 @@ extern "C" {
 #define MW_EPARSE 3      /* model file could not be parsed / unsupported    */
 #define MW_EHIP 4        /* HIP runtime failure                            */
 #define MW_ENOTFOUND 5   /* unknown joint / model / field name             */
+#define MW_ECAPACITY 6   /* a per-step capacity was exceeded: contact points /
+                            constraint rows were dropped (the step ran without
+                            them; DART would have kept them)                */
 
 /* JointControlMode, same numbering as scenario::core::JointControlMode
  * (cpp/scenario/core/include/scenario/core/Joint.h:37-75). */
@@ -198,7 +201,10 @@ int mw_get_contact_bodies(const mw_sim* sim, int32_t w, int32_t* bodies, int32_t
  * such a model), 1 one world per lane (small compiled trees), 2 one world per
  * wavefront (any tree of <= 48 bodies; MWSTEP_WAVE_TREE=1 forces it) -- and the
  * number of constraint rows the wave kernel dropped so far (its per-step
- * capacity is 64 active rows; 0 in every test and bench configuration). */
+ * capacity is 64 active rows; 0 in every test and bench configuration).
+ * mw_run returns MW_ECAPACITY when its run dropped rows (the state has
+ * advanced without them); mw_run_device, which does not synchronise, leaves
+ * the check to mw_constraint_overflow. */
 int mw_float_kernel(const mw_sim* sim, int32_t* kind);
 int mw_constraint_overflow(const mw_sim* sim, int64_t* rows);
 

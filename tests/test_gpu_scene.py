@@ -376,3 +376,20 @@ def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
     print(f"fixed 16-joint tree on the scene kernel, one step x{W}: max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
     assert wq <= 1e-5 and wqd <= 1e-4
     sc.close()
+
+
+def test_capacity_overflow_fails_loudly(require_gpu):
+    """A world with more contact points than the per-step capacity (8 cubes
+    side by side in face contact on the ground: 32 ground corners plus the
+    box-box face points) drops points; the synchronous run reports it
+    (MW_ECAPACITY -> RuntimeError naming the dropped count) instead of
+    stepping on silently, and the counter keeps the total."""
+    from mwstep import native as N
+    models = [(cube_urdf(), (0.1999 * k, 0.0, 0.0999, 1, 0, 0, 0), f"c{k}") for k in range(8)]
+    sc = _scene(models, 2)
+    with pytest.raises(RuntimeError, match="capacity"):
+        sc.run()
+    assert sc.overflow() > 0
+    err = N.lib().mw_last_error().decode()
+    assert "dropped" in err
+    sc.close()
