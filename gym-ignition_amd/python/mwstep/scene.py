@@ -52,6 +52,7 @@ class Scene:
     def insert_model(self, urdf: str, pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "",
                      worlds: Optional[Sequence[int]] = None) -> int:
         """World::insertModel into worlds [w0, w0 + nw) (default: all); returns the model index."""
+        self._touch()
         w0, nw = (0, self.n_worlds) if worlds is None else (worlds[0], worlds[1])
         p = np.ascontiguousarray(pose, dtype=np.float64)
         m = ctypes.c_int32()
@@ -80,16 +81,19 @@ class Scene:
 
     def set_present(self, m: int, present, w0: int = 0, nw: Optional[int] = None) -> None:
         """present: False / 0 remove, True / 1 (re-)insert at the insertion pose, 2 resume with the state kept"""
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         N.check(N.lib().mw_scene_set_present(self.handle, m, w0, nw, int(present)), "set_present")
 
     def replace_model(self, m: int, urdf: str, pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "") -> None:
+        self._touch()
         p = np.ascontiguousarray(pose, dtype=np.float64)
         N.check(N.lib().mw_scene_replace_model(self.handle, m, urdf.encode(), N.dptr(p), name.encode()),
                 "replace_model")
         self.models[m] = self._info(m)
 
     def set_world_ground(self, enabled: bool, w0: int = 0, nw: Optional[int] = None) -> None:
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         N.check(N.lib().mw_scene_set_world_ground(self.handle, w0, nw, 1 if enabled else 0), "set_world_ground")
 
@@ -107,9 +111,11 @@ class Scene:
 
     # ----------------------------------------------------------- stepping
     def run(self, paused: bool = False) -> None:
+        self._touch()
         N.check(N.lib().mw_scene_run(self.handle, 1 if paused else 0), "run")
 
     def run_device(self, runs: int = 1) -> None:
+        self._touch()
         N.check(N.lib().mw_scene_run_device(self.handle, runs), "run_device")
 
     def set_stream(self, stream: int) -> None:
@@ -126,10 +132,12 @@ class Scene:
         return g.tolist()
 
     def set_gravity(self, g: Sequence[float]) -> None:
+        self._touch()
         a = np.ascontiguousarray(g, dtype=np.float64)
         N.check(N.lib().mw_scene_set_gravity(self.handle, N.dptr(a)), "set_gravity")
 
     def set_ground_plane(self, enabled: bool = True, mu: float = 1.0) -> None:
+        self._touch()
         N.check(N.lib().mw_scene_set_ground_plane(self.handle, 1 if enabled else 0, float(mu)), "set_ground_plane")
 
     # ------------------------------------------------------------- joints
@@ -146,9 +154,35 @@ class Scene:
         local = range(info["dofs"]) if dofs is None else dofs
         return np.ascontiguousarray([info["first"] + d for d in local], dtype=np.int32)
 
+    # The joint state changes only through runs and the mutators below, so the
+    # per-env ScenarI/O path (a handful of getters per env step, each a C call
+    # into the host mirror of the last run) reads each state field once per
+    # run for small scenes and slices it.
+    _STATE = ("q", "qd", "qdd", "force")
+    _CACHE_MAX = 4096  # worlds x dofs of a cached field
+
+    def _touch(self) -> None:
+        self.__dict__.setdefault("_cache", {}).clear()
+
+    def _cached(self, what: str) -> Optional[np.ndarray]:
+        nd = sum(i["dofs"] for i in self.models)
+        if what not in self._STATE or nd == 0 or self.n_worlds * nd > self._CACHE_MAX:
+            return None
+        cache = self.__dict__.setdefault("_cache", {})
+        full = cache.get(what)
+        if full is None:
+            full = np.zeros((self.n_worlds, nd))
+            N.check(N.lib().mw_scene_get_joints(self.handle, self._FIELDS[what], 0, self.n_worlds, None, 0,
+                                                N.dptr(full)), f"get {what}")
+            cache[what] = full
+        return full
+
     def get(self, what: str, m: Optional[int] = None, w0: int = 0, nw: Optional[int] = None, dofs=None) -> np.ndarray:
         nw = self.n_worlds - w0 if nw is None else nw
         sel = self._sel(m, dofs)
+        full = self._cached(what)
+        if full is not None:
+            return full[w0:w0 + nw].copy() if sel is None else full[w0:w0 + nw][:, sel]
         nd = (sum(i["dofs"] for i in self.models) if sel is None else len(sel))
         out = np.zeros((nw, nd))
         if nd:
@@ -158,6 +192,7 @@ class Scene:
 
     def set(self, what: str, values, m: Optional[int] = None, w0: int = 0, nw: Optional[int] = None,
             dofs=None) -> None:
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         sel = self._sel(m, dofs)
         nd = (sum(i["dofs"] for i in self.models) if sel is None else len(sel))
@@ -167,6 +202,7 @@ class Scene:
 
     def set_control_mode(self, mode: int, m: Optional[int] = None, w0: int = 0, nw: Optional[int] = None,
                          dofs=None) -> None:
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         sel = self._sel(m, dofs)
         N.check(N.lib().mw_scene_set_control_mode(self.handle, w0, nw, N.iptr(sel),
@@ -178,6 +214,7 @@ class Scene:
         return v.value
 
     def set_pid(self, dof: int, gains) -> None:
+        self._touch()
         g = np.ascontiguousarray(gains, dtype=np.float64)
         N.check(N.lib().mw_scene_set_joint_pid(self.handle, dof, N.dptr(g)), "set_pid")
 
@@ -187,6 +224,7 @@ class Scene:
         return g
 
     def set_joint_param(self, dof: int, which: int, value: float) -> None:
+        self._touch()
         N.check(N.lib().mw_scene_set_joint_param(self.handle, dof, which, float(value)), "set_joint_param")
 
     def joint_param(self, dof: int, which: int) -> float:
@@ -195,6 +233,7 @@ class Scene:
         return v.value
 
     def set_controller_period(self, m: int, period: float) -> None:
+        self._touch()
         N.check(N.lib().mw_scene_set_controller_period(self.handle, m, float(period)), "set_controller_period")
 
     def controller_period(self, m: int) -> float:
@@ -216,11 +255,13 @@ class Scene:
         return out
 
     def reset_base_pose(self, m: int, pose, w0: int = 0, nw: Optional[int] = None) -> None:
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         p = np.ascontiguousarray(np.broadcast_to(np.asarray(pose, dtype=np.float64), (nw, 7)))
         N.check(N.lib().mw_scene_reset_base_pose(self.handle, m, w0, nw, N.dptr(p)), "reset_base_pose")
 
     def reset_base_velocity(self, m: int, lin_ang, w0: int = 0, nw: Optional[int] = None) -> None:
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         v = np.ascontiguousarray(np.broadcast_to(np.asarray(lin_ang, dtype=np.float64), (nw, 6)))
         N.check(N.lib().mw_scene_reset_base_velocity(self.handle, m, w0, nw, N.dptr(v)), "reset_base_velocity")
@@ -235,6 +276,7 @@ class Scene:
 
     def apply_world_wrench(self, m: int, link: int, wrench, duration: float, w0: int = 0,
                            nw: Optional[int] = None) -> None:
+        self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         v = np.ascontiguousarray(np.broadcast_to(np.asarray(wrench, dtype=np.float64), (nw, 6)))
         N.check(N.lib().mw_scene_apply_world_wrench(self.handle, m, link, w0, nw, N.dptr(v), float(duration)),
