@@ -75,7 +75,7 @@ struct FloatF {
     int32_t levels;
     int32_t fanout;
     int32_t dual;          // some joint has damping: impulses need the non-implicit inertias
-    int32_t pad2_;
+    int32_t fixed;         // the base is welded to the world (generic fixed-base trees, wave kernel)
     int8_t body_depth[kMaxBodies];
     int8_t body_srank[kMaxBodies];
     uint64_t body_path[kMaxBodies];  // bit k: body k is body i or one of its ancestors

@@ -1,4 +1,4 @@
-// model.cpp -- minimal XML reader + URDF -> chain compiler (see model.hpp).
+// model.cpp -- minimal XML reader + URDF / SDF -> tree compiler (see model.hpp).
 #include "model.hpp"
 
 #include <cctype>
@@ -16,6 +16,7 @@ namespace {
 // ------------------------------------------------------------------ XML ----
 struct XNode {
     std::string tag;
+    std::string text;  // character data directly inside the element (SDF values)
     std::map<std::string, std::string> attr;
     std::vector<std::unique_ptr<XNode>> kids;
 
@@ -126,7 +127,7 @@ private:
             if (starts("<![CDATA[")) { skip_until("]]>"); continue; }
             if (starts("<?")) { skip_until("?>"); continue; }
             if (s_[i_] == '<') { n->kids.push_back(element()); continue; }
-            ++i_;  // character data is not used by URDF
+            n->text.push_back(s_[i_++]);  // character data (SDF element values)
         }
     }
 };
@@ -265,23 +266,30 @@ std::string read_source(const std::string& s) {
     return ss.str();
 }
 
-}  // namespace
-
-ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
-    const std::string text = read_source(path_or_xml);
-    XmlReader rd(text);
-    auto root = rd.parse();
-    if (root->tag != "robot")
-        throw std::runtime_error("only URDF <robot> models are supported (got <" + root->tag + ">)");
-
-    ChainModel out;
-    out.name = root->get("name") ? *root->get("name") : "model";
-
+// The front-ends below describe a model the way URDF does: link contents in
+// the link frame, joint origins in the parent link frame, the child link frame
+// = the joint frame.  compile_description() then lumps fixed joints and numbers
+// the moving joints depth-first.
+struct Description {
+    std::string name;
     std::map<std::string, Link> links;
     std::vector<std::string> link_order;
+    std::vector<Joint> joints;
+    M3 R = eye();  // model pose in the world
+    V3 p{};
+};
+
+// ------------------------------------------------------------ URDF -----
+Description describe_urdf(const XNode* root, const double pose[7]) {
+    Description D;
+    D.name = root->get("name") ? *root->get("name") : "model";
+    D.R = quat_wxyz(pose[3], pose[4], pose[5], pose[6]);
+    D.p = {pose[0], pose[1], pose[2]};
+    std::map<std::string, Link>& links = D.links;
     for (const XNode* le : root->children("link")) {
         const std::string* nm = le->get("name");
         if (!nm) throw std::runtime_error("<link> without name");
+        if (links.count(*nm)) throw std::runtime_error("duplicate link '" + *nm + "'");
         Link L;
         if (const XNode* ine = le->child("inertial")) {
             const XNode* o = ine->child("origin");
@@ -321,10 +329,9 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
             L.shapes.push_back(sh);
         }
         links[*nm] = L;
-        link_order.push_back(*nm);
+        D.link_order.push_back(*nm);
     }
 
-    std::vector<Joint> joints;
     for (const XNode* je : root->children("joint")) {
         Joint J;
         const std::string* nm = je->get("name");
@@ -361,8 +368,261 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
             throw std::runtime_error("unsupported joint type '" + J.type + "' (" + J.name + ")");
         if (!links.count(J.parent) || !links.count(J.child))
             throw std::runtime_error("joint " + J.name + " references an unknown link");
-        joints.push_back(J);
+        D.joints.push_back(J);
     }
+    return D;
+}
+
+// ------------------------------------------------------------- SDF -----
+// SDF 1.6 / 1.7 frame semantics (sdformat, as read by World::insertModel ->
+// utils::getSdfRootFromString, cpp/scenario/gazebo/src/World.cpp:70-180):
+// <link><pose> is the link frame in the model frame, <joint><pose> the joint
+// frame in the CHILD link frame, <axis><xyz> is expressed in the joint frame
+// (or the model frame with <use_parent_model_frame> / expressed_in="__model__"),
+// <limit> and <dynamics> live inside <axis>; <inertial><pose> and
+// <collision><pose> are in the link frame.  A joint whose parent is "world"
+// attaches the model to the world where the model frame is placed.
+struct Pose3 {
+    M3 R = eye();
+    V3 p{};
+};
+Pose3 compose(const Pose3& a, const Pose3& b) { return {mul(a.R, b.R), add(mul(a.R, b.p), a.p)}; }
+Pose3 inverse(const Pose3& a) {
+    const M3 Rt = transpose(a.R);
+    return {Rt, scale(mul(Rt, a.p), -1.0)};
+}
+
+std::string trimmed(const std::string& s) {
+    const size_t b = s.find_first_not_of(" \t\r\n");
+    if (b == std::string::npos) return "";
+    const size_t e = s.find_last_not_of(" \t\r\n");
+    return s.substr(b, e - b + 1);
+}
+
+std::vector<double> sdf_numbers(const XNode* el, const char* tag, size_t n) {
+    const XNode* c = el ? el->child(tag) : nullptr;
+    if (!c) return {};
+    auto v = numbers(c->text);
+    if (v.size() != n)
+        throw std::runtime_error("expected " + std::to_string(n) + " numbers in <" + tag + ">");
+    return v;
+}
+
+double sdf_num(const XNode* el, const char* tag, double dflt) {
+    auto v = sdf_numbers(el, tag, 1);
+    return v.empty() ? dflt : v[0];
+}
+
+bool sdf_bool(const XNode* el, const char* tag, bool dflt) {
+    const XNode* c = el ? el->child(tag) : nullptr;
+    if (!c) return dflt;
+    const std::string t = trimmed(c->text);
+    return t == "1" || t == "true";
+}
+
+// <pose>x y z roll pitch yaw</pose> of `el` (identity when absent)
+Pose3 sdf_pose(const XNode* el, const std::string& what) {
+    const XNode* c = el ? el->child("pose") : nullptr;
+    if (!c) return {};
+    for (const char* a : {"relative_to", "frame"}) {
+        const std::string* rel = c->get(a);
+        if (rel && !rel->empty())
+            throw std::runtime_error("<pose " + std::string(a) + "=\"" + *rel + "\"> of " + what +
+                                     " is not supported (poses must use the default frames)");
+    }
+    auto v = numbers(c->text);
+    if (v.size() != 6) throw std::runtime_error("expected 6 numbers in the <pose> of " + what);
+    return {rpy({v[3], v[4], v[5]}), {v[0], v[1], v[2]}};
+}
+
+Description describe_sdf(const XNode* root, const double pose[7]) {
+    auto models = root->children("model");
+    if (models.empty())
+        throw std::runtime_error(root->child("world") ? "the SDF holds a <world>, not a <model>"
+                                                      : "The SDF does not contain a <model>");
+    if (models.size() > 1) throw std::runtime_error("the SDF holds several models");
+    const XNode* me = models[0];
+    if (me->child("model") || me->child("include"))
+        throw std::runtime_error("nested models and <include> are not supported");
+    Description D;
+    D.name = me->get("name") ? *me->get("name") : "model";
+    // World::insertModel: a non-identity insertion pose replaces the model's
+    // <pose> (World.cpp:169-177), the identity keeps it
+    const bool identity = pose[0] == 0.0 && pose[1] == 0.0 && pose[2] == 0.0 && pose[3] == 1.0 &&
+                          pose[4] == 0.0 && pose[5] == 0.0 && pose[6] == 0.0;
+    if (identity) {
+        const Pose3 X = sdf_pose(me, "model '" + D.name + "'");
+        D.R = X.R;
+        D.p = X.p;
+    } else {
+        D.R = quat_wxyz(pose[3], pose[4], pose[5], pose[6]);
+        D.p = {pose[0], pose[1], pose[2]};
+    }
+
+    // links: contents in the SDF link frame
+    std::map<std::string, Pose3> X_link;  // link frame in the model frame
+    std::map<std::string, Link> raw;
+    for (const XNode* le : me->children("link")) {
+        const std::string* nm = le->get("name");
+        if (!nm) throw std::runtime_error("<link> without name");
+        if (*nm == "world") throw std::runtime_error("a link may not be named 'world'");
+        if (raw.count(*nm)) throw std::runtime_error("duplicate link '" + *nm + "'");
+        X_link[*nm] = sdf_pose(le, "link '" + *nm + "'");
+        Link L;
+        // sdformat's defaults: mass 1, unit principal moments
+        L.mass = 1.0;
+        M3 Iin = eye();
+        Pose3 Xi;
+        if (const XNode* ine = le->child("inertial")) {
+            Xi = sdf_pose(ine, "the inertial of link '" + *nm + "'");
+            L.mass = sdf_num(ine, "mass", 1.0);
+            if (const XNode* ie = ine->child("inertia")) {
+                const double ixx = sdf_num(ie, "ixx", 1.0), iyy = sdf_num(ie, "iyy", 1.0),
+                             izz = sdf_num(ie, "izz", 1.0), ixy = sdf_num(ie, "ixy", 0.0),
+                             ixz = sdf_num(ie, "ixz", 0.0), iyz = sdf_num(ie, "iyz", 0.0);
+                Iin = {ixx, ixy, ixz, ixy, iyy, iyz, ixz, iyz, izz};
+            }
+        }
+        L.com = Xi.p;
+        L.I = mul(Xi.R, mul(Iin, transpose(Xi.R)));
+        for (const XNode* ce : le->children("collision")) {
+            const Pose3 Xc = sdf_pose(ce, "a collision of link '" + *nm + "'");
+            const XNode* ge = ce->child("geometry");
+            const XNode* box = ge ? ge->child("box") : nullptr;
+            const XNode* sph = ge ? ge->child("sphere") : nullptr;
+            Shape sh;
+            sh.R = Xc.R;
+            sh.p = Xc.p;
+            if (box) {
+                auto v = sdf_numbers(box, "size", 3);
+                if (v.empty()) v = {1.0, 1.0, 1.0};
+                sh.type = Shape::Box;
+                sh.size = {0.5 * v[0], 0.5 * v[1], 0.5 * v[2]};
+            } else if (sph) {
+                sh.type = Shape::Sphere;
+                sh.size = {sdf_num(sph, "radius", 1.0), 0.0, 0.0};
+            } else {
+                ++L.unsupported;
+                continue;
+            }
+            L.shapes.push_back(sh);
+        }
+        raw[*nm] = L;
+        D.link_order.push_back(*nm);
+    }
+    if (raw.empty()) throw std::runtime_error("model '" + D.name + "' has no links");
+
+    // joints: the joint frame X_J is given in the child link frame; the
+    // description's child link frame becomes the joint frame F(C) = X_C X_J
+    struct SJ {
+        Joint J;
+        Pose3 XJ;        // joint frame in the child link frame
+        V3 axis_raw{};   // as written
+        bool axis_model = false;
+    };
+    std::vector<SJ> sjs;
+    bool world_used = false;
+    for (const XNode* je : me->children("joint")) {
+        SJ s;
+        Joint& J = s.J;
+        const std::string* nm = je->get("name");
+        const std::string* ty = je->get("type");
+        if (!nm || !ty) throw std::runtime_error("malformed <joint>");
+        J.name = *nm;
+        J.type = *ty;
+        const XNode* pa = je->child("parent");
+        const XNode* ch = je->child("child");
+        if (!pa || !ch) throw std::runtime_error("joint " + J.name + " needs <parent> and <child>");
+        J.parent = trimmed(pa->text);
+        J.child = trimmed(ch->text);
+        if (J.parent == "world") world_used = true;
+        else if (!raw.count(J.parent)) throw std::runtime_error("joint " + J.name + " references an unknown link");
+        if (!raw.count(J.child)) throw std::runtime_error("joint " + J.name + " references an unknown link");
+        if (J.type != "fixed" && J.type != "revolute" && J.type != "continuous" && J.type != "prismatic")
+            throw std::runtime_error("unsupported joint type '" + J.type + "' (" + J.name + ")");
+        s.XJ = sdf_pose(je, "joint '" + J.name + "'");
+        const XNode* ax = je->child("axis");
+        if (J.type != "fixed") {
+            auto v = sdf_numbers(ax, "xyz", 3);
+            s.axis_raw = v.empty() ? V3{0, 0, 1} : V3{v[0], v[1], v[2]};
+            const XNode* xe = ax ? ax->child("xyz") : nullptr;
+            const std::string* ei = xe ? xe->get("expressed_in") : nullptr;
+            s.axis_model = sdf_bool(ax, "use_parent_model_frame", false) || (ei && *ei == "__model__");
+            if (ei && !ei->empty() && *ei != "__model__" && *ei != J.name)
+                throw std::runtime_error("joint " + J.name + ": axis expressed_in=\"" + *ei + "\" is not supported");
+            if (const XNode* lim = ax ? ax->child("limit") : nullptr) {
+                J.effort = sdf_num(lim, "effort", -1.0);
+                J.velocity = sdf_num(lim, "velocity", -1.0);
+                J.lower = sdf_num(lim, "lower", -1e16);
+                J.upper = sdf_num(lim, "upper", 1e16);
+            } else {
+                J.effort = J.velocity = -1.0;
+                J.lower = -1e16;
+                J.upper = 1e16;
+            }
+            // a negative effort / velocity is not enforced (SDF spec)
+            if (J.effort < 0.0) J.effort = 1e300;
+            if (J.velocity < 0.0) J.velocity = 1e300;
+            if (J.type == "revolute" && J.lower <= -1e16 && J.upper >= 1e16) J.type = "continuous";
+            if (J.type == "continuous") { J.lower = -1e300; J.upper = 1e300; }
+            if (J.type == "prismatic") {
+                if (J.lower <= -1e16) J.lower = -1e300;
+                if (J.upper >= 1e16) J.upper = 1e300;
+            }
+            if (const XNode* dyn = ax ? ax->child("dynamics") : nullptr) {
+                J.damping = sdf_num(dyn, "damping", 0.0);
+                J.friction = sdf_num(dyn, "friction", 0.0);
+            }
+        }
+        sjs.push_back(s);
+    }
+
+    // the description frame of every link: the joint frame for a child link,
+    // the model frame for the root (its contents move by its link pose)
+    std::map<std::string, Pose3> F;
+    std::map<std::string, int> parent_joint;
+    for (size_t k = 0; k < sjs.size(); ++k) {
+        const SJ& s = sjs[k];
+        if (parent_joint.count(s.J.child))
+            throw std::runtime_error("link '" + s.J.child + "' is the child of several joints");
+        parent_joint[s.J.child] = static_cast<int>(k);
+        F[s.J.child] = compose(X_link[s.J.child], s.XJ);
+    }
+    for (auto& n : D.link_order)
+        if (!F.count(n)) F[n] = Pose3{};
+    F["world"] = Pose3{};
+
+    if (world_used) {
+        D.links["world"] = Link{};
+        D.link_order.insert(D.link_order.begin(), "world");
+    }
+    for (auto& n : D.link_order) {
+        if (n == "world") continue;
+        const Pose3 Xc = compose(inverse(F[n]), X_link[n]);  // SDF link frame in F(n)
+        D.links[n] = lump(Link{}, raw[n], Xc.R, Xc.p);
+    }
+    for (SJ& s : sjs) {
+        Joint J = s.J;
+        const Pose3 O = compose(inverse(F[J.parent]), F[J.child]);
+        J.R = O.R;
+        J.p = O.p;
+        if (J.type != "fixed") {
+            V3 a = s.axis_model ? mul(transpose(F[J.child].R), s.axis_raw) : s.axis_raw;
+            const double an = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+            if (an == 0.0) throw std::runtime_error("zero joint axis in " + J.name);
+            J.axis = scale(a, 1.0 / an);
+        }
+        D.joints.push_back(J);
+    }
+    return D;
+}
+
+ChainModel compile_description(Description D) {
+    ChainModel out;
+    out.name = D.name;
+    std::map<std::string, Link>& links = D.links;
+    const std::vector<std::string>& link_order = D.link_order;
+    std::vector<Joint>& joints = D.joints;
 
     // root link
     std::map<std::string, int> is_child;
@@ -372,22 +632,26 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
         if (!is_child.count(n)) roots.push_back(n);
     if (roots.size() != 1) throw std::runtime_error("the model must have exactly one root link");
 
-    M3 baseR = quat_wxyz(pose[3], pose[4], pose[5], pose[6]);
-    V3 baseP{pose[0], pose[1], pose[2]};
+    M3 baseR = D.R;
+    V3 baseP = D.p;
     std::string base = roots[0];
     if (base == "world") {
-        int found = -1;
+        int found = -1, attached = 0;
         for (size_t k = 0; k < joints.size(); ++k)
             if (joints[k].parent == "world") {
-                if (found >= 0) throw std::runtime_error("more than one joint attached to 'world'");
+                ++attached;
                 found = static_cast<int>(k);
             }
-        if (found < 0 || joints[found].type != "fixed")
-            throw std::runtime_error("the 'world' link must be attached by one fixed joint");
-        baseP = add(baseP, mul(baseR, joints[found].p));
-        baseR = mul(baseR, joints[found].R);
-        base = joints[found].child;
-        joints.erase(joints.begin() + found);
+        if (attached == 0) throw std::runtime_error("nothing is attached to the 'world' link");
+        if (attached == 1 && joints[found].type == "fixed") {
+            // the usual fixed base: the welded link is the base body
+            baseP = add(baseP, mul(baseR, joints[found].p));
+            baseR = mul(baseR, joints[found].R);
+            base = joints[found].child;
+            joints.erase(joints.begin() + found);
+        }
+        // otherwise the massless 'world' link itself is the fixed base and the
+        // joints attached to it hang from the model frame
     } else {
         // floating base: the root link moves with a free joint; its world pose is
         // the insertion pose (World::insertModel, World.cpp:70-180)
@@ -490,6 +754,17 @@ ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
         if (owner[kv.first] == kv.first) out.unsupported_shapes += kv.second.unsupported;
     if (out.bodies.empty() && !out.floating) throw std::runtime_error("the model has no moving joints");
     return out;
+}
+
+}  // namespace
+
+ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
+    const std::string text = read_source(path_or_xml);
+    XmlReader rd(text);
+    auto root = rd.parse();
+    if (root->tag == "robot") return compile_description(describe_urdf(root.get(), pose));
+    if (root->tag == "sdf") return compile_description(describe_sdf(root.get(), pose));
+    throw std::runtime_error("expected a URDF <robot> or an SDF <sdf> model (got <" + root->tag + ">)");
 }
 
 }  // namespace mw

@@ -1,4 +1,4 @@
-// model.hpp -- host-side model compiler: URDF -> flat fixed-base kinematic tree.
+// model.hpp -- host-side model compiler: URDF or SDF -> flat kinematic tree.
 //
 // Mirrors what the reference does when a URDF is inserted
 // (World::insertModel, cpp/scenario/gazebo/src/World.cpp:70-180 ->
@@ -66,7 +66,9 @@ struct ChainModel {
     int dofs() const { return static_cast<int>(bodies.size()); }
 };
 
-// Parse a URDF file path or inline URDF string.  pose = {x,y,z,qw,qx,qy,qz}.
+// Parse a URDF or SDF model (file path or inline string).  pose =
+// {x,y,z,qw,qx,qy,qz}; for SDF the identity keeps the model's <pose>
+// (World::insertModel, World.cpp:169-177).
 // Throws std::runtime_error with a message on unsupported / malformed input.
 ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]);
 

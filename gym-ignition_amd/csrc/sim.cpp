@@ -121,6 +121,12 @@ struct mw_sim {
     // articulated models on a floating base (float_tree.hpp): the joint state
     // of a fixed-base model plus the base block above
     bool float_tree = false;
+    // a fixed-base tree outside the compiled chain topologies (more than 9
+    // dofs, or branched other than the Panda): the world-per-wavefront kernel
+    // with a welded base (FloatF::fixed); its joint and base state live where a
+    // floating tree's do
+    bool fixed_tree = false;
+    bool fbase() const { return floating || fixed_tree; }
     mw::FloatF h_float{};
     mw::FloatF* d_float = nullptr;
     float* d_ws = nullptr;        // constraint-row workspace [words][W]
@@ -345,6 +351,7 @@ void build_float(mw_sim* s) {
     F.dual = 0;
     for (int i = 0; i < n; ++i)
         if (M.bodies[i].damping != 0.0) F.dual = 1;
+    F.fixed = s->fixed_tree ? 1 : 0;
 }
 
 int upload_params(mw_sim* s) {
@@ -391,7 +398,7 @@ int baked_id(const mw_sim* s) {
 
 int pull_state(mw_sim* s) {
     if (!s->host_stale) return MW_OK;
-    if (s->floating) {
+    if (s->fbase()) {
         MW_HIP(hipMemcpyAsync(s->h_base, s->fdev.base, 13 * static_cast<size_t>(s->W) * sizeof(float),
                               hipMemcpyDeviceToHost, s->stream));
         if (!s->float_tree) {
@@ -551,10 +558,19 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     } catch (const std::exception& e) {
         return fail(MW_EPARSE, e.what());
     }
-    if (s->model.dofs() > 9 && !(s->model.floating && s->model.dofs() <= mw::kMaxBodies))
-        return fail(MW_EPARSE, "fixed-base models with more than 9 dofs are not supported by this build");
+    if (s->model.dofs() > mw::kMaxBodies)
+        return fail(MW_EPARSE, "models with more than " + std::to_string(mw::kMaxBodies) +
+                                   " moving joints are not supported by this build");
     s->floating = s->model.floating;
-    s->float_tree = s->floating && s->model.dofs() > 0;
+    s->fixed_tree = false;
+    if (!s->floating) {
+        // fixed bases: the compiled chain topologies run on the lane kernels,
+        // every other tree on the world-per-wavefront kernel with a welded base
+        std::vector<int> parents;
+        for (const auto& b : s->model.bodies) parents.push_back(b.parent);
+        s->fixed_tree = s->model.dofs() > 9 || mw::kernel_topology(parents.data(), s->model.dofs()) < 0;
+    }
+    s->float_tree = (s->floating && s->model.dofs() > 0) || s->fixed_tree;
     if (s->float_tree) {
         std::vector<int> parents;
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
@@ -566,12 +582,12 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
             damped = damped || b.damping != 0.0;
         }
         if (n_shapes > static_cast<size_t>(mw::kMaxFloatShapes))
-            return fail(MW_EPARSE, "a floating-base model may have at most " +
+            return fail(MW_EPARSE, "an articulated model may have at most " +
                                        std::to_string(mw::kMaxFloatShapes) + " box / sphere collision shapes");
         s->n = s->model.dofs();
         build_float(s);
         if (s->h_float.n_slots > mw::kMaxFloatSlots)
-            return fail(MW_EPARSE, "a floating-base model may have at most " + std::to_string(mw::kMaxFloatSlots) +
+            return fail(MW_EPARSE, "an articulated model may have at most " + std::to_string(mw::kMaxFloatSlots) +
                                        " contact slots (8 per box, 1 per sphere)");
         // small compiled topologies: one world per lane (float_tree.hpp); any
         // other tree: one world per wavefront (wave_tree.hpp)
@@ -588,6 +604,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
             s->wave = !compiled || *force_wave != '0' || damped;
         else
             s->wave = !compiled || s->W <= kWaveWorldsMax || damped;
+        if (s->fixed_tree) s->wave = true;  // the lane kernel has no welded-base mode
         {
             std::vector<int> depth(s->n, 0);
             int max_depth = 0;
@@ -598,7 +615,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
             }
             s->wave_depth_ok = max_depth <= mw::kWaveMaxDepthHost;
             if (s->wave && !s->wave_depth_ok)
-                return fail(MW_EPARSE, "the kinematic tree of this floating-base model is deeper than " +
+                return fail(MW_EPARSE, "the kinematic tree of this model is deeper than " +
                                            std::to_string(mw::kWaveMaxDepthHost) + " joints");
         }
         s->n_slots = s->h_float.n_slots;
@@ -694,7 +711,7 @@ int mw_initialize(mw_sim* s) {
         s->stream_set = true;
     }
     s->n = s->model.dofs();
-    if (s->floating) {
+    if (s->fbase()) {
         const size_t W = static_cast<size_t>(s->W);
         const size_t ns = static_cast<size_t>(s->n_slots);
         const size_t nf = (13 + 7 + 6 + 7 * ns) * W;
@@ -1161,6 +1178,36 @@ int mw_model_export(const mw_sim* s, double* out, int32_t len) {
     return MW_OK;
 }
 
+int mw_model_export_base(const mw_sim* s, double* out) {
+    if (!s || !out) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    const mw::ChainModel& m = s->model;
+    double* o = out;
+    *o++ = m.floating ? 1.0 : 0.0;
+    for (double v : m.base_R) *o++ = v;
+    for (double v : m.base_p) *o++ = v;
+    *o++ = m.base_mass;
+    for (double v : m.base_com) *o++ = v;
+    for (double v : m.base_Ic) *o++ = v;
+    return MW_OK;
+}
+
+int mw_model_export_shapes(const mw_sim* s, int32_t body, double* out, int32_t max_shapes, int32_t* count) {
+    if (!s || !count || (max_shapes > 0 && !out)) return fail(MW_EINVAL, "null argument");
+    if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (body < -1 || body >= s->model.dofs()) return fail(MW_EINVAL, "body index out of range");
+    const std::vector<mw::Shape>& sh = body < 0 ? s->model.base_shapes : s->model.bodies[body].shapes;
+    *count = static_cast<int32_t>(sh.size());
+    for (int32_t k = 0; k < std::min<int32_t>(max_shapes, *count); ++k) {
+        double* o = out + 16 * k;
+        *o++ = static_cast<double>(sh[k].type);
+        for (double v : sh[k].size) *o++ = v;
+        for (double v : sh[k].R) *o++ = v;
+        for (double v : sh[k].p) *o++ = v;
+    }
+    return MW_OK;
+}
+
 int mw_get_joint_positions(const mw_sim* cs, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, double* out) {
     mw_sim* s = const_cast<mw_sim*>(cs);
     return getter(s, w0, nw, d, nd, out, [&](int dof, int w) { return double(s->hq()[s->idx(dof, w)]); });
@@ -1376,10 +1423,42 @@ int mw_is_floating(const mw_sim* s, int32_t* floating) {
 
 static float* base_at(const mw_sim* s, int f, int w) { return s->h_base + static_cast<size_t>(f) * s->W + w; }
 
+// the base of a fixed-base model is the model frame, at rest (Model::basePosition
+// reads the model's Pose component, Model.cpp:976-994)
+static int fixed_base_pose(const mw_sim* s, int32_t w0, int32_t nw, double* out, bool velocity) {
+    if (!out || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null output");
+    const auto& R = s->model.base_R;
+    const double tr = R[0] + R[4] + R[8];
+    double q[4];
+    if (tr > 0) {
+        const double k = 0.5 / std::sqrt(tr + 1.0);
+        q[0] = 0.25 / k; q[1] = (R[7] - R[5]) * k; q[2] = (R[2] - R[6]) * k; q[3] = (R[3] - R[1]) * k;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        const double k = 2.0 * std::sqrt(1.0 + R[0] - R[4] - R[8]);
+        q[0] = (R[7] - R[5]) / k; q[1] = 0.25 * k; q[2] = (R[1] + R[3]) / k; q[3] = (R[2] + R[6]) / k;
+    } else if (R[4] > R[8]) {
+        const double k = 2.0 * std::sqrt(1.0 + R[4] - R[0] - R[8]);
+        q[0] = (R[2] - R[6]) / k; q[1] = (R[1] + R[3]) / k; q[2] = 0.25 * k; q[3] = (R[5] + R[7]) / k;
+    } else {
+        const double k = 2.0 * std::sqrt(1.0 + R[8] - R[0] - R[4]);
+        q[0] = (R[3] - R[1]) / k; q[1] = (R[2] + R[6]) / k; q[2] = (R[5] + R[7]) / k; q[3] = 0.25 * k;
+    }
+    for (int32_t k = 0; k < nw; ++k) {
+        if (velocity) {
+            for (int f = 0; f < 6; ++f) out[6 * k + f] = 0.0;
+        } else {
+            for (int f = 0; f < 3; ++f) out[7 * k + f] = s->model.base_p[f];
+            for (int f = 0; f < 4; ++f) out[7 * k + 3 + f] = q[f];
+        }
+    }
+    return MW_OK;
+}
+
 int mw_get_base_pose(const mw_sim* cs, int32_t w0, int32_t nw, double* out) {
     mw_sim* s = const_cast<mw_sim*>(cs);
-    int rc = check_free(s);
+    int rc = check_sim(s);
     if (rc) return rc;
+    if (!s->floating) return fixed_base_pose(s, w0, nw, out, false);
     if (!out || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null output");
     if ((rc = pull_state(s))) return rc;
     // Model::basePosition / baseOrientation (Model.cpp:976-994): x y z, qw qx qy qz
@@ -1390,8 +1469,9 @@ int mw_get_base_pose(const mw_sim* cs, int32_t w0, int32_t nw, double* out) {
 
 int mw_get_base_velocity(const mw_sim* cs, int32_t w0, int32_t nw, double* out) {
     mw_sim* s = const_cast<mw_sim*>(cs);
-    int rc = check_free(s);
+    int rc = check_sim(s);
     if (rc) return rc;
+    if (!s->floating) return fixed_base_pose(s, w0, nw, out, true);
     if (!out || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad world range or null output");
     if ((rc = pull_state(s))) return rc;
     // Model::baseWorldLinearVelocity / baseWorldAngularVelocity (Model.cpp:1024-1075):
@@ -1450,7 +1530,7 @@ int mw_set_ground_plane(mw_sim* s, int32_t enabled, double mu) {
     if (!(mu >= 0.0)) return fail(MW_EINVAL, "the friction coefficient must be >= 0");
     s->ground = enabled != 0;
     s->ground_mu = mu;
-    if (s->floating && s->initialized) return upload_params(s);
+    if (s->fbase() && s->initialized) return upload_params(s);
     if (s->float_tree && s->loaded) build_float(s);
     else if (s->floating && s->loaded) build_free(s);
     return MW_OK;
@@ -1476,7 +1556,7 @@ int mw_get_contacts(const mw_sim* s, int32_t w, double* out, int32_t cap, int32_
     if (!n || (cap > 0 && !out)) return fail(MW_EINVAL, "null argument");
     if (w < 0 || w >= s->W) return fail(MW_EINVAL, "world index out of range");
     *n = 0;
-    if (!s->floating || !s->contacts) return MW_OK;
+    if (!s->fbase() || !s->contacts) return MW_OK;
     if (s->contacts_stale) {
         mw_sim* m = const_cast<mw_sim*>(s);
         const size_t Wc = static_cast<size_t>(s->W);
@@ -1516,7 +1596,7 @@ int mw_get_contact_bodies(const mw_sim* s, int32_t w, int32_t* out, int32_t cap,
     int32_t total = 0;
     // the same slot walk as mw_get_contacts (fills the host mirror if stale)
     if ((rc = mw_get_contacts(s, w, scratch, 0, &total))) return rc;
-    const uint32_t mask = (s->floating && s->contacts) ? s->h_cmask[w] : 0u;
+    const uint32_t mask = (s->fbase() && s->contacts) ? s->h_cmask[w] : 0u;
     int32_t k = 0;
     for (int slot = 0; slot < s->n_slots; ++slot) {
         if (!((mask >> slot) & 1u)) continue;

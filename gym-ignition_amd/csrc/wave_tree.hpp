@@ -228,17 +228,22 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
             }
         }
     }
-    SI IA0 = rigid_base(*F);
-    IA0 += L.acc[MAXN].I;
-    const SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
-                             Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
-                  L.acc[MAXN].B;
-    L0.factor(IA0);
-    const SV a0 = L0.solve(-1.f * B0);
-    if (dual) {
-        SI IA0n = rigid_base(*F);
-        IA0n += L.acc[MAXN].In;
-        L0.factor(IA0n);  // L0 leaves with the impulses' (non-implicit) base inertia
+    // a welded base (F->fixed: generic fixed-base trees) does not move: a0 = 0
+    // and it absorbs every impulse (wave_response), V0 stays 0
+    SV a0 = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    if (!F->fixed) {
+        SI IA0 = rigid_base(*F);
+        IA0 += L.acc[MAXN].I;
+        const SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
+                                 Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
+                      L.acc[MAXN].B;
+        L0.factor(IA0);
+        a0 = L0.solve(-1.f * B0);
+        if (dual) {
+            SI IA0n = rigid_base(*F);
+            IA0n += L.acc[MAXN].In;
+            L0.factor(IA0n);  // L0 leaves with the impulses' (non-implicit) base inertia
+        }
     }
     // outward: accelerations (the V record now carries a)
     for (int d = 0; d < levels; ++d) {
@@ -300,7 +305,7 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
     Jrow[0] = Fi.w.x; Jrow[1] = Fi.w.y; Jrow[2] = Fi.w.z; Jrow[3] = Fi.v.x; Jrow[4] = Fi.v.y; Jrow[5] = Fi.v.z;
     jv += Fi.w.x * L.nu[0] + Fi.w.y * L.nu[1] + Fi.w.z * L.nu[2] + Fi.v.x * L.nu[3] + Fi.v.y * L.nu[4] +
           Fi.v.z * L.nu[5];
-    const SV dV0 = L0.solve(-1.f * Bi);
+    const SV dV0 = F->fixed ? SV{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}} : L0.solve(-1.f * Bi);
     MJrow[0] = dV0.w.x; MJrow[1] = dV0.w.y; MJrow[2] = dV0.w.z;
     MJrow[3] = dV0.v.x; MJrow[4] = dV0.v.y; MJrow[5] = dV0.v.z;
     SV dv_prev = dV0;

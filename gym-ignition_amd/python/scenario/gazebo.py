@@ -89,6 +89,18 @@ def _read(path_or_string: str) -> str:
         return f.read()
 
 
+def _sdf_model_pose(root) -> core.Pose:
+    """<model><pose>x y z roll pitch yaw</pose> as a Pose (wxyz)."""
+    pe = root.find("model/pose")
+    v = [float(x) for x in pe.text.split()] if pe is not None and pe.text and pe.text.strip() else [0.0] * 6
+    cr, sr = math.cos(v[3] / 2), math.sin(v[3] / 2)
+    cp, sp = math.cos(v[4] / 2), math.sin(v[4] / 2)
+    cy, sy = math.cos(v[5] / 2), math.sin(v[5] / 2)
+    q = [cr * cp * cy + sr * sp * sy, sr * cp * cy - cr * sp * sy,
+         cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy]
+    return core.Pose(v[:3], q)
+
+
 def get_world_name_from_sdf(sdf: str, world_index: int = 0) -> str:
     root = ET.fromstring(_read(sdf).strip())
     worlds = root.findall("world")
@@ -837,6 +849,9 @@ class World:
         self._gravity = [0.0, 0.0, -9.8]
         self._ground_mu = None     # a static model with a plane collision is in the world
         self._ground_name = None
+        # removed models stay listed until the next (paused or unpaused) run
+        # processes the removal request (World::removeModel, World.cpp:432-453)
+        self._removing: List[str] = []
 
     def to_gazebo(self) -> "World":
         return self
@@ -865,7 +880,7 @@ class World:
         return True
 
     def model_names(self) -> List[str]:
-        return list(self._models.keys())
+        return list(self._models.keys()) + [n for n in self._removing if n not in self._models]
 
     def get_model(self, model_name: str):
         if model_name not in self._models:
@@ -927,11 +942,11 @@ class World:
         if name in self._models:
             _err(f"Model '{name}' already exists in world '{self._name}'")
             return False
-        if root.tag != "robot":
-            static = (root.find("model/static") is not None and
-                      root.find("model/static").text.strip().lower() in ("1", "true"))
-            if not static or root.findall("model/joint"):
-                _err("only static SDF models and URDF robots are supported by this build")
+        static = root.tag != "robot" and (root.find("model/static") is not None and
+                                          root.find("model/static").text.strip().lower() in ("1", "true"))
+        if static:
+            if root.findall("model/joint"):
+                _err("static SDF models with joints are not supported by this build")
                 return False
             self._models[name] = StaticModel(name, pose)
             plane = root.find("model/link/collision/geometry/plane")
@@ -943,6 +958,9 @@ class World:
                 self._ground_name = f"{name}::{link.get('name', 'link')}"
                 self._simulator._set_ground(self, True, self._ground_mu)
             return True
+        if root.tag != "robot" and [float(v) for v in (*pose.position, *pose.orientation)] == [0, 0, 0, 1, 0, 0, 0]:
+            # the identity keeps the SDF model's own <pose> (World.cpp:169-177)
+            pose = _sdf_model_pose(root)
         try:
             view = self._simulator._place_model(self, model_string,
                                                 list(pose.position) + list(pose.orientation), name)
@@ -958,6 +976,7 @@ class World:
             return False
         removed = self._models.pop(model_name)
         removed._close()
+        self._removing.append(model_name)
         if self._ground_name is not None and self._ground_name.split("::")[0] == model_name:
             self._ground_mu = self._ground_name = None
             self._simulator._set_ground(self, False, 1.0)
@@ -965,6 +984,7 @@ class World:
 
     # called by GazeboSimulator.run before the scene steps
     def _update(self, paused: bool, sim_time_ns: int) -> None:
+        self._removing.clear()
         if not self._physics:
             return
         self._time_ns = sim_time_ns

@@ -294,13 +294,147 @@ class ChainModel:
         return self.model.n
 
 
+def _mat_to_rpy(R: np.ndarray) -> np.ndarray:
+    """Inverse of _rpy (R = Rz(y) Ry(p) Rx(r))."""
+    p = math.asin(max(-1.0, min(1.0, -R[2, 0])))
+    return np.array([math.atan2(R[2, 1], R[2, 2]), p, math.atan2(R[1, 0], R[0, 0])])
+
+
+def _sdf_pose(el) -> np.ndarray:
+    """4x4 homogeneous transform of the <pose> child of `el` (x y z r p y)."""
+    T = np.eye(4)
+    pe = el.find("pose") if el is not None else None
+    if pe is not None and pe.text and pe.text.strip():
+        v = [float(x) for x in pe.text.split()]
+        T[:3, :3] = _rpy(v[3:6])
+        T[:3, 3] = v[:3]
+    return T
+
+
+def _sdf_val(el, path, default):
+    e = el.find(path) if el is not None else None
+    return float(e.text) if e is not None and e.text and e.text.strip() else default
+
+
+def _origin(T: np.ndarray) -> str:
+    xyz = " ".join(repr(float(v)) for v in T[:3, 3])
+    rpy = " ".join(repr(float(v)) for v in _mat_to_rpy(T[:3, :3]))
+    return f'<origin xyz="{xyz}" rpy="{rpy}"/>'
+
+
+def sdf_to_urdf(text: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0.0)):
+    """Rewrite an SDF <model> as the URDF that describes the same multibody,
+    for the oracle's URDF reader (independent of the product's C++ SDF
+    front-end).  SDF 1.6 frames: link pose in the model frame, joint pose in
+    the child link frame, axis in the joint frame unless
+    use_parent_model_frame; <limit>/<dynamics> inside <axis>; sdformat's
+    inertial defaults (mass 1, unit inertia).  The URDF child-link frame is
+    the joint frame, the root link's frame the model frame.  Returns (urdf,
+    xyz, wxyz): the model pose (the insertion pose unless it is the
+    identity, World.cpp:169-177)."""
+    root = ET.fromstring(text.strip())
+    me = root.find("model")
+    Tm = _sdf_pose(me)
+    if tuple(pose_xyz) == (0.0, 0.0, 0.0) and tuple(pose_wxyz) == (1.0, 0.0, 0.0, 0.0):
+        w, x, y, z = _rot_to_quat(Tm[:3, :3])
+        pose_xyz, pose_wxyz = tuple(Tm[:3, 3]), (w, x, y, z)
+    X = {le.get("name"): _sdf_pose(le) for le in me.findall("link")}
+    F = {n: np.eye(4) for n in X}
+    F["world"] = np.eye(4)
+    jts = me.findall("joint")
+    for je in jts:
+        F[je.find("child").text.strip()] = X[je.find("child").text.strip()] @ _sdf_pose(je)
+    out = [f'<robot name="{me.get("name", "model")}">']
+    if any(je.find("parent").text.strip() == "world" for je in jts):
+        out.append('<link name="world"/>')
+    for le in me.findall("link"):
+        n = le.get("name")
+        C = np.linalg.inv(F[n]) @ X[n]          # SDF link frame in the URDF link frame
+        ine = le.find("inertial")
+        Ti = C @ _sdf_pose(ine)
+        m = _sdf_val(ine, "mass", 1.0)
+        ie = ine.find("inertia") if ine is not None else None
+        g = lambda k, d: _sdf_val(ie, k, d)
+        I = np.array([[g("ixx", 1.0), g("ixy", 0.0), g("ixz", 0.0)],
+                      [g("ixy", 0.0), g("iyy", 1.0), g("iyz", 0.0)],
+                      [g("ixz", 0.0), g("iyz", 0.0), g("izz", 1.0)]])
+        I = Ti[:3, :3] @ I @ Ti[:3, :3].T
+        xyz = " ".join(repr(float(v)) for v in Ti[:3, 3])
+        f = lambda v: repr(float(v))
+        out.append(f'<link name="{n}"><inertial><origin xyz="{xyz}" rpy="0 0 0"/><mass value="{f(m)}"/>'
+                   f'<inertia ixx="{f(I[0,0])}" ixy="{f(I[0,1])}" ixz="{f(I[0,2])}" iyy="{f(I[1,1])}" '
+                   f'iyz="{f(I[1,2])}" izz="{f(I[2,2])}"/></inertial>')
+        for ce in le.findall("collision"):
+            Tc = C @ _sdf_pose(ce)
+            box, sph = ce.find("geometry/box/size"), ce.find("geometry/sphere/radius")
+            if box is not None:
+                geo = f'<box size="{box.text.strip()}"/>'
+            elif sph is not None:
+                geo = f'<sphere radius="{sph.text.strip()}"/>'
+            else:
+                continue
+            out.append(f'<collision>{_origin(Tc)}<geometry>{geo}</geometry></collision>')
+        out.append("</link>")
+    for je in jts:
+        pa, ch, jt = je.find("parent").text.strip(), je.find("child").text.strip(), je.get("type")
+        O = np.linalg.inv(F[pa]) @ F[ch]
+        body = [f'<joint name="{je.get("name")}" type="{{TYPE}}">', _origin(O),
+                f'<parent link="{pa}"/><child link="{ch}"/>']
+        if jt != "fixed":
+            ax = je.find("axis")
+            xe = ax.find("xyz") if ax is not None else None
+            a = np.array([float(v) for v in xe.text.split()]) if xe is not None else np.array([0.0, 0.0, 1.0])
+            upm = ax is not None and ax.find("use_parent_model_frame") is not None and \
+                ax.find("use_parent_model_frame").text.strip() in ("1", "true")
+            if upm or (xe is not None and xe.get("expressed_in") == "__model__"):
+                a = F[ch][:3, :3].T @ a
+            body.append(f'<axis xyz="{" ".join(repr(float(v)) for v in a)}"/>')
+            lo, hi = _sdf_val(ax, "limit/lower", -1e16), _sdf_val(ax, "limit/upper", 1e16)
+            eff, vel = _sdf_val(ax, "limit/effort", -1.0), _sdf_val(ax, "limit/velocity", -1.0)
+            eff, vel = (eff if eff >= 0 else math.inf), (vel if vel >= 0 else math.inf)
+            lim = f'effort="{float(eff)!r}" velocity="{float(vel)!r}"'
+            if jt == "revolute" and lo <= -1e16 and hi >= 1e16:
+                jt = "continuous"
+            if jt == "prismatic":
+                lo, hi = (-math.inf if lo <= -1e16 else lo), (math.inf if hi >= 1e16 else hi)
+            if jt != "continuous":
+                lim += f' lower="{float(lo)!r}" upper="{float(hi)!r}"'
+            body.append(f"<limit {lim}/>")
+            body.append(f'<dynamics damping="{float(_sdf_val(ax, "dynamics/damping", 0.0))!r}" '
+                        f'friction="{float(_sdf_val(ax, "dynamics/friction", 0.0))!r}"/>')
+        body[0] = body[0].replace("{TYPE}", jt)
+        out.append("".join(body) + "</joint>")
+    out.append("</robot>")
+    return "".join(out), tuple(pose_xyz), tuple(pose_wxyz)
+
+
+def _rot_to_quat(R: np.ndarray):
+    """Unit quaternion (w, x, y, z) of a rotation matrix (Shepperd)."""
+    t = np.trace(R)
+    if t > 0:
+        s = 2.0 * math.sqrt(1.0 + t)
+        return (0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s)
+    i = int(np.argmax(np.diag(R)))
+    j, k = (i + 1) % 3, (i + 2) % 3
+    s = 2.0 * math.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k])
+    q = [0.0] * 4
+    q[0] = (R[k, j] - R[j, k]) / s
+    q[1 + i] = 0.25 * s
+    q[1 + j] = (R[j, i] + R[i, j]) / s
+    q[1 + k] = (R[k, i] + R[i, k]) / s
+    return tuple(q)
+
+
 def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0.0),
               gravity=(0.0, 0.0, -9.8)) -> ChainModel:
     text = path_or_string
     if not path_or_string.lstrip().startswith("<"):
         with open(path_or_string) as f:
             text = f.read()
-    root = ET.fromstring(text)
+    root = ET.fromstring(text.strip())
+    if root.tag == "sdf":
+        text, pose_xyz, pose_wxyz = sdf_to_urdf(text, pose_xyz, pose_wxyz)
+        root = ET.fromstring(text)
     links: Dict[str, _Link] = {}
     for le in root.findall("link"):
         L = _Link()
@@ -357,11 +491,13 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
     floating = root_link != "world"
     if not floating:
         wj = [j for j in joints if j.parent == "world"]
-        assert len(wj) == 1 and wj[0].jtype == "fixed", "only a fixed world joint is supported"
-        base_p = base_p + base_R @ wj[0].p
-        base_R = base_R @ wj[0].R
-        root_link = wj[0].child
-        joints = [j for j in joints if j is not wj[0]]
+        assert wj, "nothing is attached to the world link"
+        if len(wj) == 1 and wj[0].jtype == "fixed":
+            base_p = base_p + base_R @ wj[0].p
+            base_R = base_R @ wj[0].R
+            root_link = wj[0].child
+            joints = [j for j in joints if j is not wj[0]]
+        # else: the massless world link is the fixed base, its joints hang from the model frame
 
     # lump fixed joints into their parent (sdformat URDF import behaviour)
     owner = {n: n for n in links}            # link -> body it was lumped into

@@ -166,3 +166,145 @@ def test_multi_world_is_one_batched_scene(require_gpu):
     assert gazebo.run()
     assert gazebo.get_world("w3").get_model("pendulum").joint_positions()[0] != q3
     gazebo.close()
+
+
+def test_world_api_with_sdf_model(require_gpu):
+    """tests/test_scenario/test_world.py:73-146 (test_world_api): gravity,
+    model names, default / custom names and poses, URDF file and string, the
+    SDF cube of tests/common/utils.py:100-146 inserted from a string, removal
+    taking effect at the next run, no time without the Physics system."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    from test_sdf_models import REF_CUBE_SDF
+    import tempfile
+    gazebo, _ = _gazebo()
+    world = gazebo.get_world()
+    gravity = [0, 0, 10.0]
+    assert world.set_gravity(gravity)
+    assert world.gravity() == pytest.approx(gravity)
+    assert len(world.model_names()) == 0
+    assert not world.insert_model("")
+    with tempfile.NamedTemporaryFile("w", suffix=".urdf", delete=False) as f:
+        f.write(cube_urdf())
+        cube_file = f.name
+    assert world.insert_model(cube_file)
+    assert len(world.model_names()) == 1
+    default_model_name = scenario.get_model_name_from_sdf(cube_file, 0)
+    assert default_model_name in world.model_names()
+    cube1 = world.get_model(default_model_name)
+    assert cube1.name() == default_model_name
+    assert cube1.base_position() == pytest.approx([0, 0, 0])
+    assert cube1.base_orientation() == pytest.approx([1, 0, 0, 0])
+    assert not world.insert_model(cube_file)
+    assert len(world.model_names()) == 1
+    custom_model_name = "other_cube"
+    custom_model_pose = core.Pose([1, 1, 0], [0, 0, 0, 1])
+    assert world.insert_model(cube_file, custom_model_pose, custom_model_name)
+    assert custom_model_name in world.model_names() and len(world.model_names()) == 2
+    cube2 = world.get_model(custom_model_name)
+    assert cube1 != cube2
+    assert cube2.name() == custom_model_name
+    assert cube2.base_position() == pytest.approx(custom_model_pose.position)
+    assert cube2.base_orientation() == pytest.approx(custom_model_pose.orientation)
+    assert world.insert_model_from_string(cube_urdf(), core.Pose([1, 0, 0], [0, 0, 0, 1]), "cube3")
+    assert "cube3" in world.model_names()
+    cube_4_pose = core.Pose([2, 0, 0], [0, 0, 0, 1])
+    assert world.insert_model_from_string(REF_CUBE_SDF, cube_4_pose, "cube4")
+    assert "cube4" in world.model_names()
+    cube4 = world.get_model("cube4")
+    assert cube4.base_position() == pytest.approx([2, 0, 0])
+    assert cube4.base_orientation() == pytest.approx([0, 0, 0, 1])
+    assert cube4.link_names() == ["box_link"]
+    assert world.remove_model(default_model_name)
+    assert len(world.model_names()) == 4
+    gazebo.run(paused=True)
+    assert len(world.model_names()) == 3
+    gazebo.run()
+    gazebo.run()
+    gazebo.run()
+    assert world.time() == 0.0
+    gazebo.close()
+
+
+def test_sdf_cube_falls_and_lands(require_gpu):
+    """The reference's SDF cube (1 m edge, 1 kg, unit inertia, model pose
+    0 0 0.5 kept under the identity insertion pose) lifted to z = 2: free fall
+    z = 2 - g t^2 / 2 (semi-implicit Euler: g dt^2 k (k + 1) / 2 after k
+    steps) until it touches the plane, then rests on it (z = 0.5, weight
+    carried by the contact)."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    from test_sdf_models import REF_CUBE_SDF
+    gazebo, get_model_file = _gazebo()
+    world = gazebo.get_world()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("ground_plane"))
+    assert world.insert_model_from_string(REF_CUBE_SDF)
+    box = world.get_model("box")
+    assert box.base_position() == pytest.approx([0, 0, 0.5])
+    assert box.reset_base_pose([0, 0, 2.0], [1, 0, 0, 0])
+    assert box.enable_contacts(True)
+    gazebo.run(paused=True)
+    assert box.base_position()[2] == pytest.approx(2.0)
+    dt = 1e-3
+    for k in range(1, 301):
+        assert gazebo.run()
+        z = box.base_position()[2]
+        assert z == pytest.approx(2.0 - G * dt * dt * k * (k + 1) / 2, abs=2e-5), k
+    for _ in range(1200):
+        assert gazebo.run()
+    assert box.base_position()[2] == pytest.approx(0.5, abs=2e-3)
+    assert box.get_link("box_link").in_contact()
+    fz = box.get_link("box_link").contact_wrench()[2]
+    assert fz == pytest.approx(G * 1.0, abs=0.05)
+    gazebo.close()
+
+
+def test_sdf_and_urdf_pendulum_trajectories_agree(require_gpu, oracle):
+    """The pendulum written as SDF (a revolute joint to the world, link and
+    inertial poses in the model frame) and the shipped URDF pendulum, inserted
+    into two worlds of one simulator: their joint trajectories agree over 500
+    steps from the same reset, and both follow the fp64 oracle."""
+    from scenario import gazebo as scenario
+    from mwstep import get_model_file
+    cm = oracle.load_urdf(get_model_file("pendulum"))
+    M = cm.model
+    E = np.array(M.E[0]).reshape(3, 3)
+    Rj, pj = cm.base_R @ E, cm.base_R @ np.array(M.r[0]) + cm.base_p
+    rpy = oracle._mat_to_rpy(Rj)
+    I = [M.Ic[0][k] for k in range(6)]
+    f = lambda v: " ".join(f"{x:.17g}" for x in v)
+    sdf = f"""<sdf version='1.7'><model name='pendulum'>
+      <link name='pole'><pose>{f((*pj, *rpy))}</pose>
+        <inertial><pose>{f(M.com[0])} 0 0 0</pose><mass>{M.mass[0]:.17g}</mass>
+          <inertia><ixx>{I[0]:.17g}</ixx><iyy>{I[1]:.17g}</iyy><izz>{I[2]:.17g}</izz>
+                   <ixy>{I[3]:.17g}</ixy><ixz>{I[4]:.17g}</ixz><iyz>{I[5]:.17g}</iyz></inertia></inertial></link>
+      <joint name='{cm.joint_names[0]}' type='revolute'><parent>world</parent><child>pole</child>
+        <axis><xyz>{f(M.axis[0])}</xyz></axis></joint></model></sdf>"""
+    gazebo, _ = _gazebo(["w_urdf", "w_sdf"])
+    models = []
+    for wn, text in (("w_urdf", open(get_model_file("pendulum")).read()), ("w_sdf", sdf)):
+        world = gazebo.get_world(wn)
+        assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+        assert world.insert_model_from_string(text)
+        m = world.get_model("pendulum")
+        assert m.reset_joint_positions([0.7]) and m.reset_joint_velocities([0.0])
+        models.append(m)
+    gazebo.run(paused=True)
+    q_u, q_s = [], []
+    for _ in range(500):
+        assert gazebo.run()
+        q_u.append(models[0].joint_positions()[0])
+        q_s.append(models[1].joint_positions()[0])
+    q_u, q_s = np.array(q_u), np.array(q_s)
+    err = float(np.abs(q_u - q_s).max())
+    print(f"SDF vs URDF pendulum over 500 steps: max |dq| {err:.2e}")
+    assert err <= 1e-5
+    # the fp64 oracle from the same start
+    q, qd = np.array([0.7]), np.array([0.0])
+    worst = 0.0
+    for k in range(500):
+        q, qd, *_ = oracle.step(cm, 1e-3, q, qd, np.full(1, oracle.FORCE, np.int32), np.zeros(1), 20)
+        worst = max(worst, abs(float(q[0]) - q_s[k]))
+    assert worst <= 1e-4, worst
+    gazebo.close()

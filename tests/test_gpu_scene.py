@@ -335,15 +335,13 @@ def _fixed_tree_urdf(n=16, seed=9):
 
 def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
     """A welded random 16-joint branched tree (damping, Coulomb friction,
-    joints beyond their limits, random torques): one step on the scene
-    kernel against the fp64 tree oracle or_step (ABA + joint LCP) for 256
-    worlds of random states: q within 1e-5, qd within 1e-4.  The model is
-    refused by mw_load_model (chain kernels) and runs here instead."""
+    joints beyond their limits, random torques): one step against the fp64
+    tree oracle or_step (ABA + joint LCP) for 256 worlds of random states, on
+    the scene kernel and through mw_sim (the world-per-wavefront kernel with a
+    welded base, FloatF::fixed): q within 1e-5, qd within 1e-4."""
     from mwstep import native as N
     from mwstep.sim import Simulator
     text = _fixed_tree_urdf()
-    with pytest.raises(RuntimeError):
-        Simulator(text, n_worlds=1)
     W = 256
     rng = np.random.default_rng(4)
     cm = oracle.load_urdf(text)
@@ -376,6 +374,24 @@ def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
     print(f"fixed 16-joint tree on the scene kernel, one step x{W}: max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
     assert wq <= 1e-5 and wqd <= 1e-4
     sc.close()
+    sim = Simulator(text, n_worlds=W, pgs_iters=50)
+    assert not sim.floating and sim.float_kernel() == 2
+    sim.set("reset_q", q)
+    sim.set("reset_qd", qd)
+    sim.run(paused=True)
+    sim.set_control_mode(N.MODE_FORCE)
+    sim.set("force_target", tau)
+    sim.run()
+    sq, sqd = sim.get("q"), sim.get("qd")
+    wq = wqd = 0.0
+    for w in range(W):
+        oq, oqd, *_ = oracle.step(cm, 1e-3, q[w], qd[w], np.full(n, oracle.FORCE, np.int32), tau[w], 50)
+        wq = max(wq, float(np.abs(sq[w] - oq).max()))
+        wqd = max(wqd, float(np.abs(sqd[w] - oqd).max()))
+    print(f"fixed 16-joint tree through mw_sim (wave kernel, welded base): max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
+    assert wq <= 1e-5 and wqd <= 1e-4
+    assert np.allclose(sim.base_pose()[:, :3], 0.0) and sim.constraint_overflow() == 0
+    sim.close()
 
 
 def test_capacity_overflow_fails_loudly(require_gpu):

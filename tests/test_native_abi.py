@@ -160,13 +160,16 @@ def test_fixed_joint_lumping(N, oracle):
      "deeper than 12"),
     ("<robot name='x'><link name='a'/></robot>", "has no mass"),
     ("<robot name='x'><link name='world'/>", "XML"),
-    ("<sdf><model name='m'/></sdf>", "URDF"),
-    ("<robot name='x'><link name='world'/><link name='a'/><joint name='w' type='fixed'>"
-     "<parent link='world'/><child link='a'/></joint>"
-     "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<link name='c'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
-     "<joint name='j1' type='revolute'><parent link='a'/><child link='b'/></joint>"
-     "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>", "topology"),
+    ("<sdf><model name='m'/></sdf>", "no links"),
+    ("<mjcf/>", "URDF"),
+    # a welded chain of 13 joints: the fixed-base tree runs on the wave kernel, whose stack is 12 deep
+    ("<robot name='x'><link name='world'/><joint name='w' type='fixed'><parent link='world'/><child link='l0'/>"
+     "</joint>" + "".join(
+        f"<link name='l{i}'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+        for i in range(14)) + "".join(
+        f"<joint name='j{i}' type='revolute'><parent link='l{i}'/><child link='l{i + 1}'/></joint>"
+        for i in range(13)) + "</robot>",
+     "deeper than 12"),
 ])
 def test_unsupported_models_fail_loudly(N, bad, why):
     rc, h = _create(N)
@@ -177,6 +180,36 @@ def test_unsupported_models_fail_loudly(N, bad, why):
         assert why.lower() in N.last_error().lower()
     finally:
         N.lib().mw_destroy(h)
+
+
+def test_generic_fixed_base_trees_take_the_wave_kernel(N):
+    """A branched fixed-base tree outside the compiled chain topologies is
+    accepted (no longer refused) and routed to the
+    world-per-wavefront kernel with a welded base; so is a hinge to the world."""
+    trees = [
+        "<robot name='x'><link name='world'/><link name='a'/><joint name='w' type='fixed'>"
+        "<parent link='world'/><child link='a'/></joint>"
+        "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+        "<link name='c'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+        "<joint name='j1' type='revolute'><parent link='a'/><child link='b'/></joint>"
+        "<joint name='j2' type='revolute'><parent link='a'/><child link='c'/></joint></robot>",
+        "<robot name='y'><link name='world'/>"
+        "<link name='b'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+        "<link name='c'><inertial><mass value='1'/><inertia ixx='1' iyy='1' izz='1'/></inertial></link>"
+        "<joint name='j1' type='revolute'><parent link='world'/><child link='b'/></joint>"
+        "<joint name='j2' type='prismatic'><parent link='world'/><child link='c'/></joint></robot>",
+    ]
+    for text in trees:
+        rc, h = _create(N)
+        try:
+            p = np.array([0, 0, 1, 1, 0, 0, 0], dtype=np.float64)
+            N.check(N.lib().mw_load_model(h, text.encode(), N.dptr(p), b""))
+            k, f = ctypes.c_int32(), ctypes.c_int32()
+            N.check(N.lib().mw_float_kernel(h, ctypes.byref(k)))
+            N.check(N.lib().mw_is_floating(h, ctypes.byref(f)))
+            assert k.value == 2 and f.value == 0
+        finally:
+            N.lib().mw_destroy(h)
 
 
 def test_initialize_without_model_or_gpu_reports_error(N, cartpole_file):
