@@ -390,7 +390,9 @@ def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
         wqd = max(wqd, float(np.abs(sqd[w] - oqd).max()))
     print(f"fixed 16-joint tree through mw_sim (wave kernel, welded base): max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")
     assert wq <= 1e-5 and wqd <= 1e-4
-    assert np.allclose(sim.base_pose()[:, :3], 0.0) and sim.constraint_overflow() == 0
+    # the welded base stays where the model was inserted (Model::basePosition)
+    assert np.allclose(sim.base_pose()[:, :3], cm.base_p) and np.allclose(sim.base_velocity(), 0.0)
+    assert sim.constraint_overflow() == 0
     sim.close()
 
 
