@@ -58,6 +58,37 @@ __device__ __forceinline__ f3 mulT(const M3& R, f3 v) {
     return {R.m[0] * v.x + R.m[3] * v.y + R.m[6] * v.z, R.m[1] * v.x + R.m[4] * v.y + R.m[7] * v.z,
             R.m[2] * v.x + R.m[5] * v.y + R.m[8] * v.z};
 }
+
+// Ground-contact slots of a collision shape (Physics.cpp:687-1219 builds box,
+// sphere and cylinder collisions; oracle.c: or_slot_point is the fp64 twin).
+// Returns the shape-frame point of slot c: box (h = half extents) corner c
+// (bits x y z); sphere its centre (the caller lowers it by the radius);
+// cylinder (h = {radius, half length}, axis z): 4 rim points per cap (c & 4:
+// the +z cap), 90 degrees apart starting at the rim point deepest along the
+// plane normal, so a lying cylinder touches at the exact ends of its contact
+// line and a standing one on a square of its rim.  nz = the plane normal (world
+// +z) in the shape frame = the third row of the shape's world rotation.
+__device__ __forceinline__ f3 shape_slot_point(int type, const float* h, f3 nz, int c) {
+    const bool box = (type == 0), cyl = (type == 2);
+    float ux = -nz.x, uy = -nz.y;
+    const float n2 = ux * ux + uy * uy;
+    const bool tilted = n2 > 1e-12f;
+    const float inv = tilted ? 1.f / sqrtf(n2) : 0.f;
+    ux = tilted ? ux * inv : 1.f;
+    uy = tilted ? uy * inv : 0.f;
+    const int j = c & 3;  // 0: u, 1: z x u, 2: -u, 3: -(z x u)
+    const float dx = (j == 0) ? ux : ((j == 1) ? -uy : ((j == 2) ? -ux : uy));
+    const float dy = (j == 0) ? uy : ((j == 1) ? ux : ((j == 2) ? -uy : -ux));
+    const float zc = (c & 4) ? h[1] : -h[1];
+    return {box ? ((c & 4) ? h[0] : -h[0]) : (cyl ? h[0] * dx : 0.f),
+            box ? ((c & 2) ? h[1] : -h[1]) : (cyl ? h[0] * dy : 0.f),
+            box ? ((c & 1) ? h[2] : -h[2]) : (cyl ? zc : 0.f)};
+}
+// third row of Rb SR (the world +z axis in the shape frame)
+__device__ __forceinline__ f3 shape_plane_normal(const M3& Rb, const float* SR) {
+    return {Rb.m[6] * SR[0] + Rb.m[7] * SR[3] + Rb.m[8] * SR[6], Rb.m[6] * SR[1] + Rb.m[7] * SR[4] + Rb.m[8] * SR[7],
+            Rb.m[6] * SR[2] + Rb.m[7] * SR[5] + Rb.m[8] * SR[8]};
+}
 __device__ __forceinline__ f3 mul(const Sy& S, f3 v) {
     return {S.xx * v.x + S.xy * v.y + S.xz * v.z, S.xy * v.x + S.yy * v.y + S.yz * v.z,
             S.xz * v.x + S.yz * v.y + S.zz * v.z};

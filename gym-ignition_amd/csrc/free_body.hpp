@@ -109,15 +109,14 @@ __device__ __forceinline__ SV minv_mul(const FreeF& __restrict__ F, const SV& x)
     return {{o[0], o[1], o[2]}, {o[3], o[4], o[5]}};
 }
 
-// body-frame point of slot k of shape s (box corner k; sphere: centre)
-__device__ __forceinline__ f3 slot_point(const FreeF& F, int s, int k) {
-    const float* h = F.shape_size[s];
+// body-frame point of slot k of shape s (box corner k; sphere: centre;
+// cylinder: rim point k, chain_dyn.hpp shape_slot_point) for body rotation Rb
+__device__ __forceinline__ f3 slot_point(const FreeF& F, int s, int k, const M3& Rb) {
     const float* R = F.shape_R[s];
-    const float lx = (k & 4) ? h[0] : -h[0], ly = (k & 2) ? h[1] : -h[1], lz = (k & 1) ? h[2] : -h[2];
-    const bool box = (F.shape_type[s] == 0);
-    const float ax = box ? lx : 0.f, ay = box ? ly : 0.f, az = box ? lz : 0.f;
-    return {F.shape_p[s][0] + R[0] * ax + R[1] * ay + R[2] * az, F.shape_p[s][1] + R[3] * ax + R[4] * ay + R[5] * az,
-            F.shape_p[s][2] + R[6] * ax + R[7] * ay + R[8] * az};
+    const f3 l = shape_slot_point(F.shape_type[s], F.shape_size[s], shape_plane_normal(Rb, R), k);
+    return {F.shape_p[s][0] + R[0] * l.x + R[1] * l.y + R[2] * l.z,
+            F.shape_p[s][1] + R[3] * l.x + R[4] * l.y + R[5] * l.z,
+            F.shape_p[s][2] + R[6] * l.x + R[7] * l.y + R[8] * l.z};
 }
 
 // Contact slot record in LDS (31 words: odd, so a wave's accesses to one
@@ -168,7 +167,7 @@ __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (sphere && k > 0) break;
-                f3 b = slot_point(F, s, k);
+                f3 b = slot_point(F, s, k, R);
                 f3 xw = S.p + mul(R, b);
                 float depth = -xw.z;
                 if (sphere) {  // its lowest point

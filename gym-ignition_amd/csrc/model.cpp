@@ -313,6 +313,7 @@ Description describe_urdf(const XNode* root, const double pose[7]) {
             const XNode* ge = ce->child("geometry");
             const XNode* box = ge ? ge->child("box") : nullptr;
             const XNode* sph = ge ? ge->child("sphere") : nullptr;
+            const XNode* cyl = ge ? ge->child("cylinder") : nullptr;
             Shape sh;
             sh.R = rpy(vec_attr(o, "rpy", {0, 0, 0}));
             sh.p = vec_attr(o, "xyz", {0, 0, 0});
@@ -322,6 +323,9 @@ Description describe_urdf(const XNode* root, const double pose[7]) {
             } else if (sph) {
                 sh.type = Shape::Sphere;
                 sh.size = {num_attr(sph, "radius", 0.0), 0.0, 0.0};
+            } else if (cyl) {
+                sh.type = Shape::Cylinder;
+                sh.size = {num_attr(cyl, "radius", 0.0), 0.5 * num_attr(cyl, "length", 0.0), 0.0};
             } else {
                 ++L.unsupported;
                 continue;
@@ -490,6 +494,7 @@ Description describe_sdf(const XNode* root, const double pose[7]) {
             const XNode* ge = ce->child("geometry");
             const XNode* box = ge ? ge->child("box") : nullptr;
             const XNode* sph = ge ? ge->child("sphere") : nullptr;
+            const XNode* cyl = ge ? ge->child("cylinder") : nullptr;
             Shape sh;
             sh.R = Xc.R;
             sh.p = Xc.p;
@@ -501,6 +506,9 @@ Description describe_sdf(const XNode* root, const double pose[7]) {
             } else if (sph) {
                 sh.type = Shape::Sphere;
                 sh.size = {sdf_num(sph, "radius", 1.0), 0.0, 0.0};
+            } else if (cyl) {  // sdformat defaults: radius 0.5, length 1
+                sh.type = Shape::Cylinder;
+                sh.size = {sdf_num(cyl, "radius", 0.5), 0.5 * sdf_num(cyl, "length", 1.0), 0.0};
             } else {
                 ++L.unsupported;
                 continue;

@@ -40,10 +40,11 @@ struct ChainBody {
     std::vector<struct Shape> shapes;  // collision shapes of the (lumped) link, body frame
 };
 
-// A collision shape in its body's frame: box (size = half extents) or sphere
-// (size[0] = radius).  Other URDF geometries are counted, not modelled.
+// A collision shape in its body's frame: box (size = half extents), sphere
+// (size[0] = radius) or cylinder along z (size = {radius, half length}).
+// Meshes and other geometries are counted, not modelled.
 struct Shape {
-    enum Type : int { Box = 0, Sphere = 1 } type = Box;
+    enum Type : int { Box = 0, Sphere = 1, Cylinder = 2 } type = Box;
     std::array<double, 3> size{};
     std::array<double, 9> R{};
     std::array<double, 3> p{};
@@ -59,7 +60,7 @@ struct ChainModel {
     std::array<double, 3> base_com{};
     std::array<double, 6> base_Ic{};   // about the COM: xx yy zz xy xz yz
     std::vector<Shape> base_shapes;    // collision shapes of the base body
-    int unsupported_shapes = 0;        // collision geometries other than box / sphere
+    int unsupported_shapes = 0;        // collision geometries other than box / sphere / cylinder
     std::array<double, 9> base_R{};  // base pose in world
     std::array<double, 3> base_p{};
     std::vector<ChainBody> bodies; // depth-first: bodies[i].parent < i (-1 = base)

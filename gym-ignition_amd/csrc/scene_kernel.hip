@@ -296,6 +296,7 @@ __device__ __forceinline__ int sc_box_sphere(f3 h, f3 c, const M3& R, float rad,
 // normal from B into A, up to 4 points / depths
 __device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, int tb, f3 sb, f3 cb, const M3& Rb,
                                           f3& n, f3* pts, float* deps) {
+    if (ta == 2 || tb == 2) return 0;  // cylinders collide with the ground plane only (this build)
     if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, pts, deps);
     if (ta == 1 && tb == 1) {
         const f3 d = ca - cb;
@@ -615,9 +616,8 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                     const bool sphere = (P->shape_type[sh] == 1);
                     const float* h = P->shape_size[sh];
                     const float* SR = P->shape_R[sh];
-                    const float lx = sphere ? 0.f : ((c & 4) ? h[0] : -h[0]);
-                    const float ly = sphere ? 0.f : ((c & 2) ? h[1] : -h[1]);
-                    const float lz = sphere ? 0.f : ((c & 1) ? h[2] : -h[2]);
+                    const f3 lp = shape_slot_point(P->shape_type[sh], h, shape_plane_normal(nd.Rw, SR), c);
+                    const float lx = lp.x, ly = lp.y, lz = lp.z;
                     const f3 bb = {P->shape_p[sh][0] + SR[0] * lx + SR[1] * ly + SR[2] * lz,
                                    P->shape_p[sh][1] + SR[3] * lx + SR[4] * ly + SR[5] * lz,
                                    P->shape_p[sh][2] + SR[6] * lx + SR[7] * ly + SR[8] * lz};

@@ -385,9 +385,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             const bool sphere = (F->shape_type[sh] == 1);
             const float* h = F->shape_size[sh];
             const float* SR = F->shape_R[sh];
-            const float lx = sphere ? 0.f : ((c & 4) ? h[0] : -h[0]);
-            const float ly = sphere ? 0.f : ((c & 2) ? h[1] : -h[1]);
-            const float lz = sphere ? 0.f : ((c & 1) ? h[2] : -h[2]);
+            const f3 lp = shape_slot_point(F->shape_type[sh], h, shape_plane_normal(Rb, SR), c);
+            const float lx = lp.x, ly = lp.y, lz = lp.z;
             f3 bb = {F->shape_p[sh][0] + SR[0] * lx + SR[1] * ly + SR[2] * lz,
                      F->shape_p[sh][1] + SR[3] * lx + SR[4] * ly + SR[5] * lz,
                      F->shape_p[sh][2] + SR[6] * lx + SR[7] * ly + SR[8] * lz};

@@ -35,6 +35,47 @@
 #include <math.h>
 #include <string.h>
 
+/* Ground-contact slots of a collision shape (Physics.cpp:687-1219 builds box,
+ * sphere and cylinder collisions; the kernels' twin is chain_dyn.hpp
+ * shape_slot_point): the shape-frame point of slot c.  Box (h = half
+ * extents): corner c (bits x y z); sphere: its centre (lowered by the radius by
+ * the caller); cylinder (h = {radius, half length}, axis z): 4 rim points per
+ * cap (c & 4: the +z cap), 90 degrees apart from the rim point deepest along
+ * the plane normal.  RS = the shape's world rotation (Rb SR). */
+void or_slot_point(int type, const double* h, const double* RS, int c, double l[3])
+{
+    l[0] = l[1] = l[2] = 0.0;
+    if (type == 0) {
+        l[0] = (c & 4) ? h[0] : -h[0];
+        l[1] = (c & 2) ? h[1] : -h[1];
+        l[2] = (c & 1) ? h[2] : -h[2];
+    } else if (type == 2) {
+        double ux = -RS[6], uy = -RS[7];   /* -(world z in the shape frame), projected on the cap plane */
+        const double n2 = ux * ux + uy * uy;
+        if (n2 > 1e-12) {
+            const double inv = 1.0 / sqrt(n2);
+            ux *= inv;
+            uy *= inv;
+        } else {
+            ux = 1.0;
+            uy = 0.0;
+        }
+        const int j = c & 3;
+        const double dx = (j == 0) ? ux : ((j == 1) ? -uy : ((j == 2) ? -ux : uy));
+        const double dy = (j == 0) ? uy : ((j == 1) ? ux : ((j == 2) ? -uy : -ux));
+        l[0] = h[0] * dx;
+        l[1] = h[0] * dy;
+        l[2] = (c & 4) ? h[1] : -h[1];
+    }
+}
+
+static void rot_mul(const double* A, const double* B, double* C)
+{
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) C[r * 3 + k] = A[r * 3] * B[k] + A[r * 3 + 1] * B[3 + k] + A[r * 3 + 2] * B[6 + k];
+}
+
+
 /* ---------------- small dense helpers (6x6 row-major) ---------------- */
 
 static void m6_zero(double* A) { memset(A, 0, 36 * sizeof(double)); }
@@ -839,10 +880,12 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
             const double* h = m->shape_size[k];
             const double* SR = m->shape_R[k];
             const double* sp = m->shape_p[k];
-            if (m->shape_type[k] == 0) {
+            if (m->shape_type[k] != 1) {
+                double RS[9];
+                rot_mul(R, SR, RS);
                 for (int corner = 0; corner < 8; ++corner) {
-                    const double l[3] = {(corner & 4) ? h[0] : -h[0], (corner & 2) ? h[1] : -h[1],
-                                         (corner & 1) ? h[2] : -h[2]};
+                    double l[3];
+                    or_slot_point(m->shape_type[k], h, RS, corner, l);
                     double b[3], x[3];
                     for (int r = 0; r < 3; ++r) b[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
                     for (int r = 0; r < 3; ++r) x[r] = s->p[r] + R[r * 3] * b[0] + R[r * 3 + 1] * b[1] + R[r * 3 + 2] * b[2];
@@ -1457,14 +1500,12 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
             const double* hh = m->shape_size[sh];
             const double* SR = m->shape_R[sh];
             const double* sp = m->shape_p[sh];
-            const int corners = (m->shape_type[sh] == 0) ? 8 : 1;
+            const int corners = (m->shape_type[sh] == 1) ? 1 : 8;
+            double RS[9];
+            rot_mul(Rb, SR, RS);
             for (int corner = 0; corner < corners; ++corner) {
-                double l[3] = {0, 0, 0};
-                if (m->shape_type[sh] == 0) {
-                    l[0] = (corner & 4) ? hh[0] : -hh[0];
-                    l[1] = (corner & 2) ? hh[1] : -hh[1];
-                    l[2] = (corner & 1) ? hh[2] : -hh[2];
-                }
+                double l[3];
+                or_slot_point(m->shape_type[sh], hh, RS, corner, l);
                 double b[3], x[3];
                 for (int r = 0; r < 3; ++r) b[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
                 for (int r = 0; r < 3; ++r) x[r] = pb[r] + Rb[r * 3] * b[0] + Rb[r * 3 + 1] * b[1] + Rb[r * 3 + 2] * b[2];
@@ -1899,6 +1940,7 @@ int or_collide(int type_a, const double* size_a, const double* c_a, const double
                const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
                double* depths)
 {
+    if (type_a == 2 || type_b == 2) return 0;  /* cylinders: ground plane only (this build) */
     if (type_a == 0 && type_b == 0) return box_box(size_a, c_a, R_a, size_b, c_b, R_b, normal, points, depths);
     if (type_a == 1 && type_b == 1) {
         double d[3] = {c_a[0] - c_b[0], c_a[1] - c_b[1], c_a[2] - c_b[2]};
@@ -2028,14 +2070,12 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
                 const double* hh = fm->shape_size[sh];
                 const double* SR = fm->shape_R[sh];
                 const double* sp = fm->shape_p[sh];
-                const int corners = (fm->shape_type[sh] == 0) ? 8 : 1;
+                const int corners = (fm->shape_type[sh] == 1) ? 1 : 8;
+                double RS[9];
+                rot_mul(Rb, SR, RS);
                 for (int corner = 0; corner < corners; ++corner) {
-                    double l[3] = {0, 0, 0}, b3[3], x[3];
-                    if (fm->shape_type[sh] == 0) {
-                        l[0] = (corner & 4) ? hh[0] : -hh[0];
-                        l[1] = (corner & 2) ? hh[1] : -hh[1];
-                        l[2] = (corner & 1) ? hh[2] : -hh[2];
-                    }
+                    double l[3], b3[3], x[3];
+                    or_slot_point(fm->shape_type[sh], hh, RS, corner, l);
                     for (int r = 0; r < 3; ++r) b3[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
                     for (int r = 0; r < 3; ++r) x[r] = pb[r] + Rb[r * 3] * b3[0] + Rb[r * 3 + 1] * b3[1] + Rb[r * 3 + 2] * b3[2];
                     double dep = -x[2];

@@ -291,6 +291,9 @@ int or_scene_step(const or_scene_model* m, double dt, or_scene_state* st, const 
  * type 0 box (size = half extents), 1 sphere (size[0] = radius); pose (c, R
  * row-major, columns = shape axes in the world).  Writes up to 4 points and
  * depths and the unit normal from B into A; returns the point count. */
+/* shape-frame point of ground-contact slot c (box corner, sphere centre,
+ * cylinder rim point); RS = the shape's world rotation */
+void or_slot_point(int type, const double* h, const double* RS, int c, double l[3]);
 int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
                const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
                double* depths);

@@ -367,10 +367,14 @@ def sdf_to_urdf(text: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0
         for ce in le.findall("collision"):
             Tc = C @ _sdf_pose(ce)
             box, sph = ce.find("geometry/box/size"), ce.find("geometry/sphere/radius")
+            cyl = ce.find("geometry/cylinder")
             if box is not None:
                 geo = f'<box size="{box.text.strip()}"/>'
             elif sph is not None:
                 geo = f'<sphere radius="{sph.text.strip()}"/>'
+            elif cyl is not None:
+                geo = (f'<cylinder radius="{_sdf_val(cyl, "radius", 0.5)!r}" '
+                       f'length="{_sdf_val(cyl, "length", 1.0)!r}"/>')
             else:
                 continue
             out.append(f'<collision>{_origin(Tc)}<geometry>{geo}</geometry></collision>')
@@ -455,11 +459,15 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
             geo = ce.find("geometry")
             box = geo.find("box") if geo is not None else None
             sph = geo.find("sphere") if geo is not None else None
+            cyl = geo.find("cylinder") if geo is not None else None
             SR, sp = _rpy(_vec(o, "rpy", [0, 0, 0])), _vec(o, "xyz", [0, 0, 0])
             if box is not None:
                 L.shapes.append((0, 0.5 * _vec(box, "size", [0, 0, 0]), SR, sp))
             elif sph is not None:
                 L.shapes.append((1, np.array([float(sph.get("radius")), 0.0, 0.0]), SR, sp))
+            elif cyl is not None:   # axis z: (radius, half length)
+                L.shapes.append((2, np.array([float(cyl.get("radius")), 0.5 * float(cyl.get("length")), 0.0]),
+                                 SR, sp))
         links[le.get("name")] = L
     joints: List[_Joint] = []
     for je in root.findall("joint"):

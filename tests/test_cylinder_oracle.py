@@ -1,0 +1,130 @@
+"""Cylinder collisions (Physics.cpp:687-1219 builds box, sphere and
+cylinder collision shapes) in the fp64 oracle, pinned before the kernels are
+compared with it (CPU):
+
+  * the slot geometry (or_slot_point): a standing cylinder touches on a square
+    of its bottom rim, a lying one at the two exact ends of its contact line,
+    a tilted one first at the deepest rim point;
+  * a standing cylinder carries its weight (the contact KAT shape of
+    tests/test_scenario/test_contacts.py:58-122) at rest at half its length;
+  * a lying cylinder released with spin about its axis rolls without slipping:
+    v = omega r, and the final speed is omega0 r / 3 (a solid cylinder,
+    I = m r^2 / 2, angular momentum about the contact line conserved);
+  * the URDF and SDF cylinder geometry compile alike in the product's C++
+    compiler and the oracle's reader.
+"""
+
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+G = 9.8
+
+
+def cylinder_urdf(mass=2.0, r=0.1, length=0.4, name="can", rpy="0 0 0"):
+    ixx = mass * (3 * r * r + length * length) / 12.0
+    izz = 0.5 * mass * r * r
+    return (f'<robot name="{name}"><link name="{name}"><inertial><mass value="{mass}"/>'
+            f'<inertia ixx="{ixx}" iyy="{ixx}" izz="{izz}" ixy="0" ixz="0" iyz="0"/></inertial>'
+            f'<collision><origin rpy="{rpy}" xyz="0 0 0"/><geometry><cylinder radius="{r}" length="{length}"/>'
+            f'</geometry></collision></link></robot>')
+
+
+def _Rx(a):
+    c, s = math.cos(a), math.sin(a)
+    return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+
+
+def _slot(oracle, RS, c, h=(0.1, 0.2, 0.0)):
+    lib = oracle.lib()
+    l = np.zeros(3)
+    hh = np.array(h, dtype=np.float64)
+    RSa = np.ascontiguousarray(RS, dtype=np.float64).ravel()
+    lib.or_slot_point(2, hh.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                      RSa.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), c,
+                      l.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return l
+
+
+def test_slot_geometry(oracle):
+    lib = oracle.lib()
+    lib.or_slot_point.restype = None
+    # standing: the 4 points of each cap at 90 degrees, radius r
+    pts = np.array([_slot(oracle, np.eye(3), c) for c in range(8)])
+    np.testing.assert_allclose(np.linalg.norm(pts[:, :2], axis=1), 0.1)
+    np.testing.assert_allclose(pts[:4, 2], -0.2)
+    np.testing.assert_allclose(pts[4:, 2], 0.2)
+    np.testing.assert_allclose(pts[0], [0.1, 0, -0.2], atol=1e-15)
+    # lying (axis along world y after Rx(90 deg)): slot 0 / 4 are the lowest
+    # points of the two caps, exactly on the contact line
+    R = _Rx(math.pi / 2)
+    for c in (0, 4):
+        w = R @ _slot(oracle, R, c)
+        assert w[2] == pytest.approx(-0.1, abs=1e-15)
+    w = np.array([R @ _slot(oracle, R, c) for c in range(8)])
+    assert w[:, 2].min() == pytest.approx(-0.1)
+    # tilted: slot 0 of the lower cap is the deepest of all rim points
+    R = _Rx(0.3)
+    w0 = R @ _slot(oracle, R, 0)
+    ang = np.linspace(0, 2 * np.pi, 721)
+    rim = np.stack([0.1 * np.cos(ang), 0.1 * np.sin(ang), np.full_like(ang, -0.2)], 1) @ R.T
+    assert w0[2] == pytest.approx(rim[:, 2].min(), abs=1e-6)
+
+
+def test_standing_cylinder_carries_its_weight(oracle):
+    cm = oracle.load_urdf(cylinder_urdf(), pose_xyz=(0, 0, 0.25))
+    w = oracle.FreeWorld(cm, mu=1.0)
+    for _ in range(600):
+        w.step()
+    assert w.p[2] == pytest.approx(0.2, abs=2e-3)
+    assert len(w.contacts) == 4
+    fz = sum(c[2][2] for c in w.contacts)
+    assert fz == pytest.approx(2.0 * G, abs=0.05)
+    for p, n, f, d in w.contacts:
+        assert list(n) == [0, 0, 1]
+
+
+def test_lying_cylinder_rolls_without_slipping(oracle):
+    r, m = 0.1, 2.0
+    # the collision cylinder lies along the body x axis (rpy: pitch 90 deg)
+    ixx = m * (3 * r * r + 0.16) / 12.0
+    text = (f'<robot name="roll"><link name="roll"><inertial><mass value="{m}"/>'
+            f'<inertia ixx="{0.5 * m * r * r}" iyy="{ixx}" izz="{ixx}" ixy="0" ixz="0" iyz="0"/></inertial>'
+            f'<collision><origin rpy="0 {math.pi / 2} 0" xyz="0 0 0"/><geometry>'
+            f'<cylinder radius="{r}" length="0.4"/></geometry></collision></link></robot>')
+    cm = oracle.load_urdf(text, pose_xyz=(0, 0, r))
+    w = oracle.FreeWorld(cm, mu=1.0, pgs_iters=100)
+    for _ in range(100):
+        w.step()
+    assert len(w.contacts) == 2
+    w0 = -10.0   # spin about +x: rolls towards +y
+    w.set_twist([w0, 0, 0], [0, 0, 0])
+    for _ in range(1500):
+        w.step()
+    om, v = w.twist
+    vw = w.R @ v
+    omw = w.R @ om
+    assert vw[1] == pytest.approx(-omw[0] * r, rel=0.02)           # rolling: v = omega r
+    assert vw[1] == pytest.approx(-w0 * r / 3.0, rel=0.03)          # I = m r^2 / 2
+    assert w.p[2] == pytest.approx(r, abs=2e-3) and abs(vw[0]) < 1e-3
+    assert len(w.contacts) == 2
+
+
+def test_cylinder_geometry_compiles_alike(oracle):
+    from mwstep import native as N
+    from test_sdf_models import _compile, _compare
+    N.lib()
+    rc, got = _compile(N, cylinder_urdf(rpy="0.3 0.2 0.1"), (0, 0, 1, 1, 0, 0, 0))
+    assert rc == 0
+    sh = got["shapes"][-1]
+    assert len(sh) == 1 and sh[0, 0] == 2 and list(sh[0, 1:3]) == [0.1, 0.2]
+    _compare(got, oracle.load_urdf(cylinder_urdf(rpy="0.3 0.2 0.1"), pose_xyz=(0, 0, 1)))
+    sdf = ("<sdf version='1.6'><model name='c'><link name='l'><collision name='k'><pose>0 0 0.1 0 0.5 0</pose>"
+           "<geometry><cylinder><radius>0.05</radius><length>0.3</length></cylinder></geometry></collision>"
+           "</link></model></sdf>")
+    rc, got = _compile(N, sdf)
+    assert rc == 0 and got["shapes"][-1][0, 0] == 2
+    np.testing.assert_allclose(got["shapes"][-1][0, 1:3], [0.05, 0.15])
+    _compare(got, oracle.load_urdf(sdf))

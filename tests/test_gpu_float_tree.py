@@ -44,16 +44,21 @@ def _quat_to_R(q):
 TREE_PARENTS = [-1, 0, 1, 1, 3, 3, 0, 6, -1, 8, 8, 8, 11, 2, -1, 14]
 
 
-def tree_urdf(parents=TREE_PARENTS, seed=5, damping=0.0):
+def tree_urdf(parents=TREE_PARENTS, seed=5, damping=0.0, cylinders=False):
     """A floating box base with a random branched tree: revolute / prismatic
     joints about random unit axes, random origins and masses, a sphere on
     every leaf; `damping` > 0 adds viscous joint damping of that size times a
-    random factor in [0.5, 1.5] to every joint."""
+    random factor in [0.5, 1.5] to every joint; `cylinders`: a cylinder base
+    and cylinders on the first two leaves (Physics.cpp builds cylinder
+    collisions; 8 rim slots each)."""
     rng = np.random.default_rng(seed)
+    base_geo = ('<origin rpy="0 1.5708 0"/><geometry><cylinder radius="0.12" length="0.4"/></geometry>'
+                if cylinders else '<geometry><box size="0.4 0.3 0.12"/></geometry>')
     parts = ['<link name="base"><inertial><mass value="4.0"/>'
              '<inertia ixx="0.05" iyy="0.06" izz="0.07" ixy="0.002" ixz="0" iyz="0"/></inertial>'
-             '<collision><geometry><box size="0.4 0.3 0.12"/></geometry></collision></link>']
+             f'<collision>{base_geo}</collision></link>']
     leaves = set(range(len(parents))) - {p for p in parents if p >= 0}
+    cyl_leaves = set(sorted(leaves)[:2]) if cylinders else set()
     for i, pa in enumerate(parents):
         axis = rng.normal(size=3)
         axis /= np.linalg.norm(axis)
@@ -62,7 +67,9 @@ def tree_urdf(parents=TREE_PARENTS, seed=5, damping=0.0):
                '<limit lower="-1.5" upper="1.5" effort="50" velocity="30"/>')
         xyz = " ".join(f"{v:.3f}" for v in rng.uniform(-0.15, 0.15, 3))
         rpy = " ".join(f"{v:.3f}" for v in rng.uniform(-0.5, 0.5, 3))
-        tip = ('<collision><origin xyz="0 0 -0.1"/><geometry><sphere radius="0.03"/></geometry></collision>'
+        tip = ('<collision><origin xyz="0 0 -0.1" rpy="0.3 0 0.2"/><geometry><cylinder radius="0.03" '
+               'length="0.1"/></geometry></collision>' if i in cyl_leaves else
+               '<collision><origin xyz="0 0 -0.1"/><geometry><sphere radius="0.03"/></geometry></collision>'
                if i in leaves else "")
         m = rng.uniform(0.2, 1.0)
         dyn = f'<dynamics damping="{damping * rng.uniform(0.5, 1.5):.4f}"/>' if damping > 0 else ""
@@ -84,6 +91,10 @@ def _model(name):
         return tree_urdf()
     if name == "tree16d":  # joint damping: DART's implicit damping + the dual (impulse) recursion
         return tree_urdf(damping=2.0)
+    if name == "tree16c":  # cylinder collisions on the base and two leaves
+        return tree_urdf(cylinders=True)
+    if name.endswith("c"):
+        return chain_urdf(int(name[-2]), cylinder_tip=True)
     return chain_urdf(int(name[-1]))
 
 
@@ -111,7 +122,8 @@ def _random_states(cm, W, rng):
 
 @pytest.mark.parametrize("name, kernel", [("quadruped", "lane"), ("chain1", "lane"), ("chain2", "lane"),
                                           ("chain3", "lane"), ("quadruped", "wave"), ("chain2", "wave"),
-                                          ("humanoid32", "wave"), ("tree16", "wave"), ("tree16d", "wave")])
+                                          ("humanoid32", "wave"), ("tree16", "wave"), ("tree16d", "wave"),
+                                          ("chain2c", "lane"), ("chain2c", "wave"), ("tree16c", "wave")])
 def test_one_step_parity_with_contacts(require_gpu, oracle, monkeypatch, name, kernel):
     from mwstep import native as N
     from mwstep.sim import Simulator

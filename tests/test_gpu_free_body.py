@@ -16,6 +16,7 @@ first slice: single floating bodies).
 import numpy as np
 import pytest
 
+from test_cylinder_oracle import cylinder_urdf
 from test_free_body_oracle import cube_urdf, sphere_urdf
 
 pytestmark = pytest.mark.gpu
@@ -63,10 +64,11 @@ def _quat_to_R(q):
                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
 
 
-@pytest.mark.parametrize("urdf", ["cube", "double", "sphere"])
+@pytest.mark.parametrize("urdf", ["cube", "double", "sphere", "cylinder"])
 def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
     from mwstep.sim import Simulator
-    text = {"cube": cube_urdf(), "double": cube_urdf(True), "sphere": sphere_urdf()}[urdf]
+    text = {"cube": cube_urdf(), "double": cube_urdf(True), "sphere": sphere_urdf(),
+            "cylinder": cylinder_urdf(rpy="0.2 0 0")}[urdf]
     W, pgs = 256, 50
     rng = np.random.default_rng(5)
     sim = Simulator(text, n_worlds=W, pgs_iters=pgs)
@@ -171,3 +173,48 @@ def test_run_device_equals_run(require_gpu):
     assert len(sims[0].contacts(5)) > 0
     for s in sims:
         s.close()
+
+
+def test_cylinder_kats_on_the_free_body_kernel(require_gpu, oracle):
+    """The oracle's cylinder KATs (tests/test_cylinder_oracle.py) on the HIP
+    free-body kernel: a standing cylinder rests at half its length carrying its
+    weight on 4 rim points; a lying one spun about its axis rolls without
+    slipping at omega0 r / 3; both follow the fp64 oracle step by step."""
+    import math
+    from mwstep.sim import Simulator
+    from test_cylinder_oracle import cylinder_urdf
+    sim = Simulator(cylinder_urdf(), n_worlds=2, pose=(0, 0, 0.25, 1, 0, 0, 0), pgs_iters=100)
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    for _ in range(600):
+        sim.run()
+    p = sim.base_pose()
+    assert p[:, 2] == pytest.approx(0.2, abs=2e-3)
+    c = sim.contacts(0)
+    assert len(c) == 4 and float(np.sum(c[:, 8])) == pytest.approx(2.0 * G, abs=0.05)
+    sim.close()
+    r, m = 0.1, 2.0
+    ixx = m * (3 * r * r + 0.16) / 12.0
+    text = (f'<robot name="roll"><link name="roll"><inertial><mass value="{m}"/>'
+            f'<inertia ixx="{0.5 * m * r * r}" iyy="{ixx}" izz="{ixx}" ixy="0" ixz="0" iyz="0"/></inertial>'
+            f'<collision><origin rpy="0 {math.pi / 2} 0" xyz="0 0 0"/><geometry>'
+            f'<cylinder radius="{r}" length="0.4"/></geometry></collision></link></robot>')
+    sim = Simulator(text, n_worlds=2, pose=(0, 0, r, 1, 0, 0, 0), pgs_iters=100)
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    ow = oracle.FreeWorld(oracle.load_urdf(text, pose_xyz=(0, 0, r)), mu=1.0, pgs_iters=100)
+    for _ in range(100):
+        sim.run()
+        ow.step()
+    sim.reset_base_velocity([[0, 0, 0, -10.0, 0, 0]] * 2)
+    ow.set_twist(ow.R.T @ np.array([-10.0, 0, 0]), [0, 0, 0])
+    worst = 0.0
+    for k in range(1500):
+        sim.run()
+        ow.step()
+        worst = max(worst, float(np.abs(sim.base_pose()[0, :3] - ow.p).max()))
+    v = sim.base_velocity()[0]
+    assert v[1] == pytest.approx(10.0 * r / 3.0, rel=0.03) and v[1] == pytest.approx(-v[3] * r, rel=0.02)
+    print(f"rolling cylinder: v {v[1]:.4f} (omega0 r / 3 = {10 * r / 3:.4f}), max |dp| vs oracle {worst:.2e}")
+    assert worst <= 2e-4
+    sim.close()

@@ -170,6 +170,47 @@ def test_one_step_parity_random_piles(require_gpu, oracle):
     sc.close()
 
 
+def test_cylinders_on_the_ground_one_step(require_gpu, oracle):
+    """Cylinder collisions (ground plane only in this build: 4 rim points per
+    cap from the deepest one, chain_dyn.hpp shape_slot_point / oracle.c
+    or_slot_point) on the scene kernel: a free cylinder at random tilts and
+    heights next to a cube, one step vs the fp64 scene oracle over 256 worlds
+    (poses 1e-5, velocities 2e-3, contact points 1e-5); a model pair with a
+    cylinder makes no body-body contact (documented restriction)."""
+    from test_cylinder_oracle import cylinder_urdf
+    W, pgs, mu = 256, 50, 0.8
+    rng = np.random.default_rng(9)
+    texts = [cylinder_urdf(), cube_urdf()]
+    base = [(0.0, 0.0, 0.2), (0.05, 0.0, 0.3)]
+    cms = [oracle.load_urdf(t, pose_xyz=b) for t, b in zip(texts, base)]
+    sc = _scene([(t, (*b, 1, 0, 0, 0), nm) for t, b, nm in zip(texts, base, ["can", "cube"])], W, pgs, mu)
+    poses = np.array([np.concatenate([[0, 0, rng.uniform(0.08, 0.22)], _rand_quat(rng, np.pi)]) for _ in range(W)])
+    sc.reset_base_pose(0, poses)
+    sc.reset_base_velocity(0, np.column_stack([rng.uniform(-0.5, 0.5, (W, 3)), rng.uniform(-2, 2, (W, 3))]))
+    sc.run(paused=True)
+    orcs = [_oracle_from_gpu(oracle, cms, sc, w, pgs, mu) for w in range(W)]
+    sc.run()
+    worst = dict(pose=0.0, vel=0.0, point=0.0)
+    n_contact = 0
+    for w in range(W):
+        ow = orcs[w]
+        ow.step()
+        e = _compare(oracle, cms, sc, ow, w)
+        gc = sc.contacts(w)
+        assert len(gc) == len(ow.contacts), (w, len(gc), len(ow.contacts))
+        for row, (oc, who) in zip(gc, ow.contacts):
+            assert tuple(int(v) for v in row[10:14]) == who and who[2] < 0
+            n_contact += who[0] == 0
+            worst["point"] = max(worst["point"], float(np.abs(row[0:3] - oc[0:3]).max()))
+        worst["pose"] = max(worst["pose"], e["pose"])
+        worst["vel"] = max(worst["vel"], e["vel"])
+    print(f"cylinders x{W}: one-step " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
+          f", {n_contact} cylinder-ground contact points")
+    assert n_contact > W
+    assert worst["pose"] <= 1e-5 and worst["point"] <= 1e-5 and worst["vel"] <= 2e-3
+    sc.close()
+
+
 @pytest.mark.parametrize("double", [False, True])
 def test_three_cubes_kat(require_gpu, double):
     """tests/test_scenario/test_contacts.py:125-236 through the scene API."""

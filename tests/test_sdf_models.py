@@ -180,10 +180,14 @@ def random_sdf_tree(seed, attach="floating", n_links=7):
         for _ in range(rng.integers(0, 3)):
             if slots + 8 > 32:
                 break
-            box = rng.random() < 0.4
-            slots += 8 if box else 1
+            u = rng.random()
+            box, cyl = u < 0.3, 0.3 <= u < 0.55
+            slots += 8 if (box or cyl) else 1
             if box:
                 geo = f"<box><size>{' '.join(f'{v:.17g}' for v in rng.uniform(0.05, 0.4, 3))}</size></box>"
+            elif cyl:
+                geo = (f"<cylinder><radius>{rng.uniform(0.02, 0.2):.17g}</radius>"
+                       f"<length>{rng.uniform(0.05, 0.5):.17g}</length></cylinder>")
             else:
                 geo = f"<sphere><radius>{rng.uniform(0.02, 0.2):.17g}</radius></sphere>"
             col += f"<collision name='c{k}_{len(col)}'><pose>{_pose(rng, 0.2)}</pose><geometry>{geo}</geometry></collision>"
