@@ -182,9 +182,11 @@ int mw_controller_period(const mw_sim* sim, double* period);
 
 /* ---- floating bases (root link not attached to "world": a DART FreeJoint
  * root).  This build steps single floating bodies and articulated models on
- * a floating base (serial chains of 1..3 joints, the quadruped tree), with
- * box / sphere collision shapes on any link against a ground plane z = 0 and
- * a contact LCP with friction ---- */
+ * a floating base (any tree of <= 48 bodies), with box / sphere / cylinder
+ * collision shapes on any link against a ground plane z = 0 and a contact LCP
+ * with friction.  Fixed-base trees outside the compiled chain topologies run
+ * on the same world-per-wavefront kernel with a welded base; for every
+ * fixed-base model the base getters return the model frame at rest ---- */
 int mw_is_floating(const mw_sim* sim, int32_t* floating);
 /* Model::basePosition / baseOrientation: out [nw][7] = x y z qw qx qy qz. */
 int mw_get_base_pose(const mw_sim* sim, int32_t w0, int32_t nw, double* out);
