@@ -178,13 +178,14 @@ def main():
     panda = None
     if not args.no_panda and args.task != "PandaPositionTracking":
         panda = panda_leg(args, dev, torch, dist, world_size, rank)
-    contacts = quadruped = humanoid = None
+    contacts = quadruped = humanoid = humanoid_warm = None
     if not args.no_contact_leg:
         if rank == 0 and world_size == 1:
             contacts = contact_leg(args, dev, torch)
             quadruped = quadruped_leg(args, dev, torch)
         # BASELINE config 5: 512 global humanoid worlds split over the ranks
         humanoid = humanoid_leg(args, dev, torch, dist, world_size, rank)
+        humanoid_warm = humanoid_leg(args, dev, torch, dist, world_size, rank, pgs_opts=(1e-6, True))
     runtime = None
     if rank == 0 and world_size == 1 and not args.no_runtime_leg:
         runtime = runtime_leg(args, dev)
@@ -251,6 +252,7 @@ def main():
             "contacts_floating": contacts,
             "quadruped_floating": quadruped,
             "humanoid_c5": humanoid,
+            "humanoid_c5_warm_pgs": humanoid_warm,
             "runtime_c1": runtime,
             "scene_multi_model": scene,
         }
@@ -521,7 +523,7 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
     return out
 
 
-def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512, pgs=50):
+def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512, pgs=50, pgs_opts=(0.0, False)):
     """BASELINE config 5: 512 iCub-class humanoids in total (models/humanoid32.urdf:
     32 dofs, 36.4 kg, floating base, box feet) split over the ranks, standing on
     the ground plane under the JointController PID hold (stiff legs / torso,
@@ -543,18 +545,25 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
     xy = rng.uniform(-5, 5, (W_global, 2))
     out = float_tree_leg(args, dev, torch, "humanoid32", e - b, pgs, 0.535, gains,
                          q0[b:e], np.zeros((e - b, n)), xy[b:e], K=200, G=20, warm=40,
-                         dist=dist, world_size=world_size)
+                         dist=dist, world_size=world_size, pgs_opts=pgs_opts)
     out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
     out["scaling"] = "strong"
     out["worlds_per_gpu"] = e - b
     out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
                        f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "
                        f"PGS {pgs} iterations, dt = 1 ms (BASELINE.json configs[4])")
+    if pgs_opts[0] > 0.0 or pgs_opts[1]:
+        out["workload"] = out["workload"].replace(
+            f"PGS {pgs} iterations", f"PGS warm-started from the previous step's impulses, ending when a sweep "
+            f"changes no constraint velocity by more than {pgs_opts[0]:g} m/s (at most {pgs} sweeps; "
+            f"mw_set_pgs_options)")
+        out["accuracy"] = ("closer to the exact boxed-LCP step (DART's Dantzig result) than the cold PGS-50 "
+                           "step: tests/test_gpu_float_tree.py::test_humanoid_warm_started_pgs")
     return out
 
 
 def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, K=500, G=50, warm=100,
-                   dist=None, world_size=1):
+                   dist=None, world_size=1, pgs_opts=(0.0, False)):
     """Time W floating-base worlds of `model` under a PID hold, one physics
     step per run, replayed from hipGraphs of mw_run_device; with several ranks
     the timed region is bracketed by barriers and the max over ranks is kept."""
@@ -567,6 +576,8 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, 
                     stream=stream.cuda_stream, pose=(0, 0, z0, 1, 0, 0, 0))
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
+    if pgs_opts[0] > 0.0 or pgs_opts[1]:
+        sim.set_pgs_options(*pgs_opts)
     sim.set("reset_q", q0)
     pose = np.column_stack([xy, np.full(W, z0), np.ones(W), np.zeros((W, 3))])
     sim.reset_base_pose(pose)

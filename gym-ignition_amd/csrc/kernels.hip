@@ -593,6 +593,14 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     const int w = xcd_block();  // XCD-aware (xcd.hpp): neighbouring worlds share state lines
     const int lane = lane_id();
     __shared__ WaveWorld<MAXN> L;
+    // warm start: a world whose base or joints were reset starts cold
+    bool warm_reset = A.first && D.rflag[w] != 0;
+    if (A.warm) {
+        if (A.first && lane < N) warm_reset = warm_reset || S.rflag[static_cast<size_t>(lane) * W + w] != 0;
+        warm_reset = __ballot(warm_reset) != 0;
+        for (int e = lane; e < kWaveWarmWords; e += kWaveLanes)
+            L.xw[e] = warm_reset ? 0.f : D.warm[static_cast<size_t>(e) * W + w];
+    }
     FreeState base = load_base(D, W, w, A.first);
     uint32_t act = 0u;
     float cmd = 0.f, vc = 0.f;
@@ -626,7 +634,8 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
                 L.tau[lane] = dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
             MW_PROF_T(tb);
             MW_PROF_ACC(0, ta, tb);
-            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, L.qdd, &ovf, prof);
+            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0, L.qdd, &ovf,
+                                           prof);
             MW_PROF_T(tc);
             MW_PROF_ACC(7, ta, tc);
         }
@@ -648,6 +657,8 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
         store_base(D, W, w, base);
         if (ovf) atomicAdd(overflow, ovf);
     }
+    if (A.warm)  // also after a paused run: it may have consumed a reset
+        for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) D.warm[static_cast<size_t>(e) * W + w] = L.xw[e];
     if (want_contacts && !A.paused) {
         if (lane == 0) D.cmask[w] = active;
         if (lane < 32 && ((active >> lane) & 1u)) {

@@ -40,6 +40,7 @@ struct FreeDev {
     uint8_t* rflag = nullptr;  // [W] bit0 pose reset, bit1 velocity reset
     float* cdata = nullptr;    // [kMaxFreeSlots][7][W] contact point xyz, force xyz, depth
     uint32_t* cmask = nullptr; // [W] active contact slots
+    float* warm = nullptr;     // [kWaveWarmWords][W] previous step's PGS impulses (wave kernel, warm start)
 };
 
 // One launch of the scenario kernel covers up to 64 substeps of a run.
@@ -50,6 +51,8 @@ struct RunArgs {
     int pgs_iters;
     int first;            // first launch of the run: resets + force commands apply
     uint64_t pid_gate;    // bit s: the JointController computes a new PID force at substep s
+    float pgs_tol;        // > 0: a PGS sweep that moved no impulse by more than pgs_tol max|x| ends the solve
+    int warm;             // PGS starts from the previous step's impulses (wave kernel)
 };
 
 // Task description for the device-side env (see sim.cpp for the sources).
@@ -107,6 +110,8 @@ hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const struct Float
                            const FreeDev& D, const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow,
                            hipStream_t st);
 constexpr int kWaveMaxDepthHost = 12;
+// words of the wave kernel's warm-start record per world (wave_tree.hpp kWaveWarmWords)
+constexpr int kWaveWarmWordsHost = 3 * 32 + 3 * kMaxBodies;
 // workspace words per world of a floating-tree model, -1 if n is not compiled in
 int float_workspace_words(int n, int n_slots);
 

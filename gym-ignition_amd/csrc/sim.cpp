@@ -139,6 +139,9 @@ struct mw_sim {
     mw::PidF* h_pid = nullptr;    // pinned staging copy
     bool pid_dirty = true;        // gains changed since the last upload
     int* d_overflow = nullptr;    // constraint rows dropped by the wave kernel
+    float* d_warm = nullptr;      // wave kernel: previous step's PGS impulses [kWaveWarmWordsHost][W]
+    double pgs_tol = 0.0;         // mw_set_pgs_options
+    bool pgs_warm = false;
     int* h_overflow = nullptr;    // pinned copy read back with each synchronous run
     int64_t overflow_seen = 0;    // drops already reported
     mw::SimDev dev;
@@ -540,6 +543,7 @@ void mw_destroy(mw_sim* s) {
         (void)hipFree(s->d_pid);
         (void)hipHostFree(s->h_pid);
         (void)hipFree(s->d_overflow);
+        (void)hipFree(s->d_warm);
         (void)hipHostFree(s->h_overflow);
         (void)hipHostFree(s->h_base);
         (void)hipHostFree(s->h_cdata);
@@ -726,6 +730,9 @@ int mw_initialize(mw_sim* s) {
                 MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
                 MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int), hipHostMallocDefault));
                 *s->h_overflow = 0;
+                const size_t wb = static_cast<size_t>(mw::kWaveWarmWordsHost) * W * sizeof(float);
+                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_warm), wb));
+                MW_HIP(hipMemsetAsync(s->d_warm, 0, wb, s->stream));
             } else {
                 const size_t words = static_cast<size_t>(mw::float_workspace_words(s->n, s->n_slots));
                 MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ws), words * W * sizeof(float)));
@@ -740,6 +747,7 @@ int mw_initialize(mw_sim* s) {
         s->fdev.cdata = f + 26 * W;
         s->fdev.cmask = reinterpret_cast<uint32_t*>(f + nf);
         s->fdev.rflag = reinterpret_cast<uint8_t*>(s->fdev.cmask + W);
+        s->fdev.warm = s->d_warm;
         MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_base), 13 * W * sizeof(float), hipHostMallocDefault));
         MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_cdata), 7 * ns * W * sizeof(float),
                              hipHostMallocDefault));
@@ -948,6 +956,8 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
     a.paused = paused ? 1 : 0;
     a.pgs_iters = s->cfg.pgs_iters;
+    a.pgs_tol = static_cast<float>(s->pgs_tol);
+    a.warm = (s->wave && s->pgs_warm && s->d_warm) ? 1 : 0;
     a.first = 1;
     const int spr = s->cfg.steps_per_run;
     int done = 0;
@@ -1522,6 +1532,27 @@ int mw_reset_base_velocity(mw_sim* s, int32_t w0, int32_t nw, const double* in) 
         s->h_rflag[w0 + k] |= 2u;
     }
     s->free_dirty = true;
+    return MW_OK;
+}
+
+int mw_set_pgs_options(mw_sim* s, double tol, int32_t warm_start) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    if (!(tol >= 0.0) || tol >= 1.0) return fail(MW_EINVAL, "the PGS velocity tolerance must be in [0, 1)");
+    const bool warm = warm_start != 0;
+    if (warm && !s->pgs_warm && s->d_warm) {
+        // a fresh warm start: no stale impulses from before the option was off
+        MW_HIP(hipMemsetAsync(s->d_warm, 0, static_cast<size_t>(mw::kWaveWarmWordsHost) * s->W * sizeof(float),
+                              s->stream));
+    }
+    s->pgs_tol = tol;
+    s->pgs_warm = warm;
+    return MW_OK;
+}
+
+int mw_pgs_options(const mw_sim* s, double* tol, int32_t* warm_start) {
+    if (!s || !tol || !warm_start) return fail(MW_EINVAL, "null argument");
+    *tol = s->pgs_tol;
+    *warm_start = s->pgs_warm ? 1 : 0;
     return MW_OK;
 }
 

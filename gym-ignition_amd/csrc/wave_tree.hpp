@@ -34,6 +34,11 @@ namespace dev {
 constexpr int kWaveLanes = 64;
 constexpr int kWaveMaxRows = 64;
 constexpr int kWaveMaxDepth = 12;
+// warm-start record of the PGS impulses by row identity: contact slot rows
+// 3 slot + d (d: normal, t1, t2), joint rows kWaveWarmJoint0 + 3 dof + t (t:
+// limit, servo, Coulomb) -- oracle.h OR_WARM_* (its slot capacity is larger)
+constexpr int kWaveWarmJoint0 = 3 * kMaxFloatSlots;
+constexpr int kWaveWarmWords = kWaveWarmJoint0 + 3 * kMaxBodies;
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 
@@ -91,6 +96,7 @@ struct WaveWorld {
     float s_x[kMaxFloatSlots][3];   // impulses (output)
     // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
     float stack[kWaveMaxDepth][7][kWaveLanes];
+    float xw[kWaveWarmWords];    // warm-start impulses (RunArgs::warm)
 };
 
 __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63u); }
@@ -336,12 +342,68 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
     return jv;
 }
 
+// Projected Gauss-Seidel sweeps over the rows (see wave_step): impulses x[r]
+// uniform in registers, residual w_c = sum_r A[c][r] x_r in lane c, rows in
+// order, padded to blocks of 8 with inert rows.  TOL: end once a sweep changed
+// no row's constraint velocity w_r = (A x)_r by more than pgs_tol -- measured
+// in velocity space, where the redundant contact corners' null directions (A
+// conditioned ~1e5 by CFM 1e-5: impulse changes there move nothing, and fp32
+// round-off keeps them moving) do not count.  One wave max per sweep; a
+// separate instance so the fixed-count solve pays nothing for it.
+template <int MAXN, bool TOL>
+__device__ __forceinline__ void wave_pgs(const WaveWorld<MAXN>& L, const float (&a)[kWaveMaxRows],
+                                         float (&x)[kWaveMaxRows], int Rpad, int ncr, float mu, int pgs_iters,
+                                         float pgs_tol) {
+    for (int it = 0; it < pgs_iters; ++it) {
+        float w = 0.f;
+#pragma unroll
+        for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
+            if (rb >= Rpad) break;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w += a[rb + k] * x[rb + k];
+        }
+        const float w_start = w;
+        float h = 0.f;  // mu x_normal of the current contact (set by its normal row)
+#pragma unroll
+        for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
+            if (rb >= Rpad) break;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = rb + k;
+                // dependent chain per row: lane read of w_r, one fma, the
+                // clamp, one fma into w (x + b/A_rr and w - A[.][r] x_r are
+                // formed off the chain)
+                const F4 c = L.rc[r];
+                const float xb = fmaf(c.x, c.y, x[r]);
+                const float wpre = fmaf(-a[r], x[r], w);
+                float v = fmaf(-read_lane(w, r), c.y, xb);
+                if (r % 3 == 0) {
+                    v = clamp_ordered(v, c.z, c.w);  // normal row (0, inf) or joint row
+                    h = mu * v;                      // friction bound of this contact
+                } else {  // friction row |x| <= mu x_normal, or joint row
+                    const bool fr = r < ncr;
+                    v = clamp_ordered(v, fr ? -h : c.z, fr ? h : c.w);
+                }
+                w = fmaf(a[r], v, wpre);
+                x[r] = v;
+            }
+        }
+        if (TOL) {
+            float d = fabsf(w - w_start);
+#pragma unroll
+            for (int m = 1; m < kWaveLanes; m <<= 1) d = fmaxf(d, __shfl_xor(d, m));
+            if (d <= pgs_tol) break;
+        }
+    }
+}
+
 // One engine step of world L (state in L.q / L.qd / base; joint forces in
 // L.tau).  Returns the active slot mask; *overflow += rows dropped.
 template <int MAXN, bool CONS>
 __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                               FreeState& base, WaveWorld<MAXN>& L, float dt, int pgs_iters,
-                                              float* qdd_out, int* overflow, unsigned long long* prof) {
+                                              float pgs_tol, bool warm, float* qdd_out, int* overflow,
+                                              unsigned long long* prof) {
     const int lane = lane_id();
     const int NV = 6 + N;
     MW_PROF_T(t0);
@@ -609,42 +671,19 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         }
         const float mu = F->mu;
         float x[kWaveMaxRows];
-#pragma unroll
-        for (int r = 0; r < kWaveMaxRows; ++r) x[r] = 0.f;
-        for (int it = 0; it < pgs_iters; ++it) {
-            float w = 0.f;
-#pragma unroll
-            for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
-                if (rb >= Rpad) break;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) w += a[rb + k] * x[rb + k];
-            }
-            float h = 0.f;  // mu x_normal of the current contact (set by its normal row)
-#pragma unroll
-            for (int rb = 0; rb < kWaveMaxRows; rb += 8) {
-                if (rb >= Rpad) break;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int r = rb + k;
-                    // dependent chain per row: lane read of w_r, one fma, the
-                    // clamp, one fma into w (x + b/A_rr and w - A[.][r] x_r
-                    // are formed off the chain)
-                    const F4 c = L.rc[r];
-                    const float xb = fmaf(c.x, c.y, x[r]);
-                    const float wpre = fmaf(-a[r], x[r], w);
-                    float v = fmaf(-read_lane(w, r), c.y, xb);
-                    if (r % 3 == 0) {
-                        v = clamp_ordered(v, c.z, c.w);  // normal row (0, inf) or joint row
-                        h = mu * v;                      // friction bound of this contact
-                    } else {  // friction row |x| <= mu x_normal, or joint row
-                        const bool fr = r < ncr;
-                        v = clamp_ordered(v, fr ? -h : c.z, fr ? h : c.w);
-                    }
-                    w = fmaf(a[r], v, wpre);
-                    x[r] = v;
-                }
-            }
+        // warm start: every row from the previous step's impulse of the same
+        // row identity (contact slot / joint row), else 0
+        float x0 = 0.f;
+        if (warm && lane < R) {
+            const int src = L.src[lane];
+            x0 = L.xw[(src < kJointRow) ? src : kWaveWarmJoint0 + (src - kJointRow)];
         }
+#pragma unroll
+        for (int r = 0; r < kWaveMaxRows; ++r) x[r] = warm ? read_lane(x0, r) : 0.f;
+        if (pgs_tol > 0.f)
+            wave_pgs<MAXN, true>(L, a, x, Rpad, ncr, mu, pgs_iters, pgs_tol);
+        else
+            wave_pgs<MAXN, false>(L, a, x, Rpad, ncr, mu, pgs_iters, 0.f);
         MW_PROF_T(t5);
         MW_PROF_ACC(5, t4, t5);
         // ---- nu += MJ^T x (lane = component); impulses to the slots ----------------
@@ -664,6 +703,15 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             if (src < kJointRow) L.s_x[src / 3][src % 3] = xl;
         }
         if (lane < NV) L.nu[lane] += dnu;
+        if (warm) {
+            for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) L.xw[e] = 0.f;
+            if (lane < R) {
+                const int src = L.src[lane];
+                L.xw[(src < kJointRow) ? src : kWaveWarmJoint0 + (src - kJointRow)] = xl;
+            }
+        }
+    } else if (warm) {
+        for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) L.xw[e] = 0.f;
     }
 
     // ---- integratePositions ---------------------------------------------------

@@ -97,6 +97,8 @@ SIGNATURES = [
     ("mw_joint_param", ctypes.c_int, [_P, _I, _I, _D]),
     ("mw_model_export", ctypes.c_int, [_P, _D, _I]),
     ("mw_model_export_base", ctypes.c_int, [_P, _D]),
+    ("mw_set_pgs_options", ctypes.c_int, [_P, ctypes.c_double, _I]),
+    ("mw_pgs_options", ctypes.c_int, [_P, _D, _IP]),
     ("mw_model_export_shapes", ctypes.c_int, [_P, _I, _D, _I, _IP]),
     ("mw_device_params", ctypes.c_int, [_P, _P, _I]),
     ("mw_device_float_params", ctypes.c_int, [_P, _P, _I]),

@@ -276,6 +276,15 @@ class Simulator:
                                               cap, ctypes.byref(n)), "contact_bodies")
         return out[:min(n.value, cap)].copy()
 
+    def set_pgs_options(self, tol: float = 0.0, warm_start: bool = False) -> None:
+        """mw_set_pgs_options: PGS tolerance exit and warm start (world-per-wavefront kernel)."""
+        N.check(N.lib().mw_set_pgs_options(self.handle, float(tol), 1 if warm_start else 0), "set_pgs_options")
+
+    def pgs_options(self):
+        t, w = ctypes.c_double(), ctypes.c_int32()
+        N.check(N.lib().mw_pgs_options(self.handle, ctypes.byref(t), ctypes.byref(w)))
+        return t.value, bool(w.value)
+
     def float_kernel(self) -> int:
         """0: not an articulated floating model, 1: world-per-lane kernel, 2: world-per-wavefront kernel."""
         v = ctypes.c_int32()

@@ -197,6 +197,18 @@ int mw_get_base_velocity(const mw_sim* sim, int32_t w0, int32_t nw, double* out)
  * the next run (pose first, then the velocity). */
 int mw_reset_base_pose(mw_sim* sim, int32_t w0, int32_t nw, const double* pose);
 int mw_reset_base_velocity(mw_sim* sim, int32_t w0, int32_t nw, const double* lin_ang);
+/* Contact / joint-row solver options of the world-per-wavefront kernel
+ * (articulated floating bases, generic fixed trees).  DART's primary boxed-LCP
+ * solver is Dantzig's exact pivoting method [EXT]; the kernel runs projected
+ * Gauss-Seidel sweeps (mw_config.pgs_iters).  tol > 0 ends the sweeps once a
+ * sweep changed no row's constraint velocity (J dqd, m/s or rad/s) by more
+ * than tol -- velocity space, where the redundant contact corners' null
+ * directions do not count; warm_start != 0 starts
+ * every row from the previous step's impulse of the same contact slot / joint
+ * row (cold after a reset of the world).  Defaults: 0, 0 (a fixed sweep
+ * count from zero).  Other kernels ignore both. */
+int mw_set_pgs_options(mw_sim* sim, double tol, int32_t warm_start);
+int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
 /* The world's ground plane (z = 0, normal +z) and its friction coefficient. */
 int mw_set_ground_plane(mw_sim* sim, int32_t enabled, double mu);
 /* Model::enableContacts / contactsEnabled (Model.cpp:674-700). */

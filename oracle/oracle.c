@@ -1462,6 +1462,16 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                   const double* cmd, int pgs_iters, double* c_pos, double* c_force, double* c_depth,
                   int32_t* c_body)
 {
+    return or_float_step_warm(m, dt, s, mode, cmd, pgs_iters, 0.0, 0, c_pos, c_force, c_depth, c_body);
+}
+
+/* The impulses of the previous step's rows, by row identity: contact slot
+ * rows 3 slot + d (d: normal, t1, t2), joint rows OR_WARM_JOINT0 + 3 dof + t
+ * (t: limit, servo, Coulomb) -- the kernels' warm-start layout. */
+int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, const int32_t* mode,
+                       const double* cmd, int pgs_iters, double pgs_tol, double* warm, double* c_pos,
+                       double* c_force, double* c_depth, int32_t* c_body)
+{
     const or_model* t = &m->tree;
     const int n = t->n, nv = 6 + n;
     or_fkin k;
@@ -1492,6 +1502,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
     int nc = 0;
     double cw[OR_MAXFC][3], depth[OR_MAXFC], cb[OR_MAXFC][3];
     int cbody[OR_MAXFC];
+    int slot_id = 0, cslot[OR_MAXFC];
     if (m->ground) {
         for (int sh = 0; sh < m->n_shapes; ++sh) {
             const int bi = m->shape_body[sh];
@@ -1503,7 +1514,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
             const int corners = (m->shape_type[sh] == 1) ? 1 : 8;
             double RS[9];
             rot_mul(Rb, SR, RS);
-            for (int corner = 0; corner < corners; ++corner) {
+            for (int corner = 0; corner < corners; ++corner, ++slot_id) {
                 double l[3];
                 or_slot_point(m->shape_type[sh], hh, RS, corner, l);
                 double b[3], x[3];
@@ -1521,6 +1532,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                     memcpy(cb[nc], b, sizeof b);
                     depth[nc] = dep;
                     cbody[nc] = bi;
+                    cslot[nc] = slot_id;
                     ++nc;
                 }
             }
@@ -1535,6 +1547,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
     double bb[3 * OR_MAXFC + 3 * OR_MAXB], lo[3 * OR_MAXFC + 3 * OR_MAXB], hi[3 * OR_MAXFC + 3 * OR_MAXB];
     double cfm[3 * OR_MAXFC + 3 * OR_MAXB], x[3 * OR_MAXFC + 3 * OR_MAXB];
     int kind[3 * OR_MAXFC + 3 * OR_MAXB];
+    int wid[3 * OR_MAXFC + 3 * OR_MAXB];
     int nr = 0;
     const double nrm[3] = {0, 0, 1};
     double t1[3], t2[3];
@@ -1563,6 +1576,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
             bb[nr] = -vrel + bounce;
             kind[nr] = d == 0 ? K_NORMAL : K_FRIC;
             cfm[nr] = OR_C_CFM;
+            wid[nr] = 3 * cslot[c] + d;
             ++nr;
         }
     }
@@ -1582,6 +1596,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                 if (bounce > OR_MAX_ERV) bounce = OR_MAX_ERV;
                 if (bounce < -OR_MAX_ERV) bounce = -OR_MAX_ERV;
                 bb[nr] = -qdi + bounce;
+                wid[nr] = OR_WARM_JOINT0 + 3 * i;
                 rows_i[nri++] = nr++;
             }
         }
@@ -1593,6 +1608,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                 bb[nr] = vc - qdi;
                 lo[nr] = -t->effort[i] * dt;
                 hi[nr] = t->effort[i] * dt;
+                wid[nr] = OR_WARM_JOINT0 + 3 * i + 1;
                 rows_i[nri++] = nr++;
             }
         }
@@ -1600,6 +1616,7 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
             bb[nr] = -qdi;
             hi[nr] = t->friction[i] * dt;
             lo[nr] = -hi[nr];
+            wid[nr] = OR_WARM_JOINT0 + 3 * i + 2;
             rows_i[nri++] = nr++;
         }
         for (int r = 0; r < nri; ++r) {
@@ -1619,10 +1636,12 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                 A[r * nr + c] = a;
             }
             A[r * nr + r] *= 1.0 + cfm[r];
-            x[r] = 0.0;
+            x[r] = warm ? warm[wid[r]] : 0.0;
         }
         g_pgs_sweeps = 0;
         for (int it = 0; it < pgs_budget(pgs_iters); ++it) {
+            double x_start[3 * OR_MAXFC + 3 * OR_MAXB];
+            memcpy(x_start, x, sizeof(double) * (size_t)nr);
             for (int r = 0; r < nr; ++r) {
                 double acc_r = bb[r];
                 for (int c = 0; c < nr; ++c) acc_r -= A[r * nr + c] * x[c];
@@ -1639,6 +1658,17 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
                 x[r] = v;
             }
             pgs_count(it);
+            /* tolerance exit (the kernels' pgs_tol): the sweep changed no row's
+             * constraint velocity (A x)_r by more than pgs_tol */
+            if (pgs_tol > 0.0 && pgs_iters >= 0) {
+                double dmax = 0.0;
+                for (int r = 0; r < nr; ++r) {
+                    double dw = 0.0;
+                    for (int c = 0; c < nr; ++c) dw += A[r * nr + c] * (x[c] - x_start[c]);
+                    if (fabs(dw) > dmax) dmax = fabs(dw);
+                }
+                if (dmax <= pgs_tol) break;
+            }
         }
         if (pgs_iters < 0) {
             int findex[3 * OR_MAXFC + 3 * OR_MAXB];
@@ -1650,6 +1680,10 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
         }
         for (int r = 0; r < nr; ++r)
             for (int e = 0; e < nv; ++e) nu[e] += MJ[r][e] * x[r];
+    }
+    if (warm) {
+        for (int e = 0; e < OR_WARM_WORDS; ++e) warm[e] = 0.0;
+        for (int r = 0; r < nr; ++r) warm[wid[r]] = x[r];
     }
 
     /* integratePositions: q += dt qd; T0 <- T0 exp(dt V0) */

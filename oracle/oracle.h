@@ -172,6 +172,18 @@ typedef struct {
 int or_float_step(const or_float_model* m, double dt, or_float_state* s, const int32_t* mode,
                   const double* cmd, int pgs_iters, double* c_pos, double* c_force, double* c_depth,
                   int32_t* c_body);
+/* or_float_step with the kernels' solver options: pgs_tol > 0 ends the sweeps
+ * once a sweep changed no row's constraint velocity (A x)_r by more than
+ * pgs_tol; warm (NULL:
+ * cold) holds the previous step's impulses by row identity (3 slot + d for
+ * contact slots, OR_WARM_JOINT0 + 3 dof + t for joint rows) and receives this
+ * step's. */
+#define OR_WARM_SLOTS OR_MAXFC
+#define OR_WARM_JOINT0 (3 * OR_WARM_SLOTS)
+#define OR_WARM_WORDS (OR_WARM_JOINT0 + 3 * OR_MAXB)
+int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, const int32_t* mode,
+                       const double* cmd, int pgs_iters, double pgs_tol, double* warm, double* c_pos,
+                       double* c_force, double* c_depth, int32_t* c_body);
 
 /* Floating-base mass matrix ((6+n)^2, row-major) and bias h (gravity +
  * velocity products) at a state (test cross-checks). */

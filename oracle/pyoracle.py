@@ -93,6 +93,7 @@ class OrFreeState(ctypes.Structure):
 
 OR_MAXFS = 16
 OR_MAXFC = 8 * OR_MAXFS
+OR_WARM_WORDS = 3 * OR_MAXFC + 3 * OR_MAXB   # oracle.h OR_WARM_WORDS
 
 
 class OrFloatModel(ctypes.Structure):
@@ -171,6 +172,9 @@ def lib():
         FM, FS = ctypes.POINTER(OrFloatModel), ctypes.POINTER(OrFloatState)
         L.or_float_step.argtypes = [FM, ctypes.c_double, FS, I32, D, ctypes.c_int, D, D, D, I32]
         L.or_float_step.restype = ctypes.c_int
+        L.or_float_step_warm.argtypes = [FM, ctypes.c_double, FS, I32, D, ctypes.c_int, ctypes.c_double, D, D, D,
+                                         D, I32]
+        L.or_float_step_warm.restype = ctypes.c_int
         L.or_scene_step.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, I32, D, D, ctypes.c_int,
                                     D, I32]
         L.or_scene_step.restype = ctypes.c_int
@@ -813,7 +817,7 @@ class FloatWorld:
     kernel.  Base pose (p, R), base twist V = [w; v] in the base frame."""
 
     def __init__(self, cm: ChainModel, dt: float = 1e-3, ground: bool = True, mu: float = 1.0,
-                 pgs_iters: int = 100):
+                 pgs_iters: int = 100, pgs_tol: float = 0.0, warm_start: bool = False):
         assert cm.floating
         m = OrFloatModel()
         ctypes.pointer(m.tree)[0] = cm.model
@@ -840,6 +844,10 @@ class FloatWorld:
         m.mu = mu
         self.m, self.cm = m, cm
         self.dt, self.pgs = dt, pgs_iters
+        # the kernels' solver options (or_float_step_warm): tolerance exit and
+        # warm start from the previous step's impulses (by contact slot / joint row)
+        self.pgs_tol = pgs_tol
+        self.warm = np.zeros(OR_WARM_WORDS) if warm_start else None
         self.s = OrFloatState()
         self.set_pose(cm.base_p, cm.base_R)
         self.mode = np.zeros(cm.n, dtype=np.int32)
@@ -893,8 +901,15 @@ class FloatWorld:
         cmd = self.cmd if cmd is None else np.ascontiguousarray(cmd, dtype=float)
         cp, cf, cd = np.zeros(3 * OR_MAXFC), np.zeros(3 * OR_MAXFC), np.zeros(OR_MAXFC)
         cb = np.zeros(OR_MAXFC, dtype=np.int32)
-        nc = lib().or_float_step(ctypes.byref(self.m), self.dt, ctypes.byref(self.s), _p(mode, ctypes.c_int32),
-                                 _p(cmd), self.pgs, _p(cp), _p(cf), _p(cd), _p(cb, ctypes.c_int32))
+        if self.pgs_tol > 0.0 or self.warm is not None:
+            nc = lib().or_float_step_warm(ctypes.byref(self.m), self.dt, ctypes.byref(self.s),
+                                          _p(mode, ctypes.c_int32), _p(cmd), self.pgs, self.pgs_tol,
+                                          _p(self.warm) if self.warm is not None else None,
+                                          _p(cp), _p(cf), _p(cd), _p(cb, ctypes.c_int32))
+        else:
+            nc = lib().or_float_step(ctypes.byref(self.m), self.dt, ctypes.byref(self.s),
+                                     _p(mode, ctypes.c_int32), _p(cmd), self.pgs, _p(cp), _p(cf), _p(cd),
+                                     _p(cb, ctypes.c_int32))
         self.contacts = [(cp[3 * i:3 * i + 3].copy(), cf[3 * i:3 * i + 3].copy(), float(cd[i]), int(cb[i]))
                          for i in range(nc)]
         return nc

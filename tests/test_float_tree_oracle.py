@@ -167,3 +167,43 @@ def test_standing_quadruped_carries_its_weight(oracle, quad_file):
         assert c[1][2] > 0 and c[2] > 0                           # pushing up, penetrating
     assert np.ptp(heights[-500:]) < 1e-4                           # at rest
     assert abs(heights[-1] - 0.4408) < 2e-3                        # feet 3 cm spheres, small sag
+
+
+def test_warm_started_pgs_mode(oracle):
+    """or_float_step_warm (the wave kernel's mw_set_pgs_options twin): without
+    options it is or_float_step bit for bit; the warm record holds the step's
+    impulses by contact slot (3 slot + d) and joint row; on the standing
+    humanoid the normal impulses of the record carry the weight (m g dt), and
+    the velocity-tolerance exit runs fewer sweeps than the budget while staying
+    within 1e-4 of the fixed-count step."""
+    import ctypes
+    from mwstep import get_model_file
+    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    n = cm.n
+    mode = np.full(n, oracle.FORCE, np.int32)
+    a = oracle.FloatWorld(cm, pgs_iters=50)
+    b = oracle.FloatWorld(cm, pgs_iters=50, warm_start=True)
+    for _ in range(200):
+        a.step(mode, np.zeros(n))
+        b.warm[:] = 0.0            # cold every step: identical arithmetic
+        b.step(mode, np.zeros(n))
+    assert np.array_equal(a.q, b.q) and np.array_equal(a.V, b.V)
+    # the record: normal impulses at 3 slot, their sum m g dt
+    normals = b.warm[0:3 * oracle.OR_MAXFC:3]
+    mass = cm.free.mass + sum(cm.model.mass[i] for i in range(n))
+    assert np.count_nonzero(normals) == len(b.contacts)
+    assert normals.sum() == pytest.approx(mass * 9.8 * 1e-3, rel=0.02)
+    # tolerance exit
+    c = oracle.FloatWorld(cm, pgs_iters=50, pgs_tol=1e-6, warm_start=True)
+    c.s = oracle.OrFloatState()
+    ctypes.pointer(c.s)[0] = b.s
+    c.warm[:] = b.warm
+    sweeps = []
+    for _ in range(50):
+        c.step(mode, np.zeros(n))
+        s = ctypes.c_int()
+        oracle.lib().or_pgs_stats(ctypes.byref(s), None)
+        sweeps.append(s.value)
+        b.step(mode, np.zeros(n))
+    assert np.mean(sweeps) < 50
+    assert np.abs(c.q - b.q).max() <= 1e-4 and np.abs(c.p - b.p).max() <= 1e-5

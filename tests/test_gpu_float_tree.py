@@ -478,3 +478,114 @@ def test_wave_run_device_equals_run(require_gpu):
     assert np.array_equal(sims[0].contacts(3), sims[1].contacts(3))
     for s in sims:
         s.close()
+
+
+def test_humanoid_warm_started_pgs(require_gpu, oracle):
+    """mw_set_pgs_options (tolerance exit + warm start, the world-per-wavefront
+    kernel, velocity tolerance 1e-6) on BASELINE config 5's model: 16 humanoids dropped from 0-3 cm
+    with joint offsets, a host PD hold applied as joint forces (so the oracle
+    gets the same torques), 400 steps.
+      * closed loop vs the fp64 oracle in the same mode (or_float_step_warm,
+        same tolerance): the tolerance exit ends fp32 and fp64 solves at different
+        sweeps and the warm start carries that difference forward, so the
+        bounds are the contact tolerances of the one-step tests (q 1e-3 rad,
+        base 1e-4 m) rather than the cold solve's round-off;
+      * every 40 steps, teacher-forced from the warm run's state: its step and
+        a cold PGS-50 step (a second simulator reset to the same state) are
+        compared with the exact boxed-LCP step (OR_PGS_CONVERGED, what DART's
+        Dantzig solver returns [EXT]);
+      * the warm solve is cheaper than the cold PGS-50 solve."""
+    import time
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    import os
+    W, H, tol = 16, 400, float(os.environ.get("MW_TEST_PGS_TOL", "1e-6"))
+    rng = np.random.default_rng(3)
+    path = get_model_file("humanoid32")
+    cm = oracle.load_urdf(path, pose_xyz=(0, 0, HUMANOID_Z))
+    n = cm.n
+    sims = []
+    for warm in (True, False):
+        sim = Simulator(path, n_worlds=W, pgs_iters=50, pose=(0, 0, HUMANOID_Z, 1, 0, 0, 0))
+        assert sim.float_kernel() == 2
+        sim.set_ground_plane(True, 1.0)
+        sim.enable_contacts(True)
+        if warm:
+            sim.set_pgs_options(tol, True)
+            assert sim.pgs_options() == (tol, True)
+        sims.append(sim)
+    sim, cold_sim = sims
+    z = (HUMANOID_Z + rng.uniform(0.0, 0.03, W)).astype(np.float32).astype(np.float64)
+    q0 = rng.uniform(-0.05, 0.05, (W, n)).astype(np.float32).astype(np.float64)
+    sim.reset_base_pose(np.column_stack([np.zeros((W, 2)), z, np.ones(W), np.zeros((W, 3))]))
+    sim.set("reset_q", q0)
+    sim.run(paused=True)
+    for s_ in sims:
+        s_.set_control_mode(N.MODE_FORCE)
+    kp = np.array([p for p, _ in _humanoid_gains(sim.joint_names)])
+    kd = np.array([d for _, d in _humanoid_gains(sim.joint_names)])
+    ows = []
+    for w in range(4):
+        ow = oracle.FloatWorld(cm, pgs_iters=50, pgs_tol=tol, warm_start=True)
+        ow.set_pose([0, 0, z[w]], np.eye(3))
+        ow.set_joints(q0[w], np.zeros(n))
+        ows.append(ow)
+    mode = np.full(n, oracle.FORCE, np.int32)
+    worst_q = worst_p = 0.0
+    ew, ec = [], []
+    for k in range(H):
+        gq, gqd = sim.get("q"), sim.get("qd")
+        tau = np.clip(-kp * gq - kd * gqd, -80, 80).astype(np.float32).astype(np.float64)
+        sample = k % 40 == 20
+        if sample:
+            p0, v0 = sim.base_pose(), sim.base_velocity()
+            cold_sim.reset_base_pose(p0)
+            cold_sim.reset_base_velocity(v0)
+            cold_sim.set("reset_q", gq)
+            cold_sim.set("reset_qd", gqd)
+            cold_sim.run(paused=True)
+            cold_sim.set("force_target", tau)
+            cold_sim.run()
+        sim.set("force_target", tau)
+        sim.run()
+        for w, ow in enumerate(ows):
+            ow.step(mode, np.clip(-kp * ow.q - kd * ow.qd, -80, 80))
+        if sample:
+            gqd1, cqd1 = sim.get("qd"), cold_sim.get("qd")
+            for w in range(W):
+                R0 = _quat_to_R(p0[w, 3:])
+                exact = oracle.FloatWorld(cm, pgs_iters=oracle.PGS_CONVERGED)
+                exact.set_pose(p0[w, :3], R0)
+                exact.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
+                exact.set_joints(gq[w], gqd[w])
+                exact.step(mode, tau[w])
+                ew.append(float(np.abs(gqd1[w] - exact.qd).max()))
+                ec.append(float(np.abs(cqd1[w] - exact.qd).max()))
+        if k % 50 == 49:
+            gq = sim.get("q")
+            p = sim.base_pose()
+            for w, ow in enumerate(ows):
+                worst_q = max(worst_q, float(np.abs(gq[w] - ow.q).max()))
+                worst_p = max(worst_p, float(np.abs(p[w, :3] - ow.p).max()))
+    assert sim.constraint_overflow() == 0
+    ew, ec = np.array(ew), np.array(ec)
+    print(f"warm-started PGS (tol {tol}): closed loop vs oracle q {worst_q:.2e}, base {worst_p:.2e}; "
+          f"|qd - exact LCP| over {len(ew)} teacher-forced steps: warm median {np.median(ew):.2e} "
+          f"p90 {np.percentile(ew, 90):.2e} max {ew.max():.2e}; cold PGS-50 median {np.median(ec):.2e} "
+          f"p90 {np.percentile(ec, 90):.2e} max {ec.max():.2e}")
+    assert worst_q <= 1e-3 and worst_p <= 1e-4
+    assert np.median(ew) <= np.median(ec) + 1e-5 and np.percentile(ew, 90) <= 2 * np.percentile(ec, 90) + 1e-4
+    # cost: the same 16 worlds, 100 steps, cold PGS-50 vs warm
+    times = []
+    for s_ in (cold_sim, sim):
+        s_.run_device(5)
+        s_.get("q")
+        t0 = time.perf_counter()
+        s_.run_device(100)
+        s_.get("q")
+        times.append((time.perf_counter() - t0) / 100)
+    print(f"per step (16 worlds): cold PGS-50 {times[0] * 1e6:.1f} us, warm + tol {times[1] * 1e6:.1f} us")
+    assert times[1] < times[0]
+    for s_ in sims:
+        s_.close()
