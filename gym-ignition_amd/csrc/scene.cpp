@@ -400,7 +400,18 @@ int flush(mw_scene* s, bool defer) {
 
 // queue the D2H copies of the joint state planes (q, qd, qdd: the rows of
 // the scene's bodies) and of the base states
-int queue_readback(mw_scene* s) {
+// what a synchronous run must read back: the base block only when some
+// model has a floating base (a welded base never moves from its insertion
+// pose, which the host mirror holds), the drop counter only when the scene can
+// exceed a capacity (collision shapes, or more joint rows than the LCP holds)
+bool needs_base_readback(const mw_scene* s) {
+    for (const auto& sm : s->models)
+        if (sm.m.floating) return true;
+    return false;
+}
+bool can_overflow(const mw_scene* s) { return s->hp.n_shapes > 0 || 3 * s->NB > mw::kScMaxRows; }
+
+int queue_readback(mw_scene* s, bool base = true) {
     const size_t plane = s->jrows * sizeof(float), rows = static_cast<size_t>(s->NB) * s->W * sizeof(float);
     if (rows && 3 * plane <= (size_t{1} << 20)) {
         // small scenes: one copy of the three planes beats three copies
@@ -411,7 +422,7 @@ int queue_readback(mw_scene* s) {
                                   hipMemcpyDeviceToHost, s->stream));
     }
     const size_t brows = static_cast<size_t>(13 * s->models.size()) * s->W * sizeof(float);
-    if (brows) SC_HIP(hipMemcpyAsync(s->h_base, s->d_base, brows, hipMemcpyDeviceToHost, s->stream));
+    if (brows && base) SC_HIP(hipMemcpyAsync(s->h_base, s->d_base, brows, hipMemcpyDeviceToHost, s->stream));
     s->idle = false;
     return MW_OK;
 }
@@ -883,9 +894,11 @@ int mw_scene_run(mw_scene* s, int32_t paused) {
     // the joint and base state are queued back to back
     if (int rc = scene_run(s, paused, true)) return rc;
     if (s->models.empty()) return MW_OK;
-    if (int rc = queue_readback(s)) return rc;
+    // per-env runs (BASELINE config 1): skip the copies that cannot carry news
+    if (int rc = queue_readback(s, needs_base_readback(s))) return rc;
     // the drop counter rides on the same synchronisation
-    SC_HIP(hipMemcpyAsync(s->h_overflow, s->dev.overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    if (can_overflow(s))
+        SC_HIP(hipMemcpyAsync(s->h_overflow, s->dev.overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     if (int rc = sync(s)) return rc;
     clear_consumed(s);
     s->joints_stale = s->base_stale = false;

@@ -30,6 +30,12 @@ class Scene:
         self.step_size = step_size
         self.steps_per_run = steps_per_run
         self.models: List[dict] = []
+        self._models_changed()
+
+    def _models_changed(self) -> None:
+        # the per-env ScenarI/O path asks for the same selections every step
+        self._selcache = {}
+        self._nd = sum(i["dofs"] for i in self.models)
 
     @property
     def handle(self) -> ctypes.c_void_p:
@@ -59,6 +65,7 @@ class Scene:
         N.check(N.lib().mw_scene_insert_model(self.handle, urdf.encode(), N.dptr(p), name.encode(), w0, nw,
                                               ctypes.byref(m)), "insert_model")
         self.models.append(self._info(m.value))
+        self._models_changed()
         return m.value
 
     def _info(self, m: int) -> dict:
@@ -91,6 +98,7 @@ class Scene:
         N.check(N.lib().mw_scene_replace_model(self.handle, m, urdf.encode(), N.dptr(p), name.encode()),
                 "replace_model")
         self.models[m] = self._info(m)
+        self._models_changed()
 
     def set_world_ground(self, enabled: bool, w0: int = 0, nw: Optional[int] = None) -> None:
         self._touch()
@@ -150,9 +158,13 @@ class Scene:
         """global dof indices of model m (local indices `dofs`), or every dof"""
         if m is None:
             return None if dofs is None else np.ascontiguousarray(dofs, dtype=np.int32)
-        info = self.models[m]
-        local = range(info["dofs"]) if dofs is None else dofs
-        return np.ascontiguousarray([info["first"] + d for d in local], dtype=np.int32)
+        key = (m, None if dofs is None else tuple(int(d) for d in dofs))
+        sel = self._selcache.get(key)
+        if sel is None:
+            info = self.models[m]
+            local = range(info["dofs"]) if dofs is None else key[1]
+            sel = self._selcache[key] = np.ascontiguousarray([info["first"] + d for d in local], dtype=np.int32)
+        return sel
 
     # The joint state changes only through runs and the mutators below, so the
     # per-env ScenarI/O path (a handful of getters per env step, each a C call
@@ -165,7 +177,7 @@ class Scene:
         self.__dict__.setdefault("_cache", {}).clear()
 
     def _cached(self, what: str) -> Optional[np.ndarray]:
-        nd = sum(i["dofs"] for i in self.models)
+        nd = self._nd
         if what not in self._STATE or nd == 0 or self.n_worlds * nd > self._CACHE_MAX:
             return None
         cache = self.__dict__.setdefault("_cache", {})
@@ -183,7 +195,7 @@ class Scene:
         full = self._cached(what)
         if full is not None:
             return full[w0:w0 + nw].copy() if sel is None else full[w0:w0 + nw][:, sel]
-        nd = (sum(i["dofs"] for i in self.models) if sel is None else len(sel))
+        nd = (self._nd if sel is None else len(sel))
         out = np.zeros((nw, nd))
         if nd:
             N.check(N.lib().mw_scene_get_joints(self.handle, self._FIELDS[what], w0, nw, N.iptr(sel),
@@ -195,7 +207,7 @@ class Scene:
         self._touch()
         nw = self.n_worlds - w0 if nw is None else nw
         sel = self._sel(m, dofs)
-        nd = (sum(i["dofs"] for i in self.models) if sel is None else len(sel))
+        nd = (self._nd if sel is None else len(sel))
         v = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.float64), (nw, nd)))
         N.check(N.lib().mw_scene_set_joints(self.handle, self._FIELDS[what], w0, nw, N.iptr(sel),
                                             0 if sel is None else len(sel), N.dptr(v)), f"set {what}")
@@ -352,7 +364,7 @@ class SceneView:
 
     # ---- joints (local dof indices, this world)
     def get(self, what: str, w0: int = 0, nw: Optional[int] = None, dofs=None) -> np.ndarray:
-        return self.scene.get(what, self.m, self.w, 1, None if dofs is None else list(np.asarray(dofs)))
+        return self.scene.get(what, self.m, self.w, 1, None if dofs is None else tuple(np.asarray(dofs).tolist()))
 
     def set(self, what: str, values, w0: int = 0, nw: Optional[int] = None, dofs=None) -> None:
         self.scene.set(what, values, self.m, self.w, 1, None if dofs is None else list(np.asarray(dofs)))
