@@ -585,6 +585,27 @@ Description describe_sdf(const XNode* root, const double pose[7]) {
         sjs.push_back(s);
     }
 
+    // <static>true</static> (World::insertModel -> a static model in the
+    // physics engine): every root link is welded to the world where the model
+    // frame is placed
+    if (sdf_bool(me, "static", false)) {
+        for (const SJ& s : sjs)
+            if (s.J.type != "fixed")
+                throw std::runtime_error("static models with moving joints are not supported (joint " + s.J.name + ")");
+        std::map<std::string, int> has_parent;
+        for (const SJ& s : sjs) has_parent[s.J.child] = 1;
+        for (auto& n : D.link_order) {
+            if (has_parent.count(n)) continue;
+            SJ s;
+            s.J.name = "__static_" + n;
+            s.J.type = "fixed";
+            s.J.parent = "world";
+            s.J.child = n;
+            s.XJ = Pose3{};
+            sjs.push_back(s);
+            world_used = true;
+        }
+    }
     // the description frame of every link: the joint frame for a child link,
     // the model frame for the root (its contents move by its link pose)
     std::map<std::string, Pose3> F;
@@ -757,10 +778,14 @@ ChainModel compile_description(Description D) {
         out.base_com = B.com;
         out.base_Ic = {B.I[0], B.I[4], B.I[8], B.I[1], B.I[2], B.I[5]};
         out.base_shapes = B.shapes;
+    } else {
+        // a welded base (incl. static models) is a collider for the other models
+        out.base_shapes = links[base].shapes;
     }
     for (auto& kv : links)
         if (owner[kv.first] == kv.first) out.unsupported_shapes += kv.second.unsupported;
-    if (out.bodies.empty() && !out.floating) throw std::runtime_error("the model has no moving joints");
+    if (out.bodies.empty() && !out.floating && out.base_shapes.empty())
+        throw std::runtime_error("the model has no moving joints and no collision shapes");
     return out;
 }
 

@@ -312,7 +312,8 @@ void build_float(mw_sim* s) {
     F.mu = static_cast<float>(s->ground_mu);
     F.ground = s->ground ? 1 : 0;
     std::vector<std::pair<int, const mw::Shape*>> shapes;
-    for (const auto& sh : M.base_shapes) shapes.push_back({-1, &sh});
+    if (!s->fixed_tree)  // a welded base never touches the ground
+        for (const auto& sh : M.base_shapes) shapes.push_back({-1, &sh});
     for (int b = 0; b < M.dofs(); ++b)
         for (const auto& sh : M.bodies[b].shapes) shapes.push_back({b, &sh});
     int slot = 0;
@@ -565,6 +566,9 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     if (s->model.dofs() > mw::kMaxBodies)
         return fail(MW_EPARSE, "models with more than " + std::to_string(mw::kMaxBodies) +
                                    " moving joints are not supported by this build");
+    if (!s->model.floating && s->model.dofs() == 0)
+        return fail(MW_EPARSE, "a welded model without moving joints has no dynamics of its own: insert it into a "
+                               "scene (World.insert_model) where it is a collider");
     s->floating = s->model.floating;
     s->fixed_tree = false;
     if (!s->floating) {
@@ -579,7 +583,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         std::vector<int> parents;
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
         s->topo = mw::kernel_topology(parents.data(), s->model.dofs());
-        size_t n_shapes = s->model.base_shapes.size();
+        size_t n_shapes = s->fixed_tree ? 0 : s->model.base_shapes.size();
         bool damped = false;  // joint damping: the wave kernel (its dual recursion) only
         for (const auto& b : s->model.bodies) {
             n_shapes += b.shapes.size();

@@ -944,7 +944,9 @@ class World:
             return False
         static = root.tag != "robot" and (root.find("model/static") is not None and
                                           root.find("model/static").text.strip().lower() in ("1", "true"))
-        if static:
+        solid = [g for g in root.findall("model/link/collision/geometry")
+                 if g.find("box") is not None or g.find("sphere") is not None or g.find("cylinder") is not None]
+        if static and not solid:
             if root.findall("model/joint"):
                 _err("static SDF models with joints are not supported by this build")
                 return False
@@ -958,6 +960,8 @@ class World:
                 self._ground_name = f"{name}::{link.get('name', 'link')}"
                 self._simulator._set_ground(self, True, self._ground_mu)
             return True
+        # a static model with box / sphere / cylinder collisions is a welded
+        # collider of the scene (the model compiler welds its links to the world)
         if root.tag != "robot" and [float(v) for v in (*pose.position, *pose.orientation)] == [0, 0, 0, 1, 0, 0, 0]:
             # the identity keeps the SDF model's own <pose> (World.cpp:169-177)
             pose = _sdf_model_pose(root)

@@ -349,8 +349,15 @@ def sdf_to_urdf(text: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0
     for je in jts:
         F[je.find("child").text.strip()] = X[je.find("child").text.strip()] @ _sdf_pose(je)
     out = [f'<robot name="{me.get("name", "model")}">']
-    if any(je.find("parent").text.strip() == "world" for je in jts):
+    st = me.find("static")
+    static = st is not None and st.text is not None and st.text.strip() in ("1", "true")
+    # a static model: its root links are welded to the world at the model frame
+    roots = [n for n in X if n not in {je.find("child").text.strip() for je in jts}] if static else []
+    if static or any(je.find("parent").text.strip() == "world" for je in jts):
         out.append('<link name="world"/>')
+    for n in roots:
+        out.append(f'<joint name="__static_{n}" type="fixed"><origin xyz="0 0 0" rpy="0 0 0"/>'
+                   f'<parent link="world"/><child link="{n}"/></joint>')
     for le in me.findall("link"):
         n = le.get("name")
         C = np.linalg.inv(F[n]) @ X[n]          # SDF link frame in the URDF link frame

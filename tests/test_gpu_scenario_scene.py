@@ -308,3 +308,45 @@ def test_sdf_and_urdf_pendulum_trajectories_agree(require_gpu, oracle):
         worst = max(worst, abs(float(q[0]) - q_s[k]))
     assert worst <= 1e-4, worst
     gazebo.close()
+
+
+def test_static_sdf_collider(require_gpu, oracle):
+    """A static SDF model with box / cylinder collisions (a table: top and a
+    leg, yawed model frame) is a welded collider (Physics.cpp:687-1219 creates
+    static models in the engine): a ball dropped on the table top comes to rest
+    on it at top + r, carried by its contact with the table (weight within
+    0.05 N), the table does not move, and the ball follows the fp64 scene
+    oracle (position within 1e-4 m over 800 steps)."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    from scene_models import sphere_urdf
+    from test_sdf_models import STATIC_TABLE_SDF
+    gazebo, get_model_file = _gazebo()
+    world = gazebo.get_world()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("ground_plane"))
+    assert world.insert_model_from_string(STATIC_TABLE_SDF)
+    table = world.get_model("table")
+    assert table.base_position() == pytest.approx([0.5, 0, 0]) and table.dofs() == 0
+    ball_text = sphere_urdf(1.0, 0.05)
+    assert world.insert_model_from_string(ball_text, core.Pose([0.5, 0, 0.8], [1.0, 0, 0, 0]), "ball")
+    ball = world.get_model("ball")
+    assert ball.enable_contacts(True)
+    cms = [oracle.load_urdf(STATIC_TABLE_SDF), oracle.load_urdf(ball_text, pose_xyz=(0.5, 0, 0.8))]
+    ow = oracle.SceneWorld(cms, mu=1.0, pgs_iters=50)
+    worst = 0.0
+    for k in range(800):
+        assert gazebo.run()
+        ow.step()
+        if k % 50 == 49:
+            worst = max(worst, float(np.abs(np.array(ball.base_position()) - ow.p(1)).max()))
+    z = ball.base_position()[2]
+    print(f"ball on a static SDF table: z {z:.5f} (top 0.5 + r 0.05), max |dp| vs oracle {worst:.2e}")
+    assert z == pytest.approx(0.55, abs=2e-3)
+    assert worst <= 1e-4
+    assert table.base_position() == pytest.approx([0.5, 0, 0])
+    cs = ball.contacts()
+    assert len(cs) == 1 and cs[0].body_b.startswith("table::")
+    fz = sum(p.force[2] for p in cs[0].points)
+    assert fz == pytest.approx(G * 1.0, abs=0.05)
+    gazebo.close()

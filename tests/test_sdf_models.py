@@ -276,3 +276,54 @@ def test_sdf_and_urdf_of_one_model_compile_alike(N, oracle, pendulum_file):
 def test_unsupported_sdf_fails_loudly(N, text, needle):
     rc, msg = _compile(N, text)
     assert rc != 0 and needle in msg, msg
+
+
+STATIC_TABLE_SDF = """<sdf version='1.7'><model name='table'><static>true</static><pose>0.5 0 0 0 0 0.3</pose>
+  <link name='top'><pose>0 0 0.45 0 0 0</pose>
+    <collision name='c'><geometry><box><size>1 0.8 0.1</size></box></geometry></collision></link>
+  <link name='leg'><pose>0.4 0.3 0.2 0 0 0</pose>
+    <collision name='c'><geometry><cylinder><radius>0.03</radius><length>0.4</length></cylinder></geometry></collision>
+  </link></model></sdf>"""
+
+
+def test_static_sdf_model_is_a_welded_collider(N, oracle):
+    """<static>true</static>: every root link welded to the world at the model
+    frame, no moving joints, the links' shapes on the (fixed) base; the
+    oracle's rewrite agrees.  A welded model without joints is a scene
+    collider only: mw_sim refuses it."""
+    cfg = N.MwConfig(1e-3, 1.0, 1, 1, 0, 0)
+    h = ctypes.c_void_p()
+    N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
+    try:
+        p = np.array(IDENT, dtype=np.float64)
+        assert N.lib().mw_load_model(h, STATIC_TABLE_SDF.encode(), N.dptr(p), b"") == N.MW_EPARSE
+        assert "scene" in N.last_error()
+    finally:
+        N.lib().mw_destroy(h)
+    cm = oracle.load_urdf(STATIC_TABLE_SDF)
+    assert not cm.floating and cm.n == 0 and len(cm.base_shapes) == 2
+    np.testing.assert_allclose(cm.base_p, [0.5, 0, 0], atol=1e-12)
+    # the same shapes through the scene compiler (mw_scene_model_export has no
+    # shape export: compare the oracle's lumped shapes with the C++ ones via a
+    # fixed-base carrier model that mw_sim accepts)
+    carrier = STATIC_TABLE_SDF.replace("<static>true</static>", "").replace(
+        "</model>", "<link name='w'/><joint name='hinge' type='revolute'><parent>top</parent><child>w</child>"
+        "<axis><xyz>0 0 1</xyz></axis></joint><joint name='weld' type='fixed'><parent>world</parent>"
+        "<child>top</child></joint><joint name='weld2' type='fixed'><parent>top</parent><child>leg</child>"
+        "</joint></model>")
+    rc, got = _compile(N, carrier)
+    assert rc == 0, got
+    ref = oracle.load_urdf(carrier)
+    assert got["base_frame"] == ref.base_link == "top"
+    _compare_shapes(got["shapes"][-1], ref.base_shapes, 1e-10)
+    # geometry of the welded shapes in the static model's base frame: the
+    # table top 0.45 above the model frame, the leg cylinder offset
+    tops = sorted(ref.base_shapes, key=lambda s: s[0])
+    assert [s[0] for s in tops] == [0, 2]
+
+
+def test_static_sdf_model_with_joints_fails_loudly(N):
+    text = STATIC_TABLE_SDF.replace("</model>", "<joint name='j' type='revolute'><parent>top</parent>"
+                                    "<child>leg</child></joint></model>")
+    rc, msg = _compile(N, text)
+    assert rc != 0 and "static" in msg
