@@ -61,6 +61,17 @@ class Limit:
         return f"Limit(min={self.min}, max={self.max})"
 
 
+class JointLimit:
+    """core::JointLimit (utils.h): per-DoF min / max vectors."""
+
+    def __init__(self, min=(), max=()):  # noqa: A002
+        self.min = [float(v) for v in min]
+        self.max = [float(v) for v in max]
+
+    def __repr__(self):
+        return f"JointLimit(min={self.min}, max={self.max})"
+
+
 class PID:
     """scenario::core::PID (cpp/scenario/core/include/scenario/core/Joint.h:505-523):
     gains plus command / integral limits, with the SWIG binding's undercase

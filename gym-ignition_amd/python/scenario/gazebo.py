@@ -284,6 +284,52 @@ class Joint:
             return False
         return self._set_param(N.PARAM_MAX_GENERALIZED_FORCE, max_force)
 
+    # acceleration targets: stored for controllers, no effect on the physics
+    # (JointAccelerationTarget, Joint.cpp:747-845)
+    def set_acceleration_target(self, acceleration: float, dof: int = 0) -> bool:
+        if dof != 0:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        self._model._acc_targets[self._name] = float(acceleration)
+        return True
+
+    def acceleration_target(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        if self._name not in self._model._acc_targets:
+            raise RuntimeError(f"Joint '{self._name}' has no acceleration target")
+        return self._model._acc_targets[self._name]
+
+    # vectorised (multi-DoF) forms of the per-DoF accessors (core/Joint.h)
+    def joint_position_target(self) -> List[float]:
+        return [self.position_target()]
+
+    def joint_velocity_target(self) -> List[float]:
+        return [self.velocity_target()]
+
+    def joint_acceleration_target(self) -> List[float]:
+        return [self.acceleration_target()]
+
+    def joint_generalized_force_target(self) -> List[float]:
+        return [self.generalized_force_target()]
+
+    def joint_max_generalized_force(self) -> List[float]:
+        return [self.max_generalized_force()]
+
+    def set_joint_position_target(self, target: Sequence[float]) -> bool:
+        return len(target) == 1 and self.set_position_target(target[0])
+
+    def set_joint_velocity_target(self, target: Sequence[float]) -> bool:
+        return len(target) == 1 and self.set_velocity_target(target[0])
+
+    def set_joint_acceleration_target(self, target: Sequence[float]) -> bool:
+        return len(target) == 1 and self.set_acceleration_target(target[0])
+
+    def set_joint_generalized_force_target(self, target: Sequence[float]) -> bool:
+        return len(target) == 1 and self.set_generalized_force_target(target[0])
+
+    def set_joint_max_generalized_force(self, max_force: Sequence[float]) -> bool:
+        return len(max_force) == 1 and self.set_max_generalized_force(max_force[0])
+
     def position_limit(self, dof: int = 0) -> core.Limit:
         from mwstep import native as N
         self._check_dof(dof)
@@ -308,6 +354,8 @@ class Model:
         self._pending_vel = None
         self._export = None  # exported model rows (link forward kinematics)
         self._history: Optional[collections.deque] = None
+        self._acc_targets: Dict[str, float] = {}   # JointAccelerationTarget (no physics effect)
+        self._base_targets: Dict[str, list] = {}   # Base*Target components (no physics effect)
 
     # -- identity
     def to_gazebo(self) -> "Model":
@@ -335,6 +383,95 @@ class Model:
 
     def base_frame(self) -> str:
         return self._sim.base_frame
+
+    def nr_of_joints(self) -> int:
+        return len(self._sim.joint_names)
+
+    def nr_of_links(self) -> int:
+        return len(self.link_names())
+
+    def links_in_contact(self) -> List[str]:
+        # Model::linksInContact (Model.cpp:725-736)
+        return [n for n in self.link_names() if self.get_link(n).in_contact()]
+
+    def joint_limits(self, joint_names: Sequence[str] = ()) -> core.JointLimit:
+        # Model::jointLimits (Model.cpp:797-815): serialised position limits
+        lims = [j.position_limit() for j in self.joints(joint_names)]
+        return core.JointLimit([lm.min for lm in lims], [lm.max for lm in lims])
+
+    def set_joint_acceleration_targets(self, accelerations: Sequence[float],
+                                       joint_names: Sequence[str] = ()) -> bool:
+        names = list(joint_names) or list(self._sim.joint_names)
+        if len(accelerations) != len(names):
+            _err("Wrong number of elements (joint_dofs=%d)" % len(names))
+            return False
+        for n in names:
+            if n not in self._joints:
+                _err(f"Joint '{n}' not found in model '{self._name}'")
+                return False
+        for n, a in zip(names, accelerations):
+            self._acc_targets[n] = float(a)
+        return True
+
+    def joint_acceleration_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
+        return [self.get_joint(n).acceleration_target() for n in (joint_names or self._sim.joint_names)]
+
+    # -- base targets (Model.cpp:1077-1246): stored for controllers, the
+    # physics does not read them; a getter of a target never set raises
+    def set_base_pose_target(self, position: Sequence[float], orientation: Sequence[float]) -> bool:
+        self._base_targets["pose"] = [list(map(float, position)), list(map(float, orientation))]
+        return True
+
+    def set_base_position_target(self, position: Sequence[float]) -> bool:
+        orientation = self._base_targets.get("pose", [None, [1.0, 0.0, 0.0, 0.0]])[1]
+        return self.set_base_pose_target(position, orientation)
+
+    def set_base_orientation_target(self, orientation: Sequence[float]) -> bool:
+        position = self._base_targets.get("pose", [[0.0, 0.0, 0.0], None])[0]
+        return self.set_base_pose_target(position, orientation)
+
+    def set_base_world_velocity_target(self, linear: Sequence[float], angular: Sequence[float]) -> bool:
+        return self.set_base_world_linear_velocity_target(linear) and \
+            self.set_base_world_angular_velocity_target(angular)
+
+    def set_base_world_linear_velocity_target(self, linear: Sequence[float]) -> bool:
+        self._base_targets["lin_vel"] = list(map(float, linear))
+        return True
+
+    def set_base_world_angular_velocity_target(self, angular: Sequence[float]) -> bool:
+        self._base_targets["ang_vel"] = list(map(float, angular))
+        return True
+
+    def set_base_world_linear_acceleration_target(self, linear: Sequence[float]) -> bool:
+        self._base_targets["lin_acc"] = list(map(float, linear))
+        return True
+
+    def set_base_world_angular_acceleration_target(self, angular: Sequence[float]) -> bool:
+        self._base_targets["ang_acc"] = list(map(float, angular))
+        return True
+
+    def _base_target(self, key: str, what: str):
+        if key not in self._base_targets:
+            raise RuntimeError(f"model '{self._name}' has no {what} target")
+        return self._base_targets[key]
+
+    def base_position_target(self) -> List[float]:
+        return list(self._base_target("pose", "base pose")[0])
+
+    def base_orientation_target(self) -> List[float]:
+        return list(self._base_target("pose", "base pose")[1])
+
+    def base_world_linear_velocity_target(self) -> List[float]:
+        return list(self._base_target("lin_vel", "base linear velocity"))
+
+    def base_world_angular_velocity_target(self) -> List[float]:
+        return list(self._base_target("ang_vel", "base angular velocity"))
+
+    def base_world_linear_acceleration_target(self) -> List[float]:
+        return list(self._base_target("lin_acc", "base linear acceleration"))
+
+    def base_world_angular_acceleration_target(self) -> List[float]:
+        return list(self._base_target("ang_acc", "base angular acceleration"))
 
     def base_position(self) -> List[float]:
         # Model::basePosition (Model.cpp:976-984); a fixed base stays at its insertion pose
@@ -667,6 +804,15 @@ class Link:
 
     def name(self, scoped: bool = False) -> str:
         return f"{self._model.name()}::{self._name}" if scoped else self._name
+
+    def mass(self) -> float:
+        # Link::mass (Link.cpp:198-204) of the compiled body: links welded by
+        # fixed joints are lumped into one body (their masses summed)
+        ex = self._model._sim.export_model()
+        n = self._model._sim.dofs
+        if self._body >= 0:
+            return float(ex[34 * self._body + 17])
+        return float(ex[34 * n + 3]) if self._model._sim.floating else 0.0
 
     def position(self) -> List[float]:
         return self._model._link_state(self._body)[1].tolist()

@@ -350,3 +350,56 @@ def test_static_sdf_collider(require_gpu, oracle):
     fz = sum(p.force[2] for p in cs[0].points)
     assert fz == pytest.approx(G * 1.0, abs=0.05)
     gazebo.close()
+
+
+def test_model_api_completion(require_gpu):
+    """ScenarI/O accessors without physics effect (core/Model.h, Joint.h,
+    Link.h): nrOfJoints / nrOfLinks, jointLimits (Model.cpp:797-815),
+    linksInContact (:725-736), joint acceleration targets (stored, a missing
+    one raises like getExistingComponentData), the Base*Target components
+    (:1077-1246; setBasePositionTarget keeps the orientation, default
+    identity), the vectorised Joint forms and Link::mass."""
+    import math
+    from scenario import core
+    from scenario import gazebo as scenario
+    gazebo, get_model_file = _gazebo()
+    world = gazebo.get_world()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("ground_plane"))
+    assert world.insert_model(get_model_file("cartpole"))
+    assert world.insert_model_from_string(cube_urdf(), core.Pose([2, 0, 0.1], [1.0, 0, 0, 0]), "cube")
+    cart = world.get_model("cartpole")
+    cube = world.get_model("cube")
+    assert cart.nr_of_joints() == 2 and cart.nr_of_links() == len(cart.link_names()) == 3
+    lim = cart.joint_limits()
+    assert len(lim.min) == 2 and lim.max[1] == math.inf
+    assert lim.min[0] == cart.get_joint(cart.joint_names()[0]).position_limit().min
+    with pytest.raises(RuntimeError):
+        cart.joint_acceleration_targets()
+    assert cart.set_joint_acceleration_targets([1.0, -2.0])
+    assert cart.joint_acceleration_targets() == [1.0, -2.0]
+    j = cart.get_joint(cart.joint_names()[1])
+    assert j.acceleration_target() == -2.0 and j.joint_acceleration_target() == [-2.0]
+    assert j.set_joint_acceleration_target([0.5]) and j.acceleration_target() == 0.5
+    assert not cart.set_joint_acceleration_targets([1.0])
+    assert j.joint_max_generalized_force() == [j.max_generalized_force()]
+    with pytest.raises(RuntimeError):
+        cube.base_position_target()
+    assert cube.set_base_position_target([1, 2, 3])
+    assert cube.base_position_target() == [1, 2, 3] and cube.base_orientation_target() == [1, 0, 0, 0]
+    assert cube.set_base_orientation_target([0, 0, 0, 1]) and cube.base_position_target() == [1, 2, 3]
+    assert cube.set_base_world_velocity_target([0.1, 0, 0], [0, 0, 0.2])
+    assert cube.base_world_linear_velocity_target() == [0.1, 0, 0]
+    assert cube.base_world_angular_velocity_target() == [0, 0, 0.2]
+    assert cube.set_base_world_linear_acceleration_target([0, 0, -1])
+    assert cube.base_world_linear_acceleration_target() == [0, 0, -1]
+    with pytest.raises(RuntimeError):
+        cube.base_world_angular_acceleration_target()
+    assert cube.get_link("cube").mass() == pytest.approx(5.0)
+    pole = cart.get_link(cart.link_names()[-1])
+    assert pole.mass() > 0.0
+    assert cube.enable_contacts(True)
+    for _ in range(100):
+        assert gazebo.run()
+    assert cube.links_in_contact() == ["cube"]
+    gazebo.close()
