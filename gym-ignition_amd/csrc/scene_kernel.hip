@@ -63,14 +63,21 @@ struct ScWorld {
     static constexpr int kStride = MAXNV + 1;     // odd: lane-strided rows are conflict-free
     static constexpr int kAStride = kScMaxRows + 1;
     ScNode node[kScMaxNodes];
-    WaveAcc acc[kScMaxNodes];
+    // phase-disjoint storage (one wave runs the phases in program order):
+    // the ABA's child -> parent accumulators, the response passes' per-lane
+    // stacks, then the Delassus matrix -- 37 KiB instead of 69 KiB, so two
+    // worlds fit in a CU's 160 KiB of LDS instead of one
+    union {
+        WaveAcc acc[kScMaxNodes];
+        float stack[kScMaxDepth][7][kWaveLanes];
+        float A[kScMaxRows][kAStride];
+    };
     float l0[kScMaxModels][28];   // Chol6 (l[21], id[6]) of every floating base
     float q[kScMaxBodies], qd[kScMaxBodies], qdd[kScMaxBodies], tau[kScMaxBodies], vc[kScMaxBodies];
     uint32_t act[kScMaxBodies];
     float nu[MAXNV];
     float J[kScMaxRows][kStride];
     float MJ[kScMaxRows][kStride];
-    float A[kScMaxRows][kAStride];
     F4 rc[kScMaxRows];            // {b, 1/A_rr, lo, hi}
     int32_t src[kScMaxRows];      // contact rows 3 c + d; joint rows kJointRow + 3 body + type
     float rb[kScMaxRows], rlo[kScMaxRows], rhi[kScMaxRows];
@@ -78,7 +85,6 @@ struct ScWorld {
     float c_d[kScMaxContacts];
     int32_t c_na[kScMaxContacts], c_nb[kScMaxContacts];
     float c_x[kScMaxContacts][3];
-    float stack[kScMaxDepth][7][kWaveLanes];
 };
 
 // ODE dPlaneSpace (oracle.c plane_space), float32
