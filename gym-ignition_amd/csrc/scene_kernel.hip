@@ -298,11 +298,55 @@ __device__ __forceinline__ int sc_box_sphere(f3 h, f3 c, const M3& R, float rad,
     return 1;
 }
 
-// shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius):
-// normal from B into A, up to 4 points / depths
+// cylinder (h = {radius, half length}, axis z) against a sphere: oracle.c
+// cylinder_sphere in float32 (nbs from the cylinder into the sphere, the point
+// on the cylinder surface)
+__device__ __forceinline__ int sc_cylinder_sphere(f3 h, f3 c, const M3& R, float rad, f3 s, f3& nbs, f3& pt,
+                                                  float& dep) {
+    const f3 l = mulT(R, s - c);
+    const float rho = sqrtf(l.x * l.x + l.y * l.y);
+    const bool inside = rho <= h.x && fabsf(l.z) <= h.y;
+    if (!inside) {
+        const float k = rho > h.x ? h.x / rho : 1.f;
+        const f3 q = {l.x * k, l.y * k, fminf(fmaxf(l.z, -h.y), h.y)};
+        f3 e = l - q;
+        const float dist = sqrtf(dot(e, e));
+        if (dist > rad || dist == 0.f) return 0;
+        e = (1.f / dist) * e;
+        nbs = mul(R, e);
+        pt = c + mul(R, q);
+        dep = rad - dist;
+        return 1;
+    }
+    const float gs = h.x - rho, gc = h.y - fabsf(l.z);
+    const bool side = gs < gc && rho > 0.f;
+    const float sg = l.z >= 0.f ? 1.f : -1.f;
+    const float ir = side ? 1.f / rho : 0.f;
+    const f3 e = {side ? l.x * ir : 0.f, side ? l.y * ir : 0.f, side ? 0.f : sg};
+    const f3 q = {side ? h.x * e.x : l.x, side ? h.x * e.y : l.y, side ? l.z : sg * h.y};
+    nbs = mul(R, e);
+    pt = c + mul(R, q);
+    dep = rad + (side ? gs : gc);
+    return 1;
+}
+
+// shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius,
+// 2 cylinder: size = {radius, half length}): normal from B into A, up to 4
+// points / depths
 __device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, int tb, f3 sb, f3 cb, const M3& Rb,
                                           f3& n, f3* pts, float* deps) {
-    if (ta == 2 || tb == 2) return 0;  // cylinders collide with the ground plane only (this build)
+    if ((ta == 2 && tb == 1) || (ta == 1 && tb == 2)) {
+        f3 nbs;
+        if (ta == 2) {  // cylinder A, sphere B: n from B into A
+            if (!sc_cylinder_sphere(sa, ca, Ra, sb.x, cb, nbs, pts[0], deps[0])) return 0;
+            n = -nbs;
+            return 1;
+        }
+        if (!sc_cylinder_sphere(sb, cb, Rb, sa.x, ca, nbs, pts[0], deps[0])) return 0;
+        n = nbs;
+        return 1;
+    }
+    if (ta == 2 || tb == 2) return 0;  // cylinder-box, cylinder-cylinder: not in this build
     if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, pts, deps);
     if (ta == 1 && tb == 1) {
         const f3 d = ca - cb;

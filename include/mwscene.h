@@ -14,9 +14,10 @@
  *                                       Link.cpp:484-560, Physics.cpp:1446-1525
  *   JointController (PID, period gating) JointController.cpp:114-331
  * Models are trees on a fixed or floating base (URDF or SDF) with box /
- * sphere / cylinder collision shapes; they touch the ground plane, and box and
- * sphere shapes touch those of every other model of their world (DART + ODE
- * collision detector [EXT]; cylinders collide with the ground only).  A model inserted into
+ * sphere / cylinder collision shapes; they touch the ground plane, and the
+ * box-box, box-sphere, sphere-sphere and cylinder-sphere pairs of different
+ * models of a world touch each other (DART + ODE collision detector [EXT];
+ * cylinder-box and cylinder-cylinder pairs are not collided in this build).  A model inserted into
  * some worlds of a scene is absent from the others.
  *
  * Indexing: models in insertion order; joints ("dofs") numbered globally,

@@ -1970,11 +1970,69 @@ static int box_sphere(const double* h, const double* c, const double* R, double 
     return 1;
 }
 
+/* cylinder (h = {radius, half length}, axis = local z) against a sphere;
+ * same conventions as box_sphere: nbs from the cylinder into the sphere, the
+ * point on the cylinder surface.  Outside: the closest point of the solid
+ * cylinder; centre inside: the nearest of the side and the two caps. */
+static int cylinder_sphere(const double* h, const double* c, const double* R, double rad, const double* s,
+                           double nbs[3], double* pt, double* dep)
+{
+    const double d[3] = {s[0] - c[0], s[1] - c[1], s[2] - c[2]};
+    double l[3], q[3];
+    for (int k = 0; k < 3; ++k) l[k] = R[k] * d[0] + R[3 + k] * d[1] + R[6 + k] * d[2];
+    const double rho = sqrt(l[0] * l[0] + l[1] * l[1]);
+    const int inside = rho <= h[0] && fabs(l[2]) <= h[1];
+    if (!inside) {
+        const double k = rho > h[0] ? h[0] / rho : 1.0;
+        q[0] = l[0] * k;
+        q[1] = l[1] * k;
+        q[2] = l[2] < -h[1] ? -h[1] : (l[2] > h[1] ? h[1] : l[2]);
+        double e[3] = {l[0] - q[0], l[1] - q[1], l[2] - q[2]};
+        const double dist = sqrt(dot3(e, e));
+        if (dist > rad || dist == 0.0) return 0;
+        for (int k2 = 0; k2 < 3; ++k2) e[k2] /= dist;
+        for (int r = 0; r < 3; ++r) {
+            nbs[r] = R[r * 3] * e[0] + R[r * 3 + 1] * e[1] + R[r * 3 + 2] * e[2];
+            pt[r] = c[r] + R[r * 3] * q[0] + R[r * 3 + 1] * q[1] + R[r * 3 + 2] * q[2];
+        }
+        *dep = rad - dist;
+        return 1;
+    }
+    const double gs = h[0] - rho, gc = h[1] - fabs(l[2]);
+    double e[3];
+    if (gs < gc && rho > 0.0) {   /* through the side */
+        e[0] = l[0] / rho; e[1] = l[1] / rho; e[2] = 0.0;
+        q[0] = h[0] * e[0]; q[1] = h[0] * e[1]; q[2] = l[2];
+        *dep = rad + gs;
+    } else {                      /* through a cap */
+        const double sg = l[2] >= 0.0 ? 1.0 : -1.0;
+        e[0] = 0.0; e[1] = 0.0; e[2] = sg;
+        q[0] = l[0]; q[1] = l[1]; q[2] = sg * h[1];
+        *dep = rad + gc;
+    }
+    for (int r = 0; r < 3; ++r) {
+        nbs[r] = R[r * 3] * e[0] + R[r * 3 + 1] * e[1] + R[r * 3 + 2] * e[2];
+        pt[r] = c[r] + R[r * 3] * q[0] + R[r * 3 + 1] * q[1] + R[r * 3 + 2] * q[2];
+    }
+    return 1;
+}
+
 int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
                const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
                double* depths)
 {
-    if (type_a == 2 || type_b == 2) return 0;  /* cylinders: ground plane only (this build) */
+    if ((type_a == 2 && type_b == 1) || (type_a == 1 && type_b == 2)) {
+        double nbs[3];
+        if (type_a == 2) {   /* cylinder A, sphere B: n from B into A */
+            if (!cylinder_sphere(size_a, c_a, R_a, size_b[0], c_b, nbs, points, depths)) return 0;
+            for (int k = 0; k < 3; ++k) normal[k] = -nbs[k];
+            return 1;
+        }
+        if (!cylinder_sphere(size_b, c_b, R_b, size_a[0], c_a, nbs, points, depths)) return 0;
+        memcpy(normal, nbs, sizeof nbs);
+        return 1;
+    }
+    if (type_a == 2 || type_b == 2) return 0;  /* cylinder-box, cylinder-cylinder: not in this build */
     if (type_a == 0 && type_b == 0) return box_box(size_a, c_a, R_a, size_b, c_b, R_b, normal, points, depths);
     if (type_a == 1 && type_b == 1) {
         double d[3] = {c_a[0] - c_b[0], c_a[1] - c_b[1], c_a[2] - c_b[2]};

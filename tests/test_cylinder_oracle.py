@@ -128,3 +128,55 @@ def test_cylinder_geometry_compiles_alike(oracle):
     assert rc == 0 and got["shapes"][-1][0, 0] == 2
     np.testing.assert_allclose(got["shapes"][-1][0, 1:3], [0.05, 0.15])
     _compare(got, oracle.load_urdf(sdf))
+
+
+def test_cylinder_sphere_closed_forms(oracle):
+    """or_collide cylinder (type 2, size {r, half length}) vs sphere: normal
+    from B into A, the point on the cylinder surface; outside the solid
+    (cap face, side, rim) and with the sphere centre inside it."""
+    I = np.eye(3)
+    cyl = [0.1, 0.2, 0.0]
+    # sphere B above the top cap of cylinder A: n from B into A = -z
+    n, pts, dep = oracle.collide(2, cyl, [0, 0, 0], I, 1, [0.05], [0.03, 0, 0.24], I)
+    assert np.allclose(n, [0, 0, -1]) and dep[0] == pytest.approx(0.01) and np.allclose(pts[0], [0.03, 0, 0.2])
+    # sphere A beside the side of cylinder B (rotated: axis along x)
+    Ry = np.array([[0, 0, 1], [0, 1, 0], [-1, 0, 0]])
+    n, pts, dep = oracle.collide(1, [0.05], [0.1, 0.14, 0], I, 2, cyl, [0, 0, 0], Ry)
+    assert np.allclose(n, [0, 1, 0]) and dep[0] == pytest.approx(0.01) and np.allclose(pts[0], [0.1, 0.1, 0])
+    # beyond the rim: the closest point is on the rim circle
+    c = np.array([0.1 + 0.03, 0, 0.2 + 0.04])
+    n, pts, dep = oracle.collide(2, cyl, [0, 0, 0], I, 1, [0.06], c, I)
+    assert dep[0] == pytest.approx(0.06 - 0.05) and np.allclose(pts[0], [0.1, 0, 0.2])
+    np.testing.assert_allclose(n, -np.array([0.6, 0, 0.8]))
+    # centre inside, nearer the side than the caps
+    n, pts, dep = oracle.collide(2, cyl, [0, 0, 0], I, 1, [0.05], [0.08, 0, 0.0], I)
+    assert np.allclose(n, [-1, 0, 0]) and dep[0] == pytest.approx(0.07) and np.allclose(pts[0], [0.1, 0, 0])
+    # apart
+    assert len(oracle.collide(2, cyl, [0, 0, 0], I, 1, [0.05], [0, 0, 0.3], I)[1]) == 0
+    # cylinder-box pairs are not collided in this build
+    assert len(oracle.collide(2, cyl, [0, 0, 0], I, 0, [0.1, 0.1, 0.1], [0, 0, 0.25], I)[1]) == 0
+
+
+PILLAR = ('<robot name="pillar"><link name="world"/><joint name="fix" type="fixed"><parent link="world"/>'
+          '<child link="p"/><origin xyz="0 0 0.3"/></joint><link name="p"><inertial><mass value="10"/>'
+          '<inertia ixx="1" iyy="1" izz="1" ixy="0" ixz="0" iyz="0"/></inertial><collision><geometry>'
+          '<cylinder radius="0.15" length="0.6"/></geometry></collision></link></robot>')
+
+
+def ball_urdf(mass=1.0, r=0.05):
+    i = 0.4 * mass * r * r
+    return (f'<robot name="ball"><link name="ball"><inertial><mass value="{mass}"/>'
+            f'<inertia ixx="{i}" iyy="{i}" izz="{i}" ixy="0" ixz="0" iyz="0"/></inertial>'
+            f'<collision><geometry><sphere radius="{r}"/></geometry></collision></link></robot>')
+
+
+def test_ball_rests_on_a_pillar(oracle):
+    """A ball dropped on a welded cylinder (a pillar) rests on its top cap at
+    0.6 + r, carried by the cylinder-sphere contact."""
+    cms = [oracle.load_urdf(PILLAR), oracle.load_urdf(ball_urdf(), pose_xyz=(0.02, 0, 0.75))]
+    sw = oracle.SceneWorld(cms, pgs_iters=50)
+    for _ in range(600):
+        sw.step()
+    assert sw.p(1)[2] == pytest.approx(0.65, abs=2e-3)
+    fz = sum(c[8] for c, who in sw.contacts if 0 in (who[0], who[2]) and 1 in (who[0], who[2]))
+    assert abs(fz) == pytest.approx(1.0 * G, abs=0.05)

@@ -452,3 +452,78 @@ def test_capacity_overflow_fails_loudly(require_gpu):
     err = N.lib().mw_last_error().decode()
     assert "dropped" in err
     sc.close()
+
+
+def test_cylinder_sphere_contacts(require_gpu, oracle):
+    """Cylinder-sphere contacts on the scene kernel (sc_cylinder_sphere, the
+    float32 restatement of oracle.c cylinder_sphere): one step over 256 worlds
+    of a tilted floating cylinder with a ball pressed against its cap, side or
+    rim (poses 1e-5, velocities 2e-3, contact points 1e-5 vs the fp64 scene
+    oracle), and a ball dropped on a welded pillar resting on its top cap
+    (closed loop within 1e-4 m of the oracle)."""
+    from test_cylinder_oracle import PILLAR, ball_urdf, cylinder_urdf
+    W, pgs, mu = 256, 50, 0.8
+    rng = np.random.default_rng(21)
+    texts = [cylinder_urdf(), ball_urdf(1.0, 0.06)]
+    base = [(0.0, 0.0, 0.5), (0.0, 0.0, 0.8)]
+    cms = [oracle.load_urdf(t, pose_xyz=b) for t, b in zip(texts, base)]
+    sc = _scene([(t, (*b, 1, 0, 0, 0), nm) for t, b, nm in zip(texts, base, ["can", "ball"])], W, pgs, mu)
+    qc = np.array([_rand_quat(rng, 1.2) for _ in range(W)])
+    pc = np.column_stack([np.zeros((W, 2)), np.full(W, 0.5)])
+    # ball centre: a point on the cylinder surface (cap, side or rim) pushed in by up to 1 cm
+    pts = []
+    for w in range(W):
+        R = _quat_to_R(qc[w])
+        kind = w % 3
+        ang = rng.uniform(0, 2 * np.pi)
+        if kind == 0:
+            local = np.array([0.05 * np.cos(ang), 0.05 * np.sin(ang), 0.2 + 0.06 - rng.uniform(0, 0.01)])
+        elif kind == 1:
+            rr = 0.1 + 0.06 - rng.uniform(0, 0.01)
+            local = np.array([rr * np.cos(ang), rr * np.sin(ang), rng.uniform(-0.15, 0.15)])
+        else:
+            dirn = np.array([0.6 * np.cos(ang), 0.6 * np.sin(ang), 0.8])
+            local = np.array([0.1 * np.cos(ang), 0.1 * np.sin(ang), 0.2]) + (0.06 - rng.uniform(0, 0.01)) * dirn
+        pts.append(pc[w] + R @ local)
+    sc.reset_base_pose(0, np.column_stack([pc, qc]))
+    sc.reset_base_pose(1, np.column_stack([np.array(pts), np.ones(W), np.zeros((W, 3))]))
+    for m in range(2):
+        sc.reset_base_velocity(m, np.column_stack([rng.uniform(-0.3, 0.3, (W, 3)), rng.uniform(-1, 1, (W, 3))]))
+    sc.run(paused=True)
+    orcs = [_oracle_from_gpu(oracle, cms, sc, w, pgs, mu) for w in range(W)]
+    sc.run()
+    worst = dict(pose=0.0, vel=0.0, point=0.0)
+    n_pairs = 0
+    for w in range(W):
+        ow = orcs[w]
+        ow.step()
+        e = _compare(oracle, cms, sc, ow, w)
+        gc = sc.contacts(w)
+        assert len(gc) == len(ow.contacts), (w, len(gc), len(ow.contacts))
+        for row, (oc, who) in zip(gc, ow.contacts):
+            assert tuple(int(v) for v in row[10:14]) == who
+            n_pairs += who[2] >= 0
+            worst["point"] = max(worst["point"], float(np.abs(row[0:3] - oc[0:3]).max()))
+        worst["pose"] = max(worst["pose"], e["pose"])
+        worst["vel"] = max(worst["vel"], e["vel"])
+    print(f"cylinder-sphere x{W}: one-step " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
+          f", {n_pairs} cylinder-sphere contact points")
+    assert n_pairs > W // 2
+    assert worst["pose"] <= 1e-5 and worst["point"] <= 1e-5 and worst["vel"] <= 2e-3
+    sc.close()
+    # the pillar KAT through the scene kernel
+    texts = [PILLAR, ball_urdf()]
+    cms = [oracle.load_urdf(PILLAR), oracle.load_urdf(texts[1], pose_xyz=(0.02, 0, 0.75))]
+    sc = _scene([(PILLAR, (0, 0, 0, 1, 0, 0, 0), "pillar"), (texts[1], (0.02, 0, 0.75, 1, 0, 0, 0), "ball")],
+                2, pgs, 1.0)
+    ow = oracle.SceneWorld(cms, pgs_iters=pgs, mu=1.0)
+    worst = 0.0
+    for k in range(600):
+        sc.run()
+        ow.step()
+        if k % 50 == 49:
+            worst = max(worst, float(np.abs(sc.base_pose(1, 0, 1)[0, :3] - ow.p(1)).max()))
+    z = sc.base_pose(1, 0, 1)[0, 2]
+    print(f"ball on a pillar: z {z:.5f} (0.6 + 0.05), max |dp| vs oracle {worst:.2e}")
+    assert z == pytest.approx(0.65, abs=2e-3) and worst <= 1e-4
+    sc.close()
