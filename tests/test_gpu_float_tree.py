@@ -501,13 +501,14 @@ def test_humanoid_warm_started_pgs(require_gpu, oracle):
     from mwstep.sim import Simulator
     import os
     W, H, tol = 16, 400, float(os.environ.get("MW_TEST_PGS_TOL", "1e-6"))
+    warm_iters = int(os.environ.get("MW_TEST_WARM_ITERS", "50"))
     rng = np.random.default_rng(3)
     path = get_model_file("humanoid32")
     cm = oracle.load_urdf(path, pose_xyz=(0, 0, HUMANOID_Z))
     n = cm.n
     sims = []
     for warm in (True, False):
-        sim = Simulator(path, n_worlds=W, pgs_iters=50, pose=(0, 0, HUMANOID_Z, 1, 0, 0, 0))
+        sim = Simulator(path, n_worlds=W, pgs_iters=warm_iters if warm else 50, pose=(0, 0, HUMANOID_Z, 1, 0, 0, 0))
         assert sim.float_kernel() == 2
         sim.set_ground_plane(True, 1.0)
         sim.enable_contacts(True)
@@ -527,7 +528,7 @@ def test_humanoid_warm_started_pgs(require_gpu, oracle):
     kd = np.array([d for _, d in _humanoid_gains(sim.joint_names)])
     ows = []
     for w in range(4):
-        ow = oracle.FloatWorld(cm, pgs_iters=50, pgs_tol=tol, warm_start=True)
+        ow = oracle.FloatWorld(cm, pgs_iters=warm_iters, pgs_tol=tol, warm_start=True)
         ow.set_pose([0, 0, z[w]], np.eye(3))
         ow.set_joints(q0[w], np.zeros(n))
         ows.append(ow)
