@@ -256,9 +256,16 @@ Link lump(const Link& a, const Link& b, const M3& R, const V3& p) {
     return out;
 }
 
+// directory of the model file being compiled (relative mesh URIs); empty for
+// an inline model string (relative to the working directory)
+thread_local std::string g_model_dir;
+
 std::string read_source(const std::string& s) {
     size_t k = s.find_first_not_of(" \t\r\n");
+    g_model_dir.clear();
     if (k != std::string::npos && s[k] == '<') return s;
+    const size_t sl = s.rfind('/');
+    g_model_dir = (sl == std::string::npos) ? std::string(".") : s.substr(0, sl);
     std::ifstream f(s);
     if (!f) throw std::runtime_error("cannot open model file '" + s + "'");
     std::stringstream ss;
@@ -326,6 +333,11 @@ Description describe_urdf(const XNode* root, const double pose[7]) {
             } else if (cyl) {
                 sh.type = Shape::Cylinder;
                 sh.size = {num_attr(cyl, "radius", 0.0), 0.5 * num_attr(cyl, "length", 0.0), 0.0};
+            } else if (const XNode* me = ge ? ge->child("mesh") : nullptr) {
+                const std::string* fn = me->get("filename");
+                if (!fn) throw std::runtime_error("<mesh> without filename in link " + *nm);
+                sh = mesh_shape(load_mesh_vertices(resolve_mesh_uri(*fn, g_model_dir)),
+                                vec_attr(me, "scale", {1, 1, 1}), sh.R, sh.p);
             } else {
                 ++L.unsupported;
                 continue;
@@ -509,6 +521,13 @@ Description describe_sdf(const XNode* root, const double pose[7]) {
             } else if (cyl) {  // sdformat defaults: radius 0.5, length 1
                 sh.type = Shape::Cylinder;
                 sh.size = {sdf_num(cyl, "radius", 0.5), 0.5 * sdf_num(cyl, "length", 1.0), 0.0};
+            } else if (const XNode* me = ge ? ge->child("mesh") : nullptr) {
+                const XNode* uri = me->child("uri");
+                if (!uri) throw std::runtime_error("<mesh> without <uri> in link '" + *nm + "'");
+                auto sc = sdf_numbers(me, "scale", 3);
+                if (sc.empty()) sc = {1.0, 1.0, 1.0};
+                sh = mesh_shape(load_mesh_vertices(resolve_mesh_uri(uri->text, g_model_dir)), {sc[0], sc[1], sc[2]},
+                                sh.R, sh.p);
             } else {
                 ++L.unsupported;
                 continue;

@@ -41,14 +41,25 @@ struct ChainBody {
 };
 
 // A collision shape in its body's frame: box (size = half extents), sphere
-// (size[0] = radius) or cylinder along z (size = {radius, half length}).
-// Meshes and other geometries are counted, not modelled.
+// (size[0] = radius), cylinder along z (size = {radius, half length}) or mesh
+// (mesh.cpp: size = half extents of its bounding box, R / p = the mesh frame
+// moved to the box centre, points = its ground-contact support points in that
+// frame).  Other geometries are counted, not modelled.
+constexpr int kMeshMaxPoints = 16;
 struct Shape {
-    enum Type : int { Box = 0, Sphere = 1, Cylinder = 2 } type = Box;
+    enum Type : int { Box = 0, Sphere = 1, Cylinder = 2, Mesh = 3 } type = Box;
     std::array<double, 3> size{};
     std::array<double, 9> R{};
     std::array<double, 3> p{};
+    std::vector<std::array<double, 3>> points;  // Mesh only
 };
+
+// mesh.cpp: vertices of an STL / OBJ file; URI -> file path (the reference's
+// asFullPath); the Mesh shape of scaled vertices under collision pose (R, p).
+std::vector<std::array<double, 3>> load_mesh_vertices(const std::string& path);
+std::string resolve_mesh_uri(const std::string& uri, const std::string& model_dir);
+Shape mesh_shape(const std::vector<std::array<double, 3>>& verts, const std::array<double, 3>& scale,
+                 const std::array<double, 9>& R, const std::array<double, 3>& p);
 
 struct ChainModel {
     std::string name;              // robot name

@@ -273,9 +273,15 @@ void build_params(mw_scene* s) {
             const bool movable = !(nd == node && !cm.floating);
             P.shape_slot0[shape] = slot;
             if (movable) {
-                const int ns = (sh.type == mw::Shape::Sphere) ? 1 : 8;
+                const int ns = (sh.type == mw::Shape::Sphere) ? 1
+                               : (sh.type == mw::Shape::Mesh) ? static_cast<int>(sh.points.size())
+                                                              : 8;
                 if (slot + ns > mw::kScMaxGroundSlots) throw std::runtime_error("too many ground contact slots");
-                for (int k = 0; k < ns; ++k) P.slot_shape[slot + k] = static_cast<int16_t>(shape);
+                for (int k = 0; k < ns; ++k) {
+                    P.slot_shape[slot + k] = static_cast<int16_t>(shape);
+                    if (sh.type == mw::Shape::Mesh)
+                        for (int e = 0; e < 3; ++e) P.slot_pt[slot + k][e] = static_cast<float>(sh.points[k][e]);
+                }
                 slot += ns;
             }
             ++shape;
@@ -720,9 +726,12 @@ int mw_scene_replace_model(mw_scene* s, int32_t model, const char* urdf, const d
     for (int i = 0; same && i < cm.dofs(); ++i) {
         same = cm.bodies[i].parent == old.m.bodies[i].parent && cm.bodies[i].shapes.size() == old.m.bodies[i].shapes.size();
         for (size_t k = 0; same && k < cm.bodies[i].shapes.size(); ++k)
-            same = cm.bodies[i].shapes[k].type == old.m.bodies[i].shapes[k].type;
+            same = cm.bodies[i].shapes[k].type == old.m.bodies[i].shapes[k].type &&
+                   cm.bodies[i].shapes[k].points.size() == old.m.bodies[i].shapes[k].points.size();
     }
-    for (size_t k = 0; same && k < cm.base_shapes.size(); ++k) same = cm.base_shapes[k].type == old.m.base_shapes[k].type;
+    for (size_t k = 0; same && k < cm.base_shapes.size(); ++k)
+        same = cm.base_shapes[k].type == old.m.base_shapes[k].type &&
+               cm.base_shapes[k].points.size() == old.m.base_shapes[k].points.size();
     if (!same) return fail(MW_EINVAL, "the replacement model must have the same tree, base and collision shapes");
     const std::string nm = (name && *name) ? name : cm.name;
     for (size_t k = 0; k < s->models.size(); ++k)

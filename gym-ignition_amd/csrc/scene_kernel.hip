@@ -666,7 +666,9 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                     const bool sphere = (P->shape_type[sh] == 1);
                     const float* h = P->shape_size[sh];
                     const float* SR = P->shape_R[sh];
-                    const f3 lp = shape_slot_point(P->shape_type[sh], h, shape_plane_normal(nd.Rw, SR), c);
+                    const f3 lp = (P->shape_type[sh] == 3)
+                                      ? mk(P->slot_pt[slot][0], P->slot_pt[slot][1], P->slot_pt[slot][2])
+                                      : shape_slot_point(P->shape_type[sh], h, shape_plane_normal(nd.Rw, SR), c);
                     const float lx = lp.x, ly = lp.y, lz = lp.z;
                     const f3 bb = {P->shape_p[sh][0] + SR[0] * lx + SR[1] * ly + SR[2] * lz,
                                    P->shape_p[sh][1] + SR[3] * lx + SR[4] * ly + SR[5] * lz,
@@ -714,8 +716,11 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                                  P->shape_R[sb][8]}};
                 const f3 ca = A_.pw + mul(A_.Rw, mk(P->shape_p[sa][0], P->shape_p[sa][1], P->shape_p[sa][2]));
                 const f3 cb = B_.pw + mul(B_.Rw, mk(P->shape_p[sb][0], P->shape_p[sb][1], P->shape_p[sb][2]));
-                np = sc_collide(P->shape_type[sa], mk(P->shape_size[sa][0], P->shape_size[sa][1], P->shape_size[sa][2]),
-                                ca, mul3(A_.Rw, SRa), P->shape_type[sb],
+                // a mesh collides with other models as its bounding box (type 3 -> 0)
+                const int ta = P->shape_type[sa] == 3 ? 0 : P->shape_type[sa];
+                const int tb = P->shape_type[sb] == 3 ? 0 : P->shape_type[sb];
+                np = sc_collide(ta, mk(P->shape_size[sa][0], P->shape_size[sa][1], P->shape_size[sa][2]),
+                                ca, mul3(A_.Rw, SRa), tb,
                                 mk(P->shape_size[sb][0], P->shape_size[sb][1], P->shape_size[sb][2]), cb,
                                 mul3(B_.Rw, SRb), nrm, pts, deps);
             }

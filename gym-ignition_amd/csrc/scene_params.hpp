@@ -25,7 +25,7 @@ constexpr int kScMaxNodes = kScMaxModels + kScMaxBodies;   // <= 64 lanes
 constexpr int kScMaxNv = 6 * kScMaxModels + kScMaxBodies;   // 96 coordinates
 constexpr int kScMaxShapes = 48;
 constexpr int kScMaxPairs = 128;        // shape pairs of different models (2 lane passes)
-constexpr int kScMaxGroundSlots = 128;  // 8 corners per box, 1 per sphere (2 lane passes)
+constexpr int kScMaxGroundSlots = 128;  // 8 per box / cylinder, 1 per sphere, <= 16 per mesh (2 lane passes)
 constexpr int kScMaxContacts = 32;      // contact points per step (3 rows each)
 constexpr int kScMaxRows = 96;
 constexpr int kScWrenchSlots = 4;       // concurrent wrenches (distinct expiries) per link
@@ -75,7 +75,8 @@ struct SceneF {
     // collision shapes, model by model (base first, then by body)
     int32_t shape_node[kScMaxShapes];   // node owning the shape
     int32_t shape_model[kScMaxShapes];
-    int32_t shape_type[kScMaxShapes];   // 0 box (half extents), 1 sphere (radius)
+    int32_t shape_type[kScMaxShapes];   // 0 box (half extents), 1 sphere (radius), 2 cylinder, 3 mesh
+                                        // (bounding box half extents; ground slots at slot_pt)
     int32_t shape_slot0[kScMaxShapes];  // first ground slot
     float shape_size[kScMaxShapes][3];
     float shape_R[kScMaxShapes][9];     // shape pose in the node frame
@@ -83,6 +84,7 @@ struct SceneF {
     int16_t pair_a[kScMaxPairs];        // shape indices, model(a) < model(b)
     int16_t pair_b[kScMaxPairs];
     int16_t slot_shape[kScMaxGroundSlots];
+    float slot_pt[kScMaxGroundSlots][3];  // mesh slots: support point in the shape frame
 };
 
 // per-model JointController period gates of one launch (bit s: the PID of the

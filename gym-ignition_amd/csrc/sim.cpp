@@ -563,6 +563,24 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     } catch (const std::exception& e) {
         return fail(MW_EPARSE, e.what());
     }
+    // mesh collisions are modelled by the scene kernel (scene.cpp); the
+    // single-model kernels keep box / sphere / cylinder shapes.  A floating
+    // model would fall through the ground without its mesh: refuse it.
+    {
+        int meshes = 0;
+        auto strip = [&](std::vector<mw::Shape>& v) {
+            const size_t n0 = v.size();
+            v.erase(std::remove_if(v.begin(), v.end(), [](const mw::Shape& sh) { return sh.type == mw::Shape::Mesh; }),
+                    v.end());
+            meshes += static_cast<int>(n0 - v.size());
+        };
+        strip(s->model.base_shapes);
+        for (auto& b : s->model.bodies) strip(b.shapes);
+        if (meshes && s->model.floating)
+            return fail(MW_EPARSE, "mesh collisions on a floating model are supported in scenes (mw_scene / the "
+                                   "ScenarI/O World.insert_model), not on mw_sim");
+        s->model.unsupported_shapes += meshes;
+    }
     if (s->model.dofs() > mw::kMaxBodies)
         return fail(MW_EPARSE, "models with more than " + std::to_string(mw::kMaxBodies) +
                                    " moving joints are not supported by this build");
@@ -1218,6 +1236,36 @@ int mw_model_export_shapes(const mw_sim* s, int32_t body, double* out, int32_t m
         for (double v : sh[k].size) *o++ = v;
         for (double v : sh[k].R) *o++ = v;
         for (double v : sh[k].p) *o++ = v;
+    }
+    return MW_OK;
+}
+
+int mw_compile_collisions(const char* model, const double pose[7], double* out, int32_t max_shapes, int32_t* count) {
+    if (!model || !count || (max_shapes > 0 && !out)) return fail(MW_EINVAL, "null argument");
+    const double ident[7] = {0, 0, 0, 1, 0, 0, 0};
+    mw::ChainModel cm;
+    try {
+        cm = mw::compile_urdf(model, pose ? pose : ident);
+    } catch (const std::exception& e) {
+        return fail(MW_EPARSE, e.what());
+    }
+    std::vector<std::pair<int, const mw::Shape*>> all;
+    for (const auto& sh : cm.base_shapes) all.push_back({-1, &sh});
+    for (int b = 0; b < cm.dofs(); ++b)
+        for (const auto& sh : cm.bodies[b].shapes) all.push_back({b, &sh});
+    *count = static_cast<int32_t>(all.size());
+    for (int32_t k = 0; k < std::min<int32_t>(max_shapes, *count); ++k) {
+        const mw::Shape& sh = *all[k].second;
+        double* o = out + MW_COLLISION_WORDS * k;
+        std::fill(o, o + MW_COLLISION_WORDS, 0.0);
+        *o++ = all[k].first;
+        *o++ = static_cast<double>(sh.type);
+        for (double v : sh.size) *o++ = v;
+        for (double v : sh.R) *o++ = v;
+        for (double v : sh.p) *o++ = v;
+        *o++ = static_cast<double>(sh.points.size());
+        for (const auto& pt : sh.points)
+            for (double v : pt) *o++ = v;
     }
     return MW_OK;
 }

@@ -100,6 +100,7 @@ SIGNATURES = [
     ("mw_set_pgs_options", ctypes.c_int, [_P, ctypes.c_double, _I]),
     ("mw_pgs_options", ctypes.c_int, [_P, _D, _IP]),
     ("mw_model_export_shapes", ctypes.c_int, [_P, _I, _D, _I, _IP]),
+    ("mw_compile_collisions", ctypes.c_int, [_S, _D, _D, _I, _IP]),
     ("mw_device_params", ctypes.c_int, [_P, _P, _I]),
     ("mw_device_float_params", ctypes.c_int, [_P, _P, _I]),
     ("mw_baked_model", ctypes.c_int, [_P, _IP]),

@@ -82,6 +82,22 @@ def get_empty_world() -> str:
     return _EMPTY_WORLD
 
 
+_MESH_URDF = re.compile(r'(<mesh\b[^>]*?\bfilename\s*=\s*")([^"]+)(")')
+_MESH_SDF = re.compile(r'(<mesh\b[^>]*>(?:(?!</mesh>).)*?<uri>\s*)([^<]+?)(\s*</uri>)', re.S)
+
+
+def _absolute_mesh_uris(text: str, base_dir: str) -> str:
+    """Relative mesh URIs of a model read from a file resolve against the
+    file's directory, as the reference's asFullPath(uri, sdf FilePath) does
+    (Physics.cpp:905); the model compiler gets the text with absolute paths."""
+    def fix(m):
+        uri = m.group(2).strip()
+        if uri.startswith(("/", "model://", "package://", "file://")):
+            return m.group(0)
+        return m.group(1) + os.path.join(base_dir, uri) + m.group(3)
+    return _MESH_SDF.sub(fix, _MESH_URDF.sub(fix, text))
+
+
 def _read(path_or_string: str) -> str:
     if path_or_string.lstrip().startswith("<"):
         return path_or_string
@@ -1064,6 +1080,8 @@ class World:
         except OSError as e:
             _err(f"Failed to read model file: {e}")
             return False
+        if os.path.isfile(model_file):
+            text = _absolute_mesh_uris(text, os.path.dirname(os.path.abspath(model_file)))
         return self.insert_model_from_string(text, pose, override_model_name)
 
     def insert_model_from_string(self, model_string: str, pose: core.Pose = None,
@@ -1091,7 +1109,7 @@ class World:
         static = root.tag != "robot" and (root.find("model/static") is not None and
                                           root.find("model/static").text.strip().lower() in ("1", "true"))
         solid = [g for g in root.findall("model/link/collision/geometry")
-                 if g.find("box") is not None or g.find("sphere") is not None or g.find("cylinder") is not None]
+                 if any(g.find(t) is not None for t in ("box", "sphere", "cylinder", "mesh"))]
         if static and not solid:
             if root.findall("model/joint"):
                 _err("static SDF models with joints are not supported by this build")
@@ -1106,7 +1124,7 @@ class World:
                 self._ground_name = f"{name}::{link.get('name', 'link')}"
                 self._simulator._set_ground(self, True, self._ground_mu)
             return True
-        # a static model with box / sphere / cylinder collisions is a welded
+        # a static model with box / sphere / cylinder / mesh collisions is a welded
         # collider of the scene (the model compiler welds its links to the world)
         if root.tag != "robot" and [float(v) for v in (*pose.position, *pose.orientation)] == [0, 0, 0, 1, 0, 0, 0]:
             # the identity keeps the SDF model's own <pose> (World.cpp:169-177)

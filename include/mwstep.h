@@ -136,6 +136,18 @@ int mw_model_export_base(const mw_sim* sim, double out[23]);
  * doubles; *count receives the number of shapes, at most `max_shapes` are
  * written (Physics.cpp:687-1219 creates one collision per <collision>). */
 int mw_model_export_shapes(const mw_sim* sim, int32_t body, double* out, int32_t max_shapes, int32_t* count);
+/* Compile a model (URDF / SDF file path or string; no simulator, no GPU) and
+ * export every collision it holds, base first then by body, as the scene
+ * kernel sees them (Physics.cpp:687-1219 builds one shape per <collision>;
+ * meshes :897-931): per shape MW_COLLISION_WORDS doubles {body (-1 = base),
+ * type (0 box, 1 sphere, 2 cylinder, 3 mesh), size[3], R[9], p[3], npts,
+ * points[16][3]} -- a mesh's size is its bounding box half extents, p the box
+ * centre, points its ground-contact support points in the shape frame
+ * (gym-ignition_amd/csrc/mesh.cpp).  mw_sim drops mesh shapes (fixed-base
+ * models) or refuses them (floating models): meshes run in scenes. */
+#define MW_COLLISION_WORDS 66
+int mw_compile_collisions(const char* model, const double pose[7], double* out, int32_t max_shapes,
+                          int32_t* count);
 
 /* Copy of the float32 parameter block the kernels read (struct ChainF of
  * gym-ignition_amd/csrc/chain_params.hpp), for tests and tools. */

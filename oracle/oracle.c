@@ -2162,12 +2162,15 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
                 const double* hh = fm->shape_size[sh];
                 const double* SR = fm->shape_R[sh];
                 const double* sp = fm->shape_p[sh];
-                const int corners = (fm->shape_type[sh] == 1) ? 1 : 8;
+                const int corners = (fm->shape_type[sh] == 1) ? 1 : (fm->shape_type[sh] == 3) ? fm->shape_npts[sh] : 8;
                 double RS[9];
                 rot_mul(Rb, SR, RS);
                 for (int corner = 0; corner < corners; ++corner) {
                     double l[3], b3[3], x[3];
-                    or_slot_point(fm->shape_type[sh], hh, RS, corner, l);
+                    if (fm->shape_type[sh] == 3)   /* mesh: its support points */
+                        memcpy(l, fm->shape_pts[sh][corner], sizeof l);
+                    else
+                        or_slot_point(fm->shape_type[sh], hh, RS, corner, l);
                     for (int r = 0; r < 3; ++r) b3[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
                     for (int r = 0; r < 3; ++r) x[r] = pb[r] + Rb[r * 3] * b3[0] + Rb[r * 3 + 1] * b3[1] + Rb[r * 3 + 2] * b3[2];
                     double dep = -x[2];
@@ -2211,8 +2214,11 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
                         }
                     }
                     double nrm[3], pts[12], deps[4];
-                    const int np = or_collide(A->shape_type[sa], A->shape_size[sa], cA, RA, B->shape_type[sb],
-                                              B->shape_size[sb], cB, RB, nrm, pts, deps);
+                    /* a mesh collides with other models as its bounding box */
+                    const int ta = A->shape_type[sa] == 3 ? 0 : A->shape_type[sa];
+                    const int tb = B->shape_type[sb] == 3 ? 0 : B->shape_type[sb];
+                    const int np = or_collide(ta, A->shape_size[sa], cA, RA, tb, B->shape_size[sb], cB, RB, nrm, pts,
+                                              deps);
                     for (int i = 0; i < np && nc < OR_SC_MAXC; ++i) {
                         memcpy(cp[nc], pts + 3 * i, sizeof cp[nc]);
                         memcpy(cn[nc], nrm, sizeof nrm);

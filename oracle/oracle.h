@@ -141,6 +141,7 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
 /* ------------------------------------------------------------------ */
 #define OR_MAXFS 16
 #define OR_MAXFC (8 * OR_MAXFS)
+#define OR_MESH_MAXP 16
 
 typedef struct {
     or_model tree;               /* moving bodies; parent -1 = the base body  */
@@ -150,12 +151,18 @@ typedef struct {
     int32_t n_shapes;
     int32_t ground;
     int32_t shape_body[OR_MAXFS];        /* -1 = base                        */
-    int32_t shape_type[OR_MAXFS];        /* 0 box (half extents), 1 sphere   */
+    int32_t shape_type[OR_MAXFS];        /* 0 box (half extents), 1 sphere,  */
+                                         /* 2 cylinder, 3 mesh               */
     double shape_size[OR_MAXFS][3];
     double shape_R[OR_MAXFS][9];
     double shape_p[OR_MAXFS][3];
     double gravity[3];           /* world frame                               */
     double mu;
+    /* type 3 mesh (scenes only): size = half extents of its bounding box (the
+     * shape frame sits at the box centre), ground-contact support points in
+     * the shape frame */
+    int32_t shape_npts[OR_MAXFS];
+    double shape_pts[OR_MAXFS][OR_MESH_MAXP][3];
 } or_float_model;
 
 typedef struct {

@@ -93,6 +93,7 @@ class OrFreeState(ctypes.Structure):
 
 OR_MAXFS = 16
 OR_MAXFC = 8 * OR_MAXFS
+OR_MESH_MAXP = 16   # oracle.h: support points per mesh
 OR_WARM_WORDS = 3 * OR_MAXFC + 3 * OR_MAXB   # oracle.h OR_WARM_WORDS
 
 
@@ -111,6 +112,8 @@ class OrFloatModel(ctypes.Structure):
         ("shape_p", (ctypes.c_double * 3) * OR_MAXFS),
         ("gravity", ctypes.c_double * 3),
         ("mu", ctypes.c_double),
+        ("shape_npts", ctypes.c_int32 * OR_MAXFS),
+        ("shape_pts", ((ctypes.c_double * 3) * OR_MESH_MAXP) * OR_MAXFS),
     ]
 
 
@@ -386,6 +389,11 @@ def sdf_to_urdf(text: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0
             elif cyl is not None:
                 geo = (f'<cylinder radius="{_sdf_val(cyl, "radius", 0.5)!r}" '
                        f'length="{_sdf_val(cyl, "length", 1.0)!r}"/>')
+            elif ce.find("geometry/mesh/uri") is not None:
+                me = ce.find("geometry/mesh")
+                sc = me.find("scale")
+                geo = (f'<mesh filename="{me.find("uri").text.strip()}" '
+                       f'scale="{sc.text.strip() if sc is not None else "1 1 1"}"/>')
             else:
                 continue
             out.append(f'<collision>{_origin(Tc)}<geometry>{geo}</geometry></collision>')
@@ -440,12 +448,87 @@ def _rot_to_quat(R: np.ndarray):
     return tuple(q)
 
 
+# --------------------------------------------------------------------------
+# mesh collisions (Physics.cpp:897-931 attaches the loaded mesh with the
+# collision pose and the SDF <scale>): restated independently of the model
+# compiler's csrc/mesh.cpp -- STL (binary / ASCII) and OBJ vertices, the
+# support points along 26 fixed directions (8 cube corners, 12 edges, 6 faces;
+# the first vertex of the maximum; at most OR_MESH_MAXP distinct ones) and the
+# bounding box in the mesh frame (the shape frame is moved to its centre).
+# --------------------------------------------------------------------------
+_MESH_DIRS = np.array([(-1, -1, -1), (-1, -1, 1), (-1, 1, -1), (-1, 1, 1), (1, -1, -1), (1, -1, 1), (1, 1, -1),
+                       (1, 1, 1), (-1, -1, 0), (-1, 1, 0), (1, -1, 0), (1, 1, 0), (-1, 0, -1), (-1, 0, 1),
+                       (1, 0, -1), (1, 0, 1), (0, -1, -1), (0, -1, 1), (0, 1, -1), (0, 1, 1), (-1, 0, 0),
+                       (1, 0, 0), (0, -1, 0), (0, 1, 0), (0, 0, -1), (0, 0, 1)], dtype=float)
+
+
+def mesh_vertices(path: str) -> np.ndarray:
+    """[V, 3] vertices of an STL (binary or ASCII) or Wavefront OBJ file."""
+    low = path.lower()
+    with open(path, "rb") as f:
+        data = f.read()
+    if low.endswith(".stl"):
+        if len(data) >= 84:
+            n = int(np.frombuffer(data[80:84], dtype="<u4")[0])
+            if len(data) == 84 + 50 * n:
+                rec = np.frombuffer(data[84:], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)),
+                                                               ("a", "<u2")]), count=n)
+                return rec["v"].reshape(-1, 3).astype(float)
+        toks = data.decode("ascii", "replace").split()
+        v = [[float(toks[i + 1]), float(toks[i + 2]), float(toks[i + 3])]
+             for i, t in enumerate(toks) if t == "vertex"]
+    elif low.endswith(".obj"):
+        v = [[float(x) for x in ln.split()[1:4]] for ln in data.decode("ascii", "replace").splitlines()
+             if ln.startswith(("v ", "v\t"))]
+    else:
+        raise ValueError(f"mesh '{path}': only STL and OBJ collision meshes are supported")
+    if not v:
+        raise ValueError(f"mesh '{path}' has no vertices")
+    return np.array(v, dtype=float)
+
+
+def resolve_mesh_uri(uri: str, model_dir: str = "") -> str:
+    uri = uri.strip()
+    if uri.startswith("file://"):
+        return uri[7:]
+    for pre in ("model://", "package://"):
+        if uri.startswith(pre):
+            rest = uri[len(pre):]
+            for var in ("GZ_SIM_RESOURCE_PATH", "IGN_GAZEBO_RESOURCE_PATH", "SDF_PATH", "ROS_PACKAGE_PATH"):
+                for d in os.environ.get(var, "").split(":"):
+                    if d and os.path.exists(os.path.join(d, rest)):
+                        return os.path.join(d, rest)
+            if model_dir and "/" in rest and os.path.exists(os.path.join(model_dir, rest.split("/", 1)[1])):
+                return os.path.join(model_dir, rest.split("/", 1)[1])
+            raise ValueError(f"cannot resolve mesh URI '{uri}'")
+    if uri.startswith("/") or not model_dir:
+        return uri
+    return os.path.join(model_dir, uri)
+
+
+def mesh_shape(verts, scale, SR, sp):
+    """(3, size, R, p) of a mesh collision: size = [half extents, support
+    points (shape frame, flattened)]; p = the bounding-box centre."""
+    v = np.asarray(verts, dtype=float) * np.asarray(scale, dtype=float)
+    lo, hi = v.min(axis=0), v.max(axis=0)
+    c, half = 0.5 * (lo + hi), 0.5 * (hi - lo)
+    pick: List[int] = []
+    for d in _MESH_DIRS:
+        i = int(np.argmax(d[0] * v[:, 0] + d[1] * v[:, 1] + d[2] * v[:, 2]))
+        if i not in pick and len(pick) < OR_MESH_MAXP:
+            pick.append(i)
+    pts = v[pick] - c
+    return (3, np.concatenate([half, pts.reshape(-1)]), SR, np.asarray(sp, dtype=float) + SR @ c)
+
+
 def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0.0),
               gravity=(0.0, 0.0, -9.8)) -> ChainModel:
     text = path_or_string
+    model_dir = ""
     if not path_or_string.lstrip().startswith("<"):
         with open(path_or_string) as f:
             text = f.read()
+        model_dir = os.path.dirname(path_or_string) or "."
     root = ET.fromstring(text.strip())
     if root.tag == "sdf":
         text, pose_xyz, pose_wxyz = sdf_to_urdf(text, pose_xyz, pose_wxyz)
@@ -479,6 +562,10 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
             elif cyl is not None:   # axis z: (radius, half length)
                 L.shapes.append((2, np.array([float(cyl.get("radius")), 0.5 * float(cyl.get("length")), 0.0]),
                                  SR, sp))
+            elif geo is not None and geo.find("mesh") is not None:
+                me = geo.find("mesh")
+                verts = mesh_vertices(resolve_mesh_uri(me.get("filename"), model_dir))
+                L.shapes.append(mesh_shape(verts, _vec(me, "scale", [1, 1, 1]), SR, sp))
         links[le.get("name")] = L
     joints: List[_Joint] = []
     for je in root.findall("joint"):
@@ -601,8 +688,9 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
             F.gravity[k] = gravity[k]
         for k, v in enumerate([B.I[0, 0], B.I[1, 1], B.I[2, 2], B.I[0, 1], B.I[0, 2], B.I[1, 2]]):
             F.Ic[k] = v
-        F.n_shapes = len(B.shapes)
-        for i, (t, sz, SR, sp) in enumerate(B.shapes):
+        solid = [sh for sh in B.shapes if sh[0] != 3]   # meshes: scenes only (SceneWorld)
+        F.n_shapes = len(solid)
+        for i, (t, sz, SR, sp) in enumerate(solid):
             F.shape_type[i] = t
             for k in range(3):
                 F.shape_size[i][k] = sz[k]
@@ -836,7 +924,8 @@ class FloatWorld:
         for k in range(6):
             m.base_Ic[k] = F.Ic[k]
         shapes = [(-1, F.shape_type[i], np.array(F.shape_size[i][:]), np.array(F.shape_R[i][:]).reshape(3, 3),
-                   np.array(F.shape_p[i][:])) for i in range(F.n_shapes)] + list(cm.body_shapes)
+                   np.array(F.shape_p[i][:])) for i in range(F.n_shapes)] + [
+                       sh for sh in cm.body_shapes if sh[1] != 3]   # meshes: scenes only (SceneWorld)
         assert len(shapes) <= OR_MAXFS
         m.n_shapes = len(shapes)
         for i, (b, t, sz, SR, sp) in enumerate(shapes):
@@ -984,6 +1073,12 @@ class SceneWorld:
                     fm.shape_p[i][k] = sp[k]
                 for k in range(9):
                     fm.shape_R[i][k] = np.asarray(SR).flat[k]
+                if t == 3:   # mesh: sz = half extents, then the support points
+                    pts = np.asarray(sz[3:]).reshape(-1, 3)
+                    fm.shape_npts[i] = len(pts)
+                    for c, pt in enumerate(pts):
+                        for k in range(3):
+                            fm.shape_pts[i][c][k] = pt[k]
             s0 = self.st.s[m]
             for k in range(3):
                 s0.p[k] = cm.base_p[k]
