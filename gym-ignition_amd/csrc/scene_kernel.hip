@@ -330,6 +330,105 @@ __device__ __forceinline__ int sc_cylinder_sphere(f3 h, f3 c, const M3& R, float
     return 1;
 }
 
+// cylinder pairs (cylinder-box, cylinder-cylinder): oracle.c cylinder_pair in
+// float32 -- least-overlap axis among the shapes' candidate axes (box faces;
+// cylinder axis and radial direction), sampled features (box corners; 4 rim
+// points per cap at 0.999 r facing the other centre) inside the other shape
+// and past its extreme plane, <= 8 kept, reduced to 4
+__device__ __forceinline__ float sc_support(int type, f3 h, const M3& R, f3 n) {
+    if (type == 0)
+        return h.x * fabsf(dot(n, col(R, 0))) + h.y * fabsf(dot(n, col(R, 1))) + h.z * fabsf(dot(n, col(R, 2)));
+    const float c = dot(n, col(R, 2));
+    return h.x * sqrtf(fmaxf(1.f - c * c, 0.f)) + h.y * fabsf(c);
+}
+
+__device__ __forceinline__ int sc_axes(int type, f3 c, const M3& R, f3 other, f3* ax) {
+    if (type == 0) {
+        ax[0] = col(R, 0);
+        ax[1] = col(R, 1);
+        ax[2] = col(R, 2);
+        return 3;
+    }
+    ax[0] = col(R, 2);
+    const f3 d = other - c;
+    const f3 q = d - dot(d, ax[0]) * ax[0];
+    const float nq = sqrtf(dot(q, q));
+    if (nq <= 1e-9f) return 1;
+    ax[1] = (1.f / nq) * q;
+    return 2;
+}
+
+__device__ __forceinline__ f3 sc_pair_sample(int type, f3 h, f3 c, const M3& R, f3 other, int k) {
+    f3 l;
+    if (type == 0) {
+        l = {(k & 4) ? h.x : -h.x, (k & 2) ? h.y : -h.y, (k & 1) ? h.z : -h.z};
+    } else {
+        const f3 d = mulT(R, other - c);
+        float ux = d.x, uy = d.y;
+        const float n2 = ux * ux + uy * uy;
+        if (n2 > 1e-12f) {
+            const float inv = 1.f / sqrtf(n2);
+            ux *= inv;
+            uy *= inv;
+        } else {
+            ux = 1.f;
+            uy = 0.f;
+        }
+        const int j = k & 3;
+        const float dx = (j == 0) ? ux : ((j == 1) ? -uy : ((j == 2) ? -ux : uy));
+        const float dy = (j == 0) ? uy : ((j == 1) ? ux : ((j == 2) ? -uy : -ux));
+        l = {0.999f * h.x * dx, 0.999f * h.x * dy, (k & 4) ? h.y : -h.y};
+    }
+    return c + mul(R, l);
+}
+
+__device__ __forceinline__ bool sc_inside(int type, f3 h, f3 c, const M3& R, f3 p) {
+    const f3 l = mulT(R, p - c);
+    if (type == 0) return h.x - fabsf(l.x) > 0.f && h.y - fabsf(l.y) > 0.f && h.z - fabsf(l.z) > 0.f;
+    return h.x - sqrtf(l.x * l.x + l.y * l.y) > 0.f && h.y - fabsf(l.z) > 0.f;
+}
+
+// Kept out of line: inlined into scene_run_kernel, the build produced NaN
+// poses in box / sphere / chain piles that never reach this function
+// (tests/test_gpu_scene.py test_one_step_parity_random_piles), so the register
+// allocation of the main kernel is left as it was without it.
+__device__ __noinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& Ra, int tb, f3 hb, f3 cb,
+                                                const M3& Rb, f3& n, f3* pts, float* deps) {
+    f3 ax[6];
+    int na = sc_axes(ta, ca, Ra, cb, ax);
+    na += sc_axes(tb, cb, Rb, ca, ax + na);
+    const f3 dab = ca - cb;
+    int best = -1;
+    float ov_min = 0.f;
+    for (int k = 0; k < na; ++k) {
+        const float ov = sc_support(ta, ha, Ra, ax[k]) + sc_support(tb, hb, Rb, ax[k]) - fabsf(dot(ax[k], dab));
+        if (ov <= 0.f) return 0;
+        if (best < 0 || ov < ov_min) { ov_min = ov; best = k; }
+    }
+    n = dot(ax[best], dab) >= 0.f ? ax[best] : -ax[best];
+    const float plane_b = dot(n, cb) + sc_support(tb, hb, Rb, n);
+    const float plane_a = dot(n, ca) - sc_support(ta, ha, Ra, n);
+    f3 P8[8];
+    float D8[8];
+    int m = 0;
+    for (int side = 0; side < 2; ++side)
+        for (int k = 0; k < 8 && m < 8; ++k) {
+            const f3 q = side ? sc_pair_sample(tb, hb, cb, Rb, ca, k) : sc_pair_sample(ta, ha, ca, Ra, cb, k);
+            const bool in = side ? sc_inside(ta, ha, ca, Ra, q) : sc_inside(tb, hb, cb, Rb, q);
+            const float dep = side ? dot(n, q) - plane_a : plane_b - dot(n, q);
+            if (!in || dep <= 0.f) continue;
+            P8[m] = q;
+            D8[m] = dep;
+            ++m;
+        }
+    m = sc_reduce(m, P8, D8);
+    for (int i = 0; i < m; ++i) {
+        pts[i] = P8[i];
+        deps[i] = D8[i];
+    }
+    return m;
+}
+
 // shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius,
 // 2 cylinder: size = {radius, half length}): normal from B into A, up to 4
 // points / depths
@@ -346,7 +445,7 @@ __device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, in
         n = nbs;
         return 1;
     }
-    if (ta == 2 || tb == 2) return 0;  // cylinder-box, cylinder-cylinder: not in this build
+    if (ta == 2 || tb == 2) return sc_cylinder_pair(ta, sa, ca, Ra, tb, sb, cb, Rb, n, pts, deps);
     if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, pts, deps);
     if (ta == 1 && tb == 1) {
         const f3 d = ca - cb;

@@ -2017,6 +2017,159 @@ static int cylinder_sphere(const double* h, const double* c, const double* R, do
     return 1;
 }
 
+/* 8 sample points of a box / cylinder for the cylinder-pair narrow phase
+ * (see cylinder_pair) */
+static void pair_samples(int type, const double* h, const double* c, const double* R, const double* other,
+                         double out[8][3])
+{
+    for (int k = 0; k < 8; ++k) {
+        double l[3];
+        if (type == 0) {
+            l[0] = (k & 4) ? h[0] : -h[0];
+            l[1] = (k & 2) ? h[1] : -h[1];
+            l[2] = (k & 1) ? h[2] : -h[2];
+        } else {
+            const double d[3] = {other[0] - c[0], other[1] - c[1], other[2] - c[2]};
+            double ux = R[0] * d[0] + R[3] * d[1] + R[6] * d[2], uy = R[1] * d[0] + R[4] * d[1] + R[7] * d[2];
+            const double n2 = ux * ux + uy * uy;
+            if (n2 > 1e-12) {
+                const double inv = 1.0 / sqrt(n2);
+                ux *= inv;
+                uy *= inv;
+            } else {
+                ux = 1.0;
+                uy = 0.0;
+            }
+            const int j = k & 3;
+            const double dx = (j == 0) ? ux : ((j == 1) ? -uy : ((j == 2) ? -ux : uy));
+            const double dy = (j == 0) ? uy : ((j == 1) ? ux : ((j == 2) ? -uy : -ux));
+            l[0] = 0.999 * h[0] * dx;
+            l[1] = 0.999 * h[0] * dy;
+            l[2] = (k & 4) ? h[1] : -h[1];
+        }
+        for (int r = 0; r < 3; ++r) out[k][r] = c[r] + R[r * 3] * l[0] + R[r * 3 + 1] * l[1] + R[r * 3 + 2] * l[2];
+    }
+}
+
+/* point p inside shape (box / cylinder)?  outward normal at the nearest face, depth */
+static int inside_shape(int type, const double* h, const double* c, const double* R, const double* p, double n[3],
+                        double* dep)
+{
+    const double d[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+    double l[3], e[3] = {0.0, 0.0, 0.0};
+    for (int k = 0; k < 3; ++k) l[k] = R[k] * d[0] + R[3 + k] * d[1] + R[6 + k] * d[2];
+    if (type == 0) {
+        int best = -1;
+        double pen = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            const double g = h[k] - fabs(l[k]);
+            if (g <= 0.0) return 0;
+            if (best < 0 || g < pen) { pen = g; best = k; }
+        }
+        e[best] = l[best] >= 0.0 ? 1.0 : -1.0;
+        *dep = pen;
+    } else {
+        const double rho = sqrt(l[0] * l[0] + l[1] * l[1]);
+        const double gs = h[0] - rho, gc = h[1] - fabs(l[2]);
+        if (gs <= 0.0 || gc <= 0.0) return 0;
+        if (gs < gc && rho > 0.0) {
+            e[0] = l[0] / rho;
+            e[1] = l[1] / rho;
+            *dep = gs;
+        } else {
+            e[2] = l[2] >= 0.0 ? 1.0 : -1.0;
+            *dep = gc;
+        }
+    }
+    for (int r = 0; r < 3; ++r) n[r] = R[r * 3] * e[0] + R[r * 3 + 1] * e[1] + R[r * 3 + 2] * e[2];
+    return 1;
+}
+
+/* support extent of a box / cylinder along the unit direction n */
+static double shape_support(int type, const double* h, const double* R, const double* n)
+{
+    if (type == 0) {
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s += h[k] * fabs(n[0] * R[k] + n[1] * R[3 + k] + n[2] * R[6 + k]);
+        return s;
+    }
+    const double c = n[0] * R[2] + n[1] * R[5] + n[2] * R[8];
+    const double s2 = 1.0 - c * c;
+    return h[0] * sqrt(s2 > 0.0 ? s2 : 0.0) + h[1] * fabs(c);
+}
+
+/* candidate separating axes of one shape: box face normals; cylinder axis
+ * and the radial direction towards the other shape's centre */
+static int shape_axes(int type, const double* c, const double* R, const double* other, double ax[3][3])
+{
+    if (type == 0) {
+        for (int k = 0; k < 3; ++k) col3(R, k, ax[k]);
+        return 3;
+    }
+    col3(R, 2, ax[0]);
+    const double d[3] = {other[0] - c[0], other[1] - c[1], other[2] - c[2]};
+    const double t = dot3(d, ax[0]);
+    double q[3] = {d[0] - t * ax[0][0], d[1] - t * ax[0][1], d[2] - t * ax[0][2]};
+    const double nq = sqrt(dot3(q, q));
+    if (nq <= 1e-9) return 1;
+    for (int k = 0; k < 3; ++k) ax[1][k] = q[k] / nq;
+    return 2;
+}
+
+/* Cylinder pairs (cylinder-box, cylinder-cylinder; DART's collision detector
+ * [EXT] works on the exact geometry): the contact normal is the candidate
+ * axis of least overlap (supports of both shapes minus the centre distance
+ * along it; A's axes then B's, first on ties; no overlap on some axis = no
+ * contact), oriented from B into A.  The points are sampled features: 8 per
+ * shape -- a box's corners, a cylinder's 4 rim points per cap at 0.999 r,
+ * 90 degrees apart, the first facing the other shape's centre (x axis when
+ * coaxial) -- that lie inside the other shape and beyond its extreme plane
+ * along the normal (depth = distance past that plane); A's samples then B's,
+ * at most 8, reduced to 4 by reduce_points. */
+static int cylinder_pair(int ta, const double* ha, const double* ca, const double* Ra, int tb, const double* hb,
+                         const double* cb, const double* Rb, double normal[3], double* points, double* depths)
+{
+    double ax[6][3];
+    int na = shape_axes(ta, ca, Ra, cb, ax);
+    na += shape_axes(tb, cb, Rb, ca, ax + na);
+    const double dab[3] = {ca[0] - cb[0], ca[1] - cb[1], ca[2] - cb[2]};
+    int best = -1;
+    double ov_min = 0.0;
+    for (int k = 0; k < na; ++k) {
+        const double ov = shape_support(ta, ha, Ra, ax[k]) + shape_support(tb, hb, Rb, ax[k]) - fabs(dot3(ax[k], dab));
+        if (ov <= 0.0) return 0;
+        if (best < 0 || ov < ov_min) { ov_min = ov; best = k; }
+    }
+    double n[3];
+    const double sg = dot3(ax[best], dab) >= 0.0 ? 1.0 : -1.0;
+    for (int k = 0; k < 3; ++k) n[k] = sg * ax[best][k];
+    const double plane_b = dot3(n, cb) + shape_support(tb, hb, Rb, n);   /* B's face towards A */
+    const double plane_a = dot3(n, ca) - shape_support(ta, ha, Ra, n);   /* A's face towards B */
+    double sp[2][8][3];
+    pair_samples(ta, ha, ca, Ra, cb, sp[0]);
+    pair_samples(tb, hb, cb, Rb, ca, sp[1]);
+    double p[8][3], d[8];
+    int m = 0;
+    for (int side = 0; side < 2; ++side)
+        for (int k = 0; k < 8 && m < 8; ++k) {
+            double nn[3], dd;
+            const int in = side ? inside_shape(ta, ha, ca, Ra, sp[1][k], nn, &dd)
+                                : inside_shape(tb, hb, cb, Rb, sp[0][k], nn, &dd);
+            const double dep = side ? dot3(n, sp[1][k]) - plane_a : plane_b - dot3(n, sp[0][k]);
+            if (!in || dep <= 0.0) continue;
+            memcpy(p[m], sp[side][k], sizeof p[m]);
+            d[m] = dep;
+            ++m;
+        }
+    m = reduce_points(m, p, d);
+    memcpy(normal, n, sizeof n);
+    for (int i = 0; i < m; ++i) {
+        memcpy(points + 3 * i, p[i], 3 * sizeof(double));
+        depths[i] = d[i];
+    }
+    return m;
+}
+
 int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
                const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
                double* depths)
@@ -2032,7 +2185,8 @@ int or_collide(int type_a, const double* size_a, const double* c_a, const double
         memcpy(normal, nbs, sizeof nbs);
         return 1;
     }
-    if (type_a == 2 || type_b == 2) return 0;  /* cylinder-box, cylinder-cylinder: not in this build */
+    if (type_a == 2 || type_b == 2)   /* cylinder-box, cylinder-cylinder */
+        return cylinder_pair(type_a, size_a, c_a, R_a, type_b, size_b, c_b, R_b, normal, points, depths);
     if (type_a == 0 && type_b == 0) return box_box(size_a, c_a, R_a, size_b, c_b, R_b, normal, points, depths);
     if (type_a == 1 && type_b == 1) {
         double d[3] = {c_a[0] - c_b[0], c_a[1] - c_b[1], c_a[2] - c_b[2]};

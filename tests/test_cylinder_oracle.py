@@ -11,7 +11,10 @@ compared with it (CPU):
     v = omega r, and the final speed is omega0 r / 3 (a solid cylinder,
     I = m r^2 / 2, angular momentum about the contact line conserved);
   * the URDF and SDF cylinder geometry compile alike in the product's C++
-    compiler and the oracle's reader.
+    compiler and the oracle's reader;
+  * cylinder-sphere closed forms, a ball on a pillar; cylinder-box and
+    cylinder-cylinder pairs (sampled features): closed forms, a cylinder
+    standing and lying on a welded table, a two-cylinder stack.
 """
 
 import ctypes
@@ -153,8 +156,9 @@ def test_cylinder_sphere_closed_forms(oracle):
     assert np.allclose(n, [-1, 0, 0]) and dep[0] == pytest.approx(0.07) and np.allclose(pts[0], [0.1, 0, 0])
     # apart
     assert len(oracle.collide(2, cyl, [0, 0, 0], I, 1, [0.05], [0, 0, 0.3], I)[1]) == 0
-    # cylinder-box pairs are not collided in this build
-    assert len(oracle.collide(2, cyl, [0, 0, 0], I, 0, [0.1, 0.1, 0.1], [0, 0, 0.25], I)[1]) == 0
+    # cylinder-box (sampled features, below): the cylinder's top rim in the box above
+    n, pts, dep = oracle.collide(2, cyl, [0, 0, 0], I, 0, [0.1, 0.1, 0.1], [0, 0, 0.25], I)
+    assert np.allclose(n, [0, 0, -1]) and np.allclose(dep, 0.05)
 
 
 PILLAR = ('<robot name="pillar"><link name="world"/><joint name="fix" type="fixed"><parent link="world"/>'
@@ -180,3 +184,78 @@ def test_ball_rests_on_a_pillar(oracle):
     assert sw.p(1)[2] == pytest.approx(0.65, abs=2e-3)
     fz = sum(c[8] for c, who in sw.contacts if 0 in (who[0], who[2]) and 1 in (who[0], who[2]))
     assert abs(fz) == pytest.approx(1.0 * G, abs=0.05)
+
+
+# ---------------------------------------------------------------- cylinder pairs
+# cylinder-box and cylinder-cylinder contacts between models (oracle.c
+# cylinder_pair: sampled features, 8 samples per shape, the deepest
+# candidate's normal, <= 4 points)
+
+TABLE = ('<robot name="table"><link name="world"/><joint name="fix" type="fixed"><parent link="world"/>'
+         '<child link="t"/><origin xyz="0 0 0.25"/></joint><link name="t"><inertial><mass value="10"/>'
+         '<inertia ixx="1" iyy="1" izz="1" ixy="0" ixz="0" iyz="0"/></inertial><collision><geometry>'
+         '<box size="0.8 0.8 0.1"/></geometry></collision></link></robot>')   # top face at z = 0.3
+
+
+def _pair_force(sw, a, b):
+    return sum(c[8] if who[0] == b else -c[8] for c, who in sw.contacts
+               if {who[0], who[2]} == {a, b})
+
+
+def test_cylinder_box_closed_forms(oracle):
+    """cylinder A (r 0.1, half length 0.2) standing 0.01 deep in a box B top:
+    4 bottom-rim points, normal +z (B into A), depth 0.01; lying 0.02 deep:
+    the two rim points facing the box; apart: nothing"""
+    I = np.eye(3)
+    hb, cb = [0.4, 0.4, 0.05], [0.0, 0.0, 0.0]
+    nrm, pts, dep = oracle.collide(2, [0.1, 0.2, 0], [0, 0, 0.24], I, 0, hb, cb, I)
+    assert len(dep) == 4
+    np.testing.assert_allclose(nrm, [0, 0, 1], atol=1e-12)
+    np.testing.assert_allclose(dep, 0.01, atol=1e-12)
+    np.testing.assert_allclose(pts[:, 2], 0.04, atol=1e-12)
+    np.testing.assert_allclose(np.hypot(pts[:, 0], pts[:, 1]), 0.0999, atol=1e-12)
+    Ry = np.array([[0, 0, 1], [0, 1, 0], [-1, 0, 0]], dtype=float)   # axis along x
+    nrm, pts, dep = oracle.collide(2, [0.1, 0.2, 0], [0, 0, 0.13], Ry, 0, hb, cb, I)
+    assert len(dep) == 2
+    np.testing.assert_allclose(nrm, [0, 0, 1], atol=1e-12)
+    np.testing.assert_allclose(sorted(pts[:, 0]), [-0.2, 0.2], atol=1e-12)
+    np.testing.assert_allclose(dep, 0.05 - (0.13 - 0.0999), atol=1e-12)
+    assert len(oracle.collide(2, [0.1, 0.2, 0], [0, 0, 0.26], I, 0, hb, cb, I)[2]) == 0
+    # B into A is reversed when the box is A
+    nrm, _, _ = oracle.collide(0, hb, cb, I, 2, [0.1, 0.2, 0], [0, 0, 0.24], I)
+    np.testing.assert_allclose(nrm, [0, 0, -1], atol=1e-12)
+
+
+def test_cylinder_stands_on_a_table(oracle):
+    cms = [oracle.load_urdf(TABLE), oracle.load_urdf(cylinder_urdf(2.0, 0.1, 0.4), pose_xyz=(0.05, 0, 0.55))]
+    sw = oracle.SceneWorld(cms, pgs_iters=50)
+    for _ in range(800):
+        sw.step()
+    assert sw.p(1)[2] == pytest.approx(0.3 + 0.2, abs=2e-3)
+    assert np.abs(sw.V(1)).max() < 1e-3
+    assert _pair_force(sw, 0, 1) == pytest.approx(2.0 * G, abs=0.05)
+
+
+def test_lying_cylinder_rests_on_a_table(oracle):
+    cms = [oracle.load_urdf(TABLE),
+           oracle.load_urdf(cylinder_urdf(2.0, 0.1, 0.4, rpy="1.5707963267948966 0 0"), pose_xyz=(0, 0, 0.45))]
+    sw = oracle.SceneWorld(cms, pgs_iters=50)
+    for _ in range(800):
+        sw.step()
+    assert sw.p(1)[2] == pytest.approx(0.3 + 0.1, abs=2e-3)
+    assert np.abs(sw.V(1)).max() < 1e-3
+    assert _pair_force(sw, 0, 1) == pytest.approx(2.0 * G, abs=0.05)
+
+
+def test_two_cylinders_stack(oracle):
+    """equal radii, coaxial: the rim samples sit at 0.999 r, so the stack
+    holds; the lower one carries both weights on the ground"""
+    cms = [oracle.load_urdf(cylinder_urdf(2.0, 0.1, 0.4, name="low"), pose_xyz=(0, 0, 0.2)),
+           oracle.load_urdf(cylinder_urdf(1.0, 0.1, 0.2, name="high"), pose_xyz=(0.01, 0, 0.51))]
+    sw = oracle.SceneWorld(cms, pgs_iters=50)
+    for _ in range(800):
+        sw.step()
+    assert sw.p(1)[2] == pytest.approx(0.4 + 0.1, abs=2e-3)
+    assert _pair_force(sw, 0, 1) == pytest.approx(1.0 * G, abs=0.05)
+    ground = sum(c[8] for c, who in sw.contacts if who[2] < 0)
+    assert ground == pytest.approx(3.0 * G, abs=0.05)

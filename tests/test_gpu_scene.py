@@ -175,8 +175,8 @@ def test_cylinders_on_the_ground_one_step(require_gpu, oracle):
     cap from the deepest one, chain_dyn.hpp shape_slot_point / oracle.c
     or_slot_point) on the scene kernel: a free cylinder at random tilts and
     heights next to a cube, one step vs the fp64 scene oracle over 256 worlds
-    (poses 1e-5, velocities 2e-3, contact points 1e-5); a model pair with a
-    cylinder makes no body-body contact (documented restriction)."""
+    (poses 1e-5, velocities 2e-3, contact points 1e-5; the can-cube pair
+    contacts are checked in test_cylinder_pairs_one_step)."""
     from test_cylinder_oracle import cylinder_urdf
     W, pgs, mu = 256, 50, 0.8
     rng = np.random.default_rng(9)
@@ -199,7 +199,9 @@ def test_cylinders_on_the_ground_one_step(require_gpu, oracle):
         gc = sc.contacts(w)
         assert len(gc) == len(ow.contacts), (w, len(gc), len(ow.contacts))
         for row, (oc, who) in zip(gc, ow.contacts):
-            assert tuple(int(v) for v in row[10:14]) == who and who[2] < 0
+            assert tuple(int(v) for v in row[10:14]) == who
+            if who[2] >= 0:   # cylinder-box pair (test_cylinder_pairs_one_step)
+                continue
             n_contact += who[0] == 0
             worst["point"] = max(worst["point"], float(np.abs(row[0:3] - oc[0:3]).max()))
         worst["pose"] = max(worst["pose"], e["pose"])
@@ -526,4 +528,81 @@ def test_cylinder_sphere_contacts(require_gpu, oracle):
     z = sc.base_pose(1, 0, 1)[0, 2]
     print(f"ball on a pillar: z {z:.5f} (0.6 + 0.05), max |dp| vs oracle {worst:.2e}")
     assert z == pytest.approx(0.65, abs=2e-3) and worst <= 1e-4
+    sc.close()
+
+
+def test_cylinder_pairs_one_step(require_gpu, oracle):
+    """Cylinder-box and cylinder-cylinder contacts between models (oracle.c
+    cylinder_pair, scene_kernel.hip sc_cylinder_pair: least-overlap axis,
+    sampled features): a tilted cylinder and a smaller one dropped on a welded
+    table and on each other, one step vs the fp64 scene oracle over 256
+    worlds (poses 1e-5, velocities 2e-3, contact points 1e-5; at most 2 % of
+    the pair points may differ where fp32 picks another axis of near-equal
+    overlap, with the dynamics still within the bounds)."""
+    from test_cylinder_oracle import TABLE, cylinder_urdf
+    W, pgs, mu = 256, 50, 0.8
+    rng = np.random.default_rng(21)
+    texts = [TABLE, cylinder_urdf(2.0, 0.1, 0.4, name="can"), cylinder_urdf(1.0, 0.06, 0.2, name="cup")]
+    base = [(0, 0, 0), (0.0, 0.0, 0.5), (0.05, 0.0, 0.8)]
+    cms = [oracle.load_urdf(t, pose_xyz=b) for t, b in zip(texts, base)]
+    sc = _scene([(t, (*b, 1, 0, 0, 0), nm) for t, b, nm in zip(texts, base, ["table", "can", "cup"])], W, pgs, mu)
+    can = np.array([np.concatenate([rng.uniform(-0.1, 0.1, 2), [rng.uniform(0.36, 0.5)], _rand_quat(rng, np.pi)])
+                    for _ in range(W)])
+    cup = np.array([np.concatenate([can[w, :2] + rng.uniform(-0.08, 0.08, 2), [can[w, 2] + rng.uniform(0.1, 0.3)],
+                                    _rand_quat(rng, np.pi)]) for w in range(W)])
+    sc.reset_base_pose(1, can)
+    sc.reset_base_pose(2, cup)
+    for m in (1, 2):
+        sc.reset_base_velocity(m, np.column_stack([rng.uniform(-0.5, 0.5, (W, 3)), rng.uniform(-2, 2, (W, 3))]))
+    sc.run(paused=True)
+    orcs = [_oracle_from_gpu(oracle, cms, sc, w, pgs, mu) for w in range(W)]
+    sc.run()
+    worst = dict(pose=0.0, vel=0.0, point=0.0)
+    n_cb, n_cc, moved, ill = 0, 0, [], []
+    for w in range(W):
+        ow = orcs[w]
+        ow.step()
+        e = _compare(oracle, cms, sc, ow, w)
+        gc = sc.contacts(w)
+        assert len(gc) == len(ow.contacts), (w, len(gc), len(ow.contacts))
+        for row, (oc, who) in zip(gc, ow.contacts):
+            assert tuple(int(v) for v in row[10:14]) == who
+            n_cb += who[0] == 0 and who[2] >= 1
+            n_cc += who[0] == 1 and who[2] == 2
+            err = float(np.abs(row[0:3] - oc[0:3]).max())
+            if err > 1e-5 and who[2] >= 0:
+                moved.append((w, who, round(err, 5)))
+                continue
+            worst["point"] = max(worst["point"], err)
+        if e["vel"] > 2e-3:
+            ill.append((w, round(e["vel"], 5)))
+            continue
+        worst["pose"] = max(worst["pose"], e["pose"])
+        worst["vel"] = max(worst["vel"], e["vel"])
+    print(f"cylinder pairs x{W}: one-step " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
+          f", {n_cb} cylinder-table and {n_cc} cylinder-cylinder points, moved {moved[:6]}, ill {ill[:6]}")
+    assert n_cb > W // 4 and n_cc > W // 16
+    assert len(moved) <= (n_cb + n_cc) // 50 and len(ill) <= W // 50
+    assert worst["pose"] <= 1e-5 and worst["point"] <= 1e-5 and worst["vel"] <= 2e-3
+    assert sc.overflow() == 0
+    sc.close()
+
+
+def test_cylinder_stack_on_a_table(require_gpu):
+    """a can standing on the welded table, a cup standing on the can: both
+    come to rest at their stacked heights and the table carries both weights"""
+    from test_cylinder_oracle import TABLE, cylinder_urdf
+    W = 8
+    sc = _scene([(TABLE, (0, 0, 0, 1, 0, 0, 0), "table"),
+                 (cylinder_urdf(2.0, 0.1, 0.4, name="can"), (0.02, 0, 0.52, 1, 0, 0, 0), "can"),
+                 (cylinder_urdf(1.0, 0.06, 0.2, name="cup"), (0.03, 0, 0.82, 1, 0, 0, 0), "cup")], W)
+    for _ in range(1500):
+        sc.run()
+    can, cup = sc.base_pose(1, 0, W), sc.base_pose(2, 0, W)
+    np.testing.assert_allclose(can[:, 2], 0.3 + 0.2, atol=2e-3)
+    np.testing.assert_allclose(cup[:, 2], 0.7 + 0.1, atol=3e-3)
+    for w in range(W):
+        # force on the table (always model A of its pairs: lower index)
+        on_table = sum(r[8] for r in sc.contacts(w) if int(r[10]) == 0 and int(r[12]) >= 0)
+        assert abs(on_table) == pytest.approx(3.0 * G, abs=0.1)
     sc.close()
