@@ -11,9 +11,9 @@
 // The shape frame is the mesh frame moved to the bounding box centre, so the
 // box half extents are Shape::size and the points are relative to the centre.
 //
-// Formats: STL (binary and ASCII) and Wavefront OBJ (`v` records).  Other
-// formats (COLLADA, ...) throw: a collision that cannot be modelled fails
-// loudly instead of silently dropping contacts.
+// Formats: STL (binary and ASCII), Wavefront OBJ (`v` records) and COLLADA
+// (model.cpp dae_vertices).  Other formats throw: a collision that cannot be
+// modelled fails loudly instead of silently dropping contacts.
 
 #include <array>
 #include <cmath>
@@ -107,10 +107,11 @@ bool exists(const std::string& p) {
 }  // namespace
 
 std::vector<std::array<double, 3>> load_mesh_vertices(const std::string& path) {
-    const bool stl = ends_with_ci(path, ".stl"), obj = ends_with_ci(path, ".obj");
-    if (!stl && !obj) throw std::runtime_error("mesh '" + path + "': only STL and OBJ collision meshes are supported");
+    const bool stl = ends_with_ci(path, ".stl"), obj = ends_with_ci(path, ".obj"), dae = ends_with_ci(path, ".dae");
+    if (!stl && !obj && !dae)
+        throw std::runtime_error("mesh '" + path + "': only STL, OBJ and COLLADA collision meshes are supported");
     const std::string data = read_file(path);
-    const std::vector<V3> v = stl ? stl_vertices(path, data) : obj_vertices(path, data);
+    const std::vector<V3> v = stl ? stl_vertices(path, data) : obj ? obj_vertices(path, data) : dae_vertices(path, data);
     if (v.empty()) throw std::runtime_error("mesh '" + path + "' has no vertices");
     return v;
 }

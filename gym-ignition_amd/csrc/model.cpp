@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <memory>
 #include <sstream>
@@ -809,6 +810,109 @@ ChainModel compile_description(Description D) {
 }
 
 }  // namespace
+
+// COLLADA (.dae) collision meshes, as ign-common's ColladaLoader reads them
+// for MeshManager::Load (Physics.cpp:905): the POSITION sources of the
+// geometries instantiated by the visual scene's nodes (<instance_geometry>),
+// each under its node chain's transform (<matrix> row-major, <translate>,
+// <rotate> axis + degrees, <scale>, composed in document order), scaled by
+// <asset><unit meter>; without instantiating nodes, every geometry as stored.
+// <up_axis> is not applied (vertices stay in the file's frame).
+std::vector<std::array<double, 3>> dae_vertices(const std::string& path, const std::string& data) {
+    XmlReader rd(data);
+    auto root = rd.parse();
+    if (root->tag != "COLLADA") throw std::runtime_error("mesh '" + path + "' is not a COLLADA document");
+    double unit = 1.0;
+    if (const XNode* as = root->child("asset"))
+        if (const XNode* u = as->child("unit")) unit = num_attr(u, "meter", 1.0);
+    std::vector<std::pair<std::string, std::vector<V3>>> geoms;
+    if (const XNode* lg = root->child("library_geometries"))
+        for (const XNode* g : lg->children("geometry")) {
+            const XNode* me = g->child("mesh");
+            const XNode* vt = me ? me->child("vertices") : nullptr;
+            if (!vt) continue;
+            std::string src;
+            for (const XNode* in : vt->children("input"))
+                if (in->get("semantic") && *in->get("semantic") == "POSITION" && in->get("source"))
+                    src = in->get("source")->substr(1);
+            std::vector<V3> v;
+            for (const XNode* so : me->children("source")) {
+                if (!so->get("id") || *so->get("id") != src) continue;
+                const XNode* fa = so->child("float_array");
+                if (!fa) continue;
+                int stride = 3;
+                if (const XNode* tc = so->child("technique_common"))
+                    if (const XNode* ac = tc->child("accessor")) stride = static_cast<int>(num_attr(ac, "stride", 3));
+                if (stride < 3) throw std::runtime_error("mesh '" + path + "': POSITION stride below 3");
+                const std::vector<double> f = numbers(fa->text);
+                for (size_t k = 0; k + 2 < f.size(); k += stride) v.push_back({f[k], f[k + 1], f[k + 2]});
+            }
+            geoms.push_back({g->get("id") ? *g->get("id") : std::string(), v});
+        }
+    using M4 = std::array<double, 16>;
+    auto mul4 = [](const M4& a, const M4& b) {
+        M4 c{};
+        for (int r = 0; r < 4; ++r)
+            for (int k = 0; k < 4; ++k)
+                c[r * 4 + k] = a[r * 4] * b[k] + a[r * 4 + 1] * b[4 + k] + a[r * 4 + 2] * b[8 + k] + a[r * 4 + 3] * b[12 + k];
+        return c;
+    };
+    const M4 I4 = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    std::vector<V3> out;
+    bool instanced = false;
+    std::function<void(const XNode*, M4)> walk = [&](const XNode* nd, M4 M) {
+        for (const auto& k : nd->kids) {
+            const std::vector<double> f = numbers(k->text);
+            M4 T = I4;
+            if (k->tag == "matrix" && f.size() == 16) {
+                for (int i = 0; i < 16; ++i) T[i] = f[i];
+            } else if (k->tag == "translate" && f.size() == 3) {
+                T[3] = f[0]; T[7] = f[1]; T[11] = f[2];
+            } else if (k->tag == "scale" && f.size() == 3) {
+                T[0] = f[0]; T[5] = f[1]; T[10] = f[2];
+            } else if (k->tag == "rotate" && f.size() == 4) {
+                const double n = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+                const double x = f[0] / n, y = f[1] / n, z = f[2] / n, a = f[3] * M_PI / 180.0;
+                const double c = std::cos(a), s = std::sin(a), t = 1.0 - c;
+                T = {t * x * x + c, t * x * y - s * z, t * x * z + s * y, 0, t * x * y + s * z, t * y * y + c,
+                     t * y * z - s * x, 0, t * x * z - s * y, t * y * z + s * x, t * z * z + c, 0, 0, 0, 0, 1};
+            } else {
+                continue;
+            }
+            M = mul4(M, T);
+        }
+        for (const XNode* ig : nd->children("instance_geometry")) {
+            const std::string* url = ig->get("url");
+            if (!url || url->empty()) continue;
+            for (const auto& g : geoms)
+                if (g.first == url->substr(1)) {
+                    instanced = true;
+                    for (const V3& p : g.second)
+                        out.push_back({M[0] * p[0] + M[1] * p[1] + M[2] * p[2] + M[3],
+                                       M[4] * p[0] + M[5] * p[1] + M[6] * p[2] + M[7],
+                                       M[8] * p[0] + M[9] * p[1] + M[10] * p[2] + M[11]});
+                }
+        }
+        for (const XNode* ch : nd->children("node")) walk(ch, M);
+    };
+    const XNode* vs = nullptr;
+    if (const XNode* lv = root->child("library_visual_scenes")) {
+        std::string want;
+        if (const XNode* sc = root->child("scene"))
+            if (const XNode* iv = sc->child("instance_visual_scene"))
+                if (iv->get("url")) want = iv->get("url")->substr(1);
+        for (const XNode* v : lv->children("visual_scene"))
+            if (!vs || (v->get("id") && *v->get("id") == want)) vs = v;
+    }
+    if (vs) walk(vs, I4);
+    if (!instanced) {
+        out.clear();
+        for (const auto& g : geoms) out.insert(out.end(), g.second.begin(), g.second.end());
+    }
+    for (V3& p : out)
+        for (double& x : p) x *= unit;
+    return out;
+}
 
 ChainModel compile_urdf(const std::string& path_or_xml, const double pose[7]) {
     const std::string text = read_source(path_or_xml);

@@ -57,6 +57,8 @@ struct Shape {
 // mesh.cpp: vertices of an STL / OBJ file; URI -> file path (the reference's
 // asFullPath); the Mesh shape of scaled vertices under collision pose (R, p).
 std::vector<std::array<double, 3>> load_mesh_vertices(const std::string& path);
+// model.cpp (it owns the XML reader): vertices of a COLLADA document
+std::vector<std::array<double, 3>> dae_vertices(const std::string& path, const std::string& data);
 std::string resolve_mesh_uri(const std::string& uri, const std::string& model_dir);
 Shape mesh_shape(const std::vector<std::array<double, 3>>& verts, const std::array<double, 3>& scale,
                  const std::array<double, 9>& R, const std::array<double, 3>& p);

@@ -477,14 +477,92 @@ def mesh_vertices(path: str) -> np.ndarray:
         toks = data.decode("ascii", "replace").split()
         v = [[float(toks[i + 1]), float(toks[i + 2]), float(toks[i + 3])]
              for i, t in enumerate(toks) if t == "vertex"]
+    elif low.endswith(".dae"):
+        v = _dae_vertices(path, data)
     elif low.endswith(".obj"):
         v = [[float(x) for x in ln.split()[1:4]] for ln in data.decode("ascii", "replace").splitlines()
              if ln.startswith(("v ", "v\t"))]
     else:
-        raise ValueError(f"mesh '{path}': only STL and OBJ collision meshes are supported")
+        raise ValueError(f"mesh '{path}': only STL, OBJ and COLLADA collision meshes are supported")
     if not v:
         raise ValueError(f"mesh '{path}' has no vertices")
     return np.array(v, dtype=float)
+
+
+def _dae_vertices(path: str, data: bytes) -> list:
+    """COLLADA as ign-common's ColladaLoader reads it for MeshManager::Load:
+    POSITION sources of the geometries the visual scene's nodes instantiate,
+    under the node chains' transforms (matrix / translate / rotate in degrees /
+    scale, in document order), times <unit meter>; no instancing node: every
+    geometry as stored; <up_axis> not applied."""
+    root = ET.fromstring(data)
+    for el in root.iter():
+        el.tag = el.tag.split("}", 1)[-1]
+    unit = root.find("asset/unit")
+    unit = float(unit.get("meter", "1")) if unit is not None else 1.0
+    geoms = []
+    for g in root.findall("library_geometries/geometry"):
+        me = g.find("mesh")
+        vt = me.find("vertices") if me is not None else None
+        if vt is None:
+            continue
+        src = ""
+        for i in vt.findall("input"):
+            if i.get("semantic") == "POSITION" and i.get("source"):
+                src = i.get("source")[1:]
+        pts = []
+        for so in me.findall("source"):
+            fa = so.find("float_array")
+            if so.get("id") != src or fa is None:
+                continue
+            ac = so.find("technique_common/accessor")
+            stride = int(float(ac.get("stride", "3"))) if ac is not None else 3
+            f = [float(x) for x in (fa.text or "").split()]
+            pts += [f[k:k + 3] for k in range(0, len(f) - 2, stride)]
+        geoms.append((g.get("id", ""), pts))
+    out, inst = [], [False]
+
+    def walk(nd, M):
+        for k in nd:
+            f = [float(x) for x in (k.text or "").split()]
+            T = np.eye(4)
+            if k.tag == "matrix" and len(f) == 16:
+                T = np.array(f).reshape(4, 4)
+            elif k.tag == "translate" and len(f) == 3:
+                T[:3, 3] = f
+            elif k.tag == "scale" and len(f) == 3:
+                T[0, 0], T[1, 1], T[2, 2] = f
+            elif k.tag == "rotate" and len(f) == 4:
+                n = math.sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2])
+                x, y, z, a = f[0] / n, f[1] / n, f[2] / n, f[3] * math.pi / 180.0
+                c, s_, t = math.cos(a), math.sin(a), 1.0 - math.cos(a)
+                T[:3, :3] = [[t * x * x + c, t * x * y - s_ * z, t * x * z + s_ * y],
+                             [t * x * y + s_ * z, t * y * y + c, t * y * z - s_ * x],
+                             [t * x * z - s_ * y, t * y * z + s_ * x, t * z * z + c]]
+            else:
+                continue
+            M = M @ T
+        for ig in nd.findall("instance_geometry"):
+            url = ig.get("url", "")
+            for gid, pts in geoms:
+                if url and gid == url[1:]:
+                    inst[0] = True
+                    out.extend((M[:3, :3] @ np.array(p) + M[:3, 3]).tolist() for p in pts)
+        for ch in nd.findall("node"):
+            walk(ch, M)
+
+    scenes = root.findall("library_visual_scenes/visual_scene")
+    want = root.find("scene/instance_visual_scene")
+    want = want.get("url", "")[1:] if want is not None else ""
+    vs = None
+    for v in scenes:
+        if vs is None or v.get("id") == want:
+            vs = v
+    if vs is not None:
+        walk(vs, np.eye(4))
+    if not inst[0]:
+        out = [p for _, pts in geoms for p in pts]
+    return [[x * unit for x in p] for p in out]
 
 
 def resolve_mesh_uri(uri: str, model_dir: str = "") -> str:

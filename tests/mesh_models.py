@@ -86,3 +86,28 @@ def mesh_body_sdf(uri, mass=2.0, half=(0.1, 0.1, 0.1), scale=(1, 1, 1), pose="0 
             f'<collision name="c"><pose>{pose}</pose><geometry><mesh><uri>{uri}</uri>'
             f'<scale>{scale[0]} {scale[1]} {scale[2]}</scale></mesh></geometry></collision>'
             f'</link></model></sdf>')
+
+
+def write_dae(path, geoms, nodes, unit=1.0, extra_geom=None):
+    """COLLADA fixture: geoms = {id: [V, 3] positions}; nodes = list of
+    (transform elements xml, [geometry ids], [child nodes]) instantiated by the
+    visual scene; extra_geom = an id of geoms left un-instantiated"""
+    def node_xml(n):
+        tr, gids, kids = n
+        return ("<node>" + tr + "".join(f'<instance_geometry url="#{g}"/>' for g in gids) +
+                "".join(node_xml(k) for k in kids) + "</node>")
+    lib = ""
+    for gid, v in geoms.items():
+        arr = " ".join(repr(float(x)) for x in np.asarray(v).reshape(-1))
+        lib += (f'<geometry id="{gid}"><mesh><source id="{gid}-pos"><float_array id="{gid}-arr" count="{v.size}">'
+                f'{arr}</float_array><technique_common><accessor source="#{gid}-arr" count="{len(v)}" stride="3">'
+                f'<param name="X" type="float"/><param name="Y" type="float"/><param name="Z" type="float"/>'
+                f'</accessor></technique_common></source><vertices id="{gid}-vtx"><input semantic="POSITION" '
+                f'source="#{gid}-pos"/></vertices></mesh></geometry>')
+    text = ('<?xml version="1.0" encoding="utf-8"?>\n<COLLADA xmlns="http://www.collada.org/2005/11/COLLADASchema" '
+            f'version="1.4.1"><asset><unit name="u" meter="{unit!r}"/><up_axis>Z_UP</up_axis></asset>'
+            f'<library_geometries>{lib}</library_geometries><library_visual_scenes><visual_scene id="scene">'
+            + "".join(node_xml(n) for n in nodes) +
+            '</visual_scene></library_visual_scenes><scene><instance_visual_scene url="#scene"/></scene></COLLADA>')
+    with open(path, "w") as fh:
+        fh.write(text)

@@ -5,7 +5,7 @@ side:
   * the model compiler (gym-ignition_amd/csrc/mesh.cpp via mw_compile_collisions)
     and the oracle's independent numpy restatement (pyoracle.mesh_shape) give
     the same shape: bounding box, pose, support points -- for binary STL, ASCII
-    STL and OBJ files, URDF and SDF front-ends, scales and collision poses,
+    STL, OBJ and COLLADA files (node transforms, units), URDF and SDF front-ends, scales and collision poses,
     relative / file:// / model:// URIs;
   * a box-shaped mesh IS the box: its support points are the 8 corners in the
     box's slot order, so a scene with the mesh cube steps bit-identically to
@@ -130,7 +130,7 @@ def test_relative_and_model_uris(N, oracle, tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("text,needle", [
     (mesh_body_urdf("/nonexistent/rock.stl"), "cannot open mesh"),
-    (mesh_body_urdf("/tmp/rock.dae"), "STL and OBJ"),
+    (mesh_body_urdf("/tmp/rock.ply"), "STL, OBJ and COLLADA"),
     (mesh_body_urdf("model://nowhere/rock.stl"), "cannot resolve"),
 ])
 def test_bad_meshes_fail_loudly(N, text, needle):
@@ -216,3 +216,38 @@ def test_mesh_body_rests_on_a_box_of_another_model(oracle, tmp_path):
     assert sw.p(1)[2] == pytest.approx(0.35 + 0.05, abs=2e-3)
     fz = sum(c[8] for c, who in sw.contacts if who[2] == 1 or who[0] == 1)
     assert abs(fz) == pytest.approx(1.0 * G, abs=0.1)
+
+
+def test_collada_meshes(N, oracle, tmp_path):
+    """COLLADA: the instanced geometries under their node transforms (matrix,
+    translate, rotate, scale; nested nodes), times <unit meter>; a geometry no
+    node instantiates is ignored.  Exact-arithmetic case checked against a
+    hand-computed box, rotated rock case C++ == oracle."""
+    from mesh_models import write_dae
+    cube = cube_vertices((2.0, 2.0, 2.0))
+    far = cube + 100.0                                   # not instantiated
+    perm = "<matrix>0 1 0 1 0 0 1 0 1 0 0 2 0 0 0 1</matrix>"   # x' = y + 1, y' = z, z' = x + 2
+    path = str(tmp_path / "cube.dae")
+    write_dae(path, {"cube": cube, "far": far}, [(perm, ["cube"], [])], unit=0.0625)
+    rc, got = _collisions(N, mesh_body_urdf(path))
+    assert rc == 0, got
+    assert int(got[0, 1]) == 3 and int(got[0, 17]) == 8
+    np.testing.assert_array_equal(got[0, 2:5], [0.125, 0.125, 0.125])
+    np.testing.assert_array_equal(got[0, 14:17], [0.0625, 0.0, 0.125])   # box centre (mesh frame)
+    _check_against_oracle(got, oracle.load_urdf(mesh_body_urdf(path)), tol=0.0)
+    # the same box as STL gives the same shape
+    stl = str(tmp_path / "cube.stl")
+    write_stl_binary(stl, cube_vertices((0.125,) * 3) + [0.0625, 0.0, 0.125], CUBE_TRIS)
+    rc, ref = _collisions(N, mesh_body_urdf(stl))
+    np.testing.assert_array_equal(got[0, 2:17], ref[0, 2:17])
+    # nested nodes with translate / rotate / scale, a rock instanced twice
+    v, f = rock_vertices(3)
+    nodes = [("<translate>0.5 0 0</translate><rotate>0 0 1 30</rotate>", ["rock"],
+              [("<scale>1 2 1</scale><translate>0 0 0.25</translate>", ["rock"], [])])]
+    path = str(tmp_path / "rock.dae")
+    write_dae(path, {"rock": v}, nodes, unit=1.0)
+    text = mesh_body_urdf(path, scale=(1.0, 0.5, 2.0))
+    rc, got = _collisions(N, text)
+    assert rc == 0, got
+    _check_against_oracle(got, oracle.load_urdf(text), tol=1e-12)
+    assert int(got[0, 17]) >= 8
