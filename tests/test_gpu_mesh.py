@@ -11,8 +11,9 @@ restatement), and through the ScenarI/O mirror:
     tolerances of test_gpu_scene.py; at most 1 % of the pair points may come
     from another box-box clipping feature at deep overlaps, same normal);
   * a box-shaped mesh steps bit-identically to the box on the GPU too;
-  * World.insert_model of a URDF file whose mesh URI is relative to the file:
-    the rock falls, comes to rest, and its contact wrench carries its weight.
+  * World.insert_model of a URDF file whose mesh URI (OBJ, COLLADA) is
+    relative to the file: the rock falls, comes to rest, and its contact
+    wrench carries its weight.
 """
 
 import numpy as np
@@ -106,15 +107,21 @@ def test_box_mesh_equals_box_on_gpu(require_gpu, tmp_path):
         np.testing.assert_array_equal(a, b)
 
 
-def test_scenario_rock_from_file_rests_on_the_ground(require_gpu, tmp_path):
+@pytest.mark.parametrize("fmt", ["obj", "dae"])
+def test_scenario_rock_from_file_rests_on_the_ground(require_gpu, tmp_path, fmt):
     from scenario import core
     from scenario import gazebo as scenario
     from mwstep import get_model_file
+    from mesh_models import write_dae
     v, f = rock_vertices(4)
     (tmp_path / "meshes").mkdir()
-    write_obj(str(tmp_path / "meshes" / "rock.obj"), v, f)
+    if fmt == "obj":
+        write_obj(str(tmp_path / "meshes" / "rock.obj"), v, f)
+    else:   # the same rock in centimetres under a node translation
+        write_dae(str(tmp_path / "meshes" / "rock.dae"), {"rock": 100.0 * v},
+                  [("<translate>0 0 1</translate>", ["rock"], [])], unit=0.01)
     model_file = tmp_path / "rock.urdf"
-    model_file.write_text(mesh_body_urdf("meshes/rock.obj", mass=3.0, half=(0.12, 0.08, 0.06)))
+    model_file.write_text(mesh_body_urdf(f"meshes/rock.{fmt}", mass=3.0, half=(0.12, 0.08, 0.06)))
     gazebo = scenario.GazeboSimulator(0.001, 1.0, 1)
     assert gazebo.initialize()
     world = gazebo.get_world().to_gazebo()
