@@ -5,8 +5,10 @@
 // resolved URI, AttachMeshShape with the collision pose and the SDF <scale>).
 // Here a mesh becomes a Shape::Mesh: its contact points against the ground
 // plane are support points of its vertex set (the vertices extreme along 26
-// fixed directions, at most kMeshMaxPoints of them -- every one a vertex of the
-// convex hull; a box-shaped mesh gives exactly its 8 corners), and against the
+// fixed directions, then along 136 Fibonacci-sphere directions while fewer
+// than kMeshMaxPoints were found -- every one a vertex of the convex hull; a
+// box-shaped mesh gives exactly its 8 corners, a mesh of at most 16 hull
+// vertices all of them), and against the
 // shapes of other models it collides as its bounding box in the mesh frame.
 // The shape frame is the mesh frame moved to the bounding box centre, so the
 // box half extents are Shape::size and the points are relative to the centre.
@@ -196,6 +198,23 @@ Shape mesh_shape(const std::vector<std::array<double, 3>>& verts, const std::arr
         bool seen = false;
         for (size_t j : pick) seen = seen || j == best;
         if (!seen && pick.size() < static_cast<size_t>(kMeshMaxPoints)) pick.push_back(best);
+    }
+    // room left: the extremes along 136 Fibonacci-sphere directions (a mesh
+    // with at most 16 hull vertices ends up with all of them)
+    const double golden = M_PI * (3.0 - std::sqrt(5.0));
+    for (int k = 0; k < 136 && pick.size() < static_cast<size_t>(kMeshMaxPoints); ++k) {
+        const double z = 1.0 - (2.0 * k + 1.0) / 136.0;
+        const double r = std::sqrt(1.0 - z * z), phi = golden * k;
+        const double d[3] = {r * std::cos(phi), r * std::sin(phi), z};
+        size_t best = 0;
+        double bv = d[0] * v[0][0] + d[1] * v[0][1] + d[2] * v[0][2];
+        for (size_t i = 1; i < v.size(); ++i) {
+            const double s = d[0] * v[i][0] + d[1] * v[i][1] + d[2] * v[i][2];
+            if (s > bv) { bv = s; best = i; }
+        }
+        bool seen = false;
+        for (size_t j : pick) seen = seen || j == best;
+        if (!seen) pick.push_back(best);
     }
     for (size_t i : pick) sh.points.push_back({v[i][0] - c[0], v[i][1] - c[1], v[i][2] - c[2]});
     return sh;

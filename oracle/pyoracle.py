@@ -453,7 +453,8 @@ def _rot_to_quat(R: np.ndarray):
 # collision pose and the SDF <scale>): restated independently of the model
 # compiler's csrc/mesh.cpp -- STL (binary / ASCII) and OBJ vertices, the
 # support points along 26 fixed directions (8 cube corners, 12 edges, 6 faces;
-# the first vertex of the maximum; at most OR_MESH_MAXP distinct ones) and the
+# the first vertex of the maximum), then along 136 Fibonacci-sphere directions
+# while fewer than OR_MESH_MAXP distinct ones were found, and the
 # bounding box in the mesh frame (the shape frame is moved to its centre).
 # --------------------------------------------------------------------------
 _MESH_DIRS = np.array([(-1, -1, -1), (-1, -1, 1), (-1, 1, -1), (-1, 1, 1), (1, -1, -1), (1, -1, 1), (1, 1, -1),
@@ -594,6 +595,16 @@ def mesh_shape(verts, scale, SR, sp):
     for d in _MESH_DIRS:
         i = int(np.argmax(d[0] * v[:, 0] + d[1] * v[:, 1] + d[2] * v[:, 2]))
         if i not in pick and len(pick) < OR_MESH_MAXP:
+            pick.append(i)
+    golden = math.pi * (3.0 - math.sqrt(5.0))
+    for k in range(136):   # room left: Fibonacci-sphere directions
+        if len(pick) >= OR_MESH_MAXP:
+            break
+        z = 1.0 - (2.0 * k + 1.0) / 136.0
+        r, phi = math.sqrt(1.0 - z * z), golden * k
+        d = (r * math.cos(phi), r * math.sin(phi), z)
+        i = int(np.argmax(d[0] * v[:, 0] + d[1] * v[:, 1] + d[2] * v[:, 2]))
+        if i not in pick:
             pick.append(i)
     pts = v[pick] - c
     return (3, np.concatenate([half, pts.reshape(-1)]), SR, np.asarray(sp, dtype=float) + SR @ c)

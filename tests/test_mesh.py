@@ -97,7 +97,7 @@ def test_compiler_matches_oracle_restatement(N, oracle, tmp_path, seed):
         assert rc == 0, got
         cm = oracle.load_urdf(text)
         _check_against_oracle(got, cm)
-        assert 6 <= int(got[0, 17]) <= 16
+        assert int(got[0, 17]) == 12   # every hull vertex of the 12-vertex rock
         # every support point is a (scaled) vertex of the mesh
         pts = got[0, 18:18 + 3 * int(got[0, 17])].reshape(-1, 3) + (
             np.asarray(got[0, 14:17]) - np.asarray(xyz)) @ oracle._rpy(rpy)   # back to the mesh frame
