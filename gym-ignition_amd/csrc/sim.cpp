@@ -563,23 +563,41 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     } catch (const std::exception& e) {
         return fail(MW_EPARSE, e.what());
     }
-    // mesh collisions are modelled by the scene kernel (scene.cpp); the
-    // single-model kernels keep box / sphere / cylinder shapes.  A floating
-    // model would fall through the ground without its mesh: refuse it.
+    // Mesh collisions (scene.cpp models them as ground slots at their support
+    // points).  Articulated floating models: every support point becomes a
+    // zero-radius sphere at that point (the same ground contact: normal +z,
+    // depth -z, in slot order).  Fixed bases never touch the ground here: their
+    // meshes are dropped (counted).  A joint-less floating body (free-body
+    // kernel, <= 2 shapes) with a mesh is refused: insert it into a scene.
     {
         int meshes = 0;
-        auto strip = [&](std::vector<mw::Shape>& v) {
-            const size_t n0 = v.size();
-            v.erase(std::remove_if(v.begin(), v.end(), [](const mw::Shape& sh) { return sh.type == mw::Shape::Mesh; }),
-                    v.end());
-            meshes += static_cast<int>(n0 - v.size());
+        const bool expand = s->model.floating && s->model.dofs() > 0;
+        auto convert = [&](std::vector<mw::Shape>& v) {
+            std::vector<mw::Shape> out;
+            for (const mw::Shape& sh : v) {
+                if (sh.type != mw::Shape::Mesh) {
+                    out.push_back(sh);
+                    continue;
+                }
+                ++meshes;
+                if (!expand) continue;
+                for (const auto& pt : sh.points) {
+                    mw::Shape sp;
+                    sp.type = mw::Shape::Sphere;
+                    sp.R = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+                    for (int r = 0; r < 3; ++r)
+                        sp.p[r] = sh.p[r] + sh.R[3 * r] * pt[0] + sh.R[3 * r + 1] * pt[1] + sh.R[3 * r + 2] * pt[2];
+                    out.push_back(sp);
+                }
+            }
+            v.swap(out);
         };
-        strip(s->model.base_shapes);
-        for (auto& b : s->model.bodies) strip(b.shapes);
-        if (meshes && s->model.floating)
-            return fail(MW_EPARSE, "mesh collisions on a floating model are supported in scenes (mw_scene / the "
+        convert(s->model.base_shapes);
+        for (auto& b : s->model.bodies) convert(b.shapes);
+        if (meshes && s->model.floating && !expand)
+            return fail(MW_EPARSE, "a joint-less floating body with a mesh collision runs in scenes (mw_scene / the "
                                    "ScenarI/O World.insert_model), not on mw_sim");
-        s->model.unsupported_shapes += meshes;
+        if (!expand) s->model.unsupported_shapes += meshes;
     }
     if (s->model.dofs() > mw::kMaxBodies)
         return fail(MW_EPARSE, "models with more than " + std::to_string(mw::kMaxBodies) +

@@ -994,6 +994,20 @@ class FreeWorld:
         return nc
 
 
+def _mesh_points_as_spheres(shapes):
+    """(body, type, size, R, p) list with every mesh replaced by zero-radius
+    spheres at its support points (mw_sim's articulated floating models: the
+    same ground contacts as the scene's mesh slots)"""
+    out = []
+    for (b, t, sz, SR, sp) in shapes:
+        if t != 3:
+            out.append((b, t, sz, SR, sp))
+            continue
+        for pt in np.asarray(sz[3:]).reshape(-1, 3):
+            out.append((b, 1, np.zeros(3), np.eye(3), np.asarray(sp, dtype=float) + np.asarray(SR) @ pt))
+    return out
+
+
 class FloatWorld:
     """fp64 articulated floating-base model on the ground plane (or_float_step):
     DART FreeJoint root + the joint tree, dense CRBA/RNEA dynamics, contact
@@ -1012,9 +1026,7 @@ class FloatWorld:
             m.gravity[k] = F.gravity[k]
         for k in range(6):
             m.base_Ic[k] = F.Ic[k]
-        shapes = [(-1, F.shape_type[i], np.array(F.shape_size[i][:]), np.array(F.shape_R[i][:]).reshape(3, 3),
-                   np.array(F.shape_p[i][:])) for i in range(F.n_shapes)] + [
-                       sh for sh in cm.body_shapes if sh[1] != 3]   # meshes: scenes only (SceneWorld)
+        shapes = _mesh_points_as_spheres([(-1, *sh) for sh in cm.base_shapes] + list(cm.body_shapes))
         assert len(shapes) <= OR_MAXFS
         m.n_shapes = len(shapes)
         for i, (b, t, sz, SR, sp) in enumerate(shapes):

@@ -35,9 +35,10 @@ def quad_file():
 STAND = np.array([0.6, -1.2] * 4)
 
 
-def chain_urdf(n=2, floating=True, cylinder_tip=False):
+def chain_urdf(n=2, floating=True, cylinder_tip=False, mesh_tip=None):
     """A floating box base with an n-link revolute chain (links: 0.3 m rods,
-    alternating y / x axes), a sphere (or a tilted cylinder) at the tip."""
+    alternating y / x axes), a sphere (or a tilted cylinder, or the mesh file
+    mesh_tip, tilted) at the tip."""
     links = ['<link name="base"><inertial><mass value="3.0"/>'
              '<inertia ixx="0.02" iyy="0.03" izz="0.04" ixy="0.001" ixz="0" iyz="0"/></inertial>'
              '<collision><geometry><box size="0.3 0.2 0.1"/></geometry></collision></link>']
@@ -50,6 +51,8 @@ def chain_urdf(n=2, floating=True, cylinder_tip=False):
         z = "-0.05" if i == 0 else "-0.3"
         geo = ('<origin xyz="0 0 -0.3" rpy="0.4 1.1 0"/><geometry><cylinder radius="0.04" length="0.12"/>'
                '</geometry>' if cylinder_tip else
+               f'<origin xyz="0 0 -0.3" rpy="0.3 -0.5 0.2"/><geometry><mesh filename="{mesh_tip}" scale="0.5 0.5 0.5"/>'
+               '</geometry>' if mesh_tip else
                '<origin xyz="0 0 -0.3"/><geometry><sphere radius="0.04"/></geometry>')
         tip = f'<collision>{geo}</collision>' if i == n - 1 else ""
         links.append(f'<joint name="j{i}" type="revolute"><parent link="{parent}"/><child link="l{i}"/>'

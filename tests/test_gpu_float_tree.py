@@ -20,6 +20,8 @@ quadruped, models/quadruped.urdf, and floating serial chains of 1..3 joints).
   * mw_run_device (no readback, graph-capturable) equals repeated mw_run.
 """
 
+import os
+
 import numpy as np
 import pytest
 
@@ -95,6 +97,12 @@ def _model(name):
         return tree_urdf(cylinders=True)
     if name.endswith("c"):
         return chain_urdf(int(name[-2]), cylinder_tip=True)
+    if name.endswith("m"):  # a mesh (the 12-vertex rock) at the tip: zero-radius spheres at its support points
+        import tempfile
+        from mesh_models import rock_vertices, write_obj
+        path = os.path.join(tempfile.mkdtemp(), "rock.obj")
+        write_obj(path, *rock_vertices(6))
+        return chain_urdf(int(name[-2]), mesh_tip=path)
     return chain_urdf(int(name[-1]))
 
 
@@ -123,7 +131,8 @@ def _random_states(cm, W, rng):
 @pytest.mark.parametrize("name, kernel", [("quadruped", "lane"), ("chain1", "lane"), ("chain2", "lane"),
                                           ("chain3", "lane"), ("quadruped", "wave"), ("chain2", "wave"),
                                           ("humanoid32", "wave"), ("tree16", "wave"), ("tree16d", "wave"),
-                                          ("chain2c", "lane"), ("chain2c", "wave"), ("tree16c", "wave")])
+                                          ("chain2c", "lane"), ("chain2c", "wave"), ("tree16c", "wave"),
+                                          ("chain2m", "lane"), ("chain2m", "wave")])
 def test_one_step_parity_with_contacts(require_gpu, oracle, monkeypatch, name, kernel):
     from mwstep import native as N
     from mwstep.sim import Simulator
