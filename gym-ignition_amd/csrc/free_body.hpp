@@ -36,10 +36,12 @@ struct FreeF {
     float mu;             // Coulomb friction with the ground
     int32_t n_shapes;
     int32_t ground;       // ground plane z = 0 present
-    int32_t shape_type[kMaxFreeShapes];  // 0 box, 1 sphere
+    int32_t shape_type[kMaxFreeShapes];  // 0 box, 1 sphere, 2 cylinder, 3 mesh points
     float shape_size[kMaxFreeShapes][3]; // box half extents / sphere radius
     float shape_R[kMaxFreeShapes][9];
     float shape_p[kMaxFreeShapes][3];
+    int32_t mesh_npts[kMaxFreeShapes];   // type 3: support points (<= 8, one per slot)
+    float mesh_pt[kMaxFreeShapes][8][3]; // in the shape frame
 };
 
 namespace dev {
@@ -113,7 +115,8 @@ __device__ __forceinline__ SV minv_mul(const FreeF& __restrict__ F, const SV& x)
 // cylinder: rim point k, chain_dyn.hpp shape_slot_point) for body rotation Rb
 __device__ __forceinline__ f3 slot_point(const FreeF& F, int s, int k, const M3& Rb) {
     const float* R = F.shape_R[s];
-    const f3 l = shape_slot_point(F.shape_type[s], F.shape_size[s], shape_plane_normal(Rb, R), k);
+    const f3 l = (F.shape_type[s] == 3) ? mk(F.mesh_pt[s][k][0], F.mesh_pt[s][k][1], F.mesh_pt[s][k][2])
+                                        : shape_slot_point(F.shape_type[s], F.shape_size[s], shape_plane_normal(Rb, R), k);
     return {F.shape_p[s][0] + R[0] * l.x + R[1] * l.y + R[2] * l.z,
             F.shape_p[s][1] + R[3] * l.x + R[4] * l.y + R[5] * l.z,
             F.shape_p[s][2] + R[6] * l.x + R[7] * l.y + R[8] * l.z};
@@ -164,9 +167,10 @@ __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt
         for (int s = 0; s < kMaxFreeShapes; ++s) {
             if (s >= F.n_shapes) break;
             const bool sphere = (F.shape_type[s] == 1);
+            const int nk = sphere ? 1 : (F.shape_type[s] == 3) ? F.mesh_npts[s] : 8;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (sphere && k > 0) break;
+                if (k >= nk) break;
                 f3 b = slot_point(F, s, k, R);
                 f3 xw = S.p + mul(R, b);
                 float depth = -xw.z;

@@ -291,6 +291,9 @@ void build_free(mw_sim* s) {
             F.shape_p[i][k] = static_cast<float>(sh.p[k]);
         }
         for (int k = 0; k < 9; ++k) F.shape_R[i][k] = static_cast<float>(sh.R[k]);
+        F.mesh_npts[i] = static_cast<int32_t>(sh.points.size());
+        for (size_t c = 0; c < sh.points.size() && c < 8; ++c)
+            for (int k = 0; k < 3; ++k) F.mesh_pt[i][c][k] = static_cast<float>(sh.points[c][k]);
     }
 }
 
@@ -566,12 +569,14 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     // Mesh collisions (scene.cpp models them as ground slots at their support
     // points).  Articulated floating models: every support point becomes a
     // zero-radius sphere at that point (the same ground contact: normal +z,
-    // depth -z, in slot order).  Fixed bases never touch the ground here: their
-    // meshes are dropped (counted).  A joint-less floating body (free-body
-    // kernel, <= 2 shapes) with a mesh is refused: insert it into a scene.
+    // depth -z, in slot order).  A joint-less floating body (free-body kernel,
+    // 2 shape entries of 8 slots): the mesh splits into entries of <= 8
+    // points.  Fixed bases never touch the ground here: their meshes are
+    // dropped (counted).
     {
         int meshes = 0;
         const bool expand = s->model.floating && s->model.dofs() > 0;
+        const bool free_body = s->model.floating && s->model.dofs() == 0;
         auto convert = [&](std::vector<mw::Shape>& v) {
             std::vector<mw::Shape> out;
             for (const mw::Shape& sh : v) {
@@ -580,6 +585,15 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
                     continue;
                 }
                 ++meshes;
+                if (free_body) {  // the free-body kernel: <= 8 points (one slot block) per shape entry
+                    for (size_t c0 = 0; c0 < sh.points.size(); c0 += 8) {
+                        mw::Shape part = sh;
+                        part.points.assign(sh.points.begin() + c0,
+                                           sh.points.begin() + std::min(sh.points.size(), c0 + 8));
+                        out.push_back(part);
+                    }
+                    continue;
+                }
                 if (!expand) continue;
                 for (const auto& pt : sh.points) {
                     mw::Shape sp;
@@ -594,10 +608,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         };
         convert(s->model.base_shapes);
         for (auto& b : s->model.bodies) convert(b.shapes);
-        if (meshes && s->model.floating && !expand)
-            return fail(MW_EPARSE, "a joint-less floating body with a mesh collision runs in scenes (mw_scene / the "
-                                   "ScenarI/O World.insert_model), not on mw_sim");
-        if (!expand) s->model.unsupported_shapes += meshes;
+        if (!s->model.floating) s->model.unsupported_shapes += meshes;
     }
     if (s->model.dofs() > mw::kMaxBodies)
         return fail(MW_EPARSE, "models with more than " + std::to_string(mw::kMaxBodies) +
@@ -672,7 +683,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     if (s->floating) {
         if (s->model.base_shapes.size() > static_cast<size_t>(mw::kMaxFreeShapes))
             return fail(MW_EPARSE, "a floating body may have at most " + std::to_string(mw::kMaxFreeShapes) +
-                                       " box / sphere collision shapes in this build");
+                                       " collision shape entries in this build (a mesh takes one per 8 support points)");
         s->model_name = (name && *name) ? name : s->model.name;
         s->loaded = true;
         s->n = 0;

@@ -143,10 +143,10 @@ int mw_model_export_shapes(const mw_sim* sim, int32_t body, double* out, int32_t
  * type (0 box, 1 sphere, 2 cylinder, 3 mesh), size[3], R[9], p[3], npts,
  * points[16][3]} -- a mesh's size is its bounding box half extents, p the box
  * centre, points its ground-contact support points in the shape frame
- * (gym-ignition_amd/csrc/mesh.cpp).  mw_sim: an articulated floating model's
- * mesh contacts the ground at its support points (zero-radius spheres),
- * fixed-base models drop mesh shapes, a joint-less floating mesh body is
- * refused (it runs in scenes). */
+ * (gym-ignition_amd/csrc/mesh.cpp).  mw_sim: a floating model's mesh
+ * contacts the ground at its support points (articulated: zero-radius
+ * spheres; joint-less: free-body shape entries of <= 8 points), fixed-base
+ * models drop mesh shapes. */
 #define MW_COLLISION_WORDS 66
 int mw_compile_collisions(const char* model, const double pose[7], double* out, int32_t max_shapes,
                           int32_t* count);

@@ -883,9 +883,13 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
             if (m->shape_type[k] != 1) {
                 double RS[9];
                 rot_mul(R, SR, RS);
-                for (int corner = 0; corner < 8; ++corner) {
+                const int corners = (m->shape_type[k] == 3) ? m->mesh_npts[k] : 8;
+                for (int corner = 0; corner < corners; ++corner) {
                     double l[3];
-                    or_slot_point(m->shape_type[k], h, RS, corner, l);
+                    if (m->shape_type[k] == 3)   /* mesh entry: its support points */
+                        memcpy(l, m->mesh_pt[k][corner], sizeof l);
+                    else
+                        or_slot_point(m->shape_type[k], h, RS, corner, l);
                     double b[3], x[3];
                     for (int r = 0; r < 3; ++r) b[r] = sp[r] + SR[r * 3] * l[0] + SR[r * 3 + 1] * l[1] + SR[r * 3 + 2] * l[2];
                     for (int r = 0; r < 3; ++r) x[r] = s->p[r] + R[r * 3] * b[0] + R[r * 3 + 1] * b[1] + R[r * 3 + 2] * b[2];

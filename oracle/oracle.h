@@ -119,6 +119,9 @@ typedef struct {
     double shape_p[OR_MAXSHAPES][3];
     double gravity[3];          /* world frame                                */
     double mu;                  /* Coulomb friction with the ground           */
+    /* type 3: mesh support points of the shape entry (<= 8, shape frame) */
+    int32_t mesh_npts[OR_MAXSHAPES];
+    double mesh_pt[OR_MAXSHAPES][8][3];
 } or_free_model;
 
 typedef struct {

@@ -83,6 +83,8 @@ class OrFreeModel(ctypes.Structure):
         ("shape_p", (ctypes.c_double * 3) * OR_MAXSHAPES),
         ("gravity", ctypes.c_double * 3),
         ("mu", ctypes.c_double),
+        ("mesh_npts", ctypes.c_int32 * OR_MAXSHAPES),
+        ("mesh_pt", ((ctypes.c_double * 3) * 8) * OR_MAXSHAPES),
     ]
 
 
@@ -777,9 +779,23 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
             F.gravity[k] = gravity[k]
         for k, v in enumerate([B.I[0, 0], B.I[1, 1], B.I[2, 2], B.I[0, 1], B.I[0, 2], B.I[1, 2]]):
             F.Ic[k] = v
-        solid = [sh for sh in B.shapes if sh[0] != 3]   # meshes: scenes only (SceneWorld)
+        solid = []   # a mesh splits into entries of <= 8 support points (one slot block each)
+        for (t, sz, SR, sp) in B.shapes:
+            if t != 3:
+                solid.append((t, sz, SR, sp))
+                continue
+            pts = np.asarray(sz[3:]).reshape(-1, 3)
+            for c0 in range(0, len(pts), 8):
+                solid.append((3, np.concatenate([sz[:3], pts[c0:c0 + 8].reshape(-1)]), SR, sp))
+        assert len(solid) <= OR_MAXSHAPES
         F.n_shapes = len(solid)
         for i, (t, sz, SR, sp) in enumerate(solid):
+            if t == 3:
+                pts = np.asarray(sz[3:]).reshape(-1, 3)
+                F.mesh_npts[i] = len(pts)
+                for c, pt in enumerate(pts):
+                    for k in range(3):
+                        F.mesh_pt[i][c][k] = pt[k]
             F.shape_type[i] = t
             for k in range(3):
                 F.shape_size[i][k] = sz[k]

@@ -64,11 +64,22 @@ def _quat_to_R(q):
                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
 
 
-@pytest.mark.parametrize("urdf", ["cube", "double", "sphere", "cylinder"])
+def _rock_body_urdf():
+    """a free body whose collision is the 12-vertex rock mesh (two shape
+    entries of 8 + 4 support points on the free-body kernel)"""
+    import os
+    import tempfile
+    from mesh_models import mesh_body_urdf, rock_vertices, write_stl_binary
+    path = os.path.join(tempfile.mkdtemp(), "rock.stl")
+    write_stl_binary(path, *rock_vertices(7))
+    return mesh_body_urdf(path, mass=3.0, half=(0.12, 0.08, 0.06), rpy=(0.2, 0.1, -0.3))
+
+
+@pytest.mark.parametrize("urdf", ["cube", "double", "sphere", "cylinder", "rock"])
 def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
     from mwstep.sim import Simulator
-    text = {"cube": cube_urdf(), "double": cube_urdf(True), "sphere": sphere_urdf(),
-            "cylinder": cylinder_urdf(rpy="0.2 0 0")}[urdf]
+    text = {"cube": cube_urdf, "double": lambda: cube_urdf(True), "sphere": sphere_urdf,
+            "cylinder": lambda: cylinder_urdf(rpy="0.2 0 0"), "rock": _rock_body_urdf}[urdf]()
     W, pgs = 256, 50
     rng = np.random.default_rng(5)
     sim = Simulator(text, n_worlds=W, pgs_iters=pgs)
@@ -76,7 +87,8 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
     sim.enable_contacts(True)
     q = rng.normal(size=(W, 4))
     q /= np.linalg.norm(q, axis=1, keepdims=True)
-    pos = np.column_stack([rng.uniform(-1, 1, W), rng.uniform(-1, 1, W), rng.uniform(0.05, 0.2, W)])
+    zr = (0.0, 0.09) if urdf == "rock" else (0.05, 0.2)   # the rock is a few cm across
+    pos = np.column_stack([rng.uniform(-1, 1, W), rng.uniform(-1, 1, W), rng.uniform(*zr, W)])
     lin = rng.uniform(-0.5, 0.5, (W, 3))
     ang = rng.uniform(-2, 2, (W, 3))
     sim.reset_base_pose(np.column_stack([pos, q]).astype(np.float32).astype(np.float64))

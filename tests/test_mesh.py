@@ -13,8 +13,8 @@ side:
   * KATs on the fp64 scene oracle: an irregular mesh dropped on the ground
     comes to rest with its weight carried by its support points, and a mesh
     body rests on a box of another model (bounding-box pair contact);
-  * loud failures: unsupported formats, missing files, floating mesh models on
-    mw_sim (meshes run in scenes).
+  * loud failures: unsupported formats, missing files, a free body with more
+    shape entries than mw_sim's free-body kernel holds.
 
 Mesh-vs-plane contact in DART (FCL / ODE collision detectors [EXT]) generates
 points from the triangles; the support-point restatement is pinned by the
@@ -138,17 +138,28 @@ def test_bad_meshes_fail_loudly(N, text, needle):
     assert rc == N.MW_EPARSE and needle in msg
 
 
-def test_mw_sim_refuses_floating_mesh_models(N, tmp_path):
+def test_mw_sim_free_body_mesh_entries(N, tmp_path):
+    """mw_sim's free-body kernel holds 2 shape entries of 8 slots: a mesh
+    takes one entry per 8 support points; beyond 2 entries the model fails
+    loudly"""
     path = str(tmp_path / "cube.stl")
     write_stl_binary(path, cube_vertices(), CUBE_TRIS)
+    v, f = rock_vertices(7)
+    rock = str(tmp_path / "rock.stl")
+    write_stl_binary(rock, v, f)
     cfg = N.MwConfig(1e-3, 1.0, 1, 2, 0, 0)
-    h = ctypes.c_void_p()
-    N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
-    try:
-        assert N.lib().mw_load_model(h, mesh_body_urdf(path).encode(), N.dptr(IDENT), b"") == N.MW_EPARSE
-        assert "scene" in N.last_error()
-    finally:
-        N.lib().mw_destroy(h)
+    for uri, extra, ok in ((path, "", True), (rock, "", True), (rock, '<collision><geometry><box size="0.1 0.1 0.1"/>'
+                                                                     '</geometry></collision>', False)):
+        h = ctypes.c_void_p()
+        N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
+        try:
+            text = mesh_body_urdf(uri).replace("</link>", extra + "</link>")
+            rc = N.lib().mw_load_model(h, text.encode(), N.dptr(IDENT), b"")
+            assert (rc == 0) == ok, N.last_error()
+            if not ok:
+                assert rc == N.MW_EPARSE and "entries" in N.last_error()
+        finally:
+            N.lib().mw_destroy(h)
 
 
 def test_mesh_cube_scene_equals_box_scene(oracle, tmp_path):
