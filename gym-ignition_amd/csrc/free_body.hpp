@@ -113,10 +113,12 @@ __device__ __forceinline__ SV minv_mul(const FreeF& __restrict__ F, const SV& x)
 
 // body-frame point of slot k of shape s (box corner k; sphere: centre;
 // cylinder: rim point k, chain_dyn.hpp shape_slot_point) for body rotation Rb
+template <bool MESH>
 __device__ __forceinline__ f3 slot_point(const FreeF& F, int s, int k, const M3& Rb) {
     const float* R = F.shape_R[s];
-    const f3 l = (F.shape_type[s] == 3) ? mk(F.mesh_pt[s][k][0], F.mesh_pt[s][k][1], F.mesh_pt[s][k][2])
-                                        : shape_slot_point(F.shape_type[s], F.shape_size[s], shape_plane_normal(Rb, R), k);
+    const f3 l = (MESH && F.shape_type[s] == 3)
+                     ? mk(F.mesh_pt[s][k][0], F.mesh_pt[s][k][1], F.mesh_pt[s][k][2])
+                     : shape_slot_point(F.shape_type[s], F.shape_size[s], shape_plane_normal(Rb, R), k);
     return {F.shape_p[s][0] + R[0] * l.x + R[1] * l.y + R[2] * l.z,
             F.shape_p[s][1] + R[3] * l.x + R[4] * l.y + R[5] * l.z,
             F.shape_p[s][2] + R[6] * l.x + R[7] * l.y + R[8] * l.z};
@@ -144,6 +146,9 @@ struct Contacts {
 };
 
 // One engine step; the contacts of the step stay in C (positions, impulses).
+// MESH: some shape entry holds mesh support points (a separate instance, so
+// the box / sphere / cylinder bodies keep the unrolled slot loop).
+template <bool MESH>
 __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt, int pgs_iters, FreeState& S,
                                           Contacts& C) {
     const FreeF& F = *Fp;
@@ -167,11 +172,11 @@ __device__ __forceinline__ void free_step(const FreeF* __restrict__ Fp, float dt
         for (int s = 0; s < kMaxFreeShapes; ++s) {
             if (s >= F.n_shapes) break;
             const bool sphere = (F.shape_type[s] == 1);
-            const int nk = sphere ? 1 : (F.shape_type[s] == 3) ? F.mesh_npts[s] : 8;
+            const int nk = sphere ? 1 : (MESH && F.shape_type[s] == 3) ? F.mesh_npts[s] : 8;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (k >= nk) break;
-                f3 b = slot_point(F, s, k, R);
+                f3 b = slot_point<MESH>(F, s, k, R);
                 f3 xw = S.p + mul(R, b);
                 float depth = -xw.z;
                 if (sphere) {  // its lowest point

@@ -480,6 +480,7 @@ __device__ __forceinline__ void store_contact(const FreeDev& D, int W, int w, in
 // velocity resets (WorldPoseCmd / WorldVelocityCmd, Model.cpp:256-360 ->
 // Physics.cpp:1535-1590), the substeps, and the contacts of the last substep
 // (Physics.cpp:2351-2540: point, force on the body = impulse / dt, depth).
+template <bool MESH>
 __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__ F, FreeDev D, int W, RunArgs A,
                                                        int want_contacts) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -490,7 +491,7 @@ __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__
     C.active = 0u;
     C.rec = slots + threadIdx.x;
     if (!A.paused) {
-        for (int s = 0; s < A.substeps; ++s) free_step(F, A.dt, A.pgs_iters, S, C);
+        for (int s = 0; s < A.substeps; ++s) free_step<MESH>(F, A.dt, A.pgs_iters, S, C);
     }
     store_base(D, W, w, S);
     if (want_contacts && !A.paused) {
@@ -963,10 +964,13 @@ hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool
     }
 }
 
-hipError_t launch_free_run(const FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts,
+hipError_t launch_free_run(const FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts, int mesh,
                            hipStream_t st) {
     const int B = dev::kFreeLanes;  // the contact slot records in LDS assume 64-thread blocks
-    hipLaunchKernelGGL(dev::free_run_kernel, grid_for(W, B), dim3(B), 0, st, F, D, W, a, contacts);
+    if (mesh)
+        hipLaunchKernelGGL(dev::free_run_kernel<true>, grid_for(W, B), dim3(B), 0, st, F, D, W, a, contacts);
+    else
+        hipLaunchKernelGGL(dev::free_run_kernel<false>, grid_for(W, B), dim3(B), 0, st, F, D, W, a, contacts);
     return hipGetLastError();
 }
 

@@ -95,7 +95,7 @@ hipError_t launch_scenario_run(const ChainF* P, int n, int topo, bool cons, bool
                                const PidSet& pid, int W, const RunArgs& a, hipStream_t st);
 
 // F: the model's FreeF block in device memory (free_body.hpp)
-hipError_t launch_free_run(const struct FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts,
+hipError_t launch_free_run(const struct FreeF* F, const FreeDev& D, int W, const RunArgs& a, int contacts, int mesh,
                            hipStream_t st);
 
 // Articulated model on a floating base (float_tree.hpp); F: its FloatF block

@@ -934,7 +934,9 @@ static int run_free(mw_sim* s, int paused, bool readback = true) {
     a.pgs_iters = s->cfg.pgs_iters;
     a.first = 1;
     a.substeps = paused ? 0 : s->cfg.steps_per_run;
-    MW_HIP(mw::launch_free_run(s->d_free, s->fdev, s->W, a, s->contacts ? 1 : 0, s->stream));
+    int mesh = 0;
+    for (int k = 0; k < s->h_free.n_shapes; ++k) mesh |= s->h_free.shape_type[k] == mw::Shape::Mesh;
+    MW_HIP(mw::launch_free_run(s->d_free, s->fdev, s->W, a, s->contacts ? 1 : 0, mesh, s->stream));
     if (!paused) {
         s->iterations += s->cfg.steps_per_run;
         s->stepped = true;
