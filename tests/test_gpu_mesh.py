@@ -140,3 +140,42 @@ def test_scenario_rock_from_file_rests_on_the_ground(require_gpu, tmp_path, fmt)
     assert link.contact_wrench()[2] == pytest.approx(3.0 * G, abs=0.1)
     assert np.abs(rock.base_world_linear_velocity()).max() < 1e-3
     gazebo.close()
+
+
+def test_static_mesh_collider_through_scenario(require_gpu, oracle, tmp_path):
+    """A static SDF model whose collision is a mesh (a 0.6 x 0.6 x 0.1 slab as
+    binary STL, top at 0.5) is a welded scene collider: a ball dropped on it
+    rests at top + r and follows the fp64 scene oracle (which restates the
+    mesh independently) within 1e-4 m over 800 steps."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    from mwstep import get_model_file
+    from scene_models import sphere_urdf
+    path = str(tmp_path / "slab.stl")
+    write_stl_binary(path, cube_vertices((0.3, 0.3, 0.05)), CUBE_TRIS)
+    slab = ('<?xml version="1.0"?><sdf version="1.7"><model name="slab"><static>true</static>'
+            '<pose>0.2 0 0.45 0 0 0.3</pose><link name="l"><collision name="c"><geometry><mesh>'
+            f'<uri>{path}</uri></mesh></geometry></collision></link></model></sdf>')
+    gazebo = scenario.GazeboSimulator(0.001, 1.0, 1)
+    assert gazebo.initialize()
+    world = gazebo.get_world().to_gazebo()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("ground_plane"))
+    assert world.insert_model_from_string(slab)
+    ball_text = sphere_urdf(1.0, 0.05)
+    assert world.insert_model_from_string(ball_text, core.Pose([0.25, 0.05, 0.8], [1.0, 0, 0, 0]), "ball")
+    ball = world.get_model("ball")
+    cms = [oracle.load_urdf(slab), oracle.load_urdf(ball_text, pose_xyz=(0.25, 0.05, 0.8))]
+    assert cms[0].base_shapes[0][0] == 3 and not cms[0].floating
+    ow = oracle.SceneWorld(cms, mu=1.0, pgs_iters=50)
+    worst = 0.0
+    for k in range(800):
+        assert gazebo.run()
+        ow.step()
+        if k % 50 == 49:
+            worst = max(worst, float(np.abs(np.array(ball.base_position()) - ow.p(1)).max()))
+    z = ball.base_position()[2]
+    print(f"ball on a static mesh slab: z {z:.5f} (top 0.5 + r 0.05), max |dp| vs oracle {worst:.2e}")
+    assert z == pytest.approx(0.55, abs=2e-3)
+    assert worst <= 1e-4
+    gazebo.close()
