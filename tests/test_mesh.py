@@ -262,3 +262,22 @@ def test_collada_meshes(N, oracle, tmp_path):
     assert rc == 0, got
     _check_against_oracle(got, oracle.load_urdf(text), tol=1e-12)
     assert int(got[0, 17]) >= 8
+
+
+def test_degenerate_meshes(N, oracle, tmp_path):
+    """an empty file fails loudly; a flat mesh (a square) is a zero-thickness
+    box whose support points are its 4 corners, alike in both compilers"""
+    empty = tmp_path / "empty.obj"
+    empty.write_text("# nothing\n")
+    rc, msg = _collisions(N, mesh_body_urdf(str(empty)))
+    assert rc == N.MW_EPARSE and "no vertices" in msg
+    sq = np.array([[-0.1, -0.1, 0], [0.1, -0.1, 0], [0.1, 0.1, 0], [-0.1, 0.1, 0]], dtype=float)
+    path = str(tmp_path / "square.obj")
+    write_obj(path, sq, [(0, 1, 2), (0, 2, 3)])
+    rc, got = _collisions(N, mesh_body_urdf(path, rpy=(0.3, 0, 0)))
+    assert rc == 0, got
+    np.testing.assert_allclose(got[0, 2:5], [0.1, 0.1, 0.0], atol=1e-12)
+    assert int(got[0, 17]) == 4
+    pts = got[0, 18:30].reshape(4, 3)
+    np.testing.assert_allclose(sorted(map(tuple, pts)), sorted(map(tuple, sq)), atol=1e-12)
+    _check_against_oracle(got, oracle.load_urdf(mesh_body_urdf(path, rpy=(0.3, 0, 0))))
