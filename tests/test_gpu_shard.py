@@ -6,6 +6,9 @@
     headline CartPole task (BASELINE configs[1]) and the Panda PID task
     (configs[3], the 1 -> 8 GPU strong split): resets are keyed by the global
     world index, so a world's trajectory does not depend on the rank count;
+  * the same for floating bases with ground contacts (configs[4]'s humanoid
+    split, on the wave kernel with cold and warm-started PGS, and the
+    quadruped on the lane kernel): W worlds == two sims of W/2 worlds;
   * mw_run_device with a pending joint reset and a force command equals mw_run
     (the command slab is copied out of a staging buffer, so clearing the host
     mirror right after the asynchronous launch cannot drop it);
@@ -72,6 +75,69 @@ def test_panda_shards_bit_identical(require_gpu):
     n_done = _run_split("PandaPositionTracking", W, T, 80, targets)
     assert n_done >= W  # every world hit the 80-step TimeLimit at least once
     del torch
+
+
+def _float_sim(model, W, q0, pose, vel, pgs_opts):
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    sim = Simulator(get_model_file(model), n_worlds=W, pgs_iters=50, pose=(0, 0, 0.6, 1, 0, 0, 0))
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    if pgs_opts is not None:
+        sim.set_pgs_options(*pgs_opts)
+    sim.set("reset_q", q0)
+    sim.reset_base_pose(pose)
+    sim.reset_base_velocity(vel)
+    sim.run(paused=True)
+    sim.set_controller_period(1e-3)
+    for d in range(sim.dofs):
+        sim.set_pid(d, [300.0, 0.0, 3.0, -80.0, 80.0, 0.0, 0.0, -1.0])
+    sim.set_control_mode(N.MODE_POSITION)
+    sim.set("position_target", np.zeros_like(q0))
+    return sim
+
+
+@pytest.mark.parametrize("model,z0,pgs_opts", [("humanoid32", 0.56, None),
+                                               ("humanoid32", 0.56, (1e-6, True)),
+                                               ("quadruped", 0.47, None)])
+def test_floating_shards_bit_identical(require_gpu, model, z0, pgs_opts):
+    """BASELINE config 5 splits 512 humanoids over the ranks (bench.py
+    humanoid_leg: the 8-GPU share is 64 worlds): a sim of W worlds equals two
+    sims of W/2 worlds holding the two halves' initial states BIT FOR BIT over
+    150 steps with ground impacts, sliding and (parametrised) the warm-started
+    PGS, on the wave kernel (humanoid) and the lane kernel (quadruped)."""
+    W, T = 128, 150
+    rng = np.random.default_rng(11)
+    from mwstep import get_model_file
+    from mwstep.sim import Simulator
+    p = Simulator(get_model_file(model), n_worlds=1)
+    n = p.dofs
+    p.close()
+    q0 = rng.uniform(-0.1, 0.1, (W, n))
+    quat = rng.normal(size=(W, 4)) * np.array([1.0, 0.05, 0.05, 0.05])
+    quat[:, 0] = np.abs(quat[:, 0]) + 1.0
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), z0 + rng.uniform(0.0, 0.08, W), quat])
+    vel = np.column_stack([rng.uniform(-0.5, 0.5, (W, 2)), rng.uniform(-0.3, 0.0, W), rng.uniform(-0.5, 0.5, (W, 3))])
+    full = _float_sim(model, W, q0, pose, vel, pgs_opts)
+    h = W // 2
+    halves = [_float_sim(model, h, q0[k * h:(k + 1) * h], pose[k * h:(k + 1) * h], vel[k * h:(k + 1) * h], pgs_opts)
+              for k in range(2)]
+    for t in range(T):
+        full.run()
+        for s in halves:
+            s.run()
+        if t % 50 == 49 or t == T - 1:
+            for what in ("q", "qd"):
+                assert np.array_equal(full.get(what), np.concatenate([s.get(what) for s in halves])), (what, t)
+            assert np.array_equal(full.base_pose(), np.concatenate([s.base_pose() for s in halves])), t
+            assert np.array_equal(full.base_velocity(), np.concatenate([s.base_velocity() for s in halves])), t
+    # the window holds impacts and contacts (not a trivially resting state)
+    assert sum(len(full.contacts(w)) for w in range(0, W, 8)) > 0
+    assert full.constraint_overflow() == 0
+    for s in [full] + halves:
+        s.close()
 
 
 @pytest.mark.parametrize("model", ["cartpole", "pendulum"])
