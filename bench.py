@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--graph-chunk", type=int, default=100)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    p.add_argument("--cpu-leg-seconds", type=float, default=4.0, help="CPU baseline budget of the other configs")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-sweep", action="store_true")
@@ -153,7 +154,10 @@ def main():
                 "value": round(2048 * K / r["elapsed"], 1), "unit": "env·steps/s",
                 "ms_per_step": round(r["elapsed"] / K * 1e3, 6),
                 "kernel_us_per_launch": round(r["kernel_us"], 3), "bytes_per_env_step": pb,
-                "kernel": f"vecenv_step_kernel<1,3,false,false,false,{penvs[0].sim.baked_model()}>"}
+                "kernel": f"vecenv_step_kernel<1,3,false,false,false,{penvs[0].sim.baked_model()}>",
+                "roofline": hbm_roofline(pb * 2048, r["kernel_us"], None, "vecenv_step_kernel (Pendulum)")}
+        if not args.no_cpu_baseline:
+            pend["cpu_baseline"] = cpu_vec_baseline("PendulumSwingUp", args.seed, args.cpu_leg_seconds)
         for e in penvs:
             e.close()
 
@@ -178,14 +182,15 @@ def main():
     panda = None
     if not args.no_panda and args.task != "PandaPositionTracking":
         panda = panda_leg(args, dev, torch, dist, world_size, rank)
-    contacts = quadruped = humanoid = humanoid_warm = None
+    contacts = quadruped = humanoid = humanoid_pgs = None
     if not args.no_contact_leg:
         if rank == 0 and world_size == 1:
             contacts = contact_leg(args, dev, torch)
             quadruped = quadruped_leg(args, dev, torch)
         # BASELINE config 5: 512 global humanoid worlds split over the ranks
         humanoid = humanoid_leg(args, dev, torch, dist, world_size, rank)
-        humanoid_warm = humanoid_leg(args, dev, torch, dist, world_size, rank, pgs_opts=(1e-6, True))
+        # the same workload on the PGS sweeps alone (the round-2 default): the exact solve's cost
+        humanoid_pgs = humanoid_leg(args, dev, torch, dist, world_size, rank, exact=False)
     runtime = None
     if rank == 0 and world_size == 1 and not args.no_runtime_leg:
         runtime = runtime_leg(args, dev)
@@ -241,7 +246,11 @@ def main():
                 "launch_floor_us": round(floor_us, 3) if floor_us else None,
                 "launch_floor_note": "per-node time of a hipGraph of 1-element kernels, same replay pattern: "
                                      "the dispatch floor of a one-kernel-per-step closed loop",
+                "regime": "launch/latency-bound: the kernel sits within ~1 us of the launch floor at this "
+                          "world count; 'bound' names the roofline axis, the HBM roof is reached only at "
+                          "~1M worlds (world_sweep)",
             },
+            "gathered_obs_shape": timed["gathered_obs_shape"],
             "world_sweep": sweep,
             "cpu_baseline": cpu,
             "obs_max_abs_err_vs_oracle": parity,
@@ -252,7 +261,7 @@ def main():
             "contacts_floating": contacts,
             "quadruped_floating": quadruped,
             "humanoid_c5": humanoid,
-            "humanoid_c5_warm_pgs": humanoid_warm,
+            "humanoid_c5_pgs_only": humanoid_pgs,
             "runtime_c1": runtime,
             "scene_multi_model": scene,
         }
@@ -301,6 +310,7 @@ def make_groups(task, W, S, dev, seed, offset, **kw):
 
 
 def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, gather=False):
+    n_global = sum(e.n_worlds for e in envs) * world_size  # equal slabs per rank (--worlds per GPU)
     """W untimed warmup steps, then EXACTLY K steps replayed from hipGraphs of
     `chunk` step launches, bracketed by barrier + synchronize; max over ranks.
     Every step reads its action slice where the policy wrote it (the device
@@ -350,7 +360,7 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
         st0 = groups[0][1]
         with torch.cuda.stream(st0):
             obs = torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs
-            gather_obs(obs)
+            gather_obs(obs, n_global=n_global)
         torch.cuda.synchronize(dev)
     ev_start, ev_end = hip_event(), hip_event()
     ev_join = [hip_event() for _ in range(S - 1)]
@@ -377,7 +387,7 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
     if gather:
         with torch.cuda.stream(st0):
             obs = torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs
-            gather_obs(obs)  # final observation tensor, RCCL over xGMI
+            gathered = gather_obs(obs, n_global=n_global)  # final observation tensor, RCCL over xGMI
     torch.cuda.synchronize(dev)
     if world_size > 1:
         dist.barrier()
@@ -391,7 +401,8 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
     for ev in [ev_start, ev_end] + ev_join:
         hip_runtime().hipEventDestroy(ev)
     return {"elapsed": elapsed, "kernel_us": kernel_us, "G": G,
-            "stream": groups[0][1], "groups": S}
+            "stream": groups[0][1], "groups": S,
+            "gathered_obs_shape": list(gathered.shape) if gather else None}
 
 
 _HIP = None
@@ -501,8 +512,11 @@ def panda_leg(args, dev, torch, dist, world_size=1, rank=0, W_global=1024):
     tr = pmc_traffic("PandaPositionTracking", W)
     out["traffic"] = tr["bytes_per_launch"] if tr else None
     out["algorithmic_bytes_per_launch"] = bpe * W
+    out["roofline"] = hbm_roofline(bpe * W, r["kernel_us"], tr, out["kernel"])
     for e_ in envs:
         e_.close()
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_panda_baseline(args.cpu_leg_seconds)
     return out
 
 
@@ -523,7 +537,8 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
     return out
 
 
-def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512, pgs=50, pgs_opts=(0.0, False)):
+def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512, pgs=50, pgs_opts=(0.0, False),
+                 exact=True):
     """BASELINE config 5: 512 iCub-class humanoids in total (models/humanoid32.urdf:
     32 dofs, 36.4 kg, floating base, box feet) split over the ranks, standing on
     the ground plane under the JointController PID hold (stiff legs / torso,
@@ -545,13 +560,18 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
     xy = rng.uniform(-5, 5, (W_global, 2))
     out = float_tree_leg(args, dev, torch, "humanoid32", e - b, pgs, 0.535, gains,
                          q0[b:e], np.zeros((e - b, n)), xy[b:e], K=200, G=20, warm=40,
-                         dist=dist, world_size=world_size, pgs_opts=pgs_opts)
+                         dist=dist, world_size=world_size, pgs_opts=pgs_opts, exact=exact)
     out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
     out["scaling"] = "strong"
     out["worlds_per_gpu"] = e - b
+    solve = ("PGS 50 sweeps then the exact boxed LCP (wave_lcp.hpp, <= 24 linear solves per world-step; "
+             "DART's Dantzig result)" if exact else f"PGS {pgs} iterations only (mw_set_lcp_solver PGS)")
     out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
                        f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "
-                       f"PGS {pgs} iterations, dt = 1 ms (BASELINE.json configs[4])")
+                       f"{solve}, dt = 1 ms (BASELINE.json configs[4])")
+    out["roofline"] = valu_roofline(out["kernel_us_per_launch"], e - b, exact)
+    if exact and rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_humanoid_baseline(args.cpu_leg_seconds)
     if pgs_opts[0] > 0.0 or pgs_opts[1]:
         out["workload"] = out["workload"].replace(
             f"PGS {pgs} iterations", f"PGS warm-started from the previous step's impulses, ending when a sweep "
@@ -563,7 +583,7 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
 
 
 def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, K=500, G=50, warm=100,
-                   dist=None, world_size=1, pgs_opts=(0.0, False)):
+                   dist=None, world_size=1, pgs_opts=(0.0, False), exact=True):
     """Time W floating-base worlds of `model` under a PID hold, one physics
     step per run, replayed from hipGraphs of mw_run_device; with several ranks
     the timed region is bracketed by barriers and the max over ranks is kept."""
@@ -578,6 +598,8 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, 
     sim.enable_contacts(True)
     if pgs_opts[0] > 0.0 or pgs_opts[1]:
         sim.set_pgs_options(*pgs_opts)
+    if not exact:
+        sim.set_lcp_solver(False)
     sim.set("reset_q", q0)
     pose = np.column_stack([xy, np.full(W, z0), np.ones(W), np.zeros((W, 3))])
     sim.reset_base_pose(pose)
@@ -626,7 +648,8 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, 
            "float_kernel": {1: "world per lane (float_tree.hpp)", 2: "world per wavefront (wave_tree.hpp)"}.get(sim.float_kernel()),
            "contact_points_sampled": f"{sum(pts)} in {len(pts)} worlds",
            "base_z_range_after": [round(float(z.min()), 4), round(float(z.max()), 4)],
-           "constraint_overflow": int(sim.constraint_overflow())}
+           "constraint_overflow": int(sim.constraint_overflow()),
+           "lcp_unconverged_world_steps": int(sim.lcp_unconverged()) if sim.float_kernel() == 2 else None}
     sim.close()
     return out
 
@@ -767,6 +790,161 @@ def contact_leg(args, dev, torch):
            "worlds_in_contact_sampled": f"{in_contact}/{W // 16}"}
     sim.close()
     return out
+
+
+VALU_PEAK_PER_S = 1024 * 2.4e9 / 2  # wave-instructions/s: 1,024 SIMDs, one wave64 VALU op per 2 cycles (MI355X_MICROARCH.md)
+
+
+def hbm_roofline(bytes_per_launch, kernel_us, traffic, kernel):
+    """HBM roofline of one launch: algorithmic bytes / measured launch time."""
+    gbs = bytes_per_launch / (kernel_us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 6), "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "traffic_source": traffic["source"] if traffic else None,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch), "kernel": kernel,
+            "kernel_us_per_launch": round(kernel_us, 3),
+            "regime": "launch/latency (one dependent chain per world; far below the HBM roof)"}
+
+
+def valu_roofline(kernel_us, W, exact):
+    """VALU-issue roofline of the world-per-wavefront kernel (config 5): the
+    SQ_INSTS_VALU count per launch from the committed rocprofv3 PMC pass
+    (profiles/pmc_summary_wave.json, scripts/pmc_summary.py) over this
+    launch's measured time, against the chip's VALU issue rate."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary_wave.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = None
+    if not d or d.get("worlds") != W or d.get("exact_lcp") != exact:
+        return {"bound": "valu-issue", "achieved": None, "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
+                "frac": None, "kernel_us_per_launch": kernel_us,
+                "note": f"no PMC summary for {W} worlds (exact_lcp={exact}) in profiles/pmc_summary_wave.json"}
+    rate = d["valu_insts_per_launch"] / (kernel_us * 1e-6)
+    return {"bound": "valu-issue", "achieved": round(rate, 1), "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
+            "frac": round(rate / VALU_PEAK_PER_S, 6), "valu_insts_per_launch": d["valu_insts_per_launch"],
+            "valu_insts_per_wave_step": round(d["valu_insts_per_launch"] / W, 1),
+            "lone_wave_ceiling_frac": round(W / 1024 * 0.5, 4),
+            "kernel_us_per_launch": kernel_us, "source": os.path.relpath(path, ROOT),
+            "regime": "latency: one world per wavefront, <= 1 wave per SIMD, a lone wave issues one VALU op "
+                      "per 4 cycles at best"}
+
+
+def host_threads():
+    """Host cores this process may use, at most 16 (the GPU box's CPU share)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        return ""
+
+
+def _threaded(make, run, seconds, probe_units):
+    """Size a per-thread sample to ~`seconds` from a one-thread probe of
+    `probe_units`, then run it on every host thread at once (the oracle's C
+    calls release the GIL).  make() -> per-thread state; run(state, units)."""
+    from concurrent.futures import ThreadPoolExecutor
+    st = make()
+    t0 = time.perf_counter()
+    run(st, probe_units)
+    per_unit = (time.perf_counter() - t0) / probe_units
+    units = int(max(probe_units, seconds / max(per_unit, 1e-9)))
+    threads = host_threads()
+    states = [make() for _ in range(threads)]
+    with ThreadPoolExecutor(threads) as pool:
+        t0 = time.perf_counter()
+        list(pool.map(lambda x: run(x, units), states))
+        wall = time.perf_counter() - t0
+    return threads, units, wall
+
+
+def cpu_vec_baseline(task, seed, seconds, Wc=2048):
+    """fp64 C oracle VecEnv of `task` (the same env the GPU runs) on every host thread."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from mwstep import get_model_file
+    from mwstep.vecenv import TASKS
+    kind, model = TASKS[task]
+    cm = pyoracle.load_urdf(get_model_file(model))
+    acts = np.random.default_rng(43).uniform(-50.0, 50.0, (64, Wc))
+
+    def make():
+        e = pyoracle.VecEnv(cm, pyoracle.make_task(kind, seed=seed), Wc)
+        e.reset()
+        return e
+
+    def run(e, T):
+        for t0 in range(0, T, 64):
+            e.rollout(acts[:min(64, T - t0)])
+
+    threads, T, wall = _threaded(make, run, seconds, 10)
+    return {"value": round(threads * Wc * T / wall, 1), "unit": "env·steps/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x {Wc} worlds x {T} env steps of {task}, fp64 C oracle "
+                      f"({wall:.1f} s wall; {cpu_model_name()})"}
+
+
+def cpu_panda_baseline(seconds, Wc=64):
+    """BASELINE config 4 on the host: the fp64 oracle's Panda (9-dof tree,
+    joint-limit LCP, PGS 20) under the JointController PID, sinusoidal targets
+    on joints 1 and 6 (or_pid_rollout), Wc worlds per thread, every host thread."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from mwstep import get_model_file
+    cm = pyoracle.load_urdf(get_model_file("panda"))
+    n = cm.n
+    lo, hi = np.array(cm.model.lower[:n]), np.array(cm.model.upper[:n])
+    q0 = np.tile((lo + hi) / 2, (Wc, 1))
+    amp = np.zeros(n)
+    amp[0], amp[5] = 0.9 * (2 * 2.8973) / 2, 0.9 * (3.7525 + 0.0175) / 2
+    from mwstep.models import PANDA_PID_GAINS_1000HZ
+    # ScenarI/O's setPID clamps the command to +-effort (Joint.cpp:504-513)
+    gains = [pyoracle.pid_gains(*PANDA_PID_GAINS_1000HZ[nm], cmdmax=cm.model.effort[i], cmdmin=-cm.model.effort[i])
+             for i, nm in enumerate(cm.joint_names)]
+
+    def make():
+        return [q0.copy(), np.zeros((Wc, n)), None]
+
+    def run(st, T):
+        st[2] = pyoracle.pid_rollout(cm, st[0], st[1], q0, amp, 0.33, gains, T, pgs_iters=20, states=st[2])
+
+    threads, T, wall = _threaded(make, run, seconds, 20)
+    return {"value": round(threads * Wc * T / wall, 1), "unit": "env·steps/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x {Wc} Panda worlds x {T} PID-tracking steps (physics + PID, no task "
+                      f"I/O), fp64 C oracle ({wall:.1f} s wall; {cpu_model_name()})"}
+
+
+def cpu_humanoid_baseline(seconds):
+    """BASELINE config 5 on the host: one fp64 oracle humanoid (dense CRBA +
+    contact LCP solved exactly, PGS_CONVERGED -- the GPU default's problem)
+    under the PID hold per thread (or_float_pid_rollout), every host thread."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from mwstep import get_model_file
+    cm = pyoracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    n = cm.n
+    stiff = ["leg" in nm or "torso" in nm for nm in cm.joint_names]
+    gains = [pyoracle.pid_gains(500.0 if s_ else 50.0, 0.0, 5.0 if s_ else 0.5, cmdmax=80.0, cmdmin=-80.0)
+             for s_ in stiff]
+
+    def make():
+        fw = pyoracle.FloatWorld(cm, pgs_iters=pyoracle.PGS_CONVERGED)
+        return [fw, None]
+
+    def run(st, T):
+        st[1] = pyoracle.float_pid_rollout(st[0], np.zeros(n), gains, T, states=st[1])
+
+    threads, T, wall = _threaded(make, run, seconds, 5)
+    return {"value": round(threads * T / wall, 1), "unit": "env·steps/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x 1 humanoid x {T} steps standing under the PID hold, exact contact "
+                      f"LCP, fp64 C oracle ({wall:.1f} s wall; {cpu_model_name()})"}
 
 
 def pmc_traffic(task, W):

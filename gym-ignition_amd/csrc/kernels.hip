@@ -626,7 +626,7 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
         L.vc[lane] = vc;
     }
     uint32_t active = 0u;
-    int ovf = 0;
+    int ovf = 0, unconv = 0;
     unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
@@ -635,8 +635,8 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
                 L.tau[lane] = dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
             MW_PROF_T(tb);
             MW_PROF_ACC(0, ta, tb);
-            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0, L.qdd, &ovf,
-                                           prof);
+            active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0,
+                                           A.lcp_solves, L.qdd, &ovf, &unconv, prof);
             MW_PROF_T(tc);
             MW_PROF_ACC(7, ta, tc);
         }
@@ -657,6 +657,7 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     if (lane == 0) {
         store_base(D, W, w, base);
         if (ovf) atomicAdd(overflow, ovf);
+        if (unconv) atomicAdd(overflow + 1, unconv);  // exact LCP solves that ran out of budget
     }
     if (A.warm)  // also after a paused run: it may have consumed a reset
         for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) D.warm[static_cast<size_t>(e) * W + w] = L.xw[e];

@@ -53,6 +53,7 @@ struct RunArgs {
     uint64_t pid_gate;    // bit s: the JointController computes a new PID force at substep s
     float pgs_tol;        // > 0: a PGS sweep that moved no impulse by more than pgs_tol max|x| ends the solve
     int warm;             // PGS starts from the previous step's impulses (wave kernel)
+    int lcp_solves;       // > 0: the wave kernel solves its boxed LCP exactly within that many linear solves
 };
 
 // Task description for the device-side env (see sim.cpp for the sources).

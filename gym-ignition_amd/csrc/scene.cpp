@@ -91,6 +91,7 @@ struct mw_scene {
     void* d_misc = nullptr;        // present [W] | ncontact [W] | overflow | wlast [S][NN][W]
     float* d_wrench = nullptr;     // [S][6][NN][W]
     float* d_contact = nullptr;    // [C][12][W]
+    float* d_wphys = nullptr;      // [4][W]: gravity xyz, ground friction per world
     mw::PidF* d_pid = nullptr;
     // pinned host mirrors with the device layouts
     uint8_t* h_joint = nullptr;
@@ -101,6 +102,7 @@ struct mw_scene {
     float* h_contact = nullptr;
     int32_t* h_ncontact = nullptr;
     int32_t* h_overflow = nullptr;  // pinned copy of the device drop counter
+    float* h_wphys = nullptr;       // pinned mirror of d_wphys (uploaded with the presence words)
     int64_t overflow_seen = 0;      // drops already reported
     mw::PidF* h_pid = nullptr;
     size_t jrows = 0;              // NBMAX * W
@@ -381,6 +383,7 @@ int flush(mw_scene* s, bool defer) {
     if (s->present_dirty) {
         SC_HIP(hipMemcpyAsync(s->dev.present, s->h_present, s->W * sizeof(uint32_t), hipMemcpyHostToDevice,
                               s->stream));
+        SC_HIP(hipMemcpyAsync(s->d_wphys, s->h_wphys, 4 * s->W * sizeof(float), hipMemcpyHostToDevice, s->stream));
     }
     if (s->wrench_dirty) {
         const size_t nn = static_cast<size_t>(SLOTS) * NNMAX * s->W;
@@ -566,6 +569,12 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_contact), static_cast<size_t>(CMAX) * 12 * W * sizeof(float)));
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), NBMAX * sizeof(mw::PidF)));
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->dp), sizeof(mw::SceneF)));
+    SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_wphys), 4 * W * sizeof(float)));
+    SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_wphys), 4 * W * sizeof(float), hipHostMallocDefault));
+    for (size_t w = 0; w < W; ++w) {
+        for (int k = 0; k < 3; ++k) s->h_wphys[k * W + w] = static_cast<float>(s->gravity[k]);
+        s->h_wphys[3 * W + w] = static_cast<float>(s->mu);
+    }
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_present), W * sizeof(uint32_t), hipHostMallocDefault));
     std::memset(s->h_present, 0, W * sizeof(uint32_t));
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_wlast), nwl * sizeof(int32_t), hipHostMallocDefault));
@@ -602,6 +611,7 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     D.wlast = reinterpret_cast<int32_t*>(mp + W * sizeof(uint32_t) + W * sizeof(int32_t) + 64);
     D.wrench = s->d_wrench;
     D.contact = s->d_contact;
+    D.wphys = s->d_wphys;
     s->mode.assign(s->jrows, MW_MODE_IDLE);
     s->cmd64.assign(s->jrows, 0.0);
     s->ptgt64.assign(s->jrows, 0.0);
@@ -622,6 +632,8 @@ void mw_scene_destroy(mw_scene* s) {
     (void)hipFree(s->d_contact);
     (void)hipFree(s->d_pid);
     (void)hipFree(s->dp);
+    (void)hipFree(s->d_wphys);
+    (void)hipHostFree(s->h_wphys);
     (void)hipHostFree(s->h_joint);
     (void)hipHostFree(s->h_base);
     (void)hipHostFree(s->h_present);
@@ -945,6 +957,38 @@ int mw_scene_set_gravity(mw_scene* s, const double g[3]) {
     for (int k = 0; k < 3; ++k) s->gravity[k] = g[k];
     try { build_params(s); } catch (const std::exception& e) { return fail(MW_EPARSE, e.what()); }
     s->params_dirty = true;
+    return mw_scene_set_world_gravity(s, 0, s->W, g);
+}
+
+// World::setGravity of the worlds [w0, w0 + nw) (World.cpp:301-319: every
+// world has its own Gravity component)
+int mw_scene_set_world_gravity(mw_scene* s, int32_t w0, int32_t nw, const double g[3]) {
+    if (int rc = check(s)) return rc;
+    if (!g) return fail(MW_EINVAL, "null argument");
+    if (w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "world range out of bounds");
+    const size_t W = static_cast<size_t>(s->W);
+    for (int w = w0; w < w0 + nw; ++w)
+        for (int k = 0; k < 3; ++k) s->h_wphys[k * W + w] = static_cast<float>(g[k]);
+    s->present_dirty = true;
+    return MW_OK;
+}
+
+int mw_scene_world_gravity(const mw_scene* s, int32_t w, double g[3]) {
+    if (int rc = check(s)) return rc;
+    if (!g) return fail(MW_EINVAL, "null argument");
+    if (w < 0 || w >= s->W) return fail(MW_EINVAL, "world out of range");
+    for (int k = 0; k < 3; ++k) g[k] = s->h_wphys[static_cast<size_t>(k) * s->W + w];
+    return MW_OK;
+}
+
+// friction coefficient of the ground plane of the worlds [w0, w0 + nw)
+// (every contact of those worlds uses it)
+int mw_scene_set_world_friction(mw_scene* s, int32_t w0, int32_t nw, double mu) {
+    if (int rc = check(s)) return rc;
+    if (!(mu >= 0.0)) return fail(MW_EINVAL, "the friction coefficient must be >= 0");
+    if (w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "world range out of bounds");
+    for (int w = w0; w < w0 + nw; ++w) s->h_wphys[3 * static_cast<size_t>(s->W) + w] = static_cast<float>(mu);
+    s->present_dirty = true;
     return MW_OK;
 }
 
@@ -964,6 +1008,7 @@ int mw_scene_set_ground_plane(mw_scene* s, int32_t enabled, double mu) {
     s->mu = mu;
     try { build_params(s); } catch (const std::exception& e) { return fail(MW_EPARSE, e.what()); }
     s->params_dirty = true;
+    if (int rc = mw_scene_set_world_friction(s, 0, s->W, mu)) return rc;
     return mw_scene_set_world_ground(s, 0, s->W, enabled);
 }
 

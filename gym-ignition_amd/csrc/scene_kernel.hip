@@ -587,7 +587,7 @@ __device__ __forceinline__ float sc_dof_force(const SceneF* __restrict__ P, cons
 template <int MAXNV>
 __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeState& base, uint32_t present,
                         const float (&wr)[kScWrenchSlots][6], const int32_t (&wl)[kScWrenchSlots], int iter,
-                        float dt, int pgs_iters, int& nc_out, int& ovf) {
+                        float dt, int pgs_iters, const f3 gw, float mu, int& nc_out, int& ovf) {
     const int lane = lane_id();
     const int NB = P->n_bodies, NV = P->nv;
     const bool isnode = lane < P->n_nodes;
@@ -603,7 +603,6 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     const int srank = P->node_srank[lane];
     const int pnode = isbody ? (b.parent >= 0 ? P->body_node[b.parent] : md.node0) : 0;
     const int levels = P->levels, fanout = P->fanout;
-    const f3 gw = mk(P->g[0], P->g[1], P->g[2]);
     const bool dual = P->dual != 0;
     // external wrench of this node at this iteration (world force at the
     // origin, world torque), summed over the active records
@@ -985,7 +984,6 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             }
         }
         // ---- PGS (rows in order; lane c owns rows c and c + 64)
-        const float mu = P->mu;
         float x0 = 0.f, x1 = 0.f, w0 = 0.f, w1 = 0.f;
         const bool two = NR > kWaveLanes;
         if (NR <= kWaveLanes) {
@@ -1118,6 +1116,9 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
     __shared__ ScWorld<MAXNV> L;
     const int NB = P->n_bodies, NN = P->n_nodes;
     const uint32_t present = D.present[w];
+    // the world's gravity and ground friction (uniform loads)
+    const f3 gw = mk(D.wphys[w], D.wphys[static_cast<size_t>(W) + w], D.wphys[2 * static_cast<size_t>(W) + w]);
+    const float mu = D.wphys[3 * static_cast<size_t>(W) + w];
     // the base lanes: node0 of every model (lane m of the base arrays = model)
     const bool baselane = lane < NN && P->node_body[lane] < 0;
     const int bm = baselane ? P->node_model[lane] : 0;
@@ -1192,7 +1193,7 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         for (int s = 0; s < A.substeps; ++s) {
             if (lane < NB && ((present >> P->body_model[lane]) & 1u))
                 L.tau[lane] = sc_dof_force(P, D, pid, G, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
-            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, nc, ovf);
+            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, gw, mu, nc, ovf);
         }
     }
     if (lane < NB) {

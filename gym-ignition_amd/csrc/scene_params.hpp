@@ -112,6 +112,7 @@ struct SceneDev {
     float* contact;
     int32_t* ncontact;
     int32_t* overflow;   // contact points / rows dropped (capacity)
+    float* wphys;        // [4][W] per-world physics: gravity xyz (World::setGravity), ground friction
 };
 
 // per-launch arguments

@@ -144,6 +144,8 @@ struct mw_sim {
     bool pgs_warm = false;
     int* h_overflow = nullptr;    // pinned copy read back with each synchronous run
     int64_t overflow_seen = 0;    // drops already reported
+    int32_t lcp_mode = MW_LCP_EXACT;  // mw_set_lcp_solver (wave kernel)
+    int32_t lcp_solves = 24;          // linear-solve budget of the exact solve per step
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]
@@ -724,6 +726,26 @@ int mw_device_params(const mw_sim* s, void* out, int32_t bytes) {
     return MW_OK;
 }
 
+// Device buffers of the world-per-wavefront kernel: PID gains, the overflow
+// counters ([0] constraint rows dropped, [1] exact-LCP solves that ran out of
+// budget) and the warm-start record of the PGS impulses.  Called at
+// initialisation, or when a model switches to the kernel mid-life (joint
+// damping set after mw_initialize).
+static int alloc_wave_buffers(mw_sim* s) {
+    const size_t W = static_cast<size_t>(s->W);
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), mw::kMaxBodies * sizeof(mw::PidF)));
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), mw::kMaxBodies * sizeof(mw::PidF),
+                         hipHostMallocDefault));
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), 2 * sizeof(int)));
+    MW_HIP(hipMemsetAsync(s->d_overflow, 0, 2 * sizeof(int), s->stream));
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), 2 * sizeof(int), hipHostMallocDefault));
+    s->h_overflow[0] = s->h_overflow[1] = 0;
+    const size_t wb = static_cast<size_t>(mw::kWaveWarmWordsHost) * W * sizeof(float);
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_warm), wb));
+    MW_HIP(hipMemsetAsync(s->d_warm, 0, wb, s->stream));
+    return MW_OK;
+}
+
 int mw_constraint_overflow(const mw_sim* s, int64_t* rows) {
     int rc = check_sim(s);
     if (rc) return rc;
@@ -734,6 +756,19 @@ int mw_constraint_overflow(const mw_sim* s, int64_t* rows) {
     MW_HIP(hipMemcpyAsync(&v, s->d_overflow, sizeof(int), hipMemcpyDeviceToHost, s->stream));
     MW_HIP(hipStreamSynchronize(s->stream));
     *rows = v;
+    return MW_OK;
+}
+
+int mw_lcp_unconverged(const mw_sim* s, int64_t* worlds) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!worlds) return fail(MW_EINVAL, "null argument");
+    *worlds = 0;
+    if (!s->d_overflow) return MW_OK;
+    int v[2] = {0, 0};
+    MW_HIP(hipMemcpyAsync(v, s->d_overflow, 2 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    *worlds = v[1];
     return MW_OK;
 }
 
@@ -774,16 +809,7 @@ int mw_initialize(mw_sim* s) {
         if (s->float_tree) {
             MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_float), sizeof(mw::FloatF)));
             if (s->wave) {
-                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), mw::kMaxBodies * sizeof(mw::PidF)));
-                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), mw::kMaxBodies * sizeof(mw::PidF),
-                                     hipHostMallocDefault));
-                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), sizeof(int)));
-                MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
-                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int), hipHostMallocDefault));
-                *s->h_overflow = 0;
-                const size_t wb = static_cast<size_t>(mw::kWaveWarmWordsHost) * W * sizeof(float);
-                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_warm), wb));
-                MW_HIP(hipMemsetAsync(s->d_warm, 0, wb, s->stream));
+                if (int rc = alloc_wave_buffers(s)) return rc;
             } else {
                 const size_t words = static_cast<size_t>(mw::float_workspace_words(s->n, s->n_slots));
                 MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ws), words * W * sizeof(float)));
@@ -1011,6 +1037,7 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     a.pgs_iters = s->cfg.pgs_iters;
     a.pgs_tol = static_cast<float>(s->pgs_tol);
     a.warm = (s->wave && s->pgs_warm && s->d_warm) ? 1 : 0;
+    a.lcp_solves = s->wave ? s->lcp_solves : 0;
     a.first = 1;
     const int spr = s->cfg.steps_per_run;
     int done = 0;
@@ -1045,7 +1072,7 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
         MW_HIP(hipMemcpyAsync(s->h_block, s->d_block, s->state_bytes, hipMemcpyDeviceToHost, s->stream));
         if (s->float_tree && (rc = read_base(s, paused))) return rc;
         if (s->h_overflow)
-            MW_HIP(hipMemcpyAsync(s->h_overflow, s->d_overflow, sizeof(int), hipMemcpyDeviceToHost, s->stream));
+            MW_HIP(hipMemcpyAsync(s->h_overflow, s->d_overflow, 2 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
         MW_HIP(hipStreamSynchronize(s->stream));
         s->contacts_stale = false;
     } else {
@@ -1174,13 +1201,9 @@ int mw_set_joint_param(mw_sim* s, int32_t dof, int32_t which, double value) {
                 return fail(MW_EPARSE, "joint damping on this floating-base model needs the world-per-wavefront "
                                        "kernel, whose depth limit the tree exceeds");
             if (s->initialized && !s->d_pid) {
-                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), mw::kMaxBodies * sizeof(mw::PidF)));
-                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), mw::kMaxBodies * sizeof(mw::PidF),
-                                     hipHostMallocDefault));
-                MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), sizeof(int)));
-                MW_HIP(hipMemsetAsync(s->d_overflow, 0, sizeof(int), s->stream));
-                MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int), hipHostMallocDefault));
-                *s->h_overflow = 0;
+                int rc = alloc_wave_buffers(s);
+                if (rc) return rc;
+                s->fdev.warm = s->d_warm;
                 s->pid_dirty = true;
             }
             s->wave = true;
@@ -1622,6 +1645,9 @@ int mw_set_pgs_options(mw_sim* s, double tol, int32_t warm_start) {
     if (!s) return fail(MW_EINVAL, "null simulator handle");
     if (!(tol >= 0.0) || tol >= 1.0) return fail(MW_EINVAL, "the PGS velocity tolerance must be in [0, 1)");
     const bool warm = warm_start != 0;
+    if (warm && s->initialized && !s->wave)
+        return fail(MW_ESTATE, "warm-started PGS needs the world-per-wavefront kernel (articulated floating "
+                               "bases / generic fixed trees); this model runs on another kernel");
     if (warm && !s->pgs_warm && s->d_warm) {
         // a fresh warm start: no stale impulses from before the option was off
         MW_HIP(hipMemsetAsync(s->d_warm, 0, static_cast<size_t>(mw::kWaveWarmWordsHost) * s->W * sizeof(float),
@@ -1629,6 +1655,23 @@ int mw_set_pgs_options(mw_sim* s, double tol, int32_t warm_start) {
     }
     s->pgs_tol = tol;
     s->pgs_warm = warm;
+    return MW_OK;
+}
+
+int mw_set_lcp_solver(mw_sim* s, int32_t mode, int32_t max_solves) {
+    if (!s) return fail(MW_EINVAL, "null simulator handle");
+    if (mode != MW_LCP_PGS && mode != MW_LCP_EXACT) return fail(MW_EINVAL, "unknown LCP solver mode");
+    if (mode == MW_LCP_EXACT && (max_solves < 1 || max_solves > 256))
+        return fail(MW_EINVAL, "the exact solve's budget must be 1..256 linear solves per step");
+    s->lcp_mode = mode;
+    s->lcp_solves = (mode == MW_LCP_EXACT) ? max_solves : 0;
+    return MW_OK;
+}
+
+int mw_lcp_solver(const mw_sim* s, int32_t* mode, int32_t* max_solves) {
+    if (!s || !mode || !max_solves) return fail(MW_EINVAL, "null argument");
+    *mode = s->lcp_mode;
+    *max_solves = s->lcp_solves;
     return MW_OK;
 }
 

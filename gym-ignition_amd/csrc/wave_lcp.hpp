@@ -1,0 +1,329 @@
+// wave_lcp.hpp -- exact solve of the world-per-wavefront kernel's boxed LCP
+// (contact normal rows x_n >= 0, friction rows |x_t| <= mu x_n, joint rows in
+// [lo, hi]), the problem DART's primary boxed-LCP solver (Dantzig pivoting,
+// BoxedLcpConstraintSolver [EXT], reached from ForwardStep at
+// /root/reference/cpp/scenario/plugins/Physics/Physics.cpp:1824-1835) solves
+// exactly.  Specification: oracle.c lcp_refine / boxqp_solve (the fixed point
+// of the friction boxes with the box QP of every round solved exactly).
+//
+// Lane r owns row r: its Delassus row a[c] = A[r][c] (the PGS registers of
+// wave_step), its impulse x_r and its row data.  After the PGS sweeps:
+//
+//   1. semismooth Newton rounds on the coupled conditions: a row is held at
+//      a bound when its gradient g = A x - b pushes it outward, a friction row
+//      held at +-mu x_n moves with its normal (d_t = +-mu d_n), every other
+//      row is free; the Newton system (free rows, coupled columns folded into
+//      their normal's column) is solved by Gaussian elimination with partial
+//      pivoting over the lanes; the step is accepted only when it lowers the
+//      largest complementarity residual (halved up to 3 times);
+//   2. if a round fails, the oracle's own method: friction boxes frozen at the
+//      current normals, the box QP solved by the primal active-set method
+//      (one bound joins or leaves the working set per step), the boxes
+//      updated, until they stop moving;
+//
+// within a budget of linear solves per step.  Converged = every row's
+// complementarity residual (oracle lcp_residual, velocity units) within fp32
+// round-off of its own terms.  A world that runs out of budget keeps its
+// current impulses (feasible, never worse than the PGS start) and is counted.
+#pragma once
+
+namespace mw {
+namespace dev {
+
+constexpr float kLcpRelTol = 4e-6f;   // residual <= kLcpRelTol (|b| + sum |A_rc x_c|) + kLcpAbsTol
+constexpr float kLcpAbsTol = 1e-7f;   // m/s or rad/s
+constexpr int kLcpLineSearch = 3;     // step halvings of a Newton round
+
+__device__ __forceinline__ float wave_fmax(float v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+
+__device__ __forceinline__ float wave_fmin(float v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = fminf(v, __shfl_xor(v, m));
+    return v;
+}
+
+// first lane holding the wave maximum of v
+__device__ __forceinline__ int wave_argmax(float v) {
+    const float m = wave_fmax(v);
+    return __builtin_ctzll(static_cast<unsigned long long>(__ballot(v == m)));
+}
+
+__device__ __forceinline__ bool mask_bit(uint64_t m, int i) { return ((m >> i) & 1ull) != 0ull; }
+
+// Row data of lane r (r < n): rhs b, kind, bounds of box rows, the contact's
+// normal row for friction rows.
+struct LcpRow {
+    float b, lo, hi;
+    int kind;   // 0 normal, 1 friction, 2 box (joint limit / servo / Coulomb)
+    int nrow;   // friction: lane of its normal row; else the lane itself
+    bool live;  // r < n
+};
+
+// w_r = sum_c A[r][c] x_c and mag = sum_c |A[r][c] x_c| (round-off scale)
+template <int RC>
+__device__ __forceinline__ float lcp_matvec(const float (&a)[kWaveMaxRows], float xl, int n, float& mag) {
+    float w = 0.f, m = 0.f;
+#pragma unroll
+    for (int c = 0; c < RC; ++c) {
+        if ((c & 7) == 0 && c >= n) break;
+        const float t = a[c] * read_lane(xl, c);
+        w += t;
+        m += fabsf(t);
+    }
+    mag = m;
+    return w;
+}
+
+// box of row r at the lane-distributed impulses xl (friction: [-mu x_n, mu x_n])
+__device__ __forceinline__ void lcp_bounds(const LcpRow& R, float xl, float mu, float& L, float& U) {
+    const float xn = __shfl(xl, R.nrow);
+    const float u = mu * fmaxf(xn, 0.f);
+    L = (R.kind == 1) ? -u : R.lo;
+    U = (R.kind == 1) ? u : R.hi;
+}
+
+// complementarity residual of row r (oracle lcp_residual, velocity units),
+// relative to its round-off scale: <= 1 is converged
+__device__ __forceinline__ float lcp_row_residual(const LcpRow& R, float xl, float w, float mag, float arr, float L,
+                                                  float U, float tolx, float& e_abs) {
+    if (!R.live) {
+        e_abs = 0.f;
+        return 0.f;
+    }
+    const float s = R.b - w;
+    float e;
+    if (xl < L - tolx || xl > U + tolx)
+        e = ((xl < L) ? (L - xl) : (xl - U)) * arr;
+    else if (U - L <= tolx)
+        e = 0.f;
+    else if (xl <= L + tolx)
+        e = fmaxf(s, 0.f);
+    else if (xl >= U - tolx)
+        e = fmaxf(-s, 0.f);
+    else
+        e = fabsf(s);
+    e_abs = e;
+    return e * rcp(kLcpRelTol * (fabsf(R.b) + mag) + kLcpAbsTol);
+}
+
+// Gaussian elimination with partial pivoting, lane = row: k[c] = K[lane][c],
+// rhs = rhs[lane], rows / columns >= n are ignored.  Returns d[lane].
+// Column j is eliminated at step j; the registers shift by one column per
+// step (k[0] is always the current column), so no register is indexed at run
+// time.  The pivot row of step j is kept in LDS (U, kLcpUStride floats per
+// row: the row's columns j.. at 0.., its rhs at kLcpRhs) for the
+// back substitution, where lane l gathers U[l][j - l] (stride - 1 odd: the 64
+// lanes hit 64 banks).
+constexpr int kLcpUStride = 66;
+constexpr int kLcpRhs = 64;
+
+template <int RC>
+__device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U) {
+    const int lane = lane_id();
+    bool used = lane >= n;
+    for (int j = 0; j < n; ++j) {
+        const int p = wave_argmax(used ? -1.f : fabsf(k[0]));
+        float piv = read_lane(k[0], p);
+        piv = (fabsf(piv) < 1e-30f) ? 1e-30f : piv;
+        const float f = (used || lane == p) ? 0.f : k[0] * rcp(piv);
+        const float prhs = read_lane(rhs, p);
+        const int left = n - j;  // live columns
+        if (lane == p) {
+            float2* u = reinterpret_cast<float2*>(U + j * kLcpUStride);
+#pragma unroll
+            for (int c = 0; c < RC; c += 2) {
+                if ((c & 7) == 0 && c >= left) break;
+                u[c / 2] = make_float2(k[c], (c + 1 < RC) ? k[c + 1] : 0.f);
+            }
+            U[j * kLcpUStride + kLcpRhs] = rhs;
+        }
+#pragma unroll
+        for (int c = 0; c + 1 < RC; ++c) {
+            if ((c & 7) == 0 && c >= left) break;
+            k[c] = fmaf(-f, read_lane(k[c + 1], p), k[c + 1]);
+        }
+        rhs = fmaf(-f, prhs, rhs);
+        used = used || lane == p;
+    }
+    // back substitution, right-looking: lane l holds row l (pivot of step l)
+    float acc = 0.f, rdiag = 1.f;
+    if (lane < n) {
+        acc = U[lane * kLcpUStride + kLcpRhs];
+        float dg = U[lane * kLcpUStride];
+        dg = (fabsf(dg) < 1e-30f) ? 1e-30f : dg;
+        rdiag = rcp(dg);
+    }
+    float dl = 0.f;
+    for (int j = n - 1; j >= 0; --j) {
+        const float dj = read_lane(acc * rdiag, j);
+        dl = (lane == j) ? dj : dl;
+        if (lane < j) acc = fmaf(-U[lane * (kLcpUStride - 1) + j], dj, acc);
+    }
+    return dl;
+}
+
+// The exact solve.  xl: lane r's impulse from the PGS (feasible), returned
+// solved.  a: the Delassus registers (a[c] = A[lane][c], CFM included).
+// Returns true when converged within max_solves linear solves.
+template <int RC>
+__device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
+                                               int max_solves, float* __restrict__ Uw, float& xl) {
+    const int lane = lane_id();
+    float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
+#pragma unroll
+    for (int c = 0; c < RC; ++c) arr = (lane == c && R.live) ? a[c] : arr;
+    int solves = 0;
+    bool converged = false;
+    int phase = 0;          // 0 semismooth Newton, 1 staggered active set (oracle lcp_refine)
+    int ws = 0;             // phase 1 working set: 0 free, 1 held at L, 2 held at U
+    float Lf = 0.f, Uf = 0.f, prev = 0.f;  // phase 1: the round's frozen box, the round's start
+    bool at_min = false, new_round = true;
+    for (int iter = 0; iter < 4 * max_solves + 8; ++iter) {
+        float mag;
+        const float w = lcp_matvec<RC>(a, xl, n, mag);
+        const float g = w - R.b;
+        float L, U;
+        lcp_bounds(R, xl, mu, L, U);
+        const float xmax = wave_fmax(R.live ? fabsf(xl) : 0.f);
+        const float tolx = 2e-6f * (1.f + xmax);
+        float e_abs;
+        const float rel = wave_fmax(lcp_row_residual(R, xl, w, mag, arr, L, U, tolx, e_abs));
+        if (rel <= 1.f) {
+            converged = true;
+            break;
+        }
+        if (solves >= max_solves) break;
+        if (phase == 1 && new_round) {
+            // a round of lcp_refine: boxes frozen at the current normals
+            new_round = false;
+            Lf = L;
+            Uf = U;
+            prev = xl;
+            if (xl <= Lf) { xl = Lf; ws = 1; }
+            else if (xl >= Uf) { xl = Uf; ws = 2; }
+            else ws = 0;
+            if (Lf == Uf || !R.live) ws = 1;
+            at_min = false;
+            continue;  // re-evaluate at the clamped start
+        }
+        if (phase == 1 && at_min) {
+            // boxqp_solve: minimiser on the working set -> release the worst multiplier
+            at_min = false;
+            float v = (ws == 1) ? -g : ((ws == 2) ? g : 0.f);
+            v = (Lf == Uf || !R.live) ? 0.f : v;
+            const float gm = wave_fmax(R.live ? fabsf(g) : 0.f);
+            const int worst = wave_argmax(v);
+            if (read_lane(v, worst) <= kLcpRelTol * (1.f + gm)) {
+                // the round's QP is solved: the next round on the updated boxes
+                if (wave_fmax(fabsf(xl - prev)) <= tolx) break;  // fixed point at the round-off floor
+                new_round = true;
+            } else if (lane == worst) {
+                ws = 0;
+            }
+            continue;
+        }
+        // ---- one linear solve: the Newton system of this round ----
+        float k[RC];
+        bool fr;
+        float coup = 0.f;  // phase 0: d_t = coup d_n of a friction row held at +-mu x_n
+        const float emax = wave_fmax(e_abs);
+        if (phase == 0) {
+            // a row is held when its gradient pushes it out of its box; a
+            // friction row on its box edge moves with its normal
+            bool fixed = !R.live;
+            if (R.kind == 0) fixed = fixed || (xl <= 0.f && g >= 0.f);
+            if (R.kind == 2) fixed = fixed || (xl <= R.lo && g >= 0.f) || (xl >= R.hi && g <= 0.f);
+            const bool nfixed = __shfl(static_cast<int>(fixed), R.nrow) != 0;
+            bool cpos = false, cneg = false;
+            if (R.kind == 1 && R.live && !fixed) {
+                if (nfixed || U <= 0.f) fixed = true;
+                else if (xl >= U && g <= 0.f) cpos = true;
+                else if (xl <= L && g >= 0.f) cneg = true;
+            }
+            fr = R.live && !fixed && !cpos && !cneg;
+            coup = cpos ? mu : (cneg ? -mu : 0.f);
+            const uint64_t freeM = __ballot(fr), cpM = __ballot(cpos), cnM = __ballot(cneg);
+#pragma unroll
+            for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
+            // x_t = +-mu x_n: the held friction column folds into its normal's
+            if ((cpM | cnM) != 0ull) {
+#pragma unroll
+                for (int c = 0; c + 2 < RC; c += 3) {
+                    const float s1 = (mask_bit(cpM, c + 1) ? 1.f : 0.f) - (mask_bit(cnM, c + 1) ? 1.f : 0.f);
+                    const float s2 = (mask_bit(cpM, c + 2) ? 1.f : 0.f) - (mask_bit(cnM, c + 2) ? 1.f : 0.f);
+                    if (fr) k[c] += mu * (s1 * a[c + 1] + s2 * a[c + 2]);
+                }
+            }
+        } else {
+            fr = R.live && ws == 0;
+            const uint64_t freeM = __ballot(fr);
+#pragma unroll
+            for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
+        }
+        float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw);
+        ++solves;
+        if (phase == 0) {
+            const float dn = __shfl(d, R.nrow);
+            d = fr ? d : coup * dn;
+            // monotone line search on the largest residual
+            bool accepted = false;
+            float step = 1.f;
+            for (int ls = 0; ls <= kLcpLineSearch; ++ls, step *= 0.5f) {
+                float xt = xl + step * d;
+                if (R.kind == 0) xt = fmaxf(xt, 0.f);
+                if (R.kind == 2) xt = fminf(fmaxf(xt, R.lo), R.hi);
+                float Lt, Ut;
+                lcp_bounds(R, xt, mu, Lt, Ut);  // the friction boxes of the projected normals
+                if (R.kind == 1) xt = fminf(fmaxf(xt, Lt), Ut);
+                xt = R.live ? xt : 0.f;
+                float mt;
+                const float wt = lcp_matvec<RC>(a, xt, n, mt);
+                const float xmt = wave_fmax(R.live ? fabsf(xt) : 0.f);
+                float et;
+                (void)lcp_row_residual(R, xt, wt, mt, arr, Lt, Ut, 2e-6f * (1.f + xmt), et);
+                if (wave_fmax(et) < emax) {
+                    xl = xt;
+                    accepted = true;
+                    break;
+                }
+            }
+            if (!accepted) {
+                phase = 1;
+                new_round = true;
+            }
+            continue;
+        }
+        // boxqp_solve step: the longest feasible step along d (at most 1)
+        const float dmax = wave_fmax(fabsf(d));
+        if (dmax <= 1e-7f * (1.f + xmax)) {
+            at_min = true;
+            continue;
+        }
+        float al = 1.f;
+        int side = 0;
+        if (fr && d < 0.f && xl + d < Lf) { al = (Lf - xl) * rcp(d); side = 1; }
+        else if (fr && d > 0.f && xl + d > Uf) { al = (Uf - xl) * rcp(d); side = 2; }
+        al = fmaxf(al, 0.f);
+        const float amin = wave_fmin(al);
+        if (amin < 1.f) {
+            const int block = wave_argmax(-al);
+            const int bside = __builtin_amdgcn_readlane(side, block);
+            xl = fr ? xl + amin * d : xl;
+            if (lane == block) {
+                xl = (bside == 1) ? Lf : Uf;
+                ws = bside;
+            }
+        } else {
+            xl = fr ? xl + d : xl;
+            at_min = true;
+        }
+    }
+    return converged;
+}
+
+}  // namespace dev
+}  // namespace mw

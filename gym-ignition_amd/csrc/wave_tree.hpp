@@ -95,7 +95,7 @@ struct WaveWorld {
     float s_R[kMaxFloatSlots][9];   // body rotation
     float s_x[kMaxFloatSlots][3];   // impulses (output)
     // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
-    float stack[kWaveMaxDepth][7][kWaveLanes];
+    alignas(16) float stack[kWaveMaxDepth][7][kWaveLanes];
     float xw[kWaveWarmWords];    // warm-start impulses (RunArgs::warm)
 };
 
@@ -126,6 +126,12 @@ __device__ __forceinline__ float clamp_ordered(float v, float lo, float hi) {
 __device__ __forceinline__ float read_lane(float x, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
+
+}  // namespace dev
+}  // namespace mw
+#include "wave_lcp.hpp"
+namespace mw {
+namespace dev {
 
 // the whole wave runs these with identical values; lane 0 stores
 #define MW_LANE0 if (lane_id() == 0)
@@ -402,8 +408,8 @@ __device__ __forceinline__ void wave_pgs(const WaveWorld<MAXN>& L, const float (
 template <int MAXN, bool CONS>
 __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                               FreeState& base, WaveWorld<MAXN>& L, float dt, int pgs_iters,
-                                              float pgs_tol, bool warm, float* qdd_out, int* overflow,
-                                              unsigned long long* prof) {
+                                              float pgs_tol, bool warm, int lcp_solves, float* qdd_out, int* overflow,
+                                              int* unconverged, unsigned long long* prof) {
     const int lane = lane_id();
     const int NV = 6 + N;
     MW_PROF_T(t0);
@@ -684,6 +690,32 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             wave_pgs<MAXN, true>(L, a, x, Rpad, ncr, mu, pgs_iters, pgs_tol);
         else
             wave_pgs<MAXN, false>(L, a, x, Rpad, ncr, mu, pgs_iters, 0.f);
+        if (lcp_solves > 0) {
+            // exact boxed LCP from the PGS impulses (wave_lcp.hpp; oracle
+            // OR_PGS_CONVERGED): lane r = row r
+            LcpRow Rw;
+            Rw.live = lane < R;
+            const F4 c = L.rc[lane < Rpad ? lane : 0];
+            Rw.kind = (lane < ncr) ? ((lane % 3 == 0) ? 0 : 1) : 2;
+            Rw.nrow = (Rw.kind == 1) ? lane - lane % 3 : lane;
+            Rw.b = Rw.live ? c.x : 0.f;
+            Rw.lo = Rw.live ? c.z : 0.f;
+            Rw.hi = Rw.live ? c.w : 0.f;
+            float xe = 0.f;
+#pragma unroll
+            for (int r = 0; r < kWaveMaxRows; ++r) xe = (lane == r && r < R) ? x[r] : xe;
+            // the elimination's pivot rows go to the responses' stack (dead here)
+            static_assert(sizeof(L.stack) >= kWaveMaxRows * kLcpUStride * sizeof(float), "LCP workspace");
+            float* U = &L.stack[0][0][0];
+            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, U, xe)
+                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, U, xe);
+#pragma unroll
+            for (int r = 0; r < kWaveMaxRows; ++r) {
+                if ((r & 7) == 0 && r >= Rpad) break;
+                x[r] = read_lane(xe, r);
+            }
+            if (!ok) MW_LANE0 { *unconverged += 1; }
+        }
         MW_PROF_T(t5);
         MW_PROF_ACC(5, t4, t5);
         // ---- nu += MJ^T x (lane = component); impulses to the slots ----------------

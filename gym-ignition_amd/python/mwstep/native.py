@@ -23,6 +23,9 @@ MODE_VELOCITY_FOLLOWER_DART, MODE_POSITION, MODE_POSITION_INTERPOLATED = 4, 5, 6
 
 JOINT_INVALID, JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_BALL = 0, 1, 2, 3, 4
 
+LCP_PGS = 0
+LCP_EXACT = 1
+
 PARAM_COULOMB_FRICTION = 0
 PARAM_VISCOUS_FRICTION = 1
 PARAM_MAX_GENERALIZED_FORCE = 2
@@ -99,6 +102,9 @@ SIGNATURES = [
     ("mw_model_export_base", ctypes.c_int, [_P, _D]),
     ("mw_set_pgs_options", ctypes.c_int, [_P, ctypes.c_double, _I]),
     ("mw_pgs_options", ctypes.c_int, [_P, _D, _IP]),
+    ("mw_set_lcp_solver", ctypes.c_int, [_P, _I, _I]),
+    ("mw_lcp_solver", ctypes.c_int, [_P, _IP, _IP]),
+    ("mw_lcp_unconverged", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     ("mw_model_export_shapes", ctypes.c_int, [_P, _I, _D, _I, _IP]),
     ("mw_compile_collisions", ctypes.c_int, [_S, _D, _D, _I, _IP]),
     ("mw_device_params", ctypes.c_int, [_P, _P, _I]),
@@ -173,6 +179,9 @@ SCENE_SIGNATURES = [
     ("mw_scene_set_gravity", ctypes.c_int, [_P, _D]),
     ("mw_scene_gravity", ctypes.c_int, [_P, _D]),
     ("mw_scene_set_ground_plane", ctypes.c_int, [_P, _I, ctypes.c_double]),
+    ("mw_scene_set_world_gravity", ctypes.c_int, [_P, _I, _I, _D]),
+    ("mw_scene_world_gravity", ctypes.c_int, [_P, _I, _D]),
+    ("mw_scene_set_world_friction", ctypes.c_int, [_P, _I, _I, ctypes.c_double]),
     ("mw_scene_get_joints", ctypes.c_int, [_P, _I, _I, _I, _IP, _I, _D]),
     ("mw_scene_set_joints", ctypes.c_int, [_P, _I, _I, _I, _IP, _I, _D]),
     ("mw_scene_set_control_mode", ctypes.c_int, [_P, _I, _I, _IP, _I, _I]),

@@ -144,6 +144,24 @@ class Scene:
         a = np.ascontiguousarray(g, dtype=np.float64)
         N.check(N.lib().mw_scene_set_gravity(self.handle, N.dptr(a)), "set_gravity")
 
+    def set_world_gravity(self, g: Sequence[float], w0: int = 0, nw: Optional[int] = None) -> None:
+        """World::setGravity of worlds [w0, w0 + nw) (each world its own gravity)."""
+        self._touch()
+        a = np.ascontiguousarray(g, dtype=np.float64)
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_scene_set_world_gravity(self.handle, w0, nw, N.dptr(a)), "set_world_gravity")
+
+    def world_gravity(self, w: int) -> List[float]:
+        g = np.zeros(3)
+        N.check(N.lib().mw_scene_world_gravity(self.handle, w, N.dptr(g)))
+        return g.tolist()
+
+    def set_world_friction(self, mu: float, w0: int = 0, nw: Optional[int] = None) -> None:
+        """Ground-plane friction coefficient of worlds [w0, w0 + nw)."""
+        self._touch()
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_scene_set_world_friction(self.handle, w0, nw, float(mu)), "set_world_friction")
+
     def set_ground_plane(self, enabled: bool = True, mu: float = 1.0) -> None:
         self._touch()
         N.check(N.lib().mw_scene_set_ground_plane(self.handle, 1 if enabled else 0, float(mu)), "set_ground_plane")

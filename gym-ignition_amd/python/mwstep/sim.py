@@ -285,6 +285,22 @@ class Simulator:
         N.check(N.lib().mw_pgs_options(self.handle, ctypes.byref(t), ctypes.byref(w)))
         return t.value, bool(w.value)
 
+    def set_lcp_solver(self, exact: bool = True, max_solves: int = 24) -> None:
+        """mw_set_lcp_solver: exact boxed LCP after the PGS sweeps (default) or the sweeps alone."""
+        N.check(N.lib().mw_set_lcp_solver(self.handle, N.LCP_EXACT if exact else N.LCP_PGS, int(max_solves)),
+                "set_lcp_solver")
+
+    def lcp_solver(self):
+        m, k = ctypes.c_int32(), ctypes.c_int32()
+        N.check(N.lib().mw_lcp_solver(self.handle, ctypes.byref(m), ctypes.byref(k)))
+        return m.value == N.LCP_EXACT, k.value
+
+    def lcp_unconverged(self) -> int:
+        """World-steps whose exact LCP solve ran out of its budget."""
+        v = ctypes.c_int64()
+        N.check(N.lib().mw_lcp_unconverged(self.handle, ctypes.byref(v)))
+        return v.value
+
     def float_kernel(self) -> int:
         """0: not an articulated floating model, 1: world-per-lane kernel, 2: world-per-wavefront kernel."""
         v = ctypes.c_int32()

@@ -1035,7 +1035,7 @@ class World:
             return False
         self._gravity = [float(g) for g in gravity]
         try:
-            self._simulator._set_gravity(self._gravity)
+            self._simulator._set_gravity(self, self._gravity)
         except RuntimeError as e:
             _err(str(e))
             return False
@@ -1188,7 +1188,6 @@ class GazeboSimulator:
         self._iterations = 0
         self._scene = None
         self._slots: List[tuple] = []   # per scene slot: (name, text, pose) of its current model
-        self._ground_mu = 1.0
 
     def step_size(self) -> float:
         return self._step_size
@@ -1301,19 +1300,14 @@ class GazeboSimulator:
             self._scene.set_present(view.m, 0, view.w, 1)
 
     def _set_ground(self, world: World, enabled: bool, mu: float) -> None:
-        if enabled and mu != self._ground_mu:
-            # the plane's friction is scene-wide; keep the other worlds' planes
-            self._ground_mu = mu
-            grounds = [ww._ground_name is not None for ww in self._worlds.values()]
-            self._scene.set_ground_plane(True, mu)
-            for ww, g in zip(self._worlds.values(), grounds):
-                self._scene.set_world_ground(g, ww._index, 1)
+        # the plane's presence and friction are per world
+        if enabled:
+            self._scene.set_world_friction(mu, world._index, 1)
         self._scene.set_world_ground(enabled, world._index, 1)
 
-    def _set_gravity(self, g: List[float]) -> None:
-        if len(self._worlds) > 1:
-            _warn("the gravity of a batched simulator is shared by all of its worlds")
-        self._scene.set_gravity(g)
+    def _set_gravity(self, world: World, g: List[float]) -> None:
+        # World::setGravity: this world's Gravity component only (World.cpp:301-319)
+        self._scene.set_world_gravity(g, world._index, 1)
 
     def world_names(self) -> List[str]:
         return list(self._worlds.keys())

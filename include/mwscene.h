@@ -95,6 +95,13 @@ int mw_scene_run(mw_scene* sc, int32_t paused);
 int mw_scene_run_device(mw_scene* sc, int32_t runs);
 int mw_scene_time(const mw_scene* sc, double* seconds);
 int mw_scene_set_gravity(mw_scene* sc, const double g[3]);
+/* World::setGravity / gravity of single worlds (World.cpp:301-319: each world
+ * keeps its own Gravity component); mw_scene_set_gravity sets every world. */
+int mw_scene_set_world_gravity(mw_scene* sc, int32_t w0, int32_t nw, const double g[3]);
+int mw_scene_world_gravity(const mw_scene* sc, int32_t w, double g[3]);
+/* Friction coefficient of the ground plane of single worlds (every contact of
+ * those worlds uses it); mw_scene_set_ground_plane sets every world's. */
+int mw_scene_set_world_friction(mw_scene* sc, int32_t w0, int32_t nw, double mu);
 int mw_scene_gravity(const mw_scene* sc, double g[3]);
 /* the ground plane's friction, and the plane in (enabled) or out of every world */
 int mw_scene_set_ground_plane(mw_scene* sc, int32_t enabled, double mu);

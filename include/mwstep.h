@@ -223,6 +223,21 @@ int mw_reset_base_velocity(mw_sim* sim, int32_t w0, int32_t nw, const double* li
  * count from zero).  Other kernels ignore both. */
 int mw_set_pgs_options(mw_sim* sim, double tol, int32_t warm_start);
 int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
+/* The boxed-LCP solver of the world-per-wavefront kernel.  MW_LCP_EXACT
+ * (default, max_solves 24): after the PGS sweeps, the LCP is solved exactly
+ * -- semismooth Newton rounds on the coupled friction conditions, then the
+ * active-set method of the box QP with the friction boxes updated to their
+ * fixed point -- with at most max_solves dense linear solves (Gaussian
+ * elimination over the wave's lanes) per world-step; DART's primary solver is
+ * Dantzig's exact pivoting method [EXT], reached from ForwardStep
+ * (Physics.cpp:1824-1835).  MW_LCP_PGS: the PGS sweeps alone. */
+#define MW_LCP_PGS 0
+#define MW_LCP_EXACT 1
+int mw_set_lcp_solver(mw_sim* sim, int32_t mode, int32_t max_solves);
+int mw_lcp_solver(const mw_sim* sim, int32_t* mode, int32_t* max_solves);
+/* World-steps whose exact LCP solve ran out of budget since mw_initialize
+ * (they keep the best feasible impulses found; 0 = every solve converged). */
+int mw_lcp_unconverged(const mw_sim* sim, int64_t* world_steps);
 /* The world's ground plane (z = 0, normal +z) and its friction coefficient. */
 int mw_set_ground_plane(mw_sim* sim, int32_t enabled, double mu);
 /* Model::enableContacts / contactsEnabled (Model.cpp:674-700). */

@@ -429,13 +429,34 @@ void or_rnea(const or_model* m, const double* q, const double* qd,
  * latest solve, and its final complementarity residual. */
 #define OR_PGS_WARM 300
 #define OR_LCP_MAXN (3 * OR_MAXFC + 3 * OR_MAXB > 3 * OR_MAXCONTACTS ? 3 * OR_MAXFC + 3 * OR_MAXB : 3 * OR_MAXCONTACTS)
-static int g_pgs_sweeps = 0;
-static double g_pgs_delta = 0.0;
+static _Thread_local int g_pgs_sweeps = 0;
+static _Thread_local double g_pgs_delta = 0.0;
 
 void or_pgs_stats(int* sweeps, double* last_delta)
 {
     if (sweeps) *sweeps = g_pgs_sweeps;
     if (last_delta) *last_delta = g_pgs_delta;
+}
+
+/* Test hook: a copy of the latest floating-tree LCP (rows, Delassus matrix
+ * with CFM, rhs, bounds, row kinds 0 normal / 1 friction / 2 box, the friction
+ * coefficient) and the impulses the solve returned -- lets tests/ replay the
+ * exact problem the kernels solve (tests/test_lcp_exact.py). */
+#define OR_CAP_MAXN (3 * OR_MAXFC + 3 * OR_MAXB)
+static _Thread_local double g_cap_A[OR_CAP_MAXN * OR_CAP_MAXN], g_cap_b[OR_CAP_MAXN], g_cap_lo[OR_CAP_MAXN],
+    g_cap_hi[OR_CAP_MAXN], g_cap_x[OR_CAP_MAXN], g_cap_mu;
+static _Thread_local int g_cap_kind[OR_CAP_MAXN], g_cap_n = 0;
+
+int or_lcp_last(int cap, double* A, double* b, double* lo, double* hi, int* kind, double* x, double* mu)
+{
+    const int n = g_cap_n;
+    if (n > cap) return -n;
+    for (int r = 0; r < n; ++r) {
+        for (int c = 0; c < n; ++c) A[r * n + c] = g_cap_A[r * n + c];
+        b[r] = g_cap_b[r]; lo[r] = g_cap_lo[r]; hi[r] = g_cap_hi[r]; kind[r] = g_cap_kind[r]; x[r] = g_cap_x[r];
+    }
+    *mu = g_cap_mu;
+    return n;
 }
 
 static int pgs_budget(int iters) { return iters >= 0 ? iters : OR_PGS_WARM; }
@@ -521,7 +542,7 @@ static double lcp_residual(int n, const double* A, int lda, const double* b, con
 static int boxqp_solve(int n, const double* A, int lda, const double* b, const double* L, const double* U,
                        double* x)
 {
-    static double K[OR_LCP_MAXN * OR_LCP_MAXN];
+    static _Thread_local double K[OR_LCP_MAXN * OR_LCP_MAXN];
     double g[OR_LCP_MAXN], c[OR_LCP_MAXN], d[OR_LCP_MAXN];
     int fidx[OR_LCP_MAXN], ws[OR_LCP_MAXN]; /* ws: 0 free, 1 held at L, 2 held at U */
     for (int r = 0; r < n; ++r) {
@@ -604,10 +625,18 @@ static int boxqp_solve(int n, const double* A, int lda, const double* b, const d
 static void lcp_refine(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
                        const int* findex, double mu, double* x)
 {
-    double L[OR_LCP_MAXN], U[OR_LCP_MAXN], prev[OR_LCP_MAXN];
+    double L[OR_LCP_MAXN], U[OR_LCP_MAXN], prev[OR_LCP_MAXN], nb[OR_LCP_MAXN];
     int round = 0, failed = 0;
-    for (; round < 100; ++round) {
-        for (int r = 0; r < n; ++r) row_bounds(r, lo, hi, findex, mu, x, &L[r], &U[r]);
+    /* nb: the normal impulses the friction boxes are built from.  The first
+     * rounds take the latest normals (plain staggering); a fixed point the
+     * plain iteration circles (a period-2 cycle of two boxes) is reached by
+     * averaging: nb <- (nb + x) / 2 after round 20.  Either way the fixed
+     * point is x_n = nb, the coupled conditions. */
+    for (int r = 0; r < n; ++r) nb[r] = x[r];
+    for (; round < 400; ++round) {
+        const double om = round < 20 ? 1.0 : 0.5;
+        for (int r = 0; r < n; ++r) nb[r] = round == 0 ? x[r] : om * x[r] + (1.0 - om) * nb[r];
+        for (int r = 0; r < n; ++r) row_bounds(r, lo, hi, findex, mu, nb, &L[r], &U[r]);
         for (int r = 0; r < n; ++r) {  /* a negative normal cannot occur: x_n >= 0 */
             if (L[r] > U[r]) { const double t = L[r]; L[r] = U[r]; U[r] = t; }
             prev[r] = x[r];
@@ -618,7 +647,12 @@ static void lcp_refine(int n, const double* A, int lda, const double* b, const d
             dmax = fabs(x[r] - prev[r]) > dmax ? fabs(x[r] - prev[r]) : dmax;
             xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
         }
-        if (dmax <= 1e-14 * (1.0 + xm)) { ++round; break; }
+        if (dmax <= 1e-14 * (1.0 + xm)) {
+            /* x solved the QP of its own boxes: done when nb = x_n */
+            double dn = 0.0;
+            for (int r = 0; r < n; ++r) dn = fabs(x[r] - nb[r]) > dn ? fabs(x[r] - nb[r]) : dn;
+            if (dn <= 1e-13 * (1.0 + xm)) { ++round; break; }
+        }
     }
     double xm = 0.0;
     for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
@@ -1481,7 +1515,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
     or_fkin k;
     float_kin(m, s, &k);
 
-    static double M[(6 + OR_MAXB) * (6 + OR_MAXB)];
+    static _Thread_local double M[(6 + OR_MAXB) * (6 + OR_MAXB)];
     double h[6 + OR_MAXB], rhs[6 + OR_MAXB], acc[6 + OR_MAXB], nu[6 + OR_MAXB];
     or_float_dynamics(m, s, M, h);
     double Mi[(6 + OR_MAXB) * (6 + OR_MAXB)];
@@ -1545,9 +1579,9 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
 
     /* rows: J, rhs, bounds kind */
     enum { K_NORMAL, K_FRIC, K_BOX };
-    static double J[3 * OR_MAXFC + 3 * OR_MAXB][6 + OR_MAXB];
-    static double MJ[3 * OR_MAXFC + 3 * OR_MAXB][6 + OR_MAXB];
-    static double A[(3 * OR_MAXFC + 3 * OR_MAXB) * (3 * OR_MAXFC + 3 * OR_MAXB)];
+    static _Thread_local double J[3 * OR_MAXFC + 3 * OR_MAXB][6 + OR_MAXB];
+    static _Thread_local double MJ[3 * OR_MAXFC + 3 * OR_MAXB][6 + OR_MAXB];
+    static _Thread_local double A[(3 * OR_MAXFC + 3 * OR_MAXB) * (3 * OR_MAXFC + 3 * OR_MAXB)];
     double bb[3 * OR_MAXFC + 3 * OR_MAXB], lo[3 * OR_MAXFC + 3 * OR_MAXB], hi[3 * OR_MAXFC + 3 * OR_MAXB];
     double cfm[3 * OR_MAXFC + 3 * OR_MAXB], x[3 * OR_MAXFC + 3 * OR_MAXB];
     int kind[3 * OR_MAXFC + 3 * OR_MAXB];
@@ -1642,6 +1676,15 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
             A[r * nr + r] *= 1.0 + cfm[r];
             x[r] = warm ? warm[wid[r]] : 0.0;
         }
+        g_cap_n = nr;
+        g_cap_mu = m->mu;
+        for (int r = 0; r < nr; ++r) {
+            for (int c = 0; c < nr; ++c) g_cap_A[r * nr + c] = A[r * nr + c];
+            g_cap_b[r] = bb[r];
+            g_cap_kind[r] = kind[r];
+            g_cap_lo[r] = kind[r] == K_BOX ? lo[r] : (kind[r] == K_NORMAL ? 0.0 : -INFINITY);
+            g_cap_hi[r] = kind[r] == K_BOX ? hi[r] : INFINITY;
+        }
         g_pgs_sweeps = 0;
         for (int it = 0; it < pgs_budget(pgs_iters); ++it) {
             double x_start[3 * OR_MAXFC + 3 * OR_MAXB];
@@ -1682,6 +1725,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
             }
             lcp_refine(nr, A, nr, bb, lo, hi, findex, m->mu, x);
         }
+        for (int r = 0; r < nr; ++r) g_cap_x[r] = x[r];
         for (int r = 0; r < nr; ++r)
             for (int e = 0; e < nv; ++e) nu[e] += MJ[r][e] * x[r];
     }
@@ -2216,7 +2260,7 @@ int or_collide(int type_a, const double* size_a, const double* c_a, const double
 /* dense solve with pivoting for the scene (n <= OR_SC_MAXNV) */
 static void scene_solve(int n, const double* A_in, const double* b, double* x)
 {
-    static double A[OR_SC_MAXNV * OR_SC_MAXNV];
+    static _Thread_local double A[OR_SC_MAXNV * OR_SC_MAXNV];
     double y[OR_SC_MAXNV];
     memcpy(A, A_in, (size_t)n * n * sizeof(double));
     memcpy(y, b, (size_t)n * sizeof(double));
@@ -2234,7 +2278,7 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
                   const double* cmd, const double* wrench, int pgs_iters, double* c_out, int32_t* c_who)
 {
     const int K = sm->n_models;
-    static or_fkin kin[OR_SC_MAXM];
+    static _Thread_local or_fkin kin[OR_SC_MAXM];
     int off[OR_SC_MAXM], nbase[OR_SC_MAXM];
     int NV = 0;
     for (int m = 0; m < K; ++m) {
@@ -2244,14 +2288,14 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
         float_kin(&sm->model[m], &st->s[m], &kin[m]);
     }
     /* block-diagonal M, h; rhs with damping, commands and wrenches */
-    static double M[OR_SC_MAXNV * OR_SC_MAXNV], Mi[OR_SC_MAXNV * OR_SC_MAXNV];
+    static _Thread_local double M[OR_SC_MAXNV * OR_SC_MAXNV], Mi[OR_SC_MAXNV * OR_SC_MAXNV];
     double rhs[OR_SC_MAXNV], acc[OR_SC_MAXNV], nu[OR_SC_MAXNV];
     for (int e = 0; e < NV * NV; ++e) M[e] = 0.0;
     for (int m = 0; m < K; ++m) {
         const or_float_model* fm = &sm->model[m];
         const or_model* t = &fm->tree;
         const int n = t->n, nvm = 6 + n, nb = nbase[m], o = off[m];
-        static double Mm[(6 + OR_MAXB) * (6 + OR_MAXB)];
+        static _Thread_local double Mm[(6 + OR_MAXB) * (6 + OR_MAXB)];
         double hm[6 + OR_MAXB];
         or_float_model tmp = *fm;
         for (int r = 0; r < 3; ++r) tmp.gravity[r] = sm->gravity[r];
@@ -2389,12 +2433,12 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
     /* ---- rows: contacts (normal, t1, t2), then joint rows model by model ---- */
     enum { K_NORMAL, K_FRIC, K_BOX };
     const int maxr = 3 * OR_SC_MAXC + 3 * OR_MAXB;
-    static double J[3 * OR_SC_MAXC + 3 * OR_MAXB][OR_SC_MAXNV];
-    static double MJ[3 * OR_SC_MAXC + 3 * OR_MAXB][OR_SC_MAXNV];
-    static double A[(3 * OR_SC_MAXC + 3 * OR_MAXB) * (3 * OR_SC_MAXC + 3 * OR_MAXB)];
-    static double bb[3 * OR_SC_MAXC + 3 * OR_MAXB], lo[3 * OR_SC_MAXC + 3 * OR_MAXB],
+    static _Thread_local double J[3 * OR_SC_MAXC + 3 * OR_MAXB][OR_SC_MAXNV];
+    static _Thread_local double MJ[3 * OR_SC_MAXC + 3 * OR_MAXB][OR_SC_MAXNV];
+    static _Thread_local double A[(3 * OR_SC_MAXC + 3 * OR_MAXB) * (3 * OR_SC_MAXC + 3 * OR_MAXB)];
+    static _Thread_local double bb[3 * OR_SC_MAXC + 3 * OR_MAXB], lo[3 * OR_SC_MAXC + 3 * OR_MAXB],
         hi[3 * OR_SC_MAXC + 3 * OR_MAXB], cfm[3 * OR_SC_MAXC + 3 * OR_MAXB], x[3 * OR_SC_MAXC + 3 * OR_MAXB];
-    static int kind[3 * OR_SC_MAXC + 3 * OR_MAXB];
+    static _Thread_local int kind[3 * OR_SC_MAXC + 3 * OR_MAXB];
     (void)maxr;
     int nr = 0;
     double tb1[OR_SC_MAXC][3], tb2[OR_SC_MAXC][3];
@@ -2520,7 +2564,7 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
             pgs_count(it);
         }
         if (pgs_iters < 0) {
-            static int findex[3 * OR_SC_MAXC + 3 * OR_MAXB];
+            static _Thread_local int findex[3 * OR_SC_MAXC + 3 * OR_MAXB];
             for (int r = 0; r < nr; ++r) findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
             lcp_refine(nr, A, nr, bb, lo, hi, findex, sm->mu, x);
         }
@@ -2562,4 +2606,47 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
         if (c_who) memcpy(c_who + 4 * c, who[c], sizeof who[c]);
     }
     return nc;
+}
+
+/* ------------------------------------------------------------------ */
+/* CPU-baseline rollouts (bench.py's cpu_baseline of BASELINE configs 4 */
+/* and 5): T engine steps under the JointController PID hold, in C so   */
+/* the timing is the oracle's physics, not Python.  Error = q - target  */
+/* (JointController.cpp:308), the PID every step (period = dt).         */
+/* ------------------------------------------------------------------ */
+
+/* W fixed-base worlds [W][n]: targets q0 + amp sin(2 pi freq t). */
+void or_pid_rollout(const or_model* m, double dt, int W, int T, double* q, double* qd, const double* q0,
+                    const double* amp, double freq, const or_pid_gains* g, or_pid_state* st, int pgs_iters)
+{
+    const int n = m->n;
+    int32_t mode[OR_MAXB];
+    double tau[OR_MAXB], qdd[OR_MAXB], frc[OR_MAXB];
+    for (int i = 0; i < n; ++i) mode[i] = OR_FORCE;
+    for (int t = 0; t < T; ++t) {
+        const double s = sin(2.0 * OR_PI * freq * (t + 1) * dt);
+        for (int w = 0; w < W; ++w) {
+            double* qw = q + (size_t)w * n;
+            double* qdw = qd + (size_t)w * n;
+            for (int i = 0; i < n; ++i)
+                tau[i] = or_pid_update(&g[i], &st[(size_t)w * n + i], qw[i] - (q0[(size_t)w * n + i] + amp[i] * s), dt);
+            or_step(m, dt, qw, qdw, mode, tau, pgs_iters, qdd, frc);
+        }
+    }
+}
+
+/* One floating-base world, targets fixed (the humanoid's PID hold). */
+void or_float_pid_rollout(const or_float_model* m, double dt, int T, or_float_state* s, const double* target,
+                          const or_pid_gains* g, or_pid_state* st, int pgs_iters)
+{
+    const int n = m->tree.n;
+    int32_t mode[OR_MAXB];
+    double tau[OR_MAXB];
+    static _Thread_local double cp[3 * OR_MAXFC], cf[3 * OR_MAXFC], cd[OR_MAXFC];
+    static _Thread_local int32_t cb[OR_MAXFC];
+    for (int i = 0; i < n; ++i) mode[i] = OR_FORCE;
+    for (int t = 0; t < T; ++t) {
+        for (int i = 0; i < n; ++i) tau[i] = or_pid_update(&g[i], &st[i], s->q[i] - target[i], dt);
+        or_float_step(m, dt, s, mode, tau, pgs_iters, cp, cf, cd, cb);
+    }
 }

@@ -89,6 +89,8 @@ int or_step(const or_model* m, double dt, double* q, double* qd,
 void or_pgs(int n, const double* A, const double* b, const double* lo,
             const double* hi, double* x, int iters);
 void or_pgs_stats(int* sweeps, double* last_delta);
+/* test hook: the latest floating-tree LCP and its solution (n rows, or -n if cap < n) */
+int or_lcp_last(int cap, double* A, double* b, double* lo, double* hi, int* kind, double* x, double* mu);
 
 /* Joint PID of the ScenarI/O JointController (Position / Velocity modes,
  * cpp/scenario/plugins/JointController/JointController.cpp:129-190). */
@@ -194,6 +196,14 @@ int or_float_step(const or_float_model* m, double dt, or_float_state* s, const i
 int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, const int32_t* mode,
                        const double* cmd, int pgs_iters, double pgs_tol, double* warm, double* c_pos,
                        double* c_force, double* c_depth, int32_t* c_body);
+
+/* CPU-baseline rollouts under the JointController PID hold (bench.py):
+ * W fixed-base worlds (q, qd, q0, PID states [W][n]; targets
+ * q0 + amp sin(2 pi freq t)), or one floating-base world (fixed targets). */
+void or_pid_rollout(const or_model* m, double dt, int W, int T, double* q, double* qd, const double* q0,
+                    const double* amp, double freq, const or_pid_gains* g, or_pid_state* st, int pgs_iters);
+void or_float_pid_rollout(const or_float_model* m, double dt, int T, or_float_state* s, const double* target,
+                          const or_pid_gains* g, or_pid_state* st, int pgs_iters);
 
 /* Floating-base mass matrix ((6+n)^2, row-major) and bias h (gravity +
  * velocity products) at a state (test cross-checks). */

@@ -184,6 +184,10 @@ def lib():
                                     D, I32]
         L.or_scene_step.restype = ctypes.c_int
         L.or_float_dynamics.argtypes = [FM, FS, D, D]
+        G, PS = ctypes.POINTER(OrPidGains), ctypes.POINTER(OrPidState)
+        L.or_pid_rollout.argtypes = [M, ctypes.c_double, ctypes.c_int, ctypes.c_int, D, D, D, D, ctypes.c_double,
+                                     G, PS, ctypes.c_int]
+        L.or_float_pid_rollout.argtypes = [FM, ctypes.c_double, ctypes.c_int, FS, D, G, PS, ctypes.c_int]
         L.or_pid_update.argtypes = [ctypes.POINTER(OrPidGains), ctypes.POINTER(OrPidState),
                                     ctypes.c_double, ctypes.c_double]
         L.or_pid_update.restype = ctypes.c_double
@@ -1264,6 +1268,45 @@ def pgs_stats():
     n, d = ctypes.c_int(0), ctypes.c_double(0.0)
     lib().or_pgs_stats(ctypes.byref(n), ctypes.byref(d))
     return n.value, d.value
+
+
+def pid_rollout(cm: ChainModel, q, qd, q0, amp, freq, gains, T, dt=1e-3, pgs_iters=20, states=None):
+    """T steps of W fixed-base worlds under the JointController PID (or_pid_rollout,
+    C; releases the GIL): q, qd [W, n] updated in place; targets q0 + amp sin(2 pi f t)."""
+    W, n = q.shape
+    g = (OrPidGains * n)(*gains)
+    st = states if states is not None else (OrPidState * (W * n))()
+    lib().or_pid_rollout(ctypes.byref(cm.model), dt, W, T, _p(q), _p(qd), _p(np.ascontiguousarray(q0)),
+                         _p(np.ascontiguousarray(amp, dtype=float)), freq, g, st, pgs_iters)
+    return st
+
+
+def float_pid_rollout(fw: "FloatWorld", target, gains, T, states=None):
+    """T steps of one FloatWorld under the PID hold (or_float_pid_rollout, C)."""
+    n = fw.cm.n
+    g = (OrPidGains * n)(*gains)
+    st = states if states is not None else (OrPidState * n)()
+    lib().or_float_pid_rollout(ctypes.byref(fw.m), fw.dt, T, ctypes.byref(fw.s),
+                               _p(np.ascontiguousarray(target, dtype=float)), g, st, fw.pgs)
+    return st
+
+
+def lcp_last():
+    """The latest floating-tree LCP the oracle solved (test hook): dict of the
+    Delassus matrix A (with CFM), rhs b, bounds lo/hi (friction rows: +-inf,
+    bounded by mu x_normal), row kinds (0 normal, 1 friction, 2 box), mu and
+    the solution x the step used; None when the step had no rows."""
+    cap = 3 * 8 * 16 + 3 * 48
+    A = np.zeros(cap * cap)
+    b, lo, hi, x = (np.zeros(cap) for _ in range(4))
+    kind = np.zeros(cap, np.int32)
+    mu = ctypes.c_double(0.0)
+    n = lib().or_lcp_last(cap, _p(A), _p(b), _p(lo), _p(hi), kind.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          _p(x), ctypes.byref(mu))
+    if n <= 0:
+        return None
+    return dict(A=A[:n * n].reshape(n, n).copy(), b=b[:n].copy(), lo=lo[:n].copy(), hi=hi[:n].copy(),
+                kind=kind[:n].copy(), mu=mu.value, x=x[:n].copy())
 
 
 def pgs(A, b, lo, hi, iters=100):

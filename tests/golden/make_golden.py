@@ -74,7 +74,7 @@ def humanoid():
     from mwstep import get_model_file
     cm = pyoracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, HUMANOID_Z))
     names = list(cm.joint_names)
-    ow = pyoracle.FloatWorld(cm, pgs_iters=50)
+    ow = pyoracle.FloatWorld(cm, pgs_iters=pyoracle.PGS_CONVERGED)  # the wave kernel's exact LCP
     n = cm.n
     gains = humanoid_gains(names)
     og = [pyoracle.pid_gains(p, 0.0, d, cmdmax=80.0, cmdmin=-80.0) for p, d in gains]

@@ -168,6 +168,60 @@ def test_multi_world_is_one_batched_scene(require_gpu):
     gazebo.close()
 
 
+def _ground_plane_sdf(mu):
+    return ('<sdf version="1.6"><model name="ground_plane"><static>true</static><link name="link">'
+            '<collision name="collision"><geometry><plane><normal>0 0 1</normal><size>100 100</size></plane>'
+            f'</geometry><surface><friction><ode><mu>{mu}</mu></ode></friction></surface></collision>'
+            '</link></model></sdf>')
+
+
+def test_per_world_gravity_and_ground_friction(require_gpu):
+    """World::setGravity and the ground plane's friction act on their own world
+    only (World.cpp:301-319: each world of a server keeps its own Gravity
+    component), although all worlds of the simulator are one batched scene:
+    free-falling cubes fall with their world's gravity (z = z0 - g t^2 / 2
+    under semi-implicit Euler), a cube pushed sideways on the ground slides
+    to rest sooner on the rougher plane."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    names = ["low", "earth", "rough"]
+    gazebo, get_model_file = _gazebo(names)
+    grav = {"low": -1.62, "earth": -9.8, "rough": -9.8}
+    for n in names:
+        w = gazebo.get_world(n)
+        assert w.set_physics_engine(scenario.PhysicsEngine_dart)
+        assert w.set_gravity([0.0, 0.0, grav[n]])
+    for n in names:
+        assert gazebo.get_world(n).gravity() == pytest.approx([0.0, 0.0, grav[n]])
+    for n in ("low", "earth"):
+        assert gazebo.get_world(n).insert_model(get_model_file("cube"), core.Pose([0, 0, 5.0], [1., 0, 0, 0]), "c")
+    T = 200
+    for _ in range(T):
+        assert gazebo.run()
+    dt = 1e-3
+    for n in ("low", "earth"):
+        z = gazebo.get_world(n).get_model("c").base_position()[2]
+        # semi-implicit Euler from rest: z_T = z0 + g dt^2 T (T + 1) / 2
+        assert z == pytest.approx(5.0 + grav[n] * dt * dt * T * (T + 1) / 2, abs=1e-4), n
+    gazebo.close()
+    # friction per world: the same push on two planes of different mu
+    gazebo, get_model_file = _gazebo(["smooth", "rough"])
+    for n, mu in (("smooth", 0.1), ("rough", 0.8)):
+        w = gazebo.get_world(n)
+        assert w.set_physics_engine(scenario.PhysicsEngine_dart)
+        assert w.insert_model(_ground_plane_sdf(mu))
+        assert w.insert_model(get_model_file("cube"), core.Pose([0, 0, 0.1], [1., 0, 0, 0]), "c")
+        assert w.get_model("c").to_gazebo().reset_base_world_velocity([1.0, 0, 0], [0, 0, 0])
+    for _ in range(300):
+        assert gazebo.run()
+    v = {n: gazebo.get_world(n).get_model("c").base_world_linear_velocity()[0] for n in ("smooth", "rough")}
+    x = {n: gazebo.get_world(n).get_model("c").base_position()[0] for n in ("smooth", "rough")}
+    # Coulomb deceleration mu g: after 0.3 s the smooth cube still slides at ~1 - 0.1 * 9.8 * 0.3
+    assert v["smooth"] == pytest.approx(1.0 - 0.1 * 9.8 * 0.3, abs=0.05)
+    assert abs(v["rough"]) < 1e-3 and x["rough"] < x["smooth"]
+    gazebo.close()
+
+
 def test_world_api_with_sdf_model(require_gpu):
     """tests/test_scenario/test_world.py:73-146 (test_world_api): gravity,
     model names, default / custom names and poses, URDF file and string, the

@@ -428,7 +428,9 @@ def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
     sq, sqd = sim.get("q"), sim.get("qd")
     wq = wqd = 0.0
     for w in range(W):
-        oq, oqd, *_ = oracle.step(cm, 1e-3, q[w], qd[w], np.full(n, oracle.FORCE, np.int32), tau[w], 50)
+        # mw_sim's wave kernel solves the joint-row LCP exactly (wave_lcp.hpp)
+        oq, oqd, *_ = oracle.step(cm, 1e-3, q[w], qd[w], np.full(n, oracle.FORCE, np.int32), tau[w],
+                                  oracle.PGS_CONVERGED)
         wq = max(wq, float(np.abs(sq[w] - oq).max()))
         wqd = max(wqd, float(np.abs(sqd[w] - oqd).max()))
     print(f"fixed 16-joint tree through mw_sim (wave kernel, welded base): max|dq| {wq:.2e}, max|dqd| {wqd:.2e}")

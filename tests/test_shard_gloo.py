@@ -27,14 +27,17 @@ def _worker(rank, ws, port, n_global, q):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     b, e = shard_range(n_global, rank, ws)
     obs = torch.arange(b, e, dtype=torch.float32).repeat_interleave(4).reshape(-1, 4)
-    g = gather_obs(obs)
+    g = gather_obs(obs, n_global=n_global)
+    g2 = gather_obs(obs)  # slab sizes gathered first
+    assert torch.equal(g, g2)
     q.put((rank, b, e, g.numpy().tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gather_obs_world_order():
-    ws, n = 2, 10
+@pytest.mark.parametrize("ws,n", [(2, 10), (3, 1024), (2, 7)])
+def test_gather_obs_world_order(ws, n):
+    """Equal and unequal slabs (1024 worlds over 3 ranks: 342 / 341 / 341)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -46,7 +49,8 @@ def test_gather_obs_world_order():
         p.join(timeout=120)
         assert p.exitcode == 0
     res.sort()
-    assert [(b, e) for _, b, e, _ in res] == [(0, 5), (5, 10)]
+    from mwstep.shard import shard_range
+    assert [(b, e) for _, b, e, _ in res] == [shard_range(n, r, ws) for r in range(ws)]
     expect = [[float(w)] * 4 for w in range(n)]
     for _, _, _, g in res:
         assert g == expect
