@@ -104,6 +104,8 @@ struct mw_scene {
     int32_t* h_overflow = nullptr;  // pinned copy of the device drop counter
     float* h_wphys = nullptr;       // pinned mirror of d_wphys (uploaded with the presence words)
     int64_t overflow_seen = 0;      // drops already reported
+    int32_t lcp_mode = MW_LCP_EXACT;  // mw_scene_set_lcp_solver
+    int32_t lcp_solves = 24;
     mw::PidF* h_pid = nullptr;
     size_t jrows = 0;              // NBMAX * W
     // host-only component data
@@ -757,13 +759,18 @@ int mw_scene_replace_model(mw_scene* s, int32_t model, const char* urdf, const d
     sm.period_ns = std::numeric_limits<int64_t>::max();
     sm.prev_ns = 0;
     sm.stepped = false;
+    // commit only when the parameter block builds: on failure the slot keeps
+    // its previous model (name, tree and device parameters stay consistent)
+    SceneModel prev = old;
     old = sm;
     try {
         build_params(s);
     } catch (const std::exception& e) {
+        s->models[model] = prev;
+        try { build_params(s); } catch (const std::exception&) {}
         return fail(MW_EPARSE, e.what());
     }
-    for (int i = 0; i < cm.dofs(); ++i) s->pid[old.body0 + i] = kDefaultPid;
+    for (int i = 0; i < cm.dofs(); ++i) s->pid[s->models[model].body0 + i] = kDefaultPid;
     s->params_dirty = s->pid_dirty = true;
     return MW_OK;
 }
@@ -875,6 +882,7 @@ static int scene_run(mw_scene* s, int32_t paused, bool defer) {
     a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
     a.paused = paused ? 1 : 0;
     a.pgs_iters = s->cfg.pgs_iters;
+    a.lcp_solves = s->lcp_solves;
     a.first = 1;
     a.want_contacts = 1;
     const int spr = s->cfg.steps_per_run;
@@ -1344,6 +1352,34 @@ int mw_scene_apply_world_wrench(mw_scene* s, int32_t model, int32_t link, int32_
                 static_cast<float>(wrench[(w - w0) * 6 + e]);
     }
     s->wrench_dirty = true;
+    return MW_OK;
+}
+
+int mw_scene_set_lcp_solver(mw_scene* s, int32_t mode, int32_t max_solves) {
+    if (int rc = check(s)) return rc;
+    if (mode != MW_LCP_PGS && mode != MW_LCP_EXACT) return fail(MW_EINVAL, "unknown LCP solver mode");
+    if (mode == MW_LCP_EXACT && (max_solves < 1 || max_solves > 256))
+        return fail(MW_EINVAL, "the exact solve's budget must be 1..256 linear solves per step");
+    s->lcp_mode = mode;
+    s->lcp_solves = (mode == MW_LCP_EXACT) ? max_solves : 0;
+    return MW_OK;
+}
+
+int mw_scene_lcp_solver(const mw_scene* s, int32_t* mode, int32_t* max_solves) {
+    if (int rc = check(s)) return rc;
+    if (!mode || !max_solves) return fail(MW_EINVAL, "null argument");
+    *mode = s->lcp_mode;
+    *max_solves = s->lcp_solves;
+    return MW_OK;
+}
+
+int mw_scene_lcp_unconverged(const mw_scene* s, int64_t* world_steps) {
+    if (int rc = check(s)) return rc;
+    if (!world_steps) return fail(MW_EINVAL, "null argument");
+    int v[2] = {0, 0};
+    SC_HIP(hipMemcpyAsync(v, s->dev.overflow, 2 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    SC_HIP(hipStreamSynchronize(s->stream));
+    *world_steps = v[1];
     return MW_OK;
 }
 

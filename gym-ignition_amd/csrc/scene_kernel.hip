@@ -392,7 +392,12 @@ __device__ __forceinline__ bool sc_inside(int type, f3 h, f3 c, const M3& R, f3 
 // poses in box / sphere / chain piles that never reach this function
 // (tests/test_gpu_scene.py test_one_step_parity_random_piles), so the register
 // allocation of the main kernel is left as it was without it.
-__device__ __noinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& Ra, int tb, f3 hb, f3 cb,
+#ifdef MW_SC_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& Ra, int tb, f3 hb, f3 cb,
                                                 const M3& Rb, f3& n, f3* pts, float* deps) {
     f3 ax[6];
     int na = sc_axes(ta, ca, Ra, cb, ax);
@@ -583,12 +588,53 @@ __device__ __forceinline__ float sc_dof_force(const SceneF* __restrict__ P, cons
     return tau;
 }
 
+// Debug builds (EXTRA=-DMW_SC_NANCHECK): after each phase of a step, the
+// first non-finite value of the node records, coordinates and contacts of a
+// world is printed (bit test of the exponent: -ffinite-math-only folds isfinite)
+#ifdef MW_SC_NANCHECK
+__device__ __forceinline__ bool sc_bad(float v) { return (__float_as_uint(v) & 0x7f800000u) == 0x7f800000u; }
+template <int MAXNV>
+__device__ void sc_nancheck(const SceneF* __restrict__ P, const ScWorld<MAXNV>& L, int phase, int nc, bool& reported) {
+    const int lane = lane_id();
+    int what = -1;
+    float val = 0.f;
+    if (lane < P->n_nodes) {
+        const ScNode& nd = L.node[lane];
+        const float* f = reinterpret_cast<const float*>(&nd);
+        for (int k = 0; k < 38; ++k)
+            if (sc_bad(f[k])) { what = k; val = f[k]; break; }
+    }
+    if (what < 0 && lane < P->nv && sc_bad(L.nu[lane])) { what = 100; val = L.nu[lane]; }
+    if (what < 0 && lane < nc) {
+        for (int k = 0; k < 3; ++k)
+            if (sc_bad(L.c_p[lane][k]) || sc_bad(L.c_n[lane][k])) { what = 200 + k; val = L.c_p[lane][k]; }
+        if (sc_bad(L.c_d[lane])) { what = 210; val = L.c_d[lane]; }
+    }
+    const uint64_t m = __ballot(what >= 0);
+    if (m && !reported) {
+        const int l = __builtin_ctzll(m);
+        if (lane == l)
+            printf("MW_SC_NANCHECK world %d phase %d lane %d field %d value %08x nc %d\n", (int)blockIdx.x, phase,
+                   lane, what, __float_as_uint(val), nc);
+        reported = true;
+    }
+}
+#define MW_SC_CHECK(ph, ncv) sc_nancheck<MAXNV>(P, L, ph, ncv, nan_reported)
+#else
+#define MW_SC_CHECK(ph, ncv)
+#endif
+
 // ------------------------------------------------------------------- step
 template <int MAXNV>
 __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeState& base, uint32_t present,
                         const float (&wr)[kScWrenchSlots][6], const int32_t (&wl)[kScWrenchSlots], int iter,
-                        float dt, int pgs_iters, const f3 gw, float mu, int& nc_out, int& ovf) {
+                        float dt, int pgs_iters, int lcp_solves, const f3 gw, float mu, int& nc_out, int& ovf,
+                        int& unconv) {
     const int lane = lane_id();
+#ifdef MW_SC_NANCHECK
+    bool nan_reported = false;
+    MW_SC_CHECK(0, 0);
+#endif
     const int NB = P->n_bodies, NV = P->nv;
     const bool isnode = lane < P->n_nodes;
     const int nbody = isnode ? P->node_body[lane] : -1;
@@ -649,6 +695,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
     float tau = 0.f, qdi = 0.f;
     if (isbody && alive) { tau = L.tau[bi]; qdi = L.qd[bi]; }
+    MW_SC_CHECK(1, 0);
     // ---- inward, deepest level first
     SV U = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Un = U;
     float psi = 0.f, tt = 0.f, psin = 0.f;
@@ -714,6 +761,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         for (int e = 0; e < 6; ++e) L.l0[m][21 + e] = L0.id[e];
     }
     if (isbase && alive) L.node[lane].V = a0;  // the V record now carries a
+    MW_SC_CHECK(2, 0);
     // ---- outward: accelerations
     float qddi = 0.f;
     for (int d = 1; d < levels; ++d) {
@@ -745,6 +793,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         for (int e = 0; e < 6; ++e) L.nu[md.coff + e] = v0[e] + dt * a[e];
     }
 
+    MW_SC_CHECK(3, 0);
     // ---- contacts: ground slots, then shape pairs
     int nc = 0;
     if (P->ground && (present & kScGroundBit)) {
@@ -850,6 +899,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         L.c_x[lane][0] = L.c_x[lane][1] = L.c_x[lane][2] = 0.f;
     }
 
+    MW_SC_CHECK(4, nc);
     // ---- joint rows of body `lane` (bit t: limit / servo / friction)
     uint32_t jbits = 0u;
     float jb[3] = {0.f, 0.f, 0.f}, jlo[3] = {0.f, 0.f, 0.f}, jhi[3] = {0.f, 0.f, 0.f};
@@ -1033,6 +1083,27 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             }
 #pragma unroll
             for (int r = 0; r < kWaveLanes; ++r) x0 = (lane == r) ? x[r] : x0;
+            if (lcp_solves > 0) {
+                // exact boxed LCP from the PGS impulses (wave_lcp.hpp; oracle
+                // OR_PGS_CONVERGED), lane r = row r; the pivot rows go to the
+                // Delassus matrix's LDS, dead once it sits in the registers
+                LcpRow Rw;
+                Rw.live = lane < NR;
+                const F4 c = L.rc[lane < Rpad ? lane : 0];
+                Rw.kind = (lane < ncr) ? ((lane % 3 == 0) ? 0 : 1) : 2;
+                Rw.nrow = (Rw.kind == 1) ? lane - lane % 3 : lane;
+                Rw.b = Rw.live ? c.x : 0.f;
+                Rw.lo = Rw.live ? c.z : 0.f;
+                Rw.hi = Rw.live ? c.w : 0.f;
+                static_assert(sizeof(L.A) >= kWaveMaxRows * kLcpUStride * sizeof(float), "LCP workspace");
+                float* Uw = &L.A[0][0];
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, Uw, x0)
+                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, Uw, x0);
+                if (!ok && lane == 0) unconv += 1;
+                x0 = Rw.live ? x0 : 0.f;
+            }
+        } else if (lcp_solves > 0 && lane == 0) {
+            unconv += 1;  // more than 64 rows: the PGS sweeps alone (counted as not solved exactly)
         }
         for (int it = 0; it < (two ? pgs_iters : 0); ++it) {
             // the residual w = A x is rebuilt at the start of every sweep (as
@@ -1092,6 +1163,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
     nc_out = nc;
 
+    MW_SC_CHECK(5, nc);
     // ---- integratePositions
     if (isbody && alive) {
         const float qn = L.nu[P->body_coord[bi]];
@@ -1188,12 +1260,13 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
             }
         }
     }
-    int nc = 0, ovf = 0;
+    int nc = 0, ovf = 0, unconv = 0;
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
             if (lane < NB && ((present >> P->body_model[lane]) & 1u))
                 L.tau[lane] = sc_dof_force(P, D, pid, G, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
-            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, gw, mu, nc, ovf);
+            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, A.lcp_solves, gw, mu, nc,
+                           ovf, unconv);
         }
     }
     if (lane < NB) {
@@ -1214,6 +1287,7 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         if (lane == 0) {
             D.ncontact[w] = nc;
             if (ovf) atomicAdd(D.overflow, ovf);
+            if (unconv) atomicAdd(D.overflow + 1, unconv);
         }
         if (A.want_contacts && lane < nc) {
             const float inv_dt = A.inv_dt;

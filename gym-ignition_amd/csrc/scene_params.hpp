@@ -111,7 +111,7 @@ struct SceneDev {
     // depth, node A, node B (-1 ground)) and their count [W]
     float* contact;
     int32_t* ncontact;
-    int32_t* overflow;   // contact points / rows dropped (capacity)
+    int32_t* overflow;   // [0] contact points / rows dropped (capacity), [1] exact LCP solves out of budget
     float* wphys;        // [4][W] per-world physics: gravity xyz (World::setGravity), ground friction
 };
 
@@ -124,6 +124,7 @@ struct SceneArgs {
     int32_t paused;
     int32_t iter0;       // simulator iterations before this launch (wrench expiry)
     int32_t want_contacts;
+    int32_t lcp_solves;  // > 0: exact boxed LCP (wave_lcp.hpp) within that many linear solves per step
 };
 
 }  // namespace mw

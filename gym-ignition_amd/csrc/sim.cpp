@@ -1818,6 +1818,10 @@ int mw_vecenv_create(mw_sim* s, const mw_task_config* cfg, mw_vecenv** out) {
     // the batched env kernels step fixed-base chains only: a floating model
     // with a matching dof count would have its base and contacts ignored
     if (s->floating) return fail(MW_EINVAL, "the batched env tasks need a fixed-base model");
+    // ... and a compiled chain topology: a generic fixed tree (wave kernel) or
+    // a branched 1-2 dof model would be stepped as a serial chain
+    if (s->fixed_tree || s->topo < 0)
+        return fail(MW_EINVAL, "the batched env tasks need a serial-chain model (or the shipped Panda tree)");
     const bool cart = cfg->kind >= MW_TASK_CARTPOLE_DISCRETE && cfg->kind <= MW_TASK_CARTPOLE_CONTINUOUS_SWINGUP;
     const bool pidtask = cfg->kind == MW_TASK_PANDA_POSITION_TRACKING;
     if (cart && n != 2) return fail(MW_EINVAL, "CartPole tasks need the 2-dof cartpole model");

@@ -240,9 +240,19 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
             const bool nfixed = __shfl(static_cast<int>(fixed), R.nrow) != 0;
             bool cpos = false, cneg = false;
             if (R.kind == 1 && R.live && !fixed) {
-                if (nfixed || U <= 0.f) fixed = true;
-                else if (xl >= U && g <= 0.f) cpos = true;
-                else if (xl <= L && g >= 0.f) cneg = true;
+                if (nfixed) {
+                    fixed = true;
+                } else if (U <= 0.f) {
+                    // a contact opening from x_n = 0: its friction rows start on the
+                    // pyramid edge they push towards (sliding); a zero gradient stays
+                    if (g < 0.f) cpos = true;
+                    else if (g > 0.f) cneg = true;
+                    else fixed = true;
+                } else if (xl >= U && g <= 0.f) {
+                    cpos = true;
+                } else if (xl <= L && g >= 0.f) {
+                    cneg = true;
+                }
             }
             fr = R.live && !fixed && !cpos && !cneg;
             coup = cpos ? mu : (cneg ? -mu : 0.f);

@@ -182,6 +182,9 @@ SCENE_SIGNATURES = [
     ("mw_scene_set_world_gravity", ctypes.c_int, [_P, _I, _I, _D]),
     ("mw_scene_world_gravity", ctypes.c_int, [_P, _I, _D]),
     ("mw_scene_set_world_friction", ctypes.c_int, [_P, _I, _I, ctypes.c_double]),
+    ("mw_scene_set_lcp_solver", ctypes.c_int, [_P, _I, _I]),
+    ("mw_scene_lcp_solver", ctypes.c_int, [_P, _IP, _IP]),
+    ("mw_scene_lcp_unconverged", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     ("mw_scene_get_joints", ctypes.c_int, [_P, _I, _I, _I, _IP, _I, _D]),
     ("mw_scene_set_joints", ctypes.c_int, [_P, _I, _I, _I, _IP, _I, _D]),
     ("mw_scene_set_control_mode", ctypes.c_int, [_P, _I, _I, _IP, _I, _I]),

@@ -162,6 +162,21 @@ class Scene:
         nw = self.n_worlds - w0 if nw is None else nw
         N.check(N.lib().mw_scene_set_world_friction(self.handle, w0, nw, float(mu)), "set_world_friction")
 
+    def set_lcp_solver(self, exact: bool = True, max_solves: int = 24) -> None:
+        """mw_scene_set_lcp_solver: exact boxed LCP after the PGS sweeps (default) or the sweeps alone."""
+        N.check(N.lib().mw_scene_set_lcp_solver(self.handle, N.LCP_EXACT if exact else N.LCP_PGS, int(max_solves)),
+                "set_lcp_solver")
+
+    def lcp_solver(self):
+        m, k = ctypes.c_int32(), ctypes.c_int32()
+        N.check(N.lib().mw_scene_lcp_solver(self.handle, ctypes.byref(m), ctypes.byref(k)))
+        return m.value == N.LCP_EXACT, k.value
+
+    def lcp_unconverged(self) -> int:
+        v = ctypes.c_int64()
+        N.check(N.lib().mw_scene_lcp_unconverged(self.handle, ctypes.byref(v)))
+        return v.value
+
     def set_ground_plane(self, enabled: bool = True, mu: float = 1.0) -> None:
         self._touch()
         N.check(N.lib().mw_scene_set_ground_plane(self.handle, 1 if enabled else 0, float(mu)), "set_ground_plane")

@@ -406,6 +406,28 @@ class Model:
     def nr_of_links(self) -> int:
         return len(self.link_names())
 
+    def _file_mass(self) -> float:
+        """Sum of the <inertial><mass> of every link in the model file (URDF:
+        links without <inertial> weigh 0; SDF: sdformat's default mass 1)."""
+        import xml.etree.ElementTree as ET
+        text = getattr(self, "_text", None)
+        if not text:
+            return 0.0
+        root = ET.fromstring(text)
+        if root.tag == "robot":
+            return float(sum(float(m.get("value", "0")) for m in root.findall("link/inertial/mass")))
+        model = root if root.tag == "model" else root.find("model")
+        total = 0.0
+        for link in model.findall("link") if model is not None else []:
+            m = link.find("inertial/mass")
+            total += float(m.text) if m is not None else 1.0
+        return total
+
+    def total_mass(self, link_names: Sequence[str] = ()) -> float:
+        # Model::totalMass (Model.cpp:413-425): the sum of Link::mass over the
+        # links (every link of the model by default)
+        return float(sum(self.get_link(n).mass() for n in (link_names or self.link_names())))
+
     def links_in_contact(self) -> List[str]:
         # Model::linksInContact (Model.cpp:725-736)
         return [n for n in self.link_names() if self.get_link(n).in_contact()]
@@ -828,7 +850,11 @@ class Link:
         n = self._model._sim.dofs
         if self._body >= 0:
             return float(ex[34 * self._body + 17])
-        return float(ex[34 * n + 3]) if self._model._sim.floating else 0.0
+        if self._model._sim.floating:
+            return float(ex[34 * n + 3])
+        # a welded base is not part of the dynamics: its (lumped) mass is what
+        # the model file holds beyond the moving bodies
+        return max(self._model._file_mass() - sum(float(ex[34 * b + 17]) for b in range(n)), 0.0)
 
     def position(self) -> List[float]:
         return self._model._link_state(self._body)[1].tolist()
@@ -1136,6 +1162,7 @@ class World:
             _err(f"Failed to insert model '{name}': {e}")
             return False
         self._models[name] = Model(self, name, view, pose)
+        self._models[name]._text = model_string
         return True
 
     def remove_model(self, model_name: str) -> bool:

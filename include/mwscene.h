@@ -102,6 +102,14 @@ int mw_scene_world_gravity(const mw_scene* sc, int32_t w, double g[3]);
 /* Friction coefficient of the ground plane of single worlds (every contact of
  * those worlds uses it); mw_scene_set_ground_plane sets every world's. */
 int mw_scene_set_world_friction(mw_scene* sc, int32_t w0, int32_t nw, double mu);
+/* Boxed-LCP solver of the scene kernel (as mw_set_lcp_solver): MW_LCP_EXACT
+ * (default, 24 linear solves per world-step) solves the contact / joint LCP
+ * exactly after the PGS sweeps when a world has <= 64 rows (worlds with more
+ * rows keep the sweeps and are counted); MW_LCP_PGS: the sweeps alone. */
+int mw_scene_set_lcp_solver(mw_scene* sc, int32_t mode, int32_t max_solves);
+int mw_scene_lcp_solver(const mw_scene* sc, int32_t* mode, int32_t* max_solves);
+/* World-steps whose exact solve ran out of budget (or had > 64 rows). */
+int mw_scene_lcp_unconverged(const mw_scene* sc, int64_t* world_steps);
 int mw_scene_gravity(const mw_scene* sc, double g[3]);
 /* the ground plane's friction, and the plane in (enabled) or out of every world */
 int mw_scene_set_ground_plane(mw_scene* sc, int32_t enabled, double mu);

@@ -615,6 +615,89 @@ static int boxqp_solve(int n, const double* A, int lda, const double* b, const d
     return -1;
 }
 
+/* Semismooth Newton rounds on the coupled conditions (the GPU's first phase,
+ * gym-ignition_amd/csrc/wave_lcp.hpp, in fp64): rows held at a bound when
+ * their gradient g = A x - b pushes outward, friction rows on their box edge
+ * coupled to their normal (d_t = +-mu d_n), the rest free; the Newton system
+ * by Gaussian elimination with partial pivoting, a monotone line search on
+ * the largest residual.  Returns the rounds that lowered the residual. */
+static int lcp_ssn(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
+                   const int* findex, double mu, double* x, int rounds)
+{
+    static _Thread_local double K[OR_LCP_MAXN * OR_LCP_MAXN];
+    double g[OR_LCP_MAXN], c[OR_LCP_MAXN], d[OR_LCP_MAXN], xt[OR_LCP_MAXN], L[OR_LCP_MAXN], U[OR_LCP_MAXN];
+    int st[OR_LCP_MAXN], idx[OR_LCP_MAXN];  /* 0 free, 1 fixed, 2 coupled +, 3 coupled - */
+    int good = 0;
+    for (int it = 0; it < rounds; ++it) {
+        double xm = 0.0;
+        for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
+        const double res = lcp_residual(n, A, lda, b, lo, hi, findex, mu, x, 1e-12 * (1.0 + xm));
+        if (res <= 1e-13) break;
+        for (int r = 0; r < n; ++r) {
+            double acc = -b[r];
+            for (int e = 0; e < n; ++e) acc += A[r * lda + e] * x[e];
+            g[r] = acc;
+            row_bounds(r, lo, hi, findex, mu, x, &L[r], &U[r]);
+        }
+        for (int r = 0; r < n; ++r) {
+            st[r] = 0;
+            if (findex[r] < 0 && ((x[r] <= L[r] && g[r] >= 0.0) || (x[r] >= U[r] && g[r] <= 0.0))) st[r] = 1;
+        }
+        for (int r = 0; r < n; ++r) {
+            if (findex[r] < 0) continue;
+            if (st[findex[r]] == 1) st[r] = 1;
+            else if (U[r] <= 0.0) st[r] = g[r] < 0.0 ? 2 : (g[r] > 0.0 ? 3 : 1);  /* an opening contact slides */
+            else if (x[r] >= U[r] && g[r] <= 0.0) st[r] = 2;
+            else if (x[r] <= L[r] && g[r] >= 0.0) st[r] = 3;
+        }
+        int nf = 0;
+        for (int r = 0; r < n; ++r)
+            if (st[r] == 0) idx[nf++] = r;
+        /* columns of the free unknowns; a coupled friction column folds into its normal's */
+        for (int i = 0; i < nf; ++i) {
+            const int r = idx[i];
+            for (int j = 0; j < nf; ++j) K[i * nf + j] = A[r * lda + idx[j]];
+            for (int t = 0; t < n; ++t) {
+                if (st[t] < 2) continue;
+                const double sg = st[t] == 2 ? mu : -mu;
+                for (int j = 0; j < nf; ++j)
+                    if (idx[j] == findex[t]) K[i * nf + j] += sg * A[r * lda + t];
+            }
+            c[i] = -g[r];
+        }
+        for (int r = 0; r < n; ++r) d[r] = 0.0;
+        if (nf > 0) {
+            double y[OR_LCP_MAXN];
+            if (!lcp_gauss(nf, K, c, y)) break;
+            for (int i = 0; i < nf; ++i) d[idx[i]] = y[i];
+        }
+        for (int t = 0; t < n; ++t)
+            if (st[t] >= 2) d[t] = (st[t] == 2 ? mu : -mu) * d[findex[t]];
+        int accepted = 0;
+        double step = 1.0;
+        for (int ls = 0; ls < 8 && !accepted; ++ls, step *= 0.5) {
+            for (int r = 0; r < n; ++r) {
+                xt[r] = x[r] + step * d[r];
+                if (findex[r] < 0) xt[r] = xt[r] < lo[r] ? lo[r] : (xt[r] > hi[r] ? hi[r] : xt[r]);
+            }
+            for (int r = 0; r < n; ++r)
+                if (findex[r] >= 0) {
+                    const double u = mu * (xt[findex[r]] > 0.0 ? xt[findex[r]] : 0.0);
+                    xt[r] = xt[r] < -u ? -u : (xt[r] > u ? u : xt[r]);
+                }
+            double xtm = 0.0;
+            for (int r = 0; r < n; ++r) xtm = fabs(xt[r]) > xtm ? fabs(xt[r]) : xtm;
+            if (lcp_residual(n, A, lda, b, lo, hi, findex, mu, xt, 1e-12 * (1.0 + xtm)) < res) {
+                for (int r = 0; r < n; ++r) x[r] = xt[r];
+                accepted = 1;
+            }
+        }
+        if (!accepted) break;
+        ++good;
+    }
+    return good;
+}
+
 /* Converged mode: staggered fixed point of the friction bounds.  With the
  * boxes [-mu x_n, mu x_n] frozen at the current normal impulses the LCP is a
  * strictly convex box QP (boxqp_solve, exact); the bounds are then updated
@@ -657,6 +740,21 @@ static void lcp_refine(int n, const double* A, int lda, const double* b, const d
     double xm = 0.0;
     for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
     g_pgs_delta = lcp_residual(n, A, lda, b, lo, hi, findex, mu, x, 1e-12 * (1.0 + xm));
+    if (g_pgs_delta > 1e-10 || failed) {
+        /* the staggered rounds stopped short (a slowly contracting friction
+         * fixed point): semismooth Newton polish, kept only if it is better */
+        double xs[OR_LCP_MAXN];
+        for (int r = 0; r < n; ++r) xs[r] = x[r];
+        lcp_ssn(n, A, lda, b, lo, hi, findex, mu, xs, 30);
+        double xsm = 0.0;
+        for (int r = 0; r < n; ++r) xsm = fabs(xs[r]) > xsm ? fabs(xs[r]) : xsm;
+        const double rs = lcp_residual(n, A, lda, b, lo, hi, findex, mu, xs, 1e-12 * (1.0 + xsm));
+        if (rs < g_pgs_delta) {
+            for (int r = 0; r < n; ++r) x[r] = xs[r];
+            g_pgs_delta = rs;
+            failed = 0;
+        }
+    }
     if (failed) g_pgs_delta = -1.0 - g_pgs_delta;
     g_pgs_sweeps += 1000000 * round;
 }

@@ -560,8 +560,17 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
             cneg = np.zeros(n, bool)
             for r in range(n):
                 if kind[r] == 1 and not fixed[r]:
-                    if nfixed[r] or U[r] <= 0:
+                    if nfixed[r]:
                         fixed[r] = True
+                    elif U[r] <= 0:
+                        # a contact opening from x_n = 0: its frictions start on the
+                        # pyramid edge they push towards (sliding), 0 if g_t = 0
+                        if g[r] < 0:
+                            cpos[r] = True
+                        elif g[r] > 0:
+                            cneg[r] = True
+                        else:
+                            fixed[r] = True
                     elif x[r] >= U[r] and g[r] <= 0:
                         cpos[r] = True
                     elif x[r] <= L[r] and g[r] >= 0:

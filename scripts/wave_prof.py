@@ -21,7 +21,7 @@ W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 PGS = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 T = 20
 PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
-          "Delassus (lane = column)", "PGS", "rows total (responses .. integrate)", "whole substep"]
+          "Delassus (lane = column)", "PGS + exact LCP", "rows total (responses .. integrate)", "whole substep"]
 
 sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=PGS, pose=(0, 0, 0.535, 1, 0, 0, 0))
 names = sim.joint_names
@@ -33,6 +33,10 @@ for d, n in enumerate(names):
     sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
 sim.set_control_mode(N.MODE_POSITION)
 sim.set("position_target", np.zeros((W, sim.dofs)))
+# solver options: MW_PROF_EXACT=0 -> PGS only; MW_PROF_WARM=1 -> warm-started sweeps
+sim.set_lcp_solver(os.environ.get("MW_PROF_EXACT", "1") != "0")
+if os.environ.get("MW_PROF_WARM", "0") != "0":
+    sim.set_pgs_options(0.0, True)
 sim.run_device(50)
 L = N.lib()
 fn = L.mw_debug_wave_prof

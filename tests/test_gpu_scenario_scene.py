@@ -168,6 +168,24 @@ def test_multi_world_is_one_batched_scene(require_gpu):
     gazebo.close()
 
 
+def test_model_total_mass(require_gpu):
+    """Model::totalMass (Model.cpp:413-425): the sum of Link::mass over the
+    links -- the CartPole's rail (welded to the world), cart and pole; the
+    humanoid's 36.4 kg; a subset of links."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    gazebo, get_model_file = _gazebo()
+    world = gazebo.get_world()
+    assert world.set_physics_engine(scenario.PhysicsEngine_dart)
+    assert world.insert_model(get_model_file("cartpole"))
+    assert world.insert_model(get_model_file("humanoid32"), core.Pose([2.0, 0, 0.6], [1., 0, 0, 0]), "h")
+    cp, h = world.get_model("cartpole"), world.get_model("h")
+    assert cp.total_mass() == pytest.approx(5.0 + 1.0 + 0.1, abs=1e-6)
+    assert cp.total_mass(["cart", "pole"]) == pytest.approx(1.1, abs=1e-6)
+    assert h.total_mass() == pytest.approx(36.4, abs=1e-3)
+    gazebo.close()
+
+
 def _ground_plane_sdf(mu):
     return ('<sdf version="1.6"><model name="ground_plane"><static>true</static><link name="link">'
             '<collision name="collision"><geometry><plane><normal>0 0 1</normal><size>100 100</size></plane>'
@@ -387,7 +405,7 @@ def test_static_sdf_collider(require_gpu, oracle):
     ball = world.get_model("ball")
     assert ball.enable_contacts(True)
     cms = [oracle.load_urdf(STATIC_TABLE_SDF), oracle.load_urdf(ball_text, pose_xyz=(0.5, 0, 0.8))]
-    ow = oracle.SceneWorld(cms, mu=1.0, pgs_iters=50)
+    ow = oracle.SceneWorld(cms, mu=1.0, pgs_iters=oracle.PGS_CONVERGED)  # the ScenarI/O scene solves exactly
     worst = 0.0
     for k in range(800):
         assert gazebo.run()

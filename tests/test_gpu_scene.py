@@ -42,9 +42,14 @@ def _rand_quat(rng, max_angle):
     return np.concatenate([[np.cos(a / 2)], axis * np.sin(a / 2)])
 
 
-def _scene(models, W, pgs=50, mu=0.8):
+def _scene(models, W, pgs=50, mu=0.8, exact=False):
+    """A scene of `models` in W worlds.  exact=False: the PGS sweeps alone, so
+    the kernel is compared with the oracle running the same algorithm (the
+    exact solve is covered by the KATs and the exact-mode tests)."""
     from mwstep.scene import Scene
     sc = Scene(n_worlds=W, pgs_iters=pgs)
+    assert sc.lcp_solver() == (True, 24)
+    sc.set_lcp_solver(exact)
     sc.set_ground_plane(True, mu)
     for text, pose, name in models:
         sc.insert_model(text, pose, name)
@@ -400,6 +405,7 @@ def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
     q, qd, tau = f32(q), f32(qd), f32(tau)
     from mwstep.scene import Scene
     sc = Scene(n_worlds=W, pgs_iters=50)
+    sc.set_lcp_solver(False)  # vs the oracle's PGS-50 step
     sc.insert_model(text, (0, 0, 0, 1, 0, 0, 0), "ftree")
     assert sc.models[0]["floating"] is False and sc.models[0]["dofs"] == n
     sc.set("reset_q", q, m=0)
