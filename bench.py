@@ -564,8 +564,10 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
     out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
     out["scaling"] = "strong"
     out["worlds_per_gpu"] = e - b
-    solve = ("PGS 50 sweeps then the exact boxed LCP (wave_lcp.hpp, <= 24 linear solves per world-step; "
-             "DART's Dantzig result)" if exact else f"PGS {pgs} iterations only (mw_set_lcp_solver PGS)")
+    solve = ("the exact boxed LCP (wave_lcp.hpp: PGS sweeps warm-started from the previous step's impulses, at "
+             "most 50, ending once a sweep moves no constraint velocity by 1e-6; then semismooth Newton / active-set "
+             "rounds, <= 24 linear solves per world-step; DART's Dantzig result)" if exact
+             else f"PGS {pgs} iterations only (mw_set_lcp_solver PGS)")
     out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
                        f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "
                        f"{solve}, dt = 1 ms (BASELINE.json configs[4])")

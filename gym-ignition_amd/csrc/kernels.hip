@@ -627,7 +627,7 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     }
     uint32_t active = 0u;
     int ovf = 0, unconv = 0;
-    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof[kWaveProfPhases] = {};
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
             MW_PROF_T(ta);

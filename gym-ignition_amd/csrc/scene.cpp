@@ -92,6 +92,7 @@ struct mw_scene {
     float* d_wrench = nullptr;     // [S][6][NN][W]
     float* d_contact = nullptr;    // [C][12][W]
     float* d_wphys = nullptr;      // [4][W]: gravity xyz, ground friction per world
+    int32_t* d_warm = nullptr;     // [kScWarmWords][W]: exact-LCP warm-start record (SceneDev::warm)
     mw::PidF* d_pid = nullptr;
     // pinned host mirrors with the device layouts
     uint8_t* h_joint = nullptr;
@@ -369,6 +370,8 @@ int flush(mw_scene* s, bool defer) {
         if (int rc = sync(s)) return rc;
     if (s->params_dirty) {
         SC_HIP(hipMemcpyAsync(s->dp, &s->hp, sizeof(mw::SceneF), hipMemcpyHostToDevice, s->stream));
+        // new slots / pairs: the warm-start keys of the old layout mean nothing
+        SC_HIP(hipMemsetAsync(s->d_warm, 0, s->W * sizeof(int32_t), s->stream));
         s->params_dirty = false;
     }
     if (s->cmd_dirty) {
@@ -572,6 +575,8 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), NBMAX * sizeof(mw::PidF)));
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->dp), sizeof(mw::SceneF)));
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_wphys), 4 * W * sizeof(float)));
+    SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_warm), mw::kScWarmWords * W * sizeof(int32_t)));
+    SC_HIP(hipMemsetAsync(s->d_warm, 0, mw::kScWarmWords * W * sizeof(int32_t), s->stream));
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_wphys), 4 * W * sizeof(float), hipHostMallocDefault));
     for (size_t w = 0; w < W; ++w) {
         for (int k = 0; k < 3; ++k) s->h_wphys[k * W + w] = static_cast<float>(s->gravity[k]);
@@ -614,6 +619,7 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     D.wrench = s->d_wrench;
     D.contact = s->d_contact;
     D.wphys = s->d_wphys;
+    D.warm = s->d_warm;
     s->mode.assign(s->jrows, MW_MODE_IDLE);
     s->cmd64.assign(s->jrows, 0.0);
     s->ptgt64.assign(s->jrows, 0.0);
@@ -635,6 +641,7 @@ void mw_scene_destroy(mw_scene* s) {
     (void)hipFree(s->d_pid);
     (void)hipFree(s->dp);
     (void)hipFree(s->d_wphys);
+    (void)hipFree(s->d_warm);
     (void)hipHostFree(s->h_wphys);
     (void)hipHostFree(s->h_joint);
     (void)hipHostFree(s->h_base);

@@ -84,8 +84,24 @@ struct ScWorld {
     float c_p[kScMaxContacts][3], c_n[kScMaxContacts][3], c_t1[kScMaxContacts][3], c_t2[kScMaxContacts][3];
     float c_d[kScMaxContacts];
     int32_t c_na[kScMaxContacts], c_nb[kScMaxContacts];
+    int32_t c_key[kScMaxContacts];  // warm-start identity: ground slot, or n_slots + 4 pair + point
     float c_x[kScMaxContacts][3];
 };
+
+// the world's exact-LCP warm-start record (SceneDev::warm); rec == nullptr: cold
+struct ScWarm {
+    int32_t* rec;
+    int W, w;
+    __device__ int32_t& n() const { return rec[w]; }
+    __device__ int32_t& key(int c) const { return rec[static_cast<size_t>(1 + c) * W + w]; }
+    __device__ float& x(int r) const {
+        return reinterpret_cast<float*>(rec)[static_cast<size_t>(1 + kScMaxContacts + r) * W + w];
+    }
+};
+
+// PGS sweeps of exact mode end once a sweep moves no constraint velocity by
+// more than this (sim.cpp kExactPgsTol): the exact solve takes over
+constexpr float kScExactPgsTol = 1e-6f;
 
 // ODE dPlaneSpace (oracle.c plane_space), float32
 __device__ __forceinline__ void plane_space_f(f3 n, f3& p, f3& q) {
@@ -277,7 +293,7 @@ __device__ __forceinline__ int sc_box_sphere(f3 h, f3 c, const M3& R, float rad,
     if (!inside) {
         f3 e = l - q;
         const float dist = sqrtf(dot(e, e));
-        if (dist > rad) return 0;
+        if (dist > rad || dist <= 0.f) return 0;  // dist 0: the centre on the face (no direction)
         e = (1.f / dist) * e;
         nbs = mul(R, e);
         pt = c + mul(R, q);
@@ -388,16 +404,14 @@ __device__ __forceinline__ bool sc_inside(int type, f3 h, f3 c, const M3& R, f3 
     return h.x - sqrtf(l.x * l.x + l.y * l.y) > 0.f && h.y - fabsf(l.z) > 0.f;
 }
 
-// Kept out of line: inlined into scene_run_kernel, the build produced NaN
-// poses in box / sphere / chain piles that never reach this function
-// (tests/test_gpu_scene.py test_one_step_parity_random_piles), so the register
-// allocation of the main kernel is left as it was without it.
-#ifdef MW_SC_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& Ra, int tb, f3 hb, f3 cb,
+// Inlined (r03).  Round 2 kept it out of line after an inlined build showed
+// NaN poses in box / sphere piles that never reach it; re-tested in r03 with
+// it inlined and the MW_SC_NANCHECK build (every phase of every step checked
+// for a non-finite pose, coordinate or contact): no non-finite value in any
+// scene test, and the inlined kernel spills less (scratch 1040 -> 944 B per
+// lane, SGPR spills 547 -> 84).  The one division that could see a zero
+// under -ffinite-math-only (sc_box_sphere's 1 / dist) is guarded.
+__device__ __forceinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& Ra, int tb, f3 hb, f3 cb,
                                                 const M3& Rb, f3& n, f3* pts, float* deps) {
     f3 ax[6];
     int na = sc_axes(ta, ca, Ra, cb, ax);
@@ -628,8 +642,8 @@ __device__ void sc_nancheck(const SceneF* __restrict__ P, const ScWorld<MAXNV>& 
 template <int MAXNV>
 __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeState& base, uint32_t present,
                         const float (&wr)[kScWrenchSlots][6], const int32_t (&wl)[kScWrenchSlots], int iter,
-                        float dt, int pgs_iters, int lcp_solves, const f3 gw, float mu, int& nc_out, int& ovf,
-                        int& unconv) {
+                        float dt, int pgs_iters, int lcp_solves, const ScWarm& warm, const f3 gw, float mu,
+                        int& nc_out, int& ovf, int& unconv) {
     const int lane = lane_id();
 #ifdef MW_SC_NANCHECK
     bool nan_reported = false;
@@ -838,6 +852,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 L.c_d[c] = dep;
                 L.c_na[c] = na;
                 L.c_nb[c] = -1;
+                L.c_key[c] = slot;
             }
             nc += __popcll(bal);
         }
@@ -882,6 +897,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 L.c_d[c] = deps[i];
                 L.c_na[c] = na;
                 L.c_nb[c] = nb;
+                L.c_key[c] = P->n_slots + 4 * pr + i;
             }
         }
         nc += total;
@@ -1044,11 +1060,28 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             // of 8 with inert rows (zero column, b = 0, bounds [0, 0])
             const int Rpad = (NR + 7) & ~7;
             if (lane >= NR && lane < Rpad) L.rc[lane] = F4{0.f, 0.f, 0.f, 0.f};
+            // warm start (exact mode): every row from the previous step's
+            // impulse of the same contact key / joint row, else 0
+            float xw = 0.f;
+            if (warm.rec && lane < NR) {
+                const int src = L.src[lane];
+                if (src < kJointRow) {
+                    const int key = L.c_key[src / 3], np = warm.n();
+                    for (int j = 0; j < np; ++j) {
+                        if (warm.key(j) == key) {
+                            xw = warm.x(3 * j + src % 3);
+                            break;
+                        }
+                    }
+                } else {
+                    xw = warm.x(kScWarmJoint0 + (src - kJointRow));
+                }
+            }
             float a[kWaveLanes], x[kWaveLanes];
 #pragma unroll
             for (int r = 0; r < kWaveLanes; ++r) {
                 a[r] = (r < NR && lane < NR) ? L.A[r][lane] : 0.f;
-                x[r] = 0.f;
+                x[r] = read_lane(xw, r);
             }
             for (int it = 0; it < pgs_iters; ++it) {
                 float w = 0.f;
@@ -1058,6 +1091,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #pragma unroll
                     for (int k = 0; k < 8; ++k) w += a[rb + k] * x[rb + k];
                 }
+                const float w_start = w;
                 float h = 0.f;
 #pragma unroll
                 for (int rb = 0; rb < kWaveLanes; rb += 8) {
@@ -1080,6 +1114,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                         x[r] = v;
                     }
                 }
+                if (lcp_solves > 0 && wave_fmax(fabsf(w - w_start)) <= kScExactPgsTol) break;
             }
 #pragma unroll
             for (int r = 0; r < kWaveLanes; ++r) x0 = (lane == r) ? x[r] : x0;
@@ -1097,8 +1132,10 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 Rw.hi = Rw.live ? c.w : 0.f;
                 static_assert(sizeof(L.A) >= kWaveMaxRows * kLcpUStride * sizeof(float), "LCP workspace");
                 float* Uw = &L.A[0][0];
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, Uw, x0)
-                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, Uw, x0);
+                int nsolve = 0, nround = 0;
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve, nround)
+                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve,
+                                                                          nround);
                 if (!ok && lane == 0) unconv += 1;
                 x0 = Rw.live ? x0 : 0.f;
             }
@@ -1160,6 +1197,25 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             const int r = r0 + lane;
             if (r < ncr && r < NR) L.c_x[r / 3][r % 3] = r0 ? x1 : x0;
         }
+        if (warm.rec) {
+            // the next step's record of the joint rows: this step's (the others 0)
+            for (int e = lane; e < 3 * NB; e += kWaveLanes) warm.x(kScWarmJoint0 + e) = 0.f;
+            __threadfence_block();
+            if (!two && lane >= ncr && lane < NR) warm.x(kScWarmJoint0 + (L.src[lane] - kJointRow)) = x0;
+        }
+    } else if (warm.rec) {
+        for (int e = lane; e < 3 * NB; e += kWaveLanes) warm.x(kScWarmJoint0 + e) = 0.f;
+    }
+    if (warm.rec) {
+        // ... and of the contacts, by key
+        const int nrec = NR > 0 ? nc : 0;
+        if (lane == 0) warm.n() = nrec;
+        if (lane < nrec) {
+            warm.key(lane) = L.c_key[lane];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) warm.x(3 * lane + d) = L.c_x[lane][d];
+        }
+        __threadfence_block();
     }
     nc_out = nc;
 
@@ -1261,12 +1317,13 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         }
     }
     int nc = 0, ovf = 0, unconv = 0;
+    const ScWarm warm{A.lcp_solves > 0 ? D.warm : nullptr, W, w};
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
             if (lane < NB && ((present >> P->body_model[lane]) & 1u))
                 L.tau[lane] = sc_dof_force(P, D, pid, G, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
-            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, A.lcp_solves, gw, mu, nc,
-                           ovf, unconv);
+            sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, A.lcp_solves, warm, gw,
+                           mu, nc, ovf, unconv);
         }
     }
     if (lane < NB) {

@@ -113,7 +113,16 @@ struct SceneDev {
     int32_t* ncontact;
     int32_t* overflow;   // [0] contact points / rows dropped (capacity), [1] exact LCP solves out of budget
     float* wphys;        // [4][W] per-world physics: gravity xyz (World::setGravity), ground friction
+    // exact-LCP warm start, the previous step's impulses by row identity:
+    // [0] contact count [W], [1 .. kScMaxContacts] contact keys (ground slot,
+    // or n_slots + 4 pair + point) [c][W], then kScWarmRows impulses [row][W]
+    // (contact c rows 3 c + d, joint rows kScWarmJoint0 + 3 body + type)
+    int32_t* warm;
 };
+
+constexpr int kScWarmJoint0 = 3 * kScMaxContacts;
+constexpr int kScWarmRows = kScWarmJoint0 + 3 * kScMaxBodies;
+constexpr int kScWarmWords = 1 + kScMaxContacts + kScWarmRows;
 
 // per-launch arguments
 struct SceneArgs {

@@ -726,6 +726,10 @@ int mw_device_params(const mw_sim* s, void* out, int32_t bytes) {
     return MW_OK;
 }
 
+// PGS sweeps of exact mode end once a sweep moves no constraint velocity by
+// more than this (m/s, rad/s): the exact solve takes over from there
+constexpr float kExactPgsTol = 1e-6f;
+
 // Device buffers of the world-per-wavefront kernel: PID gains, the overflow
 // counters ([0] constraint rows dropped, [1] exact-LCP solves that ran out of
 // budget) and the warm-start record of the PGS impulses.  Called at
@@ -1036,8 +1040,13 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     a.paused = paused ? 1 : 0;
     a.pgs_iters = s->cfg.pgs_iters;
     a.pgs_tol = static_cast<float>(s->pgs_tol);
-    a.warm = (s->wave && s->pgs_warm && s->d_warm) ? 1 : 0;
     a.lcp_solves = s->wave ? s->lcp_solves : 0;
+    // exact mode always starts from the previous step's impulses (the solve's
+    // result does not depend on its start) and ends the sweeps once they stop
+    // moving the constraint velocities: a steady contact set is then a
+    // few-sweep, zero-solve step
+    a.warm = (s->wave && (s->pgs_warm || a.lcp_solves > 0) && s->d_warm) ? 1 : 0;
+    if (a.lcp_solves > 0) a.pgs_tol = std::max(a.pgs_tol, kExactPgsTol);
     a.first = 1;
     const int spr = s->cfg.steps_per_run;
     int done = 0;

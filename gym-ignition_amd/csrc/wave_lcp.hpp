@@ -33,17 +33,44 @@ namespace dev {
 constexpr float kLcpRelTol = 4e-6f;   // residual <= kLcpRelTol (|b| + sum |A_rc x_c|) + kLcpAbsTol
 constexpr float kLcpAbsTol = 1e-7f;   // m/s or rad/s
 constexpr int kLcpLineSearch = 3;     // step halvings of a Newton round
+// A residual within kLcpLoose x the tolerance is accepted after one more
+// linear solve (the polish round) whatever that round reaches: the last
+// decade costs the redundant-corner standing LCPs (conditioned ~1e7 by the
+// CFM) many active-set rounds, while the joint velocities follow the
+// residual / sqrt(CFM) and want the tight tolerance after impacts
+constexpr float kLcpLoose = 10.f;
+
+// Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
+// ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
+// the row results up; lane 63 ends with the wave's result, read as a scalar.
+// Every lane of the wave must be active.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float v) {
+#ifdef MW_HOST_TEST
+    return v;
+#else
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWMASK, 0xf, false));
+#endif
+}
 
 __device__ __forceinline__ float wave_fmax(float v) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) v = fmaxf(v, __shfl_xor(v, m));
-    return v;
+    v = fmaxf(v, dpp_f<0x111, 0xf>(v));  // row_shr:1
+    v = fmaxf(v, dpp_f<0x112, 0xf>(v));  // row_shr:2
+    v = fmaxf(v, dpp_f<0x114, 0xf>(v));  // row_shr:4
+    v = fmaxf(v, dpp_f<0x118, 0xf>(v));  // row_shr:8 -> lane 15 of a row holds its max
+    v = fmaxf(v, dpp_f<0x142, 0xa>(v));  // row_bcast:15 into rows 1 and 3
+    v = fmaxf(v, dpp_f<0x143, 0xc>(v));  // row_bcast:31 into rows 2 and 3
+    return read_lane(v, 63);
 }
 
 __device__ __forceinline__ float wave_fmin(float v) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) v = fminf(v, __shfl_xor(v, m));
-    return v;
+    v = fminf(v, dpp_f<0x111, 0xf>(v));
+    v = fminf(v, dpp_f<0x112, 0xf>(v));
+    v = fminf(v, dpp_f<0x114, 0xf>(v));
+    v = fminf(v, dpp_f<0x118, 0xf>(v));
+    v = fminf(v, dpp_f<0x142, 0xa>(v));
+    v = fminf(v, dpp_f<0x143, 0xc>(v));
+    return read_lane(v, 63);
 }
 
 // first lane holding the wave maximum of v
@@ -78,9 +105,24 @@ __device__ __forceinline__ float lcp_matvec(const float (&a)[kWaveMaxRows], floa
     return w;
 }
 
+// v of the row's contact normal (friction rows; every other row: its own v),
+// by lane reads of the normal rows (every third row of the contact block)
+template <int RC>
+__device__ __forceinline__ float gather_normal(float v, const LcpRow& R, int n) {
+    float out = v;
+#pragma unroll
+    for (int c = 0; c < RC; c += 3) {
+        if (c >= n) break;
+        const float vc = read_lane(v, c);
+        out = (R.kind == 1 && R.nrow == c) ? vc : out;
+    }
+    return out;
+}
+
 // box of row r at the lane-distributed impulses xl (friction: [-mu x_n, mu x_n])
-__device__ __forceinline__ void lcp_bounds(const LcpRow& R, float xl, float mu, float& L, float& U) {
-    const float xn = __shfl(xl, R.nrow);
+template <int RC>
+__device__ __forceinline__ void lcp_bounds(const LcpRow& R, float xl, float mu, int n, float& L, float& U) {
+    const float xn = gather_normal<RC>(xl, R, n);
     const float u = mu * fmaxf(xn, 0.f);
     L = (R.kind == 1) ? -u : R.lo;
     U = (R.kind == 1) ? u : R.hi;
@@ -171,7 +213,8 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 // Returns true when converged within max_solves linear solves.
 template <int RC>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
-                                               int max_solves, float* __restrict__ Uw, float& xl) {
+                                               int max_solves, float* __restrict__ Uw, float& xl, int& n_solves,
+                                               int& n_rounds) {
     const int lane = lane_id();
     float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
 #pragma unroll
@@ -182,19 +225,28 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
     int ws = 0;             // phase 1 working set: 0 free, 1 held at L, 2 held at U
     float Lf = 0.f, Uf = 0.f, prev = 0.f;  // phase 1: the round's frozen box, the round's start
     bool at_min = false, new_round = true;
-    for (int iter = 0; iter < 4 * max_solves + 8; ++iter) {
+    bool polish = false;  // inside the loose band: one more solve, then accept
+    int polish_at = 0;
+    int iter = 0;
+    for (; iter < 4 * max_solves + 8; ++iter) {
         float mag;
         const float w = lcp_matvec<RC>(a, xl, n, mag);
         const float g = w - R.b;
         float L, U;
-        lcp_bounds(R, xl, mu, L, U);
+        lcp_bounds<RC>(R, xl, mu, n, L, U);
         const float xmax = wave_fmax(R.live ? fabsf(xl) : 0.f);
         const float tolx = 2e-6f * (1.f + xmax);
         float e_abs;
         const float rel = wave_fmax(lcp_row_residual(R, xl, w, mag, arr, L, U, tolx, e_abs));
-        if (rel <= 1.f) {
+        if (rel <= 1.f || (polish && rel <= kLcpLoose && solves > polish_at)) {
             converged = true;
             break;
+        }
+        if (rel > kLcpLoose) {
+            polish = false;
+        } else if (!polish) {
+            polish = true;  // the next linear solve is the polish round
+            polish_at = solves;
         }
         if (solves >= max_solves) break;
         if (phase == 1 && new_round) {
@@ -237,7 +289,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
             bool fixed = !R.live;
             if (R.kind == 0) fixed = fixed || (xl <= 0.f && g >= 0.f);
             if (R.kind == 2) fixed = fixed || (xl <= R.lo && g >= 0.f) || (xl >= R.hi && g <= 0.f);
-            const bool nfixed = __shfl(static_cast<int>(fixed), R.nrow) != 0;
+            const bool nfixed = mask_bit(static_cast<uint64_t>(__ballot(fixed)), R.nrow);
             bool cpos = false, cneg = false;
             if (R.kind == 1 && R.live && !fixed) {
                 if (nfixed) {
@@ -277,7 +329,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
         float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw);
         ++solves;
         if (phase == 0) {
-            const float dn = __shfl(d, R.nrow);
+            const float dn = gather_normal<RC>(d, R, n);
             d = fr ? d : coup * dn;
             // monotone line search on the largest residual
             bool accepted = false;
@@ -287,7 +339,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
                 if (R.kind == 0) xt = fmaxf(xt, 0.f);
                 if (R.kind == 2) xt = fminf(fmaxf(xt, R.lo), R.hi);
                 float Lt, Ut;
-                lcp_bounds(R, xt, mu, Lt, Ut);  // the friction boxes of the projected normals
+                lcp_bounds<RC>(R, xt, mu, n, Lt, Ut);  // the friction boxes of the projected normals
                 if (R.kind == 1) xt = fminf(fmaxf(xt, Lt), Ut);
                 xt = R.live ? xt : 0.f;
                 float mt;
@@ -332,6 +384,8 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
             at_min = true;
         }
     }
+    n_solves = solves;
+    n_rounds = iter;
     return converged;
 }
 

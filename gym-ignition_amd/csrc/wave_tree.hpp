@@ -103,8 +103,8 @@ __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x &
 
 // Phase timing (debug builds only: EXTRA=-DMW_WAVE_PROF, scripts/wave_prof.py):
 // shader-clock cycles per phase, summed over the worlds of a launch.
+constexpr int kWaveProfPhases = 10;  // [8] exact-LCP linear solves, [9] its rounds
 #ifdef MW_WAVE_PROF
-constexpr int kWaveProfPhases = 8;
 __device__ unsigned long long g_wave_prof[kWaveProfPhases];
 #define MW_PROF_T(var) const long long var = clock64()
 #define MW_PROF_ACC(k, a, b) (prof[k] += static_cast<unsigned long long>((b) - (a)))
@@ -395,10 +395,7 @@ __device__ __forceinline__ void wave_pgs(const WaveWorld<MAXN>& L, const float (
             }
         }
         if (TOL) {
-            float d = fabsf(w - w_start);
-#pragma unroll
-            for (int m = 1; m < kWaveLanes; m <<= 1) d = fmaxf(d, __shfl_xor(d, m));
-            if (d <= pgs_tol) break;
+            if (wave_fmax(fabsf(w - w_start)) <= pgs_tol) break;
         }
     }
 }
@@ -707,8 +704,13 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             // the elimination's pivot rows go to the responses' stack (dead here)
             static_assert(sizeof(L.stack) >= kWaveMaxRows * kLcpUStride * sizeof(float), "LCP workspace");
             float* U = &L.stack[0][0][0];
-            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, U, xe)
-                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, U, xe);
+            int nsolve = 0, nround = 0;
+            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround)
+                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround);
+#ifdef MW_WAVE_PROF
+            prof[8] += static_cast<unsigned long long>(nsolve);
+            prof[9] += static_cast<unsigned long long>(nround);
+#endif
 #pragma unroll
             for (int r = 0; r < kWaveMaxRows; ++r) {
                 if ((r & 7) == 0 && r >= Rpad) break;

@@ -230,7 +230,12 @@ int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
  * fixed point -- with at most max_solves dense linear solves (Gaussian
  * elimination over the wave's lanes) per world-step; DART's primary solver is
  * Dantzig's exact pivoting method [EXT], reached from ForwardStep
- * (Physics.cpp:1824-1835).  MW_LCP_PGS: the PGS sweeps alone. */
+ * (Physics.cpp:1824-1835).  In exact mode the sweeps always start from the
+ * previous step's impulses of the same contact slot / joint row and end once a
+ * sweep moves no constraint velocity by more than 1e-6 (at most
+ * mw_config.pgs_iters of them): only the start of the exact solve depends on
+ * them.  MW_LCP_PGS: the PGS sweeps alone (cold unless mw_set_pgs_options
+ * asks for the warm start). */
 #define MW_LCP_PGS 0
 #define MW_LCP_EXACT 1
 int mw_set_lcp_solver(mw_sim* sim, int32_t mode, int32_t max_solves);

@@ -13,6 +13,8 @@ import os
 import sys
 
 import numpy as np
+LOOSE = float(__import__('os').environ.get('LOOSE', '10'))
+BEST = int(__import__('os').environ.get('BEST', '0'))
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -22,6 +24,9 @@ import pyoracle  # noqa: E402
 f32 = np.float32
 BIG = f32(3.4e38)
 LSNORM = os.environ.get("LSNORM", "max")
+LSMODE = os.environ.get("LSMODE", "max")
+BAND = float(os.environ.get("BAND", "0"))
+SSN_MAX = int(os.environ.get("SSN_MAX", "6"))
 PGS_ON_FAIL = int(os.environ.get("PGS_ON_FAIL", "0"))
 
 
@@ -499,7 +504,7 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
     for _ in range(pgs_sweeps):
         pgs_sweep(A, b, lo0, hi0, kind, mu, x)
     arr = np.diag(A).copy()
-    RT, AT = f32(4e-6), f32(1e-7)
+    RT, AT = f32(float(__import__('os').environ.get('RT', '4e-6'))), f32(float(__import__('os').environ.get('AT', '1e-7')))
 
     def bounds(xl):
         u = mu * np.maximum(xl[nrow], 0)
@@ -513,9 +518,11 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
         return e.astype(f32), (e / (RT * (np.abs(b) + mag) + AT)).max()
 
     solves, phase, at_min, new_round = 0, 0, False, True
+    ssn_n, best_e, best_x = 0, np.inf, x.copy()
     ws = np.zeros(n, int)
     Lf = Uf = prev = None
     conv = False
+    polish, polish_at = False, 0
     for it in range(4 * max_solves + 8):
         w = (A @ x).astype(f32)
         mag = (np.abs(A) @ np.abs(x)).astype(f32)
@@ -524,9 +531,15 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
         xmax = np.abs(x).max()
         tolx = f32(2e-6) * (1 + xmax)
         e_abs, rel = res(x, w, mag, L, U, tolx)
-        if rel <= 1:
+        if rel <= 1 or (polish and rel <= LOOSE and solves > polish_at):
             conv = True
             break
+        if rel > LOOSE:
+            polish = False
+        elif not polish:
+            polish, polish_at = True, solves
+        if rel < best_e:
+            best_e, best_x = rel, x.copy()
         if solves >= max_solves:
             break
         if phase == 1 and new_round:
@@ -552,9 +565,10 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
             continue
         emax = e_abs.max()
         if phase == 0:
+            band = BAND * (1 + xmax)
             fixed = np.zeros(n, bool)
-            fixed |= (kind == 0) & (x <= 0) & (g >= 0)
-            fixed |= (kind == 2) & (((x <= lo0) & (g >= 0)) | ((x >= hi0) & (g <= 0)))
+            fixed |= (kind == 0) & (x <= band) & (g >= 0)
+            fixed |= (kind == 2) & (((x <= lo0 + band) & (g >= 0)) | ((x >= hi0 - band) & (g <= 0)))
             nfixed = fixed[nrow]
             cpos = np.zeros(n, bool)
             cneg = np.zeros(n, bool)
@@ -571,9 +585,9 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
                             cneg[r] = True
                         else:
                             fixed[r] = True
-                    elif x[r] >= U[r] and g[r] <= 0:
+                    elif x[r] >= U[r] - band and g[r] <= 0:
                         cpos[r] = True
-                    elif x[r] <= L[r] and g[r] >= 0:
+                    elif x[r] <= L[r] + band and g[r] >= 0:
                         cneg[r] = True
             fr = ~fixed & ~cpos & ~cneg
             coup = np.where(cpos, mu, np.where(cneg, -mu, 0)).astype(f32)
@@ -591,6 +605,7 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
             K[~fr, ~fr] = 1
         d = ge_solve(K, np.where(fr, -g, 0).astype(f32))
         solves += 1
+        x_prev = x.copy()
         if phase == 0:
             d = np.where(fr, d, coup * d[nrow]).astype(f32)
             acc = False
@@ -604,10 +619,24 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
                 wt = (A @ xt).astype(f32)
                 mt = (np.abs(A) @ np.abs(xt)).astype(f32)
                 et, _ = res(xt, wt, mt, Lt, Ut, f32(2e-6) * (1 + np.abs(xt).max()))
-                if et.max() < emax:
+                if LSMODE == "none" or ((et.max() < emax) if LSMODE == "max" else ((et * et).sum() < (e_abs * e_abs).sum())):
                     x, acc = xt, True
                     break
                 step *= f32(0.5)
+            if LSMODE == "none":
+                ssn_n += 1
+                if emax < best_e:
+                    best_e, best_x = emax, x_prev
+                if ssn_n >= SSN_MAX:
+                    # back to the best point seen, then the staggered phase
+                    wtmp = (A @ x).astype(f32)
+                    mtmp = (np.abs(A) @ np.abs(x)).astype(f32)
+                    Lb, Ub = bounds(x)
+                    et2, _ = res(x, wtmp, mtmp, Lb, Ub, f32(2e-6) * (1 + np.abs(x).max()))
+                    if et2.max() > best_e:
+                        x = best_x
+                    phase, new_round = 1, True
+                continue
             if not acc:
                 phase, new_round = 1, True
             continue
@@ -630,6 +659,8 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
         else:
             x = np.where(fr, x + d, x).astype(f32)
             at_min = True
+    if not conv and BEST:
+        x = best_x
     return x, solves, conv
 
 

@@ -19,6 +19,7 @@ from mwstep.sim import Simulator  # noqa: E402
 
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 PGS = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+print(f"exact={os.environ.get('MW_PROF_EXACT', '1')} warm={os.environ.get('MW_PROF_WARM', '0')}")
 T = 20
 PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
           "Delassus (lane = column)", "PGS + exact LCP", "rows total (responses .. integrate)", "whole substep"]
@@ -41,7 +42,7 @@ sim.run_device(50)
 L = N.lib()
 fn = L.mw_debug_wave_prof
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 10)()
 fn(buf)  # clear
 t0 = time.perf_counter()
 sim.run_device(T)
@@ -51,4 +52,5 @@ fn(buf)
 print(f"{W} worlds, PGS {PGS}, {T} steps: {dt / T * 1e6:.1f} us/step wall; contacts in world 0: {len(sim.contacts(0))}")
 for k, name in enumerate(PHASES):
     print(f"  {name:40s} {buf[k] / W / T:12.0f} cycles/world-step")
+print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f} rounds per world-step")
 sim.close()

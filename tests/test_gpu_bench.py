@@ -38,3 +38,14 @@ def test_driver_bench_command(require_gpu):
     assert out["rollout_fused"]["steps_per_launch"] == 1000
     assert out["panda_c4"]["worlds_per_gpu"] == 1024
     assert out["humanoid_c5"]["worlds_per_gpu"] == 512
+    # every BASELINE config leg carries its roofline and a CPU baseline
+    pend = out["pendulum_c3"]
+    assert "configs[2]" in pend["workload"] and pend["value"] > 1e6 and pend["kernel_us_per_launch"] > 0
+    for leg in ("pendulum_c3", "panda_c4", "humanoid_c5"):
+        rl_, cb = out[leg]["roofline"], out[leg]["cpu_baseline"]
+        assert rl_["peak"] > 0 and rl_["bound"] in ("hbm", "valu-issue"), leg
+        assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0, leg
+    assert out["pendulum_c3"]["roofline"]["frac"] > 0 and out["panda_c4"]["roofline"]["frac"] > 0
+    h = out["humanoid_c5"]
+    assert h["constraint_overflow"] == 0 and h["lcp_unconverged_world_steps"] is not None
+    assert "exact boxed LCP" in h["workload"] and "PGS" in out["humanoid_c5_pgs_only"]["workload"]

@@ -200,3 +200,32 @@ def test_baked_kernel_matches_generic(require_gpu, oracle, task, kind, model, mo
     assert worst <= 1e-5
     a.close()
     b.close()
+
+
+def test_pendulum_2048_worlds(require_gpu, oracle):
+    """BASELINE config 3 at its size: 2048 PendulumSwingUp worlds (continuous
+    torque U(-50, 50)).  One-step teacher-forced observation error <= 1e-4 over
+    50 steps, free-running error <= 1e-3 over 100 steps, reset observations
+    <= 1e-6, done flags equal."""
+    W = 2048
+    torch, gpu, ref = _pair(oracle, "PendulumSwingUp", 3, "pendulum", W)
+    og = gpu.reset().cpu().numpy()
+    assert np.abs(og - ref.reset()).max() <= 1e-6
+    acts = _actions(3, 150, W, seed=11)
+    n = ref.cm.n
+    worst = 0.0
+    for t in range(50):
+        gpu.set_state(torch.from_numpy(ref.q.reshape(n, W)), torch.from_numpy(ref.qd.reshape(n, W)))
+        o, _, d, _ = gpu.step(torch.from_numpy(acts[t]).cuda())
+        orf, _, drf, _ = ref.step(acts[t].astype(np.float64))
+        assert np.array_equal(d.cpu().numpy().astype(bool), drf)
+        worst = max(worst, float(np.abs(o.cpu().numpy() - orf).max()))
+    free = 0.0
+    for t in range(50, 150):
+        o, _, d, _ = gpu.step(torch.from_numpy(acts[t]).cuda())
+        orf, _, drf, _ = ref.step(acts[t].astype(np.float64))
+        m = ~(d.cpu().numpy().astype(bool) | drf)
+        free = max(free, float(np.abs(o.cpu().numpy()[m] - orf[m]).max()))
+    print(f"pendulum x{W}: one-step {worst:.2e}, free-running 100 steps {free:.2e}")
+    assert worst <= 1e-4 and free <= 1e-3
+    gpu.close()
