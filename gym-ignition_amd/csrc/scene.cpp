@@ -120,6 +120,11 @@ struct mw_scene {
     bool ran = false;              // an unpaused run produced contacts
     bool idle = true;              // nothing of ours is queued on the stream
     bool clear_cmd = false, clear_base = false;  // consumed mirrors to clear after the next sync
+    // direct runs: the kernel reads the command block out of the pinned mirror
+    // (h_joint_dev: its device address) and writes q / qd / qdd into it; the
+    // device copy of the command block is then stale until the next upload
+    float* h_joint_dev = nullptr;
+    bool dev_cmd_stale = false;
 
     size_t jidx(int d, int w) const { return static_cast<size_t>(d) * W + w; }
     float* hq() { return reinterpret_cast<float*>(h_joint); }
@@ -355,9 +360,9 @@ void clear_consumed(mw_scene* s) {
 // (asynchronous copies out of the pinned mirrors).  defer: the caller
 // synchronises later and then calls clear_consumed(); otherwise this waits
 // for the copies and clears the consumed mirrors itself.
-int flush(mw_scene* s, bool defer) {
+int flush(mw_scene* s, bool defer, bool direct = false) {
     const bool any = s->params_dirty || s->cmd_dirty || s->base_dirty || s->present_dirty || s->wrench_dirty ||
-                     s->pid_dirty;
+                     s->pid_dirty || (s->dev_cmd_stale && !direct);
     if (!any) return MW_OK;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     SC_HIP(hipStreamIsCapturing(s->stream, &cap));
@@ -374,10 +379,17 @@ int flush(mw_scene* s, bool defer) {
         SC_HIP(hipMemsetAsync(s->d_warm, 0, s->W * sizeof(int32_t), s->stream));
         s->params_dirty = false;
     }
-    if (s->cmd_dirty) {
+    if (direct) {
+        // the launch reads the command block straight out of the mirror
+        if (s->cmd_dirty) {
+            s->clear_cmd = true;
+            s->dev_cmd_stale = true;
+        }
+    } else if (s->cmd_dirty || s->dev_cmd_stale) {
         SC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(s->d_joint) + s->cmd_off(), s->h_joint + s->cmd_off(),
                               s->cmd_bytes(), hipMemcpyHostToDevice, s->stream));
-        s->clear_cmd = true;
+        s->clear_cmd = s->clear_cmd || s->cmd_dirty;
+        s->dev_cmd_stale = false;
     }
     if (s->base_dirty) {
         const size_t off = 13 * s->krows() * sizeof(float);
@@ -559,8 +571,16 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     s->jrows = static_cast<size_t>(NBMAX) * W;
     SC_HIP(hipMalloc(&s->d_joint, s->joint_bytes()));
     SC_HIP(hipMemsetAsync(s->d_joint, 0, s->joint_bytes(), s->stream));
-    SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_joint), s->cmd_off() + s->cmd_bytes(), hipHostMallocDefault));
+    // coherent: direct runs read the command block out of it and write the
+    // joint planes into it (scene_run)
+    SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_joint), s->cmd_off() + s->cmd_bytes(),
+                         hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(s->h_joint, 0, s->cmd_off() + s->cmd_bytes());
+    {
+        void* dptr = nullptr;
+        if (hipHostGetDevicePointer(&dptr, s->h_joint, 0) == hipSuccess) s->h_joint_dev = static_cast<float*>(dptr);
+        else (void)hipGetLastError();
+    }
     SC_HIP(hipMalloc(&s->d_base, s->base_bytes()));
     SC_HIP(hipMemsetAsync(s->d_base, 0, s->base_bytes(), s->stream));
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_base), s->base_bytes(), hipHostMallocDefault));
@@ -877,13 +897,24 @@ int mw_scene_model_export(const mw_scene* s, int32_t model, double* out, int32_t
     return MW_OK;
 }
 
-static int scene_run(mw_scene* s, int32_t paused, bool defer) {
+static int scene_run(mw_scene* s, int32_t paused, bool defer, bool direct = false) {
     if (int rc = check(s)) return rc;
     if (s->models.empty()) {
         if (!paused) s->iterations += s->cfg.steps_per_run;
         return MW_OK;
     }
-    if (int rc = flush(s, defer)) return rc;
+    if (int rc = flush(s, defer, direct)) return rc;
+    mw::SceneDev D = s->dev;
+    if (direct) {
+        // the command block and the readback planes in the pinned mirror
+        float* hj = s->h_joint_dev;
+        const size_t r = s->jrows;
+        D.cmd = hj + 3 * r; D.vtgt = hj + 4 * r; D.rq = hj + 5 * r; D.rqd = hj + 6 * r; D.ptgt = hj + 7 * r;
+        D.act = reinterpret_cast<uint8_t*>(hj + 8 * r);
+        D.rflag = D.act + r;
+        D.rb = hj;
+        D.rb_plane = static_cast<int32_t>(r);
+    }
     mw::SceneArgs a{};
     a.dt = static_cast<float>(s->cfg.step_size);
     a.inv_dt = static_cast<float>(1.0 / s->cfg.step_size);
@@ -911,7 +942,7 @@ static int scene_run(mw_scene* s, int32_t paused, bool defer) {
                 }
             }
         }
-        SC_HIP(mw::launch_scene_run(s->dp, s->nv, s->dev, s->d_pid, G, s->W, a, s->stream));
+        SC_HIP(mw::launch_scene_run(s->dp, s->nv, D, s->d_pid, G, s->W, a, s->stream));
         s->idle = false;
         a.first = 0;
         done += chunk;
@@ -925,13 +956,25 @@ static int scene_run(mw_scene* s, int32_t paused, bool defer) {
     return MW_OK;
 }
 
+// joint planes (q, qd, qdd) up to this size run direct (mw_scene_run)
+constexpr size_t kDirectBytes = size_t{64} << 10;
+
 int mw_scene_run(mw_scene* s, int32_t paused) {
     // one synchronisation per run: uploads, the launch and the readback of
     // the joint and base state are queued back to back
-    if (int rc = scene_run(s, paused, true)) return rc;
+    // small scenes (the per-env path, BASELINE config 1) run direct: no
+    // command upload, no joint readback copy -- one launch, one synchronisation
+    const bool direct = s->h_joint_dev && 3 * s->jrows * sizeof(float) <= kDirectBytes;
+    if (int rc = scene_run(s, paused, true, direct)) return rc;
     if (s->models.empty()) return MW_OK;
-    // per-env runs (BASELINE config 1): skip the copies that cannot carry news
-    if (int rc = queue_readback(s, needs_base_readback(s))) return rc;
+    // per-env runs: skip the copies that cannot carry news
+    if (direct) {
+        const size_t brows = static_cast<size_t>(13 * s->models.size()) * s->W * sizeof(float);
+        if (brows && needs_base_readback(s))
+            SC_HIP(hipMemcpyAsync(s->h_base, s->d_base, brows, hipMemcpyDeviceToHost, s->stream));
+    } else if (int rc = queue_readback(s, needs_base_readback(s))) {
+        return rc;
+    }
     // the drop counter rides on the same synchronisation
     if (can_overflow(s))
         SC_HIP(hipMemcpyAsync(s->h_overflow, s->dev.overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));

@@ -1332,6 +1332,11 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         D.qd[k] = L.qd[lane];
         if (!A.paused) D.qdd[k] = L.qdd[lane];
         D.cmd[k] = 0.f;
+        if (D.rb) {
+            D.rb[k] = L.q[lane];
+            D.rb[D.rb_plane + k] = L.qd[lane];
+            if (!A.paused) D.rb[2 * static_cast<size_t>(D.rb_plane) + k] = L.qdd[lane];
+        }
     }
     if (baselane) {
         auto at = [&](int f) -> float& { return D.base[static_cast<size_t>(13 * bm + f) * W + w]; };

@@ -118,6 +118,11 @@ struct SceneDev {
     // or n_slots + 4 pair + point) [c][W], then kScWarmRows impulses [row][W]
     // (contact c rows 3 c + d, joint rows kScWarmJoint0 + 3 body + type)
     int32_t* warm;
+    // direct runs (mw_scene_run of small scenes): the host-mapped q / qd / qdd
+    // planes of the pinned mirror, [3][rb_plane], written beside the device
+    // state so the run needs no readback copy; nullptr otherwise
+    float* rb;
+    int32_t rb_plane;
 };
 
 constexpr int kScWarmJoint0 = 3 * kScMaxContacts;

@@ -102,7 +102,14 @@ class Box(Space):
         if isinstance(x, list):
             x = np.array(x)
         x = np.asarray(x)
-        return x.shape == self.shape and bool(np.all(x >= self.low)) and bool(np.all(x <= self.high))
+        if x.shape != self.shape:
+            return False
+        if x.size <= 16:
+            # the per-env path checks a handful of values per step: Python
+            # floats beat two numpy reductions (NaN fails either way)
+            return all(lo <= v <= hi for v, lo, hi in
+                       zip(x.ravel().tolist(), self.low.ravel().tolist(), self.high.ravel().tolist()))
+        return bool(np.all(x >= self.low)) and bool(np.all(x <= self.high))
 
     def __repr__(self):
         return f"Box({self.low}, {self.high}, {self.shape}, {self.dtype})"

@@ -35,6 +35,7 @@ class Scene:
     def _models_changed(self) -> None:
         # the per-env ScenarI/O path asks for the same selections every step
         self._selcache = {}
+        self._touch()
         self._nd = sum(i["dofs"] for i in self.models)
 
     @property
@@ -208,6 +209,9 @@ class Scene:
 
     def _touch(self) -> None:
         self.__dict__.setdefault("_cache", {}).clear()
+        # generation of the joint state: getters above this layer memoise
+        # per generation (scenario.gazebo.Model)
+        self.gen = self.__dict__.get("gen", 0) + 1
 
     def _cached(self, what: str) -> Optional[np.ndarray]:
         nd = self._nd

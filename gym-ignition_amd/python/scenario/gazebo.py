@@ -739,11 +739,29 @@ class Model:
             dof_idx = np.asarray(dof_idx, dtype=np.int32)
         return self._sim.get(what, 0, 1, dof_idx)[0]
 
+    def _state_list(self, what: str, joint_names: Sequence[str]) -> List[float]:
+        # the per-env path reads the same joints several times per env step
+        # (observation, reward, termination): memoised per joint-state
+        # generation of the scene (every run and mutator starts a new one)
+        if self._sim is None:
+            raise RuntimeError(f"model '{self._name}' was removed")
+        gen = self._sim.scene.gen
+        key = (what, tuple(joint_names) if joint_names else ())
+        memo = self.__dict__.setdefault("_memo", {})
+        hit = memo.get(key)
+        if hit is not None and hit[0] == gen:
+            return list(hit[1])
+        val = self._get(what, self._dofs(joint_names)).tolist()
+        if len(memo) > 64:
+            memo.clear()
+        memo[key] = (gen, val)
+        return list(val)
+
     def joint_positions(self, joint_names: Sequence[str] = ()) -> List[float]:
-        return self._get("q", self._dofs(joint_names)).tolist()
+        return self._state_list("q", joint_names)
 
     def joint_velocities(self, joint_names: Sequence[str] = ()) -> List[float]:
-        return self._get("qd", self._dofs(joint_names)).tolist()
+        return self._state_list("qd", joint_names)
 
     def joint_accelerations(self, joint_names: Sequence[str] = ()) -> List[float]:
         return self._get("qdd", self._dofs(joint_names)).tolist()

@@ -614,3 +614,41 @@ def test_cylinder_stack_on_a_table(require_gpu):
         on_table = sum(r[8] for r in sc.contacts(w) if int(r[10]) == 0 and int(r[12]) >= 0)
         assert abs(on_table) == pytest.approx(3.0 * G, abs=0.1)
     sc.close()
+
+
+def test_direct_runs_match_device_runs(require_gpu):
+    """Small scenes run direct (mw_scene_run: the kernel reads the command
+    block out of the pinned mirror and writes q / qd / qdd into it, no
+    copies).  A mix of direct runs and device runs (mw_scene_run_device, which
+    must first upload the command block the direct runs left stale: control
+    modes, targets) steps exactly like direct runs alone."""
+    from mwstep import get_model_file
+    from mwstep import native as N
+    from mwstep.scene import Scene
+    scenes = []
+    for _ in range(2):
+        sc = Scene(n_worlds=2, step_size=1e-3, steps_per_run=1)
+        sc.insert_model(get_model_file("cartpole"))
+        sc.set_control_mode(N.MODE_POSITION, m=0)
+        for d in range(sc._nd):
+            sc.set_pid(d, [100.0, 0.0, 5.0, -50.0, 50.0, 0.0, 0.0, -1.0])
+        sc.set("position_target", np.full((2, sc._nd), 0.2), m=0)
+        sc.run(paused=True)
+        scenes.append(sc)
+    a, b = scenes
+    for k in range(30):
+        a.run()
+        if k % 3 == 2:
+            b.run_device(1)
+            b.get("q")  # pulls the joint planes
+        else:
+            b.run()
+        if k == 10:
+            for sc in scenes:
+                sc.set("position_target", np.full((2, sc._nd), -0.1), m=0)
+        qa, qb = a.get("q"), b.get("q")
+        assert np.array_equal(qa, qb), (k, qa, qb)
+        assert np.array_equal(a.get("qd"), b.get("qd"))
+    assert np.abs(a.get("q")).max() > 1e-3  # the targets moved the joints
+    for sc in scenes:
+        sc.close()
