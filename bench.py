@@ -819,7 +819,8 @@ def valu_roofline(kernel_us, W, exact):
             d = json.load(f)
     except (OSError, ValueError):
         d = None
-    if not d or d.get("worlds") != W or d.get("exact_lcp") != exact:
+    d = next((e for e in (d or {}).get("entries", []) if e.get("worlds") == W and e.get("exact_lcp") == exact), None)
+    if not d:
         return {"bound": "valu-issue", "achieved": None, "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
                 "frac": None, "kernel_us_per_launch": kernel_us,
                 "note": f"no PMC summary for {W} worlds (exact_lcp={exact}) in profiles/pmc_summary_wave.json"}

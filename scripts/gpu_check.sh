@@ -52,10 +52,14 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "panda pmc $ctr rc=$rc" | tee -a "$OUT/session.log"
   stop_if_fatal $rc panda_pmc
 done
-# config 5 (humanoid, wave kernel): SQ counters of the step kernel
-echo "== wave kernel SQ pmc" | tee -a "$OUT/session.log"
-timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA \
-  --kernel-trace --output-format csv -d "$OUT/pmc_wave_$tag" -o run -- python3 scripts/wave_sweep.py humanoid32 512 > "$OUT/pmc_wave_$tag.log" 2>&1
-rc=$?; echo "wave pmc rc=$rc" | tee -a "$OUT/session.log"
-stop_if_fatal $rc wave_pmc
+# config 5 (humanoid, wave kernel): SQ counters of the step kernel on the bench's
+# own humanoid legs (exact LCP, PGS only), one pass each -> profiles/pmc_summary_wave.json
+for leg in humanoid humanoid_pgs; do
+  echo "== wave kernel SQ pmc $leg" | tee -a "$OUT/session.log"
+  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_WAVE_CYCLES \
+    SQ_WAIT_ANY SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_wave_${leg}_$tag" -o run -- \
+    python3 scripts/leg_probe.py $leg > "$OUT/pmc_wave_${leg}_$tag.log" 2>&1
+  rc=$?; echo "wave pmc $leg rc=$rc" | tee -a "$OUT/session.log"
+  stop_if_fatal $rc wave_pmc
+done
 exit 0
