@@ -566,7 +566,8 @@ Description describe_sdf(const XNode* root, const double pose[7]) {
         if (J.parent == "world") world_used = true;
         else if (!raw.count(J.parent)) throw std::runtime_error("joint " + J.name + " references an unknown link");
         if (!raw.count(J.child)) throw std::runtime_error("joint " + J.name + " references an unknown link");
-        if (J.type != "fixed" && J.type != "revolute" && J.type != "continuous" && J.type != "prismatic")
+        if (J.type != "fixed" && J.type != "revolute" && J.type != "continuous" && J.type != "prismatic" &&
+            J.type != "ball")
             throw std::runtime_error("unsupported joint type '" + J.type + "' (" + J.name + ")");
         s.XJ = sdf_pose(je, "joint '" + J.name + "'");
         const XNode* ax = je->child("axis");
@@ -592,7 +593,8 @@ Description describe_sdf(const XNode* root, const double pose[7]) {
             if (J.effort < 0.0) J.effort = 1e300;
             if (J.velocity < 0.0) J.velocity = 1e300;
             if (J.type == "revolute" && J.lower <= -1e16 && J.upper >= 1e16) J.type = "continuous";
-            if (J.type == "continuous") { J.lower = -1e300; J.upper = 1e300; }
+            // a ball joint has no position limits (Joint.cpp:876-880)
+            if (J.type == "continuous" || J.type == "ball") { J.lower = -1e300; J.upper = 1e300; }
             if (J.type == "prismatic") {
                 if (J.lower <= -1e16) J.lower = -1e300;
                 if (J.upper >= 1e16) J.upper = 1e300;
@@ -765,31 +767,54 @@ ChainModel compile_description(Description D) {
     out.base_link = base;
     out.base_R = baseR;
     out.base_p = baseP;
+    // a ball joint (SDF "ball", 3 dofs, Joint.cpp:318-331) becomes three
+    // revolute joints about the x, y and z axes of its frame at one point, the
+    // first two carrying massless bodies: the same rigid motion (a spherical
+    // pair), parameterised by intrinsic X-Y-Z angles instead of DART's
+    // rotation vector -- the ScenarI/O layer converts positions, velocities,
+    // forces and resets (scenario/gazebo.py BallJoint)
+    std::vector<int> last_body(chain.size(), -1);  // the body carrying joint k's child link
     for (size_t k = 0; k < chain.size(); ++k) {
         const Joint& j = chain[k];
-        ChainBody b;
-        b.parent = parent_of[k];
-        b.joint_name = j.name;
-        b.link_name = j.child;
-        b.type = (j.type == "prismatic") ? JType::Prismatic : JType::Revolute;
-        b.continuous = (j.type == "continuous");
-        b.limited = (j.type == "revolute" || j.type == "prismatic");
-        b.E = mul(offR[j.parent], j.R);
-        b.r = add(mul(offR[j.parent], j.p), offP[j.parent]);
-        b.axis = j.axis;
-        const Link& L = links[j.child];
-        b.mass = L.mass;
-        b.com = L.com;
-        b.Ic = {L.I[0], L.I[4], L.I[8], L.I[1], L.I[2], L.I[5]};
-        b.damping = j.damping;
-        b.friction = j.friction;
-        b.lower = j.lower;
-        b.upper = j.upper;
-        b.effort = j.effort;
-        b.vel_limit = j.velocity;
-        b.shapes = L.shapes;
-        if (b.mass <= 0.0) throw std::runtime_error("moving link '" + j.child + "' has no mass");
-        out.bodies.push_back(b);
+        const bool ball = (j.type == "ball");
+        const int parts = ball ? 3 : 1;
+        for (int part = 0; part < parts; ++part) {
+            const bool carrier = (part == parts - 1);
+            ChainBody b;
+            b.parent = (part > 0) ? static_cast<int>(out.bodies.size()) - 1
+                                  : (parent_of[k] >= 0 ? last_body[parent_of[k]] : -1);
+            b.joint_name = ball ? j.name + (part == 0 ? "#x" : (part == 1 ? "#y" : "#z")) : j.name;
+            b.link_name = carrier ? j.child : j.name + (part == 0 ? "#x" : "#y");
+            b.type = (j.type == "prismatic") ? JType::Prismatic : JType::Revolute;
+            b.continuous = (j.type == "continuous" || ball);
+            b.limited = (j.type == "revolute" || j.type == "prismatic");
+            if (part == 0) {
+                b.E = mul(offR[j.parent], j.R);
+                b.r = add(mul(offR[j.parent], j.p), offP[j.parent]);
+            } else {
+                b.E = eye();
+                b.r = {0, 0, 0};
+            }
+            b.axis = ball ? std::array<double, 3>{part == 0 ? 1.0 : 0.0, part == 1 ? 1.0 : 0.0, part == 2 ? 1.0 : 0.0}
+                          : j.axis;
+            b.ball = ball ? part + 1 : 0;
+            if (carrier) {
+                const Link& L = links[j.child];
+                b.mass = L.mass;
+                b.com = L.com;
+                b.Ic = {L.I[0], L.I[4], L.I[8], L.I[1], L.I[2], L.I[5]};
+                b.shapes = L.shapes;
+                if (b.mass <= 0.0) throw std::runtime_error("moving link '" + j.child + "' has no mass");
+            }
+            b.damping = j.damping;
+            b.friction = j.friction;
+            b.lower = j.lower;
+            b.upper = j.upper;
+            b.effort = j.effort;
+            b.vel_limit = j.velocity;
+            out.bodies.push_back(b);
+        }
+        last_body[k] = static_cast<int>(out.bodies.size()) - 1;
     }
     if (out.floating) {
         const Link& B = links[base];

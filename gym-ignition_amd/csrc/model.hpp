@@ -38,6 +38,10 @@ struct ChainBody {
     double lower = -1e300, upper = 1e300;
     double effort = 1e300, vel_limit = 1e300;
     std::vector<struct Shape> shapes;  // collision shapes of the (lumped) link, body frame
+    // 1..3: part of a ball joint, the rotation about x, y or z of the joint
+    // frame (intrinsic X-Y-Z angles; parts 1 and 2 are massless, part 3
+    // carries the child link); 0: a 1-dof joint
+    int ball = 0;
 };
 
 // A collision shape in its body's frame: box (size = half extents), sphere

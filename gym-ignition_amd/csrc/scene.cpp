@@ -861,7 +861,7 @@ int mw_scene_joint_type(const mw_scene* s, int32_t dof, int32_t* type) {
     const int m = s->model_of_dof(dof);
     if (m < 0 || !type) return fail(MW_EINVAL, "bad argument");
     const mw::ChainBody& b = s->models[m].m.bodies[dof - s->models[m].body0];
-    *type = (b.type == mw::JType::Prismatic) ? MW_JOINT_PRISMATIC : MW_JOINT_REVOLUTE;
+    *type = b.ball ? MW_JOINT_BALL : ((b.type == mw::JType::Prismatic) ? MW_JOINT_PRISMATIC : MW_JOINT_REVOLUTE);
     return MW_OK;
 }
 

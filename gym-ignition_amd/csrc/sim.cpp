@@ -1180,7 +1180,8 @@ int mw_joint_type(const mw_sim* s, int32_t dof, int32_t* type) {
     if (!s || !type) return fail(MW_EINVAL, "null argument");
     if (!s->loaded) return fail(MW_ESTATE, "no model loaded");
     if (dof < 0 || dof >= s->model.dofs()) return fail(MW_EINVAL, "dof out of range");
-    *type = (s->model.bodies[dof].type == mw::JType::Prismatic) ? MW_JOINT_PRISMATIC : MW_JOINT_REVOLUTE;
+    const mw::ChainBody& b = s->model.bodies[dof];
+    *type = b.ball ? MW_JOINT_BALL : ((b.type == mw::JType::Prismatic) ? MW_JOINT_PRISMATIC : MW_JOINT_REVOLUTE);
     return MW_OK;
 }
 

@@ -357,6 +357,234 @@ class Joint:
         return self.position_limit()
 
 
+# ------------------------------------------------------------------ BallJoint
+# A ball joint (core::JointType::Ball, 3 dofs, Joint.cpp:318-331) is compiled
+# as three revolute dofs `<name>#x/#y/#z` about the axes of its frame at one
+# point (csrc/model.cpp): intrinsic X-Y-Z angles (a, b, c), R = Rx(a) Ry(b)
+# Rz(c).  This class presents DART's BallJoint coordinates over them:
+# positions = the rotation vector of R, velocities = the child's angular
+# velocity in the child frame w = J(b, c) [a', b', c'], accelerations = w',
+# forces = torques in the child frame (tau_angles = J^T tau).  J is singular
+# at b = +-pi/2 (the angle parameterisation's gimbal lock).
+def _rx(a):
+    c, s = math.cos(a), math.sin(a)
+    return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+
+
+def _ry(b):
+    c, s = math.cos(b), math.sin(b)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def _rz(c_):
+    c, s = math.cos(c_), math.sin(c_)
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+def ball_R(e) -> np.ndarray:
+    return _rx(e[0]) @ _ry(e[1]) @ _rz(e[2])
+
+
+def ball_J(e) -> np.ndarray:
+    """child-frame angular velocity per angle rate: w = J(e) e'"""
+    cb, sb, cc, sc = math.cos(e[1]), math.sin(e[1]), math.cos(e[2]), math.sin(e[2])
+    return np.array([[cb * cc, sc, 0.0], [-cb * sc, cc, 0.0], [sb, 0.0, 1.0]])
+
+
+def ball_Jdot(e, ed) -> np.ndarray:
+    cb, sb, cc, sc = math.cos(e[1]), math.sin(e[1]), math.cos(e[2]), math.sin(e[2])
+    db = np.array([[-sb * cc, 0, 0], [sb * sc, 0, 0], [cb, 0, 0]])
+    dc = np.array([[-cb * sc, cc, 0], [-cb * cc, -sc, 0], [0, 0, 0]])
+    return db * ed[1] + dc * ed[2]
+
+
+def rotvec_from_R(R) -> np.ndarray:
+    """log map of SO(3) (the rotation vector, DART BallJoint positions)"""
+    c = max(-1.0, min(1.0, (np.trace(R) - 1.0) / 2.0))
+    th = math.acos(c)
+    w = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    if th < 1e-7:
+        return 0.5 * w
+    if math.pi - th < 1e-6:
+        # near pi: the axis from the symmetric part
+        A = (R + np.eye(3)) / 2.0
+        k = int(np.argmax(np.diag(A)))
+        ax = A[:, k] / math.sqrt(max(A[k, k], 1e-300))
+        return th * ax / np.linalg.norm(ax)
+    return th / (2.0 * math.sin(th)) * w
+
+
+def R_from_rotvec(r) -> np.ndarray:
+    r = np.asarray(r, dtype=float)
+    th = float(np.linalg.norm(r))
+    if th < 1e-12:
+        return np.eye(3)
+    k = r / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+
+
+def ball_angles(R) -> np.ndarray:
+    """(a, b, c) with Rx(a) Ry(b) Rz(c) = R, b in [-pi/2, pi/2]"""
+    b = math.asin(max(-1.0, min(1.0, R[0, 2])))
+    a = math.atan2(-R[1, 2], R[2, 2])
+    c = math.atan2(-R[0, 1], R[0, 0])
+    return np.array([a, b, c])
+
+
+class BallJoint(Joint):
+    """A 3-dof ball joint over its three internal revolute dofs."""
+
+    def __init__(self, model: "Model", dof: int, name: str):
+        super().__init__(model, dof, name)
+        self._idx = [dof, dof + 1, dof + 2]
+        self._names = [f"{name}#x", f"{name}#y", f"{name}#z"]
+
+    def type(self) -> int:
+        return core.JointType_ball
+
+    def dofs(self) -> int:
+        return 3
+
+    def _check_dof(self, dof: int) -> None:
+        if not 0 <= dof < 3:
+            raise RuntimeError(f"DOF mismatch: joint '{self._name}' has 3 DoFs, requested #{dof}")
+
+    def _angles(self, what: str = "q") -> np.ndarray:
+        pend = self._model._ball_pending.get(self._name) if what == "q" else None
+        return pend if pend is not None else np.asarray(self._model._get(what, self._idx), dtype=float)
+
+    # -- state in DART's BallJoint coordinates
+    def joint_position(self) -> List[float]:
+        return rotvec_from_R(ball_R(self._angles())).tolist()
+
+    def joint_velocity(self) -> List[float]:
+        return (ball_J(self._angles()) @ self._angles("qd")).tolist()
+
+    def joint_acceleration(self) -> List[float]:
+        e, ed, edd = self._angles(), self._angles("qd"), self._angles("qdd")
+        return (ball_J(e) @ edd + ball_Jdot(e, ed) @ ed).tolist()
+
+    def _torque(self, what: str) -> List[float]:
+        return np.linalg.solve(ball_J(self._angles()).T, self._angles(what)).tolist()
+
+    def joint_generalized_force(self) -> List[float]:
+        return self._torque("force")
+
+    def joint_generalized_force_target(self) -> List[float]:
+        return self._torque("force_target")
+
+    def position(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self.joint_position()[dof]
+
+    def velocity(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self.joint_velocity()[dof]
+
+    def acceleration(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self.joint_acceleration()[dof]
+
+    def generalized_force(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self.joint_generalized_force()[dof]
+
+    def generalized_force_target(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return self.joint_generalized_force_target()[dof]
+
+    # -- conversions into the internal angles (used by Model._set)
+    def _to_internal(self, what: str, v) -> np.ndarray:
+        v = np.asarray(v, dtype=float)
+        if what == "reset_q":
+            e = ball_angles(R_from_rotvec(v))
+            self._model._ball_pending[self._name] = e
+            return e
+        if what == "reset_qd":
+            return np.linalg.solve(ball_J(self._angles()), v)
+        if what == "force_target":
+            return ball_J(self._angles()).T @ v
+        raise RuntimeError(f"Joint '{self._name}' (ball) does not support {what}")
+
+    def set_joint_generalized_force_target(self, target: Sequence[float]) -> bool:
+        return len(target) == 3 and self._model.set_joint_generalized_force_targets(list(target), [self._name])
+
+    def set_generalized_force_target(self, force: float, dof: int = 0) -> bool:
+        if not 0 <= dof < 3:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        t = self.joint_generalized_force_target()
+        t[dof] = float(force)
+        return self.set_joint_generalized_force_target(t)
+
+    def reset_joint_position(self, position: Sequence[float]) -> bool:
+        return len(position) == 3 and self._model.reset_joint_positions(list(position), [self._name])
+
+    def reset_joint_velocity(self, velocity: Sequence[float]) -> bool:
+        return len(velocity) == 3 and self._model.reset_joint_velocities(list(velocity), [self._name])
+
+    def reset_position(self, position: float, dof: int = 0) -> bool:
+        if not 0 <= dof < 3:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        p = self.joint_position()
+        p[dof] = float(position)
+        return self.reset_joint_position(p)
+
+    def reset_velocity(self, velocity: float, dof: int = 0) -> bool:
+        if not 0 <= dof < 3:
+            _err(f"Joint '{self._name}' does not have DoF#{dof}")
+            return False
+        v = self.joint_velocity()
+        v[dof] = float(velocity)
+        return self.reset_joint_velocity(v)
+
+    def reset(self, position: float = 0.0, velocity: float = 0.0, dof: int = 0) -> bool:
+        return self.reset_position(position, dof) and self.reset_velocity(velocity, dof)
+
+    # -- JointController and limits: not defined for ball joints
+    # (JointController.cpp:323-327 skips them; Joint.cpp:876-900 warns)
+    def set_control_mode(self, mode: int) -> bool:
+        if mode not in (core.JointControlMode_force, core.JointControlMode_idle):
+            _err(f"Type of joint '{self._name}' not supported by the JointController")
+            return False
+        return self._model.set_joint_control_mode(mode, [self._name])
+
+    def control_mode(self) -> int:
+        return self._model._sim.control_mode(0, self._dof)
+
+    def _unsupported(self, what: str) -> bool:
+        _err(f"Joint '{self._name}' (ball) has no {what}")
+        return False
+
+    def set_position_target(self, position: float, dof: int = 0) -> bool:
+        return self._unsupported("position target")
+
+    def set_velocity_target(self, velocity: float, dof: int = 0) -> bool:
+        return self._unsupported("velocity target")
+
+    def set_joint_position_target(self, target: Sequence[float]) -> bool:
+        return self._unsupported("position target")
+
+    def set_joint_velocity_target(self, target: Sequence[float]) -> bool:
+        return self._unsupported("velocity target")
+
+    def position_limit(self, dof: int = 0) -> core.Limit:
+        self._check_dof(dof)
+        return core.Limit(-math.inf, math.inf)
+
+    def joint_position_limit(self) -> core.Limit:
+        return core.JointLimit([-math.inf] * 3, [math.inf] * 3)
+
+    def max_generalized_force(self, dof: int = 0) -> float:
+        self._check_dof(dof)
+        return math.inf
+
+    def joint_max_generalized_force(self) -> List[float]:
+        return [math.inf] * 3
+
+
 # ---------------------------------------------------------------------- Model
 class Model:
     """An articulated model (one native simulator with a single world)."""
@@ -366,7 +594,24 @@ class Model:
         self._name = name
         self._sim = sim
         self._pose = pose
-        self._joints = {n: Joint(self, i, n) for i, n in enumerate(sim.joint_names)}
+        # ScenarI/O joints: a ball joint's three internal dofs are one Joint
+        self._joints: Dict[str, Joint] = {}
+        self._jnames: List[str] = []
+        self._ball: Dict[str, BallJoint] = {}
+        self._ball_pending: Dict[str, np.ndarray] = {}  # reset angles not yet applied by a run
+        names = list(sim.joint_names)
+        i = 0
+        while i < len(names):
+            n = names[i]
+            if n.endswith("#x") and i + 2 < len(names) and sim.joint_type(i) == 4 and names[i + 2] == n[:-2] + "#z":
+                j = BallJoint(self, i, n[:-2])
+                self._ball[j._name] = j
+                i += 3
+            else:
+                j = Joint(self, i, n)
+                i += 1
+            self._joints[j._name] = j
+            self._jnames.append(j._name)
         self._pending_vel = None
         self._export = None  # exported model rows (link forward kinematics)
         self._history: Optional[collections.deque] = None
@@ -384,10 +629,12 @@ class Model:
         return self._name
 
     def dofs(self, joint_names: Sequence[str] = ()) -> int:
-        return len(joint_names) if joint_names else self._sim.dofs
+        if not joint_names:
+            return self._sim.dofs
+        return sum(self._joints[n].dofs() if n in self._joints else 1 for n in joint_names)
 
     def joint_names(self, scoped: bool = False) -> List[str]:
-        return [f"{self._name}::{n}" if scoped else n for n in self._sim.joint_names]
+        return [f"{self._name}::{n}" if scoped else n for n in self._jnames]
 
     def get_joint(self, joint_name: str) -> Joint:
         if joint_name not in self._joints:
@@ -395,13 +642,13 @@ class Model:
         return self._joints[joint_name]
 
     def joints(self, joint_names: Sequence[str] = ()) -> List[Joint]:
-        return [self.get_joint(n) for n in (joint_names or self._sim.joint_names)]
+        return [self.get_joint(n) for n in (joint_names or self._jnames)]
 
     def base_frame(self) -> str:
         return self._sim.base_frame
 
     def nr_of_joints(self) -> int:
-        return len(self._sim.joint_names)
+        return len(self._jnames)
 
     def nr_of_links(self) -> int:
         return len(self.link_names())
@@ -439,7 +686,7 @@ class Model:
 
     def set_joint_acceleration_targets(self, accelerations: Sequence[float],
                                        joint_names: Sequence[str] = ()) -> bool:
-        names = list(joint_names) or list(self._sim.joint_names)
+        names = list(joint_names) or list(self._jnames)
         if len(accelerations) != len(names):
             _err("Wrong number of elements (joint_dofs=%d)" % len(names))
             return False
@@ -452,7 +699,7 @@ class Model:
         return True
 
     def joint_acceleration_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
-        return [self.get_joint(n).acceleration_target() for n in (joint_names or self._sim.joint_names)]
+        return [self.get_joint(n).acceleration_target() for n in (joint_names or self._jnames)]
 
     # -- base targets (Model.cpp:1077-1246): stored for controllers, the
     # physics does not read them; a getter of a target never set raises
@@ -594,13 +841,14 @@ class Model:
     # -- links and contacts (Link.cpp): the base link and the link of every joint
     def link_names(self, scoped: bool = False) -> List[str]:
         # Model::linkNames (Model.cpp:479-520); links lumped by fixed joints do not exist
-        names = [self._sim.base_frame] + list(self._sim.link_names)
+        # a ball joint's internal massless links (`<joint>#x`, `#y`) are not links
+        names = [self._sim.base_frame] + [n for n in self._sim.link_names if not self._internal_link(n)]
         return [f"{self._name}::{n}" for n in names] if scoped else names
 
     def get_link(self, link_name: str) -> "Link":
         if link_name == self._sim.base_frame:
             return Link(self, link_name, -1)
-        if link_name in self._sim.link_names:
+        if link_name in self._sim.link_names and not self._internal_link(link_name):
             return Link(self, link_name, self._sim.link_names.index(link_name))
         raise RuntimeError(f"Link '{link_name}' not found in model '{self._name}'")
 
@@ -728,9 +976,28 @@ class Model:
             _err(str(e))
             return False
 
+    def _internal_link(self, n: str) -> bool:
+        return bool(self._ball) and (n.endswith("#x") or n.endswith("#y")) and n[:-2] in self._ball
+
     # -- vectorised joint data (serialised in the requested name order)
     def _dofs(self, names: Sequence[str]):
-        return self._sim.dof_indices(list(names) if names else None)
+        if not self._ball:
+            return self._sim.dof_indices(list(names) if names else None)
+        out = []
+        for n in (names or self._jnames):
+            b = self._ball.get(n)
+            out.extend(b._names if b is not None else [n])
+        return self._sim.dof_indices(out)
+
+    def _ball_list(self, what: str, joint_names: Sequence[str]) -> List[float]:
+        # models with ball joints: DART's BallJoint coordinates for those
+        getter = {"q": "joint_position", "qd": "joint_velocity", "qdd": "joint_acceleration",
+                  "force": "joint_generalized_force", "force_target": "joint_generalized_force_target"}[what]
+        out: List[float] = []
+        for n in (joint_names or self._jnames):
+            b = self._ball.get(n)
+            out.extend(getattr(b, getter)() if b is not None else self._get(what, self._dofs([n])).tolist())
+        return out
 
     def _get(self, what: str, dof_idx) -> np.ndarray:
         if self._sim is None:
@@ -745,6 +1012,8 @@ class Model:
         # generation of the scene (every run and mutator starts a new one)
         if self._sim is None:
             raise RuntimeError(f"model '{self._name}' was removed")
+        if self._ball:
+            return self._ball_list(what, joint_names)
         gen = self._sim.scene.gen
         key = (what, tuple(joint_names) if joint_names else ())
         memo = self.__dict__.setdefault("_memo", {})
@@ -764,12 +1033,18 @@ class Model:
         return self._state_list("qd", joint_names)
 
     def joint_accelerations(self, joint_names: Sequence[str] = ()) -> List[float]:
+        if self._ball:
+            return self._ball_list("qdd", joint_names)
         return self._get("qdd", self._dofs(joint_names)).tolist()
 
     def joint_generalized_forces(self, joint_names: Sequence[str] = ()) -> List[float]:
+        if self._ball:
+            return self._ball_list("force", joint_names)
         return self._get("force", self._dofs(joint_names)).tolist()
 
     def joint_generalized_force_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
+        if self._ball:
+            return self._ball_list("force_target", joint_names)
         return self._get("force_target", self._dofs(joint_names)).tolist()
 
     def joint_velocity_targets(self, joint_names: Sequence[str] = ()) -> List[float]:
@@ -780,6 +1055,24 @@ class Model:
 
     def _set(self, what: str, values, joint_names: Sequence[str]) -> bool:
         try:
+            if self._ball:
+                # ball joints: 3 values each, in DART's BallJoint coordinates
+                names = list(joint_names) or list(self._jnames)
+                n = self.dofs(names)
+                if len(values) != n:
+                    _err(f"Wrong number of elements (joint_dofs={n})")
+                    return False
+                vals, k = [], 0
+                for nm in names:
+                    b = self._ball.get(nm)
+                    if b is not None:
+                        vals.extend(b._to_internal(what, values[k:k + 3]).tolist())
+                        k += 3
+                    else:
+                        vals.append(values[k])
+                        k += 1
+                values = vals
+                joint_names = names
             idx = self._dofs(joint_names)
             n = self._sim.dofs if idx is None else len(idx)
             if len(values) != n:
@@ -840,6 +1133,7 @@ class Model:
         if self._history is not None and not paused:
             self._history.extend(self._get("force_target", None).tolist())
         self._pending_vel = None
+        self._ball_pending.clear()
 
     def _close(self) -> None:
         if self._sim is not None:

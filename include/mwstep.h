@@ -57,6 +57,13 @@ extern "C" {
 #define MW_JOINT_REVOLUTE 2
 #define MW_JOINT_PRISMATIC 3
 #define MW_JOINT_BALL 4
+/* An SDF ball joint (3 dofs) is compiled as three revolute dofs named
+ * <joint>#x, <joint>#y, <joint>#z: rotations about the x, y, z axes of the
+ * joint frame at one point (intrinsic X-Y-Z angles), the first two on
+ * massless links <joint>#x, <joint>#y; mw_joint_type reports MW_JOINT_BALL
+ * for all three.  The ScenarI/O mirror (scenario/gazebo.py BallJoint)
+ * presents them in DART's BallJoint coordinates (rotation vector, child-frame
+ * angular velocity and torque). */
 
 /* per-joint parameters that the reference lets a just-created model change
  * (Joint::setCoulombFriction / setViscousFriction / setMaxGeneralizedForce,

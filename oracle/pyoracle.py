@@ -407,6 +407,24 @@ def sdf_to_urdf(text: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0
     for je in jts:
         pa, ch, jt = je.find("parent").text.strip(), je.find("child").text.strip(), je.get("type")
         O = np.linalg.inv(F[pa]) @ F[ch]
+        if jt == "ball":
+            # a spherical pair = three continuous joints about x, y, z of the
+            # joint frame at one point, two massless links between them
+            # (DART's BallJoint moves the child the same way; only the
+            # coordinates differ: rotation vector there, X-Y-Z angles here)
+            nm = je.get("name")
+            ax = je.find("axis")
+            dyn = (f'<dynamics damping="{float(_sdf_val(ax, "dynamics/damping", 0.0))!r}" '
+                   f'friction="{float(_sdf_val(ax, "dynamics/friction", 0.0))!r}"/>')
+            chain = [(pa, f"{nm}#x", O, "1 0 0"), (f"{nm}#x", f"{nm}#y", np.eye(4), "0 1 0"),
+                     (f"{nm}#y", ch, np.eye(4), "0 0 1")]
+            for k, (jp, jc, Oj, axs) in enumerate(chain):
+                if k < 2:
+                    out.append(f'<link name="{jc}"/>')
+                out.append(f'<joint name="{nm}#{"xyz"[k]}" type="continuous">{_origin(Oj)}'
+                           f'<parent link="{jp}"/><child link="{jc}"/><axis xyz="{axs}"/>'
+                           f'<limit effort="inf" velocity="inf"/>{dyn}</joint>')
+            continue
         body = [f'<joint name="{je.get("name")}" type="{{TYPE}}">', _origin(O),
                 f'<parent link="{pa}"/><child link="{ch}"/>']
         if jt != "fixed":

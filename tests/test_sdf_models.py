@@ -269,7 +269,7 @@ def test_sdf_and_urdf_of_one_model_compile_alike(N, oracle, pendulum_file):
     ("<sdf version='1.7'><model name='m'><link name='a'><pose relative_to='b'>0 0 0 0 0 0</pose></link></model></sdf>",
      "relative_to"),
     ("<sdf version='1.6'><model name='m'><link name='a'/><link name='b'/>"
-     "<joint name='j' type='ball'><parent>a</parent><child>b</child></joint></model></sdf>", "ball"),
+     "<joint name='j' type='universal'><parent>a</parent><child>b</child></joint></model></sdf>", "universal"),
     ("<sdf version='1.6'><model name='m'><link name='a'/>"
      "<joint name='j' type='revolute'><parent>a</parent><child>zz</child></joint></model></sdf>", "unknown link"),
 ])
@@ -327,3 +327,55 @@ def test_static_sdf_model_with_joints_fails_loudly(N):
                                     "<child>leg</child></joint></model>")
     rc, msg = _compile(N, text)
     assert rc != 0 and "static" in msg
+
+
+BALL_ARM_SDF = """<sdf version='1.7'><model name='arm'>
+  <link name='base'><pose>0 0 1 0 0 0</pose></link>
+  <joint name='fix' type='fixed'><parent>world</parent><child>base</child></joint>
+  <link name='upper'><pose>0.1 0 0.9 0.3 -0.2 0.5</pose>
+    <inertial><pose>0 0 -0.2 0 0 0</pose><mass>2</mass>
+      <inertia><ixx>0.03</ixx><iyy>0.04</iyy><izz>0.01</izz><ixy>0.001</ixy><ixz>0</ixz><iyz>0</iyz></inertia>
+    </inertial>
+    <collision name='c'><pose>0 0 -0.2 0 0 0</pose><geometry><sphere><radius>0.05</radius></sphere></geometry></collision>
+  </link>
+  <joint name='shoulder' type='ball'><pose>0 0 0.05 0 0 0</pose><parent>base</parent><child>upper</child>
+    <axis><dynamics><damping>0.2</damping></dynamics></axis></joint>
+  <link name='lower'><pose>0.1 0 0.5 0 0.4 0</pose>
+    <inertial><pose>0 0 -0.15 0 0 0</pose><mass>1</mass>
+      <inertia><ixx>0.01</ixx><iyy>0.01</iyy><izz>0.002</izz><ixy>0</ixy><ixz>0</ixz><iyz>0</iyz></inertia>
+    </inertial></link>
+  <joint name='elbow' type='revolute'><parent>upper</parent><child>lower</child>
+    <axis><xyz>0 1 0</xyz><limit><lower>-2</lower><upper>2</upper></limit></axis></joint>
+</model></sdf>"""
+
+
+def test_ball_joint_compiles_as_three_revolutes(N, oracle):
+    """SDF ball joints (Joint.cpp:318-331: 3 dofs): the product compiles a
+    spherical pair as three revolute dofs about x, y, z of the joint frame at
+    one point (massless links between), the oracle's independent reader as
+    the same three continuous URDF joints -- identical multibodies, and the
+    C-ABI reports MW_JOINT_BALL for the three dofs."""
+    rc, got = _compile(N, BALL_ARM_SDF)
+    assert rc == 0, got
+    assert got["names"] == ["shoulder#x", "shoulder#y", "shoulder#z", "elbow"]
+    assert got["links"] == ["shoulder#x", "shoulder#y", "upper", "lower"]
+    _compare(got, oracle.load_urdf(BALL_ARM_SDF))
+    out = got["out"].reshape(-1)[:34 * 4].reshape(4, 34)
+    assert out[0, 17] == out[1, 17] == 0.0 and out[2, 17] == 2.0  # masses: the child link on the z part
+    np.testing.assert_allclose(out[:3, 14:17], np.eye(3))          # axes x, y, z
+    np.testing.assert_allclose(out[1:3, 2:11], [np.eye(3).ravel()] * 2)  # no offset between the parts
+    assert list(out[:4, 33]) == [-1, 0, 1, 2]
+    cfg = N.MwConfig(1e-3, 1.0, 1, 1, 0, 0)
+    h = ctypes.c_void_p()
+    N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
+    try:
+        p = np.array(IDENT, dtype=np.float64)
+        N.check(N.lib().mw_load_model(h, BALL_ARM_SDF.encode(), N.dptr(p), b""))
+        t = ctypes.c_int32()
+        types = []
+        for d in range(4):
+            N.check(N.lib().mw_joint_type(h, d, ctypes.byref(t)))
+            types.append(t.value)
+        assert types == [4, 4, 4, 2]  # MW_JOINT_BALL x3, MW_JOINT_REVOLUTE
+    finally:
+        N.lib().mw_destroy(h)
