@@ -206,6 +206,7 @@ class Joint:
     def set_pid(self, pid: core.PID) -> bool:
         # Joint::setPID (Joint.cpp:479-525)
         try:
+            self._model._own_slot()
             self._model._sim.set_pid(self._dof, pid.to_list())
             return True
         except RuntimeError as e:
@@ -262,6 +263,7 @@ class Joint:
     def _set_param(self, which: int, value: float) -> bool:
         from mwstep import native as N
         try:
+            self._model._own_slot()
             self._model._sim.set_joint_param(self._dof, which, value)
             return True
         except RuntimeError as e:
@@ -953,6 +955,8 @@ class Model:
 
     def enable_contacts(self, enable: bool = True) -> bool:
         # Model::enableContacts (Model.cpp:686-700)
+        if bool(enable) != self._sim.contacts_enabled():
+            self._own_slot()
         self._sim.enable_contacts(enable)
         return True
 
@@ -970,11 +974,20 @@ class Model:
     def set_controller_period(self, period: float) -> bool:
         # Model::setControllerPeriod (Model.cpp:589-602)
         try:
+            self._own_slot()
             self._sim.set_controller_period(float(period))
             return True
         except RuntimeError as e:
             _err(str(e))
             return False
+
+    def _own_slot(self) -> None:
+        # joint parameters, PID gains, the controller period and contact
+        # detection are a scene slot's: before one world's model changes them,
+        # a slot shared with other worlds' models (same name, file and pose)
+        # is left for a slot of its own -- each world keeps its own
+        # components, as in the reference's per-world ECM
+        self._world._simulator._own_slot(self)
 
     def _internal_link(self, n: str) -> bool:
         return bool(self._ball) and (n.endswith("#x") or n.endswith("#y")) and n[:-2] in self._ball
@@ -1004,6 +1017,10 @@ class Model:
             raise RuntimeError(f"model '{self._name}' was removed")
         if dof_idx is not None:
             dof_idx = np.asarray(dof_idx, dtype=np.int32)
+        ov = self.__dict__.get("_state_override")
+        if ov and what in ov:
+            # moved to a slot of its own since the last run: the state it carried
+            return ov[what].copy() if dof_idx is None else ov[what][dof_idx]
         return self._sim.get(what, 0, 1, dof_idx)[0]
 
     def _state_list(self, what: str, joint_names: Sequence[str]) -> List[float]:
@@ -1134,6 +1151,7 @@ class Model:
             self._history.extend(self._get("force_target", None).tolist())
         self._pending_vel = None
         self._ball_pending.clear()
+        self.__dict__.pop("_state_override", None)
 
     def _close(self) -> None:
         if self._sim is not None:
@@ -1633,6 +1651,60 @@ class GazeboSimulator:
         if not world._physics:
             sc.set_present(slot, 0, w, 1)   # placed, not stepped until the Physics system is inserted
         return SceneView(sc, slot, w)
+
+    def _own_slot(self, model: "Model") -> None:
+        from mwstep.scene import SceneView
+        old = model._sim
+        sc, m, w = self._scene, old.m, old.w
+        shared = any(isinstance(o, Model) and o is not model and o._sim is not None and o._sim.m == m
+                     for wd in self._worlds.values() for o in wd._models.values())
+        if not shared:
+            return
+        name, text, pose = self._slots[m][:3]
+        present = sc.present(m, w)
+        # state and components of this world's model, read before the move
+        q, qd = old.get("q"), old.get("qd")
+        tgt = {k: old.get(k) for k in ("position_target", "velocity_target", "force_target")}
+        nd = sc.models[m]["dofs"]
+        modes = [old.control_mode(w, d) for d in range(nd)]
+        pids = [old.pid(d) for d in range(nd)]
+        from mwstep import native as N
+        params = [[old.joint_param(d, k) for k in (N.PARAM_COULOMB_FRICTION, N.PARAM_VISCOUS_FRICTION,
+                                                    N.PARAM_MAX_GENERALIZED_FORCE)] for d in range(nd)]
+        period, contacts = old.controller_period(), old.contacts_enabled()
+        floating = sc.models[m]["floating"]
+        pose_now, vel_now = (old.base_pose(), old.base_velocity()) if floating else (None, None)
+        slot = sc.insert_model(text, list(pose), f"{name}#{len(self._slots)}", worlds=(w, 1))
+        self._slots.append((name, text, tuple(pose), "own", w))  # never shared again
+        view = SceneView(sc, slot, w)
+        for d in range(nd):
+            view.set_pid(d, pids[d])
+            for k, v in zip((N.PARAM_COULOMB_FRICTION, N.PARAM_VISCOUS_FRICTION, N.PARAM_MAX_GENERALIZED_FORCE),
+                            params[d]):
+                view.set_joint_param(d, k, v)
+            view.set_control_mode(modes[d], dofs=[d])
+        view.set_controller_period(period)
+        view.enable_contacts(contacts)
+        view.set("reset_q", q)
+        view.set("reset_qd", qd)
+        for k, v in tgt.items():
+            for d in range(nd):
+                if k == "force_target" and v[0, d] == 0.0:
+                    continue
+                try:  # the targets the dof's control mode accepts
+                    view.set(k, v[:, d:d + 1], dofs=[d])
+                except RuntimeError:
+                    pass
+        if floating:
+            view.reset_base_pose(pose_now)
+            view.reset_base_velocity(vel_now)
+        sc.set_present(m, 0, w, 1)
+        if not present:  # insert_model placed it (placing again would reset it)
+            sc.set_present(slot, 0, w, 1)
+        model._sim = view
+        model._export = None
+        # until the next run applies the resets, the getters read the carried state
+        model._state_override = {"q": q[0].copy(), "qd": qd[0].copy(), "qdd": old.get("qdd")[0].copy()}
 
     def _remove_model(self, view) -> None:
         if self._scene is not None:

@@ -475,3 +475,50 @@ def test_model_api_completion(require_gpu):
         assert gazebo.run()
     assert cube.links_in_contact() == ["cube"]
     gazebo.close()
+
+
+def test_per_world_pid_and_joint_parameters(require_gpu):
+    """Joint::setPID / setViscousFriction / Model::setControllerPeriod act on
+    their own world (the reference keeps these components per world).  The
+    same model inserted into several worlds shares one scene slot until one
+    world changes a slot-wide parameter; that world's model then moves to a
+    slot of its own, carrying its state: the worlds whose gains did not
+    change keep tracking exactly as a never-touched world does."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    names = ["a", "b", "c"]
+    gazebo, get_model_file = _gazebo(names)
+    for n in names:
+        w = gazebo.get_world(n)
+        assert w.set_physics_engine(scenario.PhysicsEngine_dart)
+        assert w.insert_model(get_model_file("pendulum"))
+        m = w.get_model("pendulum")
+        assert m.set_joint_control_mode(core.JointControlMode_position)
+        assert m.set_joint_position_targets([0.5])
+    assert len(gazebo._slots) == 1
+    for _ in range(50):
+        assert gazebo.run()
+    q50 = [gazebo.get_world(n).get_model("pendulum").joint_positions()[0] for n in names]
+    assert q50[0] == q50[1] == q50[2]
+    # world "a": stiffer gains, mid-run
+    ja = gazebo.get_world("a").get_model("pendulum").get_joint(gazebo.get_world("a").get_model("pendulum").joint_names()[0])
+    pid_b = gazebo.get_world("b").get_model("pendulum").joints()[0].pid()
+    # (a new PID starts from a fresh state, as ign-math's does in the
+    # reference: its first derivative term kicks)
+    assert ja.set_pid(core.PID(50.0, 0.0, 0.0))
+    assert len(gazebo._slots) == 2                      # "a" left the shared slot
+    assert ja.pid().p == pytest.approx(50.0)
+    jb = gazebo.get_world("b").get_model("pendulum").joints()[0]
+    assert jb.pid().p == pytest.approx(pid_b.p)         # "b" kept its gains
+    assert ja.position() == pytest.approx(q50[0], abs=1e-12)  # the move kept the state
+    for _ in range(100):
+        assert gazebo.run()
+    qa, qb, qc = (gazebo.get_world(n).get_model("pendulum").joint_positions()[0] for n in names)
+    assert qb == qc                                     # untouched worlds stay identical
+    assert abs(qa - qb) > 1e-4 and abs(qa) < 10.0       # the retuned world moved differently
+    # the other slot-wide components follow the same rule
+    mb = gazebo.get_world("b").get_model("pendulum")
+    assert mb.set_controller_period(0.01) and len(gazebo._slots) == 3
+    assert gazebo.get_world("c").get_model("pendulum").controller_period() != pytest.approx(0.01)
+    assert gazebo.run()
+    gazebo.close()
