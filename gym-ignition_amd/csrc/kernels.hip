@@ -628,6 +628,11 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     uint32_t active = 0u;
     int ovf = 0, unconv = 0;
     unsigned long long prof[kWaveProfPhases] = {};
+    if (A.wrenches && lane <= N) {
+        // the world wrenches of this launch's substeps (lane = node: 0 the base)
+#pragma unroll
+        for (int e = 0; e < 6; ++e) L.ext[lane][e] = D.wrench[(static_cast<size_t>(e) * D.wnodes + lane) * W + w];
+    }
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
             MW_PROF_T(ta);
@@ -636,7 +641,7 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
             MW_PROF_T(tb);
             MW_PROF_ACC(0, ta, tb);
             active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0,
-                                           A.lcp_solves, L.qdd, &ovf, &unconv, prof);
+                                           A.lcp_solves, L.qdd, &ovf, &unconv, prof, A.wrenches != 0);
             MW_PROF_T(tc);
             MW_PROF_ACC(7, ta, tc);
         }

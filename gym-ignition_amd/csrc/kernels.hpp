@@ -41,7 +41,13 @@ struct FreeDev {
     float* cdata = nullptr;    // [kMaxFreeSlots][7][W] contact point xyz, force xyz, depth
     uint32_t* cmask = nullptr; // [W] active contact slots
     float* warm = nullptr;     // [kWaveWarmWords][W] previous step's PGS impulses (wave kernel, warm start)
+    // world wrenches of the launch's substeps (wave kernel, mw_apply_link_wrench):
+    // [6][node][W], world force at the link origin and world torque, node 0 the
+    // base, 1 + i body i (the host splits launches where a wrench expires)
+    float* wrench = nullptr;
+    int32_t wnodes = 0;
 };
+constexpr int kSimWrenchSlots = 4;  // concurrent wrenches (distinct expiries) per link
 
 // One launch of the scenario kernel covers up to 64 substeps of a run.
 struct RunArgs {
@@ -54,6 +60,7 @@ struct RunArgs {
     float pgs_tol;        // > 0: a PGS sweep that moved no impulse by more than pgs_tol max|x| ends the solve
     int warm;             // PGS starts from the previous step's impulses (wave kernel)
     int lcp_solves;       // > 0: the wave kernel solves its boxed LCP exactly within that many linear solves
+    int wrenches;         // FreeDev::wrench holds this launch's world wrenches
 };
 
 // Task description for the device-side env (see sim.cpp for the sources).

@@ -142,6 +142,14 @@ struct mw_sim {
     float* d_warm = nullptr;      // wave kernel: previous step's PGS impulses [kWaveWarmWordsHost][W]
     double pgs_tol = 0.0;         // mw_set_pgs_options
     bool pgs_warm = false;
+    // world wrenches (mw_apply_link_wrench, wave kernel): host records
+    // [slot][6][node][W] / [slot][node][W], device copies, the last iteration
+    // any record covers
+    std::vector<float> h_wr;
+    std::vector<int32_t> h_wl;
+    float* d_ext = nullptr;        // [6][node][W]: the summed wrenches of one launch
+    float* h_ext = nullptr;        // pinned staging of d_ext
+    int64_t wr_until = 0;
     int* h_overflow = nullptr;    // pinned copy read back with each synchronous run
     int64_t overflow_seen = 0;    // drops already reported
     int32_t lcp_mode = MW_LCP_EXACT;  // mw_set_lcp_solver (wave kernel)
@@ -550,6 +558,8 @@ void mw_destroy(mw_sim* s) {
         (void)hipHostFree(s->h_pid);
         (void)hipFree(s->d_overflow);
         (void)hipFree(s->d_warm);
+        (void)hipFree(s->d_ext);
+        (void)hipHostFree(s->h_ext);
         (void)hipHostFree(s->h_overflow);
         (void)hipHostFree(s->h_base);
         (void)hipHostFree(s->h_cdata);
@@ -982,6 +992,32 @@ static int run_free(mw_sim* s, int paused, bool readback = true) {
     return MW_OK;
 }
 
+// The world wrenches of the substeps (it0, it0 + chunk]: the launch ends
+// before the first expiry inside it (chunk shrinks), the records active
+// through it are summed per node into d_ext (Link.cpp:484-560 semantics, as
+// mw_scene_apply_world_wrench).
+static int stage_wrenches(mw_sim* s, int64_t it0, int& chunk) {
+    const int nn = s->n + 1;
+    const size_t W = static_cast<size_t>(s->W), st = static_cast<size_t>(nn) * W;
+    for (size_t k = 0; k < s->h_wl.size(); ++k) {
+        const int64_t last = s->h_wl[k];
+        if (last > it0 && last < it0 + chunk) chunk = static_cast<int>(last - it0);
+    }
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    MW_HIP(hipStreamIsCapturing(s->stream, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(MW_ESTATE, "world wrenches cannot be captured into a graph: run them outside the capture");
+    MW_HIP(hipStreamSynchronize(s->stream));  // the staging buffer of the previous launch
+    std::fill(s->h_ext, s->h_ext + 6 * st, 0.f);
+    for (int sl = 0; sl < mw::kSimWrenchSlots; ++sl)
+        for (size_t nw = 0; nw < st; ++nw) {
+            if (s->h_wl[sl * st + nw] < it0 + chunk) continue;
+            for (int e = 0; e < 6; ++e) s->h_ext[e * st + nw] += s->h_wr[(static_cast<size_t>(sl) * 6 + e) * st + nw];
+        }
+    MW_HIP(hipMemcpyAsync(s->d_ext, s->h_ext, 6 * st * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    return MW_OK;
+}
+
 static int run_impl(mw_sim* s, int paused, bool readback) {
     int rc = check_sim(s);
     if (rc) return rc;
@@ -1051,7 +1087,12 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
     const int spr = s->cfg.steps_per_run;
     int done = 0;
     do {
-        const int chunk = paused ? 0 : std::min(64, spr - done);
+        int chunk = paused ? 0 : std::min(64, spr - done);
+        a.wrenches = 0;
+        if (chunk > 0 && s->d_ext && s->wr_until > s->iterations + done) {
+            if (int rc2 = stage_wrenches(s, s->iterations + done, chunk)) return rc2;
+            a.wrenches = 1;
+        }
         a.substeps = chunk;
         a.pid_gate = 0;
         // JointController::PreUpdate period gating on the simulated time
@@ -1665,6 +1706,64 @@ int mw_set_pgs_options(mw_sim* s, double tol, int32_t warm_start) {
     }
     s->pgs_tol = tol;
     s->pgs_warm = warm;
+    return MW_OK;
+}
+
+// Link::applyWorldWrench (Link.cpp:484-560) on the batched simulator: a
+// world force at the link origin and a world torque (wrench[6 * nw]: f xyz,
+// tau xyz per world), applied from the next physics step for max(1,
+// ceil(duration / dt)) steps, as mw_scene_apply_world_wrench.  link -1 = the
+// base.  The wave kernel carries them (articulated floating bases and generic
+// fixed-base trees); other kernels fail with MW_ESTATE.
+int mw_apply_link_wrench(mw_sim* s, int32_t link, int32_t w0, int32_t nw, const double* wrench, double duration) {
+    if (!s || !s->loaded) return fail(MW_ESTATE, "no model loaded");
+    if (!s->initialized) return fail(MW_ESTATE, "the simulator is not initialized");
+    if (!wrench && nw > 0) return fail(MW_EINVAL, "null argument");
+    if (w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "world range out of bounds");
+    if (!s->wave)
+        return fail(MW_ESTATE, "world wrenches on mw_sim need the world-per-wavefront kernel (articulated floating "
+                               "bases, generic fixed-base trees); fixed-base chains and free bodies take them "
+                               "through a scene (mw_scene_apply_world_wrench)");
+    if (link < -1 || link >= s->n) return fail(MW_EINVAL, "link index out of range");
+    if (!(duration >= 0.0)) return fail(MW_EINVAL, "the wrench duration must be >= 0");
+    const int nn = s->n + 1;
+    const size_t W = static_cast<size_t>(s->W);
+    if (!s->d_ext) {
+        s->h_wr.assign(static_cast<size_t>(mw::kSimWrenchSlots) * 6 * nn * W, 0.f);
+        s->h_wl.assign(static_cast<size_t>(mw::kSimWrenchSlots) * nn * W, -1);
+        MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_ext), 6 * nn * W * sizeof(float)));
+        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ext), 6 * nn * W * sizeof(float), hipHostMallocDefault));
+        s->fdev.wrench = s->d_ext;
+        s->fdev.wnodes = nn;
+    }
+    const int node = link + 1;
+    const int64_t d_ns = static_cast<int64_t>(duration * 1e9);
+    const int64_t k = std::max<int64_t>(1, (d_ns + s->dt_ns - 1) / s->dt_ns);
+    const int64_t last = s->iterations + k;
+    if (last > std::numeric_limits<int32_t>::max()) return fail(MW_EINVAL, "wrench expiry beyond the counter range");
+    auto wl = [&](int sl, int w) -> int32_t& { return s->h_wl[(static_cast<size_t>(sl) * nn + node) * W + w]; };
+    auto wr = [&](int sl, int e, int w) -> float& {
+        return s->h_wr[((static_cast<size_t>(sl) * 6 + e) * nn + node) * W + w];
+    };
+    // validate first: a failing call changes nothing
+    for (int w = w0; w < w0 + nw; ++w) {
+        bool ok = false;
+        for (int sl = 0; sl < mw::kSimWrenchSlots && !ok; ++sl) ok = wl(sl, w) == last || wl(sl, w) <= s->iterations;
+        if (!ok) return fail(MW_ESTATE, "too many concurrent wrenches with different durations on one link");
+    }
+    for (int w = w0; w < w0 + nw; ++w) {
+        int slot = -1;
+        for (int sl = 0; sl < mw::kSimWrenchSlots && slot < 0; ++sl)
+            if (wl(sl, w) == last) slot = sl;
+        for (int sl = 0; sl < mw::kSimWrenchSlots && slot < 0; ++sl)
+            if (wl(sl, w) <= s->iterations) {
+                slot = sl;
+                for (int e = 0; e < 6; ++e) wr(sl, e, w) = 0.f;
+            }
+        wl(slot, w) = static_cast<int32_t>(last);
+        for (int e = 0; e < 6; ++e) wr(slot, e, w) += static_cast<float>(wrench[(w - w0) * 6 + e]);
+    }
+    s->wr_until = std::max(s->wr_until, last);
     return MW_OK;
 }
 

@@ -81,6 +81,7 @@ struct WaveWorld {
     WaveAcc acc[MAXN + 1];       // [MAXN] = the base
     float q[MAXN], qd[MAXN], qdd[MAXN], tau[MAXN], vc[MAXN];
     uint32_t act[MAXN];
+    float ext[MAXN + 1][6];      // this substep's world wrenches: [0] the base, [1 + i] body i (f, tau)
     float nu[kNv];
     static constexpr int kJStride = (kNv + 3) & ~3;  // float4 rows: read as uniform broadcasts
     alignas(16) float J[kWaveMaxRows][kJStride];
@@ -150,7 +151,7 @@ namespace dev {
 template <int MAXN>
 __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                        const M3& R0, const f3& p0, const SV& V0, WaveWorld<MAXN>& L, Chol6& L0,
-                                       float dt, float* qdd_out) {
+                                       float dt, float* qdd_out, bool ext) {
     const int lane = lane_id();
     const bool own = lane < N;
     const int i = own ? lane : 0;
@@ -195,6 +196,20 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     if (own) {
         tau = L.tau[i];
         qdi = L.qd[i];
+    }
+    if (ext) {
+        // this substep's world wrenches (L.ext, mw_apply_link_wrench) enter as
+        // the starting bias of each body's accumulator, in its own frame (the
+        // inward pass adds the children's contributions on top)
+        if (own) {
+            const M3 Rwi = L.body[i].Rw;
+            const float* e = L.ext[1 + i];
+            L.acc[i].B = L.acc[i].B + (-1.f) * SV{mulT(Rwi, mk(e[3], e[4], e[5])), mulT(Rwi, mk(e[0], e[1], e[2]))};
+        }
+        if (lane == 0) {
+            const float* e = L.ext[0];
+            L.acc[MAXN].B = L.acc[MAXN].B + (-1.f) * SV{mulT(R0, mk(e[3], e[4], e[5])), mulT(R0, mk(e[0], e[1], e[2]))};
+        }
     }
     // DART's implicit joint damping (Psi = (S^T AI S + dt d)^-1, force
     // tau - d qd) for the free motion; with damping the impulses use the
@@ -249,6 +264,7 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         const SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
                                  Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
                       L.acc[MAXN].B;
+
         L0.factor(IA0);
         a0 = L0.solve(-1.f * B0);
         if (dual) {
@@ -406,13 +422,13 @@ template <int MAXN, bool CONS>
 __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                               FreeState& base, WaveWorld<MAXN>& L, float dt, int pgs_iters,
                                               float pgs_tol, bool warm, int lcp_solves, float* qdd_out, int* overflow,
-                                              int* unconverged, unsigned long long* prof) {
+                                              int* unconverged, unsigned long long* prof, bool ext) {
     const int lane = lane_id();
     const int NV = 6 + N;
     MW_PROF_T(t0);
     const M3 R0 = quat_to_R(base.qw, base.qx, base.qy, base.qz);
     Chol6 L0;  // on return: the factorisation the impulses use
-    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, dt, qdd_out);
+    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, dt, qdd_out, ext);
     MW_PROF_T(t1);
     MW_PROF_ACC(1, t0, t1);
     // integrateVelocities (lane e: nu component e)

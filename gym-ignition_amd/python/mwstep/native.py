@@ -103,6 +103,7 @@ SIGNATURES = [
     ("mw_set_pgs_options", ctypes.c_int, [_P, ctypes.c_double, _I]),
     ("mw_pgs_options", ctypes.c_int, [_P, _D, _IP]),
     ("mw_set_lcp_solver", ctypes.c_int, [_P, _I, _I]),
+    ("mw_apply_link_wrench", ctypes.c_int, [_P, _I, _I, _I, _D, ctypes.c_double]),
     ("mw_lcp_solver", ctypes.c_int, [_P, _IP, _IP]),
     ("mw_lcp_unconverged", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     ("mw_model_export_shapes", ctypes.c_int, [_P, _I, _D, _I, _IP]),

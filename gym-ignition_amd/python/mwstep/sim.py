@@ -285,6 +285,15 @@ class Simulator:
         N.check(N.lib().mw_pgs_options(self.handle, ctypes.byref(t), ctypes.byref(w)))
         return t.value, bool(w.value)
 
+    def apply_world_wrench(self, link: int, wrench, duration: float, w0: int = 0, nw: Optional[int] = None) -> None:
+        """mw_apply_link_wrench (Link::applyWorldWrench, Link.cpp:484-560): world
+        force at the link origin + world torque ([nw, 6] or one row for all),
+        from the next step for max(1, ceil(duration / dt)) steps; link -1 = base."""
+        nw = self.n_worlds - w0 if nw is None else nw
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(wrench, dtype=np.float64), (nw, 6)))
+        N.check(N.lib().mw_apply_link_wrench(self.handle, int(link), int(w0), int(nw), N.dptr(v), float(duration)),
+                "apply_world_wrench")
+
     def set_lcp_solver(self, exact: bool = True, max_solves: int = 24) -> None:
         """mw_set_lcp_solver: exact boxed LCP after the PGS sweeps (default) or the sweeps alone."""
         N.check(N.lib().mw_set_lcp_solver(self.handle, N.LCP_EXACT if exact else N.LCP_PGS, int(max_solves)),

@@ -246,6 +246,17 @@ int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
 #define MW_LCP_PGS 0
 #define MW_LCP_EXACT 1
 int mw_set_lcp_solver(mw_sim* sim, int32_t mode, int32_t max_solves);
+
+/* Link::applyWorldWrench / applyWorldForce / applyWorldTorque
+ * (cpp/scenario/gazebo/src/Link.cpp:484-560) on the worlds [w0, w0 + nw):
+ * wrench[6 * nw] = world force at the link origin (xyz) and world torque
+ * (xyz) per world, applied from the next physics step for
+ * max(1, ceil(duration / dt)) steps; wrenches on one link add up (at most 4
+ * distinct expiries at once).  link -1 = the base.  Carried by the
+ * world-per-wavefront kernel (articulated floating bases, generic fixed-base
+ * trees); other models fail with MW_ESTATE (use a scene).  Not seen by graphs
+ * captured before the call. */
+int mw_apply_link_wrench(mw_sim* sim, int32_t link, int32_t w0, int32_t nw, const double* wrench, double duration);
 int mw_lcp_solver(const mw_sim* sim, int32_t* mode, int32_t* max_solves);
 /* World-steps whose exact LCP solve ran out of budget since mw_initialize
  * (they keep the best feasible impulses found; 0 = every solve converged). */
