@@ -163,12 +163,16 @@ __device__ __forceinline__ float lcp_row_residual(const LcpRow& R, float xl, flo
 constexpr int kLcpUStride = 66;
 constexpr int kLcpRhs = 64;
 
+// pivot = false: the system is symmetric positive definite (the staggered
+// rounds' principal submatrices A_FF, identity rows elsewhere), eliminated in
+// lane order without the pivot search -- the argmax's DPP chain is most of an
+// elimination step's dependent latency
 template <int RC>
-__device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U) {
+__device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U, bool pivot) {
     const int lane = lane_id();
     bool used = lane >= n;
     for (int j = 0; j < n; ++j) {
-        const int p = wave_argmax(used ? -1.f : fabsf(k[0]));
+        const int p = pivot ? wave_argmax(used ? -1.f : fabsf(k[0])) : j;
         float piv = read_lane(k[0], p);
         piv = (fabsf(piv) < 1e-30f) ? 1e-30f : piv;
         const float f = (used || lane == p) ? 0.f : k[0] * rcp(piv);
@@ -281,6 +285,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
         // ---- one linear solve: the Newton system of this round ----
         float k[RC];
         bool fr;
+        bool pivot = false;  // only a folded friction column makes the system unsymmetric
         float coup = 0.f;  // phase 0: d_t = coup d_n of a friction row held at +-mu x_n
         const float emax = wave_fmax(e_abs);
         if (phase == 0) {
@@ -312,7 +317,8 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #pragma unroll
             for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
             // x_t = +-mu x_n: the held friction column folds into its normal's
-            if ((cpM | cnM) != 0ull) {
+            pivot = (cpM | cnM) != 0ull;
+            if (pivot) {
 #pragma unroll
                 for (int c = 0; c + 2 < RC; c += 3) {
                     const float s1 = (mask_bit(cpM, c + 1) ? 1.f : 0.f) - (mask_bit(cnM, c + 1) ? 1.f : 0.f);
@@ -326,7 +332,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #pragma unroll
             for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
         }
-        float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw);
+        float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, pivot);
         ++solves;
         if (phase == 0) {
             const float dn = gather_normal<RC>(d, R, n);

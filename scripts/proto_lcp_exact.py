@@ -13,6 +13,9 @@ import os
 import sys
 
 import numpy as np
+BPP = int(__import__('os').environ.get('BPP', '0'))
+SKIP = int(__import__('os').environ.get('SKIP', '0'))
+STATS = [0, 0, 0]  # solves in phase 0, phase 1; phase-1 rounds (instrumentation)
 LOOSE = float(__import__('os').environ.get('LOOSE', '10'))
 BEST = int(__import__('os').environ.get('BEST', '0'))
 
@@ -519,6 +522,7 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
 
     solves, phase, at_min, new_round = 0, 0, False, True
     ssn_n, best_e, best_x = 0, np.inf, x.copy()
+    bpp_best, bpp_strikes = 1 << 30, 0
     ws = np.zeros(n, int)
     Lf = Uf = prev = None
     conv = False
@@ -543,12 +547,44 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
         if solves >= max_solves:
             break
         if phase == 1 and new_round:
+            STATS[2] += 1
+            bpp_best, bpp_strikes = 1 << 30, 0
             new_round = False
             Lf, Uf, prev = L.copy(), U.copy(), x.copy()
             ws = np.where(x <= Lf, 1, np.where(x >= Uf, 2, 0))
             x = np.where(x <= Lf, Lf, np.where(x >= Uf, Uf, x)).astype(f32)
             ws = np.where(Lf == Uf, 1, ws)
             at_min = False
+            continue
+        if phase == 1 and BPP and not new_round and at_min:
+            # block principal pivoting on the round's box QP (x: the subspace
+            # minimiser of the current partition)
+            at_min = False
+            gm = np.abs(g).max()
+            tg = RT * (1 + gm)
+            live = Lf != Uf
+            inf_lo = (ws == 0) & (x < Lf) & live
+            inf_hi = (ws == 0) & (x > Uf) & live
+            inf_bl = (ws == 1) & (g < -tg) & live
+            inf_bu = (ws == 2) & (g > tg) & live
+            inf = inf_lo | inf_hi | inf_bl | inf_bu
+            ninf = int(inf.sum())
+            if ninf == 0:
+                if np.abs(x - prev).max() <= tolx:
+                    break
+                new_round = True
+                continue
+            if ninf < bpp_best:
+                bpp_best, bpp_strikes = ninf, 0
+                flip = inf
+            elif bpp_strikes < 3:
+                bpp_strikes += 1
+                flip = inf
+            else:
+                flip = np.zeros(n, bool)
+                flip[int(np.nonzero(inf)[0].max())] = True
+            ws = np.where(flip & inf_lo, 1, np.where(flip & inf_hi, 2, np.where(flip & (inf_bl | inf_bu), 0, ws)))
+            x = np.where(ws == 1, Lf, np.where(ws == 2, Uf, x)).astype(f32)
             continue
         if phase == 1 and at_min:
             at_min = False
@@ -600,11 +636,16 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
                 K[fr, c] += mu * (s1 * A[fr, c + 1] + s2 * A[fr, c + 2])
         else:
             fr = ws == 0
+            if SKIP and np.abs(np.where(fr & (Lf != Uf), g, 0)).max() <= RT * (1 + np.abs(g).max()):
+                # the free rows are already stationary: the working set's minimiser
+                at_min = True
+                continue
             K = np.where(np.outer(fr, fr), A, 0).astype(f32)
             K[~fr] = 0
             K[~fr, ~fr] = 1
         d = ge_solve(K, np.where(fr, -g, 0).astype(f32))
         solves += 1
+        STATS[phase] += 1
         x_prev = x.copy()
         if phase == 0:
             d = np.where(fr, d, coup * d[nrow]).astype(f32)
@@ -640,6 +681,10 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
             if not acc:
                 phase, new_round = 1, True
             continue
+        if BPP:
+            x = np.where(fr, x + d, x).astype(f32)
+            at_min = True
+            continue
         if np.abs(d).max() <= 1e-7 * (1 + xmax):
             at_min = True
             continue
@@ -661,6 +706,8 @@ def wave_exact(p, pgs_sweeps=20, max_solves=16, x0=None):
             at_min = True
     if not conv and BEST:
         x = best_x
+    if not conv and BPP and phase == 1 and Lf is not None:
+        x = np.minimum(np.maximum(x, Lf), Uf).astype(f32)
     return x, solves, conv
 
 
