@@ -70,7 +70,7 @@ struct ScWorld {
     union {
         WaveAcc acc[kScMaxNodes];
         float stack[kScMaxDepth][7][kWaveLanes];
-        float A[kScMaxRows][kAStride];
+        alignas(16) float A[kScMaxRows][kAStride];  // also the exact LCP's pivot rows (16-byte reads)
     };
     float l0[kScMaxModels][28];   // Chol6 (l[21], id[6]) of every floating base
     float q[kScMaxBodies], qd[kScMaxBodies], qdd[kScMaxBodies], tau[kScMaxBodies], vc[kScMaxBodies];

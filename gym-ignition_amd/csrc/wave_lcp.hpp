@@ -79,6 +79,18 @@ __device__ __forceinline__ int wave_argmax(float v) {
     return __builtin_ctzll(static_cast<unsigned long long>(__ballot(v == m)));
 }
 
+// Orders one wave's LDS stores before its later loads as seen by the other
+// lanes (a wavefront-scope release / acquire around the wave barrier): the
+// compiler otherwise reasons per lane and may move a load of data another lane
+// stores above that store.
+__device__ __forceinline__ void wave_lds_sync() {
+#ifndef MW_HOST_TEST
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
 __device__ __forceinline__ bool mask_bit(uint64_t m, int i) { return ((m >> i) & 1ull) != 0ull; }
 
 // Row data of lane r (r < n): rhs b, kind, bounds of box rows, the contact's
@@ -156,11 +168,14 @@ __device__ __forceinline__ float lcp_row_residual(const LcpRow& R, float xl, flo
 // rhs = rhs[lane], rows / columns >= n are ignored.  Returns d[lane].
 // Column j is eliminated at step j; the registers shift by one column per
 // step (k[0] is always the current column), so no register is indexed at run
-// time.  The pivot row of step j is kept in LDS (U, kLcpUStride floats per
-// row: the row's columns j.. at 0.., its rhs at kLcpRhs) for the
-// back substitution, where lane l gathers U[l][j - l] (stride - 1 odd: the 64
-// lanes hit 64 banks).
-constexpr int kLcpUStride = 66;
+// time.  The pivot row of step j goes to LDS (U, kLcpUStride floats per row:
+// the row's columns j.. at 0.., its rhs at kLcpRhs) and comes back to every
+// lane as uniform-address ds_read_b128 (a broadcast: one read per 4 columns,
+// where a v_readlane per column stalled the FMA on its SGPR); the rows stay
+// there for the back substitution, where lane l gathers U[l][j - l]
+// (stride - 1 odd: the 64 lanes hit 64 banks).  U: 16-byte aligned,
+// kLcpUStride * 64 floats.
+constexpr int kLcpUStride = 68;
 constexpr int kLcpRhs = 64;
 
 // pivot = false: the system is symmetric positive definite (the staggered
@@ -169,33 +184,49 @@ constexpr int kLcpRhs = 64;
 // elimination step's dependent latency
 template <int RC>
 __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U, bool pivot) {
+    static_assert(RC % 8 == 0, "row blocks of 8");
     const int lane = lane_id();
     bool used = lane >= n;
     for (int j = 0; j < n; ++j) {
         const int p = pivot ? wave_argmax(used ? -1.f : fabsf(k[0])) : j;
-        float piv = read_lane(k[0], p);
-        piv = (fabsf(piv) < 1e-30f) ? 1e-30f : piv;
-        const float f = (used || lane == p) ? 0.f : k[0] * rcp(piv);
-        const float prhs = read_lane(rhs, p);
         const int left = n - j;  // live columns
+        float* row = U + j * kLcpUStride;
         if (lane == p) {
-            float2* u = reinterpret_cast<float2*>(U + j * kLcpUStride);
+            float4* u = reinterpret_cast<float4*>(row);
 #pragma unroll
-            for (int c = 0; c < RC; c += 2) {
+            for (int c = 0; c < RC; c += 4) {
                 if ((c & 7) == 0 && c >= left) break;
-                u[c / 2] = make_float2(k[c], (c + 1 < RC) ? k[c + 1] : 0.f);
+                u[c / 4] = make_float4(k[c], k[c + 1], k[c + 2], k[c + 3]);
             }
-            U[j * kLcpUStride + kLcpRhs] = rhs;
+            row[kLcpRhs] = rhs;
         }
+        // lane p's row is read by the other lanes: without the fence the
+        // compiler forwards lane p's own values and hoists the other lanes'
+        // loads into the store's else-branch, which runs first
+        wave_lds_sync();
+        // the pivot row back to every lane, 4 columns per read, as the update
+        // walks the columns (one wave: its LDS accesses are in order; the
+        // columns >= left are dead)
+        const float4* ur = reinterpret_cast<const float4*>(row);
+        float4 cur = ur[0];
+        const float prhs = row[kLcpRhs];
+        const float piv = (fabsf(cur.x) < 1e-30f) ? 1e-30f : cur.x;
+        const float f = (used || lane == p) ? 0.f : k[0] * rcp(piv);
 #pragma unroll
-        for (int c = 0; c + 1 < RC; ++c) {
+        for (int c = 0; c < RC; c += 4) {
             if ((c & 7) == 0 && c >= left) break;
-            k[c] = fmaf(-f, read_lane(k[c + 1], p), k[c + 1]);
+            const float4 nxt = (c + 4 < RC) ? ur[c / 4 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            k[c] = fmaf(-f, cur.y, k[c + 1]);
+            k[c + 1] = fmaf(-f, cur.z, k[c + 2]);
+            k[c + 2] = fmaf(-f, cur.w, k[c + 3]);
+            if (c + 4 < RC) k[c + 3] = fmaf(-f, nxt.x, k[c + 4]);
+            cur = nxt;
         }
         rhs = fmaf(-f, prhs, rhs);
         used = used || lane == p;
     }
     // back substitution, right-looking: lane l holds row l (pivot of step l)
+    wave_lds_sync();
     float acc = 0.f, rdiag = 1.f;
     if (lane < n) {
         acc = U[lane * kLcpUStride + kLcpRhs];

@@ -1,6 +1,9 @@
 """Run selected bench.py legs alone (one GPU) and print their JSON:
     python scripts/leg_probe.py humanoid humanoid_pgs scene contacts quadruped panda
-Legs skip their CPU baselines."""
+Legs skip their CPU baselines.  humanoid/N, humanoid_pgs/N and panda/N run
+every rank's share of an N-GPU strong split of configs 5 / 4 one after another
+on this GPU (no collective: the worlds are independent) and print each share's
+time and the max over the shares: the projected N-GPU step time."""
 import json
 import os
 import sys
@@ -30,8 +33,45 @@ def _with_budget(budget):
     _sim.Simulator.__init__ = init
 
 
+class _NoDist:
+    """stands in for torch.distributed in a rank's share run alone: the legs'
+    barriers and max-over-ranks are no-ops"""
+    class ReduceOp:
+        MAX = None
+
+    @staticmethod
+    def barrier():
+        pass
+
+    @staticmethod
+    def all_reduce(t, op=None):
+        pass
+
+
+def _shares(fn, n):
+    rows = []
+    for r in range(n):
+        o = fn(r)
+        rows.append({"rank": r, "worlds": o.get("worlds_per_gpu"), "ms_per_step": o["ms_per_step"],
+                     "kernel_us_per_launch": o.get("kernel_us_per_launch")})
+    worst = max(x["ms_per_step"] for x in rows)
+    return {"shares": rows, "projected_ms_per_step": worst}
+
+
 for spec in sys.argv[1:] or ["humanoid", "humanoid_pgs", "scene"]:
-    leg, _, budget = spec.partition("@")
+    spec_leg, _, nshare = spec.partition("/")
+    leg, _, budget = spec_leg.partition("@")
+    if nshare:
+        n = int(nshare)
+        _with_budget(int(budget) if budget else 0)
+        if leg in ("humanoid", "humanoid_pgs"):
+            out = _shares(lambda r: bench.humanoid_leg(args, dev, torch, _NoDist, n, r, exact=(leg == "humanoid")), n)
+        elif leg == "panda":
+            out = _shares(lambda r: bench.panda_leg(args, dev, torch, _NoDist, n, r), n)
+        else:
+            raise SystemExit(f"no share run for {leg}")
+        print(spec, json.dumps(out), flush=True)
+        continue
     _with_budget(int(budget) if budget else 0)
     if leg == "humanoid":
         out = bench.humanoid_leg(args, dev, torch)
