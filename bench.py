@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--no-contact-leg", action="store_true", help="skip the floating-body contact leg")
     p.add_argument("--no-runtime-leg", action="store_true", help="skip the config-1 GazeboRuntime leg")
     p.add_argument("--no-scene-leg", action="store_true", help="skip the multi-model scene leg")
+    p.add_argument("--no-share-proj", action="store_true",
+                   help="skip the projected 8-GPU strong split of configs 4 / 5 (their rank shares timed alone)")
     p.add_argument("--groups", type=int, default=1,
                    help="world groups per GPU, each on its own stream / hardware queue")
     return p.parse_args()
@@ -191,6 +193,16 @@ def main():
         humanoid = humanoid_leg(args, dev, torch, dist, world_size, rank)
         # the same workload on the PGS sweeps alone (the round-2 default): the exact solve's cost
         humanoid_pgs = humanoid_leg(args, dev, torch, dist, world_size, rank, exact=False)
+    # the 8-GPU strong split of configs 4 / 5, projected on this one GPU: every
+    # rank's share run alone, one after another (the worlds are independent,
+    # no data-path collective); the slowest share is the split's step time
+    if world_size == 1 and not args.no_share_proj:
+        if panda is not None:
+            panda["projected_split"] = share_projection(
+                lambda r: panda_leg(args, dev, torch, _NoDist, SHARE_N, r), panda["ms_per_step"], 1024)
+        if humanoid is not None:
+            humanoid["projected_split"] = share_projection(
+                lambda r: humanoid_leg(args, dev, torch, _NoDist, SHARE_N, r), humanoid["ms_per_step"], 512)
     runtime = None
     if rank == 0 and world_size == 1 and not args.no_runtime_leg:
         runtime = runtime_leg(args, dev)
@@ -270,6 +282,41 @@ def main():
         e.close()
     if world_size > 1:
         dist.destroy_process_group()
+
+
+SHARE_N = 8
+
+
+class _NoDist:
+    """torch.distributed stand-in for one rank's share run alone on one GPU:
+    the legs' barriers and max-over-ranks become no-ops"""
+    class ReduceOp:
+        MAX = None
+
+    @staticmethod
+    def barrier():
+        pass
+
+    @staticmethod
+    def all_reduce(t, op=None):
+        pass
+
+
+def share_projection(run_share, ms_1gpu, W_global, n=SHARE_N):
+    """Time every rank's share of an n-GPU strong split on this GPU, one after
+    another; the split's step time is the slowest share's (each GPU steps its
+    own worlds, no collective in the step).  Reports the projected whole-job
+    rate and its speedup over the measured one-GPU step."""
+    shares = []
+    for r in range(n):
+        o = run_share(r)
+        shares.append(o["ms_per_step"])
+    worst = max(shares)
+    return {"n_gpus": n, "worlds_per_gpu": W_global // n, "share_ms_per_step": [round(x, 6) for x in shares],
+            "ms_per_step": round(worst, 6), "value": round(W_global / (worst * 1e-3), 1),
+            "speedup_vs_1gpu": round(ms_1gpu / worst, 3),
+            "method": f"each of the {n} rank shares timed alone on this GPU (same leg code, no collective in the "
+                      "step); the split's step time is the slowest share's; projection, not an 8-GPU measurement"}
 
 
 def panda_targets(q0, T, dt, torch):

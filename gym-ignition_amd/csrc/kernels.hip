@@ -648,7 +648,12 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     }
 #ifdef MW_WAVE_PROF
     if (lane == 0)
-        for (int k = 0; k < kWaveProfPhases; ++k) atomicAdd(&g_wave_prof[k], prof[k]);
+        for (int k = 0; k < kWaveProfPhases; ++k) {
+            if (k == 11 || k == 12)
+                atomicMax(&g_wave_prof[k], prof[k]);
+            else
+                atomicAdd(&g_wave_prof[k], prof[k]);
+        }
 #else
     (void)prof;
 #endif

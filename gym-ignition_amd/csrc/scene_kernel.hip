@@ -1130,12 +1130,14 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 Rw.b = Rw.live ? c.x : 0.f;
                 Rw.lo = Rw.live ? c.z : 0.f;
                 Rw.hi = Rw.live ? c.w : 0.f;
-                static_assert(sizeof(L.A) >= kWaveMaxRows * kLcpUStride * sizeof(float), "LCP workspace");
+                static_assert(sizeof(L.A) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
                 float* Uw = &L.A[0][0];
-                int nsolve = 0, nround = 0;
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve, nround)
+                int nsolve = 0, nround = 0, nsolve1 = 0;
+                long long ge_cyc = 0;
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve, nround,
+                                                                nsolve1, ge_cyc)
                                            : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve,
-                                                                          nround);
+                                                                          nround, nsolve1, ge_cyc);
                 if (!ok && lane == 0) unconv += 1;
                 x0 = Rw.live ? x0 : 0.f;
             }

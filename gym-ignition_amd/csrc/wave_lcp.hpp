@@ -177,6 +177,7 @@ __device__ __forceinline__ float lcp_row_residual(const LcpRow& R, float xl, flo
 // kLcpUStride * 64 floats.
 constexpr int kLcpUStride = 68;
 constexpr int kLcpRhs = 64;
+constexpr int kLcpWorkFloats = 64 * kLcpUStride;  // the workspace the caller provides
 
 // pivot = false: the system is symmetric positive definite (the staggered
 // rounds' principal submatrices A_FF, identity rows elsewhere), eliminated in
@@ -249,12 +250,12 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 template <int RC>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, float* __restrict__ Uw, float& xl, int& n_solves,
-                                               int& n_rounds) {
+                                               int& n_rounds, int& n_solves_staggered, long long& ge_cycles) {
     const int lane = lane_id();
     float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
 #pragma unroll
     for (int c = 0; c < RC; ++c) arr = (lane == c && R.live) ? a[c] : arr;
-    int solves = 0;
+    int solves = 0, solves1 = 0;
     bool converged = false;
     int phase = 0;          // 0 semismooth Newton, 1 staggered active set (oracle lcp_refine)
     int ws = 0;             // phase 1 working set: 0 free, 1 held at L, 2 held at U
@@ -363,8 +364,15 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #pragma unroll
             for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
         }
+#ifdef MW_WAVE_PROF
+        const long long tg0 = clock64();
+#endif
         float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, pivot);
+#ifdef MW_WAVE_PROF
+        ge_cycles += clock64() - tg0;
+#endif
         ++solves;
+        solves1 += phase;
         if (phase == 0) {
             const float dn = gather_normal<RC>(d, R, n);
             d = fr ? d : coup * dn;
@@ -423,6 +431,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
     }
     n_solves = solves;
     n_rounds = iter;
+    n_solves_staggered = solves1;
     return converged;
 }
 

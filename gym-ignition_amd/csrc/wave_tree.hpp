@@ -104,7 +104,9 @@ __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x &
 
 // Phase timing (debug builds only: EXTRA=-DMW_WAVE_PROF, scripts/wave_prof.py):
 // shader-clock cycles per phase, summed over the worlds of a launch.
-constexpr int kWaveProfPhases = 10;  // [8] exact-LCP linear solves, [9] its rounds
+constexpr int kWaveProfPhases = 16;  // [8] exact-LCP linear solves, [9] its rounds, [10] staggered-round solves,
+                                     // [11] / [12] max solves / staggered solves of a world-step, [13] world-steps > 4 solves,
+                                     // [14] cycles in the linear solves, [15] in the PGS sweeps
 #ifdef MW_WAVE_PROF
 __device__ unsigned long long g_wave_prof[kWaveProfPhases];
 #define MW_PROF_T(var) const long long var = clock64()
@@ -703,6 +705,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             wave_pgs<MAXN, true>(L, a, x, Rpad, ncr, mu, pgs_iters, pgs_tol);
         else
             wave_pgs<MAXN, false>(L, a, x, Rpad, ncr, mu, pgs_iters, 0.f);
+        MW_PROF_T(t45);
+        MW_PROF_ACC(15, t4, t45);
         if (lcp_solves > 0) {
             // exact boxed LCP from the PGS impulses (wave_lcp.hpp; oracle
             // OR_PGS_CONVERGED): lane r = row r
@@ -718,14 +722,25 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #pragma unroll
             for (int r = 0; r < kWaveMaxRows; ++r) xe = (lane == r && r < R) ? x[r] : xe;
             // the elimination's pivot rows go to the responses' stack (dead here)
-            static_assert(sizeof(L.stack) >= kWaveMaxRows * kLcpUStride * sizeof(float), "LCP workspace");
+            static_assert(sizeof(L.stack) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
             float* U = &L.stack[0][0][0];
-            int nsolve = 0, nround = 0;
-            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround)
-                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround);
+            int nsolve = 0, nround = 0, nsolve1 = 0;
+            long long ge_cyc = 0;
+            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround, nsolve1,
+                                                           ge_cyc)
+                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround,
+                                                                     nsolve1, ge_cyc);
 #ifdef MW_WAVE_PROF
             prof[8] += static_cast<unsigned long long>(nsolve);
             prof[9] += static_cast<unsigned long long>(nround);
+            prof[10] += static_cast<unsigned long long>(nsolve1);
+            prof[11] = prof[11] > static_cast<unsigned long long>(nsolve) ? prof[11] : nsolve;
+            prof[12] = prof[12] > static_cast<unsigned long long>(nsolve1) ? prof[12] : nsolve1;
+            prof[13] += nsolve > 4 ? 1ull : 0ull;
+            prof[14] += static_cast<unsigned long long>(ge_cyc);
+#else
+            (void)nsolve1;
+            (void)ge_cyc;
 #endif
 #pragma unroll
             for (int r = 0; r < kWaveMaxRows; ++r) {

@@ -33,19 +33,7 @@ def _with_budget(budget):
     _sim.Simulator.__init__ = init
 
 
-class _NoDist:
-    """stands in for torch.distributed in a rank's share run alone: the legs'
-    barriers and max-over-ranks are no-ops"""
-    class ReduceOp:
-        MAX = None
-
-    @staticmethod
-    def barrier():
-        pass
-
-    @staticmethod
-    def all_reduce(t, op=None):
-        pass
+_NoDist = bench._NoDist
 
 
 def _shares(fn, n):

@@ -20,7 +20,7 @@ from mwstep.sim import Simulator  # noqa: E402
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 PGS = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 print(f"exact={os.environ.get('MW_PROF_EXACT', '1')} warm={os.environ.get('MW_PROF_WARM', '0')}")
-T = 20
+T = int(os.environ.get("MW_PROF_T", "20"))
 PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
           "Delassus (lane = column)", "PGS + exact LCP", "rows total (responses .. integrate)", "whole substep"]
 
@@ -34,6 +34,10 @@ for d, n in enumerate(names):
     sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
 sim.set_control_mode(N.MODE_POSITION)
 sim.set("position_target", np.zeros((W, sim.dofs)))
+if os.environ.get("MW_PROF_RANDOM", "0") != "0":
+    # the bench leg's start: joint angles U(-0.02, 0.02) (bench.humanoid_leg)
+    sim.set("reset_q", np.random.default_rng(42).uniform(-0.02, 0.02, (W, sim.dofs)))
+    sim.run(paused=True)
 # solver options: MW_PROF_EXACT=0 -> PGS only; MW_PROF_WARM=1 -> warm-started sweeps
 sim.set_lcp_solver(os.environ.get("MW_PROF_EXACT", "1") != "0")
 if os.environ.get("MW_PROF_WARM", "0") != "0":
@@ -42,7 +46,7 @@ sim.run_device(50)
 L = N.lib()
 fn = L.mw_debug_wave_prof
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 10)()
+buf = (ctypes.c_ulonglong * 16)()
 fn(buf)  # clear
 t0 = time.perf_counter()
 sim.run_device(T)
@@ -52,5 +56,8 @@ fn(buf)
 print(f"{W} worlds, PGS {PGS}, {T} steps: {dt / T * 1e6:.1f} us/step wall; contacts in world 0: {len(sim.contacts(0))}")
 for k, name in enumerate(PHASES):
     print(f"  {name:40s} {buf[k] / W / T:12.0f} cycles/world-step")
-print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f} rounds per world-step")
+print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f} rounds per world-step; "
+      f"{buf[10] / W / T:.2f} of the solves in staggered rounds; max per world-step {buf[11]} solves, "
+      f"{buf[12]} staggered; {buf[13]} of {W * T} world-steps > 4 solves; "
+      f"{buf[14] / W / T:.0f} cycles/world-step in the linear solves, {buf[15] / W / T:.0f} in the PGS sweeps")
 sim.close()

@@ -49,3 +49,8 @@ def test_driver_bench_command(require_gpu):
     h = out["humanoid_c5"]
     assert h["constraint_overflow"] == 0 and h["lcp_unconverged_world_steps"] is not None
     assert "exact boxed LCP" in h["workload"] and "PGS" in out["humanoid_c5_pgs_only"]["workload"]
+    # configs 4 / 5: the 8-GPU strong split projected from the 8 rank shares timed alone
+    for leg, wg in (("panda_c4", 1024), ("humanoid_c5", 512)):
+        ps = out[leg]["projected_split"]
+        assert ps["n_gpus"] == 8 and ps["worlds_per_gpu"] == wg // 8 and len(ps["share_ms_per_step"]) == 8, leg
+        assert ps["ms_per_step"] == max(ps["share_ms_per_step"]) and ps["speedup_vs_1gpu"] > 0, leg
