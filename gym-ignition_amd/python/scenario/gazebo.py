@@ -1621,7 +1621,8 @@ class GazeboSimulator:
     # ---- scene slots (internal)
     def _place_model(self, world: World, text: str, pose: List[float], name: str):
         """World::insertModel into `world`: reuse the slot holding the same
-        model (name, file, pose) if it is not in that world yet, else a free
+        model (name, file, pose; any pose for a floating model) if it is not
+        in that world yet, else a free
         slot of the same tree (an env randomizer's per-episode model), else a
         new slot; returns the SceneView of the model in that world."""
         from mwstep.scene import SceneView
@@ -1632,8 +1633,20 @@ class GazeboSimulator:
             if k == key and not sc.present(m, w):
                 slot = m
                 break
+        moved = False
+        if slot is None:
+            # a floating model's insert pose is only its initial base state:
+            # the slot of the same model (name, file) at another pose serves
+            # this world too, its base reset to this pose (N worlds inserting
+            # one robot at randomised poses take one slot, not N)
+            for m, k in enumerate(self._slots):
+                if len(k) == 3 and k[:2] == key[:2] and sc.models[m]["floating"] and not sc.present(m, w):
+                    slot, moved = m, True
+                    break
         if slot is not None:
             sc.set_present(slot, 1, w, 1)
+            if moved:
+                sc.reset_base_pose(slot, np.asarray(pose, dtype=np.float64).reshape(1, 7), w, 1)
         else:
             for m, k in enumerate(self._slots):
                 if not any(sc.present(m, ww) for ww in range(sc.n_worlds)):

@@ -193,6 +193,35 @@ def _ground_plane_sdf(mu):
             '</link></model></sdf>')
 
 
+def test_floating_model_at_random_poses_shares_one_slot(require_gpu):
+    """N worlds inserting one floating model at N different poses (an env's
+    randomised spawn) take one scene slot, not N (the slot capacity is 8):
+    each world's base starts at its own insert pose and falls freely from it."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    names = [f"w{k}" for k in range(12)]
+    gazebo, get_model_file = _gazebo(names)
+    rng = np.random.default_rng(3)
+    xyz = np.c_[rng.uniform(-2, 2, (12, 2)), rng.uniform(1.0, 3.0, 12)]
+    for n, p in zip(names, xyz):
+        w = gazebo.get_world(n)
+        assert w.set_physics_engine(scenario.PhysicsEngine_dart)
+        assert w.insert_model(get_model_file("cube"), core.Pose(list(p), [1., 0, 0, 0]), "c")
+    assert len(gazebo._slots) == 1
+    assert gazebo.run(paused=True)  # inserted models appear at the next (paused) run, as in the reference
+    for n, p in zip(names, xyz):
+        assert gazebo.get_world(n).get_model("c").base_position() == pytest.approx(list(p), abs=1e-6), n
+    T = 100
+    for _ in range(T):
+        assert gazebo.run()
+    dt = 1e-3
+    for n, p in zip(names, xyz):
+        pos = gazebo.get_world(n).get_model("c").base_position()
+        assert pos[:2] == pytest.approx(list(p[:2]), abs=1e-6), n
+        assert pos[2] == pytest.approx(p[2] - 9.8 * dt * dt * T * (T + 1) / 2, abs=1e-4), n
+    gazebo.close()
+
+
 def test_per_world_gravity_and_ground_friction(require_gpu):
     """World::setGravity and the ground plane's friction act on their own world
     only (World.cpp:301-319: each world of a server keeps its own Gravity
