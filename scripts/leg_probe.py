@@ -48,6 +48,7 @@ def _shares(fn, n):
 
 for spec in sys.argv[1:] or ["humanoid", "humanoid_pgs", "scene"]:
     spec_leg, _, nshare = spec.partition("/")
+    spec_leg, _, sweeps = spec_leg.partition("%")  # humanoid%20: at most 20 PGS sweeps before the exact solve
     leg, _, budget = spec_leg.partition("@")
     if nshare:
         n = int(nshare)
@@ -62,7 +63,7 @@ for spec in sys.argv[1:] or ["humanoid", "humanoid_pgs", "scene"]:
         continue
     _with_budget(int(budget) if budget else 0)
     if leg == "humanoid":
-        out = bench.humanoid_leg(args, dev, torch)
+        out = bench.humanoid_leg(args, dev, torch, pgs=int(sweeps) if sweeps else 50)
     elif leg == "humanoid_pgs":
         out = bench.humanoid_leg(args, dev, torch, exact=False)
     elif leg == "scene":
