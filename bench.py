@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--no-contact-leg", action="store_true", help="skip the floating-body contact leg")
     p.add_argument("--no-runtime-leg", action="store_true", help="skip the config-1 GazeboRuntime leg")
     p.add_argument("--no-scene-leg", action="store_true", help="skip the multi-model scene leg")
+    p.add_argument("--no-free-legs", action="store_true",
+                   help="skip the floating-cube and quadruped legs (configs 4 / 5 still run)")
+    p.add_argument("--no-pgs-leg", action="store_true", help="skip the config-5 PGS-only leg")
     p.add_argument("--no-share-proj", action="store_true",
                    help="skip the projected 8-GPU strong split of configs 4 / 5 (their rank shares timed alone)")
     p.add_argument("--groups", type=int, default=1,
@@ -98,7 +101,9 @@ def main():
     envs = make_groups(args.task, W, args.groups, dev, args.seed, rank * W)
     env = envs[0]
     K = args.steps
-    actions = make_actions(envs, args.warmup + K, dev, torch, rank)
+    # actions of the GLOBAL worlds, this rank's block sliced out: every world
+    # sees the same action sequence at any rank count
+    actions = make_actions(envs, args.warmup + K, dev, torch, 0, offset=rank * W, n_global=world_size * W)
     timed = time_steps(envs, actions, args.warmup, K, args.graph_chunk, dev, torch, dist, world_size,
                        gather=(world_size > 1))
     elapsed, kernel_us = timed["elapsed"], timed["kernel_us"]
@@ -186,13 +191,14 @@ def main():
         panda = panda_leg(args, dev, torch, dist, world_size, rank)
     contacts = quadruped = humanoid = humanoid_pgs = None
     if not args.no_contact_leg:
-        if rank == 0 and world_size == 1:
+        if rank == 0 and world_size == 1 and not args.no_free_legs:
             contacts = contact_leg(args, dev, torch)
             quadruped = quadruped_leg(args, dev, torch)
         # BASELINE config 5: 512 global humanoid worlds split over the ranks
         humanoid = humanoid_leg(args, dev, torch, dist, world_size, rank)
         # the same workload on the PGS sweeps alone (the round-2 default): the exact solve's cost
-        humanoid_pgs = humanoid_leg(args, dev, torch, dist, world_size, rank, exact=False)
+        if not args.no_pgs_leg:
+            humanoid_pgs = humanoid_leg(args, dev, torch, dist, world_size, rank, exact=False)
     # the 8-GPU strong split of configs 4 / 5, projected on this one GPU: every
     # rank's share run alone, one after another (the worlds are independent,
     # no data-path collective); the slowest share is the split's step time
@@ -263,6 +269,7 @@ def main():
                           "~1M worlds (world_sweep)",
             },
             "gathered_obs_shape": timed["gathered_obs_shape"],
+            "final_obs_sha256": timed["final_obs_sha256"],
             "world_sweep": sweep,
             "cpu_baseline": cpu,
             "obs_max_abs_err_vs_oracle": parity,
@@ -332,16 +339,36 @@ def panda_targets(q0, T, dt, torch):
     return tg.contiguous()
 
 
-def make_actions(envs, total, dev, torch, rank):
-    gen = torch.Generator(device=dev).manual_seed(43 + rank)
+def make_actions(envs, total, dev, torch, tag, offset=0, n_global=None):
+    """[total, W] actions of the envs' worlds: columns offset .. offset + W of
+    one [total, n_global] draw (seed 43 + tag), so a world's actions do not
+    depend on how the worlds are split over ranks."""
+    gen = torch.Generator(device=dev).manual_seed(43 + tag)
     env = envs[0]
     W = sum(e.n_worlds for e in envs)
+    n_global = W if n_global is None else n_global
     if env.action_dim:
         q0 = torch.cat([e.reset()[:, :e.action_dim].clone() for e in envs])
         return panda_targets(q0, total, 1e-3, torch)
     if env.discrete:
-        return torch.randint(0, 2, (total, W), generator=gen, device=dev, dtype=torch.int32)
-    return (torch.rand((total, W), generator=gen, device=dev) * 2 - 1) * 50.0
+        a = torch.randint(0, 2, (total, n_global), generator=gen, device=dev, dtype=torch.int32)
+    else:
+        a = (torch.rand((total, n_global), generator=gen, device=dev) * 2 - 1) * 50.0
+    return a[:, offset:offset + W].contiguous() if (offset or n_global != W) else a
+
+
+def state_digest(t, dist, world_size, n_global):
+    """sha256 of a final per-world state [W_local, k] gathered over the ranks
+    into global world order (mwstep.shard.gather_obs; the slab itself at one
+    rank): equal digests at different rank counts = the sharded run and its
+    gather reproduce the one-GPU result bit for bit (tests/test_gpu_multirank.py)."""
+    import hashlib
+    if world_size > 1:
+        if dist is _NoDist:
+            return None
+        from mwstep.shard import gather_obs
+        t = gather_obs(t.contiguous(), n_global=n_global)
+    return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()
 
 
 def make_groups(task, W, S, dev, seed, offset, **kw):
@@ -447,9 +474,13 @@ def time_steps(envs, actions, warmup, K, chunk, dev, torch, dist, world_size, ga
     kernel_us = hip_elapsed_ms(ev_start, ev_end) * 1e3 / K
     for ev in [ev_start, ev_end] + ev_join:
         hip_runtime().hipEventDestroy(ev)
+    final = gathered if gather else (torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs)
+    import hashlib
     return {"elapsed": elapsed, "kernel_us": kernel_us, "G": G,
             "stream": groups[0][1], "groups": S,
-            "gathered_obs_shape": list(gathered.shape) if gather else None}
+            "gathered_obs_shape": list(gathered.shape) if gather else None,
+            "final_obs_sha256": hashlib.sha256(final.detach().cpu().contiguous().numpy().tobytes()).hexdigest(),
+            "final_obs": torch.cat([g[0].obs for g in groups]) if S > 1 else groups[0][0].obs}
 
 
 _HIP = None
@@ -556,6 +587,7 @@ def panda_leg(args, dev, torch, dist, world_size=1, rank=0, W_global=1024):
            "bytes_per_env_step": bpe, "achieved_GBs": round(gbs, 3),
            "hbm_frac": round(gbs / HBM_PEAK_GBS, 6), "groups": args.groups,
            "kernel": "vecenv_pid_group_kernel<9,false,true> (one world per 16-lane row)"}
+    out["final_state_sha256"] = state_digest(r["final_obs"], dist, world_size, W_global)
     tr = pmc_traffic("PandaPositionTracking", W)
     out["traffic"] = tr["bytes_per_launch"] if tr else None
     out["algorithmic_bytes_per_launch"] = bpe * W
@@ -607,7 +639,7 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
     xy = rng.uniform(-5, 5, (W_global, 2))
     out = float_tree_leg(args, dev, torch, "humanoid32", e - b, pgs, 0.535, gains,
                          q0[b:e], np.zeros((e - b, n)), xy[b:e], K=200, G=20, warm=40,
-                         dist=dist, world_size=world_size, pgs_opts=pgs_opts, exact=exact)
+                         dist=dist, world_size=world_size, pgs_opts=pgs_opts, exact=exact, W_global=W_global)
     out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
     out["scaling"] = "strong"
     out["worlds_per_gpu"] = e - b
@@ -632,7 +664,7 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
 
 
 def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, K=500, G=50, warm=100,
-                   dist=None, world_size=1, pgs_opts=(0.0, False), exact=True):
+                   dist=None, world_size=1, pgs_opts=(0.0, False), exact=True, W_global=None):
     """Time W floating-base worlds of `model` under a PID hold, one physics
     step per run, replayed from hipGraphs of mw_run_device; with several ranks
     the timed region is bracketed by barriers and the max over ranks is kept."""
@@ -699,6 +731,10 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, 
            "base_z_range_after": [round(float(z.min()), 4), round(float(z.max()), 4)],
            "constraint_overflow": int(sim.constraint_overflow()),
            "lcp_unconverged_world_steps": int(sim.lcp_unconverged()) if sim.float_kernel() == 2 else None}
+    if W_global is not None:
+        st = torch.from_numpy(np.concatenate([sim.get("q"), sim.get("qd"), sim.base_pose(), sim.base_velocity()],
+                                             axis=1)).to(dev)
+        out["final_state_sha256"] = state_digest(st, dist, world_size, W_global)
     sim.close()
     return out
 

@@ -26,6 +26,27 @@
 namespace mw {
 namespace dev {
 
+// ------------------------------------------------- divergence detection ----
+// A world whose stored state holds a non-finite value (finite.hpp: an
+// exponent-bit test the finite-math build keeps) is flagged once (sticky until
+// mw_clear_diverged) and counted; mw_run reports the new ones (MW_EDIVERGED).
+
+__device__ __forceinline__ void mark_diverged(uint8_t* flags, unsigned long long* count, int w) {
+    if (flags && !flags[w]) {
+        flags[w] = 1;
+        atomicAdd(count, 1ull);
+    }
+}
+
+__device__ __forceinline__ bool base_nonfinite(const FreeState& b) {
+    const float v[13] = {b.p.x, b.p.y, b.p.z, b.qw, b.qx, b.qy, b.qz, b.V.w.x, b.V.w.y, b.V.w.z,
+                         b.V.v.x, b.V.v.y, b.V.v.z};
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) bad = bad || nonfinite_bits(v[k]);
+    return bad;
+}
+
 // ------------------------------------------------------ baked models ----
 // The shipped models' parameter blocks as device constants: a kernel
 // instantiated with BAKED != 0 reads the model from here, and the compiler
@@ -332,6 +353,10 @@ __global__ void __launch_bounds__(256) scenario_run_kernel(const ChainF* __restr
 #pragma unroll
     for (int d = 0; d < N; ++d) S.cmd[d * W + w] = 0.f;  // JointForceCmd zero-fill (paused too)
     store_state<N>(S, W, w, q, qd);
+    bool bad = false;
+#pragma unroll
+    for (int d = 0; d < N; ++d) bad = bad || nonfinite_bits(q[d]) || nonfinite_bits(qd[d]);
+    if (bad) mark_diverged(S.div, S.ndiv, w);
 }
 
 template <int N, int KIND>
@@ -494,6 +519,7 @@ __global__ void __launch_bounds__(256) free_run_kernel(const FreeF* __restrict__
         for (int s = 0; s < A.substeps; ++s) free_step<MESH>(F, A.dt, A.pgs_iters, S, C);
     }
     store_base(D, W, w, S);
+    if (base_nonfinite(S)) mark_diverged(D.div, D.ndiv, w);
     if (want_contacts && !A.paused) {
         D.cmask[w] = C.active;
         const float inv_dt = 1.f / A.dt;
@@ -549,6 +575,10 @@ __global__ void __launch_bounds__(64) float_run_kernel(const ChainF* __restrict_
     for (int d = 0; d < N; ++d) S.cmd[d * W + w] = 0.f;
     store_state<N>(S, W, w, X.q, X.qd);
     store_base(D, W, w, X.base);
+    bool bad = base_nonfinite(X.base);
+#pragma unroll
+    for (int d = 0; d < N; ++d) bad = bad || nonfinite_bits(X.q[d]) || nonfinite_bits(X.qd[d]);
+    if (bad) mark_diverged(D.div, D.ndiv, w);
     if (want_contacts && !A.paused) {
         D.cmask[w] = active;
         const float inv_dt = 1.f / A.dt;
@@ -657,17 +687,23 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
 #else
     (void)prof;
 #endif
+    bool bad = false;
     if (lane < N) {
         const size_t k = static_cast<size_t>(lane) * W + w;
         S.q[k] = L.q[lane];
         S.qd[k] = L.qd[lane];
         if (!A.paused) S.qdd[k] = L.qdd[lane];
         S.cmd[k] = 0.f;
+        bad = nonfinite_bits(L.q[lane]) || nonfinite_bits(L.qd[lane]);
     }
+    if (lane == 0) bad = bad || base_nonfinite(base);
+    bad = __ballot(bad) != 0;
     if (lane == 0) {
+        if (bad) mark_diverged(D.div, D.ndiv, w);
         store_base(D, W, w, base);
         if (ovf) atomicAdd(overflow, ovf);
-        if (unconv) atomicAdd(overflow + 1, unconv);  // exact LCP solves that ran out of budget
+        // exact LCP solves that ran out of budget: a 64-bit counter at words 2-3
+        if (unconv) atomicAdd(reinterpret_cast<unsigned long long*>(overflow + 2), static_cast<unsigned long long>(unconv));
     }
     if (A.warm)  // also after a paused run: it may have consumed a reset
         for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) D.warm[static_cast<size_t>(e) * W + w] = L.xw[e];

@@ -30,6 +30,11 @@ struct SimDev {
     // derivative term (gain d / dt on the position error) does not amplify
     // the float32 rounding of q += dt qd (kernels with a JointController)
     float* qlo = nullptr;
+    // divergence detection (mw_diverged): [W] sticky per-world flag set by the
+    // run kernels when a world's stored joint or base state is not finite,
+    // and the count of worlds flagged since initialisation
+    uint8_t* div = nullptr;
+    unsigned long long* ndiv = nullptr;
 };
 
 // Device arrays of a floating single-body model (free_body.hpp).
@@ -46,6 +51,8 @@ struct FreeDev {
     // base, 1 + i body i (the host splits launches where a wrench expires)
     float* wrench = nullptr;
     int32_t wnodes = 0;
+    uint8_t* div = nullptr;               // as SimDev::div / ndiv
+    unsigned long long* ndiv = nullptr;
 };
 constexpr int kSimWrenchSlots = 4;  // concurrent wrenches (distinct expiries) per link
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "chain_params.hpp"
+#include "finite.hpp"
 
 namespace mw {
 namespace dev {
@@ -12,9 +13,8 @@ namespace dev {
 // or_pid_update]; returns false (and leaves the state) for a non-finite error
 __device__ __forceinline__ bool pid_update(const PidF& g, float err, float inv_dt, float dt, float& e_last,
                                            float& ierr, float& cmd) {
-    // exponent-bits test: the kernels are built finite-math-only, where
-    // isfinite() folds to true
-    if ((__float_as_uint(err) & 0x7f800000u) == 0x7f800000u) return false;
+    // the kernels are built finite-math-only: finite.hpp's exponent-bit test
+    if (nonfinite_bits(err)) return false;
     const float pterm = g.p * err;
     ierr = ierr + g.i * dt * err;
     if (g.imax >= g.imin) ierr = fminf(fmaxf(ierr, g.imin), g.imax);

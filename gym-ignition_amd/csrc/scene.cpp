@@ -103,6 +103,8 @@ struct mw_scene {
     float* h_contact = nullptr;
     int32_t* h_ncontact = nullptr;
     int32_t* h_overflow = nullptr;  // pinned copy of the device drop counter
+    uint64_t* h_ndiv = nullptr;     // pinned copy of the count of worlds flagged diverged
+    int64_t div_seen = 0;           // flagged worlds already reported
     float* h_wphys = nullptr;       // pinned mirror of d_wphys (uploaded with the presence words)
     int64_t overflow_seen = 0;      // drops already reported
     int32_t lcp_mode = MW_LCP_EXACT;  // mw_scene_set_lcp_solver
@@ -586,7 +588,7 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_base), s->base_bytes(), hipHostMallocDefault));
     std::memset(s->h_base, 0, s->base_bytes());
     const size_t nwl = static_cast<size_t>(SLOTS) * NNMAX * W;
-    const size_t misc = W * sizeof(uint32_t) + W * sizeof(int32_t) + 64 + nwl * sizeof(int32_t);
+    const size_t misc = W * sizeof(uint32_t) + W * sizeof(int32_t) + 64 + nwl * sizeof(int32_t) + W;
     SC_HIP(hipMalloc(&s->d_misc, misc));
     SC_HIP(hipMemsetAsync(s->d_misc, 0, misc, s->stream));
     SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_wrench), 6 * nwl * sizeof(float)));
@@ -616,6 +618,10 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
         SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), sizeof(int32_t), hipHostMallocDefault));
         *s->h_overflow = 0;
     }
+    if (!s->h_ndiv) {
+        SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ndiv), sizeof(uint64_t), hipHostMallocDefault));
+        *s->h_ndiv = 0;
+    }
     SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), NBMAX * sizeof(mw::PidF), hipHostMallocDefault));
     // device views
     float* j = static_cast<float*>(s->d_joint);
@@ -636,6 +642,7 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     D.ncontact = reinterpret_cast<int32_t*>(mp + W * sizeof(uint32_t));
     D.overflow = reinterpret_cast<int32_t*>(mp + W * sizeof(uint32_t) + W * sizeof(int32_t));
     D.wlast = reinterpret_cast<int32_t*>(mp + W * sizeof(uint32_t) + W * sizeof(int32_t) + 64);
+    D.diverged = mp + W * sizeof(uint32_t) + W * sizeof(int32_t) + 64 + nwl * sizeof(int32_t);
     D.wrench = s->d_wrench;
     D.contact = s->d_contact;
     D.wphys = s->d_wphys;
@@ -671,6 +678,7 @@ void mw_scene_destroy(mw_scene* s) {
     (void)hipHostFree(s->h_contact);
     (void)hipHostFree(s->h_ncontact);
     (void)hipHostFree(s->h_overflow);
+    (void)hipHostFree(s->h_ndiv);
     (void)hipHostFree(s->h_pid);
     if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -975,12 +983,32 @@ int mw_scene_run(mw_scene* s, int32_t paused) {
     } else if (int rc = queue_readback(s, needs_base_readback(s))) {
         return rc;
     }
-    // the drop counter rides on the same synchronisation
+    // the drop counter rides on the same synchronisation, and so does the
+    // divergence count of the larger scenes (a direct run's state is in the
+    // pinned mirror already: it is checked there, below)
     if (can_overflow(s))
         SC_HIP(hipMemcpyAsync(s->h_overflow, s->dev.overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    if (!direct)
+        SC_HIP(hipMemcpyAsync(s->h_ndiv, s->dev.overflow + 4, sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
     if (int rc = sync(s)) return rc;
     clear_consumed(s);
     s->joints_stale = s->base_stale = false;
+    if (direct) {
+        // the kernel flags a world whose stored state is not finite; a direct
+        // run reads the count only when its mirror holds such a value
+        bool bad = false;
+        const uint32_t* jb = reinterpret_cast<const uint32_t*>(s->h_joint);
+        for (size_t k = 0; k < 2 * s->jrows && !bad; ++k) bad = (jb[k] & 0x7f800000u) == 0x7f800000u;
+        if (!bad && needs_base_readback(s)) {
+            const uint32_t* bb = reinterpret_cast<const uint32_t*>(s->h_base);
+            const size_t nb = static_cast<size_t>(13 * s->models.size()) * s->W;
+            for (size_t k = 0; k < nb && !bad; ++k) bad = (bb[k] & 0x7f800000u) == 0x7f800000u;
+        }
+        if (bad) {
+            SC_HIP(hipMemcpyAsync(s->h_ndiv, s->dev.overflow + 4, sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
+            if (int rc = sync(s)) return rc;
+        }
+    }
     const int64_t dropped = *s->h_overflow;
     if (dropped > s->overflow_seen) {
         const int64_t d = dropped - s->overflow_seen;
@@ -992,6 +1020,31 @@ int mw_scene_run(mw_scene* s, int32_t paused) {
                       static_cast<long long>(d), CMAX, mw::kScMaxRows);
         return fail(MW_ECAPACITY, msg);
     }
+    const int64_t nd = static_cast<int64_t>(*s->h_ndiv);
+    if (nd > s->div_seen) {
+        const int64_t d = nd - s->div_seen;
+        s->div_seen = nd;
+        return fail(MW_EDIVERGED, std::to_string(d) + " world(s) diverged in this run: their joint or base state "
+                                                      "is not finite (mw_scene_diverged lists them)");
+    }
+    return MW_OK;
+}
+
+int mw_scene_diverged(mw_scene* s, int32_t w0, int32_t nw, uint8_t* flags, int64_t* count) {
+    if (int rc = check(s)) return rc;
+    if (int rc = check_worlds(s, w0, nw)) return rc;
+    if (flags && nw) SC_HIP(hipMemcpyAsync(flags, s->dev.diverged + w0, nw, hipMemcpyDeviceToHost, s->stream));
+    uint64_t n = 0;
+    SC_HIP(hipMemcpyAsync(&n, s->dev.overflow + 4, sizeof(n), hipMemcpyDeviceToHost, s->stream));
+    SC_HIP(hipStreamSynchronize(s->stream));
+    if (count) *count = static_cast<int64_t>(n);
+    return MW_OK;
+}
+
+int mw_scene_clear_diverged(mw_scene* s, int32_t w0, int32_t nw) {
+    if (int rc = check(s)) return rc;
+    if (int rc = check_worlds(s, w0, nw)) return rc;
+    if (nw) SC_HIP(hipMemsetAsync(s->dev.diverged + w0, 0, nw, s->stream));
     return MW_OK;
 }
 
@@ -1426,10 +1479,10 @@ int mw_scene_lcp_solver(const mw_scene* s, int32_t* mode, int32_t* max_solves) {
 int mw_scene_lcp_unconverged(const mw_scene* s, int64_t* world_steps) {
     if (int rc = check(s)) return rc;
     if (!world_steps) return fail(MW_EINVAL, "null argument");
-    int v[2] = {0, 0};
-    SC_HIP(hipMemcpyAsync(v, s->dev.overflow, 2 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    uint64_t v = 0;
+    SC_HIP(hipMemcpyAsync(&v, s->dev.overflow + 2, sizeof(v), hipMemcpyDeviceToHost, s->stream));
     SC_HIP(hipStreamSynchronize(s->stream));
-    *world_steps = v[1];
+    *world_steps = static_cast<int64_t>(v);
     return MW_OK;
 }
 

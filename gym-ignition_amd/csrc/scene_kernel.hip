@@ -606,7 +606,7 @@ __device__ __forceinline__ float sc_dof_force(const SceneF* __restrict__ P, cons
 // first non-finite value of the node records, coordinates and contacts of a
 // world is printed (bit test of the exponent: -ffinite-math-only folds isfinite)
 #ifdef MW_SC_NANCHECK
-__device__ __forceinline__ bool sc_bad(float v) { return (__float_as_uint(v) & 0x7f800000u) == 0x7f800000u; }
+__device__ __forceinline__ bool sc_bad(float v) { return nonfinite_bits(v); }
 template <int MAXNV>
 __device__ void sc_nancheck(const SceneF* __restrict__ P, const ScWorld<MAXNV>& L, int phase, int nc, bool& reported) {
     const int lane = lane_id();
@@ -1328,10 +1328,12 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
                            mu, nc, ovf, unconv);
         }
     }
+    bool bad = false;
     if (lane < NB) {
         const size_t k = static_cast<size_t>(lane) * W + w;
         D.q[k] = L.q[lane];
         D.qd[k] = L.qd[lane];
+        bad = nonfinite_bits(L.q[lane]) || nonfinite_bits(L.qd[lane]);  // finite.hpp
         if (!A.paused) D.qdd[k] = L.qdd[lane];
         D.cmd[k] = 0.f;
         if (D.rb) {
@@ -1346,12 +1348,20 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         at(3) = base.qw; at(4) = base.qx; at(5) = base.qy; at(6) = base.qz;
         at(7) = base.V.w.x; at(8) = base.V.w.y; at(9) = base.V.w.z;
         at(10) = base.V.v.x; at(11) = base.V.v.y; at(12) = base.V.v.z;
+        const float v[13] = {base.p.x, base.p.y, base.p.z, base.qw, base.qx, base.qy, base.qz,
+                             base.V.w.x, base.V.w.y, base.V.w.z, base.V.v.x, base.V.v.y, base.V.v.z};
+#pragma unroll
+        for (int f = 0; f < 13; ++f) bad = bad || nonfinite_bits(v[f]);
+    }
+    if (__ballot(bad) != 0 && lane == 0 && !D.diverged[w]) {
+        D.diverged[w] = 1;  // sticky until mw_scene_clear_diverged
+        atomicAdd(reinterpret_cast<unsigned long long*>(D.overflow + 4), 1ull);
     }
     if (!A.paused) {
         if (lane == 0) {
             D.ncontact[w] = nc;
             if (ovf) atomicAdd(D.overflow, ovf);
-            if (unconv) atomicAdd(D.overflow + 1, unconv);
+            if (unconv) atomicAdd(reinterpret_cast<unsigned long long*>(D.overflow + 2), static_cast<unsigned long long>(unconv));
         }
         if (A.want_contacts && lane < nc) {
             const float inv_dt = A.inv_dt;

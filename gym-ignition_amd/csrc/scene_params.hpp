@@ -111,7 +111,9 @@ struct SceneDev {
     // depth, node A, node B (-1 ground)) and their count [W]
     float* contact;
     int32_t* ncontact;
-    int32_t* overflow;   // [0] contact points / rows dropped (capacity), [1] exact LCP solves out of budget
+    int32_t* overflow;   // [0] contact points / rows dropped (capacity), [2..3] exact LCP solves out of
+                         // budget (uint64), [4..5] worlds flagged diverged (uint64)
+    uint8_t* diverged;   // [W] sticky: the world's stored joint / base state was not finite
     float* wphys;        // [4][W] per-world physics: gravity xyz (World::setGravity), ground friction
     // exact-LCP warm start, the previous step's impulses by row identity:
     // [0] contact count [W], [1 .. kScMaxContacts] contact keys (ground slot,

@@ -152,6 +152,12 @@ struct mw_sim {
     int64_t wr_until = 0;
     int* h_overflow = nullptr;    // pinned copy read back with each synchronous run
     int64_t overflow_seen = 0;    // drops already reported
+    // divergence detection: [W] sticky per-world flags + the uint64 count of
+    // worlds flagged (device), its pinned copy (read back with every
+    // synchronous run) and the flags already reported
+    uint8_t* d_health = nullptr;
+    uint64_t* h_ndiv = nullptr;
+    int64_t div_seen = 0;
     int32_t lcp_mode = MW_LCP_EXACT;  // mw_set_lcp_solver (wave kernel)
     int32_t lcp_solves = 24;          // linear-solve budget of the exact solve per step
     mw::SimDev dev;
@@ -564,6 +570,8 @@ void mw_destroy(mw_sim* s) {
         (void)hipHostFree(s->h_base);
         (void)hipHostFree(s->h_cdata);
         (void)hipHostFree(s->h_cmask);
+        (void)hipFree(s->d_health);
+        (void)hipHostFree(s->h_ndiv);
         if (s->own_stream) (void)hipStreamDestroy(s->stream);
     }
     delete s;
@@ -750,8 +758,10 @@ static int alloc_wave_buffers(mw_sim* s) {
     MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_pid), mw::kMaxBodies * sizeof(mw::PidF)));
     MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_pid), mw::kMaxBodies * sizeof(mw::PidF),
                          hipHostMallocDefault));
-    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), 2 * sizeof(int)));
-    MW_HIP(hipMemsetAsync(s->d_overflow, 0, 2 * sizeof(int), s->stream));
+    // [0] dropped rows (int32, drained into overflow_seen), [2..3] unconverged
+    // exact-LCP world-steps (uint64)
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_overflow), 4 * sizeof(int)));
+    MW_HIP(hipMemsetAsync(s->d_overflow, 0, 4 * sizeof(int), s->stream));
     MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_overflow), 2 * sizeof(int), hipHostMallocDefault));
     s->h_overflow[0] = s->h_overflow[1] = 0;
     const size_t wb = static_cast<size_t>(mw::kWaveWarmWordsHost) * W * sizeof(float);
@@ -779,10 +789,10 @@ int mw_lcp_unconverged(const mw_sim* s, int64_t* worlds) {
     if (!worlds) return fail(MW_EINVAL, "null argument");
     *worlds = 0;
     if (!s->d_overflow) return MW_OK;
-    int v[2] = {0, 0};
-    MW_HIP(hipMemcpyAsync(v, s->d_overflow, 2 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+    uint64_t v = 0;
+    MW_HIP(hipMemcpyAsync(&v, s->d_overflow + 2, sizeof(v), hipMemcpyDeviceToHost, s->stream));
     MW_HIP(hipStreamSynchronize(s->stream));
-    *worlds = v[1];
+    *worlds = static_cast<int64_t>(v);
     return MW_OK;
 }
 
@@ -815,6 +825,16 @@ int mw_initialize(mw_sim* s) {
         s->stream_set = true;
     }
     s->n = s->model.dofs();
+    {
+        // divergence flags [W] (rounded to 8 bytes) + the uint64 count
+        const size_t rw = (static_cast<size_t>(s->W) + 7) & ~size_t{7};
+        MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_health), rw + 8));
+        MW_HIP(hipMemsetAsync(s->d_health, 0, rw + 8, s->stream));
+        MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ndiv), sizeof(uint64_t), hipHostMallocDefault));
+        *s->h_ndiv = 0;
+        s->dev.div = s->fdev.div = s->d_health;
+        s->dev.ndiv = s->fdev.ndiv = reinterpret_cast<unsigned long long*>(s->d_health + rw);
+    }
     if (s->fbase()) {
         const size_t W = static_cast<size_t>(s->W);
         const size_t ns = static_cast<size_t>(s->n_slots);
@@ -935,6 +955,17 @@ int mw_set_stream(mw_sim* s, void* stream) {
     return MW_OK;
 }
 
+// worlds newly flagged diverged by the run just read back (h_ndiv): the run
+// has advanced every world, the flagged ones hold non-finite state
+static int report_divergence(mw_sim* s) {
+    const int64_t n = static_cast<int64_t>(*s->h_ndiv);
+    if (n <= s->div_seen) return MW_OK;
+    const int64_t d = n - s->div_seen;
+    s->div_seen = n;
+    return fail(MW_EDIVERGED, std::to_string(d) + " world(s) diverged in this run: their joint or base state is "
+                                                  "not finite (mw_diverged lists them)");
+}
+
 // pending base resets: one H2D copy of [rpose | rvel] and the flags
 static int upload_base_resets(mw_sim* s) {
     const size_t W = static_cast<size_t>(s->W);
@@ -987,9 +1018,10 @@ static int run_free(mw_sim* s, int paused, bool readback = true) {
         return MW_OK;
     }
     if ((rc = read_base(s, paused))) return rc;
+    MW_HIP(hipMemcpyAsync(s->h_ndiv, s->dev.ndiv, sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
     MW_HIP(hipStreamSynchronize(s->stream));
     s->contacts_stale = false;
-    return MW_OK;
+    return report_divergence(s);
 }
 
 // The world wrenches of the substeps (it0, it0 + chunk]: the launch ends
@@ -1123,6 +1155,7 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
         if (s->float_tree && (rc = read_base(s, paused))) return rc;
         if (s->h_overflow)
             MW_HIP(hipMemcpyAsync(s->h_overflow, s->d_overflow, 2 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
+        MW_HIP(hipMemcpyAsync(s->h_ndiv, s->dev.ndiv, sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
         MW_HIP(hipStreamSynchronize(s->stream));
         s->contacts_stale = false;
     } else {
@@ -1146,7 +1179,7 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
                                       " constraint rows: a world exceeded the per-step capacity of the "
                                       "world-per-wavefront kernel (64 rows)");
     }
-    return MW_OK;
+    return readback ? report_divergence(s) : MW_OK;
 }
 
 int mw_run(mw_sim* s, int paused) { return run_impl(s, paused, true); }
@@ -1896,6 +1929,107 @@ int mw_device_ptr(mw_sim* s, const char* field, void** dptr, int64_t* stride) {
     } else return fail(MW_ENOTFOUND, "unknown field '" + f + "'");
     if (stride) *stride = s->W;
     s->host_stale = true;  // the caller may write through the view
+    return MW_OK;
+}
+
+// ------------------------------------------------ divergence, snapshots ----
+
+int mw_diverged(mw_sim* s, int32_t w0, int32_t nw, uint8_t* flags, int64_t* count) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "world range out of bounds");
+    if (flags && nw) MW_HIP(hipMemcpyAsync(flags, s->dev.div + w0, nw, hipMemcpyDeviceToHost, s->stream));
+    uint64_t n = 0;
+    MW_HIP(hipMemcpyAsync(&n, s->dev.ndiv, sizeof(n), hipMemcpyDeviceToHost, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    if (count) *count = static_cast<int64_t>(n);
+    return MW_OK;
+}
+
+int mw_clear_diverged(mw_sim* s, int32_t w0, int32_t nw) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "world range out of bounds");
+    if (nw) MW_HIP(hipMemsetAsync(s->dev.div + w0, 0, nw, s->stream));
+    return MW_OK;
+}
+
+namespace {
+
+// the device rows of the per-world record (mw_get_state): {first row, rows},
+// every row W floats
+std::vector<std::pair<float*, int>> state_rows(const mw_sim* s) {
+    std::vector<std::pair<float*, int>> v;
+    if (s->nw) {
+        v.push_back({s->dev.q, 3 * s->n});       // q, qd, qdd
+        v.push_back({s->dev.pid_e, 4 * s->n});   // pid_e, pid_i, pid_u, qlo
+    }
+    if (s->fbase()) v.push_back({s->fdev.base, 13});
+    if (s->d_warm) v.push_back({s->d_warm, mw::kWaveWarmWordsHost});
+    return v;
+}
+
+int state_words(const mw_sim* s) {
+    int k = 0;
+    for (const auto& r : state_rows(s)) k += r.second;
+    return k;
+}
+
+}  // namespace
+
+int mw_state_words(const mw_sim* s, int32_t* words) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!words) return fail(MW_EINVAL, "null argument");
+    *words = state_words(s);
+    return MW_OK;
+}
+
+int mw_get_state(mw_sim* s, int32_t w0, int32_t nw, float* out) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!out || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad argument");
+    if (!nw) return MW_OK;
+    const int K = state_words(s);
+    std::vector<float> tmp(static_cast<size_t>(K) * nw);
+    int row = 0;
+    for (const auto& r : state_rows(s)) {
+        MW_HIP(hipMemcpy2DAsync(tmp.data() + static_cast<size_t>(row) * nw, nw * sizeof(float), r.first + w0,
+                                static_cast<size_t>(s->W) * sizeof(float), nw * sizeof(float), r.second,
+                                hipMemcpyDeviceToHost, s->stream));
+        row += r.second;
+    }
+    MW_HIP(hipStreamSynchronize(s->stream));
+    for (int w = 0; w < nw; ++w)
+        for (int k = 0; k < K; ++k) out[static_cast<size_t>(w) * K + k] = tmp[static_cast<size_t>(k) * nw + w];
+    return MW_OK;
+}
+
+int mw_set_state(mw_sim* s, int32_t w0, int32_t nw, const float* in) {
+    int rc = check_sim(s);
+    if (rc) return rc;
+    if (!in || w0 < 0 || nw < 0 || w0 + nw > s->W) return fail(MW_EINVAL, "bad argument");
+    if (!nw) return MW_OK;
+    const int K = state_words(s);
+    std::vector<float> tmp(static_cast<size_t>(K) * nw);
+    for (int w = 0; w < nw; ++w)
+        for (int k = 0; k < K; ++k) tmp[static_cast<size_t>(k) * nw + w] = in[static_cast<size_t>(w) * K + k];
+    int row = 0;
+    for (const auto& r : state_rows(s)) {
+        MW_HIP(hipMemcpy2DAsync(r.first + w0, static_cast<size_t>(s->W) * sizeof(float),
+                                tmp.data() + static_cast<size_t>(row) * nw, nw * sizeof(float), nw * sizeof(float),
+                                r.second, hipMemcpyHostToDevice, s->stream));
+        row += r.second;
+    }
+    // the record replaces the worlds' state: their pending resets (joint,
+    // base) are dropped and their divergence flags cleared
+    for (int d = 0; d < s->n && s->nw; ++d)
+        for (int w = w0; w < w0 + nw; ++w) s->hrflag()[s->idx(d, w)] = 0;
+    for (int w = w0; w < w0 + nw && !s->h_rflag.empty(); ++w) s->h_rflag[w] = 0;
+    MW_HIP(hipMemsetAsync(s->dev.div + w0, 0, nw, s->stream));
+    MW_HIP(hipStreamSynchronize(s->stream));
+    s->host_stale = true;
+    s->contacts_stale = s->fbase() && s->contacts;
     return MW_OK;
 }
 

@@ -24,7 +24,8 @@
 // within a budget of linear solves per step.  Converged = every row's
 // complementarity residual (oracle lcp_residual, velocity units) within fp32
 // round-off of its own terms.  A world that runs out of budget keeps its
-// current impulses (feasible, never worse than the PGS start) and is counted.
+// current impulses projected onto the boxes of its current normals (feasible:
+// x_n >= 0, |x_t| <= mu x_n, box rows in [lo, hi]) and is counted.
 #pragma once
 
 namespace mw {
@@ -428,6 +429,20 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
             xl = fr ? xl + d : xl;
             at_min = true;
         }
+    }
+    if (!converged) {
+        // out of budget: inside a staggered round the friction rows keep to the
+        // round's boxes, frozen at its starting normals, while the normals may
+        // have shrunk since -- project onto the boxes of the current impulses
+        // (normals >= 0, box rows in [lo, hi], |x_t| <= mu x_n) so the impulses
+        // handed back are feasible
+        float xp = xl;
+        if (R.kind == 0) xp = fmaxf(xp, 0.f);
+        if (R.kind == 2) xp = fminf(fmaxf(xp, R.lo), R.hi);
+        float Lp, Up;
+        lcp_bounds<RC>(R, xp, mu, n, Lp, Up);
+        if (R.kind == 1) xp = fminf(fmaxf(xp, Lp), Up);
+        xl = R.live ? xp : 0.f;
     }
     n_solves = solves;
     n_rounds = iter;

@@ -16,7 +16,7 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__fi
 LIB_PATH = os.environ.get("MWSTEP_LIB", os.path.join(_PKG_ROOT, "libmwstep.so"))
 
 MW_OK = 0
-MW_EINVAL, MW_ESTATE, MW_EPARSE, MW_EHIP, MW_ENOTFOUND, MW_ECAPACITY = 1, 2, 3, 4, 5, 6
+MW_EINVAL, MW_ESTATE, MW_EPARSE, MW_EHIP, MW_ENOTFOUND, MW_ECAPACITY, MW_EDIVERGED = 1, 2, 3, 4, 5, 6, 7
 
 MODE_INVALID, MODE_IDLE, MODE_FORCE, MODE_VELOCITY = 0, 1, 2, 3
 MODE_VELOCITY_FOLLOWER_DART, MODE_POSITION, MODE_POSITION_INTERPOLATED = 4, 5, 6
@@ -143,6 +143,11 @@ SIGNATURES = [
     ("mw_constraint_overflow", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
     ("mw_device_ptr", ctypes.c_int, [_P, _S, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    ("mw_diverged", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int64)]),
+    ("mw_clear_diverged", ctypes.c_int, [_P, _I, _I]),
+    ("mw_state_words", ctypes.c_int, [_P, _IP]),
+    ("mw_get_state", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    ("mw_set_state", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mw_vecenv_create", ctypes.c_int, [_P, ctypes.POINTER(MwTaskConfig), ctypes.POINTER(_P)]),
     ("mw_vecenv_destroy", None, [_P]),
     ("mw_vecenv_obs_dim", ctypes.c_int, [_P, _IP]),
@@ -203,6 +208,8 @@ SCENE_SIGNATURES = [
     ("mw_scene_get_contacts", ctypes.c_int, [_P, _I, _D, _I, _IP]),
     ("mw_scene_apply_world_wrench", ctypes.c_int, [_P, _I, _I, _I, _I, _D, ctypes.c_double]),
     ("mw_scene_overflow", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    ("mw_scene_diverged", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int64)]),
+    ("mw_scene_clear_diverged", ctypes.c_int, [_P, _I, _I]),
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -233,9 +240,15 @@ def last_error() -> str:
     return lib().mw_last_error().decode()
 
 
+class DivergedError(RuntimeError):
+    """MW_EDIVERGED: the run advanced every world, and some world's state
+    became non-finite (``Simulator.diverged`` / ``Scene.diverged`` list them)."""
+
+
 def check(rc: int, what: str = "") -> None:
     if rc != MW_OK:
-        raise RuntimeError(f"{what}: {last_error()}" if what else last_error())
+        msg = f"{what}: {last_error()}" if what else last_error()
+        raise DivergedError(msg) if rc == MW_EDIVERGED else RuntimeError(msg)
 
 
 def dptr(arr) -> ctypes.POINTER(ctypes.c_double):

@@ -173,6 +173,20 @@ class Scene:
         N.check(N.lib().mw_scene_lcp_solver(self.handle, ctypes.byref(m), ctypes.byref(k)))
         return m.value == N.LCP_EXACT, k.value
 
+    def diverged(self, w0: int = 0, nw: Optional[int] = None):
+        """(flags [nw] bool, worlds flagged since initialisation): worlds whose
+        stored state became non-finite (mw_scene_diverged)."""
+        nw = self.n_worlds - w0 if nw is None else nw
+        flags = np.zeros(nw, dtype=np.uint8)
+        n = ctypes.c_int64()
+        N.check(N.lib().mw_scene_diverged(self.handle, w0, nw, flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                          ctypes.byref(n)), "diverged")
+        return flags.astype(bool), n.value
+
+    def clear_diverged(self, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_scene_clear_diverged(self.handle, w0, nw), "clear_diverged")
+
     def lcp_unconverged(self) -> int:
         v = ctypes.c_int64()
         N.check(N.lib().mw_scene_lcp_unconverged(self.handle, ctypes.byref(v)))

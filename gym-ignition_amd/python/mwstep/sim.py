@@ -304,6 +304,37 @@ class Simulator:
         N.check(N.lib().mw_lcp_solver(self.handle, ctypes.byref(m), ctypes.byref(k)))
         return m.value == N.LCP_EXACT, k.value
 
+    def diverged(self, w0: int = 0, nw: Optional[int] = None):
+        """(flags [nw] bool of worlds [w0, w0 + nw), number of worlds flagged
+        since initialisation): worlds whose stored state became non-finite
+        (mw_diverged)."""
+        nw = self.n_worlds - w0 if nw is None else nw
+        flags = np.zeros(nw, dtype=np.uint8)
+        n = ctypes.c_int64()
+        N.check(N.lib().mw_diverged(self.handle, w0, nw, flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                    ctypes.byref(n)), "diverged")
+        return flags.astype(bool), n.value
+
+    def clear_diverged(self, w0: int = 0, nw: Optional[int] = None) -> None:
+        nw = self.n_worlds - w0 if nw is None else nw
+        N.check(N.lib().mw_clear_diverged(self.handle, w0, nw), "clear_diverged")
+
+    def get_state(self, w0: int = 0, nw: Optional[int] = None) -> np.ndarray:
+        """mw_get_state: the full per-world record, float32 [nw, words]."""
+        nw = self.n_worlds - w0 if nw is None else nw
+        k = ctypes.c_int32()
+        N.check(N.lib().mw_state_words(self.handle, ctypes.byref(k)), "state_words")
+        out = np.zeros((nw, k.value), dtype=np.float32)
+        N.check(N.lib().mw_get_state(self.handle, w0, nw, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))),
+                "get_state")
+        return out
+
+    def set_state(self, state, w0: int = 0) -> None:
+        """mw_set_state: write a record of get_state back (bit-exact)."""
+        st = np.ascontiguousarray(state, dtype=np.float32)
+        N.check(N.lib().mw_set_state(self.handle, w0, st.shape[0], st.ctypes.data_as(ctypes.POINTER(ctypes.c_float))),
+                "set_state")
+
     def lcp_unconverged(self) -> int:
         """World-steps whose exact LCP solve ran out of its budget."""
         v = ctypes.c_int64()

@@ -67,6 +67,25 @@ def _device() -> int:
     return int(os.environ.get("MWSTEP_DEVICE", "0"))
 
 
+# slot-wide components of a scene model (Model._comp / _set_component): keys
+# ("pid", dof), ("param", dof, which), ("period",)
+def _read_component(view, key):
+    if key[0] == "pid":
+        return tuple(float(v) for v in view.pid(key[1]))
+    if key[0] == "param":
+        return float(view.joint_param(key[1], key[2]))
+    return float(view.controller_period())
+
+
+def _write_component(view, key, value) -> None:
+    if key[0] == "pid":
+        view.set_pid(key[1], list(value))
+    elif key[0] == "param":
+        view.set_joint_param(key[1], key[2], value)
+    else:
+        view.set_controller_period(value)
+
+
 # ---------------------------------------------------------------- SDF helpers
 _EMPTY_WORLD = """<?xml version="1.0" ?>
 <sdf version="1.6">
@@ -201,13 +220,18 @@ class Joint:
 
     def pid(self) -> core.PID:
         # Joint::pid (Joint.cpp:470-476)
-        return core.PID.from_list(self._model._sim.pid(self._dof))
+        return core.PID.from_list(self._model._comp(("pid", self._dof)))
 
     def set_pid(self, pid: core.PID) -> bool:
-        # Joint::setPID (Joint.cpp:479-525)
+        # Joint::setPID (Joint.cpp:479-525): output limits looser than the
+        # effort limit are replaced by +-effort (what the scene stores too)
         try:
-            self._model._own_slot()
-            self._model._sim.set_pid(self._dof, pid.to_list())
+            g = [float(v) for v in pid.to_list()]
+            from mwstep import native as N
+            maxf = self._model._comp(("param", self._dof, N.PARAM_MAX_GENERALIZED_FORCE))
+            if g[3] < -maxf or g[4] > maxf:
+                g[3], g[4] = -maxf, maxf
+            self._model._set_component(("pid", self._dof), tuple(g))
             return True
         except RuntimeError as e:
             _err(str(e))
@@ -261,17 +285,15 @@ class Joint:
 
     # -- parameters (only while the model was just created)
     def _set_param(self, which: int, value: float) -> bool:
-        from mwstep import native as N
         try:
-            self._model._own_slot()
-            self._model._sim.set_joint_param(self._dof, which, value)
+            self._model._set_component(("param", self._dof, which), float(value))
             return True
         except RuntimeError as e:
             _err(str(e))
             return False
 
     def _param(self, which: int) -> float:
-        return self._model._sim.joint_param(self._dof, which)
+        return self._model._comp(("param", self._dof, which))
 
     def set_coulomb_friction(self, value: float) -> bool:
         from mwstep import native as N
@@ -954,9 +976,8 @@ class Model:
         return self._sim.contacts_enabled()
 
     def enable_contacts(self, enable: bool = True) -> bool:
-        # Model::enableContacts (Model.cpp:686-700)
-        if bool(enable) != self._sim.contacts_enabled():
-            self._own_slot()
+        # Model::enableContacts (Model.cpp:686-700): a flag of this world's
+        # view of the slot (the scene detects every world's contacts)
         self._sim.enable_contacts(enable)
         return True
 
@@ -969,25 +990,59 @@ class Model:
 
     def controller_period(self) -> float:
         # Model::controllerPeriod (Model.cpp:581-587)
-        return self._sim.controller_period()
+        return self._comp(("period",))
 
     def set_controller_period(self, period: float) -> bool:
         # Model::setControllerPeriod (Model.cpp:589-602)
         try:
-            self._own_slot()
-            self._sim.set_controller_period(float(period))
+            if not (float(period) > 0.0):
+                raise RuntimeError("The controller period must be greater than zero")
+            self._set_component(("period",), float(period))
             return True
         except RuntimeError as e:
             _err(str(e))
             return False
 
-    def _own_slot(self) -> None:
-        # joint parameters, PID gains, the controller period and contact
-        # detection are a scene slot's: before one world's model changes them,
-        # a slot shared with other worlds' models (same name, file and pose)
-        # is left for a slot of its own -- each world keeps its own
-        # components, as in the reference's per-world ECM
-        self._world._simulator._own_slot(self)
+    # -- slot-wide components: PID gains, joint parameters, controller period
+    def _comp(self, key):
+        """The component `key` of this world's model: a change recorded
+        since the last run, else the scene slot's value."""
+        if self._sim is None:
+            raise RuntimeError(f"model '{self._name}' was removed")
+        pend = self.__dict__.get("_pending_comp")
+        if pend and key in pend:
+            return pend[key]
+        return _read_component(self._sim, key)
+
+    def _set_component(self, key, value) -> None:
+        """Joint::setPID / setCoulombFriction / setViscousFriction /
+        setMaxGeneralizedForce, Model::setControllerPeriod.  These components
+        belong to a scene slot, which the same model inserted into several
+        worlds shares; the reference keeps them per world (one ECM per
+        world).  A model alone in its slot changes the slot at once.  A model
+        sharing its slot records the change (a change back to the slot's
+        value cancels it), and the next run() groups the slot's models by
+        their recorded changes: the worlds that made none -- or, if every
+        world changed something, the largest group of identical changes --
+        keep the slot, every other group of identical changes moves to one
+        slot of its own (GazeboSimulator._resolve_components).  So N worlds
+        that each insert a Panda and call set_pid on every joint end up in
+        one slot, changed once."""
+        if self._sim is None:
+            raise RuntimeError(f"model '{self._name}' was removed")
+        sim = self._world._simulator
+        if not sim._slot_shared(self):
+            _write_component(self._sim, key, value)
+            return
+        if key[0] == "param":
+            # validate now (the reference's setter fails at once): a model that
+            # was already stepped refuses parameter changes
+            _write_component(self._sim, key, _read_component(self._sim, key))
+        pend = self.__dict__.setdefault("_pending_comp", {})
+        if value == _read_component(self._sim, key):
+            pend.pop(key, None)
+        else:
+            pend[key] = value
 
     def _internal_link(self, n: str) -> bool:
         return bool(self._ball) and (n.endswith("#x") or n.endswith("#y")) and n[:-2] in self._ball
@@ -1665,59 +1720,109 @@ class GazeboSimulator:
             sc.set_present(slot, 0, w, 1)   # placed, not stepped until the Physics system is inserted
         return SceneView(sc, slot, w)
 
-    def _own_slot(self, model: "Model") -> None:
-        from mwstep.scene import SceneView
-        old = model._sim
-        sc, m, w = self._scene, old.m, old.w
-        shared = any(isinstance(o, Model) and o is not model and o._sim is not None and o._sim.m == m
-                     for wd in self._worlds.values() for o in wd._models.values())
-        if not shared:
-            return
-        name, text, pose = self._slots[m][:3]
-        present = sc.present(m, w)
-        # state and components of this world's model, read before the move
-        q, qd = old.get("q"), old.get("qd")
-        tgt = {k: old.get(k) for k in ("position_target", "velocity_target", "force_target")}
-        nd = sc.models[m]["dofs"]
-        modes = [old.control_mode(w, d) for d in range(nd)]
-        pids = [old.pid(d) for d in range(nd)]
+    def _slot_models(self, m: int) -> List["Model"]:
+        return [o for wd in self._worlds.values() for o in wd._models.values()
+                if isinstance(o, Model) and o._sim is not None and o._sim.m == m]
+
+    def _slot_shared(self, model: "Model") -> bool:
+        return any(o is not model for o in self._slot_models(model._sim.m))
+
+    def _resolve_components(self) -> None:
+        """Apply the slot-wide component changes that models sharing a slot
+        recorded since the last run (Model._set_component): per slot, the
+        models are grouped by their recorded changes; the group without
+        changes (else the largest group) keeps the slot and its changes are
+        applied to it once, every other group moves to one new slot."""
+        slots = sorted({o._sim.m for wd in self._worlds.values() for o in wd._models.values()
+                        if isinstance(o, Model) and o._sim is not None and o.__dict__.get("_pending_comp")})
+        for m in slots:
+            models = self._slot_models(m)
+            groups: Dict[tuple, List[Model]] = {}
+            for o in models:
+                k = tuple(sorted((o.__dict__.get("_pending_comp") or {}).items()))
+                groups.setdefault(k, []).append(o)
+            keep = () if () in groups else max(groups, key=lambda k: len(groups[k]))
+            for k, grp in groups.items():
+                if k != keep:
+                    self._move_models(grp, m, dict(k))
+            view = groups[keep][0]._sim
+            for key, value in keep:
+                _write_component(view, key, value)
+            for o in models:
+                o.__dict__.pop("_pending_comp", None)
+
+    def _move_models(self, models: List["Model"], m: int, changes: dict) -> None:
+        """Move the models of several worlds, all sharing slot m, to one new
+        slot whose components are slot m's with `changes` applied, carrying
+        each world's state (joint state, targets, control modes, base).  If
+        the scene has no room for another slot, the changes go to slot m
+        itself (every world sharing it sees them) with a warning."""
         from mwstep import native as N
-        params = [[old.joint_param(d, k) for k in (N.PARAM_COULOMB_FRICTION, N.PARAM_VISCOUS_FRICTION,
-                                                    N.PARAM_MAX_GENERALIZED_FORCE)] for d in range(nd)]
-        period, contacts = old.controller_period(), old.contacts_enabled()
+        from mwstep.scene import SceneView
+        sc = self._scene
+        old = models[0]._sim
+        name, text, pose = self._slots[m][:3]
+        nd = sc.models[m]["dofs"]
         floating = sc.models[m]["floating"]
-        pose_now, vel_now = (old.base_pose(), old.base_velocity()) if floating else (None, None)
-        slot = sc.insert_model(text, list(pose), f"{name}#{len(self._slots)}", worlds=(w, 1))
-        self._slots.append((name, text, tuple(pose), "own", w))  # never shared again
-        view = SceneView(sc, slot, w)
+        pkeys = (N.PARAM_COULOMB_FRICTION, N.PARAM_VISCOUS_FRICTION, N.PARAM_MAX_GENERALIZED_FORCE)
+        comps = {("pid", d): _read_component(old, ("pid", d)) for d in range(nd)}
+        comps.update({("param", d, k): _read_component(old, ("param", d, k)) for d in range(nd) for k in pkeys})
+        comps[("period",)] = _read_component(old, ("period",))
+        comps.update(changes)
+        # each world's state and per-world components, read before the move
+        carried = []
+        for mdl in models:
+            v = mdl._sim
+            carried.append(dict(
+                present=sc.present(m, v.w), q=v.get("q"), qd=v.get("qd"), qdd=v.get("qdd"),
+                tgt={k: v.get(k) for k in ("position_target", "velocity_target", "force_target")},
+                modes=[v.control_mode(v.w, d) for d in range(nd)], contacts=v.contacts_enabled(),
+                base=(v.base_pose(), v.base_velocity()) if floating else None))
+        w0 = models[0]._sim.w
+        try:
+            slot = sc.insert_model(text, list(pose), f"{name}#{len(self._slots)}", worlds=(w0, 1))
+        except RuntimeError as e:
+            _warn(f"No room for another scene slot ({e}): the component change of model '{name}' "
+                  f"applies to every world sharing its slot")
+            for key, value in changes.items():
+                _write_component(old, key, value)
+            return
+        self._slots.append((name, text, tuple(pose), "own", tuple(mdl._sim.w for mdl in models)))  # never shared again
+        first = SceneView(sc, slot, w0)
+        # slot-wide components first (a parameter change rebuilds the slot)
+        for key in sorted(k for k in comps if k[0] == "param"):
+            _write_component(first, key, comps[key])
         for d in range(nd):
-            view.set_pid(d, pids[d])
-            for k, v in zip((N.PARAM_COULOMB_FRICTION, N.PARAM_VISCOUS_FRICTION, N.PARAM_MAX_GENERALIZED_FORCE),
-                            params[d]):
-                view.set_joint_param(d, k, v)
-            view.set_control_mode(modes[d], dofs=[d])
-        view.set_controller_period(period)
-        view.enable_contacts(contacts)
-        view.set("reset_q", q)
-        view.set("reset_qd", qd)
-        for k, v in tgt.items():
+            _write_component(first, ("pid", d), comps[("pid", d)])
+        _write_component(first, ("period",), comps[("period",)])
+        for mdl, c in zip(models, carried):
+            w = mdl._sim.w
+            if w != w0:
+                sc.set_present(slot, 1, w, 1)
+            view = SceneView(sc, slot, w)
             for d in range(nd):
-                if k == "force_target" and v[0, d] == 0.0:
-                    continue
-                try:  # the targets the dof's control mode accepts
-                    view.set(k, v[:, d:d + 1], dofs=[d])
-                except RuntimeError:
-                    pass
-        if floating:
-            view.reset_base_pose(pose_now)
-            view.reset_base_velocity(vel_now)
-        sc.set_present(m, 0, w, 1)
-        if not present:  # insert_model placed it (placing again would reset it)
-            sc.set_present(slot, 0, w, 1)
-        model._sim = view
-        model._export = None
-        # until the next run applies the resets, the getters read the carried state
-        model._state_override = {"q": q[0].copy(), "qd": qd[0].copy(), "qdd": old.get("qdd")[0].copy()}
+                view.set_control_mode(c["modes"][d], dofs=[d])
+            view.enable_contacts(c["contacts"])
+            view.set("reset_q", c["q"])
+            view.set("reset_qd", c["qd"])
+            for k, v in c["tgt"].items():
+                for d in range(nd):
+                    if k == "force_target" and v[0, d] == 0.0:
+                        continue
+                    try:  # the targets the dof's control mode accepts
+                        view.set(k, v[:, d:d + 1], dofs=[d])
+                    except RuntimeError:
+                        pass
+            if floating:
+                view.reset_base_pose(c["base"][0])
+                view.reset_base_velocity(c["base"][1])
+            sc.set_present(m, 0, w, 1)
+            if not c["present"]:  # placed without the Physics system: not stepped yet
+                sc.set_present(slot, 0, w, 1)
+            mdl._sim = view
+            mdl._export = None
+            # until the next run applies the resets, the getters read the carried state
+            mdl._state_override = {"q": c["q"][0].copy(), "qd": c["qd"][0].copy(), "qdd": c["qdd"][0].copy()}
 
     def _remove_model(self, view) -> None:
         if self._scene is not None:
@@ -1753,6 +1858,7 @@ class GazeboSimulator:
             self._iterations += self._steps_per_run
         t_ns = self._iterations * int(round(self._step_size * 1e9))
         try:
+            self._resolve_components()
             for w in self._worlds.values():
                 w._update(paused, t_ns)
             self._scene.run(paused)

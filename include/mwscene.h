@@ -110,6 +110,11 @@ int mw_scene_set_lcp_solver(mw_scene* sc, int32_t mode, int32_t max_solves);
 int mw_scene_lcp_solver(const mw_scene* sc, int32_t* mode, int32_t* max_solves);
 /* World-steps whose exact solve ran out of budget (or had > 64 rows). */
 int mw_scene_lcp_unconverged(const mw_scene* sc, int64_t* world_steps);
+/* Failure detection (as mw_diverged): the scene kernel flags a world whose
+ * stored joint or base state is not finite; mw_scene_run returns MW_EDIVERGED
+ * when the run flagged new worlds (ScenarI/O run() -> false). */
+int mw_scene_diverged(mw_scene* sc, int32_t w0, int32_t nw, uint8_t* flags, int64_t* count);
+int mw_scene_clear_diverged(mw_scene* sc, int32_t w0, int32_t nw);
 int mw_scene_gravity(const mw_scene* sc, double g[3]);
 /* the ground plane's friction, and the plane in (enabled) or out of every world */
 int mw_scene_set_ground_plane(mw_scene* sc, int32_t enabled, double mu);

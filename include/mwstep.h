@@ -40,6 +40,9 @@ extern "C" {
 #define MW_ECAPACITY 6   /* a per-step capacity was exceeded: contact points /
                             constraint rows were dropped (the step ran without
                             them; DART would have kept them)                */
+#define MW_EDIVERGED 7   /* a world's state became non-finite in this run (the
+                            run advanced every world; mw_diverged lists the
+                            flagged ones) -- failure detection, SURVEY.md §5 */
 
 /* JointControlMode, same numbering as scenario::core::JointControlMode
  * (cpp/scenario/core/include/scenario/core/Joint.h:37-75). */
@@ -227,7 +230,9 @@ int mw_reset_base_velocity(mw_sim* sim, int32_t w0, int32_t nw, const double* li
  * directions do not count; warm_start != 0 starts
  * every row from the previous step's impulse of the same contact slot / joint
  * row (cold after a reset of the world).  Defaults: 0, 0 (a fixed sweep
- * count from zero).  Other kernels ignore both. */
+ * count from zero).  Other kernels ignore the tolerance; warm_start != 0
+ * fails with MW_ESTATE once an initialized simulator runs on another kernel
+ * (they have no warm-start record). */
 int mw_set_pgs_options(mw_sim* sim, double tol, int32_t warm_start);
 int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
 /* The boxed-LCP solver of the world-per-wavefront kernel.  MW_LCP_EXACT
@@ -259,7 +264,9 @@ int mw_set_lcp_solver(mw_sim* sim, int32_t mode, int32_t max_solves);
 int mw_apply_link_wrench(mw_sim* sim, int32_t link, int32_t w0, int32_t nw, const double* wrench, double duration);
 int mw_lcp_solver(const mw_sim* sim, int32_t* mode, int32_t* max_solves);
 /* World-steps whose exact LCP solve ran out of budget since mw_initialize
- * (they keep the best feasible impulses found; 0 = every solve converged). */
+ * (they keep their last impulses projected onto the friction boxes of their
+ * normals and the joint rows' bounds: feasible, not optimal; 0 = every solve
+ * converged).  64-bit device counters. */
 int mw_lcp_unconverged(const mw_sim* sim, int64_t* world_steps);
 /* The world's ground plane (z = 0, normal +z) and its friction coefficient. */
 int mw_set_ground_plane(mw_sim* sim, int32_t enabled, double mu);
@@ -293,6 +300,34 @@ int mw_device_ptr(mw_sim* sim, const char* field, void** dptr, int64_t* world_st
 /* Device-to-device copy of the SoA state ([n_dofs][n_worlds] float32 each) to
  * (to_sim = 0) or from (to_sim = 1) caller buffers, on the sim's stream. */
 int mw_copy_state(mw_sim* sim, float* q_dev, float* qd_dev, int to_sim);
+
+/* ---- failure detection and per-world snapshots ----
+ * The run kernels flag a world (sticky) when the joint or base state they
+ * store is not finite -- tested on the exponent bits, the kernels being
+ * built finite-math-only -- and count the flagged worlds.  mw_run reads the
+ * count back with its state and returns MW_EDIVERGED when new worlds were
+ * flagged (the reference has no such check: GazeboSimulator::run,
+ * GazeboSimulator.cpp:202-251, only reports a failed server step);
+ * mw_run_device leaves the check to mw_diverged.  mw_diverged: flags[nw] of
+ * worlds [w0, w0 + nw) (flags may be NULL) and the number of worlds flagged
+ * since mw_initialize; mw_clear_diverged re-arms the flags of a range (after
+ * the caller reset those worlds). */
+int mw_diverged(mw_sim* sim, int32_t w0, int32_t nw, uint8_t* flags, int64_t* count);
+int mw_clear_diverged(mw_sim* sim, int32_t w0, int32_t nw);
+/* The full per-world record as float32 words, [nw][words] in host memory:
+ * q, qd, qdd, qlo (low word of the compensated joint positions), the
+ * JointController PID state pErrLast / iErr / cmd (n_dofs each, absent for
+ * joint-less bodies), the base pose and body-frame twist (13, floating and
+ * welded-tree models), and the previous step's constraint impulses that the
+ * wave kernel's warm start / exact LCP starts from (its models only).
+ * mw_set_state writes the record back (bit-exact: a restored world steps
+ * exactly as it did from the saved state), drops the worlds' pending resets
+ * and clears their divergence flags.  The simulator time, the controller
+ * period gate and the commands / targets are not per-world state and are not
+ * part of the record. */
+int mw_state_words(const mw_sim* sim, int32_t* words);
+int mw_get_state(mw_sim* sim, int32_t w0, int32_t nw, float* out);
+int mw_set_state(mw_sim* sim, int32_t w0, int32_t nw, const float* in);
 
 /* ---- batched environment (device-side Task logic) ----
  * Tasks mirror python/gym_ignition_environments/tasks/ (CartPole x3,

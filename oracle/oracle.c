@@ -1359,7 +1359,7 @@ static void vec_step_one(const or_model* m, const or_task* t, int W, int w,
     double qw[OR_MAXB], qdw[OR_MAXB], o[4];
     for (int d = 0; d < n; ++d) { qw[d] = q[d * W + w]; qdw[d] = qd[d * W + w]; }
     or_model scratch;
-    world_step(world_model(m, t, (uint32_t)w, episode[w], &scratch), t, qw, qdw, action, pgs_iters);
+    world_step(world_model(m, t, (uint32_t)(w + t->world0), episode[w], &scratch), t, qw, qdw, action, pgs_iters);
     const int no = or_task_obs(t, qw, qdw, o);
     const int tdone = task_done(t, o);
     reward[w] = task_reward(t, qw, qdw, o, tdone);
@@ -1371,7 +1371,7 @@ static void vec_step_one(const or_model* m, const or_task* t, int W, int w,
         for (int k = 0; k < no; ++k) terminal_obs[w * no + k] = o[k];
         episode[w] += 1;
         steps[w] = 0;
-        or_task_reset_state(t, (uint32_t)w, episode[w], qw, qdw);
+        or_task_reset_state(t, (uint32_t)(w + t->world0), episode[w], qw, qdw);
         or_task_obs(t, qw, qdw, o);
     }
     for (int k = 0; k < no; ++k) obs[w * no + k] = o[k];
@@ -1405,7 +1405,7 @@ void or_vec_reset(const or_model* m, const or_task* t, int W, double* q,
         double qw[OR_MAXB], qdw[OR_MAXB], o[4];
         episode[w] = 0;
         steps[w] = 0;
-        or_task_reset_state(t, (uint32_t)w, 0u, qw, qdw);
+        or_task_reset_state(t, (uint32_t)(w + t->world0), 0u, qw, qdw);
         const int no = or_task_obs(t, qw, qdw, o);
         for (int k = 0; k < no; ++k) obs[w * no + k] = o[k];
         for (int d = 0; d < n; ++d) { q[d * W + w] = qw[d]; qd[d * W + w] = qdw[d]; }

@@ -230,7 +230,9 @@ typedef struct {
     /* per-world physics randomisation (bit 0 masses, bit 1 gravity), sampled
      * from (world, episode): randomizers/cartpole.py:51-56, 100-135 */
     int32_t randomize;
-    int32_t pad_;
+    /* global index of world 0 of this env (a rank's shard: its Philox
+     * streams are keyed by the global world index, mwstep/shard.py) */
+    int32_t world0;
     double mass_low, mass_high;     /* additive mass sample, clipped at 0     */
     double gravity_mean, gravity_std;
     double gdir[3];                 /* world z axis in the base frame          */

@@ -133,7 +133,7 @@ class OrTask(ctypes.Structure):
         ("dt", ctypes.c_double),
         ("seed", ctypes.c_uint64),
         ("randomize", ctypes.c_int32),
-        ("pad_", ctypes.c_int32),
+        ("world0", ctypes.c_int32),
         ("mass_low", ctypes.c_double),
         ("mass_high", ctypes.c_double),
         ("gravity_mean", ctypes.c_double),

@@ -285,6 +285,49 @@ def test_one_step_exact_lcp_random_states(require_gpu, oracle, monkeypatch, name
     sim.close()
 
 
+def test_exact_lcp_out_of_budget_is_feasible(require_gpu, oracle, monkeypatch):
+    """a world whose exact solve runs out of its budget keeps
+    impulses inside the friction pyramid of its current normals (DART's
+    boxed LCP never returns |x_t| > mu x_n).  A budget of one linear solve
+    after 2 sweeps leaves many of the adversarial random humanoid states
+    unconverged; every contact force read back must still satisfy
+    f_z >= 0 and |f_x|, |f_y| <= mu f_z (the ground's plane-space tangents
+    are -y and +x)."""
+    from mwstep import native as N
+    from mwstep.sim import Simulator
+    text = _model("humanoid32")
+    monkeypatch.setenv("MWSTEP_WAVE_TREE", "1")
+    W, mu = 256, 0.8
+    rng = np.random.default_rng(11)
+    cm = oracle.load_urdf(text)
+    q, qd, pose, vel, tau = _random_states(cm, W, rng)
+    sim = Simulator(text, n_worlds=W, pgs_iters=2)
+    sim.set_lcp_solver(True, 1)
+    sim.set_ground_plane(True, mu)
+    sim.enable_contacts(True)
+    sim.set("reset_q", q)
+    sim.set("reset_qd", qd)
+    sim.reset_base_pose(pose)
+    sim.reset_base_velocity(vel)
+    sim.run(paused=True)
+    sim.set_control_mode(N.MODE_FORCE)
+    sim.set("force_target", tau)
+    sim.run()
+    unconv = sim.lcp_unconverged()
+    worst, n_pts = 0.0, 0
+    for w in range(W):
+        for r in sim.contacts(w):
+            fz = r[8]
+            n_pts += 1
+            worst = max(worst, (max(-fz, abs(r[6]) - mu * fz, abs(r[7]) - mu * fz)) / (1.0 + abs(fz)))
+    print(f"budget 1: {unconv}/{W} worlds unconverged, {n_pts} contact points, "
+          f"worst pyramid violation {worst:.2e} (relative to 1 N + f_z)")
+    assert unconv >= W // 10 and n_pts > 0
+    assert worst <= 1e-5
+    assert np.isfinite(sim.get("qd")).all()
+    sim.close()
+
+
 def _stand_sim(W, pgs=50):
     from mwstep import get_model_file
     from mwstep import native as N

@@ -535,19 +535,75 @@ def test_per_world_pid_and_joint_parameters(require_gpu):
     # (a new PID starts from a fresh state, as ign-math's does in the
     # reference: its first derivative term kicks)
     assert ja.set_pid(core.PID(50.0, 0.0, 0.0))
-    assert len(gazebo._slots) == 2                      # "a" left the shared slot
     assert ja.pid().p == pytest.approx(50.0)
     jb = gazebo.get_world("b").get_model("pendulum").joints()[0]
     assert jb.pid().p == pytest.approx(pid_b.p)         # "b" kept its gains
-    assert ja.position() == pytest.approx(q50[0], abs=1e-12)  # the move kept the state
-    for _ in range(100):
+    assert gazebo.run()
+    assert len(gazebo._slots) == 2                      # "a" left the shared slot at the run
+    assert ja.pid().p == pytest.approx(50.0) and jb.pid().p == pytest.approx(pid_b.p)
+    for _ in range(99):
         assert gazebo.run()
     qa, qb, qc = (gazebo.get_world(n).get_model("pendulum").joint_positions()[0] for n in names)
     assert qb == qc                                     # untouched worlds stay identical
     assert abs(qa - qb) > 1e-4 and abs(qa) < 10.0       # the retuned world moved differently
     # the other slot-wide components follow the same rule
     mb = gazebo.get_world("b").get_model("pendulum")
-    assert mb.set_controller_period(0.01) and len(gazebo._slots) == 3
+    assert mb.set_controller_period(0.01)
+    assert gazebo.run() and len(gazebo._slots) == 3
+    assert mb.controller_period() == pytest.approx(0.01)
     assert gazebo.get_world("c").get_model("pendulum").controller_period() != pytest.approx(0.01)
+    gazebo.close()
+
+
+def test_many_worlds_set_same_pid_share_one_slot(require_gpu):
+    """the reference Panda wrapper calls set_pid on every joint and
+    set_controller_period on its model (models/panda.py:48-71).  Eight worlds
+    that each insert a Panda and make the same calls keep sharing one scene
+    slot (the changes are applied to it once, at the next run); worlds that
+    make different calls move as groups, one slot per distinct set of
+    changes, and each world steps with its own gains."""
+    from scenario import core
+    from scenario import gazebo as scenario
+    names = [f"w{i}" for i in range(8)]
+    gazebo, get_model_file = _gazebo(names)
+    gains = [core.PID(600.0 - 10 * i, 0.0, 5.0) for i in range(9)]
+    for n in names:
+        w = gazebo.get_world(n)
+        assert w.set_physics_engine(scenario.PhysicsEngine_dart)
+        assert w.insert_model(get_model_file("panda"))
+        m = w.get_model("panda")
+        assert m.set_controller_period(0.001)
+        for jn, g in zip(m.joint_names(), gains):
+            assert m.get_joint(jn).set_pid(g)
+        assert m.set_joint_control_mode(core.JointControlMode_position)
+        assert m.set_joint_position_targets([0.1] * m.dofs())
     assert gazebo.run()
+    assert len(gazebo._slots) == 1
+    models = [gazebo.get_world(n).get_model("panda") for n in names]
+    for m in models:
+        assert m.controller_period() == pytest.approx(0.001)
+        assert [m.get_joint(j).pid().p for j in m.joint_names()] == pytest.approx([g.p for g in gains])
+    for _ in range(20):
+        assert gazebo.run()
+    q = [m.joint_positions() for m in models]
+    assert all(qq == q[0] for qq in q)
+    # worlds 0-2 retune joint 0 the same way, world 3 another way: two groups move
+    for i in range(4):
+        j0 = models[i].get_joint(models[i].joint_names()[0])
+        assert j0.set_pid(core.PID(100.0 if i < 3 else 50.0, 0.0, 1.0))
+    # a change back to the slot's value is no change at all
+    j0 = models[4].get_joint(models[4].joint_names()[0])
+    assert j0.set_pid(core.PID(10.0, 0.0, 0.0)) and j0.set_pid(gains[0])
+    assert gazebo.run()
+    assert len(gazebo._slots) == 3
+    assert len({m._sim.m for m in models[:3]}) == 1 and models[3]._sim.m != models[0]._sim.m
+    assert len({m._sim.m for m in models[4:]}) == 1 and models[4]._sim.m not in (models[0]._sim.m, models[3]._sim.m)
+    assert models[0].get_joint(models[0].joint_names()[0]).pid().p == pytest.approx(100.0)
+    assert models[3].get_joint(models[3].joint_names()[0]).pid().p == pytest.approx(50.0)
+    assert models[7].get_joint(models[7].joint_names()[0]).pid().p == pytest.approx(gains[0].p)
+    for _ in range(50):
+        assert gazebo.run()
+    q = [m.joint_positions() for m in models]
+    assert q[0] == q[1] == q[2] and q[4] == q[5] == q[6] == q[7]
+    assert q[0] != q[4] and q[3] != q[0] and q[3] != q[4]
     gazebo.close()

@@ -56,6 +56,64 @@ def test_gather_obs_world_order(ws, n):
         assert g == expect
 
 
+def _env_worker(rank, ws, port, n_global, T, q):
+    import sys
+    import numpy as np
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(here, "gym-ignition_amd", "python"))
+    sys.path.insert(0, os.path.join(here, "oracle"))
+    import pyoracle
+    from mwstep import get_model_file
+    from mwstep.shard import gather_obs, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    b, e = shard_range(n_global, rank, ws)
+    task = pyoracle.make_task(pyoracle.TASK_CARTPOLE_DISCRETE, seed=42, max_episode_steps=40)
+    task.world0 = b  # this rank's Philox streams: the global world indices
+    env = pyoracle.VecEnv(pyoracle.load_urdf(get_model_file("cartpole")), task, e - b)
+    env.reset()
+    acts = np.random.default_rng(7).integers(0, 2, size=(T, n_global)).astype(np.int32)
+    for t in range(T):
+        obs, _, _, _ = env.step(acts[t, b:e])
+    g = gather_obs(torch.from_numpy(obs))
+    q.put((rank, g.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws,n", [(2, 64), (3, 50)])
+def test_gather_real_env_slabs(ws, n):
+    """The gathered observations of a sharded batched env (each rank steps
+    its block of worlds, Philox resets keyed by the global world index, 100
+    steps with TimeLimit resets every 40) equal the observations of one env
+    over all worlds, bit for bit -- the property bench.py's final all-gather
+    relies on."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyoracle
+    from mwstep import get_model_file
+    T = 100
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_env_worker, args=(r, ws, port, n, T, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(ws)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    task = pyoracle.make_task(pyoracle.TASK_CARTPOLE_DISCRETE, seed=42, max_episode_steps=40)
+    env = pyoracle.VecEnv(pyoracle.load_urdf(get_model_file("cartpole")), task, n)
+    env.reset()
+    acts = np.random.default_rng(7).integers(0, 2, size=(T, n)).astype(np.int32)
+    for t in range(T):
+        ref, _, _, _ = env.step(acts[t])
+    for _, g in res:
+        assert g.shape == ref.shape and np.array_equal(g, ref)
+
+
 @pytest.mark.parametrize("n,ws", [(4096, 8), (1024, 3), (5, 8)])
 def test_shard_range_partitions(n, ws):
     import sys
