@@ -46,6 +46,10 @@ def test_driver_bench_command(require_gpu):
         assert rl_["peak"] > 0 and rl_["bound"] in ("hbm", "valu-issue"), leg
         assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0, leg
     assert out["pendulum_c3"]["roofline"]["frac"] > 0 and out["panda_c4"]["roofline"]["frac"] > 0
+    # PMC traffic of the config-3 and config-4 kernels (committed FETCH / WRITE passes)
+    assert out["pendulum_c3"]["roofline"]["traffic"] and out["panda_c4"]["roofline"]["traffic"]
+    # the headline roofline is timed on the driver clock (one launch per step)
+    assert rl["time_us_per_launch"] == pytest.approx(out["ms_per_step"] * 1e3, rel=1e-3)
     h = out["humanoid_c5"]
     assert h["constraint_overflow"] == 0 and h["lcp_unconverged_world_steps"] is not None
     assert "exact boxed LCP" in h["workload"] and "PGS" in out["humanoid_c5_pgs_only"]["workload"]
