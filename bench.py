@@ -612,7 +612,7 @@ def panda_leg(args, dev, torch, dist, world_size=1, rank=0, W_global=1024):
     return out
 
 
-def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
+def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True, exact=True):
     """Articulated floating base with contacts (BASELINE
     config 5's machinery on the authored 8-dof quadruped): W quadrupeds
     standing on the ground plane under the JointController PID (Position
@@ -623,9 +623,11 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True):
     rng = np.random.default_rng(args.seed)
     q0 = stand + rng.uniform(-0.1, 0.1, (W, 8))
     out = float_tree_leg(args, dev, torch, "quadruped", W, pgs, 0.45, [(400.0, 10.0, 60.0)] * 8,
-                         q0, np.tile(stand, (W, 1)), rng.uniform(-5, 5, (W, 2)))
+                         q0, np.tile(stand, (W, 1)), rng.uniform(-5, 5, (W, 2)), exact=exact)
+    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: two exact box-QP stages, each from the previous "
+             f"step's solution after at most {pgs} PGS sweeps)" if exact else f"PGS {pgs} iterations")
     out["workload"] = (f"{W} quadrupeds (16 kg, 8 dofs, floating base) standing on a ground plane under "
-                       f"JointController PID hold, sphere-foot / box-trunk contacts, PGS {pgs} iterations, dt = 1 ms")
+                       f"JointController PID hold, sphere-foot / box-trunk contacts, {solve}, dt = 1 ms")
     return out
 
 
@@ -880,8 +882,14 @@ def contact_leg(args, dev, torch):
     elapsed = time.perf_counter() - t0
     steps = n_rep * G
     in_contact = int(sum(len(sim.contacts(w)) > 0 for w in range(0, W, 16)))
+    exact = sim.lcp_solver()[0]
+    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: two exact box-QP stages, each from the previous "
+             "step's solution after at most 20 PGS sweeps)" if exact else "PGS 20 iterations")
     out = {"workload": f"{W} floating cubes (5 kg, 0.2 m) on a ground plane, box-plane contacts, "
-                       "normal + 2 friction rows per point, PGS 20 iterations, dt = 1 ms",
+                       f"normal + 2 friction rows per point, {solve}, dt = 1 ms",
+           "kernel": {0: "free_run_kernel (free_body.hpp, PGS only)", 2: "wave_run_kernel (world per wavefront)"}.get(
+               sim.float_kernel()),
+           "lcp_unconverged_world_steps": int(sim.lcp_unconverged()) if sim.float_kernel() == 2 else None,
            "value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
            "ms_per_step": round(elapsed / steps * 1e3, 6),
            "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),

@@ -629,7 +629,7 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
     if (A.warm) {
         if (A.first && lane < N) warm_reset = warm_reset || S.rflag[static_cast<size_t>(lane) * W + w] != 0;
         warm_reset = __ballot(warm_reset) != 0;
-        for (int e = lane; e < kWaveWarmWords; e += kWaveLanes)
+        for (int e = lane; e < kWaveWarmRecord; e += kWaveLanes)
             L.xw[e] = warm_reset ? 0.f : D.warm[static_cast<size_t>(e) * W + w];
     }
     FreeState base = load_base(D, W, w, A.first);
@@ -706,7 +706,7 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
         if (unconv) atomicAdd(reinterpret_cast<unsigned long long*>(overflow + 2), static_cast<unsigned long long>(unconv));
     }
     if (A.warm)  // also after a paused run: it may have consumed a reset
-        for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) D.warm[static_cast<size_t>(e) * W + w] = L.xw[e];
+        for (int e = lane; e < kWaveWarmRecord; e += kWaveLanes) D.warm[static_cast<size_t>(e) * W + w] = L.xw[e];
     if (want_contacts && !A.paused) {
         if (lane == 0) D.cmask[w] = active;
         if (lane < 32 && ((active >> lane) & 1u)) {

@@ -125,8 +125,9 @@ hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const struct Float
                            const FreeDev& D, const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow,
                            hipStream_t st);
 constexpr int kWaveMaxDepthHost = 12;
-// words of the wave kernel's warm-start record per world (wave_tree.hpp kWaveWarmWords)
-constexpr int kWaveWarmWordsHost = 3 * 32 + 3 * kMaxBodies;
+// words of the wave kernel's warm-start record per world (wave_tree.hpp
+// kWaveWarmRecord: the final impulses, then the exact solve's stage-1 impulses)
+constexpr int kWaveWarmWordsHost = 2 * (3 * 32 + 3 * kMaxBodies);
 // workspace words per world of a floating-tree model, -1 if n is not compiled in
 int float_workspace_words(int n, int n_slots);
 

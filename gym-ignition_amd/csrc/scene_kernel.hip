@@ -1134,10 +1134,12 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 float* Uw = &L.A[0][0];
                 int nsolve = 0, nround = 0, nsolve1 = 0;
                 long long ge_cyc = 0;
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve, nround,
-                                                                nsolve1, ge_cyc)
-                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, Uw, x0, nsolve,
-                                                                          nround, nsolve1, ge_cyc);
+                // both stages start from the sweeps' impulses (no per-stage sweeps)
+                float x1 = x0;
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, 0, 0.f, nullptr, Uw, x1, x0,
+                                                                nsolve, nround, nsolve1, ge_cyc)
+                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, 0, 0.f, nullptr, Uw,
+                                                                          x1, x0, nsolve, nround, nsolve1, ge_cyc);
                 if (!ok && lane == 0) unconv += 1;
                 x0 = Rw.live ? x0 : 0.f;
             }

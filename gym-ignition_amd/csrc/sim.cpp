@@ -523,6 +523,29 @@ int copy_str(const std::string& v, char* buf, int32_t len) {
 
 }  // namespace
 
+namespace {
+
+// the device rows of the per-world record (mw_get_state): {first row, rows},
+// every row W floats
+std::vector<std::pair<float*, int>> state_rows(const mw_sim* s) {
+    std::vector<std::pair<float*, int>> v;
+    if (s->nw) {
+        v.push_back({s->dev.q, 3 * s->n});       // q, qd, qdd
+        v.push_back({s->dev.pid_e, 4 * s->n});   // pid_e, pid_i, pid_u, qlo
+    }
+    if (s->fbase()) v.push_back({s->fdev.base, 13});
+    if (s->d_warm) v.push_back({s->d_warm, mw::kWaveWarmWordsHost});
+    return v;
+}
+
+int state_words(const mw_sim* s) {
+    int k = 0;
+    for (const auto& r : state_rows(s)) k += r.second;
+    return k;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* mw_last_error(void) { return g_last_error.c_str(); }
@@ -586,17 +609,27 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
     } catch (const std::exception& e) {
         return fail(MW_EPARSE, e.what());
     }
+    // DART solves every contact LCP exactly (wave_lcp.hpp, the default
+    // MW_LCP_EXACT): every floating model then steps on the world-per-wavefront
+    // kernel, whatever its size or world count, so the contact answer never
+    // depends on the kernel; a joint-less body is its tree with no joints.  The
+    // PGS-only lane kernels (free_body.hpp, float_tree.hpp) serve MW_LCP_PGS
+    // chosen before mw_load_model (MWSTEP_FREE_KERNEL=1 forces the free-body one)
+    const bool exact = s->lcp_mode == MW_LCP_EXACT;
+    const char* free_kernel = std::getenv("MWSTEP_FREE_KERNEL");
+    const bool free_wave = s->model.floating && s->model.dofs() == 0 && exact &&
+                           !(free_kernel && *free_kernel == '1');
     // Mesh collisions (scene.cpp models them as ground slots at their support
-    // points).  Articulated floating models: every support point becomes a
-    // zero-radius sphere at that point (the same ground contact: normal +z,
-    // depth -z, in slot order).  A joint-less floating body (free-body kernel,
-    // 2 shape entries of 8 slots): the mesh splits into entries of <= 8
-    // points.  Fixed bases never touch the ground here: their meshes are
-    // dropped (counted).
+    // points).  Articulated floating models (and joint-less bodies on the wave
+    // kernel): every support point becomes a zero-radius sphere at that point
+    // (the same ground contact: normal +z, depth -z, in slot order).  A
+    // joint-less floating body on the free-body kernel (2 shape entries of 8
+    // slots): the mesh splits into entries of <= 8 points.  Fixed bases never
+    // touch the ground here: their meshes are dropped (counted).
     {
         int meshes = 0;
-        const bool expand = s->model.floating && s->model.dofs() > 0;
-        const bool free_body = s->model.floating && s->model.dofs() == 0;
+        const bool expand = s->model.floating && (s->model.dofs() > 0 || free_wave);
+        const bool free_body = s->model.floating && s->model.dofs() == 0 && !free_wave;
         auto convert = [&](std::vector<mw::Shape>& v) {
             std::vector<mw::Shape> out;
             for (const mw::Shape& sh : v) {
@@ -645,7 +678,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
         s->fixed_tree = s->model.dofs() > 9 || mw::kernel_topology(parents.data(), s->model.dofs()) < 0;
     }
-    s->float_tree = (s->floating && s->model.dofs() > 0) || s->fixed_tree;
+    s->float_tree = (s->floating && (s->model.dofs() > 0 || free_wave)) || s->fixed_tree;
     if (s->float_tree) {
         std::vector<int> parents;
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
@@ -669,16 +702,17 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         const bool compiled = ((s->topo == 0 && s->n <= 3) || s->topo == 2) &&
                               mw::float_workspace_words(s->n, s->h_float.n_slots) >= 0;
         const char* force_wave = std::getenv("MWSTEP_WAVE_TREE");
-        // small compiled topologies at large world counts take the lane kernel;
-        // up to kWaveWorldsMax worlds the wave kernel is faster (quadruped,
-        // profiles/r01f/quadruped_*_sweep.log: 1024 worlds 62 us/step wave vs
-        // 365 lane, 16384 worlds 638 wave vs 394 lane).  MWSTEP_WAVE_TREE=1 / =0
-        // forces the wave / lane kernel.
+        // with the PGS-only solver, small compiled topologies at large world
+        // counts take the lane kernel; up to kWaveWorldsMax worlds the wave
+        // kernel is faster (quadruped, profiles/r01f/quadruped_*_sweep.log:
+        // 1024 worlds 62 us/step wave vs 365 lane, 16384 worlds 638 wave vs 394
+        // lane).  The exact solve runs on the wave kernel only.
+        // MWSTEP_WAVE_TREE=1 / =0 forces the wave / lane kernel.
         constexpr int kWaveWorldsMax = 4096;
         if (force_wave && *force_wave)
             s->wave = !compiled || *force_wave != '0' || damped;
         else
-            s->wave = !compiled || s->W <= kWaveWorldsMax || damped;
+            s->wave = !compiled || s->W <= kWaveWorldsMax || damped || exact;
         if (s->fixed_tree) s->wave = true;  // the lane kernel has no welded-base mode
         {
             std::vector<int> depth(s->n, 0);
@@ -905,15 +939,18 @@ int mw_initialize(mw_sim* s) {
     s->cmd_off = s->state_bytes;
     s->cmd_bytes = 4 * s->nw * sizeof(float) + 2 * s->nw;
     s->block_bytes = s->state_bytes + s->cmd_bytes;
-    MW_HIP(hipMalloc(&s->d_block, s->block_bytes));
+    // (a joint-less floating body on the wave kernel has no joint arrays:
+    // every allocation keeps a minimal size)
+    auto sz = [](size_t b) { return std::max<size_t>(b, 64); };
+    MW_HIP(hipMalloc(&s->d_block, sz(s->block_bytes)));
     MW_HIP(hipMalloc(&s->d_params, sizeof(mw::ChainF)));
-    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_aux), 5 * s->nw * sizeof(float)));
+    MW_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_aux), sz(5 * s->nw * sizeof(float))));
     MW_HIP(hipMemsetAsync(s->d_aux, 0, 5 * s->nw * sizeof(float), s->stream));
-    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ptgt), s->nw * sizeof(float), hipHostMallocDefault));
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_ptgt), sz(s->nw * sizeof(float)), hipHostMallocDefault));
     std::memset(s->h_ptgt, 0, s->nw * sizeof(float));
-    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_block), s->block_bytes, hipHostMallocDefault));
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_block), sz(s->block_bytes), hipHostMallocDefault));
     std::memset(s->h_block, 0, s->block_bytes);
-    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_stage), s->cmd_bytes + s->nw * sizeof(float),
+    MW_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_stage), sz(s->cmd_bytes + s->nw * sizeof(float)),
                          hipHostMallocDefault));
     MW_HIP(hipEventCreateWithFlags(&s->stage_ev, hipEventDisableTiming));
     float* base = reinterpret_cast<float*>(s->d_block);
@@ -1805,6 +1842,9 @@ int mw_set_lcp_solver(mw_sim* s, int32_t mode, int32_t max_solves) {
     if (mode != MW_LCP_PGS && mode != MW_LCP_EXACT) return fail(MW_EINVAL, "unknown LCP solver mode");
     if (mode == MW_LCP_EXACT && (max_solves < 1 || max_solves > 256))
         return fail(MW_EINVAL, "the exact solve's budget must be 1..256 linear solves per step");
+    if (mode == MW_LCP_EXACT && s->loaded && s->floating && !s->wave)
+        return fail(MW_ESTATE, "this model was loaded for the PGS-only lane kernel: select MW_LCP_EXACT before "
+                               "mw_load_model (the exact solve runs on the world-per-wavefront kernel)");
     s->lcp_mode = mode;
     s->lcp_solves = (mode == MW_LCP_EXACT) ? max_solves : 0;
     return MW_OK;
@@ -1812,8 +1852,10 @@ int mw_set_lcp_solver(mw_sim* s, int32_t mode, int32_t max_solves) {
 
 int mw_lcp_solver(const mw_sim* s, int32_t* mode, int32_t* max_solves) {
     if (!s || !mode || !max_solves) return fail(MW_EINVAL, "null argument");
-    *mode = s->lcp_mode;
-    *max_solves = s->lcp_solves;
+    // a floating model on a lane kernel runs the PGS sweeps only
+    const bool pgs_kernel = s->loaded && s->floating && !s->wave;
+    *mode = pgs_kernel ? MW_LCP_PGS : s->lcp_mode;
+    *max_solves = pgs_kernel ? 0 : s->lcp_solves;
     return MW_OK;
 }
 
@@ -1953,29 +1995,6 @@ int mw_clear_diverged(mw_sim* s, int32_t w0, int32_t nw) {
     if (nw) MW_HIP(hipMemsetAsync(s->dev.div + w0, 0, nw, s->stream));
     return MW_OK;
 }
-
-namespace {
-
-// the device rows of the per-world record (mw_get_state): {first row, rows},
-// every row W floats
-std::vector<std::pair<float*, int>> state_rows(const mw_sim* s) {
-    std::vector<std::pair<float*, int>> v;
-    if (s->nw) {
-        v.push_back({s->dev.q, 3 * s->n});       // q, qd, qdd
-        v.push_back({s->dev.pid_e, 4 * s->n});   // pid_e, pid_i, pid_u, qlo
-    }
-    if (s->fbase()) v.push_back({s->fdev.base, 13});
-    if (s->d_warm) v.push_back({s->d_warm, mw::kWaveWarmWordsHost});
-    return v;
-}
-
-int state_words(const mw_sim* s) {
-    int k = 0;
-    for (const auto& r : state_rows(s)) k += r.second;
-    return k;
-}
-
-}  // namespace
 
 int mw_state_words(const mw_sim* s, int32_t* words) {
     int rc = check_sim(s);

@@ -1,31 +1,38 @@
 // wave_lcp.hpp -- exact solve of the world-per-wavefront kernel's boxed LCP
-// (contact normal rows x_n >= 0, friction rows |x_t| <= mu x_n, joint rows in
-// [lo, hi]), the problem DART's primary boxed-LCP solver (Dantzig pivoting,
-// BoxedLcpConstraintSolver [EXT], reached from ForwardStep at
-// /root/reference/cpp/scenario/plugins/Physics/Physics.cpp:1824-1835) solves
-// exactly.  Specification: oracle.c lcp_refine / boxqp_solve (the fixed point
-// of the friction boxes with the box QP of every round solved exactly).
+// (contact normal rows x_n >= 0, friction rows boxed by mu x_n, joint rows in
+// [lo, hi]) as DART solves it: BoxedLcpConstraintSolver -> DantzigBoxedLcpSolver
+// -> ODE's dSolveLCP [EXT: dart/external/odelcpsolver], reached from
+// ForwardStep at /root/reference/cpp/scenario/plugins/Physics/Physics.cpp:1824-1835.
+// ODE's friction-index handling moves the friction rows to the end, solves
+// the other rows first and, on reaching the first friction row, sets every
+// friction box once to +-mu x_n from the normals solved so far.  A is
+// symmetric positive definite (the CFM), so the result is the unique pair of
+// strictly convex box-QP minimisers (specification: oracle.c lcp_dantzig):
+//
+//   stage 1  the normal and joint rows, friction impulses pinned at 0;
+//   stage 2  all rows, every friction row boxed by +-mu x_n of its contact's
+//            STAGE-1 normal (fixed during the stage).
 //
 // Lane r owns row r: its Delassus row a[c] = A[r][c] (the PGS registers of
-// wave_step), its impulse x_r and its row data.  After the PGS sweeps:
+// wave_step), its impulse x_r and its row data.  Each stage is a box QP with
+// fixed bounds, solved from the PGS impulses / the previous stage by
 //
-//   1. semismooth Newton rounds on the coupled conditions: a row is held at
-//      a bound when its gradient g = A x - b pushes it outward, a friction row
-//      held at +-mu x_n moves with its normal (d_t = +-mu d_n), every other
-//      row is free; the Newton system (free rows, coupled columns folded into
-//      their normal's column) is solved by Gaussian elimination with partial
-//      pivoting over the lanes; the step is accepted only when it lowers the
-//      largest complementarity residual (halved up to 3 times);
-//   2. if a round fails, the oracle's own method: friction boxes frozen at the
-//      current normals, the box QP solved by the primal active-set method
-//      (one bound joins or leaves the working set per step), the boxes
-//      updated, until they stop moving;
+//   1. semismooth Newton (primal-dual active set): a row is held at a bound
+//      when its gradient g = A x - b pushes it outward, the rest are free; the
+//      reduced system A_FF d_F = -g_F is symmetric positive definite and is
+//      eliminated in lane order without a pivot search; the step is accepted
+//      when it lowers the largest complementarity residual (halved up to 3
+//      times), with the residual b - A x accumulated compensated (Dot2);
+//   2. if a Newton step cannot lower it: the primal active-set method (one
+//      bound joins or leaves the working set per linear solve), which is
+//      monotone and finite for a strictly convex QP,
 //
-// within a budget of linear solves per step.  Converged = every row's
-// complementarity residual (oracle lcp_residual, velocity units) within fp32
-// round-off of its own terms.  A world that runs out of budget keeps its
-// current impulses projected onto the boxes of its current normals (feasible:
-// x_n >= 0, |x_t| <= mu x_n, box rows in [lo, hi]) and is counted.
+// within a budget of linear solves per world-step (both stages).  Converged =
+// every row's complementarity residual (oracle lcp_residual, velocity units)
+// within fp32 round-off of its own terms, in both stages.  A world that runs
+// out of budget keeps iterates that never leave the boxes of their stage
+// (x_n >= 0, box rows in [lo, hi], friction within +-mu x_n of the stage-1
+// normal) and is counted.
 #pragma once
 
 namespace mw {
@@ -33,13 +40,7 @@ namespace dev {
 
 constexpr float kLcpRelTol = 4e-6f;   // residual <= kLcpRelTol (|b| + sum |A_rc x_c|) + kLcpAbsTol
 constexpr float kLcpAbsTol = 1e-7f;   // m/s or rad/s
-constexpr int kLcpLineSearch = 3;     // step halvings of a Newton round
-// A residual within kLcpLoose x the tolerance is accepted after one more
-// linear solve (the polish round) whatever that round reaches: the last
-// decade costs the redundant-corner standing LCPs (conditioned ~1e7 by the
-// CFM) many active-set rounds, while the joint velocities follow the
-// residual / sqrt(CFM) and want the tight tolerance after impacts
-constexpr float kLcpLoose = 10.f;
+constexpr int kLcpLineSearch = 3;     // step halvings of a Newton step
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
 // ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
@@ -103,19 +104,29 @@ struct LcpRow {
     bool live;  // r < n
 };
 
-// w_r = sum_c A[r][c] x_c and mag = sum_c |A[r][c] x_c| (round-off scale)
+// w_r = sum_c A[r][c] x_c, compensated (Ogita-Rump-Oishi Dot2: the product
+// error by an FMA, the sum error by TwoSum, both carried in c), and
+// mag = sum_c |A[r][c] x_c| (the round-off scale of the residual test).  A
+// plain fp32 sum errs by ~R eps mag, a sizeable share of the tolerance, so
+// the last Newton steps would chase the matvec's own rounding.
 template <int RC>
 __device__ __forceinline__ float lcp_matvec(const float (&a)[kWaveMaxRows], float xl, int n, float& mag) {
-    float w = 0.f, m = 0.f;
+#pragma clang fp contract(off)
+    float w = 0.f, c = 0.f, m = 0.f;
 #pragma unroll
-    for (int c = 0; c < RC; ++c) {
-        if ((c & 7) == 0 && c >= n) break;
-        const float t = a[c] * read_lane(xl, c);
-        w += t;
-        m += fabsf(t);
+    for (int k = 0; k < RC; ++k) {
+        if ((k & 7) == 0 && k >= n) break;
+        const float xk = read_lane(xl, k);
+        const float p = a[k] * xk;
+        const float pe = fmaf(a[k], xk, -p);
+        const float t = w + p;
+        const float z = t - w;
+        c += ((w - (t - z)) + (p - z)) + pe;
+        w = t;
+        m += fabsf(p);
     }
     mag = m;
-    return w;
+    return w + c;
 }
 
 // v of the row's contact normal (friction rows; every other row: its own v),
@@ -132,24 +143,15 @@ __device__ __forceinline__ float gather_normal(float v, const LcpRow& R, int n) 
     return out;
 }
 
-// box of row r at the lane-distributed impulses xl (friction: [-mu x_n, mu x_n])
-template <int RC>
-__device__ __forceinline__ void lcp_bounds(const LcpRow& R, float xl, float mu, int n, float& L, float& U) {
-    const float xn = gather_normal<RC>(xl, R, n);
-    const float u = mu * fmaxf(xn, 0.f);
-    L = (R.kind == 1) ? -u : R.lo;
-    U = (R.kind == 1) ? u : R.hi;
-}
-
-// complementarity residual of row r (oracle lcp_residual, velocity units),
-// relative to its round-off scale: <= 1 is converged
-__device__ __forceinline__ float lcp_row_residual(const LcpRow& R, float xl, float w, float mag, float arr, float L,
+// complementarity residual of a row with box [L, U] (oracle lcp_residual,
+// velocity units), relative to its round-off scale: <= 1 is converged
+__device__ __forceinline__ float lcp_row_residual(bool live, float b, float xl, float w, float mag, float arr, float L,
                                                   float U, float tolx, float& e_abs) {
-    if (!R.live) {
+    if (!live) {
         e_abs = 0.f;
         return 0.f;
     }
-    const float s = R.b - w;
+    const float s = b - w;
     float e;
     if (xl < L - tolx || xl > U + tolx)
         e = ((xl < L) ? (L - xl) : (xl - U)) * arr;
@@ -162,7 +164,7 @@ __device__ __forceinline__ float lcp_row_residual(const LcpRow& R, float xl, flo
     else
         e = fabsf(s);
     e_abs = e;
-    return e * rcp(kLcpRelTol * (fabsf(R.b) + mag) + kLcpAbsTol);
+    return e * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol);
 }
 
 // Gaussian elimination with partial pivoting, lane = row: k[c] = K[lane][c],
@@ -245,154 +247,79 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
     return dl;
 }
 
-// The exact solve.  xl: lane r's impulse from the PGS (feasible), returned
-// solved.  a: the Delassus registers (a[c] = A[lane][c], CFM included).
-// Returns true when converged within max_solves linear solves.
+// One strictly convex box QP  min 1/2 x'Ax - b'x,  L <= x <= U  (bounds fixed,
+// per lane; a dead or pinned row has L = U), from x (inside the box): the
+// semismooth Newton steps of the header, then the primal active-set method.
+// solves counts the linear solves against `budget`.  Returns true when every
+// row's residual is within tolerance.
 template <int RC>
-__device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
-                                               int max_solves, float* __restrict__ Uw, float& xl, int& n_solves,
-                                               int& n_rounds, int& n_solves_staggered, long long& ge_cycles) {
+__device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
+                                           float arr, int n, int budget, float* __restrict__ Uw, float& xl, int& solves,
+                                           int& iters, long long& ge_cycles) {
     const int lane = lane_id();
-    float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
-#pragma unroll
-    for (int c = 0; c < RC; ++c) arr = (lane == c && R.live) ? a[c] : arr;
-    int solves = 0, solves1 = 0;
-    bool converged = false;
-    int phase = 0;          // 0 semismooth Newton, 1 staggered active set (oracle lcp_refine)
-    int ws = 0;             // phase 1 working set: 0 free, 1 held at L, 2 held at U
-    float Lf = 0.f, Uf = 0.f, prev = 0.f;  // phase 1: the round's frozen box, the round's start
-    bool at_min = false, new_round = true;
-    bool polish = false;  // inside the loose band: one more solve, then accept
-    int polish_at = 0;
-    int iter = 0;
-    for (; iter < 4 * max_solves + 8; ++iter) {
+    const bool pinned = !live || U - L <= 0.f;
+    int phase = 0;         // 0 semismooth Newton, 1 primal active set
+    int ws = 0;            // phase 1 working set: 0 free, 1 held at L, 2 held at U
+    bool at_min = false;   // phase 1: the last step reached the working set's minimiser
+    for (int it = 0; it < 4 * budget + 8; ++it, ++iters) {
         float mag;
         const float w = lcp_matvec<RC>(a, xl, n, mag);
-        const float g = w - R.b;
-        float L, U;
-        lcp_bounds<RC>(R, xl, mu, n, L, U);
-        const float xmax = wave_fmax(R.live ? fabsf(xl) : 0.f);
+        const float g = w - b;
+        const float xmax = wave_fmax(live ? fabsf(xl) : 0.f);
         const float tolx = 2e-6f * (1.f + xmax);
         float e_abs;
-        const float rel = wave_fmax(lcp_row_residual(R, xl, w, mag, arr, L, U, tolx, e_abs));
-        if (rel <= 1.f || (polish && rel <= kLcpLoose && solves > polish_at)) {
-            converged = true;
-            break;
-        }
-        if (rel > kLcpLoose) {
-            polish = false;
-        } else if (!polish) {
-            polish = true;  // the next linear solve is the polish round
-            polish_at = solves;
-        }
-        if (solves >= max_solves) break;
-        if (phase == 1 && new_round) {
-            // a round of lcp_refine: boxes frozen at the current normals
-            new_round = false;
-            Lf = L;
-            Uf = U;
-            prev = xl;
-            if (xl <= Lf) { xl = Lf; ws = 1; }
-            else if (xl >= Uf) { xl = Uf; ws = 2; }
-            else ws = 0;
-            if (Lf == Uf || !R.live) ws = 1;
-            at_min = false;
-            continue;  // re-evaluate at the clamped start
-        }
+        const float rel = wave_fmax(lcp_row_residual(live, b, xl, w, mag, arr, L, U, tolx, e_abs));
+        if (rel <= 1.f) return true;
         if (phase == 1 && at_min) {
-            // boxqp_solve: minimiser on the working set -> release the worst multiplier
+            // minimiser on the working set: release the bound with the worst
+            // multiplier; if none is wrongly signed, the free rows' residual is
+            // the fp32 solve's own error -- one more solve on the same working
+            // set from the compensated residual refines it (iterative refinement)
             at_min = false;
             float v = (ws == 1) ? -g : ((ws == 2) ? g : 0.f);
-            v = (Lf == Uf || !R.live) ? 0.f : v;
-            const float gm = wave_fmax(R.live ? fabsf(g) : 0.f);
+            v = pinned ? 0.f : v;
+            const float gm = wave_fmax(live ? fabsf(g) : 0.f);
             const int worst = wave_argmax(v);
-            if (read_lane(v, worst) <= kLcpRelTol * (1.f + gm)) {
-                // the round's QP is solved: the next round on the updated boxes
-                if (wave_fmax(fabsf(xl - prev)) <= tolx) break;  // fixed point at the round-off floor
-                new_round = true;
-            } else if (lane == worst) {
-                ws = 0;
+            if (read_lane(v, worst) > kLcpRelTol * (1.f + gm)) {
+                if (lane == worst) ws = 0;
+                continue;
             }
-            continue;
         }
-        // ---- one linear solve: the Newton system of this round ----
-        float k[RC];
+        if (solves >= budget) return false;
+        // ---- one linear solve over the free rows (SPD: no pivot search)
         bool fr;
-        bool pivot = false;  // only a folded friction column makes the system unsymmetric
-        float coup = 0.f;  // phase 0: d_t = coup d_n of a friction row held at +-mu x_n
-        const float emax = wave_fmax(e_abs);
         if (phase == 0) {
-            // a row is held when its gradient pushes it out of its box; a
-            // friction row on its box edge moves with its normal
-            bool fixed = !R.live;
-            if (R.kind == 0) fixed = fixed || (xl <= 0.f && g >= 0.f);
-            if (R.kind == 2) fixed = fixed || (xl <= R.lo && g >= 0.f) || (xl >= R.hi && g <= 0.f);
-            const bool nfixed = mask_bit(static_cast<uint64_t>(__ballot(fixed)), R.nrow);
-            bool cpos = false, cneg = false;
-            if (R.kind == 1 && R.live && !fixed) {
-                if (nfixed) {
-                    fixed = true;
-                } else if (U <= 0.f) {
-                    // a contact opening from x_n = 0: its friction rows start on the
-                    // pyramid edge they push towards (sliding); a zero gradient stays
-                    if (g < 0.f) cpos = true;
-                    else if (g > 0.f) cneg = true;
-                    else fixed = true;
-                } else if (xl >= U && g <= 0.f) {
-                    cpos = true;
-                } else if (xl <= L && g >= 0.f) {
-                    cneg = true;
-                }
-            }
-            fr = R.live && !fixed && !cpos && !cneg;
-            coup = cpos ? mu : (cneg ? -mu : 0.f);
-            const uint64_t freeM = __ballot(fr), cpM = __ballot(cpos), cnM = __ballot(cneg);
-#pragma unroll
-            for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
-            // x_t = +-mu x_n: the held friction column folds into its normal's
-            pivot = (cpM | cnM) != 0ull;
-            if (pivot) {
-#pragma unroll
-                for (int c = 0; c + 2 < RC; c += 3) {
-                    const float s1 = (mask_bit(cpM, c + 1) ? 1.f : 0.f) - (mask_bit(cnM, c + 1) ? 1.f : 0.f);
-                    const float s2 = (mask_bit(cpM, c + 2) ? 1.f : 0.f) - (mask_bit(cnM, c + 2) ? 1.f : 0.f);
-                    if (fr) k[c] += mu * (s1 * a[c + 1] + s2 * a[c + 2]);
-                }
-            }
+            const bool held = pinned || (xl <= L && g >= 0.f) || (xl >= U && g <= 0.f);
+            fr = !held;
         } else {
-            fr = R.live && ws == 0;
-            const uint64_t freeM = __ballot(fr);
-#pragma unroll
-            for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
+            fr = !pinned && ws == 0;
         }
+        const uint64_t freeM = __ballot(fr);
+        float k[RC];
+#pragma unroll
+        for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
 #ifdef MW_WAVE_PROF
         const long long tg0 = clock64();
 #endif
-        float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, pivot);
+        const float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, false);
 #ifdef MW_WAVE_PROF
         ge_cycles += clock64() - tg0;
+#else
+        (void)ge_cycles;
 #endif
         ++solves;
-        solves1 += phase;
         if (phase == 0) {
-            const float dn = gather_normal<RC>(d, R, n);
-            d = fr ? d : coup * dn;
-            // monotone line search on the largest residual
+            // monotone line search on the largest residual, iterates kept in the box
+            const float emax = wave_fmax(e_abs);
             bool accepted = false;
             float step = 1.f;
             for (int ls = 0; ls <= kLcpLineSearch; ++ls, step *= 0.5f) {
-                float xt = xl + step * d;
-                if (R.kind == 0) xt = fmaxf(xt, 0.f);
-                if (R.kind == 2) xt = fminf(fmaxf(xt, R.lo), R.hi);
-                float Lt, Ut;
-                lcp_bounds<RC>(R, xt, mu, n, Lt, Ut);  // the friction boxes of the projected normals
-                if (R.kind == 1) xt = fminf(fmaxf(xt, Lt), Ut);
-                xt = R.live ? xt : 0.f;
+                const float xt = live ? fminf(fmaxf(xl + step * d, L), U) : xl;
                 float mt;
                 const float wt = lcp_matvec<RC>(a, xt, n, mt);
-                const float xmt = wave_fmax(R.live ? fabsf(xt) : 0.f);
+                const float xmt = wave_fmax(live ? fabsf(xt) : 0.f);
                 float et;
-                (void)lcp_row_residual(R, xt, wt, mt, arr, Lt, Ut, 2e-6f * (1.f + xmt), et);
+                (void)lcp_row_residual(live, b, xt, wt, mt, arr, L, U, 2e-6f * (1.f + xmt), et);
                 if (wave_fmax(et) < emax) {
                     xl = xt;
                     accepted = true;
@@ -400,12 +327,14 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
                 }
             }
             if (!accepted) {
+                // the primal active-set method from here: working set = rows at a bound
                 phase = 1;
-                new_round = true;
+                ws = pinned ? 1 : ((xl <= L) ? 1 : ((xl >= U) ? 2 : 0));
+                at_min = false;
             }
             continue;
         }
-        // boxqp_solve step: the longest feasible step along d (at most 1)
+        // primal active set: the longest feasible step along d (at most 1)
         const float dmax = wave_fmax(fabsf(d));
         if (dmax <= 1e-7f * (1.f + xmax)) {
             at_min = true;
@@ -413,8 +342,8 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
         }
         float al = 1.f;
         int side = 0;
-        if (fr && d < 0.f && xl + d < Lf) { al = (Lf - xl) * rcp(d); side = 1; }
-        else if (fr && d > 0.f && xl + d > Uf) { al = (Uf - xl) * rcp(d); side = 2; }
+        if (fr && d < 0.f && xl + d < L) { al = (L - xl) * rcp(d); side = 1; }
+        else if (fr && d > 0.f && xl + d > U) { al = (U - xl) * rcp(d); side = 2; }
         al = fmaxf(al, 0.f);
         const float amin = wave_fmin(al);
         if (amin < 1.f) {
@@ -422,7 +351,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
             const int bside = __builtin_amdgcn_readlane(side, block);
             xl = fr ? xl + amin * d : xl;
             if (lane == block) {
-                xl = (bside == 1) ? Lf : Uf;
+                xl = (bside == 1) ? L : U;
                 ws = bside;
             }
         } else {
@@ -430,24 +359,99 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
             at_min = true;
         }
     }
-    if (!converged) {
-        // out of budget: inside a staggered round the friction rows keep to the
-        // round's boxes, frozen at its starting normals, while the normals may
-        // have shrunk since -- project onto the boxes of the current impulses
-        // (normals >= 0, box rows in [lo, hi], |x_t| <= mu x_n) so the impulses
-        // handed back are feasible
-        float xp = xl;
-        if (R.kind == 0) xp = fmaxf(xp, 0.f);
-        if (R.kind == 2) xp = fminf(fmaxf(xp, R.lo), R.hi);
-        float Lp, Up;
-        lcp_bounds<RC>(R, xp, mu, n, Lp, Up);
-        if (R.kind == 1) xp = fminf(fmaxf(xp, Lp), Up);
-        xl = R.live ? xp : 0.f;
+    return false;
+}
+
+// Projected Gauss-Seidel sweeps on a box problem with fixed per-row bounds
+// (the starting point of a stage's exact solve): row constants {b, 1/A_rr,
+// L, U} through the LDS array rc (lane r writes row r; rows >= n inert),
+// impulses uniform in registers, the residual w_c = (A x)_c distributed over
+// the lanes and updated by one column per row (wave_step's PGS without the
+// friction coupling).  Ends once a sweep moves no constraint velocity by more
+// than tol.  x: lane r's impulse, in and out.
+template <int RC>
+__device__ __forceinline__ void wave_pgs_box(const float (&a)[kWaveMaxRows], F4* __restrict__ rc, bool live, float b,
+                                             float arr, float L, float U, int n, int sweeps, float tol, float& xl) {
+    const int lane = lane_id();
+    const int npad = (n + 7) & ~7;
+    if (lane < npad) rc[lane] = live ? F4{b, rcp(arr), L, U} : F4{0.f, 0.f, 0.f, 0.f};
+    wave_lds_sync();
+    float xu[RC];
+#pragma unroll
+    for (int r = 0; r < RC; ++r) xu[r] = read_lane(xl, r);
+    for (int it = 0; it < sweeps; ++it) {
+        float w = 0.f;
+#pragma unroll
+        for (int rb = 0; rb < RC; rb += 8) {
+            if (rb >= npad) break;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w += a[rb + k] * xu[rb + k];
+        }
+        const float w_start = w;
+#pragma unroll
+        for (int rb = 0; rb < RC; rb += 8) {
+            if (rb >= npad) break;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = rb + k;
+                const F4 c = rc[r];
+                const float xb = fmaf(c.x, c.y, xu[r]);
+                const float wpre = fmaf(-a[r], xu[r], w);
+                const float v = clamp_ordered(fmaf(-read_lane(w, r), c.y, xb), c.z, c.w);
+                w = fmaf(a[r], v, wpre);
+                xu[r] = v;
+            }
+        }
+        if (wave_fmax(fabsf(w - w_start)) <= tol) break;
     }
+    float xo = xl;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) xo = (lane == r) ? xu[r] : xo;
+    xl = live ? xo : 0.f;
+}
+
+// The exact solve, DART's two stages (header).  x1: lane r's stage-1 impulse
+// of the previous step (start of stage 1), returned as this step's stage-1
+// solution; xl: the previous step's final impulse (start of the friction
+// rows in stage 2), returned solved.  sweeps > 0: up to that many PGS sweeps
+// (tolerance exit pgs_tol) on each stage's box problem before its exact solve
+// (rc: the LDS row-constant array they use).  a: the Delassus registers
+// (a[c] = A[lane][c], CFM included).  Returns true when both stages
+// converged within max_solves linear solves in total; n_solves / n_rounds /
+// n_solves2: linear solves, iterations, linear solves of stage 2.
+template <int RC>
+__device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
+                                               int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
+                                               float* __restrict__ Uw, float& x1, float& xl, int& n_solves,
+                                               int& n_rounds, int& n_solves2, long long& ge_cycles) {
+    const int lane = lane_id();
+    float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
+#pragma unroll
+    for (int c = 0; c < RC; ++c) arr = (lane == c && R.live) ? a[c] : arr;
+    int solves = 0, iters = 0;
+    const bool fric = R.kind == 1;
+    // stage 1: normal and joint rows; friction impulses pinned at 0
+    float L = (fric || !R.live) ? 0.f : R.lo;
+    float U = (fric || !R.live) ? 0.f : R.hi;
+    float x = fminf(fmaxf(x1, L), U);
+    if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L, U, n, sweeps, pgs_tol, x);
+    const bool ok1 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, solves, iters, ge_cycles);
+    x1 = R.live ? x : 0.f;
+    const int s1 = solves;
+    // stage 2: each friction row boxed by mu x_n of its contact's stage-1 normal
+    const float xn1 = gather_normal<RC>(x, R, n);
+    if (fric && R.live) {
+        U = mu * fmaxf(xn1, 0.f);
+        L = -U;
+        x = fminf(fmaxf(xl, L), U);
+    }
+    if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L, U, n, sweeps, pgs_tol, x);
+    const bool ok2 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, solves, iters, ge_cycles);
+    xl = R.live ? x : 0.f;
     n_solves = solves;
-    n_rounds = iter;
-    n_solves_staggered = solves1;
-    return converged;
+    n_rounds = iters;
+    n_solves2 = solves - s1;
+    return ok1 && ok2;
 }
 
 }  // namespace dev

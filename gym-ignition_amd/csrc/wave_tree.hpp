@@ -39,6 +39,9 @@ constexpr int kWaveMaxDepth = 12;
 // limit, servo, Coulomb) -- oracle.h OR_WARM_* (its slot capacity is larger)
 constexpr int kWaveWarmJoint0 = 3 * kMaxFloatSlots;
 constexpr int kWaveWarmWords = kWaveWarmJoint0 + 3 * kMaxBodies;
+// the record holds two such blocks: the final impulses, then the exact
+// solve's stage-1 impulses (wave_lcp.hpp: DART's frictionless first stage)
+constexpr int kWaveWarmRecord = 2 * kWaveWarmWords;
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 
@@ -97,7 +100,7 @@ struct WaveWorld {
     float s_x[kMaxFloatSlots][3];   // impulses (output)
     // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
     alignas(16) float stack[kWaveMaxDepth][7][kWaveLanes];
-    float xw[kWaveWarmWords];    // warm-start impulses (RunArgs::warm)
+    float xw[kWaveWarmRecord];   // warm-start impulses (RunArgs::warm): final, then stage 1
 };
 
 __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63u); }
@@ -693,23 +696,21 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         const float mu = F->mu;
         float x[kWaveMaxRows];
         // warm start: every row from the previous step's impulse of the same
-        // row identity (contact slot / joint row), else 0
-        float x0 = 0.f;
+        // row identity (contact slot / joint row), else 0; x1w: its stage-1
+        // impulse (exact solve)
+        float x0 = 0.f, x1w = 0.f;
+        const int wid = (lane < R) ? ((L.src[lane] < kJointRow) ? L.src[lane]
+                                                                 : kWaveWarmJoint0 + (L.src[lane] - kJointRow))
+                                   : 0;
         if (warm && lane < R) {
-            const int src = L.src[lane];
-            x0 = L.xw[(src < kJointRow) ? src : kWaveWarmJoint0 + (src - kJointRow)];
+            x0 = L.xw[wid];
+            x1w = L.xw[kWaveWarmWords + wid];
         }
-#pragma unroll
-        for (int r = 0; r < kWaveMaxRows; ++r) x[r] = warm ? read_lane(x0, r) : 0.f;
-        if (pgs_tol > 0.f)
-            wave_pgs<MAXN, true>(L, a, x, Rpad, ncr, mu, pgs_iters, pgs_tol);
-        else
-            wave_pgs<MAXN, false>(L, a, x, Rpad, ncr, mu, pgs_iters, 0.f);
-        MW_PROF_T(t45);
-        MW_PROF_ACC(15, t4, t45);
+        float x1s = 0.f;  // this step's stage-1 impulse (exact solve)
         if (lcp_solves > 0) {
-            // exact boxed LCP from the PGS impulses (wave_lcp.hpp; oracle
-            // OR_PGS_CONVERGED): lane r = row r
+            // DART's boxed LCP (wave_lcp.hpp; oracle OR_PGS_CONVERGED): lane r =
+            // row r, each of its two stages from the previous step's solution,
+            // then PGS sweeps on the stage's box problem, then the exact solve
             LcpRow Rw;
             Rw.live = lane < R;
             const F4 c = L.rc[lane < Rpad ? lane : 0];
@@ -718,18 +719,17 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             Rw.b = Rw.live ? c.x : 0.f;
             Rw.lo = Rw.live ? c.z : 0.f;
             Rw.hi = Rw.live ? c.w : 0.f;
-            float xe = 0.f;
-#pragma unroll
-            for (int r = 0; r < kWaveMaxRows; ++r) xe = (lane == r && r < R) ? x[r] : xe;
+            float xe = x0;
+            x1s = x1w;
             // the elimination's pivot rows go to the responses' stack (dead here)
             static_assert(sizeof(L.stack) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
             float* U = &L.stack[0][0][0];
             int nsolve = 0, nround = 0, nsolve1 = 0;
             long long ge_cyc = 0;
-            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround, nsolve1,
-                                                           ge_cyc)
-                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, U, xe, nsolve, nround,
-                                                                     nsolve1, ge_cyc);
+            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
+                                                           nsolve, nround, nsolve1, ge_cyc)
+                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
+                                                                     L.rc, U, x1s, xe, nsolve, nround, nsolve1, ge_cyc);
 #ifdef MW_WAVE_PROF
             prof[8] += static_cast<unsigned long long>(nsolve);
             prof[9] += static_cast<unsigned long long>(nround);
@@ -748,6 +748,17 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                 x[r] = read_lane(xe, r);
             }
             if (!ok) MW_LANE0 { *unconverged += 1; }
+            MW_PROF_T(t45);
+            MW_PROF_ACC(15, t4, t45);
+        } else {
+#pragma unroll
+            for (int r = 0; r < kWaveMaxRows; ++r) x[r] = warm ? read_lane(x0, r) : 0.f;
+            if (pgs_tol > 0.f)
+                wave_pgs<MAXN, true>(L, a, x, Rpad, ncr, mu, pgs_iters, pgs_tol);
+            else
+                wave_pgs<MAXN, false>(L, a, x, Rpad, ncr, mu, pgs_iters, 0.f);
+            MW_PROF_T(t45);
+            MW_PROF_ACC(15, t4, t45);
         }
         MW_PROF_T(t5);
         MW_PROF_ACC(5, t4, t5);
@@ -769,14 +780,15 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         }
         if (lane < NV) L.nu[lane] += dnu;
         if (warm) {
-            for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) L.xw[e] = 0.f;
+            for (int e = lane; e < kWaveWarmRecord; e += kWaveLanes) L.xw[e] = 0.f;
+            wave_lds_sync();
             if (lane < R) {
-                const int src = L.src[lane];
-                L.xw[(src < kJointRow) ? src : kWaveWarmJoint0 + (src - kJointRow)] = xl;
+                L.xw[wid] = xl;
+                L.xw[kWaveWarmWords + wid] = x1s;
             }
         }
     } else if (warm) {
-        for (int e = lane; e < kWaveWarmWords; e += kWaveLanes) L.xw[e] = 0.f;
+        for (int e = lane; e < kWaveWarmRecord; e += kWaveLanes) L.xw[e] = 0.f;
     }
 
     // ---- integratePositions ---------------------------------------------------

@@ -24,7 +24,7 @@ class Simulator:
                  pose: Sequence[float] = (0, 0, 0, 1, 0, 0, 0), name: str = "",
                  pgs_iters: int = 20, gravity: Optional[Sequence[float]] = None,
                  stream: Optional[int] = None, joint_params: Optional[dict] = None,
-                 cache_reads: bool = False):
+                 cache_reads: bool = False, lcp_exact: Optional[bool] = None):
         L = N.lib()
         cfg = N.MwConfig(step_size, rtf, steps_per_run, n_worlds, device, pgs_iters)
         h = ctypes.c_void_p()
@@ -40,6 +40,10 @@ class Simulator:
         self._cache_reads = cache_reads
         self._cache: dict = {}
         try:
+            if lcp_exact is not None:
+                # the solver picks the kernel of a floating model at load time:
+                # exact (default) -> world-per-wavefront, PGS -> the lane kernels
+                N.check(L.mw_set_lcp_solver(h, N.LCP_EXACT if lcp_exact else N.LCP_PGS, 24), "mw_set_lcp_solver")
             p = np.ascontiguousarray(pose, dtype=np.float64)
             N.check(L.mw_load_model(h, model.encode(), N.dptr(p), name.encode()), "mw_load_model")
             if gravity is not None:

@@ -235,19 +235,23 @@ int mw_reset_base_velocity(mw_sim* sim, int32_t w0, int32_t nw, const double* li
  * (they have no warm-start record). */
 int mw_set_pgs_options(mw_sim* sim, double tol, int32_t warm_start);
 int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
-/* The boxed-LCP solver of the world-per-wavefront kernel.  MW_LCP_EXACT
- * (default, max_solves 24): after the PGS sweeps, the LCP is solved exactly
- * -- semismooth Newton rounds on the coupled friction conditions, then the
- * active-set method of the box QP with the friction boxes updated to their
- * fixed point -- with at most max_solves dense linear solves (Gaussian
- * elimination over the wave's lanes) per world-step; DART's primary solver is
- * Dantzig's exact pivoting method [EXT], reached from ForwardStep
- * (Physics.cpp:1824-1835).  In exact mode the sweeps always start from the
- * previous step's impulses of the same contact slot / joint row and end once a
- * sweep moves no constraint velocity by more than 1e-6 (at most
- * mw_config.pgs_iters of them): only the start of the exact solve depends on
- * them.  MW_LCP_PGS: the PGS sweeps alone (cold unless mw_set_pgs_options
- * asks for the warm start). */
+/* The boxed-LCP solver of floating models.  MW_LCP_EXACT (default,
+ * max_solves 24) solves the LCP as DART does: DART's primary solver is ODE's
+ * Dantzig pivoting LCP [EXT], reached from ForwardStep (Physics.cpp:1824-1835),
+ * whose friction index boxes every friction row once, by mu x the normal
+ * impulses of the frictionless problem -- two strictly convex box QPs
+ * (wave_lcp.hpp), each from the previous step's solution, PGS sweeps on the
+ * stage's box problem (at most mw_config.pgs_iters, ending once a sweep moves
+ * no constraint velocity by more than 1e-6), then semismooth Newton /
+ * active-set rounds with at most max_solves dense linear solves (elimination
+ * over the wave's lanes) per world-step.  It runs on the world-per-wavefront
+ * kernel, which then steps every floating model (joint-less bodies, small
+ * trees at any world count).  MW_LCP_PGS: the coupled PGS sweeps alone (cold
+ * unless mw_set_pgs_options asks for the warm start); chosen before
+ * mw_load_model it lets a joint-less body / small compiled tree take the
+ * PGS-only lane kernels.  Selecting MW_LCP_EXACT for a model already loaded
+ * onto a lane kernel fails with MW_ESTATE; mw_lcp_solver reports the solver
+ * the model's kernel runs. */
 #define MW_LCP_PGS 0
 #define MW_LCP_EXACT 1
 int mw_set_lcp_solver(mw_sim* sim, int32_t mode, int32_t max_solves);

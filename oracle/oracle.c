@@ -417,16 +417,12 @@ void or_rnea(const or_model* m, const double* q, const double* qd,
 /* ---------------- boxed LCP ---------------- */
 
 /* Sweep budget: iters >= 0 runs exactly that many Gauss-Seidel sweeps (the
- * GPU kernels' fixed count).  iters < 0 (OR_PGS_CONVERGED) solves the boxed
- * LCP exactly: OR_PGS_WARM sweeps give an active-set guess, then lcp_refine()
- * solves the linear system of that active set and repairs it until the
- * complementarity conditions hold to round-off (friction rows bounded by
- * mu x_normal).  That is the problem DART's primary solver, the Dantzig
- * pivoting LCP of BoxedLcpConstraintSolver [EXT], solves exactly -- the
- * converged reference for the truncated sweeps of the kernels.  (Plain PGS
- * would need ~1e5+ sweeps: with CFM 1e-5 the redundant contact corners leave
- * A conditioned ~1e5.)  or_pgs_stats(): sweeps and active-set rounds of the
- * latest solve, and its final complementarity residual. */
+ * GPU kernels' PGS-only mode).  iters < 0 (OR_PGS_CONVERGED) solves the boxed
+ * LCP the way DART does (lcp_dantzig below: ODE's Dantzig solver with its
+ * friction index, two strictly convex box QPs solved exactly), after
+ * OR_PGS_WARM sweeps that only pick the starting point.  or_pgs_stats():
+ * sweeps (+ 1e6 x box-QP iterations) of the latest solve and its final
+ * complementarity residual. */
 #define OR_PGS_WARM 300
 #define OR_LCP_MAXN (3 * OR_MAXFC + 3 * OR_MAXB > 3 * OR_MAXCONTACTS ? 3 * OR_MAXFC + 3 * OR_MAXB : 3 * OR_MAXCONTACTS)
 static _Thread_local int g_pgs_sweeps = 0;
@@ -615,148 +611,78 @@ static int boxqp_solve(int n, const double* A, int lda, const double* b, const d
     return -1;
 }
 
-/* Semismooth Newton rounds on the coupled conditions (the GPU's first phase,
- * gym-ignition_amd/csrc/wave_lcp.hpp, in fp64): rows held at a bound when
- * their gradient g = A x - b pushes outward, friction rows on their box edge
- * coupled to their normal (d_t = +-mu d_n), the rest free; the Newton system
- * by Gaussian elimination with partial pivoting, a monotone line search on
- * the largest residual.  Returns the rounds that lowered the residual. */
-static int lcp_ssn(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
-                   const int* findex, double mu, double* x, int rounds)
+/* Converged mode: DART's boxed LCP.  BoxedLcpConstraintSolver hands the
+ * constraint rows to DantzigBoxedLcpSolver, i.e. ODE's dSolveLCP
+ * (dart/external/odelcpsolver/lcp.cpp; the reference installs it as
+ * libdart-external-odelcpsolver-dev, .docker/cicd-devel.Dockerfile:56-60)
+ * [EXT].  Its friction-index handling fixes the answer: the rows with
+ * findex >= 0 are permuted to the end; the pivoting solves the other rows
+ * first (normals in [0, inf), joint rows in their boxes, friction impulses
+ * still 0), and on reaching the first friction row it sets EVERY friction
+ * row's box once to +-|mu x_n| from the normal impulses solved so far
+ * (x_n = 0: the row is pinned at 0) and never updates it; the remaining
+ * pivots keep every row complementary with those boxes.  A is symmetric
+ * positive definite (the CFM), so each stage is a strictly convex box QP
+ * with a unique minimiser, whatever the pivoting order:
+ *   stage 1: x_S = argmin over the non-friction rows S, friction impulses 0;
+ *   stage 2: x = argmin over all rows, friction boxes [-mu x_n1, mu x_n1]
+ *            from the stage-1 normals.
+ * Both solved exactly here (boxqp_solve, warm-started from x).  The result
+ * is not the fixed point of the friction boxes (|x_t| <= mu x_n at the FINAL
+ * normals): where the friction saturates and the contact's normals shift
+ * with it (a sliding, pitching foot) DART keeps the boxes of the
+ * frictionless normals.  Stats: boxqp iterations of both stages; the final
+ * complementarity residual of the two stages' boxes (velocity units), < 0
+ * when a stage ran out of budget. */
+static void lcp_dantzig(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
+                        const int* findex, double mu, double* x)
 {
-    static _Thread_local double K[OR_LCP_MAXN * OR_LCP_MAXN];
-    double g[OR_LCP_MAXN], c[OR_LCP_MAXN], d[OR_LCP_MAXN], xt[OR_LCP_MAXN], L[OR_LCP_MAXN], U[OR_LCP_MAXN];
-    int st[OR_LCP_MAXN], idx[OR_LCP_MAXN];  /* 0 free, 1 fixed, 2 coupled +, 3 coupled - */
-    int good = 0;
-    for (int it = 0; it < rounds; ++it) {
-        double xm = 0.0;
-        for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
-        const double res = lcp_residual(n, A, lda, b, lo, hi, findex, mu, x, 1e-12 * (1.0 + xm));
-        if (res <= 1e-13) break;
-        for (int r = 0; r < n; ++r) {
-            double acc = -b[r];
-            for (int e = 0; e < n; ++e) acc += A[r * lda + e] * x[e];
-            g[r] = acc;
-            row_bounds(r, lo, hi, findex, mu, x, &L[r], &U[r]);
-        }
-        for (int r = 0; r < n; ++r) {
-            st[r] = 0;
-            if (findex[r] < 0 && ((x[r] <= L[r] && g[r] >= 0.0) || (x[r] >= U[r] && g[r] <= 0.0))) st[r] = 1;
-        }
-        for (int r = 0; r < n; ++r) {
-            if (findex[r] < 0) continue;
-            if (st[findex[r]] == 1) st[r] = 1;
-            else if (U[r] <= 0.0) st[r] = g[r] < 0.0 ? 2 : (g[r] > 0.0 ? 3 : 1);  /* an opening contact slides */
-            else if (x[r] >= U[r] && g[r] <= 0.0) st[r] = 2;
-            else if (x[r] <= L[r] && g[r] >= 0.0) st[r] = 3;
-        }
-        int nf = 0;
-        for (int r = 0; r < n; ++r)
-            if (st[r] == 0) idx[nf++] = r;
-        /* columns of the free unknowns; a coupled friction column folds into its normal's */
-        for (int i = 0; i < nf; ++i) {
-            const int r = idx[i];
-            for (int j = 0; j < nf; ++j) K[i * nf + j] = A[r * lda + idx[j]];
-            for (int t = 0; t < n; ++t) {
-                if (st[t] < 2) continue;
-                const double sg = st[t] == 2 ? mu : -mu;
-                for (int j = 0; j < nf; ++j)
-                    if (idx[j] == findex[t]) K[i * nf + j] += sg * A[r * lda + t];
-            }
-            c[i] = -g[r];
-        }
-        for (int r = 0; r < n; ++r) d[r] = 0.0;
-        if (nf > 0) {
-            double y[OR_LCP_MAXN];
-            if (!lcp_gauss(nf, K, c, y)) break;
-            for (int i = 0; i < nf; ++i) d[idx[i]] = y[i];
-        }
-        for (int t = 0; t < n; ++t)
-            if (st[t] >= 2) d[t] = (st[t] == 2 ? mu : -mu) * d[findex[t]];
-        int accepted = 0;
-        double step = 1.0;
-        for (int ls = 0; ls < 8 && !accepted; ++ls, step *= 0.5) {
-            for (int r = 0; r < n; ++r) {
-                xt[r] = x[r] + step * d[r];
-                if (findex[r] < 0) xt[r] = xt[r] < lo[r] ? lo[r] : (xt[r] > hi[r] ? hi[r] : xt[r]);
-            }
-            for (int r = 0; r < n; ++r)
-                if (findex[r] >= 0) {
-                    const double u = mu * (xt[findex[r]] > 0.0 ? xt[findex[r]] : 0.0);
-                    xt[r] = xt[r] < -u ? -u : (xt[r] > u ? u : xt[r]);
-                }
-            double xtm = 0.0;
-            for (int r = 0; r < n; ++r) xtm = fabs(xt[r]) > xtm ? fabs(xt[r]) : xtm;
-            if (lcp_residual(n, A, lda, b, lo, hi, findex, mu, xt, 1e-12 * (1.0 + xtm)) < res) {
-                for (int r = 0; r < n; ++r) x[r] = xt[r];
-                accepted = 1;
-            }
-        }
-        if (!accepted) break;
-        ++good;
+    static _Thread_local double As[OR_LCP_MAXN * OR_LCP_MAXN];
+    double bs[OR_LCP_MAXN], Ls[OR_LCP_MAXN], Us[OR_LCP_MAXN], xs[OR_LCP_MAXN], L[OR_LCP_MAXN] = {0}, U[OR_LCP_MAXN] = {0};
+    int sidx[OR_LCP_MAXN], nofric[OR_LCP_MAXN];
+    int ns = 0, failed = 0, iters = 0;
+    for (int r = 0; r < n; ++r) {
+        nofric[r] = -1;
+        if (findex[r] < 0) sidx[ns++] = r;
     }
-    return good;
-}
-
-/* Converged mode: staggered fixed point of the friction bounds.  With the
- * boxes [-mu x_n, mu x_n] frozen at the current normal impulses the LCP is a
- * strictly convex box QP (boxqp_solve, exact); the bounds are then updated
- * from its normals until they stop moving.  At the fixed point x satisfies
- * the complementarity conditions of the coupled boxed LCP (the fixed point
- * PGS approaches).  Stats: sweeps + 1e6 x outer rounds; the final
- * complementarity residual (velocity units). */
-static void lcp_refine(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
-                       const int* findex, double mu, double* x)
-{
-    double L[OR_LCP_MAXN], U[OR_LCP_MAXN], prev[OR_LCP_MAXN], nb[OR_LCP_MAXN];
-    int round = 0, failed = 0;
-    /* nb: the normal impulses the friction boxes are built from.  The first
-     * rounds take the latest normals (plain staggering); a fixed point the
-     * plain iteration circles (a period-2 cycle of two boxes) is reached by
-     * averaging: nb <- (nb + x) / 2 after round 20.  Either way the fixed
-     * point is x_n = nb, the coupled conditions. */
-    for (int r = 0; r < n; ++r) nb[r] = x[r];
-    for (; round < 400; ++round) {
-        const double om = round < 20 ? 1.0 : 0.5;
-        for (int r = 0; r < n; ++r) nb[r] = round == 0 ? x[r] : om * x[r] + (1.0 - om) * nb[r];
-        for (int r = 0; r < n; ++r) row_bounds(r, lo, hi, findex, mu, nb, &L[r], &U[r]);
-        for (int r = 0; r < n; ++r) {  /* a negative normal cannot occur: x_n >= 0 */
-            if (L[r] > U[r]) { const double t = L[r]; L[r] = U[r]; U[r] = t; }
-            prev[r] = x[r];
-        }
-        if (boxqp_solve(n, A, lda, b, L, U, x) < 0) { failed = 1; break; }
-        double dmax = 0.0, xm = 0.0;
-        for (int r = 0; r < n; ++r) {
-            dmax = fabs(x[r] - prev[r]) > dmax ? fabs(x[r] - prev[r]) : dmax;
-            xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
-        }
-        if (dmax <= 1e-14 * (1.0 + xm)) {
-            /* x solved the QP of its own boxes: done when nb = x_n */
-            double dn = 0.0;
-            for (int r = 0; r < n; ++r) dn = fabs(x[r] - nb[r]) > dn ? fabs(x[r] - nb[r]) : dn;
-            if (dn <= 1e-13 * (1.0 + xm)) { ++round; break; }
+    /* stage 1: the non-friction rows, friction impulses 0 */
+    for (int i = 0; i < ns; ++i) {
+        const int r = sidx[i];
+        for (int j = 0; j < ns; ++j) As[i * ns + j] = A[r * lda + sidx[j]];
+        bs[i] = b[r];
+        Ls[i] = lo[r];
+        Us[i] = hi[r];
+        xs[i] = x[r];
+    }
+    if (ns > 0) {
+        const int it = boxqp_solve(ns, As, ns, bs, Ls, Us, xs);
+        if (it < 0) failed = 1; else iters += it;
+    }
+    double x1[OR_LCP_MAXN];
+    for (int r = 0; r < n; ++r) x1[r] = 0.0;
+    for (int i = 0; i < ns; ++i) x1[sidx[i]] = xs[i];
+    const double res1 = ns > 0 ? lcp_residual(ns, As, ns, bs, Ls, Us, nofric, 0.0, xs, 1e-12) : 0.0;
+    /* stage 2: friction boxes from the stage-1 normals, all rows */
+    for (int r = 0; r < n; ++r) {
+        if (findex[r] >= 0) {
+            const double xn = x1[findex[r]];
+            const double u = xn > 0.0 ? fabs(mu * xn) : 0.0;
+            L[r] = -u;
+            U[r] = u;
+        } else {
+            L[r] = lo[r];
+            U[r] = hi[r];
+            x[r] = x1[r];
         }
     }
+    const int it2 = boxqp_solve(n, A, lda, b, L, U, x);
+    if (it2 < 0) failed = 1; else iters += it2;
     double xm = 0.0;
     for (int r = 0; r < n; ++r) xm = fabs(x[r]) > xm ? fabs(x[r]) : xm;
-    g_pgs_delta = lcp_residual(n, A, lda, b, lo, hi, findex, mu, x, 1e-12 * (1.0 + xm));
-    if (g_pgs_delta > 1e-10 || failed) {
-        /* the staggered rounds stopped short (a slowly contracting friction
-         * fixed point): semismooth Newton polish, kept only if it is better */
-        double xs[OR_LCP_MAXN];
-        for (int r = 0; r < n; ++r) xs[r] = x[r];
-        lcp_ssn(n, A, lda, b, lo, hi, findex, mu, xs, 30);
-        double xsm = 0.0;
-        for (int r = 0; r < n; ++r) xsm = fabs(xs[r]) > xsm ? fabs(xs[r]) : xsm;
-        const double rs = lcp_residual(n, A, lda, b, lo, hi, findex, mu, xs, 1e-12 * (1.0 + xsm));
-        if (rs < g_pgs_delta) {
-            for (int r = 0; r < n; ++r) x[r] = xs[r];
-            g_pgs_delta = rs;
-            failed = 0;
-        }
-    }
+    const double res2 = lcp_residual(n, A, lda, b, L, U, nofric, 0.0, x, 1e-12 * (1.0 + xm));
+    g_pgs_delta = res1 > res2 ? res1 : res2;
     if (failed) g_pgs_delta = -1.0 - g_pgs_delta;
-    g_pgs_sweeps += 1000000 * round;
+    g_pgs_sweeps += 1000000 * iters;
 }
 
 void or_pgs(int n, const double* A, const double* b, const double* lo,
@@ -777,7 +703,7 @@ void or_pgs(int n, const double* A, const double* b, const double* lo,
     if (iters < 0 && n <= OR_LCP_MAXN) {
         int findex[OR_LCP_MAXN];
         for (int r = 0; r < n; ++r) findex[r] = -1;
-        lcp_refine(n, A, n, b, lo, hi, findex, 0.0, x);
+        lcp_dantzig(n, A, n, b, lo, hi, findex, 0.0, x);
     }
 }
 
@@ -1101,7 +1027,7 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
                 hi[r] = INFINITY;
                 findex[r] = (r % 3 == 0) ? -1 : r - r % 3;
             }
-            lcp_refine(nr, &A[0][0], 3 * OR_MAXCONTACTS, b, lo, hi, findex, m->mu, x);
+            lcp_dantzig(nr, &A[0][0], 3 * OR_MAXCONTACTS, b, lo, hi, findex, m->mu, x);
         }
         for (int r = 0; r < nr; ++r)
             for (int k = 0; k < 6; ++k) V[k] += MJ[r][k] * x[r];
@@ -1821,7 +1747,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
                 findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
                 if (kind[r] == K_NORMAL) { lo[r] = 0.0; hi[r] = INFINITY; }
             }
-            lcp_refine(nr, A, nr, bb, lo, hi, findex, m->mu, x);
+            lcp_dantzig(nr, A, nr, bb, lo, hi, findex, m->mu, x);
         }
         for (int r = 0; r < nr; ++r) g_cap_x[r] = x[r];
         for (int r = 0; r < nr; ++r)
@@ -2664,7 +2590,7 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
         if (pgs_iters < 0) {
             static _Thread_local int findex[3 * OR_SC_MAXC + 3 * OR_MAXB];
             for (int r = 0; r < nr; ++r) findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
-            lcp_refine(nr, A, nr, bb, lo, hi, findex, sm->mu, x);
+            lcp_dantzig(nr, A, nr, bb, lo, hi, findex, sm->mu, x);
         }
         for (int r = 0; r < nr; ++r)
             for (int e = 0; e < NV; ++e) nu[e] += MJ[r][e] * x[r];

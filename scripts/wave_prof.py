@@ -57,7 +57,8 @@ print(f"{W} worlds, PGS {PGS}, {T} steps: {dt / T * 1e6:.1f} us/step wall; conta
 for k, name in enumerate(PHASES):
     print(f"  {name:40s} {buf[k] / W / T:12.0f} cycles/world-step")
 print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f} rounds per world-step; "
-      f"{buf[10] / W / T:.2f} of the solves in staggered rounds; max per world-step {buf[11]} solves, "
-      f"{buf[12]} staggered; {buf[13]} of {W * T} world-steps > 4 solves; "
-      f"{buf[14] / W / T:.0f} cycles/world-step in the linear solves, {buf[15] / W / T:.0f} in the PGS sweeps")
+      f"{buf[10] / W / T:.2f} of the solves in stage 2 (friction boxes); max per world-step {buf[11]} solves, "
+      f"{buf[12]} in stage 2; {buf[13]} of {W * T} world-steps > 4 solves; "
+      f"{buf[14] / W / T:.0f} cycles/world-step in the linear solves, {buf[15] / W / T:.0f} in the PGS sweeps "
+      f"(PGS-only mode) / the whole exact solve incl. its per-stage sweeps (exact mode)")
 sim.close()

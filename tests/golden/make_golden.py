@@ -12,7 +12,8 @@ to the outputs:
                          (numpy PCG64 seed 43), obs / reward / done per step
   pendulum_swingup.npz   PendulumSwingUp, 16 worlds x 300 steps, torques
                          U(-50, 50) (PCG64 seed 43)
-  humanoid_stand.npz     humanoid32 (floating base, ground contacts, PGS 50)
+  humanoid_stand.npz     humanoid32 (floating base, ground contacts, the boxed LCP
+                         solved as DART does: oracle.c lcp_dantzig)
                          under the JointController PID hold for 300 steps:
                          joint positions and base position every 10 steps,
                          final contact forces

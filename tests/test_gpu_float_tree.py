@@ -287,12 +287,14 @@ def test_one_step_exact_lcp_random_states(require_gpu, oracle, monkeypatch, name
 
 def test_exact_lcp_out_of_budget_is_feasible(require_gpu, oracle, monkeypatch):
     """a world whose exact solve runs out of its budget keeps
-    impulses inside the friction pyramid of its current normals (DART's
-    boxed LCP never returns |x_t| > mu x_n).  A budget of one linear solve
-    after 2 sweeps leaves many of the adversarial random humanoid states
-    unconverged; every contact force read back must still satisfy
-    f_z >= 0 and |f_x|, |f_y| <= mu f_z (the ground's plane-space tangents
-    are -y and +x)."""
+    impulses inside the boxes of its stage (wave_lcp.hpp): normals >= 0 and
+    every friction impulse within +-mu x_n of its contact's stage-1 normal.
+    With no PGS sweep and a budget of one linear solve, stage 1 takes the
+    solve and stage 2 none (its friction impulses are only clamped into their
+    boxes), so the stage-1 normals are the final ones and every contact force
+    read back must satisfy f_z >= 0 and |f_x|, |f_y| <= mu f_z (the ground's
+    plane-space tangents are -y and +x) -- on adversarial random humanoid
+    states where most worlds stop unconverged."""
     from mwstep import native as N
     from mwstep.sim import Simulator
     text = _model("humanoid32")
@@ -301,7 +303,7 @@ def test_exact_lcp_out_of_budget_is_feasible(require_gpu, oracle, monkeypatch):
     rng = np.random.default_rng(11)
     cm = oracle.load_urdf(text)
     q, qd, pose, vel, tau = _random_states(cm, W, rng)
-    sim = Simulator(text, n_worlds=W, pgs_iters=2)
+    sim = Simulator(text, n_worlds=W, pgs_iters=0)
     sim.set_lcp_solver(True, 1)
     sim.set_ground_plane(True, mu)
     sim.enable_contacts(True)
@@ -488,18 +490,22 @@ def test_humanoid_512_impacts_vs_converged_lcp(require_gpu, oracle, solver):
     from a host PD law on the GPU state (Force mode), so every step is
     teacher-forced: a subset of worlds is restarted in the fp64 oracle from
     the GPU state and stepped twice, with a truncated PGS (50 sweeps) and
-    with the boxed LCP solved exactly (pyoracle.PGS_CONVERGED: the solution
-    DART's Dantzig solver returns [EXT]).
+    with the boxed LCP solved as DART solves it (pyoracle.PGS_CONVERGED,
+    oracle.c lcp_dantzig: ODE's Dantzig solver with its friction index, two
+    strictly convex box QPs solved exactly [EXT]).
       * solver "exact" (the kernel's default, wave_lcp.hpp): the GPU against
-        the exact LCP is fp32 round-off -- positions 1e-5, velocities 2e-3
-        (the fp32 solve stops at a complementarity residual of a few 1e-6 m/s,
-        up to 10x that after its polish round; the redundant box-foot corners
-        make A = J M^-1 J^T + CFM conditioned ~1e7, so the joint velocities
-        carry that residual amplified by ~1/sqrt(CFM) = 300);
+        DART's LCP is fp32 round-off -- positions 1e-5, velocities 1e-3 (the
+        fp32 solve stops at a complementarity residual of a few 1e-6 m/s; the
+        redundant box-foot corners make A = J M^-1 J^T + CFM conditioned ~1e7,
+        so the joint velocities carry that residual amplified by up to
+        ~1/sqrt(CFM) = 300), every oracle solve converged;
       * solver "pgs" (mw_set_lcp_solver(PGS), 50 sweeps): against the
         same-algorithm oracle fp32 round-off (velocities 2e-3, positions
-        1e-5); against the exact LCP the PGS-50 truncation (oracle PGS-50 vs
-        exact, same inputs) plus that round-off."""
+        1e-5).  PGS couples every friction box to the CURRENT normal (DART's
+        secondary PGS solver does too), a different problem from the primary
+        solver's, whose boxes come from the frictionless normals: where the
+        friction saturates at an impact the two answers part by O(1) joint
+        velocities (reported, not bounded)."""
     from mwstep import get_model_file
     from mwstep import native as N
     from mwstep.sim import Simulator
@@ -603,25 +609,18 @@ def test_humanoid_512_impacts_vs_converged_lcp(require_gpu, oracle, solver):
           f"base z [{z.min():.3f}, {z.max():.3f}], exact LCP: max rounds {rounds}, max residual {worst_res:.1e}; "
           f"GPU unconverged world-steps {unconv}/{W * H}; oracle exact solve failed on {oracle_fail}; "
           f"qd errors > 5e-4 (world, step, error, unconverged worlds in the step): {big_qd[:40]}")
-    assert len(oracle_fail) <= len(subset) * H // 200
+    assert not oracle_fail
     assert np.isfinite(sim.get("q")).all() and np.isfinite(sim.base_pose()).all()
     assert z.min() > 0.3 and sim.constraint_overflow() == 0
     assert in_contact[subset].all()
     if solver == "exact":
-        # DART-equivalent solve: the GPU is within fp32 round-off of the exact LCP
-        assert econv["pose"] <= 1e-5 and econv["q"] <= 1e-5 and econv["vel"] <= 2e-3 and econv["qd"] <= 2e-3
+        # DART-equivalent solve: the GPU is within fp32 round-off of DART's LCP
+        assert econv["pose"] <= 1e-5 and econv["q"] <= 1e-5 and econv["vel"] <= 1e-3 and econv["qd"] <= 1e-3
         assert unconv <= W * H // 200
         sim.close()
         return
     assert unconv == 0
     assert e50["pose"] <= 1e-5 and e50["q"] <= 1e-5 and e50["vel"] <= 2e-3 and e50["qd"] <= 2e-3
-    # the GPU's distance to the exact LCP is the PGS truncation (oracle PGS-50
-    # vs exact, same inputs) plus fp32 round-off -- nothing else
-    for key in keys:
-        assert econv[key] <= trunc[key] + 2 * e50[key] + 1e-7, key
-    # and the truncation itself stays within the stated contact tolerance
-    # (measured r02: pose 1.5e-5, q 7.0e-5, vel 1.5e-2, qd 7.0e-2)
-    assert econv["pose"] <= 5e-5 and econv["q"] <= 2e-4 and econv["vel"] <= 5e-2 and econv["qd"] <= 0.15
     sim.close()
 
 

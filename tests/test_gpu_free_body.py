@@ -6,9 +6,12 @@ first slice: single floating bodies).
     cube): no contact before falling, one contact (cube::cube vs
     ground_plane::link) after 150 ms, normals +z, the vertical forces sum to
     the weight within 0.1 N, Link::contactWrench = [0, 0, sum Fz, 0, 0, 0];
-  * teacher-forced one-step parity of the HIP free-body kernel against the fp64
-    oracle (or_free_step) on random poses / twists near the ground: pose and
-    twist within 1e-5 (fp32 vs fp64), contact forces within 1e-3 relative;
+  * teacher-forced one-step parity against the fp64 oracle (or_free_step) on
+    random poses / twists near the ground: pose and twist within 1e-5 (fp32 vs
+    fp64), contact forces within 1e-3 relative -- on the world-per-wavefront
+    kernel with DART's exact boxed LCP (the default for mw_sim floating
+    models; oracle PGS_CONVERGED) and on the PGS-only free-body kernel
+    (MW_LCP_PGS chosen before the model is loaded; oracle PGS 50);
   * free fall and torque-free spin over 1000 steps against the oracle;
   * base reset semantics (visible after the next run).
 """
@@ -75,14 +78,18 @@ def _rock_body_urdf():
     return mesh_body_urdf(path, mass=3.0, half=(0.12, 0.08, 0.06), rpy=(0.2, 0.1, -0.3))
 
 
+@pytest.mark.parametrize("kernel", ["wave", "free"])
 @pytest.mark.parametrize("urdf", ["cube", "double", "sphere", "cylinder", "rock"])
-def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
+def test_one_step_parity_with_contacts(require_gpu, oracle, urdf, kernel):
     from mwstep.sim import Simulator
     text = {"cube": cube_urdf, "double": lambda: cube_urdf(True), "sphere": sphere_urdf,
             "cylinder": lambda: cylinder_urdf(rpy="0.2 0 0"), "rock": _rock_body_urdf}[urdf]()
     W, pgs = 256, 50
     rng = np.random.default_rng(5)
-    sim = Simulator(text, n_worlds=W, pgs_iters=pgs)
+    sim = Simulator(text, n_worlds=W, pgs_iters=pgs, lcp_exact=(kernel == "wave"))
+    assert sim.float_kernel() == (2 if kernel == "wave" else 0)
+    assert sim.lcp_solver()[0] is (kernel == "wave")
+    opgs = oracle.PGS_CONVERGED if kernel == "wave" else pgs
     sim.set_ground_plane(True, 0.8)
     sim.enable_contacts(True)
     q = rng.normal(size=(W, 4))
@@ -102,7 +109,7 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
     n_contact = 0
     for w in range(W):
         R0 = _quat_to_R(p0[w, 3:])
-        ow = oracle.FreeWorld(cm, ground=True, mu=0.8, pgs_iters=pgs)
+        ow = oracle.FreeWorld(cm, ground=True, mu=0.8, pgs_iters=opgs)
         ow.set_pose(p0[w, :3], R0)
         ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
         ow.step()
@@ -116,17 +123,18 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, urdf):
         for row, (p, n, f, d) in zip(gc, ow.contacts):
             assert np.abs(row[0:3] - p).max() <= 1e-5
             worst_f = max(worst_f, float(np.abs(row[6:9] - f).max()) / (1.0 + float(np.abs(f).max())))
-    print(f"free body {urdf}: one-step max|pose err| {worst_p:.2e}, max|vel err| {worst_v:.2e}, "
+    print(f"free body {urdf}, {kernel} kernel: one-step max|pose err| {worst_p:.2e}, max|vel err| {worst_v:.2e}, "
           f"force rel err {worst_f:.2e}, {n_contact}/{W} worlds in contact")
     assert n_contact > W // 4
     assert worst_p <= 1e-5 and worst_v <= 1e-4 and worst_f <= 1e-3
     sim.close()
 
 
-def test_free_fall_and_spin_parity(require_gpu, oracle):
+@pytest.mark.parametrize("exact", [True, False])
+def test_free_fall_and_spin_parity(require_gpu, oracle, exact):
     from mwstep.sim import Simulator
     text = cube_urdf()
-    sim = Simulator(text, n_worlds=2, pose=(0, 0, 10.0, 1, 0, 0, 0), gravity=(0, 0, -G))
+    sim = Simulator(text, n_worlds=2, pose=(0, 0, 10.0, 1, 0, 0, 0), gravity=(0, 0, -G), lcp_exact=exact)
     sim.reset_base_velocity([[0.3, -0.2, 1.0, 0.5, -1.0, 2.0], [0, 0, 0, 0, 0, 0]])
     sim.run(paused=True)
     cm = oracle.load_urdf(text, pose_xyz=(0, 0, 10.0))
@@ -166,11 +174,13 @@ def test_base_reset_semantics(require_gpu):
     gazebo.close()
 
 
-def test_run_device_equals_run(require_gpu):
+@pytest.mark.parametrize("exact", [True, False])
+def test_run_device_equals_run(require_gpu, exact):
     """mw_run_device (no readback, graph-capturable) == repeated mw_run."""
     from mwstep import get_model_file
     from mwstep.sim import Simulator
-    sims = [Simulator(get_model_file("cube"), n_worlds=64, pose=(0, 0, 0.3, 0.9, 0.3, 0.2, 0.1)) for _ in range(2)]
+    sims = [Simulator(get_model_file("cube"), n_worlds=64, pose=(0, 0, 0.3, 0.9, 0.3, 0.2, 0.1), lcp_exact=exact)
+            for _ in range(2)]
     for s in sims:
         s.set_ground_plane(True, 0.7)
         s.enable_contacts(True)
@@ -187,15 +197,17 @@ def test_run_device_equals_run(require_gpu):
         s.close()
 
 
-def test_cylinder_kats_on_the_free_body_kernel(require_gpu, oracle):
-    """The oracle's cylinder KATs (tests/test_cylinder_oracle.py) on the HIP
-    free-body kernel: a standing cylinder rests at half its length carrying its
-    weight on 4 rim points; a lying one spun about its axis rolls without
-    slipping at omega0 r / 3; both follow the fp64 oracle step by step."""
+@pytest.mark.parametrize("exact", [True, False])
+def test_cylinder_kats_on_mw_sim(require_gpu, oracle, exact):
+    """The oracle's cylinder KATs (tests/test_cylinder_oracle.py) on mw_sim --
+    the world-per-wavefront kernel with DART's exact LCP (default) and the
+    PGS-only free-body kernel: a standing cylinder rests at half its length
+    carrying its weight on 4 rim points; a lying one spun about its axis rolls
+    without slipping at omega0 r / 3; both follow the fp64 oracle step by step."""
     import math
     from mwstep.sim import Simulator
     from test_cylinder_oracle import cylinder_urdf
-    sim = Simulator(cylinder_urdf(), n_worlds=2, pose=(0, 0, 0.25, 1, 0, 0, 0), pgs_iters=100)
+    sim = Simulator(cylinder_urdf(), n_worlds=2, pose=(0, 0, 0.25, 1, 0, 0, 0), pgs_iters=100, lcp_exact=exact)
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
     for _ in range(600):
@@ -211,10 +223,11 @@ def test_cylinder_kats_on_the_free_body_kernel(require_gpu, oracle):
             f'<inertia ixx="{0.5 * m * r * r}" iyy="{ixx}" izz="{ixx}" ixy="0" ixz="0" iyz="0"/></inertial>'
             f'<collision><origin rpy="0 {math.pi / 2} 0" xyz="0 0 0"/><geometry>'
             f'<cylinder radius="{r}" length="0.4"/></geometry></collision></link></robot>')
-    sim = Simulator(text, n_worlds=2, pose=(0, 0, r, 1, 0, 0, 0), pgs_iters=100)
+    sim = Simulator(text, n_worlds=2, pose=(0, 0, r, 1, 0, 0, 0), pgs_iters=100, lcp_exact=exact)
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
-    ow = oracle.FreeWorld(oracle.load_urdf(text, pose_xyz=(0, 0, r)), mu=1.0, pgs_iters=100)
+    ow = oracle.FreeWorld(oracle.load_urdf(text, pose_xyz=(0, 0, r)), mu=1.0,
+                          pgs_iters=oracle.PGS_CONVERGED if exact else 100)
     for _ in range(100):
         sim.run()
         ow.step()
@@ -230,3 +243,28 @@ def test_cylinder_kats_on_the_free_body_kernel(require_gpu, oracle):
     print(f"rolling cylinder: v {v[1]:.4f} (omega0 r / 3 = {10 * r / 3:.4f}), max |dp| vs oracle {worst:.2e}")
     assert worst <= 2e-4
     sim.close()
+
+
+def test_cube_kat_exact_on_mw_sim(require_gpu):
+    """the reference's contact KAT
+    (tests/test_scenario/test_contacts.py:58-122) on mw_sim with DART's exact
+    LCP -- a cube dropped onto the plane rests on its 4 bottom corners, the
+    normal forces carry its weight within 0.1 N, and the contact answer does
+    not depend on the world count."""
+    from mwstep.sim import Simulator
+    for W in (1, 4096):
+        sim = Simulator(cube_urdf(), n_worlds=W, pose=(0, 0, 0.15, 1, 0, 0, 0))
+        assert sim.float_kernel() == 2 and sim.lcp_solver() == (True, 24)
+        sim.set_ground_plane(True, 1.0)
+        sim.enable_contacts(True)
+        for _ in range(150):
+            sim.run()
+        c = sim.contacts(0)
+        assert len(c) == 4 and np.allclose(c[:, 3:6], [0, 0, 1])
+        assert float(np.sum(c[:, 8])) == pytest.approx(5.0 * G, abs=0.1)
+        if W == 1:
+            ref = (sim.base_pose()[0].copy(), c.copy())
+        else:
+            assert np.array_equal(sim.base_pose()[0], ref[0]) and np.array_equal(c, ref[1])
+        assert sim.lcp_unconverged() == 0
+        sim.close()

@@ -106,7 +106,7 @@ def test_floating_shards_bit_identical(require_gpu, model, z0, pgs_opts):
     humanoid_leg: the 8-GPU share is 64 worlds): a sim of W worlds equals two
     sims of W/2 worlds holding the two halves' initial states BIT FOR BIT over
     150 steps with ground impacts, sliding and (parametrised) the warm-started
-    PGS, on the wave kernel (humanoid) and the lane kernel (quadruped)."""
+    PGS, for the humanoid and the quadruped (world-per-wavefront kernel)."""
     W, T = 128, 150
     rng = np.random.default_rng(11)
     from mwstep import get_model_file
@@ -137,6 +137,39 @@ def test_floating_shards_bit_identical(require_gpu, model, z0, pgs_opts):
     assert sum(len(full.contacts(w)) for w in range(0, W, 8)) > 0
     assert full.constraint_overflow() == 0
     for s in [full] + halves:
+        s.close()
+
+
+def test_contact_answer_independent_of_world_count(require_gpu):
+    """with DART's exact LCP (the default) every floating
+    model steps on one kernel whatever the world count -- round 3 switched the
+    quadruped to the PGS lane kernel above 4096 worlds.  4096 and 8192
+    quadrupeds from identical states (the first 4096 worlds of the larger run)
+    step bit for bit alike through 60 steps of drops, slides and contacts."""
+    from mwstep import get_model_file
+    from mwstep.sim import Simulator
+    rng = np.random.default_rng(5)
+    W = 8192
+    n = 8
+    q0 = rng.uniform(-0.1, 0.1, (W, n)) + np.array([0.6, -1.2] * 4)
+    quat = rng.normal(size=(W, 4)) * np.array([1.0, 0.05, 0.05, 0.05])
+    quat[:, 0] = np.abs(quat[:, 0]) + 1.0
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), 0.45 + rng.uniform(0.0, 0.05, W), quat])
+    vel = np.column_stack([rng.uniform(-0.5, 0.5, (W, 2)), rng.uniform(-0.3, 0.0, W), rng.uniform(-0.5, 0.5, (W, 3))])
+    sims = [_float_sim("quadruped", w, q0[:w], pose[:w], vel[:w], None) for w in (4096, W)]
+    for s in sims:
+        assert s.float_kernel() == 2 and s.lcp_solver() == (True, 24)
+    for t in range(60):
+        for s in sims:
+            s.run()
+    h = 4096
+    for what in ("q", "qd"):
+        assert np.array_equal(sims[0].get(what), sims[1].get(what)[:h]), what
+    assert np.array_equal(sims[0].base_pose(), sims[1].base_pose()[:h])
+    assert np.array_equal(sims[0].base_velocity(), sims[1].base_velocity()[:h])
+    assert sum(len(sims[0].contacts(w)) for w in range(0, h, 64)) > 0
+    for s in sims:
         s.close()
 
 

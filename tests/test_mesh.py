@@ -138,10 +138,14 @@ def test_bad_meshes_fail_loudly(N, text, needle):
     assert rc == N.MW_EPARSE and needle in msg
 
 
-def test_mw_sim_free_body_mesh_entries(N, tmp_path):
-    """mw_sim's free-body kernel holds 2 shape entries of 8 slots: a mesh
-    takes one entry per 8 support points; beyond 2 entries the model fails
-    loudly"""
+@pytest.mark.parametrize("exact", [False, True])
+def test_mw_sim_free_body_mesh_entries(N, tmp_path, exact):
+    """mw_sim's PGS-only free-body kernel (MW_LCP_PGS chosen before the load)
+    holds 2 shape entries of 8 slots: a mesh takes one entry per 8 support
+    points; beyond 2 entries the model fails loudly.  With the exact LCP (the
+    default) a joint-less body steps on the world-per-wavefront kernel, where
+    a mesh is one zero-radius sphere per support point (16 shapes, 32 slots):
+    all three bodies load."""
     path = str(tmp_path / "cube.stl")
     write_stl_binary(path, cube_vertices(), CUBE_TRIS)
     v, f = rock_vertices(7)
@@ -149,15 +153,21 @@ def test_mw_sim_free_body_mesh_entries(N, tmp_path):
     write_stl_binary(rock, v, f)
     cfg = N.MwConfig(1e-3, 1.0, 1, 2, 0, 0)
     for uri, extra, ok in ((path, "", True), (rock, "", True), (rock, '<collision><geometry><box size="0.1 0.1 0.1"/>'
-                                                                     '</geometry></collision>', False)):
+                                                                     '</geometry></collision>', exact)):
         h = ctypes.c_void_p()
         N.check(N.lib().mw_create(ctypes.byref(cfg), ctypes.byref(h)))
         try:
+            if not exact:
+                N.check(N.lib().mw_set_lcp_solver(h, N.LCP_PGS, 0))
             text = mesh_body_urdf(uri).replace("</link>", extra + "</link>")
             rc = N.lib().mw_load_model(h, text.encode(), N.dptr(IDENT), b"")
             assert (rc == 0) == ok, N.last_error()
             if not ok:
                 assert rc == N.MW_EPARSE and "entries" in N.last_error()
+            else:
+                m, k = ctypes.c_int32(), ctypes.c_int32()
+                N.check(N.lib().mw_lcp_solver(h, ctypes.byref(m), ctypes.byref(k)))
+                assert (m.value == N.LCP_EXACT) == exact
         finally:
             N.lib().mw_destroy(h)
 
