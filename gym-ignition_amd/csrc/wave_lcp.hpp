@@ -15,17 +15,18 @@
 //
 // Lane r owns row r: its Delassus row a[c] = A[r][c] (the PGS registers of
 // wave_step), its impulse x_r and its row data.  Each stage is a box QP with
-// fixed bounds, solved from the PGS impulses / the previous stage by
-//
-//   1. semismooth Newton (primal-dual active set): a row is held at a bound
-//      when its gradient g = A x - b pushes it outward, the rest are free; the
-//      reduced system A_FF d_F = -g_F is symmetric positive definite and is
-//      eliminated in lane order without a pivot search; the step is accepted
-//      when it lowers the largest complementarity residual (halved up to 3
-//      times), with the residual b - A x accumulated compensated (Dot2);
-//   2. if a Newton step cannot lower it: the primal active-set method (one
-//      bound joins or leaves the working set per linear solve), which is
-//      monotone and finite for a strictly convex QP,
+// fixed bounds, solved by the primal active-set method (wave_boxqp): the held
+// rows sit on a bound, the reduced system A_FF d_F = -g_F over the free rows is
+// symmetric positive definite and is eliminated in lane order without a pivot
+// search, one bound joins or leaves the working set per linear solve (monotone
+// and finite for a strictly convex QP), the residual b - A x accumulated
+// compensated (Dot2).  The working set starts from the previous step's (a row
+// on a bound last step starts held there), so a steady contact state costs one
+// linear solve per stage; PGS sweeps on the stage's box problem place the rows
+// without a record (new contacts).  A semismooth Newton start (every bound
+// change at once) was measured and dropped: on the standing humanoid's
+// redundant foot corners (cond(A) ~1e7) its steps raise the residual by 1e4
+// and fail their line search (scripts/proto_dantzig.py).
 //
 // within a budget of linear solves per world-step (both stages).  Converged =
 // every row's complementarity residual (oracle lcp_residual, velocity units)
@@ -40,7 +41,6 @@ namespace dev {
 
 constexpr float kLcpRelTol = 4e-6f;   // residual <= kLcpRelTol (|b| + sum |A_rc x_c|) + kLcpAbsTol
 constexpr float kLcpAbsTol = 1e-7f;   // m/s or rad/s
-constexpr int kLcpLineSearch = 3;     // step halvings of a Newton step
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
 // ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
@@ -108,7 +108,7 @@ struct LcpRow {
 // error by an FMA, the sum error by TwoSum, both carried in c), and
 // mag = sum_c |A[r][c] x_c| (the round-off scale of the residual test).  A
 // plain fp32 sum errs by ~R eps mag, a sizeable share of the tolerance, so
-// the last Newton steps would chase the matvec's own rounding.
+// the last refinement solves would chase the matvec's own rounding.
 template <int RC>
 __device__ __forceinline__ float lcp_matvec(const float (&a)[kWaveMaxRows], float xl, int n, float& mag) {
 #pragma clang fp contract(off)
@@ -186,14 +186,28 @@ constexpr int kLcpWorkFloats = 64 * kLcpUStride;  // the workspace the caller pr
 // rounds' principal submatrices A_FF, identity rows elsewhere), eliminated in
 // lane order without the pivot search -- the argmax's DPP chain is most of an
 // elimination step's dependent latency
+//
+// cols (pivot = false): the rows / columns that take part; row j outside it is
+// an identity row whose column is zero in every other row (a held row of the
+// active-set solve), so its step only shifts the registers and its d is 0.
 template <int RC>
-__device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U, bool pivot) {
+__device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U, bool pivot,
+                                              uint64_t cols = ~0ull) {
     static_assert(RC % 8 == 0, "row blocks of 8");
     const int lane = lane_id();
+    if (pivot) cols = ~0ull;
     bool used = lane >= n;
     for (int j = 0; j < n; ++j) {
-        const int p = pivot ? wave_argmax(used ? -1.f : fabsf(k[0])) : j;
         const int left = n - j;  // live columns
+        if (!mask_bit(cols, j)) {
+#pragma unroll
+            for (int c = 0; c < RC - 1; ++c) {
+                if ((c & 7) == 0 && c >= left) break;
+                k[c] = k[c + 1];
+            }
+            continue;
+        }
+        const int p = pivot ? wave_argmax(used ? -1.f : fabsf(k[0])) : j;
         float* row = U + j * kLcpUStride;
         if (lane == p) {
             float4* u = reinterpret_cast<float4*>(row);
@@ -232,7 +246,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
     // back substitution, right-looking: lane l holds row l (pivot of step l)
     wave_lds_sync();
     float acc = 0.f, rdiag = 1.f;
-    if (lane < n) {
+    if (lane < n && mask_bit(cols, lane)) {
         acc = U[lane * kLcpUStride + kLcpRhs];
         float dg = U[lane * kLcpUStride];
         dg = (fabsf(dg) < 1e-30f) ? 1e-30f : dg;
@@ -240,6 +254,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
     }
     float dl = 0.f;
     for (int j = n - 1; j >= 0; --j) {
+        if (!mask_bit(cols, j)) continue;
         const float dj = read_lane(acc * rdiag, j);
         dl = (lane == j) ? dj : dl;
         if (lane < j) acc = fmaf(-U[lane * (kLcpUStride - 1) + j], dj, acc);
@@ -248,52 +263,59 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 }
 
 // One strictly convex box QP  min 1/2 x'Ax - b'x,  L <= x <= U  (bounds fixed,
-// per lane; a dead or pinned row has L = U), from x (inside the box): the
-// semismooth Newton steps of the header, then the primal active-set method.
-// solves counts the linear solves against `budget`.  Returns true when every
-// row's residual is within tolerance.
+// per lane; a dead or pinned row has L = U) by the primal active-set method
+// from x (inside the box): the working set starts as ws0 (1 held at L, 2 held
+// at U, 0 free; -1: the start point's own -- at a bound or not), the held rows
+// sit on their bound, every linear solve minimises over the free rows (A_FF is
+// symmetric positive definite: no pivot search, the held rows' steps skipped)
+// and takes the longest step that stays in the box; the first bound met joins
+// the working set; at the working set's minimiser the held row whose
+// multiplier is wrongly signed by the most -- relative to its own tolerance,
+// as the residual test measures it -- leaves it.  If none is and the residual
+// still misses the tolerance, what remains is the fp32 solve's own error: one
+// more solve on the same working set from the compensated residual refines it
+// (iterative refinement).  solves counts the linear solves against `budget`.
+// Returns true when every row's residual is within tolerance.
 template <int RC>
 __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
-                                           float arr, int n, int budget, float* __restrict__ Uw, float& xl, int& solves,
-                                           int& iters, long long& ge_cycles) {
+                                           float arr, int n, int budget, float* __restrict__ Uw, float& xl, int ws0,
+                                           int& solves, int& iters, long long& ge_cycles) {
     const int lane = lane_id();
     const bool pinned = !live || U - L <= 0.f;
-    int phase = 0;         // 0 semismooth Newton, 1 primal active set
-    int ws = 0;            // phase 1 working set: 0 free, 1 held at L, 2 held at U
-    bool at_min = false;   // phase 1: the last step reached the working set's minimiser
-    for (int it = 0; it < 4 * budget + 8; ++it, ++iters) {
-        float mag;
-        const float w = lcp_matvec<RC>(a, xl, n, mag);
-        const float g = w - b;
-        const float xmax = wave_fmax(live ? fabsf(xl) : 0.f);
-        const float tolx = 2e-6f * (1.f + xmax);
-        float e_abs;
-        const float rel = wave_fmax(lcp_row_residual(live, b, xl, w, mag, arr, L, U, tolx, e_abs));
-        if (rel <= 1.f) return true;
-        if (phase == 1 && at_min) {
-            // minimiser on the working set: release the bound with the worst
-            // multiplier; if none is wrongly signed, the free rows' residual is
-            // the fp32 solve's own error -- one more solve on the same working
-            // set from the compensated residual refines it (iterative refinement)
+    int ws;
+    {
+        const float t0 = 2e-6f * (1.f + wave_fmax(live ? fabsf(xl) : 0.f));
+        const int own = (xl <= L + t0) ? 1 : ((xl >= U - t0) ? 2 : 0);
+        ws = pinned ? 1 : ((ws0 < 0) ? own : ws0);
+        xl = (ws == 1) ? L : ((ws == 2) ? U : xl);
+        xl = live ? xl : 0.f;
+    }
+    bool at_min = false;  // the last step reached the working set's minimiser
+    bool fresh = false;   // w / g / mag / xmax belong to the current x
+    float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f;
+    for (int it = 0; it < 4 * budget + 8 + n; ++it, ++iters) {
+        if (!fresh) {
+            w = lcp_matvec<RC>(a, xl, n, mag);
+            g = w - b;
+            xmax = wave_fmax(live ? fabsf(xl) : 0.f);
+            float e_abs;
+            const float rel = wave_fmax(lcp_row_residual(live, b, xl, w, mag, arr, L, U, 2e-6f * (1.f + xmax), e_abs));
+            if (rel <= 1.f) return true;
+            fresh = true;
+        }
+        if (at_min) {
             at_min = false;
             float v = (ws == 1) ? -g : ((ws == 2) ? g : 0.f);
-            v = pinned ? 0.f : v;
-            const float gm = wave_fmax(live ? fabsf(g) : 0.f);
+            v = pinned ? 0.f : v * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol);
             const int worst = wave_argmax(v);
-            if (read_lane(v, worst) > kLcpRelTol * (1.f + gm)) {
+            if (read_lane(v, worst) > 1.f) {
                 if (lane == worst) ws = 0;
                 continue;
             }
         }
         if (solves >= budget) return false;
-        // ---- one linear solve over the free rows (SPD: no pivot search)
-        bool fr;
-        if (phase == 0) {
-            const bool held = pinned || (xl <= L && g >= 0.f) || (xl >= U && g <= 0.f);
-            fr = !held;
-        } else {
-            fr = !pinned && ws == 0;
-        }
+        // ---- one linear solve over the free rows
+        const bool fr = !pinned && ws == 0;
         const uint64_t freeM = __ballot(fr);
         float k[RC];
 #pragma unroll
@@ -301,45 +323,20 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
 #ifdef MW_WAVE_PROF
         const long long tg0 = clock64();
 #endif
-        const float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, false);
+        const float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, false, freeM);
 #ifdef MW_WAVE_PROF
         ge_cycles += clock64() - tg0;
 #else
         (void)ge_cycles;
 #endif
         ++solves;
-        if (phase == 0) {
-            // monotone line search on the largest residual, iterates kept in the box
-            const float emax = wave_fmax(e_abs);
-            bool accepted = false;
-            float step = 1.f;
-            for (int ls = 0; ls <= kLcpLineSearch; ++ls, step *= 0.5f) {
-                const float xt = live ? fminf(fmaxf(xl + step * d, L), U) : xl;
-                float mt;
-                const float wt = lcp_matvec<RC>(a, xt, n, mt);
-                const float xmt = wave_fmax(live ? fabsf(xt) : 0.f);
-                float et;
-                (void)lcp_row_residual(live, b, xt, wt, mt, arr, L, U, 2e-6f * (1.f + xmt), et);
-                if (wave_fmax(et) < emax) {
-                    xl = xt;
-                    accepted = true;
-                    break;
-                }
-            }
-            if (!accepted) {
-                // the primal active-set method from here: working set = rows at a bound
-                phase = 1;
-                ws = pinned ? 1 : ((xl <= L) ? 1 : ((xl >= U) ? 2 : 0));
-                at_min = false;
-            }
-            continue;
-        }
-        // primal active set: the longest feasible step along d (at most 1)
-        const float dmax = wave_fmax(fabsf(d));
+        // the longest feasible step along d (at most 1)
+        const float dmax = wave_fmax(fr ? fabsf(d) : 0.f);
         if (dmax <= 1e-7f * (1.f + xmax)) {
             at_min = true;
             continue;
         }
+        fresh = false;
         float al = 1.f;
         int side = 0;
         if (fr && d < 0.f && xl + d < L) { al = (L - xl) * rcp(d); side = 1; }
@@ -411,14 +408,21 @@ __device__ __forceinline__ void wave_pgs_box(const float (&a)[kWaveMaxRows], F4*
 }
 
 // The exact solve, DART's two stages (header).  x1: lane r's stage-1 impulse
-// of the previous step (start of stage 1), returned as this step's stage-1
-// solution; xl: the previous step's final impulse (start of the friction
-// rows in stage 2), returned solved.  sweeps > 0: up to that many PGS sweeps
-// (tolerance exit pgs_tol) on each stage's box problem before its exact solve
-// (rc: the LDS row-constant array they use).  a: the Delassus registers
-// (a[c] = A[lane][c], CFM included).  Returns true when both stages
+// of the previous step, returned as this step's stage-1 solution; xl: the
+// previous step's final impulse, returned solved.  Each stage starts from the
+// previous step's impulse of the stage (projected onto this step's boxes),
+// runs up to min(sweeps, kLcpStageSweeps) PGS sweeps on the stage's box
+// problem (tolerance exit pgs_tol; rc: the LDS row-constant array they use),
+// then the active-set method from the previous step's working set: a row that
+// sat on a bound of its stage's box last step starts held there; a row with a
+// zero impulse last step (no record: a new contact, or a friction row of a
+// contact without normal force) takes the class of the PGS point.  At a
+// steady contact state that is one linear solve per stage.  a: the Delassus
+// registers (a[c] = A[lane][c], CFM included).  Returns true when both stages
 // converged within max_solves linear solves in total; n_solves / n_rounds /
 // n_solves2: linear solves, iterations, linear solves of stage 2.
+constexpr int kLcpStageSweeps = 12;
+
 template <int RC>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
@@ -428,25 +432,41 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
     float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
 #pragma unroll
     for (int c = 0; c < RC; ++c) arr = (lane == c && R.live) ? a[c] : arr;
+    sweeps = sweeps < kLcpStageSweeps ? sweeps : kLcpStageSweeps;
     int solves = 0, iters = 0;
     const bool fric = R.kind == 1;
+    const float x1p = R.live ? x1 : 0.f, xlp = R.live ? xl : 0.f;  // the previous step's
     // stage 1: normal and joint rows; friction impulses pinned at 0
-    float L = (fric || !R.live) ? 0.f : R.lo;
-    float U = (fric || !R.live) ? 0.f : R.hi;
-    float x = fminf(fmaxf(x1, L), U);
-    if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L, U, n, sweeps, pgs_tol, x);
-    const bool ok1 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, solves, iters, ge_cycles);
+    const float L1 = (fric || !R.live) ? 0.f : R.lo;
+    const float U1 = (fric || !R.live) ? 0.f : R.hi;
+    int ws;
+    {
+        const float t = 2e-6f * (1.f + wave_fmax(fabsf(x1p)));
+        ws = (x1p == 0.f) ? -1 : ((x1p <= L1 + t) ? 1 : ((x1p >= U1 - t) ? 2 : 0));
+    }
+    float x = fminf(fmaxf(x1p, L1), U1);
+    if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L1, U1, n, sweeps, pgs_tol, x);
+    const bool ok1 = wave_boxqp<RC>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     x1 = R.live ? x : 0.f;
     const int s1 = solves;
-    // stage 2: each friction row boxed by mu x_n of its contact's stage-1 normal
+    // stage 2: each friction row boxed by mu x_n of its contact's stage-1
+    // normal; the previous step's boxes from its own stage-1 normals
     const float xn1 = gather_normal<RC>(x, R, n);
+    const float xn1p = gather_normal<RC>(x1p, R, n);
+    float L = L1, U = U1, Lp = L1, Up = U1;
     if (fric && R.live) {
         U = mu * fmaxf(xn1, 0.f);
         L = -U;
-        x = fminf(fmaxf(xl, L), U);
+        Up = mu * fmaxf(xn1p, 0.f);
+        Lp = -Up;
     }
+    {
+        const float t = 2e-6f * (1.f + wave_fmax(fabsf(xlp)));
+        ws = (xlp == 0.f || Up - Lp <= 0.f) ? -1 : ((xlp <= Lp + t) ? 1 : ((xlp >= Up - t) ? 2 : 0));
+    }
+    x = fminf(fmaxf(xlp, L), U);
     if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L, U, n, sweeps, pgs_tol, x);
-    const bool ok2 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, solves, iters, ge_cycles);
+    const bool ok2 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     xl = R.live ? x : 0.f;
     n_solves = solves;
     n_rounds = iters;

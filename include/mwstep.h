@@ -241,10 +241,11 @@ int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
  * whose friction index boxes every friction row once, by mu x the normal
  * impulses of the frictionless problem -- two strictly convex box QPs
  * (wave_lcp.hpp), each from the previous step's solution, PGS sweeps on the
- * stage's box problem (at most mw_config.pgs_iters, ending once a sweep moves
- * no constraint velocity by more than 1e-6), then semismooth Newton /
- * active-set rounds with at most max_solves dense linear solves (elimination
- * over the wave's lanes) per world-step.  It runs on the world-per-wavefront
+ * stage's box problem (at most min(mw_config.pgs_iters, 12), ending once a
+ * sweep moves no constraint velocity by more than 1e-6), then the primal
+ * active-set method from the previous step's working set, with at most
+ * max_solves dense linear solves (elimination over the wave's lanes) per
+ * world-step.  It runs on the world-per-wavefront
  * kernel, which then steps every floating model (joint-less bodies, small
  * trees at any world count).  MW_LCP_PGS: the coupled PGS sweeps alone (cold
  * unless mw_set_pgs_options asks for the warm start); chosen before
