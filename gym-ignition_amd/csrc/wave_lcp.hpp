@@ -39,8 +39,19 @@
 namespace mw {
 namespace dev {
 
-constexpr float kLcpRelTol = 4e-6f;   // residual <= kLcpRelTol (|b| + sum |A_rc x_c|) + kLcpAbsTol
-constexpr float kLcpAbsTol = 1e-7f;   // m/s or rad/s
+// residual <= kLcpRelTol (|b| + sum |A_rc x_c|) + kLcpAbsTol: 16 fp32 ulps of
+// the row's terms (the compensated residual is accurate to ~1 ulp; rounding x
+// to fp32 moves it by ~1 ulp of mag).  At 4e-6 (r04c) a resting cube kept
+// 1.5e-4 N of tangential force and a redundant corner could stay unloaded
+// (its multiplier, set by DART's CFM, sat inside the tolerance).
+constexpr float kLcpRelTol = 1e-6f;
+constexpr float kLcpAbsTol = 1e-8f;   // m/s or rad/s
+// a refinement solve that moves no impulse by more than this (relative to
+// 1 + max |x|) has reached the fp32 floor of its working set
+constexpr float kLcpStall = 1e-7f;
+// at the floor a stage counts as converged when its residual is within this
+// factor of the tolerance
+constexpr float kLcpFloorAccept = 64.f;
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
 // ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
@@ -274,7 +285,9 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 // as the residual test measures it -- leaves it.  If none is and the residual
 // still misses the tolerance, what remains is the fp32 solve's own error: one
 // more solve on the same working set from the compensated residual refines it
-// (iterative refinement).  solves counts the linear solves against `budget`.
+// (iterative refinement), until a refinement moves nothing (kLcpStall: the
+// fp32 floor; converged if within kLcpFloorAccept of the tolerance).  solves
+// counts the linear solves against `budget`.
 // Returns true when every row's residual is within tolerance.
 template <int RC>
 __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
@@ -291,15 +304,16 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         xl = live ? xl : 0.f;
     }
     bool at_min = false;  // the last step reached the working set's minimiser
-    bool fresh = false;   // w / g / mag / xmax belong to the current x
-    float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f;
+    bool stalled = false; // ... by a refinement solve that moved nothing
+    bool fresh = false;   // w / g / mag / xmax / rel belong to the current x
+    float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f, rel = 0.f;
     for (int it = 0; it < 4 * budget + 8 + n; ++it, ++iters) {
         if (!fresh) {
             w = lcp_matvec<RC>(a, xl, n, mag);
             g = w - b;
             xmax = wave_fmax(live ? fabsf(xl) : 0.f);
             float e_abs;
-            const float rel = wave_fmax(lcp_row_residual(live, b, xl, w, mag, arr, L, U, 2e-6f * (1.f + xmax), e_abs));
+            rel = wave_fmax(lcp_row_residual(live, b, xl, w, mag, arr, L, U, 2e-6f * (1.f + xmax), e_abs));
             if (rel <= 1.f) return true;
             fresh = true;
         }
@@ -310,8 +324,12 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
             const int worst = wave_argmax(v);
             if (read_lane(v, worst) > 1.f) {
                 if (lane == worst) ws = 0;
+                stalled = false;
                 continue;
             }
+            // every multiplier is signed right and the last solve on this
+            // working set was a refinement that moved nothing: the fp32 floor
+            if (stalled) return rel <= kLcpFloorAccept;
         }
         if (solves >= budget) return false;
         // ---- one linear solve over the free rows
@@ -332,10 +350,12 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         ++solves;
         // the longest feasible step along d (at most 1)
         const float dmax = wave_fmax(fr ? fabsf(d) : 0.f);
-        if (dmax <= 1e-7f * (1.f + xmax)) {
+        if (dmax <= kLcpStall * (1.f + xmax)) {
             at_min = true;
+            stalled = true;
             continue;
         }
+        stalled = false;
         fresh = false;
         float al = 1.f;
         int side = 0;

@@ -64,7 +64,9 @@ def capture(n_worlds=8, steps=60, seed=21):
     return out
 
 f32 = np.float32
-REL, ABS = 4e-6, 1e-7
+REL, ABS = float(os.environ.get("REL", "1e-6")), float(os.environ.get("ABS", "1e-7"))
+FLOOR = os.environ.get("FLOOR", "1") != "0"
+MINSOLVE = os.environ.get("MINSOLVE", "0") != "0"
 SWEEPS = int(os.environ.get("SWEEPS", "50"))
 BUDGET = int(os.environ.get("BUDGET", "24"))
 REFINE = int(os.environ.get("REFINE", "1"))
@@ -131,16 +133,23 @@ def boxqp(A, b, L, U, x, budget, stats, ws0=None):
     for _ in range(4 * budget + 8):
         rel, e, w = residual(A, b, x, L, U, arr)
         g = w - b
-        if rel <= 1:
+        if rel <= 1 and (solves > 0 or not MINSOLVE or not (~pinned & (ws == 0)).any()):
             return x, solves, True
         if phase == 1 and at_min:
             at_min = False
+            tiny_last_ = stats.get("_tiny", False)
             v = np.where(ws == 1, -g, np.where(ws == 2, g, 0)).astype(f32)
             v[pinned] = 0
             v = v / (REL * (np.abs(b) + matvec(A, x)[1]) + ABS)
             if v.max(initial=0) > 1:
                 ws[int(np.argmax(v))] = 0
+                stats["_tiny"] = False
                 continue
+            if tiny_last_ and FLOOR:
+                # the last solve on this working set was a refinement that moved
+                # nothing: the fp32 floor
+                stats["floor"] = stats.get("floor", 0) + 1
+                return x, solves, rel <= 64
             if not REFINE:
                 return x, solves, False
         if solves >= budget:
@@ -179,7 +188,9 @@ def boxqp(A, b, L, U, x, budget, stats, ws0=None):
             continue
         if np.abs(d).max(initial=0) <= 1e-7 * (1 + np.abs(x).max(initial=0)):
             at_min = True
+            stats["_tiny"] = True
             continue
+        stats["_tiny"] = False
         al = np.ones(n, f32)
         lo_hit = fr & (d < 0) & (x + d < L)
         hi_hit = fr & (d > 0) & (x + d > U)
