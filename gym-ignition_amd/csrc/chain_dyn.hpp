@@ -247,7 +247,7 @@ __device__ __forceinline__ SI rigid(const BodyF& b, float m) {
 // the runtime joint type becomes a select between two stack objects, i.e.
 // scratch stores + loads (seen as 2x WRITE_SIZE in the r01 PMC pass).
 __device__ __forceinline__ SV motion(const BodyF& b, float s) {
-    const bool rev = (b.jtype == 0);
+    const bool rev = ((b.jtype & 1) == 0);
     const float sw = rev ? s : 0.f, sv = rev ? 0.f : s;
     return {{b.axis[0] * sw, b.axis[1] * sw, b.axis[2] * sw}, {b.axis[0] * sv, b.axis[1] * sv, b.axis[2] * sv}};
 }
@@ -260,13 +260,13 @@ __device__ __forceinline__ float proj(const BodyF& b, const SV& x) {
     const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
     const float dw = dot(a, x.w);
     const float dv = dot(a, x.v);
-    return (b.jtype == 0) ? dw : dv;
+    return ((b.jtype & 1) == 0) ? dw : dv;
 }
 
 // AI S for the body's joint: revolute S = [a; 0] -> [A a; B^T a],
 // prismatic S = [0; a] -> [B a; C a]  (component selects, see motion())
 __device__ __forceinline__ SV ais(const SI& AI, const BodyF& b) {
-    const bool rev = (b.jtype == 0);
+    const bool rev = ((b.jtype & 1) == 0);
     const f3 a = {b.axis[0], b.axis[1], b.axis[2]};
     const f3 Aa = mul(AI.A, a), Bta = mulT(AI.B, a), Ba = mul(AI.B, a), Ca = mul(AI.C, a);
     return {{rev ? Aa.x : Ba.x, rev ? Aa.y : Ba.y, rev ? Aa.z : Ba.z},
@@ -384,7 +384,7 @@ __device__ __forceinline__ void sincos_joint(float x, float* s_out, float* c_out
 }
 
 __device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p) {
-    if (b.jtype == 0) {
+    if ((b.jtype & 1) == 0) {
         float s, c;
         sincos_joint(q, &s, &c);
         const float ax = b.axis[0], ay = b.axis[1], az = b.axis[2], v = 1.f - c;
@@ -402,6 +402,94 @@ __device__ __forceinline__ void joint_pose(const BodyF& b, float q, M3& R, f3& p
         for (int k = 0; k < 9; ++k) R.m[k] = b.E[k];
         p = {b.r[0] + q * b.Ea[0], b.r[1] + q * b.Ea[1], b.r[2] + q * b.Ea[2]};
     }
+}
+
+// DART's BallJoint (oracle.c ball_part; Joint.cpp:267-331 exposes it as
+// core::JointType::Ball): positions = the rotation vector theta, velocities =
+// the child's angular velocity in its own frame (relative Jacobian [I; 0],
+// constant), positions integrated on SO(3) as R <- R exp(dt w).  The model
+// lists it as three bodies at one point, BodyF::jtype bits 4-5 = part 1, 2, 3
+// (unit axes x, y, z; the first two massless): part 1 carries the whole
+// rotation E exp(theta), theta = (q_i, q_i+1, q_i+2); parts 2 and 3 have
+// identity transforms.  Only the world-per-wavefront and scene kernels step
+// such models (sim.cpp routes them there).
+__device__ __forceinline__ int ball_part(const BodyF& b) { return (b.jtype >> 4) & 3; }
+
+// E exp(theta) (Rodrigues; 1 - cos t written 2 sin^2(t/2): no cancellation)
+__device__ __forceinline__ void ball_rot(const BodyF& b, float tx, float ty, float tz, M3& R) {
+    const float t2 = tx * tx + ty * ty + tz * tz;
+    const float t = sqrtf(t2);
+    float sh, ch;
+    sincos_joint(0.5f * t, &sh, &ch);
+    const bool tiny = t < 1e-12f;
+    const float it = tiny ? 0.f : rcp(t);
+    const float A = tiny ? 1.f : 2.f * sh * ch * it;  // sin t / t
+    const float hs = tiny ? 0.5f : sh * it;           // sin(t/2) / t
+    const float B = 2.f * hs * hs;                    // (1 - cos t) / t^2
+    const float K[9] = {0.f, -tz, ty, tz, 0.f, -tx, -ty, tx, 0.f};
+    float X[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            X[r * 3 + c] = ((r == c) ? 1.f : 0.f) + A * K[r * 3 + c] +
+                           B * (K[r * 3] * K[c] + K[r * 3 + 1] * K[3 + c] + K[r * 3 + 2] * K[6 + c]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            R.m[r * 3 + c] = b.E[r * 3] * X[c] + b.E[r * 3 + 1] * X[3 + c] + b.E[r * 3 + 2] * X[6 + c];
+}
+
+// joint transform of body i from the tree's coordinates q (a ball joint's
+// part 1 reads q[i .. i + 2]; its parts 2 and 3 do not move)
+__device__ __forceinline__ void joint_pose_tree(const BodyF& b, const float* q, int i, M3& R, f3& p) {
+    const int bp = ball_part(b);
+    if (bp == 0) {
+        joint_pose(b, q[i], R, p);
+        return;
+    }
+    if (bp == 1) {
+        ball_rot(b, q[i], q[i + 1], q[i + 2], R);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.m[k] = b.E[k];
+    }
+    p = {b.r[0], b.r[1], b.r[2]};
+}
+
+// the velocity a joint's velocity-product term ad(V, S qd) sees: a ball
+// joint's parts 2 and 3 without the ball's earlier parts (one joint of
+// constant S; oracle.c joint_bias)
+__device__ __forceinline__ SV ball_bias_velocity(const BodyF& b, const float* qd, int i, SV V) {
+    const int bp = ball_part(b);
+    if (bp >= 2) V.w.x -= qd[i - bp + 1];
+    if (bp == 3) V.w.y -= qd[i - 1];
+    return V;
+}
+
+// component k of a ball joint's new position log(exp(theta) exp(dt w)),
+// theta = th[0..2], w = w[0..2] (quaternion product; angle in [0, pi])
+__device__ __forceinline__ float ball_integrate(float t0, float t1, float t2, float w0, float w1, float w2, float dt,
+                                                int k) {
+    auto quat = [](float x, float y, float z, float (&qt)[4]) {
+        const float t = sqrtf(x * x + y * y + z * z);
+        float sh, ch;
+        sincos_joint(0.5f * t, &sh, &ch);
+        const float s = (t < 1e-12f) ? 0.5f : sh * rcp(t);
+        qt[0] = ch; qt[1] = s * x; qt[2] = s * y; qt[3] = s * z;
+    };
+    float a[4], b[4];
+    quat(t0, t1, t2, a);
+    quat(dt * w0, dt * w1, dt * w2, b);
+    float c0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    float c1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    float c2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    float c3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+    if (c0 < 0.f) { c0 = -c0; c1 = -c1; c2 = -c2; c3 = -c3; }
+    const float v = sqrtf(c1 * c1 + c2 * c2 + c3 * c3);
+    const float f = (v < 1e-20f) ? 2.f * rcp(c0) : 2.f * atan2f(v, c0) * rcp(v);
+    return f * ((k == 0) ? c1 : ((k == 1) ? c2 : c3));
 }
 
 // ABA with implicit damping over the kinematic tree TOPO: fills W, returns qdd.

@@ -151,7 +151,7 @@ __device__ __forceinline__ GBody<N> load_gbody(const ChainF* __restrict__ P, int
     g.lower = b.lower;
     g.upper = b.upper;
     g.effort = b.effort;
-    g.prism = body ? b.jtype : 0;
+    g.prism = body ? (b.jtype & 1) : 0;
     g.limited = body ? b.limited : 0;
     g.parent = body ? b.parent : -1;
     const uint32_t anc = body ? b.anc : 0u;

@@ -234,7 +234,7 @@ void build_params(mw_scene* s) {
                 f.Ea[k] = static_cast<float>(snap(b.E[k * 3] * b.axis[0] + b.E[k * 3 + 1] * b.axis[1] +
                                                   b.E[k * 3 + 2] * b.axis[2]));
             }
-            f.jtype = (b.type == mw::JType::Prismatic) ? 1 : 0;
+            f.jtype = ((b.type == mw::JType::Prismatic) ? 1 : 0) | (b.ball << 4);  // chain_dyn.hpp ball_part
             f.mass = static_cast<float>(b.mass);
             const double bc2 = b.com[0] * b.com[0] + b.com[1] * b.com[1] + b.com[2] * b.com[2];
             f.Io[0] = static_cast<float>(b.Ic[0] + b.mass * (bc2 - b.com[0] * b.com[0]));

@@ -692,13 +692,14 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 p = pw;
                 eta = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
             } else {
-                joint_pose(b, L.q[bi], R, p);
+                joint_pose_tree(b, L.q, bi, R, p);
                 const SV Sq = motion(b, L.qd[bi]);
                 const ScNode& pn = L.node[pnode];
                 V = ad_inv(R, p, pn.V) + Sq;
                 Rw = mul3(pn.Rw, R);
                 pw = pn.pw + mul(pn.Rw, p);
-                eta = {cross(V.w, Sq.w), cross(V.w, Sq.v) + cross(V.v, Sq.w)};
+                const SV Ve = ball_bias_velocity(b, L.qd, bi, V);
+                eta = {cross(Ve.w, Sq.w), cross(Ve.w, Sq.v) + cross(Ve.v, Sq.w)};
                 B = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), V, mulT(Rw, gw));
             }
             B = B + (-1.f) * SV{mulT(Rw, Tw), mulT(Rw, Fw)};
@@ -1133,13 +1134,13 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 static_assert(sizeof(L.A) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
                 float* Uw = &L.A[0][0];
                 int nsolve = 0, nround = 0, nsolve1 = 0;
-                long long ge_cyc = 0;
+                long long cyc[3] = {0, 0, 0};
                 // both stages start from the sweeps' impulses (no per-stage sweeps)
                 float x1 = x0;
                 const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, 0, 0.f, nullptr, Uw, x1, x0,
-                                                                nsolve, nround, nsolve1, ge_cyc)
+                                                                nsolve, nround, nsolve1, cyc)
                                            : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, 0, 0.f, nullptr, Uw,
-                                                                          x1, x0, nsolve, nround, nsolve1, ge_cyc);
+                                                                          x1, x0, nsolve, nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
                 x0 = Rw.live ? x0 : 0.f;
             }
@@ -1225,12 +1226,23 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 
     MW_SC_CHECK(5, nc);
     // ---- integratePositions
+    // (a ball joint's three lanes read each other's coordinates: every lane
+    // forms its new q before any is stored)
+    float q_new = 0.f;
     if (isbody && alive) {
         const float qn = L.nu[P->body_coord[bi]];
         L.qdd[bi] = (qn - L.qd[bi]) * rcp(dt);
         L.qd[bi] = qn;
-        L.q[bi] += dt * qn;
+        q_new = L.q[bi] + dt * qn;
+        const int bp = ball_part(P->b[bi]);
+        if (bp) {
+            const int i0 = bi - bp + 1;
+            q_new = ball_integrate(L.q[i0], L.q[i0 + 1], L.q[i0 + 2], L.nu[P->body_coord[i0]],
+                                   L.nu[P->body_coord[i0 + 1]], L.nu[P->body_coord[i0 + 2]], dt, bp - 1);
+        }
     }
+    __threadfence_block();
+    if (isbody && alive) L.q[bi] = q_new;
     if (isbase && alive && md.floating) {
         const int o = md.coff;
         const SV Vn = {{L.nu[o], L.nu[o + 1], L.nu[o + 2]}, {L.nu[o + 3], L.nu[o + 4], L.nu[o + 5]}};

@@ -224,7 +224,7 @@ void build_params(mw_sim* s) {
             f.Ea[k] = static_cast<float>(snap(b.E[k * 3] * b.axis[0] + b.E[k * 3 + 1] * b.axis[1] +
                                               b.E[k * 3 + 2] * b.axis[2]));
         }
-        f.jtype = (b.type == mw::JType::Prismatic) ? 1 : 0;
+        f.jtype = ((b.type == mw::JType::Prismatic) ? 1 : 0) | (b.ball << 4);  // chain_dyn.hpp ball_part
         f.mass = static_cast<float>(b.mass);
         // inertia about the body origin: Ic + m (|c|^2 1 - c c^T)
         const double c2 = b.com[0] * b.com[0] + b.com[1] * b.com[1] + b.com[2] * b.com[2];
@@ -671,12 +671,16 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
                                "scene (World.insert_model) where it is a collider");
     s->floating = s->model.floating;
     s->fixed_tree = false;
+    // ball joints (DART's BallJoint coordinates, chain_dyn.hpp ball_part):
+    // the world-per-wavefront kernel only
+    bool has_ball = false;
+    for (const auto& b : s->model.bodies) has_ball = has_ball || b.ball != 0;
     if (!s->floating) {
         // fixed bases: the compiled chain topologies run on the lane kernels,
         // every other tree on the world-per-wavefront kernel with a welded base
         std::vector<int> parents;
         for (const auto& b : s->model.bodies) parents.push_back(b.parent);
-        s->fixed_tree = s->model.dofs() > 9 || mw::kernel_topology(parents.data(), s->model.dofs()) < 0;
+        s->fixed_tree = s->model.dofs() > 9 || mw::kernel_topology(parents.data(), s->model.dofs()) < 0 || has_ball;
     }
     s->float_tree = (s->floating && (s->model.dofs() > 0 || free_wave)) || s->fixed_tree;
     if (s->float_tree) {
@@ -710,9 +714,9 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
         // MWSTEP_WAVE_TREE=1 / =0 forces the wave / lane kernel.
         constexpr int kWaveWorldsMax = 4096;
         if (force_wave && *force_wave)
-            s->wave = !compiled || *force_wave != '0' || damped;
+            s->wave = !compiled || *force_wave != '0' || damped || has_ball;
         else
-            s->wave = !compiled || s->W <= kWaveWorldsMax || damped || exact;
+            s->wave = !compiled || s->W <= kWaveWorldsMax || damped || exact || has_ball;
         if (s->fixed_tree) s->wave = true;  // the lane kernel has no welded-base mode
         {
             std::vector<int> depth(s->n, 0);
@@ -1364,7 +1368,7 @@ int mw_model_export(const mw_sim* s, double* out, int32_t len) {
     if (len < 34 * n + 3) return fail(MW_EINVAL, "export buffer too small");
     double* o = out;
     for (const mw::ChainBody& b : s->model.bodies) {
-        *o++ = (b.type == mw::JType::Prismatic) ? 1.0 : 0.0;
+        *o++ = static_cast<double>(((b.type == mw::JType::Prismatic) ? 1 : 0) | (b.ball << 4));
         *o++ = b.limited ? 1.0 : 0.0;
         for (double v : b.E) *o++ = v;
         for (double v : b.r) *o++ = v;

@@ -447,7 +447,13 @@ template <int RC>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
                                                float* __restrict__ Uw, float& x1, float& xl, int& n_solves,
-                                               int& n_rounds, int& n_solves2, long long& ge_cycles) {
+                                               int& n_rounds, int& n_solves2, long long (&cyc)[3]) {
+    // cyc (MW_WAVE_PROF builds): [0] cycles in the linear solves, [1] in the
+    // PGS sweeps, [2] in stage 1
+    long long& ge_cycles = cyc[0];
+#ifdef MW_WAVE_PROF
+    const long long tc0 = clock64();
+#endif
     const int lane = lane_id();
     float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
 #pragma unroll
@@ -465,9 +471,18 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
         ws = (x1p == 0.f) ? -1 : ((x1p <= L1 + t) ? 1 : ((x1p >= U1 - t) ? 2 : 0));
     }
     float x = fminf(fmaxf(x1p, L1), U1);
+#ifdef MW_WAVE_PROF
+    long long tp = clock64();
+#endif
     if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L1, U1, n, sweeps, pgs_tol, x);
+#ifdef MW_WAVE_PROF
+    cyc[1] += clock64() - tp;
+#endif
     const bool ok1 = wave_boxqp<RC>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     x1 = R.live ? x : 0.f;
+#ifdef MW_WAVE_PROF
+    cyc[2] += clock64() - tc0;
+#endif
     const int s1 = solves;
     // stage 2: each friction row boxed by mu x_n of its contact's stage-1
     // normal; the previous step's boxes from its own stage-1 normals
@@ -485,7 +500,13 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
         ws = (xlp == 0.f || Up - Lp <= 0.f) ? -1 : ((xlp <= Lp + t) ? 1 : ((xlp >= Up - t) ? 2 : 0));
     }
     x = fminf(fmaxf(xlp, L), U);
+#ifdef MW_WAVE_PROF
+    tp = clock64();
+#endif
     if (sweeps > 0) wave_pgs_box<RC>(a, rc, R.live, R.b, arr, L, U, n, sweeps, pgs_tol, x);
+#ifdef MW_WAVE_PROF
+    cyc[1] += clock64() - tp;
+#endif
     const bool ok2 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     xl = R.live ? x : 0.f;
     n_solves = solves;

@@ -107,9 +107,10 @@ __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x &
 
 // Phase timing (debug builds only: EXTRA=-DMW_WAVE_PROF, scripts/wave_prof.py):
 // shader-clock cycles per phase, summed over the worlds of a launch.
-constexpr int kWaveProfPhases = 16;  // [8] exact-LCP linear solves, [9] its rounds, [10] staggered-round solves,
-                                     // [11] / [12] max solves / staggered solves of a world-step, [13] world-steps > 4 solves,
-                                     // [14] cycles in the linear solves, [15] in the PGS sweeps
+constexpr int kWaveProfPhases = 20;  // [8] exact-LCP linear solves, [9] its rounds, [10] stage-2 solves,
+                                     // [11] / [12] max solves / stage-2 solves of a world-step, [13] world-steps > 4 solves,
+                                     // [14] cycles in the linear solves, [15] in the PGS sweeps / the exact solve,
+                                     // [16] in the exact solve's per-stage sweeps, [17] in its stage 1
 #ifdef MW_WAVE_PROF
 __device__ unsigned long long g_wave_prof[kWaveProfPhases];
 #define MW_PROF_T(var) const long long var = clock64()
@@ -176,7 +177,7 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     float tau = 0.f;
     for (int d = 0; d < levels; ++d) {
         if (depth == d) {
-            joint_pose(b, L.q[i], R, p);
+            joint_pose_tree(b, L.q, i, R, p);
             const SV Sq = motion(b, L.qd[i]);
             const SV Vp = (pa >= 0) ? L.body[pa].V : V0;
             const M3 Rwp = (pa >= 0) ? L.body[pa].Rw : R0;
@@ -189,7 +190,8 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
                     Rw.m[r * 3 + c] =
                         Rwp.m[r * 3] * R.m[c] + Rwp.m[r * 3 + 1] * R.m[3 + c] + Rwp.m[r * 3 + 2] * R.m[6 + c];
             pw = pwp + mul(Rwp, p);
-            eta = {cross(V.w, Sq.w), cross(V.w, Sq.v) + cross(V.v, Sq.w)};
+            const SV Ve = ball_bias_velocity(b, L.qd, i, V);
+            eta = {cross(Ve.w, Sq.w), cross(Ve.w, Sq.v) + cross(Ve.v, Sq.w)};
             B = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), V,
                            mulT(Rw, gw));
             L.body[i].V = V;
@@ -725,11 +727,11 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             static_assert(sizeof(L.stack) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
             float* U = &L.stack[0][0][0];
             int nsolve = 0, nround = 0, nsolve1 = 0;
-            long long ge_cyc = 0;
+            long long cyc[3] = {0, 0, 0};
             const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
-                                                           nsolve, nround, nsolve1, ge_cyc)
+                                                           nsolve, nround, nsolve1, cyc)
                                       : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
-                                                                     L.rc, U, x1s, xe, nsolve, nround, nsolve1, ge_cyc);
+                                                                     L.rc, U, x1s, xe, nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
             prof[8] += static_cast<unsigned long long>(nsolve);
             prof[9] += static_cast<unsigned long long>(nround);
@@ -737,10 +739,12 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             prof[11] = prof[11] > static_cast<unsigned long long>(nsolve) ? prof[11] : nsolve;
             prof[12] = prof[12] > static_cast<unsigned long long>(nsolve1) ? prof[12] : nsolve1;
             prof[13] += nsolve > 4 ? 1ull : 0ull;
-            prof[14] += static_cast<unsigned long long>(ge_cyc);
+            prof[14] += static_cast<unsigned long long>(cyc[0]);
+            prof[16] += static_cast<unsigned long long>(cyc[1]);
+            prof[17] += static_cast<unsigned long long>(cyc[2]);
 #else
             (void)nsolve1;
-            (void)ge_cyc;
+            (void)cyc;
 #endif
 #pragma unroll
             for (int r = 0; r < kWaveMaxRows; ++r) {
@@ -792,12 +796,23 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
     }
 
     // ---- integratePositions ---------------------------------------------------
+    // (a ball joint's three lanes read each other's coordinates: every lane
+    // forms its new q before any is stored)
+    float q_new = 0.f;
     if (lane < N) {
         const float qd_new = L.nu[6 + lane];
         qdd_out[lane] = (qd_new - L.qd[lane]) * rcp(dt);
         L.qd[lane] = qd_new;
-        L.q[lane] += dt * qd_new;
+        q_new = L.q[lane] + dt * qd_new;
+        const int bp = ball_part(P->b[lane]);
+        if (bp) {
+            const int i0 = lane - bp + 1;
+            q_new = ball_integrate(L.q[i0], L.q[i0 + 1], L.q[i0 + 2], L.nu[6 + i0], L.nu[7 + i0], L.nu[8 + i0], dt,
+                                   bp - 1);
+        }
     }
+    wave_lds_sync();
+    if (lane < N) L.q[lane] = q_new;
     const SV V = {{L.nu[0], L.nu[1], L.nu[2]}, {L.nu[3], L.nu[4], L.nu[5]}};
     integrate_pose(R0, V, dt, base);
     base.V = V;

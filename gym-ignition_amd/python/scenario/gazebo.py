@@ -382,46 +382,13 @@ class Joint:
 
 
 # ------------------------------------------------------------------ BallJoint
-# A ball joint (core::JointType::Ball, 3 dofs, Joint.cpp:318-331) is compiled
-# as three revolute dofs `<name>#x/#y/#z` about the axes of its frame at one
-# point (csrc/model.cpp): intrinsic X-Y-Z angles (a, b, c), R = Rx(a) Ry(b)
-# Rz(c).  This class presents DART's BallJoint coordinates over them:
-# positions = the rotation vector of R, velocities = the child's angular
-# velocity in the child frame w = J(b, c) [a', b', c'], accelerations = w',
-# forces = torques in the child frame (tau_angles = J^T tau).  J is singular
-# at b = +-pi/2 (the angle parameterisation's gimbal lock).
-def _rx(a):
-    c, s = math.cos(a), math.sin(a)
-    return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
-
-
-def _ry(b):
-    c, s = math.cos(b), math.sin(b)
-    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
-
-
-def _rz(c_):
-    c, s = math.cos(c_), math.sin(c_)
-    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
-
-
-def ball_R(e) -> np.ndarray:
-    return _rx(e[0]) @ _ry(e[1]) @ _rz(e[2])
-
-
-def ball_J(e) -> np.ndarray:
-    """child-frame angular velocity per angle rate: w = J(e) e'"""
-    cb, sb, cc, sc = math.cos(e[1]), math.sin(e[1]), math.cos(e[2]), math.sin(e[2])
-    return np.array([[cb * cc, sc, 0.0], [-cb * sc, cc, 0.0], [sb, 0.0, 1.0]])
-
-
-def ball_Jdot(e, ed) -> np.ndarray:
-    cb, sb, cc, sc = math.cos(e[1]), math.sin(e[1]), math.cos(e[2]), math.sin(e[2])
-    db = np.array([[-sb * cc, 0, 0], [sb * sc, 0, 0], [cb, 0, 0]])
-    dc = np.array([[-cb * sc, cc, 0], [-cb * cc, -sc, 0], [0, 0, 0]])
-    return db * ed[1] + dc * ed[2]
-
-
+# A ball joint (core::JointType::Ball, 3 dofs, Joint.cpp:318-331) runs in
+# DART's BallJoint coordinates natively (csrc/chain_dyn.hpp ball_part, oracle.c
+# ball_part): its three internal dofs `<name>#x/#y/#z` ARE the rotation vector
+# of the joint rotation (positions), the child's angular velocity in the child
+# frame (velocities, accelerations) and the child-frame torque (forces); the
+# kernels integrate the positions on SO(3), R <- R exp(dt w).  No angle
+# parameterisation, so no gimbal singularity.
 def rotvec_from_R(R) -> np.ndarray:
     """log map of SO(3) (the rotation vector, DART BallJoint positions)"""
     c = max(-1.0, min(1.0, (np.trace(R) - 1.0) / 2.0))
@@ -448,16 +415,8 @@ def R_from_rotvec(r) -> np.ndarray:
     return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
 
 
-def ball_angles(R) -> np.ndarray:
-    """(a, b, c) with Rx(a) Ry(b) Rz(c) = R, b in [-pi/2, pi/2]"""
-    b = math.asin(max(-1.0, min(1.0, R[0, 2])))
-    a = math.atan2(-R[1, 2], R[2, 2])
-    c = math.atan2(-R[0, 1], R[0, 0])
-    return np.array([a, b, c])
-
-
 class BallJoint(Joint):
-    """A 3-dof ball joint over its three internal revolute dofs."""
+    """A 3-dof ball joint: its three internal dofs in DART's coordinates."""
 
     def __init__(self, model: "Model", dof: int, name: str):
         super().__init__(model, dof, name)
@@ -474,29 +433,24 @@ class BallJoint(Joint):
         if not 0 <= dof < 3:
             raise RuntimeError(f"DOF mismatch: joint '{self._name}' has 3 DoFs, requested #{dof}")
 
-    def _angles(self, what: str = "q") -> np.ndarray:
-        pend = self._model._ball_pending.get(self._name) if what == "q" else None
-        return pend if pend is not None else np.asarray(self._model._get(what, self._idx), dtype=float)
+    def _vals(self, what: str) -> List[float]:
+        return np.asarray(self._model._get(what, self._idx), dtype=float).tolist()
 
     # -- state in DART's BallJoint coordinates
     def joint_position(self) -> List[float]:
-        return rotvec_from_R(ball_R(self._angles())).tolist()
+        return self._vals("q")
 
     def joint_velocity(self) -> List[float]:
-        return (ball_J(self._angles()) @ self._angles("qd")).tolist()
+        return self._vals("qd")
 
     def joint_acceleration(self) -> List[float]:
-        e, ed, edd = self._angles(), self._angles("qd"), self._angles("qdd")
-        return (ball_J(e) @ edd + ball_Jdot(e, ed) @ ed).tolist()
-
-    def _torque(self, what: str) -> List[float]:
-        return np.linalg.solve(ball_J(self._angles()).T, self._angles(what)).tolist()
+        return self._vals("qdd")
 
     def joint_generalized_force(self) -> List[float]:
-        return self._torque("force")
+        return self._vals("force")
 
     def joint_generalized_force_target(self) -> List[float]:
-        return self._torque("force_target")
+        return self._vals("force_target")
 
     def position(self, dof: int = 0) -> float:
         self._check_dof(dof)
@@ -518,18 +472,14 @@ class BallJoint(Joint):
         self._check_dof(dof)
         return self.joint_generalized_force_target()[dof]
 
-    # -- conversions into the internal angles (used by Model._set)
     def _to_internal(self, what: str, v) -> np.ndarray:
+        if what not in ("reset_q", "reset_qd", "force_target"):
+            raise RuntimeError(f"Joint '{self._name}' (ball) does not support {what}")
         v = np.asarray(v, dtype=float)
-        if what == "reset_q":
-            e = ball_angles(R_from_rotvec(v))
-            self._model._ball_pending[self._name] = e
-            return e
-        if what == "reset_qd":
-            return np.linalg.solve(ball_J(self._angles()), v)
-        if what == "force_target":
-            return ball_J(self._angles()).T @ v
-        raise RuntimeError(f"Joint '{self._name}' (ball) does not support {what}")
+        if what == "reset_q" and float(np.linalg.norm(v)) > math.pi:
+            # DART keeps the rotation vector's angle in [0, pi]
+            v = rotvec_from_R(R_from_rotvec(v))
+        return v
 
     def set_joint_generalized_force_target(self, target: Sequence[float]) -> bool:
         return len(target) == 3 and self._model.set_joint_generalized_force_targets(list(target), [self._name])
@@ -622,7 +572,6 @@ class Model:
         self._joints: Dict[str, Joint] = {}
         self._jnames: List[str] = []
         self._ball: Dict[str, BallJoint] = {}
-        self._ball_pending: Dict[str, np.ndarray] = {}  # reset angles not yet applied by a run
         names = list(sim.joint_names)
         i = 0
         while i < len(names):
@@ -1058,14 +1007,9 @@ class Model:
         return self._sim.dof_indices(out)
 
     def _ball_list(self, what: str, joint_names: Sequence[str]) -> List[float]:
-        # models with ball joints: DART's BallJoint coordinates for those
-        getter = {"q": "joint_position", "qd": "joint_velocity", "qdd": "joint_acceleration",
-                  "force": "joint_generalized_force", "force_target": "joint_generalized_force_target"}[what]
-        out: List[float] = []
-        for n in (joint_names or self._jnames):
-            b = self._ball.get(n)
-            out.extend(getattr(b, getter)() if b is not None else self._get(what, self._dofs([n])).tolist())
-        return out
+        # models with ball joints: a ball joint's three dofs hold DART's
+        # BallJoint coordinates (no conversion)
+        return self._get(what, self._dofs(joint_names)).tolist()
 
     def _get(self, what: str, dof_idx) -> np.ndarray:
         if self._sim is None:
@@ -1205,7 +1149,6 @@ class Model:
         if self._history is not None and not paused:
             self._history.extend(self._get("force_target", None).tolist())
         self._pending_vel = None
-        self._ball_pending.clear()
         self.__dict__.pop("_state_override", None)
 
     def _close(self) -> None:

@@ -152,11 +152,106 @@ static void sp_dad(const double* V, const double* F, double* out)
 
 /* ---------------- model kinematics / inertia ---------------- */
 
-static void joint_pose(const or_model* m, int i, double q, double R[9], double p[3])
+/* DART's BallJoint (a MultiDofJoint<3>; Joint.cpp:267-331 exposes it as
+ * core::JointType::Ball): positions = the rotation vector theta of the joint
+ * rotation, velocities = the child's angular velocity in its own frame, the
+ * relative Jacobian [I; 0] constant, positions integrated on SO(3) as
+ * R <- R exp(dt w) [EXT: dart/dynamics/BallJoint.cpp].  The model lists it as
+ * three bodies at one point (jtype bits 4-5 = part 1, 2, 3; unit axes x, y, z;
+ * the first two massless): part 1 carries the whole rotation E exp(theta),
+ * theta = (q_i, q_i+1, q_i+2), parts 2 and 3 have identity transforms, so the
+ * three motion axes are the child frame's and qd of the parts is w. */
+static int ball_part(const or_model* m, int i) { return (m->jtype[i] >> 4) & 3; }
+
+/* exp of a rotation vector (Rodrigues) */
+static void so3_exp(const double th[3], double R[9])
+{
+    const double t2 = th[0] * th[0] + th[1] * th[1] + th[2] * th[2], t = sqrt(t2);
+    const double A = (t < 1e-8) ? 1.0 - t2 / 6.0 : sin(t) / t;
+    const double B = (t < 1e-8) ? 0.5 - t2 / 24.0 : (1.0 - cos(t)) / t2;
+    const double K[9] = {0, -th[2], th[1], th[2], 0, -th[0], -th[1], th[0], 0};
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double kk = 0.0;
+            for (int j = 0; j < 3; ++j) kk += K[r * 3 + j] * K[j * 3 + c];
+            R[r * 3 + c] = (r == c ? 1.0 : 0.0) + A * K[r * 3 + c] + B * kk;
+        }
+}
+
+/* unit quaternion (w, x, y, z) of a rotation vector, and back (angle in [0, pi]) */
+static void rotvec_quat(const double th[3], double qt[4])
+{
+    const double t = sqrt(th[0] * th[0] + th[1] * th[1] + th[2] * th[2]);
+    const double s = (t < 1e-8) ? 0.5 - t * t / 48.0 : sin(0.5 * t) / t;
+    qt[0] = cos(0.5 * t); qt[1] = s * th[0]; qt[2] = s * th[1]; qt[3] = s * th[2];
+}
+static void quat_rotvec(const double qt[4], double th[3])
+{
+    double w = qt[0], x = qt[1], y = qt[2], z = qt[3];
+    if (w < 0.0) { w = -w; x = -x; y = -y; z = -z; }
+    const double v = sqrt(x * x + y * y + z * z);
+    const double k = (v < 1e-12) ? 2.0 / w : 2.0 * atan2(v, w) / v;
+    th[0] = k * x; th[1] = k * y; th[2] = k * z;
+}
+
+/* BallJoint::integratePositions: theta <- log(exp(theta) exp(dt w)) */
+static void ball_integrate(double th[3], const double w[3], double dt)
+{
+    double a[4], b[4], c[4];
+    const double dw[3] = {dt * w[0], dt * w[1], dt * w[2]};
+    rotvec_quat(th, a);
+    rotvec_quat(dw, b);
+    c[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    c[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    c[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    c[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+    quat_rotvec(c, th);
+}
+
+/* integratePositions of the tree's joints: q += dt qd, a ball joint on SO(3) */
+static void integrate_joint_positions(const or_model* m, double* q, const double* qd, double dt)
+{
+    for (int i = 0; i < m->n; ++i) {
+        const int bp = ball_part(m, i);
+        if (bp == 1) {
+            ball_integrate(q + i, qd + i, dt);
+            i += 2;
+        } else if (bp == 0) {
+            q[i] += dt * qd[i];
+        }
+    }
+}
+
+/* ad(V, S qd) of joint i (the velocity-product acceleration); a ball joint's
+ * parts 2 and 3 see V without the ball's earlier parts (one joint of
+ * constant S: the ball's own S qd x S qd vanishes) */
+static void joint_bias(const or_model* m, int i, const double* qd, const double V[6], const double Sq[6], double out[6])
+{
+    const int bp = ball_part(m, i);
+    double Ve[6];
+    memcpy(Ve, V, sizeof Ve);
+    if (bp >= 2) Ve[0] -= qd[i - bp + 1];
+    if (bp == 3) Ve[1] -= qd[i - 1];
+    sp_ad(Ve, Sq, out);
+}
+
+static void joint_pose(const or_model* m, int i, const double* qv, double R[9], double p[3])
 {
     const double* E = m->E[i];
     const double* a = m->axis[i];
-    if (m->jtype[i] == 0) {
+    const int bp = ball_part(m, i);
+    if (bp) {
+        double X[9];
+        if (bp == 1) so3_exp(qv + i, X);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                R[r * 3 + c] = (bp == 1) ? E[r * 3] * X[c] + E[r * 3 + 1] * X[3 + c] + E[r * 3 + 2] * X[6 + c]
+                                         : E[r * 3 + c];
+        p[0] = m->r[i][0]; p[1] = m->r[i][1]; p[2] = m->r[i][2];
+        return;
+    }
+    const double q = qv[i];
+    if ((m->jtype[i] & 1) == 0) {
         const double c = cos(q), s = sin(q), v = 1.0 - c;
         double J[9];
         J[0] = c + a[0] * a[0] * v;        J[1] = a[0] * a[1] * v - a[2] * s; J[2] = a[0] * a[2] * v + a[1] * s;
@@ -194,7 +289,7 @@ static void plucker(const double R[9], const double p[3], double X[36])
 static void motion_subspace(const or_model* m, int i, double S[6])
 {
     memset(S, 0, 6 * sizeof(double));
-    const int off = (m->jtype[i] == 0) ? 0 : 3;
+    const int off = ((m->jtype[i] & 1) == 0) ? 0 : 3;
     S[off] = m->axis[i][0]; S[off + 1] = m->axis[i][1]; S[off + 2] = m->axis[i][2];
 }
 
@@ -245,13 +340,13 @@ static void aba_full(const or_model* m, const double* q, const double* qd,
         const int pa = m->parent[i];
         const double zero6[6] = {0}, *Vpar = pa < 0 ? zero6 : V[pa];
         const double* gpar = pa < 0 ? m->gravity_base : g[pa];
-        joint_pose(m, i, q[i], R, p);
+        joint_pose(m, i, q, R, p);
         plucker(R, p, X[i]);
         motion_subspace(m, i, S[i]);
         m6_vec(X[i], Vpar, Vp);
         for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[i][k] = Vp[k] + Sq[k]; }
         for (int r = 0; r < 3; ++r) g[i][r] = R[r] * gpar[0] + R[3 + r] * gpar[1] + R[6 + r] * gpar[2];
-        sp_ad(V[i], Sq, eta[i]);
+        joint_bias(m, i, qd, V[i], Sq, eta[i]);
         body_inertia(m, i, I[i]);
         m6_vec(I[i], V[i], IV);
         sp_dad(V[i], IV, dd);
@@ -350,7 +445,7 @@ void or_crba(const or_model* m, const double* q, double* M)
     double X[OR_MAXB][36], S[OR_MAXB][6], Ic[OR_MAXB][36];
     for (int i = 0; i < n; ++i) {
         double R[9], p[3];
-        joint_pose(m, i, q[i], R, p);
+        joint_pose(m, i, q, R, p);
         plucker(R, p, X[i]);
         motion_subspace(m, i, S[i]);
         body_inertia(m, i, Ic[i]);
@@ -389,13 +484,13 @@ void or_rnea(const or_model* m, const double* q, const double* qd,
     for (int i = 0; i < n; ++i) {
         double R[9], p[3], Vp[6], ap[6], Sq[6], c[6], I[36], Ia[6], IV[6], dd[6];
         const int pa = m->parent[i];
-        joint_pose(m, i, q[i], R, p);
+        joint_pose(m, i, q, R, p);
         plucker(R, p, X[i]);
         motion_subspace(m, i, S[i]);
         m6_vec(X[i], pa < 0 ? V0 : V[pa], Vp);
         m6_vec(X[i], pa < 0 ? a0 : a[pa], ap);
         for (int k = 0; k < 6; ++k) { Sq[k] = S[i][k] * qd[i]; V[i][k] = Vp[k] + Sq[k]; }
-        sp_ad(V[i], Sq, c);
+        joint_bias(m, i, qd, V[i], Sq, c);
         for (int k = 0; k < 6; ++k) a[i][k] = ap[k] + S[i][k] * qdd[i] + c[k];
         body_inertia(m, i, I);
         m6_vec(I, a[i], Ia);
@@ -804,7 +899,7 @@ int or_step(const or_model* m, double dt, double* q, double* qd,
         }
     }
 
-    for (int i = 0; i < n; ++i) q[i] += dt * qd[i];
+    integrate_joint_positions(m, q, qd, dt);
     if (qdd_out)
         for (int i = 0; i < n; ++i) qdd_out[i] = qdd[i];
     if (force_out)
@@ -1376,7 +1471,7 @@ static void float_kin(const or_float_model* m, const or_float_state* s, or_fkin*
     const or_model* t = &m->tree;
     for (int i = 0; i < t->n; ++i) {
         double R[9], p[3];
-        joint_pose(t, i, s->q[i], R, p);
+        joint_pose(t, i, s->q, R, p);
         plucker(R, p, k->X[i]);
         motion_subspace(t, i, k->S[i]);
         const int pa = t->parent[i];
@@ -1457,7 +1552,7 @@ void or_float_dynamics(const or_float_model* m, const or_float_state* s, double*
         m6_vec(k.X[i], pa < 0 ? s->V : V[pa], Vp);
         m6_vec(k.X[i], pa < 0 ? a0 : a[pa], ap);
         for (int e = 0; e < 6; ++e) { Sq[e] = k.S[i][e] * s->qd[i]; V[i][e] = Vp[e] + Sq[e]; }
-        sp_ad(V[i], Sq, c);
+        joint_bias(t, i, s->qd, V[i], Sq, c);
         for (int e = 0; e < 6; ++e) a[i][e] = ap[e] + c[e];
         body_inertia(t, i, I);
         m6_vec(I, a[i], Ia);
@@ -1759,10 +1854,8 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
     }
 
     /* integratePositions: q += dt qd; T0 <- T0 exp(dt V0) */
-    for (int i = 0; i < n; ++i) {
-        s->qd[i] = nu[6 + i];
-        s->q[i] += dt * nu[6 + i];
-    }
+    for (int i = 0; i < n; ++i) s->qd[i] = nu[6 + i];
+    integrate_joint_positions(t, s->q, s->qd, dt);
     double phi[3] = {dt * nu[0], dt * nu[1], dt * nu[2]}, u[3] = {dt * nu[3], dt * nu[4], dt * nu[5]};
     double dR[9], dp[3], Rn[9];
     se3_exp(phi, u, dR, dp);
@@ -2600,10 +2693,8 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
     for (int m = 0; m < K; ++m) {
         or_float_state* s = &st->s[m];
         const int o = off[m], nb = nbase[m];
-        for (int i = 0; i < sm->model[m].tree.n; ++i) {
-            s->qd[i] = nu[o + nb + i];
-            s->q[i] += dt * nu[o + nb + i];
-        }
+        for (int i = 0; i < sm->model[m].tree.n; ++i) s->qd[i] = nu[o + nb + i];
+        integrate_joint_positions(&sm->model[m].tree, s->q, s->qd, dt);
         if (!nb) continue;
         double phi[3] = {dt * nu[o], dt * nu[o + 1], dt * nu[o + 2]};
         double u[3] = {dt * nu[o + 3], dt * nu[o + 4], dt * nu[o + 5]};

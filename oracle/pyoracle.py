@@ -634,6 +634,21 @@ def mesh_shape(verts, scale, SR, sp):
     return (3, np.concatenate([half, pts.reshape(-1)]), SR, np.asarray(sp, dtype=float) + SR @ c)
 
 
+def _ball_part(chain, i) -> int:
+    """1, 2, 3 for the x / y / z part of a ball joint written by sdf_to_urdf, else 0"""
+    nm = chain[i].name
+    if len(nm) < 3 or nm[-2] != "#" or nm[-1] not in "xyz" or chain[i].jtype != "continuous":
+        return 0
+    k = "xyz".index(nm[-1])
+    base = nm[:-2]
+    first = i - k
+    if first < 0 or first + 2 >= len(chain):
+        return 0
+    if all(chain[first + t].name == f"{base}#{'xyz'[t]}" for t in range(3)):
+        return k + 1
+    return 0
+
+
 def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0, 0.0, 0.0),
               gravity=(0.0, 0.0, -9.8)) -> ChainModel:
     text = path_or_string
@@ -766,6 +781,11 @@ def load_urdf(path_or_string: str, pose_xyz=(0.0, 0.0, 0.0), pose_wxyz=(1.0, 0.0
         r = off_R[j.parent] @ j.p + off_p[j.parent]
         L = links[j.child]
         M.jtype[i] = 0 if j.jtype in ("revolute", "continuous") else 1
+        # a ball joint (sdf_to_urdf: `<name>#x`, `#y`, `#z`, consecutive):
+        # DART's BallJoint coordinates (oracle.c ball_part)
+        part = _ball_part(chain, i)
+        if part:
+            M.jtype[i] = part << 4
         M.limited[i] = 1 if j.jtype in ("revolute", "prismatic") else 0
         M.parent[i] = parents[i]
         for k in range(9):

@@ -46,7 +46,7 @@ sim.run_device(50)
 L = N.lib()
 fn = L.mw_debug_wave_prof
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 20)()
 fn(buf)  # clear
 t0 = time.perf_counter()
 sim.run_device(T)

@@ -1,15 +1,36 @@
-"""Host-side coordinate maps of the ScenarI/O ball joint (scenario/gazebo.py
-BallJoint): a ball joint runs as three revolute dofs with intrinsic X-Y-Z
-angles e = (a, b, c), presented in DART's BallJoint coordinates (rotation
-vector, child-frame angular velocity / acceleration / torque).  Checked here
-against first principles: the exponential / log maps invert each other, the
-angles reproduce the rotation, and w = J(e) e', w' = J e'' + J' e' match
-finite differences of R(e(t))."""
+"""DART's BallJoint coordinates, host side (no GPU): the oracle's restatement
+(oracle.c ball_part / joint_bias / ball_integrate) and the ScenarI/O helpers.
+
+A ball joint (core::JointType::Ball, Joint.cpp:267-331) runs natively in
+DART's coordinates: positions = the rotation vector of the joint rotation,
+velocities = the child's angular velocity in the child frame, integrated as
+R <- R exp(dt w) after DART's semi-implicit velocity update [EXT:
+dart/dynamics/BallJoint.cpp].  Checked here:
+
+  * the exponential / log maps invert each other (scenario.gazebo helpers);
+  * a body held at its centre of mass by a ball joint, no gravity, stepped by
+    the fp64 oracle, equals a numpy restatement of DART's discrete scheme
+    (w' = I^-1 (tau - w x I w) at the current w, w += dt w', R <- R exp(dt w))
+    to round-off over 500 steps -- which pins the joint's velocity-product term
+    (the three-part listing must add no Euler-angle Coriolis terms) and the
+    SO(3) position update, with the rotation vector's angle kept in [0, pi];
+  * with joint damping, DART's implicit damping: (I + dt D) w' = -D w - w x I w.
+"""
 
 import math
 
 import numpy as np
 import pytest
+
+SPINNER_SDF = """<sdf version='1.7'><model name='spinner'>
+  <link name='post'/>
+  <joint name='fix' type='fixed'><parent>world</parent><child>post</child></joint>
+  <link name='body'><pose>0 0 1 0 0 0</pose>
+    <inertial><mass>3</mass>
+      <inertia><ixx>0.05</ixx><iyy>0.12</iyy><izz>0.2</izz><ixy>0.01</ixy><ixz>0</ixz><iyz>-0.02</iyz></inertia>
+    </inertial></link>
+  <joint name='pivot' type='ball'><parent>post</parent><child>body</child>{DAMP}</joint>
+</model></sdf>"""
 
 
 @pytest.fixture(scope="module")
@@ -18,8 +39,16 @@ def g():
     return gazebo
 
 
-def _skew_inv(S):
-    return np.array([S[2, 1] - S[1, 2], S[0, 2] - S[2, 0], S[1, 0] - S[0, 1]]) / 2.0
+def _skew(v):
+    return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+
+
+def _exp(v):
+    th = float(np.linalg.norm(v))
+    if th < 1e-12:
+        return np.eye(3) + _skew(v)
+    K = _skew(v / th)
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
 
 
 def test_rotvec_roundtrip(g):
@@ -28,44 +57,37 @@ def test_rotvec_roundtrip(g):
         ax = rng.normal(size=3)
         ax /= np.linalg.norm(ax)
         th = rng.uniform(0, math.pi - 1e-3)
-        r = th * ax
-        R = g.R_from_rotvec(r)
-        assert np.allclose(R @ R.T, np.eye(3), atol=1e-12) and np.linalg.det(R) == pytest.approx(1.0)
-        assert np.allclose(g.rotvec_from_R(R), r, atol=1e-9)
-    assert np.allclose(g.rotvec_from_R(np.eye(3)), 0.0)
+        R = g.R_from_rotvec(th * ax)
+        assert np.allclose(R @ R.T, np.eye(3), atol=1e-12)
+        assert np.allclose(g.rotvec_from_R(R), th * ax, atol=1e-9)
+        assert np.allclose(R, _exp(th * ax), atol=1e-12)
 
 
-def test_angles_roundtrip(g):
-    rng = np.random.default_rng(1)
-    for _ in range(200):
-        e = np.array([rng.uniform(-math.pi, math.pi), rng.uniform(-1.5, 1.5), rng.uniform(-math.pi, math.pi)])
-        R = g.ball_R(e)
-        assert np.allclose(g.ball_angles(R), e, atol=1e-9)
-        # about the joint frame's own axes, in order x, y, z
-        assert np.allclose(R, g._rx(e[0]) @ g._ry(e[1]) @ g._rz(e[2]))
-
-
-def test_velocity_and_acceleration_maps(g):
-    """w (child frame) = skew^-1(R^T dR/dt); w' = d/dt of that"""
-    rng = np.random.default_rng(2)
-    h = 1e-5
-    for _ in range(50):
-        e0 = np.array([rng.uniform(-2, 2), rng.uniform(-1.2, 1.2), rng.uniform(-2, 2)])
-        ed = rng.uniform(-2, 2, 3)
-        edd = rng.uniform(-3, 3, 3)
-        e = lambda t: e0 + ed * t + 0.5 * edd * t * t
-        w = lambda t: _skew_inv(g.ball_R(e(t)).T @ (g.ball_R(e(t + h)) - g.ball_R(e(t - h))) / (2 * h))
-        J = g.ball_J(e0)
-        assert np.allclose(J @ ed, w(0.0), atol=1e-7)
-        wdot_fd = (w(1e-3) - w(-1e-3)) / 2e-3
-        assert np.allclose(J @ edd + g.ball_Jdot(e0, ed) @ ed, wdot_fd, atol=1e-4)
-
-
-def test_torque_map_is_the_power_dual(g):
-    """tau_angles = J^T tau: the same power for every rate"""
-    rng = np.random.default_rng(3)
-    e = np.array([0.3, -0.7, 1.1])
-    J = g.ball_J(e)
-    tau = rng.normal(size=3)
-    ed = rng.normal(size=3)
-    assert (J.T @ tau) @ ed == pytest.approx(tau @ (J @ ed))
+@pytest.mark.parametrize("damping", [0.0, 0.3])
+def test_oracle_ball_joint_is_darts_discrete_rigid_body(oracle, damping):
+    text = SPINNER_SDF.replace("{DAMP}", f"<axis><dynamics><damping>{damping}</damping></dynamics></axis>"
+                              if damping else "")
+    cm = oracle.load_urdf(text)
+    assert cm.n == 3 and cm.joint_names == ["pivot#x", "pivot#y", "pivot#z"]
+    assert [cm.model.jtype[i] for i in range(3)] == [0x10, 0x20, 0x30]   # oracle.c ball_part
+    I = np.array([[0.05, 0.01, 0.0], [0.01, 0.12, -0.02], [0.0, -0.02, 0.2]])
+    D = damping * np.eye(3)
+    dt, T = 1e-3, 500
+    q = np.array([0.1, -0.2, 2.9])        # |theta| near pi: the update wraps the angle
+    qd = np.array([0.5, 0.4, 4.0])
+    mode = np.full(3, oracle.FORCE, np.int32)
+    tau = np.zeros(3)
+    R = _exp(q)
+    w = qd.copy()
+    worst_R = worst_w = 0.0
+    for _ in range(T):
+        q, qd = oracle.step(cm, dt, q, qd, mode, tau, 0)[:2]
+        # DART: ABA at the current velocity with implicit damping, then R exp(dt w)
+        wd = np.linalg.solve(I + dt * D, -D @ w - np.cross(w, I @ w))
+        w = w + dt * wd
+        R = R @ _exp(dt * w)
+        assert np.linalg.norm(q) <= math.pi + 1e-12
+        worst_R = max(worst_R, float(np.abs(_exp(q) - R).max()))
+        worst_w = max(worst_w, float(np.abs(qd - w).max()))
+    print(f"ball joint, damping {damping}: {T} steps, max |R - R_dart| {worst_R:.1e}, |w - w_dart| {worst_w:.1e}")
+    assert worst_R <= 1e-10 and worst_w <= 1e-10

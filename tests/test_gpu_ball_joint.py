@@ -6,9 +6,11 @@
     SDF reader writes the spherical pair as three continuous URDF joints);
   * the ScenarI/O BallJoint through World / Model / Joint: a body held at its
     centre of mass by a ball joint, no gravity, spun up by reset_joint_velocity
-    -- torque-free rotation, integrated beside it in numpy (RK4 of Euler's
-    equations, dt / 10): orientation, body angular velocity (BallJoint
-    velocities) and the world angular momentum."""
+    -- torque-free rotation against DART's discrete scheme restated in numpy
+    beside it (BallJoint coordinates natively: w += dt w', R <- R exp(dt w);
+    1e-5 over 0.5 s), and that scheme against the exact motion (RK4 of
+    Euler's equations, dt / 10): orientation, body angular velocity and the
+    world angular momentum."""
 
 import math
 
@@ -121,19 +123,31 @@ def test_scenario_ball_joint_torque_free_rotation(require_gpu):
     I = np.diag([0.05, 0.12, 0.2])
     R0 = scenario.R_from_rotvec(r0)
     L0 = R0 @ I @ np.array(w0)
-    T = 0.5
-    for _ in range(int(T / 1e-3)):
+    T, dt = 0.5, 1e-3
+    # DART's discrete scheme (BallJoint: ABA at the current w, w += dt w',
+    # R <- R exp(dt w)), restated in numpy beside the GPU
+    Rd, wd = R0.copy(), np.array(w0, dtype=float)
+    worst_ang = worst_w = 0.0
+    for _ in range(int(round(T / dt))):
         assert gz.run()
+        wd = wd + dt * np.linalg.solve(I, -np.cross(wd, I @ wd))
+        Rd = Rd @ scenario.R_from_rotvec(dt * wd)
+        Rg = scenario.R_from_rotvec(j.joint_position())
+        worst_ang = max(worst_ang, float(np.linalg.norm(scenario.rotvec_from_R(Rd.T @ Rg))))
+        worst_w = max(worst_w, float(np.abs(np.array(j.joint_velocity()) - wd).max()))
     R, w = _torque_free(I, w0, T, 1e-4)
     Rg = scenario.R_from_rotvec(j.joint_position())
     wg = np.array(j.joint_velocity())
     ang = float(np.linalg.norm(scenario.rotvec_from_R((R0 @ R).T @ Rg)))
     Lg = Rg @ I @ wg
     E0, Eg = 0.5 * np.dot(w0, I @ w0), 0.5 * wg @ I @ wg
-    print(f"torque-free spinner, {T} s: orientation error {ang:.2e} rad, |w - w_ref| {np.abs(wg - w).max():.2e}, "
+    print(f"torque-free spinner, {T} s: vs DART's discrete scheme orientation {worst_ang:.2e} rad, w {worst_w:.2e}; "
+          f"vs the exact motion (RK4) orientation {ang:.2e} rad, |w - w_ref| {np.abs(wg - w).max():.2e}, "
           f"|L - L0| {np.abs(Lg - L0).max():.2e} (|L0| {np.linalg.norm(L0):.3f}), energy {Eg:.5f} vs {E0:.5f}")
+    # the GPU's fp32 step against DART's scheme: round-off over 500 steps
+    assert worst_ang <= 1e-5 and worst_w <= 1e-5
+    # and the scheme itself against the exact motion: semi-implicit Euler, O(dt)
     assert abs(Eg - E0) <= 2e-3 * E0
-    # semi-implicit Euler at dt = 1 ms against the exact motion: O(dt)
     assert ang <= 5e-3 and np.abs(wg - w).max() <= 1e-2
     assert np.abs(Lg - L0).max() <= 5e-3 * np.linalg.norm(L0)
     # torques on the ball joint: child-frame torque about z spins the body up about z

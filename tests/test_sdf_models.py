@@ -350,11 +350,13 @@ BALL_ARM_SDF = """<sdf version='1.7'><model name='arm'>
 
 
 def test_ball_joint_compiles_as_three_revolutes(N, oracle):
-    """SDF ball joints (Joint.cpp:318-331: 3 dofs): the product compiles a
-    spherical pair as three revolute dofs about x, y, z of the joint frame at
-    one point (massless links between), the oracle's independent reader as
-    the same three continuous URDF joints -- identical multibodies, and the
-    C-ABI reports MW_JOINT_BALL for the three dofs."""
+    """SDF ball joints (Joint.cpp:318-331: 3 dofs): the product lists a
+    spherical pair as three bodies at one point (axes x, y, z of the joint
+    frame, massless links between) whose coordinates are DART's BallJoint
+    ones (jtype bits 4-5 = part 1..3: the rotation vector, the child-frame
+    angular velocity; chain_dyn.hpp ball_part), the oracle's independent
+    reader the same from three continuous URDF joints -- identical
+    multibodies, and the C-ABI reports MW_JOINT_BALL for the three dofs."""
     rc, got = _compile(N, BALL_ARM_SDF)
     assert rc == 0, got
     assert got["names"] == ["shoulder#x", "shoulder#y", "shoulder#z", "elbow"]
