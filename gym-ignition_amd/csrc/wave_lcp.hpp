@@ -44,8 +44,14 @@ namespace dev {
 // to fp32 moves it by ~1 ulp of mag).  At 4e-6 (r04c) a resting cube kept
 // 1.5e-4 N of tangential force and a redundant corner could stay unloaded
 // (its multiplier, set by DART's CFM, sat inside the tolerance).
-constexpr float kLcpRelTol = 1e-6f;
-constexpr float kLcpAbsTol = 1e-8f;   // m/s or rad/s
+#ifndef MW_LCP_REL_TOL
+#define MW_LCP_REL_TOL 1e-6f  // A/B builds: EXTRA=-DMW_LCP_REL_TOL=...
+#endif
+constexpr float kLcpRelTol = MW_LCP_REL_TOL;
+#ifndef MW_LCP_ABS_TOL
+#define MW_LCP_ABS_TOL 1e-8f
+#endif
+constexpr float kLcpAbsTol = MW_LCP_ABS_TOL;   // m/s or rad/s
 // a refinement solve that moves no impulse by more than this (relative to
 // 1 + max |x|) has reached the fp32 floor of its working set
 constexpr float kLcpStall = 1e-7f;
@@ -307,6 +313,7 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
     bool stalled = false; // ... by a refinement solve that moved nothing
     bool fresh = false;   // w / g / mag / xmax / rel belong to the current x
     float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f, rel = 0.f;
+    float rel_refine = 3.4e38f;  // the residual when the last refinement solve started
     for (int it = 0; it < 4 * budget + 8 + n; ++it, ++iters) {
         if (!fresh) {
             w = lcp_matvec<RC>(a, xl, n, mag);
@@ -328,8 +335,13 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
                 continue;
             }
             // every multiplier is signed right and the last solve on this
-            // working set was a refinement that moved nothing: the fp32 floor
-            if (stalled) return rel <= kLcpFloorAccept;
+            // working set was a refinement that moved nothing, or did not
+            // halve the residual (the elimination's own error at the
+            // system's conditioning): the fp32 floor
+            if (stalled || rel > 0.5f * rel_refine) return rel <= kLcpFloorAccept;
+            rel_refine = rel;
+        } else {
+            rel_refine = 3.4e38f;
         }
         if (solves >= budget) return false;
         // ---- one linear solve over the free rows

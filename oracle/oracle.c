@@ -729,8 +729,46 @@ static int boxqp_solve(int n, const double* A, int lda, const double* b, const d
  * frictionless normals.  Stats: boxqp iterations of both stages; the final
  * complementarity residual of the two stages' boxes (velocity units), < 0
  * when a stage ran out of budget. */
+/* Conditioning probe (tests only): with eps > 0 every exact LCP solve sees A
+ * with each symmetric pair of entries scaled by (1 + eps u), u uniform in
+ * [-1, 1) from a per-call LCG stream -- the perturbation storing A in fp32
+ * makes (eps ~ 6e-8).  An LCP whose answer moves as much under it as the
+ * GPU's differs from the fp64 one is ill-conditioned at fp32, not solved
+ * wrong. */
+static _Thread_local double g_lcp_eps = 0.0;
+static _Thread_local uint64_t g_lcp_seed = 0;
+
+void or_set_lcp_perturbation(double eps, uint64_t seed)
+{
+    g_lcp_eps = eps;
+    g_lcp_seed = seed;
+}
+
+static void lcp_dantzig_exact(int n, const double* A, int lda, const double* b, const double* lo,
+                              const double* hi, const int* findex, double mu, double* x);
+
 static void lcp_dantzig(int n, const double* A, int lda, const double* b, const double* lo, const double* hi,
                         const int* findex, double mu, double* x)
+{
+    if (g_lcp_eps <= 0.0 || n > OR_LCP_MAXN) {
+        lcp_dantzig_exact(n, A, lda, b, lo, hi, findex, mu, x);
+        return;
+    }
+    static _Thread_local double Ap[OR_LCP_MAXN * OR_LCP_MAXN];
+    uint64_t st = g_lcp_seed * 6364136223846793005ull + 1442695040888963407ull;
+    for (int r = 0; r < n; ++r)
+        for (int c = r; c < n; ++c) {
+            st = st * 6364136223846793005ull + 1442695040888963407ull;
+            const double u = (double)(st >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+            const double v = A[r * lda + c] * (1.0 + g_lcp_eps * u);
+            Ap[r * n + c] = v;
+            Ap[c * n + r] = v;
+        }
+    lcp_dantzig_exact(n, Ap, n, b, lo, hi, findex, mu, x);
+}
+
+static void lcp_dantzig_exact(int n, const double* A, int lda, const double* b, const double* lo,
+                              const double* hi, const int* findex, double mu, double* x)
 {
     static _Thread_local double As[OR_LCP_MAXN * OR_LCP_MAXN];
     double bs[OR_LCP_MAXN], Ls[OR_LCP_MAXN], Us[OR_LCP_MAXN], xs[OR_LCP_MAXN], L[OR_LCP_MAXN] = {0}, U[OR_LCP_MAXN] = {0};

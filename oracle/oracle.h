@@ -91,6 +91,8 @@ void or_pgs(int n, const double* A, const double* b, const double* lo,
 void or_pgs_stats(int* sweeps, double* last_delta);
 /* test hook: the latest floating-tree LCP and its solution (n rows, or -n if cap < n) */
 int or_lcp_last(int cap, double* A, double* b, double* lo, double* hi, int* kind, double* x, double* mu);
+/* tests: perturb the Delassus matrix of every exact LCP solve (0 = off) */
+void or_set_lcp_perturbation(double eps, uint64_t seed);
 
 /* Joint PID of the ScenarI/O JointController (Position / Velocity modes,
  * cpp/scenario/plugins/JointController/JointController.cpp:129-190). */

@@ -1347,6 +1347,15 @@ def lcp_last():
                 kind=kind[:n].copy(), mu=mu.value, x=x[:n].copy())
 
 
+def set_lcp_perturbation(eps: float, seed: int = 0) -> None:
+    """Conditioning probe (oracle.c or_set_lcp_perturbation): every exact LCP
+    solve sees A with its symmetric entry pairs scaled by (1 + eps u), u in
+    [-1, 1); eps = 0 turns it off."""
+    f = lib().or_set_lcp_perturbation
+    f.argtypes = [ctypes.c_double, ctypes.c_uint64]
+    f(float(eps), int(seed))
+
+
 def pgs(A, b, lo, hi, iters=100):
     A = np.ascontiguousarray(A, dtype=np.float64)
     b, lo, hi = (np.ascontiguousarray(x, dtype=np.float64) for x in (b, lo, hi))

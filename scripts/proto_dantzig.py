@@ -209,7 +209,7 @@ def boxqp(A, b, L, U, x, budget, stats, ws0=None):
     return x, solves, False
 
 
-def solve(p, x_final_prev, x1_prev, stats):
+def solve(p, x_final_prev, x1_prev, stats, prev_active=False):
     A = p["A"].astype(f32)
     b = p["b"].astype(f32)
     kind = p["kind"]
@@ -222,15 +222,19 @@ def solve(p, x_final_prev, x1_prev, stats):
     hi = np.where(kind == 0, big, np.where(kind == 2, p["hi"], 0)).astype(f32)
     # stage 1
     L1, U1 = np.where(fric, 0, lo).astype(f32), np.where(fric, 0, hi).astype(f32)
-    warm = MODE == "was"
+    warm = MODE in ("was", "was2")
+    # was2: the record marks rows active last step (a zero impulse included):
+    # a zero normal starts held at 0, a zero friction row free; PGS only when
+    # some row has no record (a new contact)
+    marked = MODE == "was2" and prev_active
     tolc = lambda v: f32(2e-6) * (f32(1) + np.abs(v).max(initial=0))
     x = np.clip(x1_prev, L1, U1).astype(f32)
     ws1 = None
     if warm:
         t = tolc(x1_prev)
         ws1 = np.where(x1_prev <= L1 + t, 1, np.where(x1_prev >= U1 - t, 2, 0))
-        ws1 = np.where(x1_prev == 0, -1, ws1)
-    if SWEEPS:
+        ws1 = np.where(x1_prev == 0, (np.where(fric, 0, 1) if marked else -1), ws1)
+    if SWEEPS and not marked:
         x = pgs(A, b, L1, U1, x, SWEEPS).astype(f32)
     x, s1, ok1 = boxqp(A, b, L1, U1, x, BUDGET, stats, ws1)
     x1 = x.copy()
@@ -245,10 +249,10 @@ def solve(p, x_final_prev, x1_prev, stats):
         Lp, Up = np.where(fric, -up, L1), np.where(fric, up, U1)
         t = tolc(x_final_prev)
         ws2 = np.where(x_final_prev <= Lp + t, 1, np.where(x_final_prev >= Up - t, 2, 0))
-        ws2 = np.where((x_final_prev == 0) | (Up - Lp <= 0), -1, ws2)
+        ws2 = np.where((x_final_prev == 0) | (Up - Lp <= 0), (np.where(fric, 0, 1) if marked else -1), ws2)
     else:
         x = np.where(fric, np.clip(x_final_prev, L2, U2), x).astype(f32)
-    if SWEEPS:
+    if SWEEPS and not marked:
         x = pgs(A, b, L2, U2, x, SWEEPS).astype(f32)
     x, s2, ok2 = boxqp(A, b, L2, U2, x, BUDGET - s1, stats, ws2)
     return x, x1, s1, s2, ok1 and ok2

@@ -24,6 +24,35 @@ T = int(os.environ.get("MW_PROF_T", "20"))
 PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
           "Delassus (lane = column)", "PGS + exact LCP", "rows total (responses .. integrate)", "whole substep"]
 
+if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
+    # the bench's contacts leg (bench.contact_leg): cubes dropped from random poses
+    sim = Simulator(get_model_file("cube"), n_worlds=W, pgs_iters=20)
+    sim.set_ground_plane(True, 1.0)
+    sim.enable_contacts(True)
+    rng = np.random.default_rng(0)
+    qq = rng.normal(size=(W, 4))
+    qq /= np.linalg.norm(qq, axis=1, keepdims=True)
+    sim.reset_base_pose(np.column_stack([rng.uniform(-5, 5, (W, 2)), rng.uniform(0.2, 0.6, W), qq]))
+    sim.reset_base_velocity(np.column_stack([rng.uniform(-1, 1, (W, 3)), rng.uniform(-3, 3, (W, 3))]))
+    sim.run(paused=True)
+    sim.run_device(200)
+    L = N.lib()
+    fn = L.mw_debug_wave_prof
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    buf = (ctypes.c_ulonglong * 20)()
+    fn(buf)
+    t0 = time.perf_counter()
+    sim.run_device(T)
+    sim.get("q")
+    dt = time.perf_counter() - t0
+    fn(buf)
+    print(f"cube x{W}: {dt / T * 1e6:.1f} us/step wall, unconverged {sim.lcp_unconverged()}")
+    for k, name in enumerate(PHASES):
+        print(f"  {name:40s} {buf[k] / W / T:12.0f} cycles/world-step")
+    print(f"  exact LCP: {buf[8] / W / T:.2f} solves per world-step, max {buf[11]}, {buf[13]} world-steps > 4; "
+          f"{buf[14] / W / T:.0f} cycles in the solves, {buf[16] / W / T:.0f} in the sweeps, "
+          f"{buf[17] / W / T:.0f} in stage 1")
+    sys.exit(0)
 sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=PGS, pose=(0, 0, 0.535, 1, 0, 0, 0))
 names = sim.joint_names
 sim.set_ground_plane(True, 1.0)
@@ -60,5 +89,6 @@ print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f}
       f"{buf[10] / W / T:.2f} of the solves in stage 2 (friction boxes); max per world-step {buf[11]} solves, "
       f"{buf[12]} in stage 2; {buf[13]} of {W * T} world-steps > 4 solves; "
       f"{buf[14] / W / T:.0f} cycles/world-step in the linear solves, {buf[15] / W / T:.0f} in the PGS sweeps "
-      f"(PGS-only mode) / the whole exact solve incl. its per-stage sweeps (exact mode)")
+      f"(PGS-only mode) / the whole exact solve incl. its per-stage sweeps (exact mode); "
+      f"{buf[16] / W / T:.0f} in the per-stage sweeps, {buf[17] / W / T:.0f} in stage 1")
 sim.close()

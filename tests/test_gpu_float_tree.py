@@ -230,9 +230,11 @@ def test_one_step_exact_lcp_random_states(require_gpu, oracle, monkeypatch, name
     are not unique) and the oracle's own exact solve does not always reach
     the complementarity conditions: worlds where it did not (residual >
     1e-6) have no reference and are counted, not compared.  Of the others,
-    at least 90% must agree with the GPU within the fp32 tolerances (the rest
-    are degenerate LCPs where two solutions both satisfy the conditions to
-    round-off, or budget exhaustion, counted by mw_lcp_unconverged)."""
+    at least 97% must agree with the GPU within the fp32 tolerances or be
+    ill-conditioned (the fp64 oracle moves as much when its Delassus matrix
+    carries a fp32-size error, pyoracle.set_lcp_perturbation: DART's
+    frictionless-stage normals over redundant contacts set the friction
+    boxes), the ill-conditioned at most 10%."""
     from mwstep import native as N
     from mwstep.sim import Simulator
     text = _model(name)
@@ -257,14 +259,25 @@ def test_one_step_exact_lcp_random_states(require_gpu, oracle, monkeypatch, name
     sim.run()
     p1, gq1, gqd1 = sim.base_pose(), sim.get("q"), sim.get("qd")
     mode = np.full(cm.n, oracle.FORCE, np.int32)
-    no_ref, agree, differ = [], 0, []
+
+    def oracle_step(w, eps=0.0, seed=0):
+        # eps > 0: the conditioning probe -- every exact LCP solve of the step
+        # sees its Delassus matrix perturbed by eps relative
+        oracle.set_lcp_perturbation(eps, seed)
+        try:
+            R0 = _quat_to_R(p0[w, 3:])
+            ow = oracle.FloatWorld(cm, ground=True, mu=mu, pgs_iters=oracle.PGS_CONVERGED)
+            ow.set_pose(p0[w, :3], R0)
+            ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
+            ow.set_joints(gq0[w], gqd0[w])
+            ow.step(mode, tau[w])
+        finally:
+            oracle.set_lcp_perturbation(0.0)
+        return ow
+
+    no_ref, agree, differ, ill = [], 0, [], []
     for w in range(W):
-        R0 = _quat_to_R(p0[w, 3:])
-        ow = oracle.FloatWorld(cm, ground=True, mu=mu, pgs_iters=oracle.PGS_CONVERGED)
-        ow.set_pose(p0[w, :3], R0)
-        ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
-        ow.set_joints(gq0[w], gqd0[w])
-        ow.step(mode, tau[w])
+        ow = oracle_step(w)
         _, res = oracle.pgs_stats()
         if not 0.0 <= res <= 1e-6:
             no_ref.append(w)
@@ -273,15 +286,24 @@ def test_one_step_exact_lcp_random_states(require_gpu, oracle, monkeypatch, name
         e_q = max(float(np.abs(gq1[w] - ow.q).max()), float(np.abs(p1[w, :3] - ow.p).max()))
         if e_qd <= 2e-3 and e_q <= 1e-5:
             agree += 1
+            continue
+        # DART's friction boxes come from the frictionless stage's normals,
+        # whose split over redundant contacts is set by the CFM alone (cond
+        # ~1e7): ill-conditioned at fp32 where the fp64 oracle moves as much
+        # when its Delassus matrix carries a fp32-size error (1e-6 relative,
+        # ~16 ulps: the order of the kernel's fp32 A)
+        sens = max(float(np.abs(oracle_step(w, 1e-6, k + 1).qd - ow.qd).max()) for k in range(4))
+        if sens >= 0.1 * e_qd and e_q <= 2e-3 * e_qd + 1e-5:
+            ill.append((w, f"{e_qd:.1e}", f"{sens:.1e}"))
         else:
-            differ.append((w, f"{e_qd:.1e}"))
+            differ.append((w, f"{e_qd:.1e}", f"{sens:.1e}"))
     unconv = sim.lcp_unconverged()
     n_ref = W - len(no_ref)
     print(f"exact LCP, random states, {name}: {agree}/{n_ref} worlds agree with the converged oracle "
-          f"(qd <= 2e-3, q / pose <= 1e-5); differ {differ}; oracle unconverged {len(no_ref)}; "
-          f"GPU unconverged {unconv}/{W}")
+          f"(qd <= 2e-3, q / pose <= 1e-5); ill-conditioned (world, |dqd|, oracle sensitivity) {ill}; "
+          f"differ {differ}; oracle unconverged {len(no_ref)}; GPU unconverged {unconv}/{W}")
     assert sim.constraint_overflow() == 0
-    assert agree >= 0.9 * n_ref
+    assert agree + len(ill) >= 0.97 * n_ref and len(ill) <= 0.1 * n_ref
     sim.close()
 
 

@@ -106,23 +106,48 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, urdf, kernel):
     p1, v1 = sim.base_pose(), sim.base_velocity()
     cm = oracle.load_urdf(text)
     worst_p = worst_v = worst_f = 0.0
-    n_contact = 0
+    n_contact, ill = 0, []
+
+    def oracle_step(w, eps=0.0, seed=0):
+        # eps > 0: the conditioning probe -- every exact LCP solve of the step
+        # sees its Delassus matrix perturbed by eps relative (pyoracle
+        # set_lcp_perturbation)
+        oracle.set_lcp_perturbation(eps, seed)
+        try:
+            R0 = _quat_to_R(p0[w, 3:])
+            ow = oracle.FreeWorld(cm, ground=True, mu=0.8, pgs_iters=opgs)
+            ow.set_pose(p0[w, :3], R0)
+            ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
+            ow.step()
+        finally:
+            oracle.set_lcp_perturbation(0.0)
+        return ow, np.concatenate([ow.R @ ow.twist[1], ow.R @ ow.twist[0]])
+
     for w in range(W):
-        R0 = _quat_to_R(p0[w, 3:])
-        ow = oracle.FreeWorld(cm, ground=True, mu=0.8, pgs_iters=opgs)
-        ow.set_pose(p0[w, :3], R0)
-        ow.set_twist(R0.T @ v0[w, 3:], R0.T @ v0[w, :3])
-        ow.step()
-        worst_p = max(worst_p, float(np.abs(p1[w, :3] - ow.p).max()),
-                      float(np.abs(_quat_to_R(p1[w, 3:]) - ow.R).max()))
-        wv = np.concatenate([ow.R @ ow.twist[1], ow.R @ ow.twist[0]])
-        worst_v = max(worst_v, float(np.abs(v1[w] - wv).max()))
+        ow, wv = oracle_step(w)
+        e_p = max(float(np.abs(p1[w, :3] - ow.p).max()), float(np.abs(_quat_to_R(p1[w, 3:]) - ow.R).max()))
+        e_v = float(np.abs(v1[w] - wv).max())
+        if kernel == "wave" and (e_v > 1e-4 or e_p > 1e-5):
+            # DART's two-stage LCP boxes the friction by the FRICTIONLESS
+            # normals; over redundant contacts (a rock's or a double box's
+            # coincident points, cond(A) ~1e7 from the CFM) their split is
+            # set by the CFM alone, and with it the saturated friction boxes:
+            # accept the world only if the fp64 oracle moves as much when its
+            # Delassus matrix carries a fp32-size error (1e-6 relative, ~16
+            # ulps: the order of the kernel's fp32 A)
+            sens = max(float(np.abs(oracle_step(w, 1e-6, k + 1)[1] - wv).max()) for k in range(4))
+            ill.append((w, f"{e_v:.1e}", f"{sens:.1e}"))
+            assert sens >= 0.1 * e_v, f"world {w}: GPU-oracle |dv| {e_v:.2e}, oracle sensitivity {sens:.2e}"
+            assert e_p <= 2e-3 * e_v + 1e-5
+            e_p = e_v = 0.0
+        worst_p = max(worst_p, e_p)
+        worst_v = max(worst_v, e_v)
         gc = sim.contacts(w)
         assert len(gc) == len(ow.contacts)
         n_contact += len(gc) > 0
         for row, (p, n, f, d) in zip(gc, ow.contacts):
             assert np.abs(row[0:3] - p).max() <= 1e-5
-        if len(gc):
+        if len(gc) and not (ill and ill[-1][0] == w):
             # the resultant: a body resting on redundant points (a cube's four
             # corners) has A of condition ~1e7 (DART's CFM), so the split of
             # the load among the corners is round-off sensitive in fp32 while
@@ -131,8 +156,10 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, urdf, kernel):
             fo = np.sum([f for (_, _, f, _) in ow.contacts], axis=0)
             worst_f = max(worst_f, float(np.abs(fg - fo).max()) / (1.0 + float(np.abs(fo).max())))
     print(f"free body {urdf}, {kernel} kernel: one-step max|pose err| {worst_p:.2e}, max|vel err| {worst_v:.2e}, "
-          f"force rel err {worst_f:.2e}, {n_contact}/{W} worlds in contact")
+          f"force rel err {worst_f:.2e}, {n_contact}/{W} worlds in contact, "
+          f"ill-conditioned (world, |dv|, oracle sensitivity): {ill}")
     assert n_contact > W // 4
+    assert len(ill) <= W // 8
     assert worst_p <= 1e-5 and worst_v <= 1e-4 and worst_f <= 1e-3
     sim.close()
 
