@@ -835,7 +835,7 @@ def scene_leg(args, dev, torch, W=4096, K=500, warm=100, G=50):
            "ms_per_step": round(elapsed / steps * 1e3, 6),
            "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
            "contacts_world0": len(rows), "cube3_support_N_world0": round(fz3, 2),
-           "dropped_rows": sc.overflow()}
+           "dropped_rows": sc.overflow(), "lcp_unconverged_world_steps": sc.lcp_unconverged()}
     sc.close()
     return out
 

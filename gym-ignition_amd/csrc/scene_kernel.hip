@@ -97,6 +97,10 @@ struct ScWarm {
     __device__ float& x(int r) const {
         return reinterpret_cast<float*>(rec)[static_cast<size_t>(1 + kScMaxContacts + r) * W + w];
     }
+    // the exact solve's stage-1 impulse of row r
+    __device__ float& x1(int r) const {
+        return reinterpret_cast<float*>(rec)[static_cast<size_t>(1 + kScMaxContacts + kScWarmRows + r) * W + w];
+    }
 };
 
 // PGS sweeps of exact mode end once a sweep moves no constraint velocity by
@@ -986,6 +990,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         }
     }
 
+    float x1s = 0.f;  // the exact solve's stage-1 impulse of row `lane` (warm record)
     if (NR > 0) {
         // ---- responses, lane = row
         for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
@@ -1063,7 +1068,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             if (lane >= NR && lane < Rpad) L.rc[lane] = F4{0.f, 0.f, 0.f, 0.f};
             // warm start (exact mode): every row from the previous step's
             // impulse of the same contact key / joint row, else 0
-            float xw = 0.f;
+            float xw = 0.f, xw1 = 0.f;  // final and stage-1 impulses of the previous step
             if (warm.rec && lane < NR) {
                 const int src = L.src[lane];
                 if (src < kJointRow) {
@@ -1071,11 +1076,13 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                     for (int j = 0; j < np; ++j) {
                         if (warm.key(j) == key) {
                             xw = warm.x(3 * j + src % 3);
+                            xw1 = warm.x1(3 * j + src % 3);
                             break;
                         }
                     }
                 } else {
                     xw = warm.x(kScWarmJoint0 + (src - kJointRow));
+                    xw1 = warm.x1(kScWarmJoint0 + (src - kJointRow));
                 }
             }
             float a[kWaveLanes], x[kWaveLanes];
@@ -1084,7 +1091,9 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 a[r] = (r < NR && lane < NR) ? L.A[r][lane] : 0.f;
                 x[r] = read_lane(xw, r);
             }
-            for (int it = 0; it < pgs_iters; ++it) {
+            // exact mode: no coupled sweeps -- each stage of the exact solve
+            // runs its own (wave_lcp.hpp), as on the world-per-wavefront kernel
+            for (int it = 0; it < (lcp_solves > 0 ? 0 : pgs_iters); ++it) {
                 float w = 0.f;
 #pragma unroll
                 for (int rb = 0; rb < kWaveLanes; rb += 8) {
@@ -1120,9 +1129,10 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #pragma unroll
             for (int r = 0; r < kWaveLanes; ++r) x0 = (lane == r) ? x[r] : x0;
             if (lcp_solves > 0) {
-                // exact boxed LCP from the PGS impulses (wave_lcp.hpp; oracle
-                // OR_PGS_CONVERGED), lane r = row r; the pivot rows go to the
-                // Delassus matrix's LDS, dead once it sits in the registers
+                // exact boxed LCP (wave_lcp.hpp; oracle OR_PGS_CONVERGED), lane
+                // r = row r, each stage from the previous step's record of that
+                // stage; the pivot rows go to the Delassus matrix's LDS, dead
+                // once it sits in the registers; the stages' sweeps use L.rc
                 LcpRow Rw;
                 Rw.live = lane < NR;
                 const F4 c = L.rc[lane < Rpad ? lane : 0];
@@ -1135,13 +1145,27 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 float* Uw = &L.A[0][0];
                 int nsolve = 0, nround = 0, nsolve1 = 0;
                 long long cyc[3] = {0, 0, 0};
-                // both stages start from the sweeps' impulses (no per-stage sweeps)
-                float x1 = x0;
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, 0, 0.f, nullptr, Uw, x1, x0,
-                                                                nsolve, nround, nsolve1, cyc)
-                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, 0, 0.f, nullptr, Uw,
-                                                                          x1, x0, nsolve, nround, nsolve1, cyc);
+                x1s = xw1;
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, pgs_iters, kScExactPgsTol,
+                                                                L.rc, Uw, x1s, x0, nsolve, nround, nsolve1, cyc)
+                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                                                                          kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
+                                                                          nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
+#ifdef MW_WAVE_PROF
+                if (lane == 0) {
+                    atomicAdd(&g_wave_prof[8], static_cast<unsigned long long>(nsolve));
+                    atomicAdd(&g_wave_prof[9], static_cast<unsigned long long>(nround));
+                    atomicAdd(&g_wave_prof[10], static_cast<unsigned long long>(nsolve1));
+                    atomicMax(&g_wave_prof[11], static_cast<unsigned long long>(nsolve));
+                    atomicAdd(&g_wave_prof[13], nsolve > 4 ? 1ull : 0ull);
+                    atomicAdd(&g_wave_prof[14], static_cast<unsigned long long>(cyc[0]));
+                    atomicAdd(&g_wave_prof[15], ok ? 0ull : 1ull);
+                    atomicAdd(&g_wave_prof[16], static_cast<unsigned long long>(cyc[1]));
+                    atomicAdd(&g_wave_prof[17], static_cast<unsigned long long>(cyc[2]));
+                    atomicAdd(&g_wave_prof[18], 1ull);
+                }
+#endif
                 x0 = Rw.live ? x0 : 0.f;
             }
         } else if (lcp_solves > 0 && lane == 0) {
@@ -1204,21 +1228,36 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         }
         if (warm.rec) {
             // the next step's record of the joint rows: this step's (the others 0)
-            for (int e = lane; e < 3 * NB; e += kWaveLanes) warm.x(kScWarmJoint0 + e) = 0.f;
+            for (int e = lane; e < 3 * NB; e += kWaveLanes) {
+                warm.x(kScWarmJoint0 + e) = 0.f;
+                warm.x1(kScWarmJoint0 + e) = 0.f;
+            }
             __threadfence_block();
-            if (!two && lane >= ncr && lane < NR) warm.x(kScWarmJoint0 + (L.src[lane] - kJointRow)) = x0;
+            if (!two && lane >= ncr && lane < NR) {
+                warm.x(kScWarmJoint0 + (L.src[lane] - kJointRow)) = x0;
+                warm.x1(kScWarmJoint0 + (L.src[lane] - kJointRow)) = x1s;
+            }
         }
     } else if (warm.rec) {
-        for (int e = lane; e < 3 * NB; e += kWaveLanes) warm.x(kScWarmJoint0 + e) = 0.f;
+        for (int e = lane; e < 3 * NB; e += kWaveLanes) {
+            warm.x(kScWarmJoint0 + e) = 0.f;
+            warm.x1(kScWarmJoint0 + e) = 0.f;
+        }
     }
     if (warm.rec) {
-        // ... and of the contacts, by key
+        // ... and of the contacts, by key (contact c's rows are 3 c + d, so
+        // lane r < ncr holds row r's stage-1 impulse in x1s)
         const int nrec = NR > 0 ? nc : 0;
         if (lane == 0) warm.n() = nrec;
         if (lane < nrec) {
             warm.key(lane) = L.c_key[lane];
 #pragma unroll
             for (int d = 0; d < 3; ++d) warm.x(3 * lane + d) = L.c_x[lane][d];
+        }
+        __threadfence_block();
+        for (int r = lane; r < 3 * nrec; r += kWaveLanes) {
+            const float v = read_lane(x1s, r & (kWaveLanes - 1));
+            warm.x1(r) = (r < ncr && r < NR && NR <= kWaveLanes) ? v : 0.f;
         }
         __threadfence_block();
     }
@@ -1408,3 +1447,19 @@ hipError_t launch_scene_run(const SceneF* P, int nv, const SceneDev& D, const Pi
 }
 
 }  // namespace mw
+
+// debug builds (EXTRA=-DMW_WAVE_PROF): the scene kernel's exact-LCP counters
+// (its own copy of g_wave_prof: [8] solves, [9] rounds, [10] stage-2 solves,
+// [11] max solves, [13] solves > 4, [14] solve cycles, [15] unconverged,
+// [16] sweep cycles, [17] stage-1 cycles, [18] exact solves); read and cleared
+extern "C" int mw_debug_scene_prof(unsigned long long* out) {
+#ifdef MW_WAVE_PROF
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mw::dev::g_wave_prof), sizeof(mw::dev::g_wave_prof)) != hipSuccess)
+        return 1;
+    const unsigned long long z[mw::dev::kWaveProfPhases] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(mw::dev::g_wave_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+#else
+    (void)out;
+    return 1;
+#endif
+}

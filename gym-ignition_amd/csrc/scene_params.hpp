@@ -129,7 +129,9 @@ struct SceneDev {
 
 constexpr int kScWarmJoint0 = 3 * kScMaxContacts;
 constexpr int kScWarmRows = kScWarmJoint0 + 3 * kScMaxBodies;
-constexpr int kScWarmWords = 1 + kScMaxContacts + kScWarmRows;
+// the impulse block twice: the final impulses, then the exact solve's stage-1
+// (frictionless) impulses (wave_lcp.hpp: DART's two stages)
+constexpr int kScWarmWords = 1 + kScMaxContacts + 2 * kScWarmRows;
 
 // per-launch arguments
 struct SceneArgs {

@@ -728,7 +728,12 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             float* U = &L.stack[0][0][0];
             int nsolve = 0, nround = 0, nsolve1 = 0;
             long long cyc[3] = {0, 0, 0};
-            const bool ok = (R <= 32) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
+#ifdef MW_LCP_FORCE64
+            constexpr int kLcpSmall = 0;   // debug builds: every solve on the 64-row instance
+#else
+            constexpr int kLcpSmall = 32;
+#endif
+            const bool ok = (R <= kLcpSmall) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
                                                            nsolve, nround, nsolve1, cyc)
                                       : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
                                                                      L.rc, U, x1s, xe, nsolve, nround, nsolve1, cyc);

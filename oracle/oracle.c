@@ -2701,6 +2701,17 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
             A[r * nr + r] *= 1.0 + cfm[r];
             x[r] = 0.0;
         }
+        if (nr <= OR_CAP_MAXN) {
+            g_cap_n = nr;
+            g_cap_mu = sm->mu;
+            for (int r = 0; r < nr; ++r) {
+                for (int c = 0; c < nr; ++c) g_cap_A[r * nr + c] = A[r * nr + c];
+                g_cap_b[r] = bb[r];
+                g_cap_kind[r] = kind[r];
+                g_cap_lo[r] = kind[r] == K_BOX ? lo[r] : (kind[r] == K_NORMAL ? 0.0 : -INFINITY);
+                g_cap_hi[r] = kind[r] == K_BOX ? hi[r] : INFINITY;
+            }
+        }
         g_pgs_sweeps = 0;
         for (int it = 0; it < pgs_budget(pgs_iters); ++it) {
             for (int r = 0; r < nr; ++r) {
@@ -2723,6 +2734,8 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
             for (int r = 0; r < nr; ++r) findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
             lcp_dantzig(nr, A, nr, bb, lo, hi, findex, sm->mu, x);
         }
+        if (nr <= OR_CAP_MAXN)
+            for (int r = 0; r < nr; ++r) g_cap_x[r] = x[r];
         for (int r = 0; r < nr; ++r)
             for (int e = 0; e < NV; ++e) nu[e] += MJ[r][e] * x[r];
     }

@@ -113,6 +113,23 @@ def pgs(A, b, L, U, x, sweeps):
     return x
 
 
+def ge_nopivot(K, r):
+    """fp32 Gaussian elimination in row order without pivoting (the kernel's
+    lcp_ge_solve with pivot = false), back substitution"""
+    K = K.astype(f32).copy()
+    r = r.astype(f32).copy()
+    n = len(r)
+    for j in range(n):
+        piv = K[j, j] if abs(K[j, j]) >= 1e-30 else f32(1e-30)
+        f = (K[j + 1:, j] / piv).astype(f32)
+        K[j + 1:, j:] = (K[j + 1:, j:] - np.outer(f, K[j, j:])).astype(f32)
+        r[j + 1:] = (r[j + 1:] - f * r[j]).astype(f32)
+    d = np.zeros(n, f32)
+    for j in range(n - 1, -1, -1):
+        d[j] = (r[j] - np.dot(K[j, j + 1:], d[j + 1:]).astype(f32)) / K[j, j]
+    return d
+
+
 def boxqp(A, b, L, U, x, budget, stats, ws0=None):
     n = len(b)
     arr = np.diag(A).copy()
@@ -166,7 +183,10 @@ def boxqp(A, b, L, U, x, budget, stats, ws0=None):
         d = np.zeros(n, f32)
         if fr.any():
             dt = np.float64 if os.environ.get("F64", "0") != "0" else f32
-            d[fr] = np.linalg.solve(A[np.ix_(fr, fr)].astype(dt), (-g[fr]).astype(dt)).astype(f32)
+            if os.environ.get("NOPIV", "0") != "0":
+                d[fr] = ge_nopivot(A[np.ix_(fr, fr)], -g[fr])
+            else:
+                d[fr] = np.linalg.solve(A[np.ix_(fr, fr)].astype(dt), (-g[fr]).astype(dt)).astype(f32)
         solves += 1
         stats["solve_rows"].append(int(fr.sum()))
         if phase == 0:

@@ -24,6 +24,34 @@ T = int(os.environ.get("MW_PROF_T", "20"))
 PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
           "Delassus (lane = column)", "PGS + exact LCP", "rows total (responses .. integrate)", "whole substep"]
 
+if os.environ.get("MW_PROF_MODEL", "humanoid32") == "scene3":
+    # the bench's scene leg (bench.scene_leg): three stacked cubes per world
+    from mwstep.scene import Scene
+    sc = Scene(n_worlds=W, pgs_iters=50)
+    sc.set_ground_plane(True, 1.0)
+    rng = np.random.default_rng(42)
+    for k, p in enumerate([(0, -0.15, 0.101), (0, 0.15, 0.101), (0, 0, 0.301)]):
+        sc.insert_model(get_model_file("cube"), tuple(p) + (1, 0, 0, 0), f"cube{k + 1}")
+        pose = np.column_stack([np.full(W, p[0]) + rng.uniform(-0.01, 0.01, W), np.full(W, p[1]),
+                                np.full(W, p[2]) + rng.uniform(0, 0.02, W), np.ones(W), np.zeros((W, 3))])
+        sc.reset_base_pose(k, pose)
+    sc.run(paused=True)
+    sc.run_device(100)
+    fn = N.lib().mw_debug_scene_prof
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    buf = (ctypes.c_ulonglong * 20)()
+    fn(buf)
+    t0 = time.perf_counter()
+    sc.run_device(T)
+    sc.get("q", 0)
+    dt = time.perf_counter() - t0
+    fn(buf)
+    ns = max(buf[18], 1)
+    print(f"scene 3 cubes x{W}: {dt / T * 1e6:.1f} us/step wall, {buf[18]} exact solves, unconverged {buf[15]}; "
+          f"per solve: {buf[8] / ns:.2f} linear solves ({buf[10] / ns:.2f} in stage 2), {buf[9] / ns:.2f} rounds, "
+          f"max {buf[11]}, {buf[13]} > 4; cycles: {buf[14] / ns:.0f} in solves, {buf[16] / ns:.0f} in sweeps, "
+          f"{buf[17] / ns:.0f} in stage 1")
+    sys.exit(0)
 if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
     # the bench's contacts leg (bench.contact_leg): cubes dropped from random poses
     sim = Simulator(get_model_file("cube"), n_worlds=W, pgs_iters=20)
