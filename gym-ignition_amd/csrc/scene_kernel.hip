@@ -88,6 +88,11 @@ struct ScWorld {
     float c_x[kScMaxContacts][3];
 };
 
+#ifdef MW_WAVE_PROF
+__device__ float g_sc_dump[8 + 64 * 64 + 7 * 64];
+__device__ unsigned int g_sc_dump_claim;
+#endif
+
 // the world's exact-LCP warm-start record (SceneDev::warm); rec == nullptr: cold
 struct ScWarm {
     int32_t* rec;
@@ -1153,6 +1158,34 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                                                                           nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
 #ifdef MW_WAVE_PROF
+                // debug dump of one hard LCP (the first with >= 6 solves): n, A,
+                // b, lo, hi, the two warm records, the result, the solve count
+                if (nsolve >= 6 && NR <= kWaveLanes) {
+                    unsigned int claim = 0u;
+                    if (lane == 0) claim = atomicCAS(&g_sc_dump_claim, 0u, 1u);
+                    claim = __builtin_amdgcn_readfirstlane(claim);
+                    if (claim == 0u) {
+                        float* D0 = g_sc_dump;
+                        for (int r = 0; r < NR; ++r) D0[8 + r * kWaveLanes + lane] = (lane < NR) ? a[r] : 0.f;
+                        float* V = D0 + 8 + kWaveLanes * kWaveLanes;
+                        if (lane < NR) {
+                            V[lane] = Rw.b;
+                            V[kWaveLanes + lane] = Rw.lo;
+                            V[2 * kWaveLanes + lane] = Rw.hi;
+                            V[3 * kWaveLanes + lane] = xw;
+                            V[4 * kWaveLanes + lane] = xw1;
+                            V[5 * kWaveLanes + lane] = x0;
+                            V[6 * kWaveLanes + lane] = static_cast<float>(Rw.kind);
+                        }
+                        if (lane == 0) {
+                            D0[0] = static_cast<float>(NR);
+                            D0[1] = static_cast<float>(nsolve);
+                            D0[2] = static_cast<float>(nsolve1);
+                            D0[3] = mu;
+                            D0[4] = ok ? 1.f : 0.f;
+                        }
+                    }
+                }
                 if (lane == 0) {
                     atomicAdd(&g_wave_prof[8], static_cast<unsigned long long>(nsolve));
                     atomicAdd(&g_wave_prof[9], static_cast<unsigned long long>(nround));
@@ -1255,10 +1288,8 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             for (int d = 0; d < 3; ++d) warm.x(3 * lane + d) = L.c_x[lane][d];
         }
         __threadfence_block();
-        for (int r = lane; r < 3 * nrec; r += kWaveLanes) {
-            const float v = read_lane(x1s, r & (kWaveLanes - 1));
-            warm.x1(r) = (r < ncr && r < NR && NR <= kWaveLanes) ? v : 0.f;
-        }
+        for (int r = lane; r < 3 * nrec; r += kWaveLanes)
+            warm.x1(r) = (r == lane && r < ncr && r < NR && NR <= kWaveLanes) ? x1s : 0.f;
         __threadfence_block();
     }
     nc_out = nc;
@@ -1448,6 +1479,9 @@ hipError_t launch_scene_run(const SceneF* P, int nv, const SceneDev& D, const Pi
 
 }  // namespace mw
 
+#ifdef MW_WAVE_PROF
+// (declared above their use through the forward declarations below)
+#endif
 // debug builds (EXTRA=-DMW_WAVE_PROF): the scene kernel's exact-LCP counters
 // (its own copy of g_wave_prof: [8] solves, [9] rounds, [10] stage-2 solves,
 // [11] max solves, [13] solves > 4, [14] solve cycles, [15] unconverged,
@@ -1460,6 +1494,20 @@ extern "C" int mw_debug_scene_prof(unsigned long long* out) {
     return hipMemcpyToSymbol(HIP_SYMBOL(mw::dev::g_wave_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
 #else
     (void)out;
+    return 1;
+#endif
+}
+
+// debug builds: the dumped hard LCP (see scene_run_kernel), then re-armed
+extern "C" int mw_debug_scene_dump(float* out, int n) {
+#ifdef MW_WAVE_PROF
+    if (n < static_cast<int>(sizeof(mw::dev::g_sc_dump) / sizeof(float))) return 2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mw::dev::g_sc_dump), sizeof(mw::dev::g_sc_dump)) != hipSuccess) return 1;
+    const unsigned int z = 0u;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mw::dev::g_sc_dump_claim), &z, sizeof(z)) == hipSuccess ? 0 : 1;
+#else
+    (void)out;
+    (void)n;
     return 1;
 #endif
 }

@@ -286,9 +286,11 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 // sit on their bound, every linear solve minimises over the free rows (A_FF is
 // symmetric positive definite: no pivot search, the held rows' steps skipped)
 // and takes the longest step that stays in the box; the first bound met joins
-// the working set; at the working set's minimiser the held row whose
-// multiplier is wrongly signed by the most -- relative to its own tolerance,
-// as the residual test measures it -- leaves it.  If none is and the residual
+// the working set; at the working set's minimiser every held row whose
+// multiplier is wrongly signed beyond its own tolerance (the scale the
+// residual test uses) leaves it -- several at once: contacts that barely
+// touch (approach velocities of 1e-7 m/s in a settling stack) would each
+// cost a solve one at a time (scripts/proto_dantzig.py MULTI).  If none is and the residual
 // still misses the tolerance, what remains is the fp32 solve's own error: one
 // more solve on the same working set from the compensated residual refines it
 // (iterative refinement), until a refinement moves nothing (kLcpStall: the
@@ -309,7 +311,9 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         xl = (ws == 1) ? L : ((ws == 2) ? U : xl);
         xl = live ? xl : 0.f;
     }
-    bool at_min = false;  // the last step reached the working set's minimiser
+    // the last step reached the working set's minimiser (a working set with
+    // no free row is its own minimiser: no solve)
+    bool at_min = __ballot(!pinned && ws == 0) == 0ull;
     bool stalled = false; // ... by a refinement solve that moved nothing
     bool fresh = false;   // w / g / mag / xmax / rel belong to the current x
     float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f, rel = 0.f;
@@ -328,9 +332,12 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
             at_min = false;
             float v = (ws == 1) ? -g : ((ws == 2) ? g : 0.f);
             v = pinned ? 0.f : v * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol);
-            const int worst = wave_argmax(v);
-            if (read_lane(v, worst) > 1.f) {
-                if (lane == worst) ws = 0;
+            // every held row whose multiplier is wrongly signed beyond its
+            // tolerance leaves at once (one solve for several micro-contacts;
+            // the method stays monotone: the next solve's blocking step keeps
+            // the iterate in the box)
+            if (wave_fmax(v) > 1.f) {
+                if (v > 1.f) ws = 0;
                 stalled = false;
                 continue;
             }

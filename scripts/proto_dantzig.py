@@ -159,7 +159,10 @@ def boxqp(A, b, L, U, x, budget, stats, ws0=None):
             v[pinned] = 0
             v = v / (REL * (np.abs(b) + matvec(A, x)[1]) + ABS)
             if v.max(initial=0) > 1:
-                ws[int(np.argmax(v))] = 0
+                if os.environ.get("MULTI", "0") != "0":
+                    ws[v > 1] = 0   # every wrongly signed multiplier at once
+                else:
+                    ws[int(np.argmax(v))] = 0
                 stats["_tiny"] = False
                 continue
             if tiny_last_ and FLOOR:

@@ -42,15 +42,27 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "scene3":
     buf = (ctypes.c_ulonglong * 20)()
     fn(buf)
     t0 = time.perf_counter()
-    sc.run_device(T)
-    sc.get("q", 0)
+    for _ in range(T):
+        sc.run()          # blocking runs: the counters are read after the last
     dt = time.perf_counter() - t0
     fn(buf)
     ns = max(buf[18], 1)
-    print(f"scene 3 cubes x{W}: {dt / T * 1e6:.1f} us/step wall, {buf[18]} exact solves, unconverged {buf[15]}; "
+    print(f"scene 3 cubes x{W}: {dt / T * 1e6:.1f} us per blocking run, {buf[18]} exact solves, unconverged {buf[15]}; "
           f"per solve: {buf[8] / ns:.2f} linear solves ({buf[10] / ns:.2f} in stage 2), {buf[9] / ns:.2f} rounds, "
           f"max {buf[11]}, {buf[13]} > 4; cycles: {buf[14] / ns:.0f} in solves, {buf[16] / ns:.0f} in sweeps, "
           f"{buf[17] / ns:.0f} in stage 1")
+    dump = np.zeros(8 + 64 * 64 + 7 * 64, dtype=np.float32)
+    fd = N.lib().mw_debug_scene_dump
+    fd.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if fd(dump.ctypes.data, dump.size) == 0 and dump[0] > 0:
+        n = int(dump[0])
+        A = dump[8:8 + 64 * 64].reshape(64, 64)[:n, :n]   # row r = lane r's registers: A[lane][r] -> transpose
+        V = dump[8 + 64 * 64:].reshape(7, 64)[:, :n]
+        out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "scene_dump.npz")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        np.savez(out, A=A.T.copy(), b=V[0], lo=V[1], hi=V[2], xw=V[3], xw1=V[4], x=V[5], kind=V[6],
+                 nsolve=dump[1], nsolve2=dump[2], mu=dump[3], ok=dump[4])
+        print(f"dumped a hard LCP: {n} rows, {int(dump[1])} solves ({int(dump[2])} in stage 2), ok {int(dump[4])}")
     sys.exit(0)
 if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
     # the bench's contacts leg (bench.contact_leg): cubes dropped from random poses
