@@ -241,7 +241,7 @@ int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
  * whose friction index boxes every friction row once, by mu x the normal
  * impulses of the frictionless problem -- two strictly convex box QPs
  * (wave_lcp.hpp), each from the previous step's solution, PGS sweeps on the
- * stage's box problem (at most min(mw_config.pgs_iters, 12), ending once a
+ * stage's box problem (at most min(mw_config.pgs_iters, 4), ending once a
  * sweep moves no constraint velocity by more than 1e-6), then the primal
  * active-set method from the previous step's working set, with at most
  * max_solves dense linear solves (elimination over the wave's lanes) per
