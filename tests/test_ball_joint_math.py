@@ -63,8 +63,9 @@ def test_rotvec_roundtrip(g):
         assert np.allclose(R, _exp(th * ax), atol=1e-12)
 
 
-@pytest.mark.parametrize("damping", [0.0, 0.3])
-def test_oracle_ball_joint_is_darts_discrete_rigid_body(oracle, damping):
+@pytest.mark.parametrize("damping, q0", [(0.0, (0.1, -0.2, 2.9)), (0.3, (0.1, -0.2, 2.9)),
+                                         (0.0, (0.0, np.pi / 2, 0.0))])
+def test_oracle_ball_joint_is_darts_discrete_rigid_body(oracle, damping, q0):
     text = SPINNER_SDF.replace("{DAMP}", f"<axis><dynamics><damping>{damping}</damping></dynamics></axis>"
                               if damping else "")
     cm = oracle.load_urdf(text)
@@ -73,7 +74,7 @@ def test_oracle_ball_joint_is_darts_discrete_rigid_body(oracle, damping):
     I = np.array([[0.05, 0.01, 0.0], [0.01, 0.12, -0.02], [0.0, -0.02, 0.2]])
     D = damping * np.eye(3)
     dt, T = 1e-3, 500
-    q = np.array([0.1, -0.2, 2.9])        # |theta| near pi: the update wraps the angle
+    q = np.array(q0)     # |theta| near pi: the update wraps the angle; (0, pi/2, 0): the old angle chart's singularity
     qd = np.array([0.5, 0.4, 4.0])
     mode = np.full(3, oracle.FORCE, np.int32)
     tau = np.zeros(3)

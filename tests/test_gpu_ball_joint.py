@@ -98,7 +98,10 @@ def _torque_free(I, w0, T, dt):
     return R, w
 
 
-def test_scenario_ball_joint_torque_free_rotation(require_gpu):
+@pytest.mark.parametrize("r0", [[0.1, -0.2, 0.15], [0.0, math.pi / 2, 0.0]])
+def test_scenario_ball_joint_torque_free_rotation(require_gpu, r0):
+    """r0 = (0, pi/2, 0): the configuration where the round-3 X-Y-Z angle chart
+    was singular -- DART's coordinates have no singularity."""
     from scenario import core
     from scenario import gazebo as scenario
     gz = scenario.GazeboSimulator(0.001, 1.0, 1)
@@ -115,7 +118,6 @@ def test_scenario_ball_joint_torque_free_rotation(require_gpu):
     assert j.set_control_mode(core.JointControlMode_force)
     assert not j.set_control_mode(core.JointControlMode_position)  # JointController skips ball joints
     w0 = [0.5, 0.4, 2.0]  # about the major axis, tilted: a stable precessing motion
-    r0 = [0.1, -0.2, 0.15]
     assert j.reset_joint_position(r0) and j.reset_joint_velocity(w0)
     gz.run(paused=True)
     assert np.allclose(j.joint_position(), r0, atol=1e-6)
