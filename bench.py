@@ -624,8 +624,9 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True, exact=True):
     q0 = stand + rng.uniform(-0.1, 0.1, (W, 8))
     out = float_tree_leg(args, dev, torch, "quadruped", W, pgs, 0.45, [(400.0, 10.0, 60.0)] * 8,
                          q0, np.tile(stand, (W, 1)), rng.uniform(-5, 5, (W, 2)), exact=exact)
-    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: two exact box-QP stages, each from the previous "
-             f"step's solution after at most {pgs} PGS sweeps)" if exact else f"PGS {pgs} iterations")
+    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: two exact box-QP stages, each the primal "
+             f"active-set method from the previous step's working set after at most {min(pgs, 4)} PGS sweeps)"
+             if exact else f"PGS {pgs} iterations")
     out["workload"] = (f"{W} quadrupeds (16 kg, 8 dofs, floating base) standing on a ground plane under "
                        f"JointController PID hold, sphere-foot / box-trunk contacts, {solve}, dt = 1 ms")
     return out
@@ -658,9 +659,9 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
     out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
     out["scaling"] = "strong"
     out["worlds_per_gpu"] = e - b
-    solve = ("the exact boxed LCP (wave_lcp.hpp: PGS sweeps warm-started from the previous step's impulses, at "
-             "most 50, ending once a sweep moves no constraint velocity by 1e-6; then semismooth Newton / active-set "
-             "rounds, <= 24 linear solves per world-step; DART's Dantzig result)" if exact
+    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: a frictionless stage, then friction boxed by its "
+             "normals; each stage the primal active-set method from the previous step's working set after at most "
+             "4 PGS sweeps, <= 24 linear solves per world-step)" if exact
              else f"PGS {pgs} iterations only (mw_set_lcp_solver PGS)")
     out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
                        f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "
@@ -830,7 +831,8 @@ def scene_leg(args, dev, torch, W=4096, K=500, warm=100, G=50):
     rows = sc.contacts(0)
     fz3 = float(sum(r[8] for r in rows if int(r[12]) == 2)) * -1.0
     out = {"workload": f"{W} worlds x 3 cubes (the three-cube contact KAT scene), box-box + box-plane "
-                       "contacts, PGS 50, dt = 1 ms, scene kernel (one world per wavefront)",
+                       "contacts, the boxed LCP solved as DART does (two exact stages, each after at most 4 PGS "
+                       "sweeps), dt = 1 ms, scene kernel (one world per wavefront)",
            "value": round(W * steps / elapsed, 1), "unit": "env·steps/s", "steps": steps,
            "ms_per_step": round(elapsed / steps * 1e3, 6),
            "kernel_us_per_launch": round(e0.elapsed_time(e1) * 1e3 / steps, 3),
@@ -883,8 +885,9 @@ def contact_leg(args, dev, torch):
     steps = n_rep * G
     in_contact = int(sum(len(sim.contacts(w)) > 0 for w in range(0, W, 16)))
     exact = sim.lcp_solver()[0]
-    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: two exact box-QP stages, each from the previous "
-             "step's solution after at most 20 PGS sweeps)" if exact else "PGS 20 iterations")
+    solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: two exact box-QP stages, each the primal "
+             "active-set method from the previous step's working set after at most 4 PGS sweeps)"
+             if exact else "PGS 20 iterations")
     out = {"workload": f"{W} floating cubes (5 kg, 0.2 m) on a ground plane, box-plane contacts, "
                        f"normal + 2 friction rows per point, {solve}, dt = 1 ms",
            "kernel": {0: "free_run_kernel (free_body.hpp, PGS only)", 2: "wave_run_kernel (world per wavefront)"}.get(
