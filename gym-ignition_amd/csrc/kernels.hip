@@ -943,6 +943,20 @@ hipError_t float_n(const ChainF* P, bool cons, const FloatF* F, const SimDev& S,
 
 #ifdef MW_WAVE_PROF
 // debug builds only: read and clear the wave kernel's phase counters
+// debug builds: the dumped hard exact LCP of the wave kernel (wave_tree.hpp), then re-armed
+extern "C" int mw_debug_wave_dump(float* out, int n) {
+#ifdef MW_WAVE_PROF
+    if (n < static_cast<int>(sizeof(dev::g_wave_dump) / sizeof(float))) return 2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_wave_dump), sizeof(dev::g_wave_dump)) != hipSuccess) return 1;
+    const unsigned int z = 0u;
+    return hipMemcpyToSymbol(HIP_SYMBOL(dev::g_wave_dump_claim), &z, sizeof(z)) == hipSuccess ? 0 : 1;
+#else
+    (void)out;
+    (void)n;
+    return 1;
+#endif
+}
+
 extern "C" int mw_debug_wave_prof(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_wave_prof), sizeof(dev::g_wave_prof)) != hipSuccess) return 1;
     const unsigned long long z[dev::kWaveProfPhases] = {};

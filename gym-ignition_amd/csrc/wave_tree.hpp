@@ -113,6 +113,10 @@ constexpr int kWaveProfPhases = 20;  // [8] exact-LCP linear solves, [9] its rou
                                      // [16] in the exact solve's per-stage sweeps, [17] in its stage 1
 #ifdef MW_WAVE_PROF
 __device__ unsigned long long g_wave_prof[kWaveProfPhases];
+// one hard exact LCP (the first world-step with >= 8 linear solves): n, A,
+// b, lo, hi, kind, both warm records, both results (scripts/wave_prof.py)
+__device__ float g_wave_dump[8 + 64 * 64 + 9 * 64];
+__device__ unsigned int g_wave_dump_claim;
 #define MW_PROF_T(var) const long long var = clock64()
 #define MW_PROF_ACC(k, a, b) (prof[k] += static_cast<unsigned long long>((b) - (a)))
 #else
@@ -738,6 +742,33 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                                       : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
                                                                      L.rc, U, x1s, xe, nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
+            if (nsolve >= 8) {
+                unsigned int claim = 0u;
+                if (lane == 0) claim = atomicCAS(&g_wave_dump_claim, 0u, 1u);
+                claim = __builtin_amdgcn_readfirstlane(claim);
+                if (claim == 0u) {
+                    float* D0 = g_wave_dump;
+                    for (int r = 0; r < R; ++r) D0[8 + r * 64 + lane] = (lane < R) ? a[r] : 0.f;
+                    float* V = D0 + 8 + 64 * 64;
+                    if (lane < R) {
+                        V[lane] = Rw.b;
+                        V[64 + lane] = Rw.lo;
+                        V[128 + lane] = Rw.hi;
+                        V[192 + lane] = static_cast<float>(Rw.kind);
+                        V[256 + lane] = x0;
+                        V[320 + lane] = x1w;
+                        V[384 + lane] = xe;
+                        V[448 + lane] = x1s;
+                    }
+                    if (lane == 0) {
+                        D0[0] = static_cast<float>(R);
+                        D0[1] = static_cast<float>(nsolve);
+                        D0[2] = static_cast<float>(nsolve1);
+                        D0[3] = mu;
+                        D0[4] = ok ? 1.f : 0.f;
+                    }
+                }
+            }
             prof[8] += static_cast<unsigned long long>(nsolve);
             prof[9] += static_cast<unsigned long long>(nround);
             prof[10] += static_cast<unsigned long long>(nsolve1);

@@ -221,7 +221,23 @@ def boxqp(A, b, L, U, x, budget, stats, ws0=None):
         al[hi_hit] = (U[hi_hit] - x[hi_hit]) / d[hi_hit]
         al = np.maximum(al, 0)
         amin = al.min(initial=1)
-        if amin < 1:
+        if amin < 1 and os.environ.get("PROJ", "0") != "0":
+            # projected full step: every row the full step pushes past a bound
+            # joins the working set there, if the objective still decreases
+            obj = lambda v: float(0.5 * v.astype(np.float64) @ (A.astype(np.float64) @ v.astype(np.float64))
+                                  - b.astype(np.float64) @ v.astype(np.float64))
+            xp = np.where(fr, np.clip(x + d, L, U), x).astype(f32)
+            if obj(xp) < obj(x):
+                hit = lo_hit | hi_hit
+                ws = np.where(lo_hit, 1, np.where(hi_hit, 2, ws))
+                x = xp
+                stats["proj"] = stats.get("proj", 0) + 1
+                continue
+            blk = int(np.argmin(al))
+            x = np.where(fr, x + amin * d, x).astype(f32)
+            x[blk] = L[blk] if lo_hit[blk] else U[blk]
+            ws[blk] = 1 if lo_hit[blk] else 2
+        elif amin < 1:
             blk = int(np.argmin(al))
             x = np.where(fr, x + amin * d, x).astype(f32)
             x[blk] = L[blk] if lo_hit[blk] else U[blk]

@@ -131,4 +131,16 @@ print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f}
       f"{buf[14] / W / T:.0f} cycles/world-step in the linear solves, {buf[15] / W / T:.0f} in the PGS sweeps "
       f"(PGS-only mode) / the whole exact solve incl. its per-stage sweeps (exact mode); "
       f"{buf[16] / W / T:.0f} in the per-stage sweeps, {buf[17] / W / T:.0f} in stage 1")
+dump = np.zeros(8 + 64 * 64 + 9 * 64, dtype=np.float32)
+fd = L.mw_debug_wave_dump
+fd.argtypes = [ctypes.c_void_p, ctypes.c_int]
+if fd(dump.ctypes.data, dump.size) == 0 and dump[0] > 0:
+    n = int(dump[0])
+    A = dump[8:8 + 64 * 64].reshape(64, 64)[:n, :n]
+    V = dump[8 + 64 * 64:].reshape(9, 64)[:, :n]
+    out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "wave_dump.npz")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    np.savez(out, A=A.T.copy(), b=V[0], lo=V[1], hi=V[2], kind=V[3], xw=V[4], xw1=V[5], x=V[6], x1=V[7],
+             nsolve=dump[1], nsolve2=dump[2], mu=dump[3], ok=dump[4])
+    print(f"dumped a hard LCP: {n} rows, {int(dump[1])} solves ({int(dump[2])} in stage 2), ok {int(dump[4])}")
 sim.close()
