@@ -1151,11 +1151,13 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 int nsolve = 0, nround = 0, nsolve1 = 0;
                 long long cyc[3] = {0, 0, 0};
                 x1s = xw1;
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32>(a, Rw, mu, NR, lcp_solves, pgs_iters, kScExactPgsTol,
-                                                                L.rc, Uw, x1s, x0, nsolve, nround, nsolve1, cyc)
-                                           : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, NR, lcp_solves, pgs_iters,
-                                                                          kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
-                                                                          nround, nsolve1, cyc);
+                // paired elimination steps (wave_lcp.hpp lcp_ge_solve)
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                                                                      kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
+                                                                      nround, nsolve1, cyc)
+                                           : wave_lcp_exact<kWaveMaxRows, true>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                                                                                kScExactPgsTol, L.rc, Uw, x1s, x0,
+                                                                                nsolve, nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
 #ifdef MW_WAVE_PROF
                 // debug dump of one hard LCP (the first with >= 6 solves): n, A,

@@ -194,10 +194,21 @@ __device__ __forceinline__ float lcp_row_residual(bool live, float b, float xl, 
 // where a v_readlane per column stalled the FMA on its SGPR); the rows stay
 // there for the back substitution, where lane l gathers U[l][j - l]
 // (stride - 1 odd: the 64 lanes hit 64 banks).  U: 16-byte aligned,
-// kLcpUStride * 64 floats.
+// kLcpUStride * 65 floats (a scratch row for the paired steps).
 constexpr int kLcpUStride = 68;
 constexpr int kLcpRhs = 64;
-constexpr int kLcpWorkFloats = 64 * kLcpUStride;  // the workspace the caller provides
+constexpr int kLcpScratchRow = 64;  // the unreduced second row of a paired step
+constexpr int kLcpWorkFloats = 65 * kLcpUStride;  // the workspace the caller provides
+// the second row of a paired step starts at this offset (its rhs at 0), so
+// that its columns from j + 2 go out as aligned float4 stores
+constexpr int kLcpBOff = 3;
+
+// Pair (pivot = false): eliminate two columns per step (one LDS round trip
+// and one dependent rcp chain per pair of rows instead of per row).  Same FMA
+// sequence as two single steps, so the same bits.  Measured (r04t/r04u): the
+// scene kernel's LCPs 1.965 -> 1.728 ms per leg step; the wave kernel's
+// linear solves slower (16.3k -> 18.1k cycles per solve), so it keeps
+// single steps.
 
 // pivot = false: the system is symmetric positive definite (the staggered
 // rounds' principal submatrices A_FF, identity rows elsewhere), eliminated in
@@ -207,13 +218,14 @@ constexpr int kLcpWorkFloats = 64 * kLcpUStride;  // the workspace the caller pr
 // cols (pivot = false): the rows / columns that take part; row j outside it is
 // an identity row whose column is zero in every other row (a held row of the
 // active-set solve), so its step only shifts the registers and its d is 0.
-template <int RC>
+template <int RC, bool Pair = false>
 __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U, bool pivot,
                                               uint64_t cols = ~0ull) {
     static_assert(RC % 8 == 0, "row blocks of 8");
     const int lane = lane_id();
     if (pivot) cols = ~0ull;
     bool used = lane >= n;
+    int boff = 0;  // offset of the lane's row in U (kLcpBOff: stored by a paired step)
     for (int j = 0; j < n; ++j) {
         const int left = n - j;  // live columns
         if (!mask_bit(cols, j)) {
@@ -222,6 +234,77 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
                 if ((c & 7) == 0 && c >= left) break;
                 k[c] = k[c + 1];
             }
+            continue;
+        }
+        if (Pair && !pivot && j + 1 < n && mask_bit(cols, j + 1)) {
+            // rows j (A) and j + 1 (S, unreduced) to LDS; every lane then
+            // forms the reduced row B = S - g A (g = S0 / A0) on the fly and
+            // takes both multiples: f1 = k0 / A0, f2 = (k1 - f1 A1) / B1.
+            // Lane j + 1 takes f1 = g, f2 = 0, i.e. ends holding B from its
+            // column 2, and stores it after the loop at the row offset kLcpBOff
+            // (16-byte aligned stores; no LDS store inside the column loop,
+            // which would serialise its loads)
+            float* rowA = U + j * kLcpUStride;
+            float* rowB = rowA + kLcpUStride;
+            float* rowS = U + kLcpScratchRow * kLcpUStride;
+            if (lane == j || lane == j + 1) {
+                float* dst = (lane == j) ? rowA : rowS;
+                float4* u = reinterpret_cast<float4*>(dst);
+#pragma unroll
+                for (int c = 0; c < RC; c += 4) {
+                    if ((c & 7) == 0 && c >= left) break;
+                    u[c / 4] = make_float4(k[c], k[c + 1], k[c + 2], k[c + 3]);
+                }
+                dst[kLcpRhs] = rhs;
+            }
+            wave_lds_sync();
+            const float4* ua = reinterpret_cast<const float4*>(rowA);
+            const float4* us = reinterpret_cast<const float4*>(rowS);
+            float4 a = ua[0], sv = us[0];
+            const float arhs = rowA[kLcpRhs], srhs = rowS[kLcpRhs];
+            const float pa = (fabsf(a.x) < 1e-30f) ? 1e-30f : a.x;
+            const float g = sv.x * rcp(pa);
+            const float b1 = fmaf(-g, a.y, sv.y);
+            const float pb = (fabsf(b1) < 1e-30f) ? 1e-30f : b1;
+            const float brhs = fmaf(-g, arhs, srhs);
+            const bool wb = lane == j + 1;
+            const bool act = !(used || lane == j || wb);
+            const float f1 = act ? k[0] * rcp(pa) : (wb ? g : 0.f);
+            const float f2 = act ? fmaf(-f1, a.y, k[1]) * rcp(pb) : 0.f;
+#pragma unroll
+            for (int c = 0; c < RC; c += 4) {
+                if ((c & 7) == 0 && c >= left) break;
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 an = (c + 4 < RC) ? ua[c / 4 + 1] : z;
+                const float4 sn = (c + 4 < RC) ? us[c / 4 + 1] : z;
+                // B at columns c + 2 .. c + 5
+                const float e0 = fmaf(-g, a.z, sv.z), e1 = fmaf(-g, a.w, sv.w);
+                const float e2 = fmaf(-g, an.x, sn.x), e3 = fmaf(-g, an.y, sn.y);
+                k[c] = fmaf(-f2, e0, fmaf(-f1, a.z, k[c + 2]));
+                k[c + 1] = fmaf(-f2, e1, fmaf(-f1, a.w, k[c + 3]));
+                if (c + 4 < RC) {
+                    k[c + 2] = fmaf(-f2, e2, fmaf(-f1, an.x, k[c + 4]));
+                    k[c + 3] = fmaf(-f2, e3, fmaf(-f1, an.y, k[c + 5]));
+                }
+                a = an;
+                sv = sn;
+            }
+            rhs = fmaf(-f2, brhs, fmaf(-f1, arhs, rhs));
+            if (wb) {
+                // row j + 1 from its pivot B1: rhs at 0, B1 at kLcpBOff, columns
+                // j + 2 .. at kLcpBOff + 1 ..
+                float4* u = reinterpret_cast<float4*>(rowB + kLcpBOff + 1);
+#pragma unroll
+                for (int c = 0; c < RC; c += 4) {
+                    if ((c & 7) == 0 && c + 2 >= left) break;
+                    u[c / 4] = make_float4(k[c], k[c + 1], k[c + 2], k[c + 3]);
+                }
+                rowB[kLcpBOff] = b1;
+                rowB[0] = rhs;
+                boff = kLcpBOff;
+            }
+            used = used || lane == j || wb;
+            ++j;
             continue;
         }
         const int p = pivot ? wave_argmax(used ? -1.f : fabsf(k[0])) : j;
@@ -264,8 +347,8 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
     wave_lds_sync();
     float acc = 0.f, rdiag = 1.f;
     if (lane < n && mask_bit(cols, lane)) {
-        acc = U[lane * kLcpUStride + kLcpRhs];
-        float dg = U[lane * kLcpUStride];
+        acc = U[lane * kLcpUStride + (boff ? 0 : kLcpRhs)];
+        float dg = U[lane * kLcpUStride + boff];
         dg = (fabsf(dg) < 1e-30f) ? 1e-30f : dg;
         rdiag = rcp(dg);
     }
@@ -274,7 +357,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
         if (!mask_bit(cols, j)) continue;
         const float dj = read_lane(acc * rdiag, j);
         dl = (lane == j) ? dj : dl;
-        if (lane < j) acc = fmaf(-U[lane * (kLcpUStride - 1) + j], dj, acc);
+        if (lane < j) acc = fmaf(-U[lane * (kLcpUStride - 1) + boff + j], dj, acc);
     }
     return dl;
 }
@@ -297,7 +380,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 // fp32 floor; converged if within kLcpFloorAccept of the tolerance).  solves
 // counts the linear solves against `budget`.
 // Returns true when every row's residual is within tolerance.
-template <int RC>
+template <int RC, bool Pair = false>
 __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
                                            float arr, int n, int budget, float* __restrict__ Uw, float& xl, int ws0,
                                            int& solves, int& iters, long long& ge_cycles) {
@@ -360,7 +443,7 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
 #ifdef MW_WAVE_PROF
         const long long tg0 = clock64();
 #endif
-        const float d = lcp_ge_solve<RC>(k, fr ? -g : 0.f, n, Uw, false, freeM);
+        const float d = lcp_ge_solve<RC, Pair>(k, fr ? -g : 0.f, n, Uw, false, freeM);
 #ifdef MW_WAVE_PROF
         ge_cycles += clock64() - tg0;
 #else
@@ -467,7 +550,7 @@ __device__ __forceinline__ void wave_pgs_box(const float (&a)[kWaveMaxRows], F4*
 #endif
 constexpr int kLcpStageSweeps = MW_LCP_STAGE_SWEEPS;
 
-template <int RC>
+template <int RC, bool Pair = false>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
                                                float* __restrict__ Uw, float& x1, float& xl, int& n_solves,
@@ -502,7 +585,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #ifdef MW_WAVE_PROF
     cyc[1] += clock64() - tp;
 #endif
-    const bool ok1 = wave_boxqp<RC>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
+    const bool ok1 = wave_boxqp<RC, Pair>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     x1 = R.live ? x : 0.f;
 #ifdef MW_WAVE_PROF
     cyc[2] += clock64() - tc0;
@@ -531,7 +614,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #ifdef MW_WAVE_PROF
     cyc[1] += clock64() - tp;
 #endif
-    const bool ok2 = wave_boxqp<RC>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
+    const bool ok2 = wave_boxqp<RC, Pair>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     xl = R.live ? x : 0.f;
     n_solves = solves;
     n_rounds = iters;

@@ -6,7 +6,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-flags = ["-O3", "-std=c++17", "-fno-slp-vectorize", "-DMW_FAST_MATH", "-ffinite-math-only", "-fno-signed-zeros"]
+flags = ["-O3", "-std=c++17", "-fno-slp-vectorize", "-DMW_FAST_MATH", "-ffinite-math-only", "-fno-signed-zeros",
+         *os.environ.get("EXTRA", "").split()]
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *flags, f"-I{ROOT}/include",
        f"-I{ROOT}/gym-ignition_amd/csrc", "-c", f"{ROOT}/gym-ignition_amd/csrc/kernels.hip",
        "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"]
