@@ -1151,7 +1151,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 int nsolve = 0, nround = 0, nsolve1 = 0;
                 long long cyc[3] = {0, 0, 0};
                 x1s = xw1;
-                // paired elimination steps (wave_lcp.hpp lcp_ge_solve)
+                // long-row elimination (wave_lcp.hpp lcp_ge_solve)
                 const bool ok = (NR <= 32) ? wave_lcp_exact<32, true>(a, Rw, mu, NR, lcp_solves, pgs_iters,
                                                                       kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
                                                                       nround, nsolve1, cyc)

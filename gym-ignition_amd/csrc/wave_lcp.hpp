@@ -203,12 +203,17 @@ constexpr int kLcpWorkFloats = 65 * kLcpUStride;  // the workspace the caller pr
 // that its columns from j + 2 go out as aligned float4 stores
 constexpr int kLcpBOff = 3;
 
-// Pair (pivot = false): eliminate two columns per step (one LDS round trip
-// and one dependent rcp chain per pair of rows instead of per row).  Same FMA
-// sequence as two single steps, so the same bits.  Measured (r04t/r04u): the
-// scene kernel's LCPs 1.965 -> 1.728 ms per leg step; the wave kernel's
-// linear solves slower (16.3k -> 18.1k cycles per solve), so it keeps
-// single steps.
+// LongRows (the scene kernel's LCPs: up to 96 rows, 20-60 of them live)
+// eliminates two columns per step (pivot = false: one LDS round trip and one
+// dependent rcp chain per pair of rows; the same FMA sequence as two single
+// steps, so the same bits), and each column loop stops at the live columns.
+// Otherwise (the wave kernels' LCPs, <= 32 rows in the common case): single
+// steps over the whole register row with no exit -- an exit from the unrolled
+// loop costs a copy of the register row on every exit edge (the compiler's
+// phi resolution), more than the dead columns' FMAs.  Measured on the legs
+// (gpurun_out r04t / r04v): scene 1.965 (single, exits) -> 1.728 ms
+// (LongRows) vs 1.886 (pairs without exits); humanoid_c5 132.6 (single,
+// exits) -> 128.9 us (no exits) vs 141.7 (pairs without exits).
 
 // pivot = false: the system is symmetric positive definite (the staggered
 // rounds' principal submatrices A_FF, identity rows elsewhere), eliminated in
@@ -218,7 +223,17 @@ constexpr int kLcpBOff = 3;
 // cols (pivot = false): the rows / columns that take part; row j outside it is
 // an identity row whose column is zero in every other row (a held row of the
 // active-set solve), so its step only shifts the registers and its d is 0.
-template <int RC, bool Pair = false>
+// c - f * b as a three-address v_fma_f32: the elimination's register shift
+// k[c] = k[c + 1] - f u[c + 1] then writes k[c]'s own register (the compiler's
+// two-address v_fmac would land in k[c + 1]'s and add a v_mov per column to
+// rotate the loop-carried registers back)
+__device__ __forceinline__ float ge_fnma(float f, float b, float c) {
+    float d;
+    asm("v_fma_f32 %0, -%1, %2, %3" : "=v"(d) : "v"(f), "v"(b), "v"(c));
+    return d;
+}
+
+template <int RC, bool LongRows = false>
 __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, float* __restrict__ U, bool pivot,
                                               uint64_t cols = ~0ull) {
     static_assert(RC % 8 == 0, "row blocks of 8");
@@ -231,12 +246,12 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
         if (!mask_bit(cols, j)) {
 #pragma unroll
             for (int c = 0; c < RC - 1; ++c) {
-                if ((c & 7) == 0 && c >= left) break;
+                if (LongRows && (c & 7) == 0 && c >= left) break;
                 k[c] = k[c + 1];
             }
             continue;
         }
-        if (Pair && !pivot && j + 1 < n && mask_bit(cols, j + 1)) {
+        if (LongRows && !pivot && j + 1 < n && mask_bit(cols, j + 1)) {
             // rows j (A) and j + 1 (S, unreduced) to LDS; every lane then
             // forms the reduced row B = S - g A (g = S0 / A0) on the fly and
             // takes both multiples: f1 = k0 / A0, f2 = (k1 - f1 A1) / B1.
@@ -252,7 +267,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
                 float4* u = reinterpret_cast<float4*>(dst);
 #pragma unroll
                 for (int c = 0; c < RC; c += 4) {
-                    if ((c & 7) == 0 && c >= left) break;
+                    if (LongRows && (c & 7) == 0 && c >= left) break;
                     u[c / 4] = make_float4(k[c], k[c + 1], k[c + 2], k[c + 3]);
                 }
                 dst[kLcpRhs] = rhs;
@@ -273,18 +288,18 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
             const float f2 = act ? fmaf(-f1, a.y, k[1]) * rcp(pb) : 0.f;
 #pragma unroll
             for (int c = 0; c < RC; c += 4) {
-                if ((c & 7) == 0 && c >= left) break;
+                if (LongRows && (c & 7) == 0 && c >= left) break;
                 const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
                 const float4 an = (c + 4 < RC) ? ua[c / 4 + 1] : z;
                 const float4 sn = (c + 4 < RC) ? us[c / 4 + 1] : z;
                 // B at columns c + 2 .. c + 5
                 const float e0 = fmaf(-g, a.z, sv.z), e1 = fmaf(-g, a.w, sv.w);
                 const float e2 = fmaf(-g, an.x, sn.x), e3 = fmaf(-g, an.y, sn.y);
-                k[c] = fmaf(-f2, e0, fmaf(-f1, a.z, k[c + 2]));
-                k[c + 1] = fmaf(-f2, e1, fmaf(-f1, a.w, k[c + 3]));
+                k[c] = ge_fnma(f2, e0, ge_fnma(f1, a.z, k[c + 2]));
+                k[c + 1] = ge_fnma(f2, e1, ge_fnma(f1, a.w, k[c + 3]));
                 if (c + 4 < RC) {
-                    k[c + 2] = fmaf(-f2, e2, fmaf(-f1, an.x, k[c + 4]));
-                    k[c + 3] = fmaf(-f2, e3, fmaf(-f1, an.y, k[c + 5]));
+                    k[c + 2] = ge_fnma(f2, e2, ge_fnma(f1, an.x, k[c + 4]));
+                    k[c + 3] = ge_fnma(f2, e3, ge_fnma(f1, an.y, k[c + 5]));
                 }
                 a = an;
                 sv = sn;
@@ -296,7 +311,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
                 float4* u = reinterpret_cast<float4*>(rowB + kLcpBOff + 1);
 #pragma unroll
                 for (int c = 0; c < RC; c += 4) {
-                    if ((c & 7) == 0 && c + 2 >= left) break;
+                    if (LongRows && (c & 7) == 0 && c + 2 >= left) break;
                     u[c / 4] = make_float4(k[c], k[c + 1], k[c + 2], k[c + 3]);
                 }
                 rowB[kLcpBOff] = b1;
@@ -313,7 +328,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
             float4* u = reinterpret_cast<float4*>(row);
 #pragma unroll
             for (int c = 0; c < RC; c += 4) {
-                if ((c & 7) == 0 && c >= left) break;
+                if (LongRows && (c & 7) == 0 && c >= left) break;
                 u[c / 4] = make_float4(k[c], k[c + 1], k[c + 2], k[c + 3]);
             }
             row[kLcpRhs] = rhs;
@@ -332,12 +347,12 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
         const float f = (used || lane == p) ? 0.f : k[0] * rcp(piv);
 #pragma unroll
         for (int c = 0; c < RC; c += 4) {
-            if ((c & 7) == 0 && c >= left) break;
+            if (LongRows && (c & 7) == 0 && c >= left) break;
             const float4 nxt = (c + 4 < RC) ? ur[c / 4 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-            k[c] = fmaf(-f, cur.y, k[c + 1]);
-            k[c + 1] = fmaf(-f, cur.z, k[c + 2]);
-            k[c + 2] = fmaf(-f, cur.w, k[c + 3]);
-            if (c + 4 < RC) k[c + 3] = fmaf(-f, nxt.x, k[c + 4]);
+            k[c] = ge_fnma(f, cur.y, k[c + 1]);
+            k[c + 1] = ge_fnma(f, cur.z, k[c + 2]);
+            k[c + 2] = ge_fnma(f, cur.w, k[c + 3]);
+            if (c + 4 < RC) k[c + 3] = ge_fnma(f, nxt.x, k[c + 4]);
             cur = nxt;
         }
         rhs = fmaf(-f, prhs, rhs);
@@ -380,7 +395,7 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
 // fp32 floor; converged if within kLcpFloorAccept of the tolerance).  solves
 // counts the linear solves against `budget`.
 // Returns true when every row's residual is within tolerance.
-template <int RC, bool Pair = false>
+template <int RC, bool LongRows = false>
 __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
                                            float arr, int n, int budget, float* __restrict__ Uw, float& xl, int ws0,
                                            int& solves, int& iters, long long& ge_cycles) {
@@ -443,7 +458,7 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
 #ifdef MW_WAVE_PROF
         const long long tg0 = clock64();
 #endif
-        const float d = lcp_ge_solve<RC, Pair>(k, fr ? -g : 0.f, n, Uw, false, freeM);
+        const float d = lcp_ge_solve<RC, LongRows>(k, fr ? -g : 0.f, n, Uw, false, freeM);
 #ifdef MW_WAVE_PROF
         ge_cycles += clock64() - tg0;
 #else
@@ -550,7 +565,7 @@ __device__ __forceinline__ void wave_pgs_box(const float (&a)[kWaveMaxRows], F4*
 #endif
 constexpr int kLcpStageSweeps = MW_LCP_STAGE_SWEEPS;
 
-template <int RC, bool Pair = false>
+template <int RC, bool LongRows = false>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
                                                float* __restrict__ Uw, float& x1, float& xl, int& n_solves,
@@ -585,7 +600,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #ifdef MW_WAVE_PROF
     cyc[1] += clock64() - tp;
 #endif
-    const bool ok1 = wave_boxqp<RC, Pair>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
+    const bool ok1 = wave_boxqp<RC, LongRows>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     x1 = R.live ? x : 0.f;
 #ifdef MW_WAVE_PROF
     cyc[2] += clock64() - tc0;
@@ -614,7 +629,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #ifdef MW_WAVE_PROF
     cyc[1] += clock64() - tp;
 #endif
-    const bool ok2 = wave_boxqp<RC, Pair>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
+    const bool ok2 = wave_boxqp<RC, LongRows>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     xl = R.live ? x : 0.f;
     n_solves = solves;
     n_rounds = iters;

@@ -737,10 +737,11 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #else
             constexpr int kLcpSmall = 32;
 #endif
-            const bool ok = (R <= kLcpSmall) ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
-                                                           nsolve, nround, nsolve1, cyc)
-                                      : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
-                                                                     L.rc, U, x1s, xe, nsolve, nround, nsolve1, cyc);
+            const bool ok = (R <= kLcpSmall)
+                                ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s,
+                                                            xe, nsolve, nround, nsolve1, cyc)
+                                : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
+                                                                      L.rc, U, x1s, xe, nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
             if (nsolve >= 8) {
                 unsigned int claim = 0u;
