@@ -472,24 +472,28 @@ __device__ __forceinline__ SV ball_bias_velocity(const BodyF& b, const float* qd
 // theta = th[0..2], w = w[0..2] (quaternion product; angle in [0, pi])
 __device__ __forceinline__ float ball_integrate(float t0, float t1, float t2, float w0, float w1, float w2, float dt,
                                                 int k) {
-    auto quat = [](float x, float y, float z, float (&qt)[4]) {
-        const float t = sqrtf(x * x + y * y + z * z);
-        float sh, ch;
-        sincos_joint(0.5f * t, &sh, &ch);
-        const float s = (t < 1e-12f) ? 0.5f : sh * rcp(t);
-        qt[0] = ch; qt[1] = s * x; qt[2] = s * y; qt[3] = s * z;
+    // fp64: the stored rotation vector is rounded to fp32 once per step
+    // (unbiased), but an fp32 composition carries ~1 ulp of systematic error
+    // at a slowly moving angle, which drifts (r04r: 5e-5 rad after 500 steps
+    // at |theta| = pi/2 against DART's fp64 scheme); one joint part per lane,
+    // off the hot path
+    auto quat = [](double x, double y, double z, double (&qt)[4]) {
+        const double t = sqrt(x * x + y * y + z * z);
+        const double s = (t < 1e-150) ? 0.5 : sin(0.5 * t) / t;
+        qt[0] = cos(0.5 * t); qt[1] = s * x; qt[2] = s * y; qt[3] = s * z;
     };
-    float a[4], b[4];
+    double a[4], b[4];
+    const double h = dt;
     quat(t0, t1, t2, a);
-    quat(dt * w0, dt * w1, dt * w2, b);
-    float c0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
-    float c1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
-    float c2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
-    float c3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
-    if (c0 < 0.f) { c0 = -c0; c1 = -c1; c2 = -c2; c3 = -c3; }
-    const float v = sqrtf(c1 * c1 + c2 * c2 + c3 * c3);
-    const float f = (v < 1e-20f) ? 2.f * rcp(c0) : 2.f * atan2f(v, c0) * rcp(v);
-    return f * ((k == 0) ? c1 : ((k == 1) ? c2 : c3));
+    quat(h * w0, h * w1, h * w2, b);
+    double c0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    double c1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    double c2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    double c3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+    if (c0 < 0.0) { c0 = -c0; c1 = -c1; c2 = -c2; c3 = -c3; }
+    const double v = sqrt(c1 * c1 + c2 * c2 + c3 * c3);
+    const double f = (v < 1e-150) ? 2.0 / c0 : 2.0 * atan2(v, c0) / v;
+    return static_cast<float>(f * ((k == 0) ? c1 : ((k == 1) ? c2 : c3)));
 }
 
 // ABA with implicit damping over the kinematic tree TOPO: fills W, returns qdd.

@@ -52,7 +52,7 @@ def test_driver_bench_command(require_gpu):
     assert rl["time_us_per_launch"] == pytest.approx(out["ms_per_step"] * 1e3, rel=1e-3)
     h = out["humanoid_c5"]
     assert h["constraint_overflow"] == 0 and h["lcp_unconverged_world_steps"] is not None
-    assert "exact boxed LCP" in h["workload"] and "PGS" in out["humanoid_c5_pgs_only"]["workload"]
+    assert "boxed LCP solved as DART does" in h["workload"] and "PGS" in out["humanoid_c5_pgs_only"]["workload"]
     # configs 4 / 5: the 8-GPU strong split projected from the 8 rank shares timed alone
     for leg, wg in (("panda_c4", 1024), ("humanoid_c5", 512)):
         ps = out[leg]["projected_split"]
