@@ -737,11 +737,19 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #else
             constexpr int kLcpSmall = 32;
 #endif
-            const bool ok = (R <= kLcpSmall)
-                                ? wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s,
-                                                            xe, nsolve, nround, nsolve1, cyc)
-                                : wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol,
-                                                                      L.rc, U, x1s, xe, nsolve, nround, nsolve1, cyc);
+            // three register widths (wave_lcp.hpp: the elimination runs the
+            // whole register row): a free body's 4-corner LCP (12 rows) on 16
+            // columns took contacts_floating 195 -> 167 us (gpurun_out r04z)
+            bool ok;
+            if (R <= 16 && kLcpSmall > 0)
+                ok = wave_lcp_exact<16>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
+                                        nsolve1, cyc);
+            else if (R <= kLcpSmall)
+                ok = wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
+                                        nsolve1, cyc);
+            else
+                ok = wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
+                                                  nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
             if (nsolve >= 8) {
                 unsigned int claim = 0u;
