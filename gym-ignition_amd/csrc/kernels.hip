@@ -1102,3 +1102,55 @@ hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, int 
 }
 
 }  // namespace mw
+
+// ---- test hook: one linear solve of the exact LCP's active-set method -------
+// (include/mwstep.h mw_debug_lcp_solve; tests/test_gpu_lcp_solve.py checks both
+// paths against numpy on random SPD systems with held rows)
+namespace mw {
+namespace dev {
+__global__ void __launch_bounds__(64) debug_lcp_solve_kernel(const float* __restrict__ A, const float* __restrict__ rhs,
+                                                             uint64_t freeM, int n, int method, float* __restrict__ d) {
+    __shared__ float Uw[kLcpWorkFloats];
+    const int lane = lane_id();
+    float a[kWaveMaxRows];
+#pragma unroll
+    for (int r = 0; r < kWaveMaxRows; ++r) a[r] = (r < n && lane < n) ? A[r * n + lane] : 0.f;
+    const float rh = (lane < n) ? rhs[lane] : 0.f;
+    float out;
+    if (method == 0) {
+        out = (n <= 32) ? lcp_mfma_solve<32>(a, rh, freeM, Uw) : lcp_mfma_solve<64>(a, rh, freeM, Uw);
+    } else {
+        const bool fr = mask_bit(freeM, lane);
+        float k[kWaveMaxRows];
+#pragma unroll
+        for (int c = 0; c < kWaveMaxRows; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
+        out = lcp_ge_solve<kWaveMaxRows>(k, fr ? rh : 0.f, n, Uw, false, freeM);
+    }
+    d[lane] = out;
+}
+}  // namespace dev
+}  // namespace mw
+
+extern "C" int mw_debug_lcp_solve(const float* A, const float* rhs, uint64_t free_mask, int32_t n, int32_t method,
+                                  float* d) {
+    if (!A || !rhs || !d || n < 1 || n > mw::dev::kWaveMaxRows || method < 0 || method > 1) return 2;
+    float *dA = nullptr, *dr = nullptr, *dd = nullptr;
+    const size_t nn = static_cast<size_t>(n) * n;
+    int rc = 1;
+    if (hipMalloc(reinterpret_cast<void**>(&dA), nn * sizeof(float)) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dr), 64 * sizeof(float)) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dd), 64 * sizeof(float)) == hipSuccess &&
+        hipMemcpy(dA, A, nn * sizeof(float), hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dr, rhs, n * sizeof(float), hipMemcpyHostToDevice) == hipSuccess) {
+        const uint64_t live = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+        hipLaunchKernelGGL(mw::dev::debug_lcp_solve_kernel, dim3(1), dim3(64), 0, 0, dA, dr, free_mask & live, n,
+                           method, dd);
+        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(d, dd, n * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess)
+            rc = 0;
+    }
+    (void)hipFree(dA);
+    (void)hipFree(dr);
+    (void)hipFree(dd);
+    return rc;
+}

@@ -515,6 +515,14 @@ void quat_of(const std::array<double, 9>& R, double q[4]) {
 }
 
 // model m enters worlds [w0, w0 + nw) at its insertion pose, joints at rest
+// A reset, insertion or removal of a world's models re-arms its divergence
+// flag (mwscene.h): a world that diverged, was reset and diverges again is
+// reported again.
+int rearm_diverged(mw_scene* s, int32_t w0, int32_t nw) {
+    if (s->dev.diverged && nw > 0) SC_HIP(hipMemsetAsync(s->dev.diverged + w0, 0, nw, s->stream));
+    return MW_OK;
+}
+
 int place_model(mw_scene* s, int m, int32_t w0, int32_t nw) {
     if (int rc = pull_joints(s)) return rc;
     const SceneModel& sm = s->models[m];
@@ -547,7 +555,7 @@ int place_model(mw_scene* s, int m, int32_t w0, int32_t nw) {
                 s->h_wlast[(static_cast<size_t>(sl) * NNMAX + nd) * s->W + w] = -1;
     }
     s->present_dirty = s->base_dirty = s->cmd_dirty = s->wrench_dirty = true;
-    return MW_OK;
+    return rearm_diverged(s, w0, nw);
 }
 
 }  // namespace
@@ -738,7 +746,7 @@ int mw_scene_set_present(mw_scene* s, int32_t model, int32_t w0, int32_t nw, int
         else s->h_present[w] &= ~(1u << model);
     }
     s->present_dirty = true;
-    return MW_OK;
+    return present == 2 ? MW_OK : rearm_diverged(s, w0, nw);
 }
 
 int mw_scene_set_world_ground(mw_scene* s, int32_t w0, int32_t nw, int32_t enabled) {
@@ -1202,6 +1210,7 @@ int mw_scene_set_joints(mw_scene* s, int32_t field, int32_t w0, int32_t nw, cons
             }
         }
     s->cmd_dirty = true;
+    if (field == MW_SC_RESET_POSITION || field == MW_SC_RESET_VELOCITY) return rearm_diverged(s, w0, nw);
     return MW_OK;
 }
 
@@ -1377,7 +1386,7 @@ int mw_scene_reset_base_pose(mw_scene* s, int32_t model, int32_t w0, int32_t nw,
         s->hbflag()[static_cast<size_t>(model) * s->W + w0 + w] |= 1u;
     }
     s->base_dirty = true;
-    return MW_OK;
+    return rearm_diverged(s, w0, nw);
 }
 
 int mw_scene_reset_base_velocity(mw_scene* s, int32_t model, int32_t w0, int32_t nw, const double* v) {
@@ -1390,7 +1399,7 @@ int mw_scene_reset_base_velocity(mw_scene* s, int32_t model, int32_t w0, int32_t
         s->hbflag()[static_cast<size_t>(model) * s->W + w0 + w] |= 2u;
     }
     s->base_dirty = true;
-    return MW_OK;
+    return rearm_diverged(s, w0, nw);
 }
 
 int mw_scene_get_contacts(const mw_scene* cs, int32_t w, double* out, int32_t cap, int32_t* n) {

@@ -111,6 +111,12 @@ struct ScWarm {
 // PGS sweeps of exact mode end once a sweep moves no constraint velocity by
 // more than this (sim.cpp kExactPgsTol): the exact solve takes over
 constexpr float kScExactPgsTol = 1e-6f;
+// PGS sweeps per stage of the exact solve (wave_lcp.hpp STAGE_SWEEPS; the
+// wave kernels keep 4)
+#ifndef MW_SC_STAGE_SWEEPS
+#define MW_SC_STAGE_SWEEPS 6
+#endif
+constexpr int kScStageSweeps = MW_SC_STAGE_SWEEPS;
 
 // ODE dPlaneSpace (oracle.c plane_space), float32
 __device__ __forceinline__ void plane_space_f(f3 n, f3& p, f3& q) {
@@ -1152,10 +1158,10 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 long long cyc[3] = {0, 0, 0};
                 x1s = xw1;
                 // long-row elimination (wave_lcp.hpp lcp_ge_solve)
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true, kScStageSweeps>(a, Rw, mu, NR, lcp_solves, pgs_iters,
                                                                       kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
                                                                       nround, nsolve1, cyc)
-                                           : wave_lcp_exact<kWaveMaxRows, true>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                                           : wave_lcp_exact<kWaveMaxRows, true, kScStageSweeps>(a, Rw, mu, NR, lcp_solves, pgs_iters,
                                                                                 kScExactPgsTol, L.rc, Uw, x1s, x0,
                                                                                 nsolve, nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;

@@ -514,6 +514,14 @@ int setter(mw_sim* s, int32_t w0, int32_t nw, const int32_t* dofs, int32_t ndofs
     return MW_OK;
 }
 
+// A reset of a world's state re-arms its divergence flag (the flags mark
+// worlds whose state is not finite; a reset replaces that state): worlds that
+// diverged, were reset and diverge again are reported again (mwstep.h).
+int rearm_diverged(mw_sim* s, int32_t w0, int32_t nw) {
+    if (s->dev.div && nw > 0) MW_HIP(hipMemsetAsync(s->dev.div + w0, 0, nw, s->stream));
+    return MW_OK;
+}
+
 int copy_str(const std::string& v, char* buf, int32_t len) {
     if (!buf || len <= 0) return fail(MW_EINVAL, "invalid output buffer");
     if (static_cast<int32_t>(v.size()) + 1 > len) return fail(MW_EINVAL, "output buffer too small");
@@ -1533,23 +1541,25 @@ int mw_set_joint_position_targets(mw_sim* s, int32_t w0, int32_t nw, const int32
 
 int mw_reset_joint_positions(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
     // Joint::resetPosition writes JointPositionReset, applied by the next run (Joint.cpp:132-156)
-    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+    const int rc = setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
         if (!dry) {
             s->hrq()[s->idx(dof, w)] = static_cast<float>(x);
             s->hrflag()[s->idx(dof, w)] |= 1u | 4u;  // Joint::resetPosition also resets the PID
         }
         return MW_OK;
     });
+    return rc ? rc : rearm_diverged(s, w0, nw);
 }
 
 int mw_reset_joint_velocities(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, const double* v) {
-    return setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
+    const int rc = setter(s, w0, nw, d, nd, v, [&](int dof, int w, double x, bool dry) {
         if (!dry) {
             s->hrqd()[s->idx(dof, w)] = static_cast<float>(x);
             s->hrflag()[s->idx(dof, w)] |= 2u | 4u;
         }
         return MW_OK;
     });
+    return rc ? rc : rearm_diverged(s, w0, nw);
 }
 
 int mw_set_joint_control_mode(mw_sim* s, int32_t w0, int32_t nw, const int32_t* d, int32_t nd, int32_t mode) {
@@ -1749,7 +1759,7 @@ int mw_reset_base_pose(mw_sim* s, int32_t w0, int32_t nw, const double* in) {
         s->h_rflag[w0 + k] |= 1u;
     }
     s->free_dirty = true;
-    return MW_OK;
+    return rearm_diverged(s, w0, nw);
 }
 
 int mw_reset_base_velocity(mw_sim* s, int32_t w0, int32_t nw, const double* in) {
@@ -1763,7 +1773,7 @@ int mw_reset_base_velocity(mw_sim* s, int32_t w0, int32_t nw, const double* in) 
         s->h_rflag[w0 + k] |= 2u;
     }
     s->free_dirty = true;
-    return MW_OK;
+    return rearm_diverged(s, w0, nw);
 }
 
 int mw_set_pgs_options(mw_sim* s, double tol, int32_t warm_start) {

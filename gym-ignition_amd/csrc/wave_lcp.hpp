@@ -58,6 +58,11 @@ constexpr float kLcpStall = 1e-7f;
 // at the floor a stage counts as converged when its residual is within this
 // factor of the tolerance
 constexpr float kLcpFloorAccept = 64.f;
+// the active-set method's linear solves: 1 = block LDL^T on the matrix cores
+// (lcp_mfma_solve), 0 = Gaussian elimination over the lanes (lcp_ge_solve)
+#ifndef MW_LCP_MFMA
+#define MW_LCP_MFMA 1
+#endif
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
 // ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
@@ -377,6 +382,184 @@ __device__ __forceinline__ float lcp_ge_solve(float (&k)[RC], float rhs, int n, 
     return dl;
 }
 
+// ---- the active-set method's linear solve on the matrix cores ------------------
+// S d = rhs over the free rows (freeM; a held or dead row is an identity row and
+// column, rhs 0, d 0), S = the Delassus registers a[] (lane c: a[r] = A[r][c]),
+// symmetric positive definite on the free rows (DART's CFM).  Block LDL^T with
+// 2x2 pivot blocks and no pivot search (SPD), right-looking: every block step
+// is ONE v_mfma_f32_32x32x2_f32 per 32x32 tile -- the rank-2 update
+// S -= P D^-1 P^T of the trailing matrix, P = the two pivot columns, with
+// fp32 operands and fp32 accumulation (exact f32 FMAs on gfx950) -- instead of
+// two elimination steps of lcp_ge_solve (an LDS round trip and ~32 FMAs
+// each).  The tiles live in the MFMA accumulator layout: lane l holds column
+// l % 32, rows 8 (i / 4) + 4 (l / 32) + i % 4 in accumulator i, so row j of a
+// tile -- by symmetry its column j, the pivot panel -- is accumulator
+// 4 (j / 8) + j % 4 of one lane half, and one v_permlane32_swap turns it into
+// the MFMA's A operand (lane l: P[l % 32][l / 32]).  R <= 32: tile T00;
+// R <= 64: the upper tiles T00, T01, T11 (T10 = T01^T is not kept).  Block
+// steps whose two rows are both held are skipped (stage 1 holds every
+// friction row).  The forward substitution rides along (rhs in lane = row),
+// the L columns go to LDS (Lw, column-major, stride 65: the back substitution's
+// lane c reads row j of column c conflict-free), D^-1 is applied per 2x2
+// block, then the back substitution by lane reads of d.
+constexpr int kLcpLStride = 65;
+constexpr int kLcpMfmaWorkFloats = 64 * kLcpLStride;
+
+// x's lanes 32..63 <-> y's lanes 0..31 (v_permlane32_swap_b32)
+__device__ __forceinline__ void lane_swap32(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]);
+    y = __uint_as_float(r[1]);
+}
+// the value of lane l ^ 32
+__device__ __forceinline__ float lane_xor32(float v) {
+    float lo = v, hi = v;
+    lane_swap32(lo, hi);  // lo = [v_lo, v_lo], hi = [v_hi, v_hi]
+    return (lane_id() >= 32) ? lo : hi;
+}
+
+// The pivot block's inverse (d00, d01, d11; uniform) of rows / columns J, J + 1
+// of tile T, and this lane's panel entry P[lane % 32][J + lane / 32].
+template <int J>
+__device__ __forceinline__ void mfma_pivot(const v16f& T, float& d00, float& d01, float& d11) {
+    constexpr int i = 4 * (J / 8) + (J % 4), hl = 32 * ((J / 4) % 2);
+    const float s00 = read_lane(T[i], J + hl), s01 = read_lane(T[i], J + 1 + hl);
+    const float s11 = read_lane(T[i + 1], J + 1 + hl);
+    const float idet = rcp(fmaf(s00, s11, -s01 * s01));
+    d00 = s11 * idet;
+    d01 = -s01 * idet;
+    d11 = s00 * idet;
+}
+template <int J>
+__device__ __forceinline__ float mfma_panel(const v16f& T) {
+    constexpr int i = 4 * (J / 8) + (J % 4);
+    float x = T[i], y = T[i + 1];
+    lane_swap32(x, y);
+    return ((J / 4) % 2) ? y : x;
+}
+
+template <int RC>
+struct MfmaLdl {
+    v16f T00, T01, T11;
+    float r, y;
+    uint64_t freeM;
+    float* Lw;
+
+    // block step of rows / columns J, J + 1: factorisation (one MFMA per tile)
+    // and forward substitution
+    template <int J>
+    __device__ __forceinline__ void step() {
+        if (((freeM >> J) & 3ull) == 0ull) return;  // two held rows: identity, nothing to do
+        const int lane = lane_id();
+        const int c = lane & 31;
+        const bool hi = lane >= 32;
+        constexpr int JT = J % 32;
+        float d00, d01, d11, mine, mineb = 0.f, othb = 0.f;
+        if constexpr (J < 32) {
+            mfma_pivot<JT>(T00, d00, d01, d11);
+            mine = mfma_panel<JT>(T00);
+            if constexpr (RC == 64) {
+                mineb = mfma_panel<JT>(T01);
+                othb = lane_xor32(mineb);
+            }
+        } else {
+            mfma_pivot<JT>(T11, d00, d01, d11);
+            mine = mfma_panel<JT>(T11);
+        }
+        const float oth = lane_xor32(mine);
+        // L[c][J + h] of this lane's panel (P D^-1; D^-1 symmetric)
+        const float dh = hi ? d11 : d00;
+        const float Lm = fmaf(mine, dh, oth * d01);
+        const int lcol = (J + (hi ? 1 : 0)) * kLcpLStride;
+        if constexpr (J < 32) {
+            T00 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mine, Lm, T00, 0, 0, 0);
+            Lw[lcol + c] = Lm;
+            if constexpr (RC == 64) {
+                const float Lb = fmaf(mineb, dh, othb * d01);
+                T01 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mine, Lb, T01, 0, 0, 0);
+                T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mineb, Lb, T11, 0, 0, 0);
+                Lw[lcol + 32 + c] = Lb;
+            }
+        } else {
+            T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mine, Lm, T11, 0, 0, 0);
+            Lw[lcol + 32 + c] = Lm;
+        }
+        // forward substitution, lane = row: rows below the pair take
+        // P[row][J..J+1] D^-1 (rows < 32 from the top panel, rows >= 32 from
+        // the bottom one -- the T11 panel for J >= 32)
+        const float zj = read_lane(r, J), zj1 = read_lane(r, J + 1);
+        float p0, p1;
+        if constexpr (J < 32 && RC == 64) {
+            p0 = hi ? othb : mine;
+            p1 = hi ? mineb : oth;
+        } else {
+            p0 = hi ? oth : mine;
+            p1 = hi ? mine : oth;
+        }
+        const float l0 = fmaf(p0, d00, p1 * d01), l1 = fmaf(p0, d01, p1 * d11);
+        if (lane > J + 1) r = fmaf(-l0, zj, fmaf(-l1, zj1, r));
+        if (lane == J) y = fmaf(d00, zj, d01 * zj1);
+        if (lane == J + 1) y = fmaf(d01, zj, d11 * zj1);
+    }
+    template <int J>
+    __device__ __forceinline__ void forward() {
+        step<J>();
+        if constexpr (J + 2 < RC) forward<J + 2>();
+    }
+    // back substitution L^T d = y of pair J, then the pairs before it
+    template <int J>
+    __device__ __forceinline__ void backward() {
+        if (((freeM >> J) & 3ull) != 0ull) {
+            const int lane = lane_id();
+            const float dj = read_lane(y, J), dj1 = read_lane(y, J + 1);
+            if (lane < J) {
+                const float* col = Lw + lane * kLcpLStride;
+                y = fmaf(-col[J], dj, fmaf(-col[J + 1], dj1, y));
+            }
+        }
+        if constexpr (J >= 2) backward<J - 2>();
+    }
+};
+
+template <int RC>
+__device__ __forceinline__ float lcp_mfma_solve(const float (&a)[kWaveMaxRows], float rhs, uint64_t freeM,
+                                                float* __restrict__ Lw) {
+    static_assert(RC == 32 || RC == 64, "one or two tile rows");
+    const int lane = lane_id();
+    const int c = lane & 31;
+    const bool hi = lane >= 32;
+    MfmaLdl<RC> M;
+    M.freeM = freeM;
+    M.Lw = Lw;
+    M.T01 = v16f{};
+    M.T11 = v16f{};
+    // ---- the masked tiles: free x free entries of A, identity elsewhere
+    const bool cf0 = mask_bit(freeM, c), cf1 = mask_bit(freeM, 32 + c);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r0 = 8 * (i / 4) + (i % 4), r1 = r0 + 4;
+        const int rr = hi ? r1 : r0;  // this lane's row of accumulator i
+        const bool rf = hi ? mask_bit(freeM, r1) : mask_bit(freeM, r0);
+        float x = a[r0], y = a[r1];
+        lane_swap32(x, y);  // x: A[rr][c] (T00), y: A[rr][32 + c] (T01)
+        M.T00[i] = (rf && cf0) ? x : ((rr == c) ? 1.f : 0.f);
+        if constexpr (RC == 64) {
+            M.T01[i] = (rf && cf1) ? y : 0.f;
+            const bool rf1 = hi ? mask_bit(freeM, 32 + r1) : mask_bit(freeM, 32 + r0);
+            float u = a[32 + r0], v = a[32 + r1];
+            lane_swap32(u, v);  // v: A[32 + rr][32 + c]
+            M.T11[i] = (rf1 && cf1) ? v : ((rr == c) ? 1.f : 0.f);
+        }
+    }
+    // rhs of a held / dead row is 0 (its d is 0)
+    M.r = mask_bit(freeM, lane) ? rhs : 0.f;
+    M.y = 0.f;
+    M.template forward<0>();
+    wave_lds_sync();
+    M.template backward<RC - 2>();
+    return mask_bit(freeM, lane) ? M.y : 0.f;
+}
+
 // One strictly convex box QP  min 1/2 x'Ax - b'x,  L <= x <= U  (bounds fixed,
 // per lane; a dead or pinned row has L = U) by the primal active-set method
 // from x (inside the box): the working set starts as ws0 (1 held at L, 2 held
@@ -414,6 +597,8 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
     bool at_min = __ballot(!pinned && ws == 0) == 0ull;
     bool stalled = false; // ... by a refinement solve that moved nothing
     bool fresh = false;   // w / g / mag / xmax / rel belong to the current x
+    bool single = false;  // release one row at a time (after a blocked multi-release)
+    uint64_t released = 0ull;  // the rows of the last release
     float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f, rel = 0.f;
     float rel_refine = 3.4e38f;  // the residual when the last refinement solve started
     for (int it = 0; it < 4 * budget + 8 + n; ++it, ++iters) {
@@ -431,11 +616,18 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
             float v = (ws == 1) ? -g : ((ws == 2) ? g : 0.f);
             v = pinned ? 0.f : v * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol);
             // every held row whose multiplier is wrongly signed beyond its
-            // tolerance leaves at once (one solve for several micro-contacts;
-            // the method stays monotone: the next solve's blocking step keeps
-            // the iterate in the box)
-            if (wave_fmax(v) > 1.f) {
-                if (v > 1.f) ws = 0;
+            // tolerance leaves at once (one solve for several micro-contacts).
+            // Each step stays in the box and does not raise the objective, but
+            // with several rows released a released row can block the next
+            // step at zero length and rejoin; once that happens the rows leave
+            // one at a time, the most violated first (the textbook primal
+            // active-set rule, finite for a strictly convex QP).
+            const float vmax = wave_fmax(v);
+            if (vmax > 1.f) {
+                bool rel_me = v > 1.f;
+                if (single) rel_me = lane == __builtin_ctzll(static_cast<unsigned long long>(__ballot(v == vmax)));
+                if (rel_me) ws = 0;
+                released = __ballot(rel_me);
                 stalled = false;
                 continue;
             }
@@ -452,13 +644,18 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         // ---- one linear solve over the free rows
         const bool fr = !pinned && ws == 0;
         const uint64_t freeM = __ballot(fr);
-        float k[RC];
-#pragma unroll
-        for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
 #ifdef MW_WAVE_PROF
         const long long tg0 = clock64();
 #endif
+#if MW_LCP_MFMA
+        // block LDL^T on the matrix cores (R <= 32: one tile, else three)
+        const float d = lcp_mfma_solve<(RC <= 32) ? 32 : 64>(a, fr ? -g : 0.f, freeM, Uw);
+#else
+        float k[RC];
+#pragma unroll
+        for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
         const float d = lcp_ge_solve<RC, LongRows>(k, fr ? -g : 0.f, n, Uw, false, freeM);
+#endif
 #ifdef MW_WAVE_PROF
         ge_cycles += clock64() - tg0;
 #else
@@ -483,6 +680,9 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         if (amin < 1.f) {
             const int block = wave_argmax(-al);
             const int bside = __builtin_amdgcn_readlane(side, block);
+            // a row of a multi-row release blocks at once: release singly from now on
+            if (amin <= 0.f && mask_bit(released, block) && __builtin_popcountll(released) > 1) single = true;
+            released = 0ull;
             xl = fr ? xl + amin * d : xl;
             if (lane == block) {
                 xl = (bside == 1) ? L : U;
@@ -491,6 +691,7 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         } else {
             xl = fr ? xl + d : xl;
             at_min = true;
+            released = 0ull;
         }
     }
     return false;
@@ -565,7 +766,10 @@ __device__ __forceinline__ void wave_pgs_box(const float (&a)[kWaveMaxRows], F4*
 #endif
 constexpr int kLcpStageSweeps = MW_LCP_STAGE_SWEEPS;
 
-template <int RC, bool LongRows = false>
+// STAGE_SWEEPS: the cap on the sweeps per stage (the scene kernel's
+// three-cube stacks converge more often with 6: 3253 -> 2575 unconverged
+// world-steps, 1.757 -> 1.708 ms, profiles/r04z ab_sweeps)
+template <int RC, bool LongRows = false, int STAGE_SWEEPS = kLcpStageSweeps>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
                                                float* __restrict__ Uw, float& x1, float& xl, int& n_solves,
@@ -580,7 +784,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
     float arr = 1.f;  // A_rr (a dynamic register index would go to scratch)
 #pragma unroll
     for (int c = 0; c < RC; ++c) arr = (lane == c && R.live) ? a[c] : arr;
-    sweeps = sweeps < kLcpStageSweeps ? sweeps : kLcpStageSweeps;
+    sweeps = sweeps < STAGE_SWEEPS ? sweeps : STAGE_SWEEPS;
     int solves = 0, iters = 0;
     const bool fric = R.kind == 1;
     const float x1p = R.live ? x1 : 0.f, xlp = R.live ? xl : 0.f;  // the previous step's

@@ -145,6 +145,8 @@ SIGNATURES = [
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("mw_diverged", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_clear_diverged", ctypes.c_int, [_P, _I, _I]),
+    ("mw_debug_lcp_solve", ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                          ctypes.c_uint64, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mw_state_words", ctypes.c_int, [_P, _IP]),
     ("mw_get_state", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mw_set_state", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),

@@ -112,7 +112,11 @@ int mw_scene_lcp_solver(const mw_scene* sc, int32_t* mode, int32_t* max_solves);
 int mw_scene_lcp_unconverged(const mw_scene* sc, int64_t* world_steps);
 /* Failure detection (as mw_diverged): the scene kernel flags a world whose
  * stored joint or base state is not finite; mw_scene_run returns MW_EDIVERGED
- * when the run flagged new worlds (ScenarI/O run() -> false). */
+ * when the run flagged new worlds (ScenarI/O run() -> false).  A joint or
+ * base reset (mw_scene_set_joints with a reset field, mw_scene_reset_base_*),
+ * inserting a model into a world or removing it re-arms the world's flag, so
+ * a world that diverges again after a reset is reported again; the count is
+ * of flag events. */
 int mw_scene_diverged(mw_scene* sc, int32_t w0, int32_t nw, uint8_t* flags, int64_t* count);
 int mw_scene_clear_diverged(mw_scene* sc, int32_t w0, int32_t nw);
 int mw_scene_gravity(const mw_scene* sc, double g[3]);

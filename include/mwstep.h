@@ -314,17 +314,22 @@ int mw_copy_state(mw_sim* sim, float* q_dev, float* qd_dev, int to_sim);
  * flagged (the reference has no such check: GazeboSimulator::run,
  * GazeboSimulator.cpp:202-251, only reports a failed server step);
  * mw_run_device leaves the check to mw_diverged.  mw_diverged: flags[nw] of
- * worlds [w0, w0 + nw) (flags may be NULL) and the number of worlds flagged
- * since mw_initialize; mw_clear_diverged re-arms the flags of a range (after
- * the caller reset those worlds). */
+ * worlds [w0, w0 + nw) (flags may be NULL) and the number of flag events
+ * since mw_initialize (a world counts again each time it is flagged after
+ * its flag was re-armed); mw_clear_diverged re-arms the flags of a range.
+ * Any reset of a world's state re-arms its flag too: mw_reset_joint_positions
+ * / _velocities, mw_reset_base_pose / _velocity and mw_set_state, so a world
+ * that diverges, is reset and diverges again is reported again. */
 int mw_diverged(mw_sim* sim, int32_t w0, int32_t nw, uint8_t* flags, int64_t* count);
 int mw_clear_diverged(mw_sim* sim, int32_t w0, int32_t nw);
-/* The full per-world record as float32 words, [nw][words] in host memory:
- * q, qd, qdd, qlo (low word of the compensated joint positions), the
- * JointController PID state pErrLast / iErr / cmd (n_dofs each, absent for
- * joint-less bodies), the base pose and body-frame twist (13, floating and
- * welded-tree models), and the previous step's constraint impulses that the
- * wave kernel's warm start / exact LCP starts from (its models only).
+/* The full per-world record as float32 words, [nw][words] in host memory, in
+ * this order: q, qd, qdd, then the JointController PID state pErrLast, iErr,
+ * cmd, then qlo (the low word of the compensated joint positions) -- n_dofs
+ * words each, absent for joint-less bodies -- then the base pose (x y z, qw qx
+ * qy qz) and body-frame twist (w, v) (13 words, floating and welded-tree
+ * models), then the previous step's constraint impulses that the wave
+ * kernel's warm start / exact LCP starts from (its models only: the final
+ * impulses, then the stage-1 impulses, per contact slot and joint row).
  * mw_set_state writes the record back (bit-exact: a restored world steps
  * exactly as it did from the saved state), drops the worlds' pending resets
  * and clears their divergence flags.  The simulator time, the controller
@@ -398,6 +403,15 @@ int mw_vecenv_counters(mw_vecenv* env, uint32_t* episode_dev, uint32_t* steps_de
  * gravity z float32 [n_worlds]) into caller device buffers; MW_ESTATE when the
  * env was created without randomisation. */
 int mw_vecenv_physics(mw_vecenv* env, float* mass_dev, float* gravity_z_dev);
+
+/* ---- test hook (not part of the ScenarI/O surface) ----
+ * One linear solve of the exact LCP's active-set method on a single wavefront
+ * (csrc/wave_lcp.hpp): S d = rhs restricted to the rows of free_mask (held
+ * rows: d = 0), S = the row-major n x n matrix A (n <= 64, symmetric positive
+ * definite on the free rows), host buffers.  method 0: block LDL^T on the
+ * matrix cores (lcp_mfma_solve, the kernels' default), 1: Gaussian
+ * elimination over the lanes (lcp_ge_solve).  Returns 0 on success. */
+int mw_debug_lcp_solve(const float* A, const float* rhs, uint64_t free_mask, int32_t n, int32_t method, float* d);
 
 #ifdef __cplusplus
 }

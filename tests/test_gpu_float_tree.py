@@ -569,7 +569,7 @@ def test_humanoid_512_impacts_vs_converged_lcp(require_gpu, oracle, solver):
     sim.set_control_mode(N.MODE_FORCE)
     gains = np.array(_humanoid_gains(sim.joint_names))
     mode = np.full(n, oracle.FORCE, np.int32)
-    subset = list(range(0, W, W // 16))
+    subset = list(range(0, W, W // 64))  # 64 of the 512 worlds re-stepped in the oracle every step
     keys = ("pose", "q", "vel", "qd")
     e50 = dict.fromkeys(keys, 0.0)
     econv = dict.fromkeys(keys, 0.0)
@@ -646,8 +646,9 @@ def test_humanoid_512_impacts_vs_converged_lcp(require_gpu, oracle, solver):
     assert in_contact[subset].all()
     if solver == "exact":
         # DART-equivalent solve: the GPU is within fp32 round-off of DART's LCP
-        assert econv["pose"] <= 1e-5 and econv["q"] <= 1e-5 and econv["vel"] <= 1e-3 and econv["qd"] <= 1e-3
-        assert unconv <= W * H // 200
+        # (north star: 1e-4) and every world-step converged
+        assert econv["pose"] <= 1e-5 and econv["q"] <= 1e-5 and econv["vel"] <= 1e-4 and econv["qd"] <= 1e-4
+        assert unconv == 0
         sim.close()
         return
     assert unconv == 0

@@ -87,17 +87,30 @@ def test_nan_world_is_flagged(require_gpu, model):
     good = [w for w in range(W) if w != bad]
     for a, b in zip(_snap(sims[0]), _snap(sims[1])):
         assert np.array_equal(a[good], b[good])   # the other worlds never notice
-    # the caller resets the world and re-arms its flag: it runs clean again
+    # the caller resets the world: the reset re-arms its flag,
+    # it runs clean again ...
     q, qd = sims[1].get("q"), sims[1].get("qd")
     sims[0].set("reset_q", q)
     sims[0].set("reset_qd", qd)
     if model == "humanoid":
         sims[0].reset_base_pose(sims[1].base_pose())
         sims[0].reset_base_velocity(sims[1].base_velocity())
-    sims[0].clear_diverged(bad, 1)
     sims[0].run()
     assert sims[0].diverged()[1] == 1 and not sims[0].diverged()[0].any()
     assert np.isfinite(sims[0].get("qd")).all()
+    # ... and a second divergence of the same world is reported again
+    qd = sims[0].get("qd")
+    qd[bad, 0] = np.inf
+    sims[0].set("reset_qd", qd)
+    with pytest.raises(N.DivergedError):
+        sims[0].run()
+    flags, count = sims[0].diverged()
+    assert count == 2 and flags.tolist() == [w == bad for w in range(W)]
+    # an explicit re-arm without a reset: the world is flagged again at once
+    sims[0].clear_diverged(bad, 1)
+    with pytest.raises(N.DivergedError):
+        sims[0].run()
+    assert sims[0].diverged()[1] == 3
     for s in sims:
         s.close()
 
@@ -124,6 +137,24 @@ def test_scenario_run_reports_divergence(require_gpu):
     assert np.isfinite(models[1].joint_positions()[0])
     flags, count = gz._scene.diverged()
     assert count == 1 and flags.tolist() == [True, False]
+    # a reset re-arms the world: it steps clean, and a second
+    # divergence after the reset is reported again
+    assert models[0].reset_joint_positions([0.3]) and models[0].reset_joint_velocities([0.0])
+    assert gz.run()
+    assert np.isfinite(models[0].joint_positions()[0])
+    assert gz._scene.diverged()[0].tolist() == [False, False]
+    assert models[0].reset_joint_velocities([float("inf")])
+    assert not gz.run()
+    assert gz.run()
+    flags, count = gz._scene.diverged()
+    assert count == 2 and flags.tolist() == [True, False]
+    # removing the model and inserting it again re-arms the world too
+    w0 = gz.get_world("a")
+    assert w0.remove_model("pendulum")
+    assert gz.run()
+    assert gz._scene.diverged()[0].tolist() == [False, False]
+    assert w0.insert_model(get_model_file("pendulum"))
+    assert gz.run()
     gz.close()
 
 
