@@ -617,6 +617,12 @@ __device__ __forceinline__ float dof_force(const ChainF* __restrict__ P, const S
     return tau;
 }
 
+// the wave kernel's step: 1 = joint space on the matrix cores (wave_crba.hpp),
+// 0 = the articulated-body recursions (wave_tree.hpp wave_step)
+#ifndef MW_WAVE_CRBA
+#define MW_WAVE_CRBA 1
+#endif
+
 template <int MAXN, bool CONS>
 __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
                                                       int N, SimDev S, FreeDev D, const PidF* __restrict__ pid,
@@ -670,8 +676,14 @@ __global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__
                 L.tau[lane] = dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
             MW_PROF_T(tb);
             MW_PROF_ACC(0, ta, tb);
+#if MW_WAVE_CRBA
+            // joint space on the matrix cores (wave_crba.hpp)
+            active = wave_step_crba<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0,
+                                                A.lcp_solves, L.qdd, &ovf, &unconv, prof, A.wrenches != 0);
+#else
             active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0,
                                            A.lcp_solves, L.qdd, &ovf, &unconv, prof, A.wrenches != 0);
+#endif
             MW_PROF_T(tc);
             MW_PROF_ACC(7, ta, tc);
         }

@@ -1158,10 +1158,10 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 long long cyc[3] = {0, 0, 0};
                 x1s = xw1;
                 // long-row elimination (wave_lcp.hpp lcp_ge_solve)
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true, kScStageSweeps>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true, kScStageSweeps, kLcpMfmaAll>(a, Rw, mu, NR, lcp_solves, pgs_iters,
                                                                       kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
                                                                       nround, nsolve1, cyc)
-                                           : wave_lcp_exact<kWaveMaxRows, true, kScStageSweeps>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                                           : wave_lcp_exact<kWaveMaxRows, true, kScStageSweeps, kLcpMfmaAll>(a, Rw, mu, NR, lcp_solves, pgs_iters,
                                                                                 kScExactPgsTol, L.rc, Uw, x1s, x0,
                                                                                 nsolve, nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
@@ -1425,7 +1425,10 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         const size_t k = static_cast<size_t>(lane) * W + w;
         D.q[k] = L.q[lane];
         D.qd[k] = L.qd[lane];
-        bad = nonfinite_bits(L.q[lane]) || nonfinite_bits(L.qd[lane]);  // finite.hpp
+        // only the world's present models count (a removed model's state is
+        // stale: it is re-initialised when the model is placed again)
+        bad = ((present >> P->body_model[lane]) & 1u) &&
+              (nonfinite_bits(L.q[lane]) || nonfinite_bits(L.qd[lane]));  // finite.hpp
         if (!A.paused) D.qdd[k] = L.qdd[lane];
         D.cmd[k] = 0.f;
         if (D.rb) {
@@ -1442,8 +1445,10 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         at(10) = base.V.v.x; at(11) = base.V.v.y; at(12) = base.V.v.z;
         const float v[13] = {base.p.x, base.p.y, base.p.z, base.qw, base.qx, base.qy, base.qz,
                              base.V.w.x, base.V.w.y, base.V.w.z, base.V.v.x, base.V.v.y, base.V.v.z};
+        bool bb = false;
 #pragma unroll
-        for (int f = 0; f < 13; ++f) bad = bad || nonfinite_bits(v[f]);
+        for (int f = 0; f < 13; ++f) bb = bb || nonfinite_bits(v[f]);
+        bad = bad || (bb && ((present >> bm) & 1u));
     }
     if (__ballot(bad) != 0 && lane == 0 && !D.diverged[w]) {
         D.diverged[w] = 1;  // sticky until mw_scene_clear_diverged

@@ -63,6 +63,15 @@ constexpr float kLcpFloorAccept = 64.f;
 #ifndef MW_LCP_MFMA
 #define MW_LCP_MFMA 1
 #endif
+// Which register widths solve on the matrix cores (bit 0: <= 16 rows, bit 1:
+// <= 32, bit 2: <= 64; the rest eliminate over the lanes).  The choice is per
+// kernel: the solve's tiles (16 / 48 accumulators) add to the kernel's peak
+// register pressure, and the wave kernels sit at 512 registers with spills
+// (A/B on the legs, gpurun_out r05d: humanoid_c5 131.8 -> 109.2 us with the
+// 32-row tile, the scene 1.74 -> 1.10 ms with the 64-row tiles; the 64-row
+// tiles in the wave kernels and any tile in the <= 16-body instance made
+// their legs slower through the spills)
+constexpr int kLcpMfmaNone = 0, kLcpMfma32 = 2, kLcpMfmaAll = 7, kLcpMfma3264 = 6;
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
 // ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
@@ -418,18 +427,25 @@ __device__ __forceinline__ float lane_xor32(float v) {
     return (lane_id() >= 32) ? lo : hi;
 }
 
-// The pivot block's inverse (d00, d01, d11; uniform) of rows / columns J, J + 1
-// of tile T, and this lane's panel entry P[lane % 32][J + lane / 32].
+// The pivot block of rows / columns J, J + 1 of tile T, eliminated by two 1x1
+// pivots (d0 = s00, l = s01 / s00, d1 = s11 - l s01: the elimination's own
+// arithmetic -- an explicit 2x2 inverse through ac - b^2 cancels on the
+// redundant contact rows, cond(A) ~1e7, and is not backward stable); uniform.
 template <int J>
-__device__ __forceinline__ void mfma_pivot(const v16f& T, float& d00, float& d01, float& d11) {
+__device__ __forceinline__ void mfma_pivot(const v16f& T, float& i0, float& l, float& i1) {
     constexpr int i = 4 * (J / 8) + (J % 4), hl = 32 * ((J / 4) % 2);
     const float s00 = read_lane(T[i], J + hl), s01 = read_lane(T[i], J + 1 + hl);
     const float s11 = read_lane(T[i + 1], J + 1 + hl);
-    const float idet = rcp(fmaf(s00, s11, -s01 * s01));
-    d00 = s11 * idet;
-    d01 = -s01 * idet;
-    d11 = s00 * idet;
+    // a zero pivot (two identical joint rows: DART's joint CFM, 1e-9, is below
+    // fp32's resolution) takes the elimination's guard (lcp_ge_solve): its
+    // column is exactly zero, the row's unknown grows large and the active-set
+    // step's blocking bound resolves the degenerate pair
+    i0 = rcp((fabsf(s00) < 1e-30f) ? 1e-30f : s00);
+    l = s01 * i0;
+    const float d1 = fmaf(-l, s01, s11);
+    i1 = rcp((fabsf(d1) < 1e-30f) ? 1e-30f : d1);
 }
+// this lane's panel entry P[lane % 32][J + lane / 32] of tile T
 template <int J>
 __device__ __forceinline__ float mfma_panel(const v16f& T) {
     constexpr int i = 4 * (J / 8) + (J % 4);
@@ -438,15 +454,24 @@ __device__ __forceinline__ float mfma_panel(const v16f& T) {
     return ((J / 4) % 2) ? y : x;
 }
 
-template <int RC>
+// LS: the column stride of the L record in Lw (column-major, L[row][col] at
+// Lw[col * LS + row]; only rows < LROWS are stored).  dsq (optional): per
+// pivot, 1 / sqrt(d) (the joint-space factorisation's Y scaling).
+template <int RC, int LS = kLcpLStride, int LROWS = 64>
 struct MfmaLdl {
     v16f T00, T01, T11;
     float r, y;
     uint64_t freeM;
     float* Lw;
+    float* dsq = nullptr;
 
-    // block step of rows / columns J, J + 1: factorisation (one MFMA per tile)
-    // and forward substitution
+    __device__ __forceinline__ void put_l(int row, int col, float v) const {
+        if (row < LROWS) Lw[col * LS + row] = v;
+    }
+
+    // block step of rows / columns J, J + 1: the two eliminated columns
+    // Q = [p0, p1 - l p0] (the second one reduced by the first), one MFMA
+    // per tile for S -= Q diag(1/d0, 1/d1) Q^T, and the forward substitution
     template <int J>
     __device__ __forceinline__ void step() {
         if (((freeM >> J) & 3ull) == 0ull) return;  // two held rows: identity, nothing to do
@@ -454,72 +479,79 @@ struct MfmaLdl {
         const int c = lane & 31;
         const bool hi = lane >= 32;
         constexpr int JT = J % 32;
-        float d00, d01, d11, mine, mineb = 0.f, othb = 0.f;
+        float i0, l, i1, mine, mineb = 0.f, othb = 0.f;
         if constexpr (J < 32) {
-            mfma_pivot<JT>(T00, d00, d01, d11);
+            mfma_pivot<JT>(T00, i0, l, i1);
             mine = mfma_panel<JT>(T00);
             if constexpr (RC == 64) {
                 mineb = mfma_panel<JT>(T01);
                 othb = lane_xor32(mineb);
             }
         } else {
-            mfma_pivot<JT>(T11, d00, d01, d11);
+            mfma_pivot<JT>(T11, i0, l, i1);
             mine = mfma_panel<JT>(T11);
         }
         const float oth = lane_xor32(mine);
-        // L[c][J + h] of this lane's panel (P D^-1; D^-1 symmetric)
-        const float dh = hi ? d11 : d00;
-        const float Lm = fmaf(mine, dh, oth * d01);
-        const int lcol = (J + (hi ? 1 : 0)) * kLcpLStride;
+        // Q[c][h] of this lane (top panel: rows c; J >= 32: rows 32 + c)
+        const float p0 = hi ? oth : mine, p1 = hi ? mine : oth;
+        const float q = hi ? fmaf(-l, p0, p1) : p0;
+        const float ih = hi ? i1 : i0;
+        const float Lm = q * ih;  // L[c][J + h]
+        const int col = J + (hi ? 1 : 0);
+        float r0 = p0, r1 = fmaf(-l, p0, p1);  // this lane's ROW of Q (lane = row)
         if constexpr (J < 32) {
-            T00 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mine, Lm, T00, 0, 0, 0);
-            Lw[lcol + c] = Lm;
+            T00 = __builtin_amdgcn_mfma_f32_32x32x2f32(-q, Lm, T00, 0, 0, 0);
+            put_l(c, col, Lm);
             if constexpr (RC == 64) {
-                const float Lb = fmaf(mineb, dh, othb * d01);
-                T01 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mine, Lb, T01, 0, 0, 0);
-                T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mineb, Lb, T11, 0, 0, 0);
-                Lw[lcol + 32 + c] = Lb;
+                const float b0 = hi ? othb : mineb, b1 = hi ? mineb : othb;
+                const float qb = hi ? fmaf(-l, b0, b1) : b0;
+                const float Lb = qb * ih;
+                T01 = __builtin_amdgcn_mfma_f32_32x32x2f32(-q, Lb, T01, 0, 0, 0);
+                T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-qb, Lb, T11, 0, 0, 0);
+                put_l(32 + c, col, Lb);
+                if (hi) {  // rows 32 + c come from the bottom panel
+                    r0 = b0;
+                    r1 = fmaf(-l, b0, b1);
+                }
             }
         } else {
-            T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-mine, Lm, T11, 0, 0, 0);
-            Lw[lcol + 32 + c] = Lm;
+            T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-q, Lm, T11, 0, 0, 0);
+            put_l(32 + c, col, Lm);
         }
-        // forward substitution, lane = row: rows below the pair take
-        // P[row][J..J+1] D^-1 (rows < 32 from the top panel, rows >= 32 from
-        // the bottom one -- the T11 panel for J >= 32)
-        const float zj = read_lane(r, J), zj1 = read_lane(r, J + 1);
-        float p0, p1;
-        if constexpr (J < 32 && RC == 64) {
-            p0 = hi ? othb : mine;
-            p1 = hi ? mineb : oth;
-        } else {
-            p0 = hi ? oth : mine;
-            p1 = hi ? mine : oth;
+        if (dsq && lane == 0) {
+            dsq[J] = sqrtf(i0);
+            dsq[J + 1] = sqrtf(i1);
         }
-        const float l0 = fmaf(p0, d00, p1 * d01), l1 = fmaf(p0, d01, p1 * d11);
-        if (lane > J + 1) r = fmaf(-l0, zj, fmaf(-l1, zj1, r));
-        if (lane == J) y = fmaf(d00, zj, d01 * zj1);
-        if (lane == J + 1) y = fmaf(d01, zj, d11 * zj1);
+        // forward substitution, lane = row, one column after the other
+        const float z0 = read_lane(r, J);
+        if (lane > J) r = fmaf(-(r0 * i0), z0, r);  // row J + 1 takes l z0
+        const float z1 = read_lane(r, J + 1);
+        if (lane > J + 1) r = fmaf(-(r1 * i1), z1, r);
+        if (lane == J) y = z0 * i0;
+        if (lane == J + 1) y = z1 * i1;
     }
     template <int J>
     __device__ __forceinline__ void forward() {
         step<J>();
         if constexpr (J + 2 < RC) forward<J + 2>();
     }
-    // back substitution L^T d = y of pair J, then the pairs before it
-    template <int J>
-    __device__ __forceinline__ void backward() {
-        if (((freeM >> J) & 3ull) != 0ull) {
-            const int lane = lane_id();
-            const float dj = read_lane(y, J), dj1 = read_lane(y, J + 1);
-            if (lane < J) {
-                const float* col = Lw + lane * kLcpLStride;
-                y = fmaf(-col[J], dj, fmaf(-col[J + 1], dj1, y));
-            }
-        }
-        if constexpr (J >= 2) backward<J - 2>();
-    }
 };
+
+// back substitution L^T d = y (lane = row, y in and d out) over the pairs of
+// freeM, from the last: row J + 1, then row J; lane c reads column c of L
+// (L[J][c] at Lw[c * LS + J])
+template <int J, int LS = kLcpLStride>
+__device__ __forceinline__ void ldl_backward(float& y, uint64_t freeM, const float* __restrict__ Lw) {
+    if (((freeM >> J) & 3ull) != 0ull) {
+        const int lane = lane_id();
+        const float* col = Lw + lane * LS;
+        const float dj1 = read_lane(y, J + 1);
+        if (lane <= J) y = fmaf(-col[J + 1], dj1, y);  // lane J: the pair's own l
+        const float dj = read_lane(y, J);
+        if (lane < J) y = fmaf(-col[J], dj, y);
+    }
+    if constexpr (J >= 2) ldl_backward<J - 2, LS>(y, freeM, Lw);
+}
 
 template <int RC>
 __device__ __forceinline__ float lcp_mfma_solve(const float (&a)[kWaveMaxRows], float rhs, uint64_t freeM,
@@ -556,7 +588,7 @@ __device__ __forceinline__ float lcp_mfma_solve(const float (&a)[kWaveMaxRows], 
     M.y = 0.f;
     M.template forward<0>();
     wave_lds_sync();
-    M.template backward<RC - 2>();
+    ldl_backward<RC - 2>(M.y, freeM, Lw);
     return mask_bit(freeM, lane) ? M.y : 0.f;
 }
 
@@ -578,7 +610,7 @@ __device__ __forceinline__ float lcp_mfma_solve(const float (&a)[kWaveMaxRows], 
 // fp32 floor; converged if within kLcpFloorAccept of the tolerance).  solves
 // counts the linear solves against `budget`.
 // Returns true when every row's residual is within tolerance.
-template <int RC, bool LongRows = false>
+template <int RC, bool LongRows = false, int MFMA = kLcpMfma32>
 __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
                                            float arr, int n, int budget, float* __restrict__ Uw, float& xl, int ws0,
                                            int& solves, int& iters, long long& ge_cycles) {
@@ -648,8 +680,18 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         const long long tg0 = clock64();
 #endif
 #if MW_LCP_MFMA
-        // block LDL^T on the matrix cores (R <= 32: one tile, else three)
-        const float d = lcp_mfma_solve<(RC <= 32) ? 32 : 64>(a, fr ? -g : 0.f, freeM, Uw);
+        // block LDL^T on the matrix cores (R <= 32: one tile, else three) for
+        // the widths the kernel's MFMA policy selects
+        float d;
+        constexpr int bit = (RC <= 16) ? 1 : ((RC <= 32) ? 2 : 4);
+        if constexpr ((MFMA & bit) == 0) {
+            float k[RC];
+#pragma unroll
+            for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
+            d = lcp_ge_solve<RC, LongRows>(k, fr ? -g : 0.f, n, Uw, false, freeM);
+        } else {
+            d = lcp_mfma_solve<(RC <= 32) ? 32 : 64>(a, fr ? -g : 0.f, freeM, Uw);
+        }
 #else
         float k[RC];
 #pragma unroll
@@ -769,7 +811,7 @@ constexpr int kLcpStageSweeps = MW_LCP_STAGE_SWEEPS;
 // STAGE_SWEEPS: the cap on the sweeps per stage (the scene kernel's
 // three-cube stacks converge more often with 6: 3253 -> 2575 unconverged
 // world-steps, 1.757 -> 1.708 ms, profiles/r04z ab_sweeps)
-template <int RC, bool LongRows = false, int STAGE_SWEEPS = kLcpStageSweeps>
+template <int RC, bool LongRows = false, int STAGE_SWEEPS = kLcpStageSweeps, int MFMA = kLcpMfma32>
 __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], const LcpRow& R, float mu, int n,
                                                int max_solves, int sweeps, float pgs_tol, F4* __restrict__ rc,
                                                float* __restrict__ Uw, float& x1, float& xl, int& n_solves,
@@ -804,7 +846,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #ifdef MW_WAVE_PROF
     cyc[1] += clock64() - tp;
 #endif
-    const bool ok1 = wave_boxqp<RC, LongRows>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
+    const bool ok1 = wave_boxqp<RC, LongRows, MFMA>(a, R.live, R.b, L1, U1, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     x1 = R.live ? x : 0.f;
 #ifdef MW_WAVE_PROF
     cyc[2] += clock64() - tc0;
@@ -833,7 +875,7 @@ __device__ __forceinline__ bool wave_lcp_exact(const float (&a)[kWaveMaxRows], c
 #ifdef MW_WAVE_PROF
     cyc[1] += clock64() - tp;
 #endif
-    const bool ok2 = wave_boxqp<RC, LongRows>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
+    const bool ok2 = wave_boxqp<RC, LongRows, MFMA>(a, R.live, R.b, L, U, arr, n, max_solves, Uw, x, ws, solves, iters, ge_cycles);
     xl = R.live ? x : 0.f;
     n_solves = solves;
     n_rounds = iters;

@@ -101,9 +101,27 @@ struct WaveWorld {
     // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
     alignas(16) float stack[kWaveMaxDepth][7][kWaveLanes];
     float xw[kWaveWarmRecord];   // warm-start impulses (RunArgs::warm): final, then stage 1
+    // joint-space step (wave_crba.hpp): generalized forces and 1/sqrt(d) of
+    // the factorisation, reversed dof order
+    float gen[kNv + 2];
+    float dsq[64];
 };
 
+// The lane index through a volatile asm: every call is a fresh value, so the
+// lane-dependent constants the phases derive from it (masks, identity
+// patterns, LDS addresses) are formed where they are used instead of being
+// hoisted out of the substep loop by LICM, where hundreds of them stayed live
+// across the whole step and spilled to scratch (the joint-space step:
+// 1408 -> see DESIGN.md bytes per lane).
+#if defined(MW_HOST_TEST) || defined(MW_LANE_PLAIN)
 __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63u); }
+#else
+__device__ __forceinline__ int lane_id() {
+    int l;
+    asm volatile("v_and_b32 %0, 63, %1" : "=v"(l) : "v"(threadIdx.x));
+    return l;
+}
+#endif
 
 // Phase timing (debug builds only: EXTRA=-DMW_WAVE_PROF, scripts/wave_prof.py):
 // shader-clock cycles per phase, summed over the worlds of a launch.
@@ -737,18 +755,21 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #else
             constexpr int kLcpSmall = 32;
 #endif
+            // the matrix-core solves this instance takes (wave_lcp.hpp: the
+            // <= 16-body instance and the 64-row width eliminate over the lanes)
+            constexpr int kWaveLcpMfma = (!MW_LCP_MFMA || MAXN <= 16) ? kLcpMfmaNone : kLcpMfma32;
             // three register widths (wave_lcp.hpp: the elimination runs the
             // whole register row): a free body's 4-corner LCP (12 rows) on 16
             // columns took contacts_floating 195 -> 167 us (gpurun_out r04z)
             bool ok;
             if (R <= 16 && kLcpSmall > 0)
-                ok = wave_lcp_exact<16>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
+                ok = wave_lcp_exact<16, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
                                         nsolve1, cyc);
             else if (R <= kLcpSmall)
-                ok = wave_lcp_exact<32>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
+                ok = wave_lcp_exact<32, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
                                         nsolve1, cyc);
             else
-                ok = wave_lcp_exact<kWaveMaxRows>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
+                ok = wave_lcp_exact<kWaveMaxRows, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
                                                   nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
             if (nsolve >= 8) {
@@ -870,3 +891,5 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 
 }  // namespace dev
 }  // namespace mw
+
+#include "wave_crba.hpp"
