@@ -617,10 +617,11 @@ __device__ __forceinline__ float dof_force(const ChainF* __restrict__ P, const S
     return tau;
 }
 
-// the wave kernel's step: 1 = joint space on the matrix cores (wave_crba.hpp),
-// 0 = the articulated-body recursions (wave_tree.hpp wave_step)
+// the wave kernel's step: 0 = the articulated-body recursions (wave_tree.hpp
+// wave_step, default), 1 = joint space on the matrix cores (wave_crba.hpp: an
+// A/B variant -- measured slower and less accurate)
 #ifndef MW_WAVE_CRBA
-#define MW_WAVE_CRBA 1
+#define MW_WAVE_CRBA 0
 #endif
 
 template <int MAXN, bool CONS>

@@ -37,6 +37,56 @@ namespace dev {
 // M row stride in the stack region (row-major; lane c reads row rr at column c)
 constexpr int kCrbaMStride = 64;
 
+// A composite rigid-body inertia in 10 numbers (a subtree is a rigid body
+// while its joints are held): mass, first moment h = m c and the rotational
+// inertia about the body ORIGIN.  Moving it to the parent frame is ~75 FMAs
+// against ~200 for the 6x6 congruence of an articulated inertia (to_parent).
+struct Rigid10 {
+    float m;
+    f3 h;
+    Sy I;
+};
+// the accumulator of a body's children (the wave kernel's WaveAcc slot, reused)
+struct CrbaAcc {
+    Rigid10 I;
+    SV B;
+};
+
+__device__ __forceinline__ Rigid10 rigid10(const BodyF& b) {
+    return {b.mass, mk(b.mass * b.com[0], b.mass * b.com[1], b.mass * b.com[2]), inertia_origin(b, b.mass)};
+}
+__device__ __forceinline__ Rigid10 operator+(const Rigid10& a, const Rigid10& b) {
+    return {a.m + b.m, a.h + b.h,
+            {a.I.xx + b.I.xx, a.I.yy + b.I.yy, a.I.zz + b.I.zz, a.I.xy + b.I.xy, a.I.xz + b.I.xz, a.I.yz + b.I.yz}};
+}
+// child (R, p: the child's orientation and origin in the parent frame) ->
+// parent: h' = R h + m p, I' = R I R^T - [p]x[Rh]x - [Rh]x[p]x - m [p]x^2
+// ([a]x[b]x = b a^T - (a.b) 1)
+__device__ __forceinline__ Rigid10 to_parent10(const M3& R, const f3& p, const Rigid10& X) {
+    const f3 hr = mul(R, X.h);
+    const Sy Ir = rot_sym(R, X.I);
+    const float ph = dot(p, hr), pp = dot(p, p);
+    const float dg = 2.f * ph + X.m * pp;
+    Sy I;
+    I.xx = Ir.xx - 2.f * hr.x * p.x - X.m * p.x * p.x + dg;
+    I.yy = Ir.yy - 2.f * hr.y * p.y - X.m * p.y * p.y + dg;
+    I.zz = Ir.zz - 2.f * hr.z * p.z - X.m * p.z * p.z + dg;
+    I.xy = Ir.xy - hr.x * p.y - p.x * hr.y - X.m * p.x * p.y;
+    I.xz = Ir.xz - hr.x * p.z - p.x * hr.z - X.m * p.x * p.z;
+    I.yz = Ir.yz - hr.y * p.z - p.y * hr.z - X.m * p.y * p.z;
+    return {X.m, hr + X.m * p, I};
+}
+// the 6 x 6 form [[I, [h]x], [[h]x^T, m 1]] (rigid() of chain_dyn.hpp)
+__device__ __forceinline__ SI si_of(const Rigid10& X) {
+    SI S;
+    S.A = X.I;
+    S.B.m[0] = 0.f;      S.B.m[1] = -X.h.z; S.B.m[2] = X.h.y;
+    S.B.m[3] = X.h.z;    S.B.m[4] = 0.f;    S.B.m[5] = -X.h.x;
+    S.B.m[6] = -X.h.y;   S.B.m[7] = X.h.x;  S.B.m[8] = 0.f;
+    S.C = {X.m, X.m, X.m, 0.f, 0.f, 0.f};
+    return S;
+}
+
 // the tile width of the joint-space factorisation
 template <int MAXN>
 struct CrbaDims {
@@ -113,7 +163,8 @@ __device__ __forceinline__ void wave_crba_tree(const ChainF* __restrict__ P, con
     const int NV = 6 + N;
     const f3 gw = mk(F->g[0], F->g[1], F->g[2]);
     const int slot = (pa >= 0) ? pa : MAXN;
-    if (lane <= MAXN) L.acc[lane] = WaveAcc{};
+    static_assert(sizeof(CrbaAcc) <= sizeof(WaveAcc), "composite accumulator in the wave slot");
+    if (lane <= MAXN) reinterpret_cast<CrbaAcc*>(&L.acc[0])[lane] = CrbaAcc{};
     // ---- forward: kinematics, velocities, RNEA accelerations (qdd = 0)
     M3 R, Rw;
     f3 p, pw;
@@ -142,6 +193,10 @@ __device__ __forceinline__ void wave_crba_tree(const ChainF* __restrict__ P, con
             L.body[i].U = A;  // the RNEA acceleration rides in the U slot (no ABA here)
             L.body[i].Rw = Rw;
             L.body[i].pw = pw;
+            // the joint transform: the CRBA climbs below and the J rows read it
+            L.body[i].R = R;
+            L.body[i].p = p;
+            L.body[i].depth = depth;
         }
     }
     // own bias force f_i = I_i a_i + B_i (- the world wrench, body frame)
@@ -154,33 +209,29 @@ __device__ __forceinline__ void wave_crba_tree(const ChainF* __restrict__ P, con
         }
     }
     // ---- backward: composite inertias and bias forces, deepest level first
+    CrbaAcc* acc = reinterpret_cast<CrbaAcc*>(&L.acc[0]);  // 16 of the slot's 48 words
     for (int d = levels - 1; d >= 0; --d) {
         const bool mine = (depth == d);
-        SI c;
-        SV cb;
-        SI Ic;
-        SV fc;
+        Rigid10 c, Ic;
+        SV cb, fc;
         if (mine) {
-            Ic = rigid(b, b.mass);
-            Ic += L.acc[i].I;
-            fc = fb + L.acc[i].B;
-            c = to_parent(R, p, Ic);
+            Ic = rigid10(b) + acc[i].I;
+            fc = fb + acc[i].B;
+            c = to_parent10(R, p, Ic);
             cb = dad_inv(R, p, fc);
         }
         for (int k = 0; k < fanout; ++k) {
             if (mine && srank == k) {
-                WaveAcc& acc = L.acc[slot];
-                SI I = acc.I;
-                I += c;
-                acc.I = I;
-                acc.B = acc.B + cb;
+                CrbaAcc& a = acc[slot];
+                a.I = a.I + c;
+                a.B = a.B + cb;
             }
         }
         if (mine) {
             // the body's own composite replaces its children's sum (nobody
             // reads the sum again)
-            L.acc[i].I = Ic;
-            L.acc[i].B = fc;
+            acc[i].I = Ic;
+            acc[i].B = fc;
         }
     }
     wave_lds_sync();
@@ -189,11 +240,11 @@ __device__ __forceinline__ void wave_crba_tree(const ChainF* __restrict__ P, con
     for (int e = lane; e < nz; e += kWaveLanes) Mm[e] = 0.f;
     wave_lds_sync();
     if (own) {
-        const SI Ic = L.acc[i].I;
+        const SI Ic = si_of(acc[i].I);
         SV Fv = ais(Ic, b);
         const int kk = N - 1 - i;
         Mm[kk * kCrbaMStride + kk] = proj(b, Fv);
-        gen[kk] = L.tau[i] - b.damping * L.qd[i] - proj(b, L.acc[i].B);
+        gen[kk] = L.tau[i] - b.damping * L.qd[i] - proj(b, acc[i].B);
         Fv = dad_inv(R, p, Fv);
         const uint64_t path = F->body_path[i] & ~(uint64_t{1} << i);
         for (uint64_t m = path; m != 0;) {
@@ -215,11 +266,12 @@ __device__ __forceinline__ void wave_crba_tree(const ChainF* __restrict__ P, con
     }
     // the base: its composite inertia (6 x 6) and bias
     {
-        SI Ic0 = rigid_base(*F);
-        Ic0 += L.acc[MAXN].I;
+        const Rigid10 base10 = {F->mass, mk(F->mass * F->com[0], F->mass * F->com[1], F->mass * F->com[2]),
+                                Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}};
+        const SI Ic0 = si_of(base10 + acc[MAXN].I);
         SV fc0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
                             Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
-                 L.acc[MAXN].B;
+                 acc[MAXN].B;
         if (ext) {
             const float* e = L.ext[0];
             fc0 = fc0 + (-1.f) * SV{mulT(R0, mk(e[3], e[4], e[5])), mulT(R0, mk(e[0], e[1], e[2]))};
@@ -252,12 +304,6 @@ __device__ __forceinline__ void wave_crba_tree(const ChainF* __restrict__ P, con
                 Mm[ke * kCrbaMStride + (NV - 1 - f)] = v;
             }
         }
-    }
-    if (own) {
-        WaveBody& s = L.body[i];
-        s.R = R;
-        s.p = p;
-        s.depth = depth;
     }
     wave_lds_sync();
 }
@@ -293,6 +339,8 @@ __device__ __forceinline__ uint32_t wave_step_crba(const ChainF* __restrict__ P,
     float* Lw = &L.MJ[0][0];
     static_assert(sizeof(L.stack) >= 64 * kCrbaMStride * sizeof(float), "M in the stack region");
     wave_crba_tree<MAXN>(P, F, N, R0, base.p, base.V, L, Mm, L.gen, ext);
+    MW_PROF_T(t0b);
+    MW_PROF_ACC(18, t0, t0b);
     const uint64_t allM = (1ull << NV) - 1ull;  // NV <= 54
     const uint64_t freeM = F->fixed ? ((1ull << N) - 1ull) : allM;
     const bool dual = F->dual != 0;
@@ -326,6 +374,7 @@ __device__ __forceinline__ uint32_t wave_step_crba(const ChainF* __restrict__ P,
     wave_lds_sync();
     MW_PROF_T(t1);
     MW_PROF_ACC(1, t0, t1);
+    MW_PROF_ACC(19, t0b, t1);
     // integrateVelocities (lane e: nu component e)
     if (lane < NV) {
         float v;

@@ -466,7 +466,7 @@ struct MfmaLdl {
     float* dsq = nullptr;
 
     __device__ __forceinline__ void put_l(int row, int col, float v) const {
-        if (row < LROWS) Lw[col * LS + row] = v;
+        if (LROWS >= 64 || row < LROWS) Lw[col * LS + row] = v;
     }
 
     // block step of rows / columns J, J + 1: the two eliminated columns
@@ -523,12 +523,16 @@ struct MfmaLdl {
             dsq[J + 1] = sqrtf(i1);
         }
         // forward substitution, lane = row, one column after the other
+        // (selects, not branches: a divergent branch here made the compiler
+        // copy whole accumulator tiles out of the AGPRs at every step)
         const float z0 = read_lane(r, J);
-        if (lane > J) r = fmaf(-(r0 * i0), z0, r);  // row J + 1 takes l z0
+        const float ra = fmaf(-(r0 * i0), z0, r);
+        r = (lane > J) ? ra : r;  // row J + 1 takes l z0
         const float z1 = read_lane(r, J + 1);
-        if (lane > J + 1) r = fmaf(-(r1 * i1), z1, r);
-        if (lane == J) y = z0 * i0;
-        if (lane == J + 1) y = z1 * i1;
+        const float rb = fmaf(-(r1 * i1), z1, r);
+        r = (lane > J + 1) ? rb : r;
+        y = (lane == J) ? z0 * i0 : y;
+        y = (lane == J + 1) ? z1 * i1 : y;
     }
     template <int J>
     __device__ __forceinline__ void forward() {
@@ -546,9 +550,11 @@ __device__ __forceinline__ void ldl_backward(float& y, uint64_t freeM, const flo
         const int lane = lane_id();
         const float* col = Lw + lane * LS;
         const float dj1 = read_lane(y, J + 1);
-        if (lane <= J) y = fmaf(-col[J + 1], dj1, y);  // lane J: the pair's own l
+        const float ya = fmaf(-col[J + 1], dj1, y);
+        y = (lane <= J) ? ya : y;  // lane J: the pair's own l
         const float dj = read_lane(y, J);
-        if (lane < J) y = fmaf(-col[J], dj, y);
+        const float yb = fmaf(-col[J], dj, y);
+        y = (lane < J) ? yb : y;
     }
     if constexpr (J >= 2) ldl_backward<J - 2, LS>(y, freeM, Lw);
 }

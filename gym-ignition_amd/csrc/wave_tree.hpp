@@ -655,7 +655,12 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         const int lr = lane & 31, lh = lane >> 5;
         const bool two = R > 32;
         v16f t00 = {}, t01 = {}, t10 = {}, t11 = {};
-        for (int k = 0; 2 * k < NV; ++k) {
+        // unrolled to the instance's coordinate count (the operand loads go
+        // out ahead of the MFMA chain; a loop to the runtime NV waited on each
+        // k-step's loads: 14.6k -> see DESIGN.md cycles per world-step);
+        // columns >= NV: J is zero there, MJ masked
+#pragma unroll
+        for (int k = 0; k < (WaveWorld<MAXN>::kNv + 1) / 2; ++k) {
             const int e = 2 * k + lh;
             const bool ev = e < NV;
             const float j0 = L.J[lr][e];

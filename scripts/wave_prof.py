@@ -131,6 +131,9 @@ print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f}
       f"{buf[14] / W / T:.0f} cycles/world-step in the linear solves, {buf[15] / W / T:.0f} in the PGS sweeps "
       f"(PGS-only mode) / the whole exact solve incl. its per-stage sweeps (exact mode); "
       f"{buf[16] / W / T:.0f} in the per-stage sweeps, {buf[17] / W / T:.0f} in stage 1")
+if buf[18] or buf[19]:
+    print(f"  joint-space step: tree passes + CRBA {buf[18] / W / T:.0f}, factorisation + free solve "
+          f"{buf[19] / W / T:.0f} cycles/world-step (both inside the first phase above)")
 dump = np.zeros(8 + 64 * 64 + 9 * 64, dtype=np.float32)
 fd = L.mw_debug_wave_dump
 fd.argtypes = [ctypes.c_void_p, ctypes.c_int]
