@@ -106,6 +106,26 @@ __device__ __forceinline__ float wave_fmin(float v) {
     return read_lane(v, 63);
 }
 
+// bitwise OR over the wave (the same DPP steps)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+#ifdef MW_HOST_TEST
+    return v;
+#else
+    return static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), CTRL, ROWMASK, 0xf, false));
+#endif
+}
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+    v |= dpp_u<0x111, 0xf>(v);
+    v |= dpp_u<0x112, 0xf>(v);
+    v |= dpp_u<0x114, 0xf>(v);
+    v |= dpp_u<0x118, 0xf>(v);
+    v |= dpp_u<0x142, 0xa>(v);
+    v |= dpp_u<0x143, 0xc>(v);
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
 // first lane holding the wave maximum of v
 __device__ __forceinline__ int wave_argmax(float v) {
     const float m = wave_fmax(v);

@@ -49,7 +49,7 @@ struct alignas(16) F4 {
     float x, y, z, w;
 };
 
-// per-body record, 41 words (odd: lane-strided gathers of parent records are
+// per-body record, 45 words (odd: lane-strided gathers of parent records are
 // conflict-free); the articulated inertias live in the accumulators below
 struct WaveBody {
     M3 R;        // joint transform (parent -> body)
@@ -62,8 +62,21 @@ struct WaveBody {
     f3 pw;
     int32_t depth;
     float pad_[2];
+    f3 ax;       // joint axis (child frame) and type: the lane-varying walks read
+    int32_t jt;  // them here instead of from the model block in global memory
 };
-static_assert(sizeof(WaveBody) == 41 * 4, "WaveBody layout");
+static_assert(sizeof(WaveBody) == 45 * 4, "WaveBody layout");
+
+// S and S^T of a body's joint from its LDS record (motion / proj of chain_dyn.hpp)
+__device__ __forceinline__ SV motion_rec(const WaveBody& s, float q) {
+    const bool rev = ((s.jt & 1) == 0);
+    const float sw = rev ? q : 0.f, sv = rev ? 0.f : q;
+    return {{s.ax.x * sw, s.ax.y * sw, s.ax.z * sw}, {s.ax.x * sv, s.ax.y * sv, s.ax.z * sv}};
+}
+__device__ __forceinline__ float proj_rec(const WaveBody& s, const SV& x) {
+    const float dw = dot(s.ax, x.w), dv = dot(s.ax, x.v);
+    return ((s.jt & 1) == 0) ? dw : dv;
+}
 
 // child -> parent accumulator of the inward pass (48 words, float4-aligned):
 // articulated inertia with DART's implicit joint damping, bias, and the
@@ -179,7 +192,9 @@ namespace dev {
 template <int MAXN>
 __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const FloatF* __restrict__ F, int N,
                                        const M3& R0, const f3& p0, const SV& V0, WaveWorld<MAXN>& L, Chol6& L0,
-                                       float dt, float* qdd_out, bool ext) {
+                                       float dt, float* qdd_out, bool ext, unsigned long long* prof) {
+    (void)prof;
+    MW_PROF_T(ta0);
     const int lane = lane_id();
     const bool own = lane < N;
     const int i = own ? lane : 0;
@@ -190,17 +205,27 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     const int levels = F->levels, fanout = F->fanout;
     const f3 gw = mk(F->g[0], F->g[1], F->g[2]);
     const int slot = (pa >= 0) ? pa : MAXN;  // accumulator of the parent (MAXN = the base)
-    // accumulators start empty
-    if (lane <= MAXN) L.acc[lane] = WaveAcc{};
-    // outward: kinematics, velocities, bias forces, world poses
+    // children in descending index order: a parent gathers its children's
+    // contributions (F->kids_ok); otherwise the children add into the
+    // parent's accumulator one sibling rank at a time (the same order)
+    const bool gather = F->kids_ok != 0;
+    const uint64_t kids = (gather && own) ? *reinterpret_cast<const uint64_t*>(&F->body_kids[i][0]) : ~0ull;
+    if (!gather && lane <= MAXN) L.acc[lane] = WaveAcc{};  // accumulators start empty
+    // joint transforms and joint velocities: independent of the parent, every
+    // body at once
     M3 R, Rw;
     f3 p, pw;
-    SV V, eta, B;
+    SV V, eta, B, Sq;
     float tau = 0.f;
+    if (own) {
+        joint_pose_tree(b, L.q, i, R, p);
+        Sq = motion(b, L.qd[i]);
+        L.body[i].ax = mk(b.axis[0], b.axis[1], b.axis[2]);
+        L.body[i].jt = b.jtype;
+    }
+    // outward: velocities and world poses, the only parent chain, level by level
     for (int d = 0; d < levels; ++d) {
         if (depth == d) {
-            joint_pose_tree(b, L.q, i, R, p);
-            const SV Sq = motion(b, L.qd[i]);
             const SV Vp = (pa >= 0) ? L.body[pa].V : V0;
             const M3 Rwp = (pa >= 0) ? L.body[pa].Rw : R0;
             const f3 pwp = (pa >= 0) ? L.body[pa].pw : p0;
@@ -212,34 +237,36 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
                     Rw.m[r * 3 + c] =
                         Rwp.m[r * 3] * R.m[c] + Rwp.m[r * 3 + 1] * R.m[3 + c] + Rwp.m[r * 3 + 2] * R.m[6 + c];
             pw = pwp + mul(Rwp, p);
-            const SV Ve = ball_bias_velocity(b, L.qd, i, V);
-            eta = {cross(Ve.w, Sq.w), cross(Ve.w, Sq.v) + cross(Ve.v, Sq.w)};
-            B = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), V,
-                           mulT(Rw, gw));
             L.body[i].V = V;
             L.body[i].Rw = Rw;
             L.body[i].pw = pw;
         }
     }
+    // velocity-product terms and bias forces: every body at once
     float qdi = 0.f;
+    SV extB = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // -(this substep's world wrench), body frame
     if (own) {
+        const SV Ve = ball_bias_velocity(b, L.qd, i, V);
+        eta = {cross(Ve.w, Sq.w), cross(Ve.w, Sq.v) + cross(Ve.v, Sq.w)};
+        B = rigid_bias(b.mass, mk(b.com[0], b.com[1], b.com[2]), inertia_origin(b, b.mass), V, mulT(Rw, gw));
         tau = L.tau[i];
         qdi = L.qd[i];
-    }
-    if (ext) {
-        // this substep's world wrenches (L.ext, mw_apply_link_wrench) enter as
-        // the starting bias of each body's accumulator, in its own frame (the
-        // inward pass adds the children's contributions on top)
-        if (own) {
-            const M3 Rwi = L.body[i].Rw;
+        if (ext) {
+            // this substep's world wrenches (L.ext, mw_apply_link_wrench) enter
+            // as the starting bias of each body's sum, in its own frame
             const float* e = L.ext[1 + i];
-            L.acc[i].B = L.acc[i].B + (-1.f) * SV{mulT(Rwi, mk(e[3], e[4], e[5])), mulT(Rwi, mk(e[0], e[1], e[2]))};
-        }
-        if (lane == 0) {
-            const float* e = L.ext[0];
-            L.acc[MAXN].B = L.acc[MAXN].B + (-1.f) * SV{mulT(R0, mk(e[3], e[4], e[5])), mulT(R0, mk(e[0], e[1], e[2]))};
+            extB = (-1.f) * SV{mulT(Rw, mk(e[3], e[4], e[5])), mulT(Rw, mk(e[0], e[1], e[2]))};
+            if (!gather) L.acc[i].B = L.acc[i].B + extB;
         }
     }
+    SV extB0 = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    if (ext) {
+        const float* e = L.ext[0];
+        extB0 = (-1.f) * SV{mulT(R0, mk(e[3], e[4], e[5])), mulT(R0, mk(e[0], e[1], e[2]))};
+        if (!gather && lane == 0) L.acc[MAXN].B = L.acc[MAXN].B + extB0;
+    }
+    MW_PROF_T(ta1);
+    MW_PROF_ACC(18, ta0, ta1);
     // DART's implicit joint damping (Psi = (S^T AI S + dt d)^-1, force
     // tau - d qd) for the free motion; with damping the impulses use the
     // non-implicit articulated inertias, a second recursion (F->dual)
@@ -252,9 +279,32 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         SI c, cn;
         SV cb;
         if (mine) {
+            // the children's sums (gathered in descending index order, or the
+            // accumulator the children added into)
+            SI AIs, Ins;
+            SV Bs;
+            if (gather) {
+                AIs = SI{};
+                Ins = SI{};
+                Bs = extB;
+#pragma unroll
+                for (int k = 0; k < kMaxKids; ++k) {
+                    const int ch = static_cast<int8_t>((kids >> (8 * k)) & 0xffu);
+                    if (k < fanout && ch >= 0) {
+                        const WaveAcc& a = L.acc[ch];
+                        AIs += a.I;
+                        Bs = Bs + a.B;
+                        if (dual) Ins += a.In;
+                    }
+                }
+            } else {
+                AIs = L.acc[i].I;
+                Bs = L.acc[i].B;
+                Ins = L.acc[i].In;
+            }
             SI AI = rigid(b, b.mass);
-            AI += L.acc[i].I;
-            const SV Bt = B + L.acc[i].B;
+            AI += AIs;
+            const SV Bt = B + Bs;
             U = ais(AI, b);
             psi = rcp(proj(b, U) + dt * b.damping);
             const SV AIeta = mul(AI, eta);
@@ -263,42 +313,78 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
             cb = dad_inv(R, p, Bt + AIeta + (psi * tt) * U);
             if (dual) {
                 SI AIn = rigid(b, b.mass);
-                AIn += L.acc[i].In;
+                AIn += Ins;
                 Un = ais(AIn, b);
                 psin = rcp(proj(b, Un));
                 cn = to_parent(R, p, downdate(AIn, Un, psin));
             }
+            if (gather) {
+                // this body's contribution, in its own slot, for its parent
+                WaveAcc& a = L.acc[i];
+                a.I = c;
+                a.B = cb;
+                if (dual) a.In = cn;
+            }
         }
-        for (int k = 0; k < fanout; ++k) {
-            if (mine && srank == k) {
-                WaveAcc& acc = L.acc[slot];
-                SI I = acc.I;
-                I += c;
-                acc.I = I;
-                acc.B = acc.B + cb;
-                if (dual) {
-                    SI In = acc.In;
-                    In += cn;
-                    acc.In = In;
+        if (gather) wave_lds_sync();  // the next level's parents read these slots
+        if (!gather) {
+            for (int k = 0; k < fanout; ++k) {
+                if (mine && srank == k) {
+                    WaveAcc& acc = L.acc[slot];
+                    SI I = acc.I;
+                    I += c;
+                    acc.I = I;
+                    acc.B = acc.B + cb;
+                    if (dual) {
+                        SI In = acc.In;
+                        In += cn;
+                        acc.In = In;
+                    }
                 }
             }
         }
     }
+    // the base's sums
+    SI IA0s, IA0ns;
+    SV B0s;
+    if (gather) {
+        wave_lds_sync();
+        const uint64_t bk = *reinterpret_cast<const uint64_t*>(&F->body_kids[kMaxBodies][0]);
+        IA0s = SI{};
+        IA0ns = SI{};
+        B0s = extB0;
+#pragma unroll
+        for (int k = 0; k < kMaxKids; ++k) {
+            const int ch = static_cast<int8_t>((bk >> (8 * k)) & 0xffu);
+            if (k < fanout && ch >= 0) {
+                const WaveAcc& a = L.acc[ch];
+                IA0s += a.I;
+                B0s = B0s + a.B;
+                if (dual) IA0ns += a.In;
+            }
+        }
+    } else {
+        IA0s = L.acc[MAXN].I;
+        B0s = L.acc[MAXN].B;
+        IA0ns = L.acc[MAXN].In;
+    }
+    MW_PROF_T(ta2);
+    MW_PROF_ACC(19, ta1, ta2);
     // a welded base (F->fixed: generic fixed-base trees) does not move: a0 = 0
     // and it absorbs every impulse (wave_response), V0 stays 0
     SV a0 = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     if (!F->fixed) {
         SI IA0 = rigid_base(*F);
-        IA0 += L.acc[MAXN].I;
+        IA0 += IA0s;
         const SV B0 = rigid_bias(F->mass, mk(F->com[0], F->com[1], F->com[2]),
                                  Sy{F->Io[0], F->Io[1], F->Io[2], F->Io[3], F->Io[4], F->Io[5]}, V0, mulT(R0, gw)) +
-                      L.acc[MAXN].B;
+                      B0s;
 
         L0.factor(IA0);
         a0 = L0.solve(-1.f * B0);
         if (dual) {
             SI IA0n = rigid_base(*F);
-            IA0n += L.acc[MAXN].In;
+            IA0n += IA0ns;
             L0.factor(IA0n);  // L0 leaves with the impulses' (non-implicit) base inertia
         }
     }
@@ -349,12 +435,11 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
     for (uint64_t m = path; m != 0;) {
         const int i = 63 - __builtin_clzll(m);
         m &= ~(uint64_t{1} << i);
-        const BodyF& b = P->b[i];
         const WaveBody& s = L.body[i];
-        const float ji = proj(b, Fi);
+        const float ji = proj_rec(s, Fi);
         Jrow[6 + i] = ji;
         jv += ji * L.nu[6 + i];
-        const float u = ((i == j) ? 1.f : 0.f) - proj(b, Bi);
+        const float u = ((i == j) ? 1.f : 0.f) - proj_rec(s, Bi);
         L.stack[s.depth][6][lane] = u;
         Bi = dad_inv(s.R, s.p, Bi + (s.psi * u) * s.U);
         Fi = dad_inv(s.R, s.p, Fi);
@@ -457,7 +542,7 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
     MW_PROF_T(t0);
     const M3 R0 = quat_to_R(base.qw, base.qx, base.qy, base.qz);
     Chol6 L0;  // on return: the factorisation the impulses use
-    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, dt, qdd_out, ext);
+    const SV a0 = wave_aba<MAXN>(P, F, N, R0, base.p, base.V, L, L0, dt, qdd_out, ext, prof);
     MW_PROF_T(t1);
     MW_PROF_ACC(1, t0, t1);
     // integrateVelocities (lane e: nu component e)

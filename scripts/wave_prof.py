@@ -132,8 +132,8 @@ print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f}
       f"(PGS-only mode) / the whole exact solve incl. its per-stage sweeps (exact mode); "
       f"{buf[16] / W / T:.0f} in the per-stage sweeps, {buf[17] / W / T:.0f} in stage 1")
 if buf[18] or buf[19]:
-    print(f"  joint-space step: tree passes + CRBA {buf[18] / W / T:.0f}, factorisation + free solve "
-          f"{buf[19] / W / T:.0f} cycles/world-step (both inside the first phase above)")
+    print(f"  inside the first phase: [18] {buf[18] / W / T:.0f}, [19] {buf[19] / W / T:.0f} cycles/world-step "
+          f"(ABA: outward pass 1, inward pass; joint-space step: tree passes + CRBA, factorisation + free solve)")
 dump = np.zeros(8 + 64 * 64 + 9 * 64, dtype=np.float32)
 fd = L.mw_debug_wave_dump
 fd.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -159,7 +159,12 @@ def test_one_step_parity_with_contacts(require_gpu, oracle, urdf, kernel):
           f"force rel err {worst_f:.2e}, {n_contact}/{W} worlds in contact, "
           f"ill-conditioned (world, |dv|, oracle sensitivity): {ill}")
     assert n_contact > W // 4
-    assert len(ill) <= W // 8
+    # excused worlds (W/64): the boxes, spheres and
+    # cylinders stay within it; the rock mesh's support points are redundant
+    # by construction (coplanar hull vertices: its frictionless stage splits
+    # the load by the CFM alone, the oracle itself moves by 1e-2..1e-1 under a
+    # 1e-6 relative error in A), measured 18 of 256 (profiles/r05a)
+    assert len(ill) <= (W // 10 if urdf == "rock" else W // 64)
     assert worst_p <= 1e-5 and worst_v <= 1e-4 and worst_f <= 1e-3
     sim.close()
 
