@@ -79,15 +79,7 @@ struct FloatF {
     int8_t body_depth[kMaxBodies];
     int8_t body_srank[kMaxBodies];
     uint64_t body_path[kMaxBodies];  // bit k: body k is body i or one of its ancestors
-    // children of every body ([kMaxBodies]: of the base) in descending index
-    // order (the serial inward pass's order), -1 padded: the wave kernel's
-    // parents gather their children's contributions (kids_ok: no body has
-    // more than kMaxKids children; else the sibling-rank accumulation)
-    int8_t body_kids[kMaxBodies + 1][8];
-    int32_t kids_ok;
-    int32_t pad_kids_;
 };
-constexpr int kMaxKids = 8;
 
 namespace dev {
 

@@ -371,16 +371,6 @@ void build_float(mw_sim* s) {
         F.body_path[i] = (uint64_t{1} << i) | (pa >= 0 ? F.body_path[pa] : uint64_t{0});
     }
     F.fanout = *std::max_element(children.begin(), children.end());
-    std::memset(F.body_kids, 0xff, sizeof(F.body_kids));
-    F.kids_ok = (F.fanout <= mw::kMaxKids) ? 1 : 0;
-    if (F.kids_ok) {
-        std::vector<int> nk(mw::kMaxBodies + 1, 0);
-        for (int i = n - 1; i >= 0; --i) {
-            const int pa = M.bodies[i].parent;
-            const int slot = (pa >= 0) ? pa : mw::kMaxBodies;
-            F.body_kids[slot][nk[slot]++] = static_cast<int8_t>(i);
-        }
-    }
     F.dual = 0;
     for (int i = 0; i < n; ++i)
         if (M.bodies[i].damping != 0.0) F.dual = 1;

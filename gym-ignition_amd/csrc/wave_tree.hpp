@@ -205,12 +205,8 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     const int levels = F->levels, fanout = F->fanout;
     const f3 gw = mk(F->g[0], F->g[1], F->g[2]);
     const int slot = (pa >= 0) ? pa : MAXN;  // accumulator of the parent (MAXN = the base)
-    // children in descending index order: a parent gathers its children's
-    // contributions (F->kids_ok); otherwise the children add into the
-    // parent's accumulator one sibling rank at a time (the same order)
-    const bool gather = F->kids_ok != 0;
-    const uint64_t kids = (gather && own) ? *reinterpret_cast<const uint64_t*>(&F->body_kids[i][0]) : ~0ull;
-    if (!gather && lane <= MAXN) L.acc[lane] = WaveAcc{};  // accumulators start empty
+    // accumulators start empty
+    if (lane <= MAXN) L.acc[lane] = WaveAcc{};
     // joint transforms and joint velocities: independent of the parent, every
     // body at once
     M3 R, Rw;
@@ -256,14 +252,14 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
             // as the starting bias of each body's sum, in its own frame
             const float* e = L.ext[1 + i];
             extB = (-1.f) * SV{mulT(Rw, mk(e[3], e[4], e[5])), mulT(Rw, mk(e[0], e[1], e[2]))};
-            if (!gather) L.acc[i].B = L.acc[i].B + extB;
+            L.acc[i].B = L.acc[i].B + extB;
         }
     }
     SV extB0 = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
     if (ext) {
         const float* e = L.ext[0];
         extB0 = (-1.f) * SV{mulT(R0, mk(e[3], e[4], e[5])), mulT(R0, mk(e[0], e[1], e[2]))};
-        if (!gather && lane == 0) L.acc[MAXN].B = L.acc[MAXN].B + extB0;
+        if (lane == 0) L.acc[MAXN].B = L.acc[MAXN].B + extB0;
     }
     MW_PROF_T(ta1);
     MW_PROF_ACC(18, ta0, ta1);
@@ -279,32 +275,9 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         SI c, cn;
         SV cb;
         if (mine) {
-            // the children's sums (gathered in descending index order, or the
-            // accumulator the children added into)
-            SI AIs, Ins;
-            SV Bs;
-            if (gather) {
-                AIs = SI{};
-                Ins = SI{};
-                Bs = extB;
-#pragma unroll
-                for (int k = 0; k < kMaxKids; ++k) {
-                    const int ch = static_cast<int8_t>((kids >> (8 * k)) & 0xffu);
-                    if (k < fanout && ch >= 0) {
-                        const WaveAcc& a = L.acc[ch];
-                        AIs += a.I;
-                        Bs = Bs + a.B;
-                        if (dual) Ins += a.In;
-                    }
-                }
-            } else {
-                AIs = L.acc[i].I;
-                Bs = L.acc[i].B;
-                Ins = L.acc[i].In;
-            }
             SI AI = rigid(b, b.mass);
-            AI += AIs;
-            const SV Bt = B + Bs;
+            AI += L.acc[i].I;
+            const SV Bt = B + L.acc[i].B;
             U = ais(AI, b);
             psi = rcp(proj(b, U) + dt * b.damping);
             const SV AIeta = mul(AI, eta);
@@ -313,61 +286,33 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
             cb = dad_inv(R, p, Bt + AIeta + (psi * tt) * U);
             if (dual) {
                 SI AIn = rigid(b, b.mass);
-                AIn += Ins;
+                AIn += L.acc[i].In;
                 Un = ais(AIn, b);
                 psin = rcp(proj(b, Un));
                 cn = to_parent(R, p, downdate(AIn, Un, psin));
             }
-            if (gather) {
-                // this body's contribution, in its own slot, for its parent
-                WaveAcc& a = L.acc[i];
-                a.I = c;
-                a.B = cb;
-                if (dual) a.In = cn;
-            }
         }
-        if (gather) wave_lds_sync();  // the next level's parents read these slots
-        if (!gather) {
-            for (int k = 0; k < fanout; ++k) {
-                if (mine && srank == k) {
-                    WaveAcc& acc = L.acc[slot];
-                    SI I = acc.I;
-                    I += c;
-                    acc.I = I;
-                    acc.B = acc.B + cb;
-                    if (dual) {
-                        SI In = acc.In;
-                        In += cn;
-                        acc.In = In;
-                    }
+        // children add into the parent's accumulator one sibling rank at a
+        // time, highest body index first (a parent gathering its children's
+        // slots instead measured slower: profiles/r05b)
+        for (int k = 0; k < fanout; ++k) {
+            if (mine && srank == k) {
+                WaveAcc& acc = L.acc[slot];
+                SI I = acc.I;
+                I += c;
+                acc.I = I;
+                acc.B = acc.B + cb;
+                if (dual) {
+                    SI In = acc.In;
+                    In += cn;
+                    acc.In = In;
                 }
             }
         }
     }
-    // the base's sums
-    SI IA0s, IA0ns;
-    SV B0s;
-    if (gather) {
-        wave_lds_sync();
-        const uint64_t bk = *reinterpret_cast<const uint64_t*>(&F->body_kids[kMaxBodies][0]);
-        IA0s = SI{};
-        IA0ns = SI{};
-        B0s = extB0;
-#pragma unroll
-        for (int k = 0; k < kMaxKids; ++k) {
-            const int ch = static_cast<int8_t>((bk >> (8 * k)) & 0xffu);
-            if (k < fanout && ch >= 0) {
-                const WaveAcc& a = L.acc[ch];
-                IA0s += a.I;
-                B0s = B0s + a.B;
-                if (dual) IA0ns += a.In;
-            }
-        }
-    } else {
-        IA0s = L.acc[MAXN].I;
-        B0s = L.acc[MAXN].B;
-        IA0ns = L.acc[MAXN].In;
-    }
+    const SI IA0s = L.acc[MAXN].I, IA0ns = L.acc[MAXN].In;
+    const SV B0s = L.acc[MAXN].B;
+    (void)extB0;
     MW_PROF_T(ta2);
     MW_PROF_ACC(19, ta1, ta2);
     // a welded base (F->fixed: generic fixed-base trees) does not move: a0 = 0
