@@ -468,6 +468,47 @@ __device__ __forceinline__ SV ball_bias_velocity(const BodyF& b, const float* qd
     return V;
 }
 
+// f64 constants of the ball-joint integrator: 1/n! for n = 0..23 (Taylor
+// coefficients, correctly rounded), then 2 pi as hi + lo and 1 / (2 pi).
+// Read through ball_coeffs()'s opaque pointer so that every use loads them
+// (off the hot path) instead of the compiler keeping them in registers.
+constexpr int kBall2PiHi = 24, kBall2PiLo = 25, kBallInv2Pi = 26;
+#ifdef MW_HOST_TEST
+static const double kBallConst[27] = {
+#else
+static __device__ const double kBallConst[27] = {
+#endif
+    1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664, 0.008333333333333333, 0.001388888888888889,
+    0.0001984126984126984, 2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07,
+    2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10, 1.1470745597729725e-11,
+    7.647163731819816e-13, 4.779477332387385e-14, 2.8114572543455206e-15, 1.5619206968586225e-16,
+    8.22063524662433e-18, 4.110317623312165e-19, 1.9572941063391263e-20, 8.896791392450574e-22,
+    3.868170170630684e-23, 6.283185307179586, 2.4492935982947064e-16, 0.15915494309189535};
+
+__device__ __forceinline__ const double* ball_coeffs() {
+#ifdef MW_HOST_TEST
+    return kBallConst;
+#else
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return kBallConst + z;
+#endif
+}
+
+// sin and cos of x, |x| <= pi/2: Taylor polynomials to x^23 / x^22 in Horner
+// form (truncation below 1e-19 at pi/2)
+__device__ __forceinline__ void ball_sincos(double x, const double* C, double& s, double& c) {
+    const double x2 = x * x;
+    double ps = C[23], pc = C[22];
+#pragma unroll
+    for (int j = 21; j >= 1; j -= 2) {
+        ps = fma(-x2, ps, C[j]);
+        pc = fma(-x2, pc, C[j - 1]);
+    }
+    s = x * ps;
+    c = pc;
+}
+
 // component k of a ball joint's new position log(exp(theta) exp(dt w)),
 // theta = th[0..2], w = w[0..2] (quaternion product; angle in [0, pi])
 __device__ __forceinline__ float ball_integrate(float t0, float t1, float t2, float w0, float w1, float w2, float dt,
@@ -477,10 +518,22 @@ __device__ __forceinline__ float ball_integrate(float t0, float t1, float t2, fl
     // at a slowly moving angle, which drifts (r04r: 5e-5 rad after 500 steps
     // at |theta| = pi/2 against DART's fp64 scheme); one joint part per lane,
     // off the hot path
-    auto quat = [](double x, double y, double z, double (&qt)[4]) {
+    // sin / cos / atan2 are this file's own (ball_sincos, below): the
+    // library's f64 versions put ~28 f64 polynomial constants in registers
+    // for the whole wave kernel (hoisted out of the step loop), 6 of them
+    // spilled to scratch (r05)
+    const double* C = ball_coeffs();
+    auto quat = [C](double x, double y, double z, double (&qt)[4]) {
         const double t = sqrt(x * x + y * y + z * z);
-        const double s = (t < 1e-150) ? 0.5 : sin(0.5 * t) / t;
-        qt[0] = cos(0.5 * t); qt[1] = s * x; qt[2] = s * y; qt[3] = s * z;
+        // t reduced by a multiple of 2 pi: the half-angle's sin and cos
+        // change sign together, which negates the quaternion (the product's
+        // sign is normalised below)
+        const double kk = rint(t * C[kBallInv2Pi]);
+        const double tr = fma(-kk, C[kBall2PiLo], fma(-kk, C[kBall2PiHi], t));
+        double sn, cs;
+        ball_sincos(0.5 * tr, C, sn, cs);
+        const double s = (t == 0.0) ? 0.5 : sn / t;
+        qt[0] = cs; qt[1] = s * x; qt[2] = s * y; qt[3] = s * z;
     };
     double a[4], b[4];
     const double h = dt;
@@ -492,7 +545,13 @@ __device__ __forceinline__ float ball_integrate(float t0, float t1, float t2, fl
     double c3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
     if (c0 < 0.0) { c0 = -c0; c1 = -c1; c2 = -c2; c3 = -c3; }
     const double v = sqrt(c1 * c1 + c2 * c2 + c3 * c3);
-    const double f = (v < 1e-150) ? 2.0 / c0 : 2.0 * atan2(v, c0) / v;
+    // phi = atan2(v, c0) in [0, pi/2]: the fp32 angle, then one correction
+    // phi0 + tan(phi - phi0) (exact up to (phi - phi0)^3 / 3 ~ 1e-22)
+    const double p0 = static_cast<double>(atan2f(static_cast<float>(v), static_cast<float>(c0)));
+    double sp, cp;
+    ball_sincos(p0, C, sp, cp);
+    const double phi = p0 + (v * cp - c0 * sp) / (c0 * cp + v * sp);
+    const double f = (v == 0.0) ? 2.0 / c0 : 2.0 * phi / v;
     return static_cast<float>(f * ((k == 0) ? c1 : ((k == 1) ? c2 : c3)));
 }
 

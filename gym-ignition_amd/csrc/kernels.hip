@@ -625,7 +625,10 @@ __device__ __forceinline__ float dof_force(const ChainF* __restrict__ P, const S
 #endif
 
 template <int MAXN, bool CONS>
-__global__ void __launch_bounds__(64) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
+#ifndef MW_WAVE_OCC
+#define MW_WAVE_OCC 1  // waves per SIMD the wave kernel is compiled for (A/B builds)
+#endif
+__global__ void __launch_bounds__(64, MW_WAVE_OCC) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
                                                       int N, SimDev S, FreeDev D, const PidF* __restrict__ pid,
                                                       int W, RunArgs A, int want_contacts, int* __restrict__ overflow) {
     const int w = xcd_block();  // XCD-aware (xcd.hpp): neighbouring worlds share state lines

@@ -89,7 +89,8 @@ struct ScWorld {
 };
 
 #ifdef MW_WAVE_PROF
-__device__ float g_sc_dump[8 + 64 * 64 + 7 * 64];
+constexpr int kScDumpFloats = 8 + 64 * 64 + 8 * 64;
+__device__ float g_sc_dump[kDumpSlots * kScDumpFloats];
 __device__ unsigned int g_sc_dump_claim;
 #endif
 
@@ -1166,14 +1167,15 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                                                                                 nsolve, nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
 #ifdef MW_WAVE_PROF
-                // debug dump of one hard LCP (the first with >= 6 solves): n, A,
-                // b, lo, hi, the two warm records, the result, the solve count
-                if (nsolve >= 6 && NR <= kWaveLanes) {
+                // debug dump of up to kDumpSlots hard LCPs (>= 8 solves, or
+                // the unconverged ones with -DMW_DUMP_FAIL): n, A, b, lo, hi,
+                // the two warm records, the result, kind, the stage-1 result
+                if (MW_DUMP_WHEN(ok, nsolve) && NR <= kWaveLanes) {
                     unsigned int claim = 0u;
-                    if (lane == 0) claim = atomicCAS(&g_sc_dump_claim, 0u, 1u);
+                    if (lane == 0) claim = atomicAdd(&g_sc_dump_claim, 1u);
                     claim = __builtin_amdgcn_readfirstlane(claim);
-                    if (claim == 0u) {
-                        float* D0 = g_sc_dump;
+                    if (claim < static_cast<unsigned int>(kDumpSlots)) {
+                        float* D0 = g_sc_dump + claim * kScDumpFloats;
                         for (int r = 0; r < NR; ++r) D0[8 + r * kWaveLanes + lane] = (lane < NR) ? a[r] : 0.f;
                         float* V = D0 + 8 + kWaveLanes * kWaveLanes;
                         if (lane < NR) {
@@ -1184,6 +1186,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                             V[4 * kWaveLanes + lane] = xw1;
                             V[5 * kWaveLanes + lane] = x0;
                             V[6 * kWaveLanes + lane] = static_cast<float>(Rw.kind);
+                            V[7 * kWaveLanes + lane] = x1s;
                         }
                         if (lane == 0) {
                             D0[0] = static_cast<float>(NR);

@@ -625,7 +625,8 @@ __device__ __forceinline__ float lcp_mfma_solve(const float (&a)[kWaveMaxRows], 
 // sit on their bound, every linear solve minimises over the free rows (A_FF is
 // symmetric positive definite: no pivot search, the held rows' steps skipped)
 // and takes the longest step that stays in the box; the first bound met joins
-// the working set; at the working set's minimiser every held row whose
+// the working set (every bound met, when the step has zero length); at the
+// working set's minimiser every held row whose
 // multiplier is wrongly signed beyond its own tolerance (the scale the
 // residual test uses) leaves it -- several at once: contacts that barely
 // touch (approach velocities of 1e-7 m/s in a settling stack) would each
@@ -634,7 +635,10 @@ __device__ __forceinline__ float lcp_mfma_solve(const float (&a)[kWaveMaxRows], 
 // more solve on the same working set from the compensated residual refines it
 // (iterative refinement), until a refinement moves nothing (kLcpStall: the
 // fp32 floor; converged if within kLcpFloorAccept of the tolerance).  solves
-// counts the linear solves against `budget`.
+// counts the linear solves against `budget`.  Termination: a step of nonzero
+// length lowers the objective; zero-length steps only add rows to the working
+// set; a release that cannot move its rows freezes them (below), and after a
+// blocked multi-release rows leave singly until the next full step.
 // Returns true when every row's residual is within tolerance.
 template <int RC, bool LongRows = false, int MFMA = kLcpMfma32>
 __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool live, float b, float L, float U,
@@ -655,8 +659,17 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
     bool at_min = __ballot(!pinned && ws == 0) == 0ull;
     bool stalled = false; // ... by a refinement solve that moved nothing
     bool fresh = false;   // w / g / mag / xmax / rel belong to the current x
-    bool single = false;  // release one row at a time (after a blocked multi-release)
+    bool single = false;  // release one row at a time (after a blocked multi-release, until the next full step)
     uint64_t released = 0ull;  // the rows of the last release
+    // rows whose release could not move them: the solve on the grown free set
+    // moved nothing, or turned the one released row straight back out of its
+    // box.  In exact arithmetic a released row with a wrongly signed
+    // multiplier always moves inward (d_r = -(A_FF^-1)_rr g_r); here its
+    // multiplier is below the fp32 solve's resolution.  Frozen rows stay on
+    // their bound for the rest of this call (their residual still counts):
+    // without this a pair of such rows cycled release / block until the
+    // budget (scene dumps, scripts/lcp_dump_check.py).
+    uint64_t frozen = 0ull;
     float w = 0.f, g = 0.f, mag = 0.f, xmax = 0.f, rel = 0.f;
     float rel_refine = 3.4e38f;  // the residual when the last refinement solve started
     for (int it = 0; it < 4 * budget + 8 + n; ++it, ++iters) {
@@ -672,7 +685,7 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         if (at_min) {
             at_min = false;
             float v = (ws == 1) ? -g : ((ws == 2) ? g : 0.f);
-            v = pinned ? 0.f : v * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol);
+            v = (pinned || mask_bit(frozen, lane)) ? 0.f : v * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol);
             // every held row whose multiplier is wrongly signed beyond its
             // tolerance leaves at once (one solve for several micro-contacts).
             // Each step stays in the box and does not raise the objective, but
@@ -733,6 +746,11 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         // the longest feasible step along d (at most 1)
         const float dmax = wave_fmax(fr ? fabsf(d) : 0.f);
         if (dmax <= kLcpStall * (1.f + xmax)) {
+            if (released) {  // the release moved nothing: back to the bounds, frozen
+                if (mask_bit(released, lane)) ws = (xl <= L) ? 1 : 2;
+                frozen |= released;
+                released = 0ull;
+            }
             at_min = true;
             stalled = true;
             continue;
@@ -748,18 +766,39 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         if (amin < 1.f) {
             const int block = wave_argmax(-al);
             const int bside = __builtin_amdgcn_readlane(side, block);
-            // a row of a multi-row release blocks at once: release singly from now on
-            if (amin <= 0.f && mask_bit(released, block) && __builtin_popcountll(released) > 1) single = true;
+            // a row of a multi-row release blocks at once: release singly
+            // until the next full step; a single released row that blocks at
+            // once is frozen, and the working set is the one before the
+            // release, at its minimiser
+            bool back = false;
+            if (amin <= 0.f && mask_bit(released, block)) {
+                if (__builtin_popcountll(released) > 1) {
+                    single = true;
+                } else {
+                    frozen |= released;
+                    back = true;
+                }
+            }
             released = 0ull;
             xl = fr ? xl + amin * d : xl;
             if (lane == block) {
                 xl = (bside == 1) ? L : U;
                 ws = bside;
             }
+            // a zero-length step: every row it blocks joins its bound now
+            // (x does not move, so each would block the next solve at zero
+            // length, one solve per row: warm starts whose friction boxes
+            // shrank)
+            if (amin <= 0.f && fr && side != 0 && al <= 0.f) {
+                xl = (side == 1) ? L : U;
+                ws = side;
+            }
+            at_min = back;
         } else {
             xl = fr ? xl + d : xl;
             at_min = true;
             released = 0ull;
+            single = false;
         }
     }
     return false;

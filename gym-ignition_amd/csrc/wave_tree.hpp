@@ -99,7 +99,9 @@ struct WaveWorld {
     uint32_t act[MAXN];
     float ext[MAXN + 1][6];      // this substep's world wrenches: [0] the base, [1 + i] body i (f, tau)
     float nu[kNv];
-    static constexpr int kJStride = (kNv + 3) & ~3;  // float4 rows: read as uniform broadcasts
+    // odd like MJ: the response pass writes, and the Delassus tiles read, one
+    // row per lane (a stride of 24/40/56 put 8 lanes on each bank)
+    static constexpr int kJStride = kNv | 1;
     alignas(16) float J[kWaveMaxRows][kJStride];
     float MJ[kWaveMaxRows][kRowStride];
     float b[kWaveMaxRows], lo[kWaveMaxRows], hi[kWaveMaxRows];
@@ -144,9 +146,17 @@ constexpr int kWaveProfPhases = 20;  // [8] exact-LCP linear solves, [9] its rou
                                      // [16] in the exact solve's per-stage sweeps, [17] in its stage 1
 #ifdef MW_WAVE_PROF
 __device__ unsigned long long g_wave_prof[kWaveProfPhases];
-// one hard exact LCP (the first world-step with >= 8 linear solves): n, A,
-// b, lo, hi, kind, both warm records, both results (scripts/wave_prof.py)
-__device__ float g_wave_dump[8 + 64 * 64 + 9 * 64];
+// up to kDumpSlots hard exact LCPs (world-steps with >= 8 linear solves, or
+// with -DMW_DUMP_FAIL the unconverged ones): n, A, b, lo, hi, kind, both warm
+// records, both results (scripts/wave_prof.py, scripts/lcp_dump_check.py)
+constexpr int kDumpSlots = 8;
+constexpr int kWaveDumpFloats = 8 + 64 * 64 + 9 * 64;
+__device__ float g_wave_dump[kDumpSlots * kWaveDumpFloats];
+#ifdef MW_DUMP_FAIL
+#define MW_DUMP_WHEN(ok, ns) (!(ok))
+#else
+#define MW_DUMP_WHEN(ok, ns) ((ns) >= 8)
+#endif
 __device__ unsigned int g_wave_dump_claim;
 #define MW_PROF_T(var) const long long var = clock64()
 #define MW_PROF_ACC(k, a, b) (prof[k] += static_cast<unsigned long long>((b) - (a)))
@@ -688,20 +698,29 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         // unrolled to the instance's coordinate count (the operand loads go
         // out ahead of the MFMA chain; a loop to the runtime NV waited on each
         // k-step's loads: 14.6k -> see DESIGN.md cycles per world-step);
-        // columns >= NV: J is zero there, MJ masked
+        // columns >= NV: J is zero there, MJ masked.  Chunks of 8 coordinates
+        // (4 k-steps) end at the world's own NV (a uniform branch), so a
+        // floating box (NV 6) in a MAXN-16 instance runs 4 k-steps, not 11.
+        constexpr int kKs = (WaveWorld<MAXN>::kNv + 1) / 2;
 #pragma unroll
-        for (int k = 0; k < (WaveWorld<MAXN>::kNv + 1) / 2; ++k) {
-            const int e = 2 * k + lh;
-            const bool ev = e < NV;
-            const float j0 = L.J[lr][e];
-            const float m0 = ev ? L.MJ[lr][e] : 0.f;
-            t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m0, t00, 0, 0, 0);
-            if (two) {
-                const float j1 = L.J[32 + lr][e];
-                const float m1 = ev ? L.MJ[32 + lr][e] : 0.f;
-                t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m1, t01, 0, 0, 0);
-                t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m0, t10, 0, 0, 0);
-                t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m1, t11, 0, 0, 0);
+        for (int k0 = 0; k0 < kKs; k0 += 4) {
+            if (2 * k0 >= NV) break;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int k = k0 + kk;
+                if (k >= kKs) break;
+                const int e = 2 * k + lh;
+                const bool ev = e < NV;
+                const float j0 = L.J[lr][e];
+                const float m0 = ev ? L.MJ[lr][e] : 0.f;
+                t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m0, t00, 0, 0, 0);
+                if (two) {
+                    const float j1 = L.J[32 + lr][e];
+                    const float m1 = ev ? L.MJ[32 + lr][e] : 0.f;
+                    t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m1, t01, 0, 0, 0);
+                    t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m0, t10, 0, 0, 0);
+                    t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m1, t11, 0, 0, 0);
+                }
             }
         }
         float a[kWaveMaxRows];
@@ -807,12 +826,12 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
                 ok = wave_lcp_exact<kWaveMaxRows, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
                                                   nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
-            if (nsolve >= 8) {
+            if (MW_DUMP_WHEN(ok, nsolve)) {
                 unsigned int claim = 0u;
-                if (lane == 0) claim = atomicCAS(&g_wave_dump_claim, 0u, 1u);
+                if (lane == 0) claim = atomicAdd(&g_wave_dump_claim, 1u);
                 claim = __builtin_amdgcn_readfirstlane(claim);
-                if (claim == 0u) {
-                    float* D0 = g_wave_dump;
+                if (claim < static_cast<unsigned int>(kDumpSlots)) {
+                    float* D0 = g_wave_dump + claim * kWaveDumpFloats;
                     for (int r = 0; r < R; ++r) D0[8 + r * 64 + lane] = (lane < R) ? a[r] : 0.f;
                     float* V = D0 + 8 + 64 * 64;
                     if (lane < R) {

@@ -24,13 +24,24 @@ from mwstep import sim as _sim  # noqa: E402
 _init = _sim.Simulator.__init__
 
 
+from mwstep import scene as _scene  # noqa: E402
+
+_sinit = _scene.Scene.__init__
+
+
 def _with_budget(budget):
     """legs named leg@B run the exact LCP with a budget of B linear solves"""
     def init(self, *a, **kw):
         _init(self, *a, **kw)
         if budget:
             self.set_lcp_solver(True, budget)
+
+    def sinit(self, *a, **kw):
+        _sinit(self, *a, **kw)
+        if budget:
+            self.set_lcp_solver(True, budget)
     _sim.Simulator.__init__ = init
+    _scene.Scene.__init__ = sinit
 
 
 _NoDist = bench._NoDist

@@ -17,6 +17,30 @@ from mwstep import get_model_file  # noqa: E402
 from mwstep import native as N  # noqa: E402
 from mwstep.sim import Simulator  # noqa: E402
 
+def save_dumps(fd, nvec, name, slots=8):
+    """The kernels' LCP dumps (up to `slots`; debug builds, see wave_tree.hpp
+    g_wave_dump): every slot as n, A (n x n), the row vectors, solve counts."""
+    per = 8 + 64 * 64 + nvec * 64
+    dump = np.zeros(slots * per, dtype=np.float32)
+    fd.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if fd(dump.ctypes.data, dump.size) != 0:
+        return
+    D = dump.reshape(slots, per)
+    used = [k for k in range(slots) if D[k, 0] > 0]
+    if not used:
+        print("no LCP dumped")
+        return
+    out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", name)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    # row r of the dump = lane r's registers a[c] = A[r][c] written at [c][r]: transpose
+    A = np.stack([D[k, 8:8 + 64 * 64].reshape(64, 64).T for k in used])
+    V = np.stack([D[k, 8 + 64 * 64:].reshape(nvec, 64) for k in used])
+    H = np.stack([D[k, :8] for k in used])
+    np.savez(out, A=A, V=V, head=H, layout=("scene" if nvec == 8 else "wave"))
+    for k in range(len(used)):
+        print(f"dumped LCP {k}: {int(H[k, 0])} rows, {int(H[k, 1])} solves ({int(H[k, 2])} in stage 2), ok {int(H[k, 4])}")
+
+
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 PGS = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 print(f"exact={os.environ.get('MW_PROF_EXACT', '1')} warm={os.environ.get('MW_PROF_WARM', '0')}")
@@ -51,18 +75,7 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "scene3":
           f"per solve: {buf[8] / ns:.2f} linear solves ({buf[10] / ns:.2f} in stage 2), {buf[9] / ns:.2f} rounds, "
           f"max {buf[11]}, {buf[13]} > 4; cycles: {buf[14] / ns:.0f} in solves, {buf[16] / ns:.0f} in sweeps, "
           f"{buf[17] / ns:.0f} in stage 1")
-    dump = np.zeros(8 + 64 * 64 + 7 * 64, dtype=np.float32)
-    fd = N.lib().mw_debug_scene_dump
-    fd.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    if fd(dump.ctypes.data, dump.size) == 0 and dump[0] > 0:
-        n = int(dump[0])
-        A = dump[8:8 + 64 * 64].reshape(64, 64)[:n, :n]   # row r = lane r's registers: A[lane][r] -> transpose
-        V = dump[8 + 64 * 64:].reshape(7, 64)[:, :n]
-        out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "scene_dump.npz")
-        os.makedirs(os.path.dirname(out), exist_ok=True)
-        np.savez(out, A=A.T.copy(), b=V[0], lo=V[1], hi=V[2], xw=V[3], xw1=V[4], x=V[5], kind=V[6],
-                 nsolve=dump[1], nsolve2=dump[2], mu=dump[3], ok=dump[4])
-        print(f"dumped a hard LCP: {n} rows, {int(dump[1])} solves ({int(dump[2])} in stage 2), ok {int(dump[4])}")
+    save_dumps(N.lib().mw_debug_scene_dump, 8, "scene_dump.npz")
     sys.exit(0)
 if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
     # the bench's contacts leg (bench.contact_leg): cubes dropped from random poses
@@ -92,6 +105,7 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
     print(f"  exact LCP: {buf[8] / W / T:.2f} solves per world-step, max {buf[11]}, {buf[13]} world-steps > 4; "
           f"{buf[14] / W / T:.0f} cycles in the solves, {buf[16] / W / T:.0f} in the sweeps, "
           f"{buf[17] / W / T:.0f} in stage 1")
+    save_dumps(L.mw_debug_wave_dump, 9, "wave_dump.npz")
     sys.exit(0)
 sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=PGS, pose=(0, 0, 0.535, 1, 0, 0, 0))
 names = sim.joint_names
@@ -134,16 +148,5 @@ print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f}
 if buf[18] or buf[19]:
     print(f"  inside the first phase: [18] {buf[18] / W / T:.0f}, [19] {buf[19] / W / T:.0f} cycles/world-step "
           f"(ABA: outward pass 1, inward pass; joint-space step: tree passes + CRBA, factorisation + free solve)")
-dump = np.zeros(8 + 64 * 64 + 9 * 64, dtype=np.float32)
-fd = L.mw_debug_wave_dump
-fd.argtypes = [ctypes.c_void_p, ctypes.c_int]
-if fd(dump.ctypes.data, dump.size) == 0 and dump[0] > 0:
-    n = int(dump[0])
-    A = dump[8:8 + 64 * 64].reshape(64, 64)[:n, :n]
-    V = dump[8 + 64 * 64:].reshape(9, 64)[:, :n]
-    out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "wave_dump.npz")
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    np.savez(out, A=A.T.copy(), b=V[0], lo=V[1], hi=V[2], kind=V[3], xw=V[4], xw1=V[5], x=V[6], x1=V[7],
-             nsolve=dump[1], nsolve2=dump[2], mu=dump[3], ok=dump[4])
-    print(f"dumped a hard LCP: {n} rows, {int(dump[1])} solves ({int(dump[2])} in stage 2), ok {int(dump[4])}")
+save_dumps(L.mw_debug_wave_dump, 9, "wave_dump.npz")
 sim.close()
