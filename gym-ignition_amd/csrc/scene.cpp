@@ -108,7 +108,7 @@ struct mw_scene {
     float* h_wphys = nullptr;       // pinned mirror of d_wphys (uploaded with the presence words)
     int64_t overflow_seen = 0;      // drops already reported
     int32_t lcp_mode = MW_LCP_EXACT;  // mw_scene_set_lcp_solver
-    int32_t lcp_solves = 24;
+    int32_t lcp_solves = 48;        // linear solves per world-step (scene leg: 24 -> 724 unconverged, 48 -> 0; profiles/r05t)
     mw::PidF* h_pid = nullptr;
     size_t jrows = 0;              // NBMAX * W
     // host-only component data

@@ -744,8 +744,15 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
 #endif
         ++solves;
         // the longest feasible step along d (at most 1)
+        // ... moves nothing: no impulse by more than kLcpStall (relative to
+        // 1 + max |x|) and no row's own residual (d_r A_rr) by more than its
+        // tolerance.  The second test keeps steps that are tiny in x but not
+        // for their row: a joint-limit row (A_rr ~ 136 on the humanoid, b ~
+        // 1e-5) needed x = -9e-8 and counted unconverged at the floor (the 8
+        // unconverged world-steps of the humanoid leg, scripts/lcp_dump_check.py)
         const float dmax = wave_fmax(fr ? fabsf(d) : 0.f);
-        if (dmax <= kLcpStall * (1.f + xmax)) {
+        const float dres = wave_fmax(fr ? fabsf(d) * arr * rcp(kLcpRelTol * (fabsf(b) + mag) + kLcpAbsTol) : 0.f);
+        if (dmax <= kLcpStall * (1.f + xmax) && dres <= 1.f) {
             if (released) {  // the release moved nothing: back to the bounds, frozen
                 if (mask_bit(released, lane)) ws = (xl <= L) ? 1 : 2;
                 frozen |= released;

@@ -163,7 +163,7 @@ class Scene:
         nw = self.n_worlds - w0 if nw is None else nw
         N.check(N.lib().mw_scene_set_world_friction(self.handle, w0, nw, float(mu)), "set_world_friction")
 
-    def set_lcp_solver(self, exact: bool = True, max_solves: int = 24) -> None:
+    def set_lcp_solver(self, exact: bool = True, max_solves: int = 48) -> None:
         """mw_scene_set_lcp_solver: exact boxed LCP after the PGS sweeps (default) or the sweeps alone."""
         N.check(N.lib().mw_scene_set_lcp_solver(self.handle, N.LCP_EXACT if exact else N.LCP_PGS, int(max_solves)),
                 "set_lcp_solver")

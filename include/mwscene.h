@@ -103,7 +103,7 @@ int mw_scene_world_gravity(const mw_scene* sc, int32_t w, double g[3]);
  * those worlds uses it); mw_scene_set_ground_plane sets every world's. */
 int mw_scene_set_world_friction(mw_scene* sc, int32_t w0, int32_t nw, double mu);
 /* Boxed-LCP solver of the scene kernel (as mw_set_lcp_solver): MW_LCP_EXACT
- * (default, 24 linear solves per world-step) solves the contact / joint LCP
+ * (default, 48 linear solves per world-step) solves the contact / joint LCP
  * exactly after the PGS sweeps when a world has <= 64 rows (worlds with more
  * rows keep the sweeps and are counted); MW_LCP_PGS: the sweeps alone. */
 int mw_scene_set_lcp_solver(mw_scene* sc, int32_t mode, int32_t max_solves);

@@ -89,3 +89,12 @@ for spec in sys.argv[1:] or ["humanoid", "humanoid_pgs", "scene"]:
         raise SystemExit(f"unknown leg {leg}")
     keep = {k: v for k, v in out.items() if k not in ("workload",)}
     print(spec, json.dumps(keep), flush=True)
+    if os.environ.get("LEG_DUMP", "0") == "1":
+        # debug library (MW_WAVE_PROF, MW_DUMP_FAIL): the leg's unconverged LCPs
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from lcp_dumps import save_dumps
+        from mwstep import native as _N
+        if leg == "scene":
+            save_dumps(_N.lib().mw_debug_scene_dump, 8, f"leg_{leg}_scene_dump.npz")
+        else:
+            save_dumps(_N.lib().mw_debug_wave_dump, 9, f"leg_{leg}_wave_dump.npz")

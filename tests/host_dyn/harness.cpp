@@ -87,3 +87,12 @@ extern "C" int hd_float_step(const ChainF* P, const FloatF* F, float* base, floa
     default: return -1;
     }
 }
+
+// the ball-joint integrator (chain_dyn.hpp ball_integrate) over n states:
+// th[3 n], w[3 n] -> out[3 n]
+extern "C" void hd_ball_integrate(const float* th, const float* w, float dt, int n, float* out) {
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k)
+            out[3 * i + k] = mw::dev::ball_integrate(th[3 * i], th[3 * i + 1], th[3 * i + 2], w[3 * i], w[3 * i + 1],
+                                            w[3 * i + 2], dt, k);
+}

@@ -48,7 +48,7 @@ def _scene(models, W, pgs=50, mu=0.8, exact=False):
     exact solve is covered by the KATs and the exact-mode tests)."""
     from mwstep.scene import Scene
     sc = Scene(n_worlds=W, pgs_iters=pgs)
-    assert sc.lcp_solver() == (True, 24)
+    assert sc.lcp_solver() == (True, 48)
     sc.set_lcp_solver(exact)
     sc.set_ground_plane(True, mu)
     for text, pose, name in models:
