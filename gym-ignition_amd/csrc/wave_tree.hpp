@@ -726,13 +726,19 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         float a[kWaveMaxRows];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const int r0 = 8 * (i / 4) + (i % 4);  // this half's row; the other half holds r0 + 4
-            const float g0 = __shfl_xor(lh ? t00[i] : t01[i], 32);
-            a[r0] = lh ? g0 : t00[i];
-            a[r0 + 4] = lh ? t01[i] : g0;
-            const float g1 = __shfl_xor(lh ? t10[i] : t11[i], 32);
-            a[32 + r0] = lh ? g1 : t10[i];
-            a[32 + r0 + 4] = lh ? t11[i] : g1;
+            // this half's row r0; the other half holds r0 + 4.  One
+            // v_permlane32_swap per tile pair: lanes < 32 get t00 of their
+            // own and of lane + 32, lanes >= 32 t01 of lane - 32 and their own
+            // (a ds_bpermute __shfl_xor + selects before)
+            const int r0 = 8 * (i / 4) + (i % 4);
+            float x0 = t00[i], y0 = t01[i];
+            lane_swap32(x0, y0);
+            a[r0] = x0;
+            a[r0 + 4] = y0;
+            float x1 = t10[i], y1 = t11[i];
+            lane_swap32(x1, y1);
+            a[32 + r0] = x1;
+            a[32 + r0 + 4] = y1;
         }
         float dg = 1.f;
 #pragma unroll
