@@ -462,18 +462,24 @@ __device__ __forceinline__ FreeState load_base(const FreeDev& D, int W, int w, b
     S.qw = at(3); S.qx = at(4); S.qy = at(5); S.qz = at(6);
     S.V = {{at(7), at(8), at(9)}, {at(10), at(11), at(12)}};
     if (first) {
+        // the reset values load together with their flag (one round trip,
+        // not a flag load and then the values: both buffers always exist)
         const uint8_t fl = D.rflag[w];
+        float rp[7], rv[6];
+#pragma unroll
+        for (int f = 0; f < 7; ++f) rp[f] = D.rpose[f * W + w];
+#pragma unroll
+        for (int f = 0; f < 6; ++f) rv[f] = D.rvel[f * W + w];
         if (fl & 1u) {
-            S.p = {D.rpose[0 * W + w], D.rpose[1 * W + w], D.rpose[2 * W + w]};
-            float qw = D.rpose[3 * W + w], qx = D.rpose[4 * W + w], qy = D.rpose[5 * W + w], qz = D.rpose[6 * W + w];
-            const float inv = 1.f / sqrtf(qw * qw + qx * qx + qy * qy + qz * qz);
-            S.qw = qw * inv; S.qx = qx * inv; S.qy = qy * inv; S.qz = qz * inv;
+            S.p = {rp[0], rp[1], rp[2]};
+            const float inv = 1.f / sqrtf(rp[3] * rp[3] + rp[4] * rp[4] + rp[5] * rp[5] + rp[6] * rp[6]);
+            S.qw = rp[3] * inv; S.qx = rp[4] * inv; S.qy = rp[5] * inv; S.qz = rp[6] * inv;
         }
         if (fl & 2u) {
             // world velocities of the base origin -> body-frame twist
             const M3 R = quat_to_R(S.qw, S.qx, S.qy, S.qz);
-            const f3 lin = {D.rvel[0 * W + w], D.rvel[1 * W + w], D.rvel[2 * W + w]};
-            const f3 ang = {D.rvel[3 * W + w], D.rvel[4 * W + w], D.rvel[5 * W + w]};
+            const f3 lin = {rv[0], rv[1], rv[2]};
+            const f3 ang = {rv[3], rv[4], rv[5]};
             S.V = {mulT(R, ang), mulT(R, lin)};
         }
         if (fl) D.rflag[w] = 0;
@@ -595,18 +601,32 @@ __global__ void __launch_bounds__(64) float_run_kernel(const ChainF* __restrict_
 // Large articulated models on a floating base, one world per wavefront
 // (wave_tree.hpp).  Same run semantics as float_run_kernel; the PID gains
 // come from a device array (any dof count).  blockIdx.x = world.
+// The first substep's PID inputs of dof d, loaded with the kernel's prologue
+// (the wave kernel: otherwise the PID phase waits on them, two dependent
+// round trips after the prologue's own).
+struct PidPre {
+    float effort, u, tgt, e, i;
+    PidF g;
+};
+
+__device__ __forceinline__ PidPre pid_preload(const ChainF* __restrict__ P, const SimDev& S,
+                                              const PidF* __restrict__ pid, int W, int w, int d) {
+    const size_t k = static_cast<size_t>(d) * W + w;
+    return PidPre{P->b[d].effort, S.pid_u[k], S.ptgt[k], S.pid_e[k], S.pid_i[k], pid[d]};
+}
+
 __device__ __forceinline__ float dof_force(const ChainF* __restrict__ P, const SimDev& S, const PidF* __restrict__ pid,
                                            int W, int w, const RunArgs& A, int s, int d, uint32_t act, float cmd,
-                                           float vc, float q, float qd) {
-    const float e = P->b[d].effort;
+                                           float vc, float q, float qd, const PidPre* pre = nullptr) {
+    const float e = pre ? pre->effort : P->b[d].effort;
     float tau = (act == kActForce && s == 0) ? fminf(fmaxf(cmd, -e), e) : 0.f;
     if (act >= kActPidPos) {
         const size_t k = static_cast<size_t>(d) * W + w;
-        float u = S.pid_u[k];
+        float u = pre ? pre->u : S.pid_u[k];
         if ((A.pid_gate >> s) & 1u) {
-            const float err = (act == kActPidPos) ? (q - S.ptgt[k]) : (qd - vc);
-            float el = S.pid_e[k], ie = S.pid_i[k];
-            if (pid_update(pid[d], err, A.inv_dt, A.dt, el, ie, u)) {
+            const float err = (act == kActPidPos) ? (q - (pre ? pre->tgt : S.ptgt[k])) : (qd - vc);
+            float el = pre ? pre->e : S.pid_e[k], ie = pre ? pre->i : S.pid_i[k];
+            if (pid_update(pre ? pre->g : pid[d], err, A.inv_dt, A.dt, el, ie, u)) {
                 S.pid_e[k] = el; S.pid_i[k] = ie; S.pid_u[k] = u;
             } else {
                 u = 0.f;
@@ -631,35 +651,58 @@ template <int MAXN, bool CONS>
 __global__ void __launch_bounds__(64, MW_WAVE_OCC) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
                                                       int N, SimDev S, FreeDev D, const PidF* __restrict__ pid,
                                                       int W, RunArgs A, int want_contacts, int* __restrict__ overflow) {
+    MW_PROF_T(tk0);
     const int w = xcd_block();  // XCD-aware (xcd.hpp): neighbouring worlds share state lines
     const int lane = lane_id();
     __shared__ WaveWorld<MAXN> L;
-    // warm start: a world whose base or joints were reset starts cold
-    bool warm_reset = A.first && D.rflag[w] != 0;
+    // Every load of the prologue is issued before any is used: the reset flags
+    // used to gate the warm-record and reset-value loads, two dependent round
+    // trips (the prologue measured 11.1k cycles per launch, profiles/r05y)
+    constexpr int kXwPerLane = (kWaveWarmRecord + kWaveLanes - 1) / kWaveLanes;
+    float xwv[kXwPerLane];
     if (A.warm) {
-        if (A.first && lane < N) warm_reset = warm_reset || S.rflag[static_cast<size_t>(lane) * W + w] != 0;
-        warm_reset = __ballot(warm_reset) != 0;
-        for (int e = lane; e < kWaveWarmRecord; e += kWaveLanes)
-            L.xw[e] = warm_reset ? 0.f : D.warm[static_cast<size_t>(e) * W + w];
-    }
-    FreeState base = load_base(D, W, w, A.first);
-    uint32_t act = 0u;
-    float cmd = 0.f, vc = 0.f;
-    if (lane < N) {
-        const size_t k = static_cast<size_t>(lane) * W + w;
-        float q = S.q[k], qd = S.qd[k];
-        if (A.first) {
-            const uint8_t f = S.rflag[k];
-            if (f) {
-                if (f & 2u) qd = S.rqd[k];
-                if (f & 1u) q = S.rq[k];
-                if (f & 4u) { S.pid_e[k] = 0.f; S.pid_i[k] = 0.f; S.pid_u[k] = 0.f; }
-                S.rflag[k] = 0;
-            }
+#pragma unroll
+        for (int j = 0; j < kXwPerLane; ++j) {
+            const int e = lane + j * kWaveLanes;
+            xwv[j] = (e < kWaveWarmRecord) ? D.warm[static_cast<size_t>(e) * W + w] : 0.f;
         }
-        act = S.act[k];
-        vc = S.vtgt[k];
-        cmd = A.first ? S.cmd[k] : 0.f;
+    }
+    const bool base_reset = A.first && D.rflag[w] != 0;
+    uint32_t act = 0u;
+    float cmd = 0.f, vc = 0.f, q = 0.f, qd = 0.f, rq = 0.f, rqd = 0.f;
+    uint8_t jflag = 0;
+    const size_t kq = static_cast<size_t>(lane) * W + w;
+    if (lane < N) {
+        q = S.q[kq];
+        qd = S.qd[kq];
+        if (A.first) {
+            jflag = S.rflag[kq];
+            rq = S.rq[kq];
+            rqd = S.rqd[kq];
+            cmd = S.cmd[kq];
+        }
+        act = S.act[kq];
+        vc = S.vtgt[kq];
+    }
+    PidPre pre0 = {};
+    if (lane < N) pre0 = pid_preload(P, S, pid, W, w, lane);
+    FreeState base = load_base(D, W, w, A.first);
+    // warm start: a world whose base or joints were reset starts cold
+    if (A.warm) {
+        const bool warm_reset = __ballot(base_reset || jflag != 0) != 0;
+#pragma unroll
+        for (int j = 0; j < kXwPerLane; ++j) {
+            const int e = lane + j * kWaveLanes;
+            if (e < kWaveWarmRecord) L.xw[e] = warm_reset ? 0.f : xwv[j];
+        }
+    }
+    if (lane < N) {
+        if (jflag) {
+            if (jflag & 2u) qd = rqd;
+            if (jflag & 1u) q = rq;
+            if (jflag & 4u) { S.pid_e[kq] = 0.f; S.pid_i[kq] = 0.f; S.pid_u[kq] = 0.f; }
+            S.rflag[kq] = 0;
+        }
         L.q[lane] = q;
         L.qd[lane] = qd;
         L.act[lane] = act;
@@ -673,11 +716,24 @@ __global__ void __launch_bounds__(64, MW_WAVE_OCC) wave_run_kernel(const ChainF*
 #pragma unroll
         for (int e = 0; e < 6; ++e) L.ext[lane][e] = D.wrench[(static_cast<size_t>(e) * D.wnodes + lane) * W + w];
     }
+#ifdef MW_WAVE_PROF
+    {
+        // the prologue's loads have landed once the first substep reads them
+        // (q / qd through LDS): time to here is issue + the first waits
+        wave_lds_sync();
+        MW_PROF_T(tk1);
+        MW_PROF_ACC(20, tk0, tk1);
+    }
+#endif
+    // the first substep's joint forces from the preloaded PID inputs (pre0
+    // dies here instead of living through the substep loop)
+    float tau0 = 0.f;
+    if (!A.paused && lane < N) tau0 = dof_force(P, S, pid, W, w, A, 0, lane, act, cmd, vc, q, qd, &pre0);
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
             MW_PROF_T(ta);
             if (lane < N)
-                L.tau[lane] = dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
+                L.tau[lane] = (s == 0) ? tau0 : dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
             MW_PROF_T(tb);
             MW_PROF_ACC(0, ta, tb);
 #if MW_WAVE_CRBA

@@ -752,8 +752,11 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 cn = to_parent(R, p, downdate(AIn, Un, psin));
             }
         }
+        // the level's own fan-out (sibling ranks are contiguous from 0; as wave_aba)
         for (int k = 0; k < fanout; ++k) {
-            if (mine && srank == k) {
+            const bool me = mine && srank == k;
+            if (__ballot(me) == 0ull) break;
+            if (me) {
                 WaveAcc& acc = L.acc[pnode];
                 SI I = acc.I;
                 I += c;
@@ -1354,10 +1357,12 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         const size_t k = static_cast<size_t>(lane) * W + w;
         float q = D.q[k], qd = D.qd[k];
         if (A.first) {
+            // reset values load with their flag (one round trip, as the wave kernel)
             const uint8_t f = D.rflag[k];
+            const float rq = D.rq[k], rqd = D.rqd[k];
             if (f) {
-                if (f & 2u) qd = D.rqd[k];
-                if (f & 1u) q = D.rq[k];
+                if (f & 2u) qd = rqd;
+                if (f & 1u) q = rq;
                 if (f & 4u) { D.pid_e[k] = 0.f; D.pid_i[k] = 0.f; D.pid_u[k] = 0.f; }
                 D.rflag[k] = 0;
             }
@@ -1381,17 +1386,19 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         if (A.first) {
             const size_t fk = static_cast<size_t>(bm) * W + w;
             const uint8_t fl = D.bflag[fk];
+            float rp[7], rv[6];
+#pragma unroll
+            for (int f = 0; f < 7; ++f) rp[f] = D.rpose[static_cast<size_t>(7 * bm + f) * W + w];
+#pragma unroll
+            for (int f = 0; f < 6; ++f) rv[f] = D.rvel[static_cast<size_t>(6 * bm + f) * W + w];
             if (fl & 1u) {
-                auto rp = [&](int f) -> float { return D.rpose[static_cast<size_t>(7 * bm + f) * W + w]; };
-                base.p = {rp(0), rp(1), rp(2)};
-                const float qw = rp(3), qx = rp(4), qy = rp(5), qz = rp(6);
-                const float inv = 1.f / sqrtf(qw * qw + qx * qx + qy * qy + qz * qz);
-                base.qw = qw * inv; base.qx = qx * inv; base.qy = qy * inv; base.qz = qz * inv;
+                base.p = {rp[0], rp[1], rp[2]};
+                const float inv = 1.f / sqrtf(rp[3] * rp[3] + rp[4] * rp[4] + rp[5] * rp[5] + rp[6] * rp[6]);
+                base.qw = rp[3] * inv; base.qx = rp[4] * inv; base.qy = rp[5] * inv; base.qz = rp[6] * inv;
             }
             if (fl & 2u) {
-                auto rv = [&](int f) -> float { return D.rvel[static_cast<size_t>(6 * bm + f) * W + w]; };
                 const M3 Rq = quat_to_R(base.qw, base.qx, base.qy, base.qz);
-                base.V = {mulT(Rq, mk(rv(3), rv(4), rv(5))), mulT(Rq, mk(rv(0), rv(1), rv(2)))};
+                base.V = {mulT(Rq, mk(rv[3], rv[4], rv[5])), mulT(Rq, mk(rv[0], rv[1], rv[2]))};
             }
             if (fl) D.bflag[fk] = 0;
         }

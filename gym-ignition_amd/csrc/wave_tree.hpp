@@ -61,7 +61,8 @@ struct WaveBody {
     M3 Rw;       // world pose (contact detection)
     f3 pw;
     int32_t depth;
-    float pad_[2];
+    int32_t parent;  // the responses' outward walk reads it here (no model-block load per body)
+    float pad_;
     f3 ax;       // joint axis (child frame) and type: the lane-varying walks read
     int32_t jt;  // them here instead of from the model block in global memory
 };
@@ -140,10 +141,12 @@ __device__ __forceinline__ int lane_id() {
 
 // Phase timing (debug builds only: EXTRA=-DMW_WAVE_PROF, scripts/wave_prof.py):
 // shader-clock cycles per phase, summed over the worlds of a launch.
-constexpr int kWaveProfPhases = 20;  // [8] exact-LCP linear solves, [9] its rounds, [10] stage-2 solves,
+constexpr int kWaveProfPhases = 22;  // [8] exact-LCP linear solves, [9] its rounds, [10] stage-2 solves,
                                      // [11] / [12] max solves / stage-2 solves of a world-step, [13] world-steps > 4 solves,
                                      // [14] cycles in the linear solves, [15] in the PGS sweeps / the exact solve,
-                                     // [16] in the exact solve's per-stage sweeps, [17] in its stage 1
+                                     // [16] in the exact solve's per-stage sweeps, [17] in its stage 1,
+                                     // [18] / [19] ABA pass 1 / inward, [20] the kernel's prologue (entry
+                                     // to the first substep: state and warm-record loads)
 #ifdef MW_WAVE_PROF
 __device__ unsigned long long g_wave_prof[kWaveProfPhases];
 // up to kDumpSlots hard exact LCPs (world-steps with >= 8 linear solves, or
@@ -228,6 +231,7 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         Sq = motion(b, L.qd[i]);
         L.body[i].ax = mk(b.axis[0], b.axis[1], b.axis[2]);
         L.body[i].jt = b.jtype;
+        L.body[i].parent = pa;
     }
     // outward: velocities and world poses, the only parent chain, level by level
     for (int d = 0; d < levels; ++d) {
@@ -305,8 +309,13 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
         // children add into the parent's accumulator one sibling rank at a
         // time, highest body index first (a parent gathering its children's
         // slots instead measured slower: profiles/r05b)
+        // (sibling ranks at one level are contiguous from 0: the rounds stop
+        // at the level's own fan-out instead of the model's -- most levels of
+        // a humanoid are chains, one round instead of five)
         for (int k = 0; k < fanout; ++k) {
-            if (mine && srank == k) {
+            const bool me = mine && srank == k;
+            if (__ballot(me) == 0ull) break;
+            if (me) {
                 WaveAcc& acc = L.acc[slot];
                 SI I = acc.I;
                 I += c;
@@ -406,10 +415,10 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
     MJrow[0] = dV0.w.x; MJrow[1] = dV0.w.y; MJrow[2] = dV0.w.z;
     MJrow[3] = dV0.v.x; MJrow[4] = dV0.v.y; MJrow[5] = dV0.v.z;
     SV dv_prev = dV0;
+    (void)P;
     for (int i = 0; i < N; ++i) {
-        const BodyF& b = P->b[i];
         const WaveBody& s = L.body[i];
-        const int pa = b.parent;
+        const int pa = s.parent;
         SV dvp_in;
         if (pa == i - 1) {
             dvp_in = dv_prev;  // the previous body (or the base for i = 0)
@@ -424,7 +433,7 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
         const float u = ((path >> i) & 1u) ? L.stack[s.depth][6][lane] : 0.f;
         const float mm = s.psi * (u - dot(s.U, dvp));
         MJrow[6 + i] = mm;
-        const SV dv = dvp + motion(b, mm);
+        const SV dv = dvp + motion_rec(s, mm);
         dv_prev = dv;
         float* st = &L.stack[s.depth][0][lane];
         st[0 * kWaveLanes] = dv.w.x; st[1 * kWaveLanes] = dv.w.y; st[2 * kWaveLanes] = dv.w.z;

@@ -42,7 +42,7 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "scene3":
     sc.run_device(100)
     fn = N.lib().mw_debug_scene_prof
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-    buf = (ctypes.c_ulonglong * 20)()
+    buf = (ctypes.c_ulonglong * 22)()
     fn(buf)
     t0 = time.perf_counter()
     for _ in range(T):
@@ -71,7 +71,7 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
     L = N.lib()
     fn = L.mw_debug_wave_prof
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-    buf = (ctypes.c_ulonglong * 20)()
+    buf = (ctypes.c_ulonglong * 22)()
     fn(buf)
     t0 = time.perf_counter()
     sim.run_device(T)
@@ -108,7 +108,7 @@ sim.run_device(50)
 L = N.lib()
 fn = L.mw_debug_wave_prof
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 20)()
+buf = (ctypes.c_ulonglong * 22)()
 fn(buf)  # clear
 t0 = time.perf_counter()
 sim.run_device(T)
@@ -127,5 +127,7 @@ print(f"  exact LCP: {buf[8] / W / T:.2f} linear solves and {buf[9] / W / T:.2f}
 if buf[18] or buf[19]:
     print(f"  inside the first phase: [18] {buf[18] / W / T:.0f}, [19] {buf[19] / W / T:.0f} cycles/world-step "
           f"(ABA: outward pass 1, inward pass; joint-space step: tree passes + CRBA, factorisation + free solve)")
+if buf[20]:
+    print(f"  kernel prologue (entry to the first substep): {buf[20] / W / T:.0f} cycles/world-launch")
 save_dumps(L.mw_debug_wave_dump, 9, "wave_dump.npz")
 sim.close()
