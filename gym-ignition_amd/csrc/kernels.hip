@@ -1036,10 +1036,12 @@ extern "C" int mw_debug_wave_prof(unsigned long long* out) {
 }
 #endif
 
-hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const FloatF* F, const SimDev& S, const FreeDev& D,
-                           const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow, hipStream_t st) {
+hipError_t launch_wave_run(const ChainF* P, int n, int depth, bool cons, const FloatF* F, const SimDev& S,
+                           const FreeDev& D, const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow,
+                           hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(W)), block(dev::kWaveLanes);
-    if (n <= 16) {
+    if (depth > dev::kWaveMaxDepth) return hipErrorInvalidValue;
+    if (n <= 16 && depth <= dev::WaveWorld<16>::kDepth) {
         if (cons)
             hipLaunchKernelGGL((dev::wave_run_kernel<16, true>), grid, block, 0, st, P, F, n, S, D, pid, W, a,
                                contacts, overflow);

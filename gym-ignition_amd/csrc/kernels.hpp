@@ -121,7 +121,8 @@ hipError_t launch_float_run(const ChainF* P, int n, int topo, bool cons, const s
 // Large floating-base trees, one world per wavefront (wave_tree.hpp): any
 // topology of <= kMaxBodies bodies and depth <= 12; pid: n PidF in device
 // memory; overflow: device counter of constraint rows dropped (> 64 per step).
-hipError_t launch_wave_run(const ChainF* P, int n, bool cons, const struct FloatF* F, const SimDev& S,
+// depth: the tree's depth in joints (the <= 16-body instance takes <= 10)
+hipError_t launch_wave_run(const ChainF* P, int n, int depth, bool cons, const struct FloatF* F, const SimDev& S,
                            const FreeDev& D, const PidF* pid, int W, const RunArgs& a, int contacts, int* overflow,
                            hipStream_t st);
 constexpr int kWaveMaxDepthHost = 12;

@@ -135,6 +135,7 @@ struct mw_sim {
     // large trees (or MWSTEP_WAVE_TREE=1): one world per wavefront (wave_tree.hpp)
     bool wave = false;
     bool wave_depth_ok = false;   // the tree fits the wave kernel's depth stack
+    int wave_depth = 0;           // the tree's depth in joints (picks the wave kernel's instance)
     mw::PidF* d_pid = nullptr;    // PID gains of every dof (device)
     mw::PidF* h_pid = nullptr;    // pinned staging copy
     bool pid_dirty = true;        // gains changed since the last upload
@@ -735,6 +736,7 @@ int mw_load_model(mw_sim* s, const char* urdf, const double pose[7], const char*
                 max_depth = std::max(max_depth, depth[i] + 1);
             }
             s->wave_depth_ok = max_depth <= mw::kWaveMaxDepthHost;
+            s->wave_depth = max_depth;
             if (s->wave && !s->wave_depth_ok)
                 return fail(MW_EPARSE, "the kinematic tree of this model is deeper than " +
                                            std::to_string(mw::kWaveMaxDepthHost) + " joints");
@@ -1188,7 +1190,7 @@ static int run_impl(mw_sim* s, int paused, bool readback) {
             }
         }
         if (s->wave)
-            MW_HIP(mw::launch_wave_run(s->d_params, s->n, needs_cons(s), s->d_float, s->dev, s->fdev, s->d_pid, s->W,
+            MW_HIP(mw::launch_wave_run(s->d_params, s->n, s->wave_depth, needs_cons(s), s->d_float, s->dev, s->fdev, s->d_pid, s->W,
                                        a, s->contacts ? 1 : 0, s->d_overflow, s->stream));
         else if (s->float_tree)
             MW_HIP(mw::launch_float_run(s->d_params, s->n, s->topo, needs_cons(s), s->d_float, s->dev, s->fdev, pid,

@@ -79,6 +79,20 @@ __device__ __forceinline__ float proj_rec(const WaveBody& s, const SV& x) {
     return ((s.jt & 1) == 0) ? dw : dv;
 }
 
+// component-wise selects (a select between two records is lowered to a
+// scratch round trip; a conditional record load to an exec-masked read that
+// is waited on at once)
+__device__ __forceinline__ f3 sel3(bool c, const f3& a, const f3& b) {
+    return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
+__device__ __forceinline__ SV selv(bool c, const SV& a, const SV& b) { return {sel3(c, a.w, b.w), sel3(c, a.v, b.v)}; }
+__device__ __forceinline__ M3 selm(bool c, const M3& a, const M3& b) {
+    M3 r;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.m[k] = c ? a.m[k] : b.m[k];
+    return r;
+}
+
 // child -> parent accumulator of the inward pass (48 words, float4-aligned):
 // articulated inertia with DART's implicit joint damping, bias, and the
 // non-implicit articulated inertia (models with damping: impulses propagate
@@ -94,16 +108,24 @@ template <int MAXN>
 struct WaveWorld {
     static constexpr int kNv = 6 + MAXN;
     static constexpr int kRowStride = kNv | 1;  // odd: lane-strided row access is conflict-free
+    // odd like MJ: the response pass writes, and the Delassus tiles read, one
+    // row per lane (a stride of 24/40/56 put 8 lanes on each bank)
+    static constexpr int kJStride = kNv | 1;
+    // the response stack's depth: the <= 16-body instance takes trees of
+    // depth <= 10 (the host routes deeper ones to the 32-body instance), so
+    // that its world record fits 4 waves per CU (LDS <= 40 KiB)
+    static constexpr int kDepth = (MAXN <= 16) ? 10 : kWaveMaxDepth;
     WaveBody body[MAXN];
-    WaveAcc acc[MAXN + 1];       // [MAXN] = the base
+    // the inward ABA's accumulators are dead once the base solve has read
+    // them; J is written from the response pass on: one LDS region
+    union {
+        WaveAcc acc[MAXN + 1];   // [MAXN] = the base
+        alignas(16) float J[kWaveMaxRows][kJStride];
+    };
     float q[MAXN], qd[MAXN], qdd[MAXN], tau[MAXN], vc[MAXN];
     uint32_t act[MAXN];
     float ext[MAXN + 1][6];      // this substep's world wrenches: [0] the base, [1 + i] body i (f, tau)
     float nu[kNv];
-    // odd like MJ: the response pass writes, and the Delassus tiles read, one
-    // row per lane (a stride of 24/40/56 put 8 lanes on each bank)
-    static constexpr int kJStride = kNv | 1;
-    alignas(16) float J[kWaveMaxRows][kJStride];
     float MJ[kWaveMaxRows][kRowStride];
     float b[kWaveMaxRows], lo[kWaveMaxRows], hi[kWaveMaxRows];
     F4 rc[kWaveMaxRows];         // PGS row constants {b, 1/A_rr, lo, hi}
@@ -115,12 +137,14 @@ struct WaveWorld {
     float s_R[kMaxFloatSlots][9];   // body rotation
     float s_x[kMaxFloatSlots][3];   // impulses (output)
     // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
-    alignas(16) float stack[kWaveMaxDepth][7][kWaveLanes];
+    alignas(16) float stack[kDepth][7][kWaveLanes];
     float xw[kWaveWarmRecord];   // warm-start impulses (RunArgs::warm): final, then stage 1
+#if defined(MW_WAVE_CRBA) && MW_WAVE_CRBA
     // joint-space step (wave_crba.hpp): generalized forces and 1/sqrt(d) of
     // the factorisation, reversed dof order
     float gen[kNv + 2];
     float dsq[64];
+#endif
 };
 
 // The lane index through a volatile asm: every call is a fresh value, so the
@@ -236,9 +260,12 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     // outward: velocities and world poses, the only parent chain, level by level
     for (int d = 0; d < levels; ++d) {
         if (depth == d) {
-            const SV Vp = (pa >= 0) ? L.body[pa].V : V0;
-            const M3 Rwp = (pa >= 0) ? L.body[pa].Rw : R0;
-            const f3 pwp = (pa >= 0) ? L.body[pa].pw : p0;
+            // the parent's record loads unconditionally (the base: record 0, unused)
+            const bool hp = pa >= 0;
+            const int pai = hp ? pa : 0;
+            const SV Vp = selv(hp, L.body[pai].V, V0);
+            const M3 Rwp = selm(hp, L.body[pai].Rw, R0);
+            const f3 pwp = sel3(hp, L.body[pai].pw, p0);
             V = ad_inv(R, p, Vp) + Sq;
 #pragma unroll
             for (int r = 0; r < 3; ++r)
@@ -355,7 +382,7 @@ __device__ __forceinline__ SV wave_aba(const ChainF* __restrict__ P, const Float
     // outward: accelerations (the V record now carries a)
     for (int d = 0; d < levels; ++d) {
         if (depth == d) {
-            const SV ap = ad_inv(R, p, (pa >= 0) ? L.body[pa].V : a0);
+            const SV ap = ad_inv(R, p, selv(pa >= 0, L.body[(pa >= 0) ? pa : 0].V, a0));
             const float qdd = psi * (tt - dot(U, ap));
             L.body[i].V = ap + eta + motion(b, qdd);
             qdd_out[i] = qdd;
@@ -430,6 +457,8 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
             dvp_in = dV0;
         }
         const SV dvp = ad_inv(s.R, s.p, dvp_in);
+        // (an unconditional read here, a select instead of the masked read,
+        // measured slower: 32.4k -> 34.5k cycles, profiles/r05ad)
         const float u = ((path >> i) & 1u) ? L.stack[s.depth][6][lane] : 0.f;
         const float mm = s.psi * (u - dot(s.U, dvp));
         MJrow[6 + i] = mm;
@@ -710,25 +739,53 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
         // columns >= NV: J is zero there, MJ masked.  Chunks of 8 coordinates
         // (4 k-steps) end at the world's own NV (a uniform branch), so a
         // floating box (NV 6) in a MAXN-16 instance runs 4 k-steps, not 11.
+        // The chunk's operands load unconditionally (MJ columns >= NV are
+        // in-bounds stale LDS, masked by a select after the load): written as
+        // `ev ? MJ[..] : 0` the load itself was conditional, an exec-masked
+        // ds_read waited on right before each MFMA, one LDS round trip per
+        // k-step.  `two` (R > 32) selects one of two loops outside.
         constexpr int kKs = (WaveWorld<MAXN>::kNv + 1) / 2;
+        if (!two) {
 #pragma unroll
-        for (int k0 = 0; k0 < kKs; k0 += 4) {
-            if (2 * k0 >= NV) break;
+            for (int k0 = 0; k0 < kKs; k0 += 4) {
+                if (2 * k0 >= NV) break;
+                float jv[4], mv[4];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const int k = k0 + kk;
-                if (k >= kKs) break;
-                const int e = 2 * k + lh;
-                const bool ev = e < NV;
-                const float j0 = L.J[lr][e];
-                const float m0 = ev ? L.MJ[lr][e] : 0.f;
-                t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m0, t00, 0, 0, 0);
-                if (two) {
-                    const float j1 = L.J[32 + lr][e];
-                    const float m1 = ev ? L.MJ[32 + lr][e] : 0.f;
-                    t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(j0, m1, t01, 0, 0, 0);
-                    t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m0, t10, 0, 0, 0);
-                    t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(j1, m1, t11, 0, 0, 0);
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int e = 2 * (k0 + kk) + lh;
+                    jv[kk] = (k0 + kk < kKs) ? L.J[lr][e] : 0.f;
+                    mv[kk] = (k0 + kk < kKs) ? L.MJ[lr][e] : 0.f;
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    if (k0 + kk >= kKs) break;
+                    const bool ev = 2 * (k0 + kk) + lh < NV;
+                    t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv[kk], ev ? mv[kk] : 0.f, t00, 0, 0, 0);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k0 = 0; k0 < kKs; k0 += 4) {
+                if (2 * k0 >= NV) break;
+                float jv0[4], mv0[4], jv1[4], mv1[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int e = 2 * (k0 + kk) + lh;
+                    const bool in = k0 + kk < kKs;
+                    jv0[kk] = in ? L.J[lr][e] : 0.f;
+                    mv0[kk] = in ? L.MJ[lr][e] : 0.f;
+                    jv1[kk] = in ? L.J[32 + lr][e] : 0.f;
+                    mv1[kk] = in ? L.MJ[32 + lr][e] : 0.f;
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    if (k0 + kk >= kKs) break;
+                    const bool ev = 2 * (k0 + kk) + lh < NV;
+                    const float m0 = ev ? mv0[kk] : 0.f, m1 = ev ? mv1[kk] : 0.f;
+                    t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv0[kk], m0, t00, 0, 0, 0);
+                    t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv0[kk], m1, t01, 0, 0, 0);
+                    t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv1[kk], m0, t10, 0, 0, 0);
+                    t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv1[kk], m1, t11, 0, 0, 0);
                 }
             }
         }

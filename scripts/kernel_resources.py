@@ -1,4 +1,4 @@
-"""Per-kernel VGPR / scratch / occupancy of kernels.hip (hipcc
+"""Per-kernel VGPR / scratch / occupancy / LDS of kernels.hip (hipcc
 -Rpass-analysis=kernel-resource-usage), as a table.  CPU only."""
 import os
 import re
@@ -19,7 +19,8 @@ for line in out.splitlines():
         cur = {"name": m.group(1)}
         rows.append(cur)
         continue
-    for key in ("VGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "SGPRs Spill", "VGPRs Spill"):
+    for key in ("VGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "SGPRs Spill", "VGPRs Spill",
+                "LDS Size [bytes/block]"):
         m = re.search(re.escape(key) + r": (\d+)", line)
         if m and cur is not None:
             cur[key] = int(m.group(1))
@@ -27,6 +28,7 @@ bad = 0
 for r in rows:
     name = re.sub(r"^_ZN2mw3dev\d+", "", r["name"])[:60]
     print(f"{name:62s} vgpr={r.get('VGPRs'):4} scratch={r.get('ScratchSize [bytes/lane]'):4} "
-          f"occ={r.get('Occupancy [waves/SIMD]')} sgpr_spill={r.get('SGPRs Spill')} vgpr_spill={r.get('VGPRs Spill')}")
+          f"occ={r.get('Occupancy [waves/SIMD]')} sgpr_spill={r.get('SGPRs Spill')} vgpr_spill={r.get('VGPRs Spill')} "
+          f"lds={r.get('LDS Size [bytes/block]')}")
     bad += (r.get("ScratchSize [bytes/lane]", 0) > 0)
 sys.exit(1 if bad else 0)
