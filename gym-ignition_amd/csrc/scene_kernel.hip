@@ -655,6 +655,8 @@ __device__ void sc_nancheck(const SceneF* __restrict__ P, const ScWorld<MAXNV>& 
 #endif
 
 // ------------------------------------------------------------------- step
+// (a real call, not inlined: __forceinline__ took scratch 944 -> 768 B per
+// lane but the scene leg 0.909 -> 0.976 ms, profiles/r05ag)
 template <int MAXNV>
 __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeState& base, uint32_t present,
                         const float (&wr)[kScWrenchSlots][6], const int32_t (&wl)[kScWrenchSlots], int iter,
