@@ -423,6 +423,9 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
     SV Bi = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Fi = Bi;
     if (k >= 0 || (k < 0 && j < 0)) { Bi = -1.f * f; Fi = f; }
     float jv = 0.f;
+    // (unrolled by 2 like the outward walk below: the next path body's record
+    // gathers are independent of this body's transform chain)
+#pragma unroll 2
     for (uint64_t m = path; m != 0;) {
         const int i = 63 - __builtin_clzll(m);
         m &= ~(uint64_t{1} << i);
@@ -443,6 +446,9 @@ __device__ __forceinline__ float wave_response(const ChainF* __restrict__ P, con
     MJrow[3] = dV0.v.x; MJrow[4] = dV0.v.y; MJrow[5] = dV0.v.z;
     SV dv_prev = dV0;
     (void)P;
+    // unrolled by 4: the next bodies' LDS records load while this one's
+    // transform runs (the loop waited on each record's broadcast reads)
+#pragma unroll 4
     for (int i = 0; i < N; ++i) {
         const WaveBody& s = L.body[i];
         const int pa = s.parent;
