@@ -70,7 +70,9 @@ constexpr float kLcpFloorAccept = 64.f;
 // (A/B on the legs, gpurun_out r05d: humanoid_c5 131.8 -> 109.2 us with the
 // 32-row tile, the scene 1.74 -> 1.10 ms with the 64-row tiles; the 64-row
 // tiles in the wave kernels and any tile in the <= 16-body instance made
-// their legs slower through the spills)
+// their legs slower through the spills; once the wave kernels ran without
+// scratch, every width in the <= 16-body instance measured faster:
+// MW_WAVE_LCP16_MFMA, wave_tree.hpp)
 constexpr int kLcpMfmaNone = 0, kLcpMfma32 = 2, kLcpMfmaAll = 7, kLcpMfma3264 = 6;
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six

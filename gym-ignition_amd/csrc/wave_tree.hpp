@@ -31,6 +31,14 @@
 namespace mw {
 namespace dev {
 
+// matrix-core widths of the <= 16-body instance's exact solve (wave_lcp.hpp
+// kLcpMfma*; A/B builds: EXTRA=-DMW_WAVE_LCP16_MFMA=0).  Every width since
+// the instance runs without scratch: contacts 121.9 -> 115.7 us, quadruped
+// 580 -> 567 us (profiles/r05ak; round 5's first A/B, with spills, had it
+// slower)
+#ifndef MW_WAVE_LCP16_MFMA
+#define MW_WAVE_LCP16_MFMA 7
+#endif
 constexpr int kWaveLanes = 64;
 constexpr int kWaveMaxRows = 64;
 constexpr int kWaveMaxDepth = 12;
@@ -889,7 +897,8 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 #endif
             // the matrix-core solves this instance takes (wave_lcp.hpp: the
             // <= 16-body instance and the 64-row width eliminate over the lanes)
-            constexpr int kWaveLcpMfma = (!MW_LCP_MFMA || MAXN <= 16) ? kLcpMfmaNone : kLcpMfma32;
+            constexpr int kWaveLcpMfma =
+                !MW_LCP_MFMA ? kLcpMfmaNone : ((MAXN <= 16) ? MW_WAVE_LCP16_MFMA : kLcpMfma32);
             // three register widths (wave_lcp.hpp: the elimination runs the
             // whole register row): a free body's 4-corner LCP (12 rows) on 16
             // columns took contacts_floating 195 -> 167 us (gpurun_out r04z)
