@@ -39,6 +39,11 @@ namespace dev {
 #ifndef MW_WAVE_LCP16_MFMA
 #define MW_WAVE_LCP16_MFMA 7
 #endif
+// ... and of the larger instances (default: the 17-32-row width only; every
+// width measured the same on the humanoid, profiles/r05am)
+#ifndef MW_WAVE_LCP32_MFMA
+#define MW_WAVE_LCP32_MFMA 2
+#endif
 constexpr int kWaveLanes = 64;
 constexpr int kWaveMaxRows = 64;
 constexpr int kWaveMaxDepth = 12;
@@ -898,7 +903,7 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             // the matrix-core solves this instance takes (wave_lcp.hpp: the
             // <= 16-body instance and the 64-row width eliminate over the lanes)
             constexpr int kWaveLcpMfma =
-                !MW_LCP_MFMA ? kLcpMfmaNone : ((MAXN <= 16) ? MW_WAVE_LCP16_MFMA : kLcpMfma32);
+                !MW_LCP_MFMA ? kLcpMfmaNone : ((MAXN <= 16) ? MW_WAVE_LCP16_MFMA : MW_WAVE_LCP32_MFMA);
             // three register widths (wave_lcp.hpp: the elimination runs the
             // whole register row): a free body's 4-corner LCP (12 rows) on 16
             // columns took contacts_floating 195 -> 167 us (gpurun_out r04z)
