@@ -637,18 +637,8 @@ __device__ __forceinline__ float dof_force(const ChainF* __restrict__ P, const S
     return tau;
 }
 
-// the wave kernel's step: 0 = the articulated-body recursions (wave_tree.hpp
-// wave_step, default), 1 = joint space on the matrix cores (wave_crba.hpp: an
-// A/B variant -- measured slower and less accurate)
-#ifndef MW_WAVE_CRBA
-#define MW_WAVE_CRBA 0
-#endif
-
 template <int MAXN, bool CONS>
-#ifndef MW_WAVE_OCC
-#define MW_WAVE_OCC 1  // waves per SIMD the wave kernel is compiled for (A/B builds)
-#endif
-__global__ void __launch_bounds__(64, MW_WAVE_OCC) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
+__global__ void __launch_bounds__(64, 1) wave_run_kernel(const ChainF* __restrict__ P, const FloatF* __restrict__ F,
                                                       int N, SimDev S, FreeDev D, const PidF* __restrict__ pid,
                                                       int W, RunArgs A, int want_contacts, int* __restrict__ overflow) {
     MW_PROF_T(tk0);
@@ -700,7 +690,12 @@ __global__ void __launch_bounds__(64, MW_WAVE_OCC) wave_run_kernel(const ChainF*
         if (jflag) {
             if (jflag & 2u) qd = rqd;
             if (jflag & 1u) q = rq;
-            if (jflag & 4u) { S.pid_e[kq] = 0.f; S.pid_i[kq] = 0.f; S.pid_u[kq] = 0.f; }
+            if (jflag & 4u) {
+                // Joint::resetPosition resets the PID (Joint.cpp:132-180): the
+                // preloaded first-substep inputs must see the reset too
+                S.pid_e[kq] = 0.f; S.pid_i[kq] = 0.f; S.pid_u[kq] = 0.f;
+                pre0.e = 0.f; pre0.i = 0.f; pre0.u = 0.f;
+            }
             S.rflag[kq] = 0;
         }
         L.q[lane] = q;
@@ -736,14 +731,8 @@ __global__ void __launch_bounds__(64, MW_WAVE_OCC) wave_run_kernel(const ChainF*
                 L.tau[lane] = (s == 0) ? tau0 : dof_force(P, S, pid, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
             MW_PROF_T(tb);
             MW_PROF_ACC(0, ta, tb);
-#if MW_WAVE_CRBA
-            // joint space on the matrix cores (wave_crba.hpp)
-            active = wave_step_crba<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0,
-                                                A.lcp_solves, L.qdd, &ovf, &unconv, prof, A.wrenches != 0);
-#else
             active = wave_step<MAXN, CONS>(P, F, N, base, L, A.dt, A.pgs_iters, A.pgs_tol, A.warm != 0,
                                            A.lcp_solves, L.qdd, &ovf, &unconv, prof, A.wrenches != 0);
-#endif
             MW_PROF_T(tc);
             MW_PROF_ACC(7, ta, tc);
         }
@@ -1178,7 +1167,7 @@ hipError_t launch_vecenv_step(const ChainF* P, int n, bool cons, bool dual, int 
 }  // namespace mw
 
 // ---- test hook: one linear solve of the exact LCP's active-set method -------
-// (include/mwstep.h mw_debug_lcp_solve; tests/test_gpu_lcp_solve.py checks both
+// (include/mwstep_testhooks.h mw_debug_lcp_solve; tests/test_gpu_lcp_solve.py checks both
 // paths against numpy on random SPD systems with held rows)
 namespace mw {
 namespace dev {
@@ -1207,24 +1196,31 @@ __global__ void __launch_bounds__(64) debug_lcp_solve_kernel(const float* __rest
 
 extern "C" int mw_debug_lcp_solve(const float* A, const float* rhs, uint64_t free_mask, int32_t n, int32_t method,
                                   float* d) {
+    // include/mwstep_testhooks.h: a test hook, not for a running simulator --
+    // its own buffers and its own stream, and it waits on that stream only
     if (!A || !rhs || !d || n < 1 || n > mw::dev::kWaveMaxRows || method < 0 || method > 1) return 2;
     float *dA = nullptr, *dr = nullptr, *dd = nullptr;
+    hipStream_t st = nullptr;
     const size_t nn = static_cast<size_t>(n) * n;
     int rc = 1;
-    if (hipMalloc(reinterpret_cast<void**>(&dA), nn * sizeof(float)) == hipSuccess &&
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dA), nn * sizeof(float)) == hipSuccess &&
         hipMalloc(reinterpret_cast<void**>(&dr), 64 * sizeof(float)) == hipSuccess &&
         hipMalloc(reinterpret_cast<void**>(&dd), 64 * sizeof(float)) == hipSuccess &&
-        hipMemcpy(dA, A, nn * sizeof(float), hipMemcpyHostToDevice) == hipSuccess &&
-        hipMemcpy(dr, rhs, n * sizeof(float), hipMemcpyHostToDevice) == hipSuccess) {
+        hipMemcpyAsync(dA, A, nn * sizeof(float), hipMemcpyHostToDevice, st) == hipSuccess &&
+        hipMemcpyAsync(dr, rhs, n * sizeof(float), hipMemcpyHostToDevice, st) == hipSuccess) {
         const uint64_t live = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
-        hipLaunchKernelGGL(mw::dev::debug_lcp_solve_kernel, dim3(1), dim3(64), 0, 0, dA, dr, free_mask & live, n,
+        hipLaunchKernelGGL(mw::dev::debug_lcp_solve_kernel, dim3(1), dim3(64), 0, st, dA, dr, free_mask & live, n,
                            method, dd);
-        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
-            hipMemcpy(d, dd, n * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess)
+        if (hipGetLastError() == hipSuccess &&
+            hipMemcpyAsync(d, dd, n * sizeof(float), hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess)
             rc = 0;
     }
+    if (st) (void)hipStreamSynchronize(st);
     (void)hipFree(dA);
     (void)hipFree(dr);
     (void)hipFree(dd);
+    if (st) (void)hipStreamDestroy(st);
     return rc;
 }

@@ -58,11 +58,6 @@ constexpr float kLcpStall = 1e-7f;
 // at the floor a stage counts as converged when its residual is within this
 // factor of the tolerance
 constexpr float kLcpFloorAccept = 64.f;
-// the active-set method's linear solves: 1 = block LDL^T on the matrix cores
-// (lcp_mfma_solve), 0 = Gaussian elimination over the lanes (lcp_ge_solve)
-#ifndef MW_LCP_MFMA
-#define MW_LCP_MFMA 1
-#endif
 // Which register widths solve on the matrix cores (bit 0: <= 16 rows, bit 1:
 // <= 32, bit 2: <= 64; the rest eliminate over the lanes).  The choice is per
 // kernel: the solve's tiles (16 / 48 accumulators) add to the kernel's peak
@@ -72,8 +67,8 @@ constexpr float kLcpFloorAccept = 64.f;
 // tiles in the wave kernels and any tile in the <= 16-body instance made
 // their legs slower through the spills; once the wave kernels ran without
 // scratch, every width in the <= 16-body instance measured faster:
-// MW_WAVE_LCP16_MFMA, wave_tree.hpp)
-constexpr int kLcpMfmaNone = 0, kLcpMfma32 = 2, kLcpMfmaAll = 7, kLcpMfma3264 = 6;
+// kWaveLcpMfmaSmall, wave_tree.hpp)
+constexpr int kLcpMfma32 = 2, kLcpMfmaAll = 7;
 
 // Wave reductions on DPP (no LDS round trip: a __shfl_xor butterfly is six
 // ds_bpermute): row prefix by row_shr 1/2/4/8, then row_bcast 15 / 31 carry
@@ -477,15 +472,13 @@ __device__ __forceinline__ float mfma_panel(const v16f& T) {
 }
 
 // LS: the column stride of the L record in Lw (column-major, L[row][col] at
-// Lw[col * LS + row]; only rows < LROWS are stored).  dsq (optional): per
-// pivot, 1 / sqrt(d) (the joint-space factorisation's Y scaling).
+// Lw[col * LS + row]; only rows < LROWS are stored).
 template <int RC, int LS = kLcpLStride, int LROWS = 64>
 struct MfmaLdl {
     v16f T00, T01, T11;
     float r, y;
     uint64_t freeM;
     float* Lw;
-    float* dsq = nullptr;
 
     __device__ __forceinline__ void put_l(int row, int col, float v) const {
         if (LROWS >= 64 || row < LROWS) Lw[col * LS + row] = v;
@@ -539,10 +532,6 @@ struct MfmaLdl {
         } else {
             T11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-q, Lm, T11, 0, 0, 0);
             put_l(32 + c, col, Lm);
-        }
-        if (dsq && lane == 0) {
-            dsq[J] = sqrtf(i0);
-            dsq[J + 1] = sqrtf(i1);
         }
         // forward substitution, lane = row, one column after the other
         // (selects, not branches: a divergent branch here made the compiler
@@ -720,7 +709,6 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
 #ifdef MW_WAVE_PROF
         const long long tg0 = clock64();
 #endif
-#if MW_LCP_MFMA
         // block LDL^T on the matrix cores (R <= 32: one tile, else three) for
         // the widths the kernel's MFMA policy selects
         float d;
@@ -733,12 +721,6 @@ __device__ __forceinline__ bool wave_boxqp(const float (&a)[kWaveMaxRows], bool 
         } else {
             d = lcp_mfma_solve<(RC <= 32) ? 32 : 64>(a, fr ? -g : 0.f, freeM, Uw);
         }
-#else
-        float k[RC];
-#pragma unroll
-        for (int c = 0; c < RC; ++c) k[c] = (fr && mask_bit(freeM, c)) ? a[c] : ((!fr && c == lane) ? 1.f : 0.f);
-        const float d = lcp_ge_solve<RC, LongRows>(k, fr ? -g : 0.f, n, Uw, false, freeM);
-#endif
 #ifdef MW_WAVE_PROF
         ge_cycles += clock64() - tg0;
 #else

@@ -31,19 +31,13 @@
 namespace mw {
 namespace dev {
 
-// matrix-core widths of the <= 16-body instance's exact solve (wave_lcp.hpp
-// kLcpMfma*; A/B builds: EXTRA=-DMW_WAVE_LCP16_MFMA=0).  Every width since
-// the instance runs without scratch: contacts 121.9 -> 115.7 us, quadruped
-// 580 -> 567 us (profiles/r05ak; round 5's first A/B, with spills, had it
-// slower)
-#ifndef MW_WAVE_LCP16_MFMA
-#define MW_WAVE_LCP16_MFMA 7
-#endif
-// ... and of the larger instances (default: the 17-32-row width only; every
-// width measured the same on the humanoid, profiles/r05am)
-#ifndef MW_WAVE_LCP32_MFMA
-#define MW_WAVE_LCP32_MFMA 2
-#endif
+// Which register widths of the exact solve take the matrix-core LDL^T
+// (wave_lcp.hpp kLcpMfma*): the <= 16-body instance every width (it runs
+// without scratch: contacts 121.9 -> 115.7 us, quadruped 580 -> 567 us,
+// profiles/r05ak), the larger instances the 17-32-row width only (the 64-row
+// tiles made their legs slower through spills)
+constexpr int kWaveLcpMfmaSmall = 7;  // kLcpMfmaAll
+constexpr int kWaveLcpMfmaLarge = 2;  // kLcpMfma32
 constexpr int kWaveLanes = 64;
 constexpr int kWaveMaxRows = 64;
 constexpr int kWaveMaxDepth = 12;
@@ -152,20 +146,13 @@ struct WaveWorld {
     // per-lane outward stack of the responses: [depth][7][lane] (dv 6, u)
     alignas(16) float stack[kDepth][7][kWaveLanes];
     float xw[kWaveWarmRecord];   // warm-start impulses (RunArgs::warm): final, then stage 1
-#if defined(MW_WAVE_CRBA) && MW_WAVE_CRBA
-    // joint-space step (wave_crba.hpp): generalized forces and 1/sqrt(d) of
-    // the factorisation, reversed dof order
-    float gen[kNv + 2];
-    float dsq[64];
-#endif
 };
 
 // The lane index through a volatile asm: every call is a fresh value, so the
 // lane-dependent constants the phases derive from it (masks, identity
 // patterns, LDS addresses) are formed where they are used instead of being
 // hoisted out of the substep loop by LICM, where hundreds of them stayed live
-// across the whole step and spilled to scratch (the joint-space step:
-// 1408 -> see DESIGN.md bytes per lane).
+// across the whole step and spilled to scratch.
 #if defined(MW_HOST_TEST) || defined(MW_LANE_PLAIN)
 __device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63u); }
 #else
@@ -895,15 +882,10 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             float* U = &L.stack[0][0][0];
             int nsolve = 0, nround = 0, nsolve1 = 0;
             long long cyc[3] = {0, 0, 0};
-#ifdef MW_LCP_FORCE64
-            constexpr int kLcpSmall = 0;   // debug builds: every solve on the 64-row instance
-#else
             constexpr int kLcpSmall = 32;
-#endif
             // the matrix-core solves this instance takes (wave_lcp.hpp: the
             // <= 16-body instance and the 64-row width eliminate over the lanes)
-            constexpr int kWaveLcpMfma =
-                !MW_LCP_MFMA ? kLcpMfmaNone : ((MAXN <= 16) ? MW_WAVE_LCP16_MFMA : MW_WAVE_LCP32_MFMA);
+            constexpr int kWaveLcpMfma = (MAXN <= 16) ? kWaveLcpMfmaSmall : kWaveLcpMfmaLarge;
             // three register widths (wave_lcp.hpp: the elimination runs the
             // whole register row): a free body's 4-corner LCP (12 rows) on 16
             // columns took contacts_floating 195 -> 167 us (gpurun_out r04z)
@@ -1038,4 +1020,3 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
 }  // namespace dev
 }  // namespace mw
 
-#include "wave_crba.hpp"

@@ -145,8 +145,6 @@ SIGNATURES = [
     ("mw_copy_state", ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
     ("mw_diverged", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int64)]),
     ("mw_clear_diverged", ctypes.c_int, [_P, _I, _I]),
-    ("mw_debug_lcp_solve", ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
-                                          ctypes.c_uint64, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mw_state_words", ctypes.c_int, [_P, _IP]),
     ("mw_get_state", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mw_set_state", ctypes.c_int, [_P, _I, _I, ctypes.POINTER(ctypes.c_float)]),
@@ -163,6 +161,12 @@ SIGNATURES = [
 # include/mwscene.h
 SC_POSITION, SC_VELOCITY, SC_ACCELERATION, SC_FORCE_TARGET = 0, 1, 2, 3
 SC_VELOCITY_TARGET, SC_POSITION_TARGET, SC_RESET_POSITION, SC_RESET_VELOCITY, SC_FORCE = 4, 5, 6, 7, 8
+# include/mwstep_testhooks.h: test-only entry points (own buffers and stream)
+TEST_SIGNATURES = [
+    ("mw_debug_lcp_solve", ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                          ctypes.c_uint64, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+]
+
 SCENE_SIGNATURES = [
     ("mw_scene_create", ctypes.c_int, [ctypes.POINTER(MwConfig), ctypes.POINTER(_P)]),
     ("mw_scene_destroy", None, [_P]),
@@ -230,7 +234,7 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} not found: build it with `make -C gym-ignition_amd` "
                 "(hipcc --offload-arch=gfx950); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES + SCENE_SIGNATURES:
+        for name, res, args in SIGNATURES + SCENE_SIGNATURES + TEST_SIGNATURES:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

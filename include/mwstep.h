@@ -404,15 +404,6 @@ int mw_vecenv_counters(mw_vecenv* env, uint32_t* episode_dev, uint32_t* steps_de
  * env was created without randomisation. */
 int mw_vecenv_physics(mw_vecenv* env, float* mass_dev, float* gravity_z_dev);
 
-/* ---- test hook (not part of the ScenarI/O surface) ----
- * One linear solve of the exact LCP's active-set method on a single wavefront
- * (csrc/wave_lcp.hpp): S d = rhs restricted to the rows of free_mask (held
- * rows: d = 0), S = the row-major n x n matrix A (n <= 64, symmetric positive
- * definite on the free rows), host buffers.  method 0: block LDL^T on the
- * matrix cores (lcp_mfma_solve, the kernels' default), 1: Gaussian
- * elimination over the lanes (lcp_ge_solve).  Returns 0 on success. */
-int mw_debug_lcp_solve(const float* A, const float* rhs, uint64_t free_mask, int32_t n, int32_t method, float* d);
-
 #ifdef __cplusplus
 }
 #endif

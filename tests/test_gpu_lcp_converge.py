@@ -43,7 +43,6 @@ def test_scene_leg_converges(bench_mod):
           f"dropped rows {out['dropped_rows']}, cube3 support {out['cube3_support_N_world0']} N")
     assert out["dropped_rows"] == 0
     assert out["lcp_unconverged_world_steps"] == 0
-    assert out["ms_per_step"] <= 1.5
 
 
 @pytest.mark.gpu

@@ -13,6 +13,7 @@ from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "mwstep.h")
 SCENE_HEADER = os.path.join(ROOT, "include", "mwscene.h")
+TEST_HEADER = os.path.join(ROOT, "include", "mwstep_testhooks.h")
 
 
 def _declared_symbols(header=HEADER):
@@ -48,6 +49,17 @@ def test_every_scene_symbol_is_exported(N):
     assert not missing, missing
     bound = {name for name, _, _ in N.SCENE_SIGNATURES}
     assert set(declared) == bound, set(declared) ^ bound
+
+
+def test_every_test_hook_is_exported(N):
+    """include/mwstep_testhooks.h (test-only entry points, kept out of the
+    ScenarI/O header): exported and bound by TEST_SIGNATURES."""
+    L = ctypes.CDLL(N.LIB_PATH)
+    declared = _declared_symbols(TEST_HEADER)
+    assert declared == ["mw_debug_lcp_solve"]
+    assert all(hasattr(L, s) for s in declared)
+    assert set(declared) == {name for name, _, _ in N.TEST_SIGNATURES}
+    assert not set(declared) & set(_declared_symbols())
 
 
 def test_scene_create_validates_arguments(N):
