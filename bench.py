@@ -661,7 +661,7 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
     out["worlds_per_gpu"] = e - b
     solve = ("the boxed LCP solved as DART does (wave_lcp.hpp: a frictionless stage, then friction boxed by its "
              "normals; each stage the primal active-set method from the previous step's working set after at most "
-             "4 PGS sweeps, <= 24 linear solves per world-step)" if exact
+             "4 PGS sweeps, <= 48 linear solves per world-step)" if exact
              else f"PGS {pgs} iterations only (mw_set_lcp_solver PGS)")
     out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
                        f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "

@@ -160,7 +160,7 @@ struct mw_sim {
     uint64_t* h_ndiv = nullptr;
     int64_t div_seen = 0;
     int32_t lcp_mode = MW_LCP_EXACT;  // mw_set_lcp_solver (wave kernel)
-    int32_t lcp_solves = 24;          // linear-solve budget of the exact solve per step
+    int32_t lcp_solves = 48;          // linear-solve budget of the exact solve per step (r06: a random humanoid impact needed 25-32)
     mw::SimDev dev;
     // host-only component data
     std::vector<int32_t> mode;      // JointControlMode per [d][w]

@@ -298,7 +298,7 @@ class Simulator:
         N.check(N.lib().mw_apply_link_wrench(self.handle, int(link), int(w0), int(nw), N.dptr(v), float(duration)),
                 "apply_world_wrench")
 
-    def set_lcp_solver(self, exact: bool = True, max_solves: int = 24) -> None:
+    def set_lcp_solver(self, exact: bool = True, max_solves: int = 48) -> None:
         """mw_set_lcp_solver: exact boxed LCP after the PGS sweeps (default) or the sweeps alone."""
         N.check(N.lib().mw_set_lcp_solver(self.handle, N.LCP_EXACT if exact else N.LCP_PGS, int(max_solves)),
                 "set_lcp_solver")

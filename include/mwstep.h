@@ -236,7 +236,7 @@ int mw_reset_base_velocity(mw_sim* sim, int32_t w0, int32_t nw, const double* li
 int mw_set_pgs_options(mw_sim* sim, double tol, int32_t warm_start);
 int mw_pgs_options(const mw_sim* sim, double* tol, int32_t* warm_start);
 /* The boxed-LCP solver of floating models.  MW_LCP_EXACT (default,
- * max_solves 24) solves the LCP as DART does: DART's primary solver is ODE's
+ * max_solves 48) solves the LCP as DART does: DART's primary solver is ODE's
  * Dantzig pivoting LCP [EXT], reached from ForwardStep (Physics.cpp:1824-1835),
  * whose friction index boxes every friction row once, by mu x the normal
  * impulses of the frictionless problem -- two strictly convex box QPs

@@ -537,6 +537,17 @@ void or_pgs_stats(int* sweeps, double* last_delta)
 static _Thread_local double g_cap_A[OR_CAP_MAXN * OR_CAP_MAXN], g_cap_b[OR_CAP_MAXN], g_cap_lo[OR_CAP_MAXN],
     g_cap_hi[OR_CAP_MAXN], g_cap_x[OR_CAP_MAXN], g_cap_mu;
 static _Thread_local int g_cap_kind[OR_CAP_MAXN], g_cap_n = 0;
+/* row identities of the capture (the kernels' warm-record index: contact slot
+ * rows 3 slot + d, joint rows OR_WARM_JOINT0 + 3 dof + type; -1 where the
+ * step has none, e.g. the scene step) and DART's stage-1 impulses of the
+ * converged mode (lcp_dantzig: friction rows 0) */
+static _Thread_local int g_cap_wid[OR_CAP_MAXN];
+static _Thread_local double g_cap_x1[OR_CAP_MAXN];
+/* per row, the magnitude of the terms b_r is formed from (sum_e |J_re nu_e|
+ * plus the bias velocity): the scale of b's rounding error in a finite
+ * precision step (tests/lcp_validity.py) */
+static _Thread_local double g_cap_bscale[OR_CAP_MAXN];
+static _Thread_local double g_last_x1[OR_CAP_MAXN + 64];
 
 int or_lcp_last(int cap, double* A, double* b, double* lo, double* hi, int* kind, double* x, double* mu)
 {
@@ -547,6 +558,18 @@ int or_lcp_last(int cap, double* A, double* b, double* lo, double* hi, int* kind
         b[r] = g_cap_b[r]; lo[r] = g_cap_lo[r]; hi[r] = g_cap_hi[r]; kind[r] = g_cap_kind[r]; x[r] = g_cap_x[r];
     }
     *mu = g_cap_mu;
+    return n;
+}
+
+int or_lcp_last_rows(int cap, int32_t* wid, double* x1, double* bscale)
+{
+    const int n = g_cap_n;
+    if (n > cap) return -n;
+    for (int r = 0; r < n; ++r) {
+        wid[r] = g_cap_wid[r];
+        x1[r] = g_cap_x1[r];
+        bscale[r] = g_cap_bscale[r];
+    }
     return n;
 }
 
@@ -794,6 +817,7 @@ static void lcp_dantzig_exact(int n, const double* A, int lda, const double* b, 
     double x1[OR_LCP_MAXN];
     for (int r = 0; r < n; ++r) x1[r] = 0.0;
     for (int i = 0; i < ns; ++i) x1[sidx[i]] = xs[i];
+    for (int r = 0; r < n && r < OR_CAP_MAXN + 64; ++r) g_last_x1[r] = x1[r];
     const double res1 = ns > 0 ? lcp_residual(ns, As, ns, bs, Ls, Us, nofric, 0.0, xs, 1e-12) : 0.0;
     /* stage 2: friction boxes from the stage-1 normals, all rows */
     for (int r = 0; r < n; ++r) {
@@ -1540,6 +1564,7 @@ void or_float_dynamics(const or_float_model* m, const or_float_state* s, double*
     const int n = t->n, nv = 6 + n;
     or_fkin k;
     float_kin(m, s, &k);
+    g_cap_n = 0;  /* a step without rows leaves no capture behind */
 
     /* CRBA: composite inertias accumulate towards the base */
     double Ic[OR_MAXB][36], I0[36];
@@ -1671,6 +1696,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
     const int n = t->n, nv = 6 + n;
     or_fkin k;
     float_kin(m, s, &k);
+    g_cap_n = 0;  /* a step without rows leaves no capture behind */
 
     static _Thread_local double M[(6 + OR_MAXB) * (6 + OR_MAXB)];
     double h[6 + OR_MAXB], rhs[6 + OR_MAXB], acc[6 + OR_MAXB], nu[6 + OR_MAXB];
@@ -1741,6 +1767,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
     static _Thread_local double A[(3 * OR_MAXFC + 3 * OR_MAXB) * (3 * OR_MAXFC + 3 * OR_MAXB)];
     double bb[3 * OR_MAXFC + 3 * OR_MAXB], lo[3 * OR_MAXFC + 3 * OR_MAXB], hi[3 * OR_MAXFC + 3 * OR_MAXB];
     double cfm[3 * OR_MAXFC + 3 * OR_MAXB], x[3 * OR_MAXFC + 3 * OR_MAXB];
+    double bsc[3 * OR_MAXFC + 3 * OR_MAXB];
     int kind[3 * OR_MAXFC + 3 * OR_MAXB];
     int wid[3 * OR_MAXFC + 3 * OR_MAXB];
     int nr = 0;
@@ -1761,14 +1788,18 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
             } else {
                 float_row(m, &k, bi, f, J[nr]);
             }
-            double vrel = 0.0;
-            for (int e = 0; e < nv; ++e) vrel += J[nr][e] * nu[e];
+            double vrel = 0.0, vabs = 0.0;
+            for (int e = 0; e < nv; ++e) {
+                vrel += J[nr][e] * nu[e];
+                vabs += fabs(J[nr][e] * nu[e]);
+            }
             double bounce = 0.0;
             if (d == 0) {
                 bounce = OR_C_ERP * depth[c] / dt;
                 if (bounce > OR_C_MAX_ERV) bounce = OR_C_MAX_ERV;
             }
             bb[nr] = -vrel + bounce;
+            bsc[nr] = vabs + bounce;
             kind[nr] = d == 0 ? K_NORMAL : K_FRIC;
             cfm[nr] = OR_C_CFM;
             wid[nr] = 3 * cslot[c] + d;
@@ -1791,6 +1822,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
                 if (bounce > OR_MAX_ERV) bounce = OR_MAX_ERV;
                 if (bounce < -OR_MAX_ERV) bounce = -OR_MAX_ERV;
                 bb[nr] = -qdi + bounce;
+                bsc[nr] = fabs(qdi) + fabs(bounce);
                 wid[nr] = OR_WARM_JOINT0 + 3 * i;
                 rows_i[nri++] = nr++;
             }
@@ -1801,6 +1833,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
             if (vc > t->vel_limit[i]) vc = t->vel_limit[i];
             if (vc - qdi != 0.0) {
                 bb[nr] = vc - qdi;
+                bsc[nr] = fabs(vc) + fabs(qdi);
                 lo[nr] = -t->effort[i] * dt;
                 hi[nr] = t->effort[i] * dt;
                 wid[nr] = OR_WARM_JOINT0 + 3 * i + 1;
@@ -1809,6 +1842,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
         }
         if (t->friction[i] != 0.0 && qdi != 0.0) {
             bb[nr] = -qdi;
+            bsc[nr] = fabs(qdi);
             hi[nr] = t->friction[i] * dt;
             lo[nr] = -hi[nr];
             wid[nr] = OR_WARM_JOINT0 + 3 * i + 2;
@@ -1838,6 +1872,9 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
         for (int r = 0; r < nr; ++r) {
             for (int c = 0; c < nr; ++c) g_cap_A[r * nr + c] = A[r * nr + c];
             g_cap_b[r] = bb[r];
+            g_cap_wid[r] = wid[r];
+            g_cap_bscale[r] = bsc[r];
+            g_cap_x1[r] = 0.0;
             g_cap_kind[r] = kind[r];
             g_cap_lo[r] = kind[r] == K_BOX ? lo[r] : (kind[r] == K_NORMAL ? 0.0 : -INFINITY);
             g_cap_hi[r] = kind[r] == K_BOX ? hi[r] : INFINITY;
@@ -1881,6 +1918,7 @@ int or_float_step_warm(const or_float_model* m, double dt, or_float_state* s, co
                 if (kind[r] == K_NORMAL) { lo[r] = 0.0; hi[r] = INFINITY; }
             }
             lcp_dantzig(nr, A, nr, bb, lo, hi, findex, m->mu, x);
+            for (int r = 0; r < nr; ++r) g_cap_x1[r] = g_last_x1[r];
         }
         for (int r = 0; r < nr; ++r) g_cap_x[r] = x[r];
         for (int r = 0; r < nr; ++r)
@@ -2435,6 +2473,7 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
     const int K = sm->n_models;
     static _Thread_local or_fkin kin[OR_SC_MAXM];
     int off[OR_SC_MAXM], nbase[OR_SC_MAXM];
+    g_cap_n = 0;  /* a step without rows leaves no capture behind */
     int NV = 0;
     for (int m = 0; m < K; ++m) {
         off[m] = NV;
@@ -2707,6 +2746,9 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
             for (int r = 0; r < nr; ++r) {
                 for (int c = 0; c < nr; ++c) g_cap_A[r * nr + c] = A[r * nr + c];
                 g_cap_b[r] = bb[r];
+                g_cap_wid[r] = -1;
+                g_cap_bscale[r] = fabs(bb[r]);
+                g_cap_x1[r] = 0.0;
                 g_cap_kind[r] = kind[r];
                 g_cap_lo[r] = kind[r] == K_BOX ? lo[r] : (kind[r] == K_NORMAL ? 0.0 : -INFINITY);
                 g_cap_hi[r] = kind[r] == K_BOX ? hi[r] : INFINITY;

@@ -91,6 +91,14 @@ void or_pgs(int n, const double* A, const double* b, const double* lo,
 void or_pgs_stats(int* sweeps, double* last_delta);
 /* test hook: the latest floating-tree LCP and its solution (n rows, or -n if cap < n) */
 int or_lcp_last(int cap, double* A, double* b, double* lo, double* hi, int* kind, double* x, double* mu);
+/* Row identities of the same capture (the kernels' warm-record index: contact
+ * slot rows 3 slot + d, joint rows OR_WARM_JOINT0 + 3 dof + type; -1 when the
+ * step has none), the converged mode's stage-1 impulses (DART's frictionless
+ * stage; 0 on friction rows, 0 everywhere after a PGS-only solve) and per row
+ * the magnitude of the terms b_r is formed from (sum_e |J_re nu_e| plus the
+ * bias velocity).  A step without rows leaves no capture (count 0).  Returns
+ * the row count (-count when cap is too small). */
+int or_lcp_last_rows(int cap, int32_t* wid, double* x1, double* bscale);
 /* tests: perturb the Delassus matrix of every exact LCP solve (0 = off) */
 void or_set_lcp_perturbation(double eps, uint64_t seed);
 

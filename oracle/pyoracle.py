@@ -1333,7 +1333,9 @@ def lcp_last():
     """The latest floating-tree LCP the oracle solved (test hook): dict of the
     Delassus matrix A (with CFM), rhs b, bounds lo/hi (friction rows: +-inf,
     bounded by mu x_normal), row kinds (0 normal, 1 friction, 2 box), mu and
-    the solution x the step used; None when the step had no rows."""
+    the solution x the step used, the rows' warm-record identities `wid`, the
+    stage-1 impulses `x1` and the b-term magnitudes `bscale`
+    (oracle.h or_lcp_last_rows); None when the step had no rows."""
     cap = 3 * 8 * 16 + 3 * 48
     A = np.zeros(cap * cap)
     b, lo, hi, x = (np.zeros(cap) for _ in range(4))
@@ -1343,8 +1345,15 @@ def lcp_last():
                           _p(x), ctypes.byref(mu))
     if n <= 0:
         return None
+    wid = np.zeros(cap, np.int32)
+    x1, bscale = np.zeros(cap), np.zeros(cap)
+    f = lib().or_lcp_last_rows
+    f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double),
+                  ctypes.POINTER(ctypes.c_double)]
+    assert f(cap, wid.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _p(x1), _p(bscale)) == n
     return dict(A=A[:n * n].reshape(n, n).copy(), b=b[:n].copy(), lo=lo[:n].copy(), hi=hi[:n].copy(),
-                kind=kind[:n].copy(), mu=mu.value, x=x[:n].copy())
+                kind=kind[:n].copy(), mu=mu.value, x=x[:n].copy(), wid=wid[:n].copy(), x1=x1[:n].copy(),
+                bscale=bscale[:n].copy())
 
 
 def set_lcp_perturbation(eps: float, seed: int = 0) -> None:

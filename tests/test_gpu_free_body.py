@@ -293,7 +293,7 @@ def test_cube_kat_exact_on_mw_sim(require_gpu):
     from mwstep.sim import Simulator
     for W in (1, 4096):
         sim = Simulator(cube_urdf(), n_worlds=W, pose=(0, 0, 0.15, 1, 0, 0, 0))
-        assert sim.float_kernel() == 2 and sim.lcp_solver() == (True, 24)
+        assert sim.float_kernel() == 2 and sim.lcp_solver() == (True, 48)
         sim.set_ground_plane(True, 1.0)
         sim.enable_contacts(True)
         for _ in range(150):

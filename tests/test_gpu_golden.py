@@ -76,6 +76,6 @@ def test_humanoid_matches_golden(require_gpu):
     fz = [sum(r[8] for r in sim.contacts(w)) for w in range(4)]
     sim.close()
     print(f"humanoid vs golden: max|dq| {wq:.2e}, max|dp| {wp:.2e}, sum Fz {fz} vs {g['contact_fz'].sum():.3f}")
-    assert wq <= 1e-3 and wp <= 1e-4
+    assert wq <= 1e-4 and wp <= 1e-5
     for f in fz:
         assert f == pytest.approx(float(g["contact_fz"].sum()), abs=0.5)

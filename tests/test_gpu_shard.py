@@ -159,7 +159,7 @@ def test_contact_answer_independent_of_world_count(require_gpu):
     vel = np.column_stack([rng.uniform(-0.5, 0.5, (W, 2)), rng.uniform(-0.3, 0.0, W), rng.uniform(-0.5, 0.5, (W, 3))])
     sims = [_float_sim("quadruped", w, q0[:w], pose[:w], vel[:w], None) for w in (4096, W)]
     for s in sims:
-        assert s.float_kernel() == 2 and s.lcp_solver() == (True, 24)
+        assert s.float_kernel() == 2 and s.lcp_solver() == (True, 48)
     h, touching = 4096, 0
     for t in range(200):
         for s in sims:
