@@ -634,27 +634,31 @@ def quadruped_leg(args, dev, torch, W=16384, pgs=20, ground=True, exact=True):
 
 def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512, pgs=50, pgs_opts=(0.0, False),
                  exact=True):
-    """BASELINE config 5: 512 iCub-class humanoids in total (models/humanoid32.urdf:
-    32 dofs, 36.4 kg, floating base, box feet) split over the ranks, standing on
-    the ground plane under the JointController PID hold (stiff legs / torso,
-    soft arms), contacts enabled, PGS 50 iterations, one physics step per run;
-    the one-world-per-wavefront kernel (wave_tree.hpp).  Initial states are
-    drawn for all 512 worlds and sliced per rank (independent of the rank count)."""
+    """BASELINE config 5: 512 iCub-class humanoids in total (models/icub.urdf:
+    the reference iCub wrapper's 32 joints and 39 links, 30.7 kg, floating
+    base, box feet) split over the ranks, inserted as the wrapper inserts
+    them -- base at (0, 0, 0.572), wxyz (0, 0, 0, 1), joints at its
+    initial_positions (python/gym_ignition_environments/models/icub.py:19-40,
+    :86) -- standing on the ground plane under the JointController PID hold
+    of that posture (stiff legs / torso, soft arms), contacts enabled, one
+    physics step per run; the one-world-per-wavefront kernel (wave_tree.hpp).
+    Worlds sit on an xy grid (no interaction); the state is independent of
+    the rank count."""
     import numpy as np
     from mwstep import get_model_file
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
     from mwstep.shard import shard_range
     from mwstep.sim import Simulator
-    probe = Simulator(get_model_file("humanoid32"), n_worlds=1)
+    probe = Simulator(get_model_file("icub"), n_worlds=1)
     names = probe.joint_names
     probe.close()
-    gains = [(500.0, 5.0, 80.0) if ("leg" in n or "torso" in n) else (50.0, 0.5, 80.0) for n in names]
-    n = len(names)
+    gains = [(p, d, 80.0) for p, d in icub_pid_gains(names)]
     b, e = shard_range(W_global, rank, world_size)
+    q0 = np.tile(icub_posture(names), (W_global, 1))
     rng = np.random.default_rng(args.seed)
-    q0 = rng.uniform(-0.02, 0.02, (W_global, n))
     xy = rng.uniform(-5, 5, (W_global, 2))
-    out = float_tree_leg(args, dev, torch, "humanoid32", e - b, pgs, 0.535, gains,
-                         q0[b:e], np.zeros((e - b, n)), xy[b:e], K=200, G=20, warm=40,
+    out = float_tree_leg(args, dev, torch, "icub", e - b, pgs, ICUB_POSE[2], gains,
+                         q0[b:e], q0[b:e], xy[b:e], K=200, G=20, warm=40, wxyz=ICUB_POSE[3:],
                          dist=dist, world_size=world_size, pgs_opts=pgs_opts, exact=exact, W_global=W_global)
     out["value"] = round(W_global * out["steps"] / out["elapsed_s"], 1)
     out["scaling"] = "strong"
@@ -663,8 +667,10 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
              "normals; each stage the primal active-set method from the previous step's working set after at most "
              "4 PGS sweeps, <= 48 linear solves per world-step)" if exact
              else f"PGS {pgs} iterations only (mw_set_lcp_solver PGS)")
-    out["workload"] = (f"{W_global} iCub-class humanoids (32 dofs, 36.4 kg, floating base, box feet) split over "
-                       f"{world_size} GPU(s), standing on a ground plane under JointController PID hold, "
+    out["workload"] = (f"{W_global} iCub-class humanoids (models/icub.urdf: the reference iCub wrapper's 32 joints "
+                       f"and 39 links, 30.7 kg, floating base, box feet) split over {world_size} GPU(s), inserted at "
+                       f"(0, 0, 0.572) wxyz (0, 0, 0, 1) with the wrapper's initial posture (icub.py:19-40, :86), "
+                       f"standing on a ground plane under a JointController PID hold of that posture, "
                        f"{solve}, dt = 1 ms (BASELINE.json configs[4])")
     out["roofline"] = valu_roofline(out["kernel_us_per_launch"], e - b, exact)
     if exact and rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -680,7 +686,7 @@ def humanoid_leg(args, dev, torch, dist=None, world_size=1, rank=0, W_global=512
 
 
 def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, K=500, G=50, warm=100,
-                   dist=None, world_size=1, pgs_opts=(0.0, False), exact=True, W_global=None):
+                   dist=None, world_size=1, pgs_opts=(0.0, False), exact=True, W_global=None, wxyz=(1, 0, 0, 0)):
     """Time W floating-base worlds of `model` under a PID hold, one physics
     step per run, replayed from hipGraphs of mw_run_device; with several ranks
     the timed region is bracketed by barriers and the max over ranks is kept."""
@@ -690,7 +696,7 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, 
     from mwstep.sim import Simulator
     stream = torch.cuda.Stream(device=dev)
     sim = Simulator(get_model_file(model), n_worlds=W, device=dev.index, pgs_iters=pgs,
-                    stream=stream.cuda_stream, pose=(0, 0, z0, 1, 0, 0, 0))
+                    stream=stream.cuda_stream, pose=(0, 0, z0, *wxyz))
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
     if pgs_opts[0] > 0.0 or pgs_opts[1]:
@@ -698,7 +704,7 @@ def float_tree_leg(args, dev, torch, model, W, pgs, z0, gains, q0, targets, xy, 
     if not exact:
         sim.set_lcp_solver(False)
     sim.set("reset_q", q0)
-    pose = np.column_stack([xy, np.full(W, z0), np.ones(W), np.zeros((W, 3))])
+    pose = np.column_stack([xy, np.full(W, z0), np.tile(np.asarray(wxyz, dtype=float), (W, 1))])
     sim.reset_base_pose(pose)
     sim.run(paused=True)
     sim.set_controller_period(1e-3)
@@ -1036,29 +1042,31 @@ def cpu_panda_baseline(seconds, Wc=64):
 
 
 def cpu_humanoid_baseline(seconds):
-    """BASELINE config 5 on the host: one fp64 oracle humanoid (dense CRBA +
-    contact LCP solved exactly, PGS_CONVERGED -- the GPU default's problem)
-    under the PID hold per thread (or_float_pid_rollout), every host thread."""
+    """BASELINE config 5 on the host: one fp64 oracle iCub-class humanoid
+    (dense CRBA + contact LCP solved exactly, PGS_CONVERGED -- the GPU
+    default's problem) from the wrapper's posture and pose under the PID hold
+    per thread (or_float_pid_rollout), every host thread."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from mwstep import get_model_file
-    cm = pyoracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
+    cm = pyoracle.load_urdf(get_model_file("icub"), pose_xyz=ICUB_POSE[:3], pose_wxyz=ICUB_POSE[3:])
     n = cm.n
-    stiff = ["leg" in nm or "torso" in nm for nm in cm.joint_names]
-    gains = [pyoracle.pid_gains(500.0 if s_ else 50.0, 0.0, 5.0 if s_ else 0.5, cmdmax=80.0, cmdmin=-80.0)
-             for s_ in stiff]
+    q0 = np.array(icub_posture(cm.joint_names))
+    gains = [pyoracle.pid_gains(p, 0.0, d, cmdmax=80.0, cmdmin=-80.0) for p, d in icub_pid_gains(cm.joint_names)]
 
     def make():
         fw = pyoracle.FloatWorld(cm, pgs_iters=pyoracle.PGS_CONVERGED)
+        fw.set_joints(q0, np.zeros(n))
         return [fw, None]
 
     def run(st, T):
-        st[1] = pyoracle.float_pid_rollout(st[0], np.zeros(n), gains, T, states=st[1])
+        st[1] = pyoracle.float_pid_rollout(st[0], q0, gains, T, states=st[1])
 
     threads, T, wall = _threaded(make, run, seconds, 5)
     return {"value": round(threads * T / wall, 1), "unit": "env·steps/s", "cores": threads, "kind": "port",
-            "sample": f"{threads} threads x 1 humanoid x {T} steps standing under the PID hold, exact contact "
+            "sample": f"{threads} threads x 1 iCub-class humanoid x {T} steps standing under the PID hold, exact contact "
                       f"LCP, fp64 C oracle ({wall:.1f} s wall; {cpu_model_name()})"}
 
 

@@ -1,1 +1,1 @@
-from . import cartpole, panda, pendulum  # noqa: F401
+from . import cartpole, icub, panda, pendulum  # noqa: F401

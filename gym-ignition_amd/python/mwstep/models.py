@@ -12,7 +12,7 @@ _FILES = {
     "panda": "panda.urdf",
     "cube": "cube.urdf",
     "quadruped": "quadruped.urdf",
-    "humanoid32": "humanoid32.urdf",
+    "icub": "icub.urdf",
     "ground_plane": "ground_plane.sdf",
 }
 
@@ -42,3 +42,34 @@ PANDA_PID_GAINS_1000HZ = {
     "panda_finger_joint1": (100.0, 0.0, 50.0),
     "panda_finger_joint2": (100.0, 0.0, 50.0),
 }
+
+
+# BASELINE config 5: the iCub-class model (models/icub.urdf, make_icub.py)
+# starts from the reference wrapper's posture and pose
+# (python/gym_ignition_environments/models/icub.py:19-40, :86) ...
+ICUB_INITIAL_POSITIONS = {
+    "l_knee": -1.05, "l_ankle_pitch": -0.57, "l_ankle_roll": -0.024,
+    "l_hip_pitch": 0.48, "l_hip_roll": 0.023, "l_hip_yaw": -0.005,
+    "l_elbow": 0.54, "l_wrist_pitch": 0.0, "l_wrist_prosup": 0.0, "l_wrist_yaw": 0.0,
+    "l_shoulder_pitch": -0.159, "l_shoulder_roll": 0.435, "l_shoulder_yaw": 0.183,
+    "neck_pitch": 0.0, "neck_roll": 0.0, "neck_yaw": 0.0,
+    "r_knee": -1.05, "r_ankle_pitch": -0.57, "r_ankle_roll": -0.024,
+    "r_hip_pitch": 0.48, "r_hip_roll": 0.023, "r_hip_yaw": -0.005,
+    "r_elbow": 0.54, "r_wrist_pitch": 0.0, "r_wrist_prosup": 0.0, "r_wrist_yaw": 0.0,
+    "r_shoulder_pitch": -0.159, "r_shoulder_roll": 0.435, "r_shoulder_yaw": 0.183,
+    "torso_pitch": 0.1, "torso_roll": 0.0, "torso_yaw": 0.0,
+}
+ICUB_POSE = (0.0, 0.0, 0.572, 0.0, 0.0, 0.0, 1.0)   # xyz, wxyz (icub.py:86)
+
+
+def icub_posture(joint_names):
+    """The wrapper's initial positions in the given joint order."""
+    return [ICUB_INITIAL_POSITIONS[n] for n in joint_names]
+
+
+def icub_pid_gains(joint_names):
+    """(P, D) of the posture hold the config-5 workload runs (JointController
+    Position mode, period = step size): stiff legs and torso, soft arms and
+    neck (explicit PD at 1 kHz: D dt / I_eff < 2 on the lightest subtrees)."""
+    stiff = ("hip", "knee", "ankle", "torso")
+    return [(500.0, 5.0) if any(k in n for k in stiff) else (50.0, 0.5) for n in joint_names]

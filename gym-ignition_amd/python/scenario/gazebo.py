@@ -814,8 +814,10 @@ class Model:
     # -- links and contacts (Link.cpp): the base link and the link of every joint
     def link_names(self, scoped: bool = False) -> List[str]:
         # Model::linkNames (Model.cpp:479-520); links lumped by fixed joints do not exist
+        # unless the file keeps them (sdformat's preserveFixedJoint: _preserved_links);
         # a ball joint's internal massless links (`<joint>#x`, `#y`) are not links
         names = [self._sim.base_frame] + [n for n in self._sim.link_names if not self._internal_link(n)]
+        names += list(self._preserved_links())
         return [f"{self._name}::{n}" for n in names] if scoped else names
 
     def get_link(self, link_name: str) -> "Link":
@@ -823,7 +825,70 @@ class Model:
             return Link(self, link_name, -1)
         if link_name in self._sim.link_names and not self._internal_link(link_name):
             return Link(self, link_name, self._sim.link_names.index(link_name))
+        kept = self._preserved_links().get(link_name)
+        if kept is not None:
+            return Link(self, link_name, kept[0], offset=kept[1:3])
         raise RuntimeError(f"Link '{link_name}' not found in model '{self._name}'")
+
+    def _preserved_links(self) -> Dict[str, tuple]:
+        """Links welded to their parent by a fixed joint that the URDF asks
+        sdformat to keep (`<gazebo reference="<joint>"><preserveFixedJoint>
+        true</preserveFixedJoint></gazebo>`, e.g. the iCub's force/torque
+        sensor frames): still links of the model (Model::linkNames, Link
+        getters) although the physics lumps their inertia into the parent
+        body (the model compiler, as DART's welded bodies move rigidly).
+        name -> (owner body, R, p of the link frame in the owner body's
+        frame, the link's own mass, has collisions, its COM in its frame)."""
+        cache = self.__dict__.get("_preserved")
+        if cache is not None:
+            return cache
+        out: Dict[str, tuple] = {}
+        text = getattr(self, "_text", None)
+        root = None
+        if text:
+            try:
+                root = ET.fromstring(text.strip())
+            except ET.ParseError:
+                root = None
+        if root is not None and root.tag == "robot":
+            keep = {g.get("reference") for g in root.findall("gazebo")
+                    if (g.findtext("preserveFixedJoint") or "").strip().lower() in ("true", "1")}
+            compiled = {self._sim.base_frame: -1}
+            compiled.update({n: i for i, n in enumerate(self._sim.link_names)})
+            links = {lk.get("name"): lk for lk in root.findall("link")}
+            pending = [j for j in root.findall("joint") if j.get("type") == "fixed" and j.get("name") in keep]
+            progress = True
+            while pending and progress:
+                progress = False
+                for j in list(pending):
+                    parent, child = j.find("parent").get("link"), j.find("child").get("link")
+                    if parent in compiled:
+                        owner, R0, p0 = compiled[parent], np.eye(3), np.zeros(3)
+                    elif parent in out:
+                        owner, R0, p0 = out[parent][:3]
+                    else:
+                        continue
+                    R, pj = _urdf_origin(j.find("origin"))
+                    lk = links.get(child)
+                    m = lk.find("inertial/mass") if lk is not None else None
+                    com = _urdf_origin(lk.find("inertial/origin"))[1] if lk is not None else np.zeros(3)
+                    out[child] = (owner, R0 @ R, p0 + R0 @ pj, float(m.get("value")) if m is not None else 0.0,
+                                  lk is not None and lk.find("collision") is not None, com)
+                    pending.remove(j)
+                    progress = True
+            # a body whose own link has no collision while exactly one kept
+            # link on it has: the body's contacts are that link's (the iCub's
+            # soles sit on the foot F/T-sensor frame)
+            owned = {}
+            for name, (owner, _R, _p, _m, col, _c) in out.items():
+                if col:
+                    owned.setdefault(owner, []).append(name)
+            own_col = {compiled[n]: (links[n].find("collision") is not None) for n in compiled if n in links}
+            self._contact_link = {b: ns[0] for b, ns in owned.items() if len(ns) == 1 and not own_col.get(b, False)}
+        else:
+            self._contact_link = {}
+        self._preserved = out
+        return out
 
     def links(self, link_names: Sequence[str] = ()) -> List["Link"]:
         return [self.get_link(n) for n in (link_names or self.link_names())]
@@ -1160,10 +1225,37 @@ class Model:
 class Link:
     """A link of a model (Link.cpp): pose, velocity and contacts."""
 
-    def __init__(self, model: "Model", name: str, body: int = -1):
+    def __init__(self, model: "Model", name: str, body: int = -1, offset=None):
         self._model = model
         self._name = name
         self._body = body  # -1 = the base link, i = the link moved by joint i
+        # a link kept on a fixed joint (Model._preserved_links): its frame in the body's
+        self._offset = offset
+
+    def _state(self):
+        """World R, p, v (of the link origin), w of this link."""
+        R, p, v, w = self._model._link_state(self._body)
+        if self._offset is None:
+            return R, p, v, w
+        Ro, po = self._offset
+        d = R @ po
+        return R @ Ro, p + d, v + np.cross(w, d), w
+
+    def _acc(self):
+        a, al = self._model._link_acc(self._body)
+        if self._offset is None:
+            return a, al
+        R, _, _, w = self._model._link_state(self._body)
+        d = R @ self._offset[1]
+        return a + np.cross(al, d) + np.cross(w, np.cross(w, d)), al
+
+    def _contact_owner(self) -> bool:
+        """Whether this link reports its body's contacts: a body's own link
+        does unless a kept link on it carries the body's collisions."""
+        m = self._model
+        m._preserved_links()
+        delegate = m._contact_link.get(self._body)
+        return (delegate == self._name) if delegate is not None else self._offset is None
 
     def to_gazebo(self) -> "Link":
         return self
@@ -1173,54 +1265,56 @@ class Link:
 
     def mass(self) -> float:
         # Link::mass (Link.cpp:198-204) of the compiled body: links welded by
-        # fixed joints are lumped into one body (their masses summed)
+        # fixed joints are lumped into one body (their masses summed), except
+        # the links the file keeps (Model._preserved_links), which have their own
+        kept = self._model._preserved_links()
+        if self._offset is not None:
+            return kept[self._name][3]
+        mine = sum(v[3] for v in kept.values() if v[0] == self._body)
         ex = self._model._sim.export_model()
         n = self._model._sim.dofs
         if self._body >= 0:
-            return float(ex[34 * self._body + 17])
+            return float(ex[34 * self._body + 17]) - mine
         if self._model._sim.floating:
-            return float(ex[34 * n + 3])
+            return float(ex[34 * n + 3]) - mine
         # a welded base is not part of the dynamics: its (lumped) mass is what
         # the model file holds beyond the moving bodies
         return max(self._model._file_mass() - sum(float(ex[34 * b + 17]) for b in range(n)), 0.0)
 
     def position(self) -> List[float]:
-        return self._model._link_state(self._body)[1].tolist()
+        return self._state()[1].tolist()
 
     def orientation(self) -> List[float]:
         # wxyz of the link rotation
-        R = self._model._link_state(self._body)[0]
-        return _quat_from_R(R)
+        return _quat_from_R(self._state()[0])
 
     def world_linear_velocity(self) -> List[float]:
-        return self._model._link_state(self._body)[2].tolist()
+        return self._state()[2].tolist()
 
     def world_angular_velocity(self) -> List[float]:
-        return self._model._link_state(self._body)[3].tolist()
+        return self._state()[3].tolist()
 
     # body-fixed (link frame) velocities and accelerations: W_R_L^T times the
     # world ones (Link.cpp bodyLinearVelocity & co., ign-gazebo issue 87 note)
     def body_linear_velocity(self) -> List[float]:
-        R, _, v, _ = self._model._link_state(self._body)
+        R, _, v, _ = self._state()
         return (R.T @ v).tolist()
 
     def body_angular_velocity(self) -> List[float]:
-        R, _, _, w = self._model._link_state(self._body)
+        R, _, _, w = self._state()
         return (R.T @ w).tolist()
 
     def world_linear_acceleration(self) -> List[float]:
-        return self._model._link_acc(self._body)[0].tolist()
+        return self._acc()[0].tolist()
 
     def world_angular_acceleration(self) -> List[float]:
-        return self._model._link_acc(self._body)[1].tolist()
+        return self._acc()[1].tolist()
 
     def body_linear_acceleration(self) -> List[float]:
-        R = self._model._link_state(self._body)[0]
-        return (R.T @ self._model._link_acc(self._body)[0]).tolist()
+        return (self._state()[0].T @ self._acc()[0]).tolist()
 
     def body_angular_acceleration(self) -> List[float]:
-        R = self._model._link_state(self._body)[0]
-        return (R.T @ self._model._link_acc(self._body)[1]).tolist()
+        return (self._state()[0].T @ self._acc()[1]).tolist()
 
     def contacts_enabled(self) -> bool:
         return self._model.contacts_enabled()
@@ -1233,7 +1327,7 @@ class Link:
         # merged into one Contact, body_a = this link; the other body is a
         # link of another model of the world or the ground plane
         sim = self._model._sim
-        if not sim.contacts_enabled():
+        if not sim.contacts_enabled() or not self._contact_owner():
             return []
         rows = sim.contact_rows()
         groups: "collections.OrderedDict[tuple, list]" = collections.OrderedDict()
@@ -1263,7 +1357,12 @@ class Link:
             _err("The force and the torque must have 3 elements")
             return False
         try:
-            self._model._sim.apply_world_wrench(self._body, list(force) + list(torque), float(duration))
+            torque = np.asarray(torque, dtype=float)
+            if self._offset is not None:
+                # a kept link's origin is off its body's: move the force there
+                R, p, _, _ = self._model._link_state(self._body)
+                torque = torque + np.cross(R @ self._offset[1], np.asarray(force, dtype=float))
+            self._model._sim.apply_world_wrench(self._body, list(force) + torque.tolist(), float(duration))
             return True
         except RuntimeError as e:
             _err(str(e))
@@ -1281,8 +1380,11 @@ class Link:
         # (W_R_L L_o_I) x f (Link.cpp:534-560)
         ex = self._model._sim.export_model()
         n = self._model._sim.dofs
-        com = ex[34 * n + 4:34 * n + 7] if self._body < 0 else ex[34 * self._body + 18:34 * self._body + 21]
-        R = self._model._link_state(self._body)[0]
+        if self._offset is not None:   # a kept link: its own inertial origin
+            com = self._model._preserved_links()[self._name][5]
+        else:
+            com = ex[34 * n + 4:34 * n + 7] if self._body < 0 else ex[34 * self._body + 18:34 * self._body + 21]
+        R = self._state()[0]
         t = np.asarray(torque, dtype=float) + np.cross(R @ com, np.asarray(force, dtype=float))
         return self.apply_world_wrench(force, t.tolist(), duration)
 
@@ -1297,6 +1399,19 @@ class Link:
                 f += fp
                 t += np.cross(np.array(p.position) - o, fp)
         return np.concatenate([f, t]).tolist()
+
+
+def _urdf_origin(el) -> tuple:
+    """(R, p) of a URDF <origin xyz rpy> (fixed-axis roll, pitch, yaw)."""
+    if el is None:
+        return np.eye(3), np.zeros(3)
+    p = np.array([float(v) for v in (el.get("xyz") or "0 0 0").split()])
+    r, pi, y = (float(v) for v in (el.get("rpy") or "0 0 0").split())
+    cr, sr, cp, sp, cy, sy = math.cos(r), math.sin(r), math.cos(pi), math.sin(pi), math.cos(y), math.sin(y)
+    R = np.array([[cy * cp, cy * sp * sr - sy * cr, cy * sp * cr + sy * sr],
+                  [sy * cp, sy * sp * sr + cy * cr, sy * sp * cr - cy * sr],
+                  [-sp, cp * sr, cp * cr]])
+    return R, p
 
 
 def _quat_from_R(R: np.ndarray) -> List[float]:
@@ -1411,7 +1526,8 @@ class World:
         for name, m in self._models.items():
             if isinstance(m, Model) and m._sim is not None and m._sim.m == slot:
                 sim = m._sim
-                return f"{name}::{sim.base_frame if link < 0 else sim.link_names[link]}"
+                m._preserved_links()   # a body's collisions may sit on a kept link
+                return f"{name}::{m._contact_link.get(link, sim.base_frame if link < 0 else sim.link_names[link])}"
         return f"model{slot}::link{link}"
 
     def set_physics_engine(self, engine: int = PhysicsEngine_dart) -> bool:

@@ -23,7 +23,7 @@ from test_gpu_float_tree import _model, _quat_to_R, _random_states  # noqa: E402
 def main():
     from mwstep import native as N
     from mwstep.sim import Simulator
-    name = sys.argv[1] if len(sys.argv) > 1 else "humanoid32"
+    name = sys.argv[1] if len(sys.argv) > 1 else "icub"
     W = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     budget = int(sys.argv[3]) if len(sys.argv) > 3 else 24
     os.environ["MWSTEP_WAVE_TREE"] = "1"

@@ -1,6 +1,6 @@
 """Prototype (numpy, float32 arithmetic) of the wave kernel's exact boxed-LCP
 solve in DART's two stages (wave_lcp.hpp, oracle.c lcp_dantzig), run on LCPs
-captured from humanoid32 drops / slides (pyoracle.lcp_last).  Mirrors the
+captured from iCub-class (models/icub.urdf) drops / slides (pyoracle.lcp_last).  Mirrors the
 device algorithm so the linear-solve counts and fp32 errors seen here are the
 kernel's:  per stage, PGS sweeps on the stage's box problem (tolerance exit
 1e-6 on the constraint velocities), then semismooth Newton (held rows: at a
@@ -31,15 +31,15 @@ import pyoracle  # noqa: E402
 
 
 def capture(n_worlds=8, steps=60, seed=21):
-    """humanoid32 drops / slides under a PD hold in the fp64 oracle (DART's LCP):
+    """iCub-class (models/icub.urdf) drops / slides under a PD hold in the fp64 oracle (DART's LCP):
     [((world, step), lcp)] (proto_lcp_exact.capture with the world index)"""
     from mwstep import get_model_file
-    cm = pyoracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    from mwstep.models import icub_pid_gains, icub_posture
+    cm = pyoracle.load_urdf(get_model_file("icub"), pose_xyz=(0, 0, 0.572), pose_wxyz=(0, 0, 0, 1))
+    post = np.array(icub_posture(cm.joint_names))
     n = cm.n
     rng = np.random.default_rng(seed)
-    stiff = [("leg" in nm or "torso" in nm) for nm in cm.joint_names]
-    kp = np.array([500.0 if s else 50.0 for s in stiff])
-    kd = np.array([5.0 if s else 0.5 for s in stiff])
+    kp, kd = np.array(icub_pid_gains(cm.joint_names)).T
     lo, hi = np.array(cm.model.lower[:n]), np.array(cm.model.upper[:n])
     out = []
     for w in range(n_worlds):
@@ -50,13 +50,13 @@ def capture(n_worlds=8, steps=60, seed=21):
         c, s_ = np.cos(ang), np.sin(ang)
         K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
         R = np.eye(3) + s_ * K + (1 - c) * K @ K
-        ow.set_pose([0, 0, 0.535 + rng.uniform(0, 0.09)], R)
+        ow.set_pose([0, 0, 0.572 + rng.uniform(0, 0.09)], R)
         ow.set_twist(R.T @ rng.uniform(-0.3, 0.3, 3),
                      R.T @ np.array([*rng.uniform(-0.8, 0.8, 2), rng.uniform(-0.5, 0)]))
-        ow.set_joints(np.clip(rng.uniform(-0.1, 0.1, n), lo, hi), rng.uniform(-0.5, 0.5, n))
+        ow.set_joints(np.clip(post + rng.uniform(-0.1, 0.1, n), lo, hi), rng.uniform(-0.5, 0.5, n))
         mode = np.full(n, pyoracle.FORCE, np.int32)
         for k in range(steps):
-            tau = np.clip(-kp * ow.q - kd * ow.qd, -80, 80)
+            tau = np.clip(-kp * (ow.q - post) - kd * ow.qd, -80, 80)
             ow.step(mode, tau)
             p = pyoracle.lcp_last()
             if p is not None and len(p["b"]) > 0:

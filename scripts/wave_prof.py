@@ -1,5 +1,5 @@
 """Phase breakdown of the one-world-per-wavefront kernel (wave_tree.hpp) on
-BASELINE config 5's workload (512 humanoid32 worlds standing, PGS 50).
+BASELINE config 5's workload (512 iCub-class worlds standing, models/icub.urdf).
 
 Needs the debug build with shader-clock phase counters:
     make -C gym-ignition_amd BUILD=build_prof LIB=libmwstep_prof.so EXTRA=-DMW_WAVE_PROF
@@ -27,7 +27,7 @@ T = int(os.environ.get("MW_PROF_T", "20"))
 PHASES = ["dof_force (PID)", "ABA (uniform)", "integrate + detect + row setup", "responses (lane = row)",
           "Delassus (lane = column)", "PGS + exact LCP", "rows total (responses .. integrate)", "whole substep"]
 
-if os.environ.get("MW_PROF_MODEL", "humanoid32") == "scene3":
+if os.environ.get("MW_PROF_MODEL", "icub") == "scene3":
     # the bench's scene leg (bench.scene_leg): three stacked cubes per world
     from mwstep.scene import Scene
     sc = Scene(n_worlds=W, pgs_iters=50)
@@ -56,7 +56,7 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "scene3":
           f"{buf[17] / ns:.0f} in stage 1")
     save_dumps(N.lib().mw_debug_scene_dump, 8, "scene_dump.npz")
     sys.exit(0)
-if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
+if os.environ.get("MW_PROF_MODEL", "icub") == "cube":
     # the bench's contacts leg (bench.contact_leg): cubes dropped from random poses
     sim = Simulator(get_model_file("cube"), n_worlds=W, pgs_iters=20)
     sim.set_ground_plane(True, 1.0)
@@ -86,20 +86,21 @@ if os.environ.get("MW_PROF_MODEL", "humanoid32") == "cube":
           f"{buf[17] / W / T:.0f} in stage 1")
     save_dumps(L.mw_debug_wave_dump, 9, "wave_dump.npz")
     sys.exit(0)
-sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=PGS, pose=(0, 0, 0.535, 1, 0, 0, 0))
+from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture  # noqa: E402
+sim = Simulator(get_model_file("icub"), n_worlds=W, pgs_iters=PGS, pose=ICUB_POSE)
 names = sim.joint_names
 sim.set_ground_plane(True, 1.0)
 sim.enable_contacts(True)
 sim.set_controller_period(1e-3)
-for d, n in enumerate(names):
-    p, dd = (500.0, 5.0) if ("leg" in n or "torso" in n) else (50.0, 0.5)
+for d, (p, dd) in enumerate(icub_pid_gains(names)):
     sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
 sim.set_control_mode(N.MODE_POSITION)
-sim.set("position_target", np.zeros((W, sim.dofs)))
-if os.environ.get("MW_PROF_RANDOM", "0") != "0":
-    # the bench leg's start: joint angles U(-0.02, 0.02) (bench.humanoid_leg)
-    sim.set("reset_q", np.random.default_rng(42).uniform(-0.02, 0.02, (W, sim.dofs)))
-    sim.run(paused=True)
+post = np.tile(icub_posture(names), (W, 1))
+sim.set("position_target", post)
+# the bench leg's start: the wrapper's posture (bench.humanoid_leg); MW_PROF_RANDOM=1 adds U(-0.02, 0.02)
+jit = np.random.default_rng(42).uniform(-0.02, 0.02, (W, sim.dofs)) if os.environ.get("MW_PROF_RANDOM", "0") != "0" else 0.0
+sim.set("reset_q", post + jit)
+sim.run(paused=True)
 # solver options: MW_PROF_EXACT=0 -> PGS only; MW_PROF_WARM=1 -> warm-started sweeps
 sim.set_lcp_solver(os.environ.get("MW_PROF_EXACT", "1") != "0")
 if os.environ.get("MW_PROF_WARM", "0") != "0":

@@ -1,5 +1,5 @@
 """Time the one-world-per-wavefront kernel (wave_tree.hpp) on BASELINE
-config 5's workload (humanoid32 standing under PID hold) for several world
+config 5's workload (the iCub-class model standing under PID hold) for several world
 counts and PGS iteration counts; the PGS cost per sweep is the slope.
     python scripts/wave_sweep.py [model] [W ...]"""
 import os
@@ -13,22 +13,24 @@ from mwstep import get_model_file  # noqa: E402
 from mwstep import native as N  # noqa: E402
 from mwstep.sim import Simulator  # noqa: E402
 
-model = sys.argv[1] if len(sys.argv) > 1 else "humanoid32"
+model = sys.argv[1] if len(sys.argv) > 1 else "icub"
 Ws = [int(a) for a in sys.argv[2:]] or [64, 512]
-z0 = {"humanoid32": 0.535, "quadruped": 0.45}[model]
+from mwstep.models import ICUB_POSE, icub_posture  # noqa: E402
+pose0 = {"icub": ICUB_POSE, "quadruped": (0, 0, 0.45, 1, 0, 0, 0)}[model]
 T = 40
 for W in Ws:
     for pgs in (0, 10, 50):
-        sim = Simulator(get_model_file(model), n_worlds=W, pgs_iters=pgs, pose=(0, 0, z0, 1, 0, 0, 0))
+        sim = Simulator(get_model_file(model), n_worlds=W, pgs_iters=pgs, pose=pose0)
         names = sim.joint_names
         sim.set_ground_plane(True, 1.0)
         sim.enable_contacts(True)
         sim.set_controller_period(1e-3)
         for d, n in enumerate(names):
-            p, dd = (500.0, 5.0) if ("leg" in n or "torso" in n or model == "quadruped") else (50.0, 0.5)
+            stiff = any(k in n for k in ("hip", "knee", "ankle", "torso")) or model == "quadruped"
+            p, dd = (500.0, 5.0) if stiff else (50.0, 0.5)
             sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
         sim.set_control_mode(N.MODE_POSITION)
-        q0 = np.tile([0.6, -1.2] * 4, (W, 1)) if model == "quadruped" else np.zeros((W, sim.dofs))
+        q0 = np.tile([0.6, -1.2] * 4 if model == "quadruped" else icub_posture(names), (W, 1))
         sim.set("reset_q", q0)
         sim.set("position_target", q0)
         sim.run(paused=True)

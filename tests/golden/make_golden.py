@@ -12,11 +12,14 @@ to the outputs:
                          (numpy PCG64 seed 43), obs / reward / done per step
   pendulum_swingup.npz   PendulumSwingUp, 16 worlds x 300 steps, torques
                          U(-50, 50) (PCG64 seed 43)
-  humanoid_stand.npz     humanoid32 (floating base, ground contacts, the boxed LCP
-                         solved as DART does: oracle.c lcp_dantzig)
-                         under the JointController PID hold for 300 steps:
-                         joint positions and base position every 10 steps,
-                         final contact forces
+  icub_stand.npz         the iCub-class model (models/icub.urdf: floating base,
+                         ground contacts, the boxed LCP solved as DART does:
+                         oracle.c lcp_dantzig) inserted as the reference's iCub
+                         wrapper inserts it (icub.py:19-40, :86: bent-knee
+                         posture at (0, 0, 0.572), wxyz (0, 0, 0, 1), 4 mm
+                         above the ground) under the JointController PID hold
+                         of that posture for 600 steps: joint positions and
+                         base position every 20 steps, final contact forces
 
     python tests/golden/make_golden.py        (rewrites the .npz files)
 """
@@ -32,13 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "gym-ignition_amd", "python"))
 
 W, T = 16, 300
-HUMANOID_Z = 0.535
-HUMANOID_STEPS, HUMANOID_EVERY = 300, 10
-
-
-def humanoid_gains(names):
-    stiff = lambda n: "leg" in n or "torso" in n
-    return [(500.0, 5.0) if stiff(n) else (50.0, 0.5) for n in names]
+HUMANOID_STEPS, HUMANOID_EVERY = 600, 20
 
 
 def vec_rollout(kind, model, actions):
@@ -70,20 +67,22 @@ def pendulum():
     return dict(actions=actions, obs0=obs0, obs=obs, reward=rew, done=done)
 
 
-def humanoid():
+def icub():
     import pyoracle
     from mwstep import get_model_file
-    cm = pyoracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, HUMANOID_Z))
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
+    cm = pyoracle.load_urdf(get_model_file("icub"), pose_xyz=ICUB_POSE[:3], pose_wxyz=ICUB_POSE[3:])
     names = list(cm.joint_names)
     ow = pyoracle.FloatWorld(cm, pgs_iters=pyoracle.PGS_CONVERGED)  # the wave kernel's exact LCP
     n = cm.n
-    gains = humanoid_gains(names)
-    og = [pyoracle.pid_gains(p, 0.0, d, cmdmax=80.0, cmdmin=-80.0) for p, d in gains]
+    q0 = np.array(icub_posture(names))
+    ow.set_joints(q0, np.zeros(n))
+    og = [pyoracle.pid_gains(p, 0.0, d, cmdmax=80.0, cmdmin=-80.0) for p, d in icub_pid_gains(names)]
     st = [pyoracle.OrPidState() for _ in range(n)]
     mode = np.full(n, pyoracle.FORCE, np.int32)
     qs, ps = [], []
     for k in range(HUMANOID_STEPS):
-        tau = np.array([pyoracle.pid_update(og[d], st[d], ow.q[d], 1e-3) for d in range(n)])
+        tau = np.array([pyoracle.pid_update(og[d], st[d], ow.q[d] - q0[d], 1e-3) for d in range(n)])
         ow.step(mode, tau)
         if k % HUMANOID_EVERY == HUMANOID_EVERY - 1:
             qs.append(ow.q.copy())
@@ -92,7 +91,7 @@ def humanoid():
     return dict(q=np.array(qs), p=np.array(ps), contact_fz=fz, joint_names=np.array(names))
 
 
-FIXTURES = {"cartpole_discrete": cartpole, "pendulum_swingup": pendulum, "humanoid_stand": humanoid}
+FIXTURES = {"cartpole_discrete": cartpole, "pendulum_swingup": pendulum, "icub_stand": icub}
 
 
 def main():

@@ -181,15 +181,21 @@ def test_warm_started_pgs_mode(oracle):
     within 1e-4 of the fixed-count step."""
     import ctypes
     from mwstep import get_model_file
-    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
+    cm = oracle.load_urdf(get_model_file("icub"), pose_xyz=ICUB_POSE[:3], pose_wxyz=ICUB_POSE[3:])
     n = cm.n
+    q0 = np.array(icub_posture(cm.joint_names))
+    kp, kd = np.array(icub_pid_gains(cm.joint_names)).T
+    hold = lambda w: np.clip(-kp * (w.q - q0) - kd * w.qd, -80, 80)
     mode = np.full(n, oracle.FORCE, np.int32)
     a = oracle.FloatWorld(cm, pgs_iters=50)
     b = oracle.FloatWorld(cm, pgs_iters=50, warm_start=True)
-    for _ in range(200):
-        a.step(mode, np.zeros(n))
+    for w in (a, b):
+        w.set_joints(q0, np.zeros(n))
+    for _ in range(600):           # lands (4 mm) and settles on its feet
+        a.step(mode, hold(a))
         b.warm[:] = 0.0            # cold every step: identical arithmetic
-        b.step(mode, np.zeros(n))
+        b.step(mode, hold(b))
     assert np.array_equal(a.q, b.q) and np.array_equal(a.V, b.V)
     # the record: normal impulses at 3 slot, their sum m g dt
     normals = b.warm[0:3 * oracle.OR_MAXFC:3]
@@ -203,10 +209,11 @@ def test_warm_started_pgs_mode(oracle):
     c.warm[:] = b.warm
     sweeps = []
     for _ in range(50):
-        c.step(mode, np.zeros(n))
+        tau = hold(b)
+        c.step(mode, tau)
         s = ctypes.c_int()
         oracle.lib().or_pgs_stats(ctypes.byref(s), None)
         sweeps.append(s.value)
-        b.step(mode, np.zeros(n))
+        b.step(mode, tau)
     assert np.mean(sweeps) < 50
     assert np.abs(c.q - b.q).max() <= 1e-4 and np.abs(c.p - b.p).max() <= 1e-5

@@ -49,23 +49,28 @@ def test_vecenv_matches_golden(require_gpu, task, name):
 
 
 def test_humanoid_matches_golden(require_gpu):
+    """BASELINE config 5's model as the reference wrapper inserts it
+    (icub_stand.npz: models/icub.urdf, the wrapper's posture and pose) under
+    the posture hold, free-running 600 steps against the fp64 fixture."""
     from mwstep import get_model_file
     from mwstep import native as N
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
     from mwstep.sim import Simulator
-    g = np.load(os.path.join(GOLDEN, "humanoid_stand.npz"))
+    g = np.load(os.path.join(GOLDEN, "icub_stand.npz"))
     import sys
     sys.path.insert(0, GOLDEN)
     import make_golden
-    sim = Simulator(get_model_file("humanoid32"), n_worlds=4, pgs_iters=50,
-                    pose=(0, 0, make_golden.HUMANOID_Z, 1, 0, 0, 0))
+    sim = Simulator(get_model_file("icub"), n_worlds=4, pgs_iters=50, pose=ICUB_POSE)
     assert list(sim.joint_names) == [str(s) for s in g["joint_names"]]
+    q0 = np.tile(icub_posture(sim.joint_names), (4, 1))
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
+    sim.set("reset_q", q0)
     sim.set_controller_period(1e-3)
-    for d, (p, dd) in enumerate(make_golden.humanoid_gains(sim.joint_names)):
+    for d, (p, dd) in enumerate(icub_pid_gains(sim.joint_names)):
         sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
     sim.set_control_mode(N.MODE_POSITION)
-    sim.set("position_target", np.zeros((4, sim.dofs)))
+    sim.set("position_target", q0)
     wq = wp = 0.0
     for k in range(make_golden.HUMANOID_STEPS):
         sim.run()
@@ -75,7 +80,7 @@ def test_humanoid_matches_golden(require_gpu):
             wp = max(wp, float(np.abs(sim.base_pose()[:, :3] - g["p"][i]).max()))
     fz = [sum(r[8] for r in sim.contacts(w)) for w in range(4)]
     sim.close()
-    print(f"humanoid vs golden: max|dq| {wq:.2e}, max|dp| {wp:.2e}, sum Fz {fz} vs {g['contact_fz'].sum():.3f}")
+    print(f"icub vs golden: max|dq| {wq:.2e}, max|dp| {wp:.2e}, sum Fz {fz} vs {g['contact_fz'].sum():.3f}")
     assert wq <= 1e-4 and wp <= 1e-5
     for f in fz:
         assert f == pytest.approx(float(g["contact_fz"].sum()), abs=0.5)

@@ -19,24 +19,26 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
-HUMANOID_Z = 0.535
-
-
 def _humanoid(W, drop=0.0):
+    """BASELINE config 5's model as the reference wrapper inserts it
+    (icub.py:19-40, :86), holding its posture (+ per-world offsets)."""
     from mwstep import get_model_file
     from mwstep import native as N
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
     from mwstep.sim import Simulator
-    sim = Simulator(get_model_file("humanoid32"), n_worlds=W, pgs_iters=50, pose=(0, 0, HUMANOID_Z + drop, 1, 0, 0, 0))
+    pose = (*ICUB_POSE[:2], ICUB_POSE[2] + drop, *ICUB_POSE[3:])
+    sim = Simulator(get_model_file("icub"), n_worlds=W, pgs_iters=50, pose=pose)
     assert sim.float_kernel() == 2
     sim.set_ground_plane(True, 1.0)
     sim.enable_contacts(True)
+    post = np.array(icub_posture(sim.joint_names))
+    sim.set("reset_q", np.tile(post, (W, 1)))
     sim.set_controller_period(1e-3)
-    for d, n in enumerate(sim.joint_names):
-        p, dd = (500.0, 5.0) if ("leg" in n or "torso" in n) else (50.0, 0.5)
+    for d, (p, dd) in enumerate(icub_pid_gains(sim.joint_names)):
         sim.set_pid(d, [p, 0.0, dd, -80.0, 80.0, 0.0, 0.0, -1.0])
     sim.set_control_mode(N.MODE_POSITION)
     rng = np.random.default_rng(3)
-    sim.set("position_target", rng.uniform(-0.1, 0.1, (W, sim.dofs)))
+    sim.set("position_target", post + rng.uniform(-0.1, 0.1, (W, sim.dofs)))
     return sim
 
 

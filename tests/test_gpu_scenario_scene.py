@@ -171,18 +171,18 @@ def test_multi_world_is_one_batched_scene(require_gpu):
 def test_model_total_mass(require_gpu):
     """Model::totalMass (Model.cpp:413-425): the sum of Link::mass over the
     links -- the CartPole's rail (welded to the world), cart and pole; the
-    humanoid's 36.4 kg; a subset of links."""
+    iCub-class model's 30.7 kg; a subset of links."""
     from scenario import core
     from scenario import gazebo as scenario
     gazebo, get_model_file = _gazebo()
     world = gazebo.get_world()
     assert world.set_physics_engine(scenario.PhysicsEngine_dart)
     assert world.insert_model(get_model_file("cartpole"))
-    assert world.insert_model(get_model_file("humanoid32"), core.Pose([2.0, 0, 0.6], [1., 0, 0, 0]), "h")
+    assert world.insert_model(get_model_file("icub"), core.Pose([2.0, 0, 0.6], [0., 0, 0, 1]), "h")
     cp, h = world.get_model("cartpole"), world.get_model("h")
     assert cp.total_mass() == pytest.approx(5.0 + 1.0 + 0.1, abs=1e-6)
     assert cp.total_mass(["cart", "pole"]) == pytest.approx(1.1, abs=1e-6)
-    assert h.total_mass() == pytest.approx(36.4, abs=1e-3)
+    assert h.total_mass() == pytest.approx(30.7, abs=1e-3)
     gazebo.close()
 
 

@@ -77,7 +77,7 @@ def test_panda_shards_bit_identical(require_gpu):
     del torch
 
 
-def _float_sim(model, W, q0, pose, vel, pgs_opts):
+def _float_sim(model, W, q0, pose, vel, pgs_opts, target=None):
     from mwstep import get_model_file
     from mwstep import native as N
     from mwstep.sim import Simulator
@@ -94,12 +94,12 @@ def _float_sim(model, W, q0, pose, vel, pgs_opts):
     for d in range(sim.dofs):
         sim.set_pid(d, [300.0, 0.0, 3.0, -80.0, 80.0, 0.0, 0.0, -1.0])
     sim.set_control_mode(N.MODE_POSITION)
-    sim.set("position_target", np.zeros_like(q0))
+    sim.set("position_target", np.zeros_like(q0) if target is None else np.tile(target, (W, 1)))
     return sim
 
 
-@pytest.mark.parametrize("model,z0,pgs_opts", [("humanoid32", 0.56, None),
-                                               ("humanoid32", 0.56, (1e-6, True)),
+@pytest.mark.parametrize("model,z0,pgs_opts", [("icub", 0.58, None),
+                                               ("icub", 0.58, (1e-6, True)),
                                                ("quadruped", 0.47, None)])
 def test_floating_shards_bit_identical(require_gpu, model, z0, pgs_opts):
     """BASELINE config 5 splits 512 humanoids over the ranks (bench.py
@@ -112,18 +112,22 @@ def test_floating_shards_bit_identical(require_gpu, model, z0, pgs_opts):
     from mwstep import get_model_file
     from mwstep.sim import Simulator
     p = Simulator(get_model_file(model), n_worlds=1)
-    n = p.dofs
+    n, names = p.dofs, list(p.joint_names)
     p.close()
-    q0 = rng.uniform(-0.1, 0.1, (W, n))
+    post = None
+    if model == "icub":   # the reference wrapper's posture (icub.py:19-40) as the hold target
+        from mwstep.models import icub_posture
+        post = np.array(icub_posture(names))
+    q0 = rng.uniform(-0.1, 0.1, (W, n)) + (0.0 if post is None else post)
     quat = rng.normal(size=(W, 4)) * np.array([1.0, 0.05, 0.05, 0.05])
     quat[:, 0] = np.abs(quat[:, 0]) + 1.0
     quat /= np.linalg.norm(quat, axis=1, keepdims=True)
     pose = np.column_stack([rng.uniform(-5, 5, (W, 2)), z0 + rng.uniform(0.0, 0.08, W), quat])
     vel = np.column_stack([rng.uniform(-0.5, 0.5, (W, 2)), rng.uniform(-0.3, 0.0, W), rng.uniform(-0.5, 0.5, (W, 3))])
-    full = _float_sim(model, W, q0, pose, vel, pgs_opts)
+    full = _float_sim(model, W, q0, pose, vel, pgs_opts, post)
     h = W // 2
-    halves = [_float_sim(model, h, q0[k * h:(k + 1) * h], pose[k * h:(k + 1) * h], vel[k * h:(k + 1) * h], pgs_opts)
-              for k in range(2)]
+    halves = [_float_sim(model, h, q0[k * h:(k + 1) * h], pose[k * h:(k + 1) * h], vel[k * h:(k + 1) * h], pgs_opts,
+                         post) for k in range(2)]
     for t in range(T):
         full.run()
         for s in halves:
@@ -151,7 +155,11 @@ def test_contact_answer_independent_of_world_count(require_gpu):
     rng = np.random.default_rng(5)
     W = 8192
     n = 8
-    q0 = rng.uniform(-0.1, 0.1, (W, n)) + np.array([0.6, -1.2] * 4)
+    post = None
+    if model == "icub":   # the reference wrapper's posture (icub.py:19-40) as the hold target
+        from mwstep.models import icub_posture
+        post = np.array(icub_posture(p.joint_names))
+    q0 = rng.uniform(-0.1, 0.1, (W, n)) + (0.0 if post is None else post) + np.array([0.6, -1.2] * 4)
     quat = rng.normal(size=(W, 4)) * np.array([1.0, 0.05, 0.05, 0.05])
     quat[:, 0] = np.abs(quat[:, 0]) + 1.0
     quat /= np.linalg.norm(quat, axis=1, keepdims=True)

@@ -19,7 +19,7 @@ def test_sim_world_wrenches_match_the_scene(require_gpu):
     from mwstep.scene import Scene
     from mwstep.sim import Simulator
     W, spr, runs = 8, 3, 15
-    path = get_model_file("humanoid32")
+    path = get_model_file("icub")
     text = open(path).read()
     pose = (0.0, 0.0, 1.0, 1.0, 0.0, 0.0, 0.0)
     sim = Simulator(path, n_worlds=W, steps_per_run=spr, pose=pose)

@@ -10,13 +10,16 @@ import numpy as np
 
 def _humanoid_stand(oracle, steps):
     from mwstep import get_model_file
-    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
+    cm = oracle.load_urdf(get_model_file("icub"), pose_xyz=ICUB_POSE[:3], pose_wxyz=ICUB_POSE[3:])
     ow = oracle.FloatWorld(cm, ground=True, mu=1.0, pgs_iters=oracle.PGS_CONVERGED)
     n = cm.n
+    post = np.array(icub_posture(cm.joint_names))
+    ow.set_joints(post, np.zeros(n))
     mode = np.full(n, oracle.FORCE, np.int32)
-    kp = np.array([500.0 if ("leg" in nm or "torso" in nm) else 50.0 for nm in cm.joint_names])
+    kp = np.array([p for p, _ in icub_pid_gains(cm.joint_names)])
     for _ in range(steps):
-        ow.step(mode, np.clip(-kp * ow.q - 0.01 * kp * ow.qd, -80, 80))
+        ow.step(mode, np.clip(-kp * (ow.q - post) - 0.01 * kp * ow.qd, -80, 80))
     return cm, ow
 
 

@@ -200,13 +200,16 @@ def test_converged_lcp_mode_is_exact(oracle):
         lo[rng.uniform(size=n) < 0.3] = 0.0
         x = oracle.pgs(A, b, lo, hi, iters=oracle.PGS_CONVERGED)
         np.testing.assert_allclose(x, _lcp_exact(A, b, lo, hi), atol=1e-9)
-    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.6))
+    from mwstep.models import icub_posture
+    cm = oracle.load_urdf(get_model_file("icub"), pose_xyz=(0, 0, 0.6), pose_wxyz=(0, 0, 0, 1))
     ow = oracle.FloatWorld(cm, pgs_iters=oracle.PGS_CONVERGED)
+    post = np.array(icub_posture(cm.joint_names))
+    ow.set_joints(post, np.zeros(cm.n))
     ow.set_twist([0.3, 0.0, 0.2], [0.5, -0.3, -0.5])
     mode = np.full(cm.n, oracle.FORCE, np.int32)
     n_contact = 0
     for _ in range(150):
-        n_contact = max(n_contact, ow.step(mode, np.clip(-500 * ow.q - 5 * ow.qd, -80, 80)))
+        n_contact = max(n_contact, ow.step(mode, np.clip(-500 * (ow.q - post) - 5 * ow.qd, -80, 80)))
         sweeps, res = oracle.pgs_stats()
         assert 0.0 <= res <= 1e-9
     assert n_contact >= 4

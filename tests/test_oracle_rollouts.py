@@ -40,13 +40,13 @@ def test_pid_rollout_equals_python_loop(oracle):
 
 def test_float_rollout_threads_match_sequential(oracle):
     from mwstep import get_model_file
-    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.535))
+    from mwstep.models import ICUB_POSE, icub_pid_gains, icub_posture
+    cm = oracle.load_urdf(get_model_file("icub"), pose_xyz=ICUB_POSE[:3], pose_wxyz=ICUB_POSE[3:])
     n = cm.n
-    gains = [oracle.pid_gains(500.0 if ("leg" in nm or "torso" in nm) else 50.0, 0.0,
-                              5.0 if ("leg" in nm or "torso" in nm) else 0.5, cmdmax=80.0, cmdmin=-80.0)
-             for nm in cm.joint_names]
+    gains = [oracle.pid_gains(p, 0.0, d, cmdmax=80.0, cmdmin=-80.0) for p, d in icub_pid_gains(cm.joint_names)]
+    post = np.array(icub_posture(cm.joint_names))
     rng = np.random.default_rng(1)
-    starts = [rng.uniform(-0.05, 0.05, n) for _ in range(4)]
+    starts = [post + rng.uniform(-0.05, 0.05, n) for _ in range(4)]
 
     def world(q0):
         fw = oracle.FloatWorld(cm, pgs_iters=oracle.PGS_CONVERGED)
@@ -56,15 +56,15 @@ def test_float_rollout_threads_match_sequential(oracle):
     seq = []
     for q0 in starts:
         fw = world(q0)
-        oracle.float_pid_rollout(fw, np.zeros(n), gains, 60)
+        oracle.float_pid_rollout(fw, post, gains, 60)
         seq.append((fw.q, fw.p))
     par = [world(q0) for q0 in starts]
-    th = [threading.Thread(target=oracle.float_pid_rollout, args=(fw, np.zeros(n), gains, 60)) for fw in par]
+    th = [threading.Thread(target=oracle.float_pid_rollout, args=(fw, post, gains, 60)) for fw in par]
     for t in th:
         t.start()
     for t in th:
         t.join()
     for (q, p), fw in zip(seq, par):
         assert np.array_equal(q, fw.q) and np.array_equal(p, fw.p)
-    # the standing humanoid stays on its feet
-    assert par[0].p[2] == pytest.approx(0.535, abs=0.02)
+    # the humanoid lands on its feet and stays up
+    assert par[0].p[2] == pytest.approx(0.565, abs=0.02)

@@ -78,7 +78,7 @@ def test_oracle_fixed_base_under_sanitizers(san, oracle, panda_file, tmp_path):
         assert np.array_equal(got, np.concatenate([rq, rqd])), np.abs(got - np.concatenate([rq, rqd])).max()
 
 
-@pytest.mark.parametrize("name", ["humanoid32", "quadruped"])
+@pytest.mark.parametrize("name", ["icub", "quadruped"])
 def test_oracle_floating_contacts_under_sanitizers(san, oracle, tmp_path, name):
     """A floating model dropped tilted onto the ground with random joint
     torques, exact two-stage LCP with warm starts, 40 steps: the final state
@@ -89,10 +89,14 @@ def test_oracle_floating_contacts_under_sanitizers(san, oracle, tmp_path, name):
     ow = oracle.FloatWorld(cm, ground=True, mu=0.8, pgs_iters=oracle.PGS_CONVERGED, warm_start=True)
     ang = 0.2
     R = np.array([[np.cos(ang), 0, np.sin(ang)], [0, 1, 0], [-np.sin(ang), 0, np.cos(ang)]])
-    z = 0.52 if name == "humanoid32" else 0.40
+    z = 0.56 if name == "icub" else 0.40
     ow.set_pose(np.array([0.1, -0.2, z]), R)
     ow.set_twist(rng.uniform(-0.5, 0.5, 3), rng.uniform(-0.3, 0.3, 3))
-    ow.set_joints(rng.uniform(-0.3, 0.3, n), rng.uniform(-1, 1, n))
+    q0 = np.zeros(n)
+    if name == "icub":
+        from mwstep.models import icub_posture
+        q0 = np.array(icub_posture(cm.joint_names))
+    ow.set_joints(q0 + rng.uniform(-0.3, 0.3, n), rng.uniform(-1, 1, n))
     mode = np.full(n, oracle.FORCE, np.int32)
     cmd = rng.uniform(-10, 10, n)
     case = tmp_path / f"{name}.bin"

@@ -29,7 +29,7 @@ def _cubes(oracle, poses, double=False, pgs=50):
 
 def test_single_floating_model_equals_float_step(oracle):
     from mwstep import get_model_file
-    cm = oracle.load_urdf(get_model_file("humanoid32"), pose_xyz=(0, 0, 0.56))
+    cm = oracle.load_urdf(get_model_file("icub"), pose_xyz=(0, 0, 0.66), pose_wxyz=(0, 0, 0, 1))
     sw = oracle.SceneWorld([cm], pgs_iters=50)
     fw = oracle.FloatWorld(cm, pgs_iters=50)
     for w in (sw,):
