@@ -105,6 +105,39 @@ def stage_boxes(p, x1):
     return (L1, U1), (L2, U2)
 
 
+# Contact detection (a box corner or sphere point below z = 0 at the start of
+# the step, Physics.cpp -> ODE/DART [EXT]) is a threshold: a point grazing
+# the plane within the fp32 resolution of its world position (~1e-7 m) can be
+# a contact for one precision and not the other.  GRAZE bounds that window.
+GRAZE = 1e-6
+
+
+def contact_set_gap(or_contacts, gpu_contacts, tol=1e-5):
+    """Contacts of the oracle's step that the GPU did not detect and the
+    GPU's that the oracle did not, matched by world point: ([oracle contact
+    index, depth], [GPU contact index, depth]).  or_contacts: FloatWorld
+    .contacts (point, force, depth, body); gpu_contacts: Simulator.contacts
+    rows (point 3, normal 3, force 3, depth)."""
+    gp = [np.asarray(r[:3], dtype=float) for r in gpu_contacts]
+    op = [np.asarray(c[0], dtype=float) for c in or_contacts]
+    only_or = [(i, float(c[2])) for i, c in enumerate(or_contacts)
+               if not any(np.abs(op[i] - g).max() <= tol for g in gp)]
+    only_gpu = [(i, float(r[9])) for i, r in enumerate(gpu_contacts)
+                if not any(np.abs(gp[i] - o).max() <= tol for o in op)]
+    return only_or, only_gpu
+
+
+def drop_contacts(p, contacts):
+    """The oracle's problem without the rows of the given contacts (contact
+    c owns rows 3c .. 3c + 2: contact rows come first, in detection order)."""
+    keep = np.ones(len(p["b"]), bool)
+    for c in contacts:
+        keep[3 * c:3 * c + 3] = False
+    q = {k: (v[keep] if isinstance(v, np.ndarray) and v.shape[:1] == keep.shape else v) for k, v in p.items()}
+    q["A"] = p["A"][np.ix_(keep, keep)]
+    return q
+
+
 def validity(p, state_row):
     """dict(ratio1, ratio2, ratio, missing) for one world: the GPU's stage-1
     and final impulses in the oracle's fp64 problem p (pyoracle.lcp_last
@@ -141,3 +174,25 @@ def oracle_ratio(p):
     e2, s2 = _complementarity(A, b, L2, U2, p["x"], bs)
     r1 = float((e1 / (REL_TOL * s1 + ABS_TOL)).max()) if S.any() else 0.0
     return max(r1, float((e2 / (REL_TOL * s2 + ABS_TOL)).max()))
+
+
+def judge(p, or_contacts, gpu_contacts, state_row):
+    """Is the GPU's step, which differs from the oracle's, a valid fp64 LCP
+    answer?  (ok, ratio, grazing): the contact sets may differ only by points
+    within GRAZE of the ground; an oracle-only grazing point's rows are
+    dropped from the problem before the GPU impulses are checked in it; a
+    GPU-only grazing point has no row in the oracle's problem (ok, ratio
+    nan: the callers count these, they cannot be checked); any other
+    difference of the contact sets is not ok."""
+    only_or, only_gpu = contact_set_gap(or_contacts, gpu_contacts)
+    grazing = [("oracle", dep) for _, dep in only_or] + [("GPU", dep) for _, dep in only_gpu]
+    if any(dep > GRAZE for _, dep in grazing):
+        return False, float("nan"), grazing
+    if only_gpu:
+        return True, float("nan"), grazing
+    if p is None:
+        return not only_or, 0.0, grazing
+    if only_or:
+        p = drop_contacts(p, [c for c, _ in only_or])
+    v = validity(p, state_row)
+    return v["ratio"] <= ACCEPT and v["missing"] == 0.0, v["ratio"], grazing

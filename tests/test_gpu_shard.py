@@ -155,11 +155,7 @@ def test_contact_answer_independent_of_world_count(require_gpu):
     rng = np.random.default_rng(5)
     W = 8192
     n = 8
-    post = None
-    if model == "icub":   # the reference wrapper's posture (icub.py:19-40) as the hold target
-        from mwstep.models import icub_posture
-        post = np.array(icub_posture(p.joint_names))
-    q0 = rng.uniform(-0.1, 0.1, (W, n)) + (0.0 if post is None else post) + np.array([0.6, -1.2] * 4)
+    q0 = rng.uniform(-0.1, 0.1, (W, n)) + np.array([0.6, -1.2] * 4)
     quat = rng.normal(size=(W, 4)) * np.array([1.0, 0.05, 0.05, 0.05])
     quat[:, 0] = np.abs(quat[:, 0]) + 1.0
     quat /= np.linalg.norm(quat, axis=1, keepdims=True)
