@@ -18,4 +18,14 @@ rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/session_$tag.log"; tail -2 "$OUT/smoke
 echo "== bench" | tee -a "$OUT/session_$tag.log"
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_$tag.json" 2> "$OUT/bench_$tag.err"
 rc=$?; echo "bench rc=$rc" | tee -a "$OUT/session_$tag.log"; tail -c 600 "$OUT/bench_$tag.json"; fatal $rc bench
+if [ "${TRACE:-1}" = "1" ]; then
+  # the driver's own command under the kernel tracer (no counters): the timed
+  # dispatches of the headline kernel (scripts/trace_summary.py)
+  echo "== rocprofv3 kernel trace of the driver command" | tee -a "$OUT/session_$tag.log"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$tag" -o run --output-format csv -- \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_prof_$tag.json" 2> "$OUT/prof_$tag.err"
+  rc=$?; echo "rocprof rc=$rc" | tee -a "$OUT/session_$tag.log"; fatal $rc rocprof
+  python scripts/trace_summary.py "$(find "$OUT/prof_$tag" -name 'run_kernel_trace.csv' | head -1)" "$OUT/bench_prof_$tag.json" \
+    > "$OUT/trace_summary_$tag.json"; cat "$OUT/trace_summary_$tag.json"
+fi
 exit 0
