@@ -8,6 +8,7 @@
 // capacity up front (no reallocation when a model is inserted mid-run), and a
 // model's presence in each world is a bit of a per-world mask.
 #include "mwscene.h"
+#include "mwstep_testhooks.h"
 
 #include <hip/hip_runtime.h>
 
@@ -22,6 +23,7 @@
 #include <vector>
 
 #include "errors.hpp"
+#include "hull.hpp"
 #include "model.hpp"
 #include "scene_params.hpp"
 
@@ -31,6 +33,27 @@ hipError_t launch_scene_run(const SceneF* P, int nv, const SceneDev& D, const Pi
 }
 
 namespace {
+
+// a hull (hull.hpp, fp64) as the scene kernel reads it (float32)
+void fill_hull(mw::ScHull& H, const mw::HostHull& h) {
+    H.nv = h.nv;
+    H.nf = h.nf;
+    H.ne = h.ne;
+    for (int k = 0; k < 3; ++k) H.ctr[k] = static_cast<float>(h.ctr[k]);
+    for (int i = 0; i < h.nv; ++i)
+        for (int k = 0; k < 3; ++k) H.v[i][k] = static_cast<float>(h.v[i][k]);
+    for (int f = 0; f < h.nf; ++f) {
+        for (int k = 0; k < 3; ++k) H.plane[f][k] = static_cast<float>(h.n[f][k]);
+        H.plane[f][3] = static_cast<float>(h.d[f]);
+        H.fnv[f] = static_cast<int8_t>(h.fnv[f]);
+        for (int t = 0; t < h.fnv[f]; ++t) H.fv[f][t] = static_cast<int8_t>(h.fv[f][t]);
+    }
+    for (int e = 0; e < h.ne; ++e)
+        for (int k = 0; k < 2; ++k) {
+            H.e[e][k] = static_cast<int8_t>(h.e[e][k]);
+            H.ef[e][k] = static_cast<int8_t>(h.ef[e][k]);
+        }
+}
 
 int fail(int code, const std::string& msg) {
     mw::set_last_error(msg);
@@ -185,6 +208,16 @@ int check_worlds(const mw_scene* s, int32_t w0, int32_t nw) {
 void build_params(mw_scene* s) {
     mw::SceneF& P = s->hp;
     std::memset(&P, 0, sizeof(P));
+    {
+        // the unit box's hull: every box's topology in the hull narrow phase
+        // (corners in the box slot order; oracle.c hull_box builds the same)
+        std::vector<std::array<double, 3>> corners;
+        for (int c = 0; c < 8; ++c)
+            corners.push_back({(c & 4) ? 1.0 : -1.0, (c & 2) ? 1.0 : -1.0, (c & 1) ? 1.0 : -1.0});
+        mw::HostHull h;
+        mw::build_hull(corners, h);
+        fill_hull(P.box_hull, h);
+    }
     const int K = static_cast<int>(s->models.size());
     P.n_models = K;
     P.ground = s->ground ? 1 : 0;
@@ -284,6 +317,16 @@ void build_params(mw_scene* s) {
             // a welded base link never touches the ground (it does not move)
             const bool movable = !(nd == node && !cm.floating);
             P.shape_slot0[shape] = slot;
+            P.shape_hull[shape] = -1;
+            if (sh.type == mw::Shape::Mesh && !mw::mesh_is_box(sh.points, sh.size)) {
+                mw::HostHull h;
+                if (mw::build_hull(sh.points, h)) {
+                    if (P.n_hulls >= mw::kScMaxHulls) throw std::runtime_error("a scene holds at most 8 mesh hulls");
+                    mw::ScHull& H = P.hull[P.n_hulls];
+                    fill_hull(H, h);
+                    P.shape_hull[shape] = static_cast<int8_t>(P.n_hulls++);
+                }
+            }
             if (movable) {
                 const int ns = (sh.type == mw::Shape::Sphere) ? 1
                                : (sh.type == mw::Shape::Mesh) ? static_cast<int>(sh.points.size())
@@ -1506,3 +1549,32 @@ int mw_scene_overflow(const mw_scene* s, int64_t* dropped) {
 }
 
 }  // extern "C"
+
+// ---- test hook (include/mwstep_testhooks.h): the hull the scene kernel's mesh
+// narrow phase uses for a point set (hull.hpp build_hull; host only) ----------
+extern "C" int mw_debug_hull(const double* pts, int32_t n, double* planes, int32_t* faces, int32_t* edges,
+                             int32_t* counts) {
+    if (!pts || !planes || !faces || !edges || !counts || n < 1 || n > mw::kHullMaxV) return MW_EINVAL;
+    std::vector<std::array<double, 3>> v(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) v[i] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    mw::HostHull h;
+    if (!mw::build_hull(v, h)) {
+        counts[0] = counts[1] = 0;
+        return MW_OK;
+    }
+    counts[0] = h.nf;
+    counts[1] = h.ne;
+    for (int f = 0; f < h.nf; ++f) {
+        for (int k = 0; k < 3; ++k) planes[4 * f + k] = h.n[f][k];
+        planes[4 * f + 3] = h.d[f];
+        faces[17 * f] = h.fnv[f];
+        for (int t = 0; t < h.fnv[f]; ++t) faces[17 * f + 1 + t] = h.fv[f][t];
+    }
+    for (int e = 0; e < h.ne; ++e) {
+        edges[4 * e] = h.e[e][0];
+        edges[4 * e + 1] = h.e[e][1];
+        edges[4 * e + 2] = h.ef[e][0];
+        edges[4 * e + 3] = h.ef[e][1];
+    }
+    return MW_OK;
+}

@@ -464,6 +464,156 @@ __device__ __forceinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& 
     return m;
 }
 
+// ---- the hull narrow phase of mesh shapes (round 6; oracle.c hull_pair) ----
+// A mesh collides with boxes and other meshes as the convex hull of its
+// support points (scene_params.hpp ScHull, built by hull.hpp on the host);
+// a box as the unit box hull scaled by its half extents.
+struct ScPoly {
+    const ScHull* H;
+    f3 s;      // vertex scale: the half extents of a box, 1 for a mesh
+    bool box;
+    __device__ __forceinline__ f3 v(int i) const { return {H->v[i][0] * s.x, H->v[i][1] * s.y, H->v[i][2] * s.z}; }
+    __device__ __forceinline__ f3 n(int f) const { return {H->plane[f][0], H->plane[f][1], H->plane[f][2]}; }
+    __device__ __forceinline__ float d(int f) const {
+        return box ? fabsf(H->plane[f][0]) * s.x + fabsf(H->plane[f][1]) * s.y + fabsf(H->plane[f][2]) * s.z
+                   : H->plane[f][3];
+    }
+    __device__ __forceinline__ f3 ctr() const { return {H->ctr[0] * s.x, H->ctr[1] * s.y, H->ctr[2] * s.z}; }
+};
+
+// closest points of segments p0 + s u, q0 + t v (s, t in [0, 1]): their midpoint
+__device__ __forceinline__ f3 sc_segment_mid(f3 p0, f3 p1, f3 q0, f3 q1) {
+    const f3 u = p1 - p0, v = q1 - q0, w = p0 - q0;
+    const float a = dot(u, u), b = dot(u, v), c = dot(v, v), d = dot(u, w), e = dot(v, w);
+    const float den = a * c - b * b;
+    float s = den > 1e-18f * a * c ? (b * e - c * d) / den : 0.f;
+    s = fminf(fmaxf(s, 0.f), 1.f);
+    float t = c > 0.f ? (b * s + e) / c : 0.f;
+    if (t < 0.f || t > 1.f) {
+        t = fminf(fmaxf(t, 0.f), 1.f);
+        s = a > 0.f ? (b * t - d) / a : 0.f;
+        s = fminf(fmaxf(s, 0.f), 1.f);
+    }
+    return 0.5f * ((p0 + s * u) + (q0 + t * v));
+}
+
+constexpr int kScClipMax = 24;   // clipped polygon (a hull face has <= 16 vertices; the oracle keeps 40)
+
+// Polytope A vs polytope B (shape frames (cA, RA), (cB, RB)): the separating-
+// axis test over both face-normal sets and the edge pairs whose Gauss-map
+// arcs cross (the faces of the Minkowski difference), reference-face clipping
+// of the incident face; the float32 restatement of oracle.c hull_pair (same
+// loops, tie rules and reduction).  Normal from B into A.  A call, not
+// inlined: only mesh pairs reach it.
+__device__ __noinline__ int sc_hull_pair(ScPoly A, f3 cA, M3 RA, ScPoly B, f3 cB, M3 RB, f3& n, f3* pts,
+                                         float* deps) {
+    float pen[2] = {3.0e38f, 3.0e38f};
+    int face[2] = {-1, -1};
+    for (int side = 0; side < 2; ++side) {
+        const ScPoly& H = side ? B : A;
+        const ScPoly& O = side ? A : B;
+        const M3& R = side ? RB : RA;
+        const M3& Ro = side ? RA : RB;
+        const f3 c = side ? cB : cA, co = side ? cA : cB;
+        for (int f = 0; f < H.H->nf; ++f) {
+            const f3 nw = mul(R, H.n(f));
+            const float dw = H.d(f) + dot(nw, c);
+            const f3 nl = mulT(Ro, nw);   // the normal in the other shape's frame
+            float mn = 3.0e38f;
+            for (int j = 0; j < O.H->nv; ++j) mn = fminf(mn, dot(nl, O.v(j)));
+            const float ov = dw - (mn + dot(nw, co));
+            if (ov < 0.f) return 0;
+            if (ov < pen[side]) { pen[side] = ov; face[side] = f; }
+        }
+    }
+    const f3 ca = cA + mul(RA, A.ctr()), cb = cB + mul(RB, B.ctr());
+    float pen_e = 3.0e38f;
+    f3 eaxis = {0.f, 0.f, 0.f};
+    int ea = -1, eb = -1;
+    for (int i = 0; i < A.H->ne; ++i) {
+        const f3 a = mul(RA, A.n(A.H->ef[i][0])), b = mul(RA, A.n(A.H->ef[i][1]));
+        const f3 bxa = cross(b, a);
+        const f3 pa0 = cA + mul(RA, A.v(A.H->e[i][0])), pa1 = cA + mul(RA, A.v(A.H->e[i][1]));
+        const f3 da = pa1 - pa0;
+        for (int j = 0; j < B.H->ne; ++j) {
+            const f3 c = -mul(RB, B.n(B.H->ef[j][0])), d = -mul(RB, B.n(B.H->ef[j][1]));
+            const f3 dxc = cross(d, c);
+            const float cba = dot(c, bxa), dba = dot(d, bxa), adc = dot(a, dxc), bdc = dot(b, dxc);
+            if (!(cba * dba < 0.f && adc * bdc < 0.f && cba * bdc > 0.f)) continue;
+            const f3 pb0 = cB + mul(RB, B.v(B.H->e[j][0])), pb1 = cB + mul(RB, B.v(B.H->e[j][1]));
+            const f3 db = pb1 - pb0;
+            f3 u = cross(da, db);
+            const float len = sqrtf(dot(u, u));
+            if (len <= 1e-6f * sqrtf(dot(da, da) * dot(db, db))) continue;
+            u = (1.f / len) * u;
+            if (dot(u, cb - ca) < 0.f) u = -u;   // A -> B
+            const f3 ul = mulT(RA, u), vl = mulT(RB, u);
+            float amax = -3.0e38f, bmin = 3.0e38f;
+            for (int p = 0; p < A.H->nv; ++p) amax = fmaxf(amax, dot(ul, A.v(p)));
+            for (int p = 0; p < B.H->nv; ++p) bmin = fminf(bmin, dot(vl, B.v(p)));
+            const float ov = (amax + dot(u, cA)) - (bmin + dot(u, cB));
+            if (ov < 0.f) return 0;
+            if (ov < pen_e) { pen_e = ov; ea = i; eb = j; eaxis = u; }
+        }
+    }
+    const bool refB = pen[1] < 0.95f * pen[0] - 1e-5f;
+    const float pen_f = refB ? pen[1] : pen[0];
+    if (ea >= 0 && pen_e < 0.95f * pen_f - 1e-5f) {
+        n = -eaxis;
+        pts[0] = sc_segment_mid(cA + mul(RA, A.v(A.H->e[ea][0])), cA + mul(RA, A.v(A.H->e[ea][1])),
+                                cB + mul(RB, B.v(B.H->e[eb][0])), cB + mul(RB, B.v(B.H->e[eb][1])));
+        deps[0] = pen_e;
+        return 1;
+    }
+    const ScPoly& Rp = refB ? B : A;
+    const ScPoly& Ip = refB ? A : B;
+    const M3& Rr = refB ? RB : RA;
+    const M3& Ri = refB ? RA : RB;
+    const f3 cr = refB ? cB : cA, ci = refB ? cA : cB;
+    const int fr = face[refB ? 1 : 0];
+    const f3 nr = mul(Rr, Rp.n(fr));   // pointing to the incident polytope
+    const float dr = Rp.d(fr) + dot(nr, cr);
+    int fi = 0;
+    float best = 3.0e38f;
+    for (int f = 0; f < Ip.H->nf; ++f) {
+        const float sdot = dot(mul(Ri, Ip.n(f)), nr);
+        if (sdot < best) { best = sdot; fi = f; }
+    }
+    f3 buf[2][kScClipMax];
+    int cnt = Ip.H->fnv[fi], cur = 0;
+    for (int k = 0; k < cnt; ++k) buf[0][k] = ci + mul(Ri, Ip.v(Ip.H->fv[fi][k]));
+    const int nrv = Rp.H->fnv[fr];
+    for (int k = 0; k < nrv && cnt > 0; ++k) {
+        const f3 r0 = cr + mul(Rr, Rp.v(Rp.H->fv[fr][k]));
+        const f3 r1 = cr + mul(Rr, Rp.v(Rp.H->fv[fr][(k + 1) % nrv]));
+        const f3 sn = cross(r1 - r0, nr);   // outward side-plane normal
+        const float s0 = dot(sn, r0);
+        int m = 0;
+        for (int i = 0; i < cnt; ++i) {
+            const f3 P = buf[cur][i], Q = buf[cur][(i + 1) % cnt];
+            const float dp = dot(sn, P) - s0, dq = dot(sn, Q) - s0;
+            if (dp <= 0.f && m < kScClipMax) buf[cur ^ 1][m++] = P;
+            if (((dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f)) && m < kScClipMax) {
+                const float t = dp / (dp - dq);
+                buf[cur ^ 1][m++] = P + t * (Q - P);
+            }
+        }
+        cnt = m;
+        cur ^= 1;
+    }
+    // the points below the reference face, compacted in place
+    float D8[kScClipMax];
+    int np = 0;
+    for (int i = 0; i < cnt; ++i) {
+        const float dep = dr - dot(nr, buf[cur][i]);
+        if (dep > 0.f) { buf[cur][np] = buf[cur][i]; D8[np] = dep; ++np; }
+    }
+    np = sc_reduce(np, buf[cur], D8);
+    n = refB ? nr : -nr;
+    for (int i = 0; i < np; ++i) { pts[i] = buf[cur][i]; deps[i] = D8[i]; }
+    return np;
+}
+
 // shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius,
 // 2 cylinder: size = {radius, half length}): normal from B into A, up to 4
 // points / depths
@@ -900,13 +1050,24 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                                  P->shape_R[sb][8]}};
                 const f3 ca = A_.pw + mul(A_.Rw, mk(P->shape_p[sa][0], P->shape_p[sa][1], P->shape_p[sa][2]));
                 const f3 cb = B_.pw + mul(B_.Rw, mk(P->shape_p[sb][0], P->shape_p[sb][1], P->shape_p[sb][2]));
-                // a mesh collides with other models as its bounding box (type 3 -> 0)
+                // a mesh with a hull against a box or such a mesh: the hull narrow
+                // phase; a box-shaped or flat mesh, and a mesh against a sphere or
+                // a cylinder, collide as the mesh's bounding box (type 3 -> 0)
+                const int ha = P->shape_type[sa] == 3 ? P->shape_hull[sa] : -1;
+                const int hb = P->shape_type[sb] == 3 ? P->shape_hull[sb] : -1;
                 const int ta = P->shape_type[sa] == 3 ? 0 : P->shape_type[sa];
                 const int tb = P->shape_type[sb] == 3 ? 0 : P->shape_type[sb];
-                np = sc_collide(ta, mk(P->shape_size[sa][0], P->shape_size[sa][1], P->shape_size[sa][2]),
-                                ca, mul3(A_.Rw, SRa), tb,
-                                mk(P->shape_size[sb][0], P->shape_size[sb][1], P->shape_size[sb][2]), cb,
-                                mul3(B_.Rw, SRb), nrm, pts, deps);
+                const f3 za = mk(P->shape_size[sa][0], P->shape_size[sa][1], P->shape_size[sa][2]);
+                const f3 zb = mk(P->shape_size[sb][0], P->shape_size[sb][1], P->shape_size[sb][2]);
+                if ((ha >= 0 || hb >= 0) && ta == 0 && tb == 0) {
+                    const ScPoly pa = ha >= 0 ? ScPoly{&P->hull[ha], mk(1.f, 1.f, 1.f), false}
+                                              : ScPoly{&P->box_hull, za, true};
+                    const ScPoly pb = hb >= 0 ? ScPoly{&P->hull[hb], mk(1.f, 1.f, 1.f), false}
+                                              : ScPoly{&P->box_hull, zb, true};
+                    np = sc_hull_pair(pa, ca, mul3(A_.Rw, SRa), pb, cb, mul3(B_.Rw, SRb), nrm, pts, deps);
+                } else {
+                    np = sc_collide(ta, za, ca, mul3(A_.Rw, SRa), tb, zb, cb, mul3(B_.Rw, SRb), nrm, pts, deps);
+                }
             }
         }
         int total = 0;

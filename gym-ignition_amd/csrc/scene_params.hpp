@@ -31,6 +31,21 @@ constexpr int kScMaxRows = 96;
 constexpr int kScWrenchSlots = 4;       // concurrent wrenches (distinct expiries) per link
 constexpr int kScMaxDepth = 12;         // tree depth of the response passes' stacks
 constexpr uint32_t kScGroundBit = 1u << 31;  // present mask: the world has a ground plane
+constexpr int kScMaxHulls = 8;          // mesh shapes with a collision hull (hull.hpp)
+
+// A mesh shape's collision hull (hull.hpp build_hull, float32, shape frame):
+// vertices, outward face planes (n, d: inside n . x <= d), face polygons
+// counter-clockwise seen from outside, edges, the vertex centroid.
+struct ScHull {
+    int32_t nv, nf, ne, pad_;
+    float ctr[4];
+    float v[16][4];
+    float plane[32][4];
+    int8_t fnv[32];
+    int8_t fv[32][16];
+    int8_t e[48][2];
+    int8_t ef[48][2];   // the two faces meeting at each edge
+};
 
 struct SceneModelF {
     int32_t floating;   // 1: DART FreeJoint root; 0: welded at (p0, R0)
@@ -85,6 +100,12 @@ struct SceneF {
     int16_t pair_b[kScMaxPairs];
     int16_t slot_shape[kScMaxGroundSlots];
     float slot_pt[kScMaxGroundSlots][3];  // mesh slots: support point in the shape frame
+    // mesh shapes against boxes and meshes of other models: the hull narrow
+    // phase (-1: a box-shaped or flat mesh, which collides as its bounding box)
+    int8_t shape_hull[kScMaxShapes];
+    int32_t n_hulls;
+    ScHull hull[kScMaxHulls];
+    ScHull box_hull;   // the unit box (half extents 1) as a hull: a box's topology for the hull narrow phase
 };
 
 // per-model JointController period gates of one launch (bit s: the PID of the

@@ -165,6 +165,7 @@ SC_VELOCITY_TARGET, SC_POSITION_TARGET, SC_RESET_POSITION, SC_RESET_VELOCITY, SC
 TEST_SIGNATURES = [
     ("mw_debug_lcp_solve", ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                           ctypes.c_uint64, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    ("mw_debug_hull", ctypes.c_int, [_D, _I, _D, _IP, _IP, _IP]),
 ]
 
 SCENE_SIGNATURES = [

@@ -21,6 +21,14 @@ extern "C" {
  * elimination over the lanes (lcp_ge_solve).  Returns 0 on success. */
 int mw_debug_lcp_solve(const float* A, const float* rhs, uint64_t free_mask, int32_t n, int32_t method, float* d);
 
+/* The convex hull the scene kernel's mesh narrow phase builds for n <= 16
+ * support points (csrc/hull.hpp build_hull, fp64, host only): counts = {faces,
+ * edges} (0, 0 for a flat set); planes [32][4] = outward normal, offset (inside
+ * n . x <= d); faces [32][17] = vertex count, then the polygon's vertex
+ * indices counter-clockwise seen from outside; edges [48][4] = the two
+ * vertices, then the two faces meeting there.  Returns 0 (MW_OK). */
+int mw_debug_hull(const double* pts, int32_t n, double* planes, int32_t* faces, int32_t* edges, int32_t* counts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2411,6 +2411,339 @@ static int cylinder_pair(int ta, const double* ha, const double* ca, const doubl
     return m;
 }
 
+/* world point of a shape-frame point: c + R v (R row-major) */
+static void mat_vec3(const double* R, const double* v, const double* c, double* out)
+{
+    for (int r = 0; r < 3; ++r) out[r] = c[r] + R[3 * r] * v[0] + R[3 * r + 1] * v[1] + R[3 * r + 2] * v[2];
+}
+
+static void rot3(const double* R, const double* v, double* out)
+{
+    for (int r = 0; r < 3; ++r) out[r] = R[3 * r] * v[0] + R[3 * r + 1] * v[1] + R[3 * r + 2] * v[2];
+}
+
+/* ---------------- convex hulls of mesh shapes (narrow phase) ----------------
+ * The reference attaches a <mesh> collision to DART as its triangle mesh
+ * (Physics.cpp:897-931) [EXT].  Restated here as the convex hull of the mesh
+ * shape's support points (the same <= OR_MESH_MAXP hull vertices that touch
+ * the ground plane; a mesh with at most that many hull vertices gets its
+ * exact hull), colliding with boxes and other meshes by the separating-axis
+ * test over face normals and edge-pair directions, with the reference face
+ * clipped against the incident face as box_box does (round 6: replaces the
+ * bounding-box stand-in).  Built in fp64 by brute force: a face is a plane
+ * through three points with every point on its inner side; coplanar points
+ * share one polygon face, ordered counter-clockwise seen from outside. */
+typedef struct {
+    int nv, nf, ne;
+    double v[OR_MESH_MAXP][3];
+    double n[OR_HULL_MAXF][3];
+    double d[OR_HULL_MAXF];                 /* inside: n . x <= d */
+    int fnv[OR_HULL_MAXF];
+    int fv[OR_HULL_MAXF][OR_MESH_MAXP];
+    int e[OR_HULL_MAXE][2];
+    int ef[OR_HULL_MAXE][2];                /* the two faces meeting at each edge */
+    double ctr[3];                          /* vertex centroid (interior) */
+} or_hull;
+
+static int or_hull_make(int np, const double* pts, or_hull* h)
+{
+    memset(h, 0, sizeof *h);
+    if (np > OR_MESH_MAXP) np = OR_MESH_MAXP;
+    h->nv = np;
+    double scale = 0.0;
+    for (int i = 0; i < np; ++i)
+        for (int k = 0; k < 3; ++k) {
+            h->v[i][k] = pts[3 * i + k];
+            h->ctr[k] += pts[3 * i + k] / np;
+            scale = fabs(pts[3 * i + k]) > scale ? fabs(pts[3 * i + k]) : scale;
+        }
+    const double eps = 1e-9 * (scale > 0.0 ? scale : 1.0);
+    for (int i = 0; i < np; ++i)
+        for (int j = i + 1; j < np; ++j)
+            for (int k = j + 1; k < np; ++k) {
+                double a[3], b[3], n[3];
+                for (int q = 0; q < 3; ++q) { a[q] = h->v[j][q] - h->v[i][q]; b[q] = h->v[k][q] - h->v[i][q]; }
+                cross3(a, b, n);
+                const double len = sqrt(dot3(n, n));
+                if (len <= 1e-12 * (scale * scale > 0.0 ? scale * scale : 1.0)) continue;   /* collinear */
+                for (int q = 0; q < 3; ++q) n[q] /= len;
+                double d = dot3(n, h->v[i]), hi = -INFINITY, lo = INFINITY;
+                for (int m = 0; m < np; ++m) {
+                    const double s = dot3(n, h->v[m]) - d;
+                    hi = s > hi ? s : hi;
+                    lo = s < lo ? s : lo;
+                }
+                if (hi > eps && lo < -eps) continue;      /* points on both sides: not a face */
+                if (hi > eps) {                          /* all above: the outward normal is -n */
+                    for (int q = 0; q < 3; ++q) n[q] = -n[q];
+                    d = -d;
+                }
+                int dup = 0;
+                for (int f = 0; f < h->nf && !dup; ++f)
+                    dup = fabs(dot3(h->n[f], n) - 1.0) < 1e-9 && fabs(h->d[f] - d) <= 4 * eps;
+                if (dup || h->nf >= OR_HULL_MAXF) continue;
+                const int f = h->nf++;
+                memcpy(h->n[f], n, sizeof n);
+                h->d[f] = d;
+            }
+    if (h->nf < 4) return 0;   /* flat or degenerate point set: no volume */
+    /* face polygons: the points on each plane, counter-clockwise about n */
+    for (int f = 0; f < h->nf; ++f) {
+        double c[3] = {0, 0, 0}, u[3], w[3], ang[OR_MESH_MAXP];
+        int idx[OR_MESH_MAXP], m = 0;
+        for (int i = 0; i < np; ++i)
+            if (fabs(dot3(h->n[f], h->v[i]) - h->d[f]) <= 4 * eps) idx[m++] = i;
+        for (int t = 0; t < m; ++t)
+            for (int q = 0; q < 3; ++q) c[q] += h->v[idx[t]][q] / m;
+        for (int q = 0; q < 3; ++q) u[q] = h->v[idx[0]][q] - c[q];
+        const double ul = sqrt(dot3(u, u));
+        for (int q = 0; q < 3; ++q) u[q] /= ul;
+        cross3(h->n[f], u, w);
+        for (int t = 0; t < m; ++t) {
+            double r[3] = {h->v[idx[t]][0] - c[0], h->v[idx[t]][1] - c[1], h->v[idx[t]][2] - c[2]};
+            ang[t] = atan2(dot3(r, w), dot3(r, u));
+        }
+        for (int a = 1; a < m; ++a)        /* insertion sort by angle */
+            for (int b = a; b > 0 && ang[b] < ang[b - 1]; --b) {
+                const double ta = ang[b]; ang[b] = ang[b - 1]; ang[b - 1] = ta;
+                const int ti = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = ti;
+            }
+        h->fnv[f] = m;
+        for (int t = 0; t < m; ++t) h->fv[f][t] = idx[t];
+        for (int t = 0; t < m; ++t) {
+            int a = idx[t], b = idx[(t + 1) % m];
+            if (a > b) { const int x = a; a = b; b = x; }
+            int seen = -1;
+            for (int e = 0; e < h->ne && seen < 0; ++e) if (h->e[e][0] == a && h->e[e][1] == b) seen = e;
+            if (seen >= 0) h->ef[seen][1] = f;
+            else if (h->ne < OR_HULL_MAXE) {
+                h->e[h->ne][0] = a; h->e[h->ne][1] = b;
+                h->ef[h->ne][0] = h->ef[h->ne][1] = f;
+                ++h->ne;
+            }
+        }
+    }
+    return 1;
+}
+
+int or_hull_build(int np, const double* pts, or_hull_info* info)
+{
+    or_hull h;
+    const int ok = or_hull_make(np, pts, &h);
+    if (info) {
+        info->nv = h.nv;
+        info->nf = ok ? h.nf : 0;
+        info->ne = ok ? h.ne : 0;
+        for (int f = 0; f < info->nf; ++f) {
+            info->n[f][0] = h.n[f][0]; info->n[f][1] = h.n[f][1]; info->n[f][2] = h.n[f][2];
+            info->d[f] = h.d[f];
+            info->fnv[f] = h.fnv[f];
+            for (int k = 0; k < h.fnv[f]; ++k) info->fv[f][k] = h.fv[f][k];
+        }
+        for (int e = 0; e < info->ne; ++e) {
+            info->e[e][0] = h.e[e][0]; info->e[e][1] = h.e[e][1];
+            info->ef[e][0] = h.ef[e][0]; info->ef[e][1] = h.ef[e][1];
+        }
+    }
+    return ok ? h.nf : 0;
+}
+
+/* the box as a hull: corners in the box slot order (bit 2: x, bit 1: y, bit 0: z) */
+static void hull_box(const double* half, or_hull* h)
+{
+    double p[8][3];
+    for (int c = 0; c < 8; ++c) {
+        p[c][0] = (c & 4 ? 1.0 : -1.0) * half[0];
+        p[c][1] = (c & 2 ? 1.0 : -1.0) * half[1];
+        p[c][2] = (c & 1 ? 1.0 : -1.0) * half[2];
+    }
+    or_hull_make(8, &p[0][0], h);
+}
+
+/* closest points of segments p0 + s u, q0 + t v (s in [0, 1], t in [0, 1]) */
+static void segment_closest(const double* p0, const double* p1, const double* q0, const double* q1, double* mid)
+{
+    double u[3], v[3], w[3];
+    for (int k = 0; k < 3; ++k) { u[k] = p1[k] - p0[k]; v[k] = q1[k] - q0[k]; w[k] = p0[k] - q0[k]; }
+    const double a = dot3(u, u), b = dot3(u, v), c = dot3(v, v), d = dot3(u, w), e = dot3(v, w);
+    const double den = a * c - b * b;
+    double s = den > 1e-18 * a * c ? (b * e - c * d) / den : 0.0;
+    s = s < 0.0 ? 0.0 : (s > 1.0 ? 1.0 : s);
+    double t = c > 0.0 ? (b * s + e) / c : 0.0;
+    if (t < 0.0 || t > 1.0) {
+        t = t < 0.0 ? 0.0 : 1.0;
+        s = a > 0.0 ? (b * t - d) / a : 0.0;
+        s = s < 0.0 ? 0.0 : (s > 1.0 ? 1.0 : s);
+    }
+    for (int k = 0; k < 3; ++k) mid[k] = 0.5 * ((p0[k] + s * u[k]) + (q0[k] + t * v[k]));
+}
+
+#define OR_HULL_CLIP 24   /* clipped polygon capacity (the scene kernel's kScClipMax) */
+
+/* hull A vs hull B (shape frames at (cA, RA), (cB, RB)): the separating-axis
+ * test over A's and B's face normals and every edge-pair direction (the
+ * smallest overlap over those axes is the penetration depth of two convex
+ * polytopes); the reference face is the face axis of least overlap (A's
+ * unless B's is smaller by 5 % + 1e-5, as box_box prefers faces over edges),
+ * the incident face the other hull's face most anti-parallel to it, clipped
+ * against the reference face's side planes; an edge pair wins only below
+ * 0.95 x the face overlap - 1e-5 (one point: the closest points' midpoint).
+ * Normal from B into A, points on the incident surface, depths along it. */
+static int hull_pair(const or_hull* A, const double* cA, const double* RA, const or_hull* B, const double* cB,
+                     const double* RB, double n[3], double* pts, double* deps)
+{
+    double WA[OR_MESH_MAXP][3], WB[OR_MESH_MAXP][3], ca[3], cb[3];
+    for (int i = 0; i < A->nv; ++i) mat_vec3(RA, A->v[i], cA, WA[i]);
+    for (int i = 0; i < B->nv; ++i) mat_vec3(RB, B->v[i], cB, WB[i]);
+    mat_vec3(RA, A->ctr, cA, ca);
+    mat_vec3(RB, B->ctr, cB, cb);
+    double pen[2] = {INFINITY, INFINITY};
+    int face[2] = {-1, -1};
+    for (int side = 0; side < 2; ++side) {
+        const or_hull* H = side ? B : A;
+        const double* R = side ? RB : RA;
+        const double* c = side ? cB : cA;
+        double (*Wo)[3] = side ? WA : WB;
+        const int no = side ? A->nv : B->nv;
+        for (int f = 0; f < H->nf; ++f) {
+            double nw[3];
+            rot3(R, H->n[f], nw);
+            const double dw = H->d[f] + dot3(nw, c);
+            double mn = INFINITY;
+            for (int j = 0; j < no; ++j) {
+                const double s = dot3(nw, Wo[j]);
+                mn = s < mn ? s : mn;
+            }
+            const double ov = dw - mn;
+            if (ov < 0.0) return 0;
+            if (ov < pen[side]) { pen[side] = ov; face[side] = f; }
+        }
+    }
+    double pen_e = INFINITY, eaxis[3] = {0, 0, 0};
+    int ea = -1, eb = -1;
+    for (int i = 0; i < A->ne; ++i)
+        for (int j = 0; j < B->ne; ++j) {
+            /* only edge pairs whose Gauss-map arcs cross (a face of the
+             * Minkowski difference; Gregorius 2013): the others never hold
+             * the least overlap */
+            double a[3], b[3], c[3], d[3], bxa[3], dxc[3];
+            rot3(RA, A->n[A->ef[i][0]], a);
+            rot3(RA, A->n[A->ef[i][1]], b);
+            rot3(RB, B->n[B->ef[j][0]], c);
+            rot3(RB, B->n[B->ef[j][1]], d);
+            for (int k = 0; k < 3; ++k) { c[k] = -c[k]; d[k] = -d[k]; }
+            cross3(b, a, bxa);
+            cross3(d, c, dxc);
+            const double cba = dot3(c, bxa), dba = dot3(d, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
+            if (!(cba * dba < 0.0 && adc * bdc < 0.0 && cba * bdc > 0.0)) continue;
+            double da[3], db[3], u[3];
+            for (int k = 0; k < 3; ++k) {
+                da[k] = WA[A->e[i][1]][k] - WA[A->e[i][0]][k];
+                db[k] = WB[B->e[j][1]][k] - WB[B->e[j][0]][k];
+            }
+            cross3(da, db, u);
+            const double len = sqrt(dot3(u, u));
+            if (len <= 1e-6 * sqrt(dot3(da, da) * dot3(db, db))) continue;   /* parallel edges */
+            for (int k = 0; k < 3; ++k) u[k] /= len;
+            const double dc[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
+            if (dot3(u, dc) < 0.0) for (int k = 0; k < 3; ++k) u[k] = -u[k];   /* A -> B */
+            double amax = -INFINITY, bmin = INFINITY;
+            for (int p = 0; p < A->nv; ++p) { const double s = dot3(u, WA[p]); amax = s > amax ? s : amax; }
+            for (int p = 0; p < B->nv; ++p) { const double s = dot3(u, WB[p]); bmin = s < bmin ? s : bmin; }
+            const double ov = amax - bmin;
+            if (ov < 0.0) return 0;
+            if (ov < pen_e) { pen_e = ov; ea = i; eb = j; memcpy(eaxis, u, sizeof u); }
+        }
+    const int refB = pen[1] < 0.95 * pen[0] - 1e-5;
+    const double pen_f = refB ? pen[1] : pen[0];
+    if (ea >= 0 && pen_e < 0.95 * pen_f - 1e-5) {
+        for (int k = 0; k < 3; ++k) n[k] = -eaxis[k];
+        segment_closest(WA[A->e[ea][0]], WA[A->e[ea][1]], WB[B->e[eb][0]], WB[B->e[eb][1]], pts);
+        deps[0] = pen_e;
+        return 1;
+    }
+    const or_hull* Rh = refB ? B : A;
+    const or_hull* Ih = refB ? A : B;
+    const double* Rr = refB ? RB : RA;
+    const double* Ri = refB ? RA : RB;
+    double (*Wr)[3] = refB ? WB : WA;
+    double (*Wi)[3] = refB ? WA : WB;
+    const int fr = face[refB ? 1 : 0];
+    double nr[3];
+    rot3(Rr, Rh->n[fr], nr);                           /* reference normal, pointing to the incident hull */
+    const double dr = Rh->d[fr] + dot3(nr, refB ? cB : cA);
+    int fi = 0;
+    double best = INFINITY;
+    for (int f = 0; f < Ih->nf; ++f) {
+        double nw[3];
+        rot3(Ri, Ih->n[f], nw);
+        const double s = dot3(nw, nr);
+        if (s < best) { best = s; fi = f; }
+    }
+    double buf[2][OR_HULL_CLIP][3];
+    int cnt = Ih->fnv[fi], cur = 0;
+    for (int k = 0; k < cnt; ++k) memcpy(buf[0][k], Wi[Ih->fv[fi][k]], sizeof buf[0][k]);
+    for (int k = 0; k < Rh->fnv[fr] && cnt > 0; ++k) {
+        const double* r0 = Wr[Rh->fv[fr][k]];
+        const double* r1 = Wr[Rh->fv[fr][(k + 1) % Rh->fnv[fr]]];
+        double e[3] = {r1[0] - r0[0], r1[1] - r0[1], r1[2] - r0[2]}, sn[3];
+        cross3(e, nr, sn);                              /* outward side-plane normal */
+        int m = 0;
+        for (int i = 0; i < cnt; ++i) {
+            const double* P = buf[cur][i];
+            const double* Q = buf[cur][(i + 1) % cnt];
+            const double dp = dot3(sn, P) - dot3(sn, r0), dq = dot3(sn, Q) - dot3(sn, r0);
+            if (dp <= 0.0 && m < OR_HULL_CLIP) memcpy(buf[cur ^ 1][m++], P, sizeof buf[0][0]);
+            if (((dp < 0.0 && dq > 0.0) || (dp > 0.0 && dq < 0.0)) && m < OR_HULL_CLIP) {
+                const double t = dp / (dp - dq);
+                for (int q = 0; q < 3; ++q) buf[cur ^ 1][m][q] = P[q] + t * (Q[q] - P[q]);
+                ++m;
+            }
+        }
+        cnt = m;
+        cur ^= 1;
+    }
+    double P8[OR_HULL_CLIP][3], D8[OR_HULL_CLIP];
+    int np = 0;
+    for (int i = 0; i < cnt; ++i) {
+        const double dep = dr - dot3(nr, buf[cur][i]);
+        if (dep > 0.0) { memcpy(P8[np], buf[cur][i], sizeof P8[np]); D8[np] = dep; ++np; }
+    }
+    np = reduce_points(np, P8, D8);
+    for (int k = 0; k < 3; ++k) n[k] = refB ? nr[k] : -nr[k];
+    for (int i = 0; i < np; ++i) {
+        memcpy(pts + 3 * i, P8[i], 3 * sizeof(double));
+        deps[i] = D8[i];
+    }
+    return np;
+}
+
+/* A mesh whose support points are exactly its bounding box's 8 corners is
+ * that box (it collides through box_box, bit for bit like the box). */
+static int mesh_is_box(int type, const double* size, int npts, const double* pts)
+{
+    if (type != 3 || npts != 8) return 0;
+    int corners = 0;
+    for (int i = 0; i < 8; ++i) {
+        int ok = 1;
+        for (int k = 0; k < 3; ++k) ok = ok && fabs(fabs(pts[3 * i + k]) - size[k]) <= 1e-12 * (1.0 + size[k]);
+        corners |= ok << ((pts[3 * i] > 0) * 4 + (pts[3 * i + 1] > 0) * 2 + (pts[3 * i + 2] > 0));
+    }
+    return corners == 0xff;
+}
+
+/* a mesh shape (type 3) against a box or another mesh: the hull narrow
+ * phase; npts / pts: the mesh shapes' support points (shape frame) */
+int or_collide_hull(int type_a, const double* size_a, int npts_a, const double* pts_a, const double* c_a,
+                    const double* R_a, int type_b, const double* size_b, int npts_b, const double* pts_b,
+                    const double* c_b, const double* R_b, double normal[3], double* points, double* depths)
+{
+    static _Thread_local or_hull ha, hb;
+    if (type_a == 3) { if (!or_hull_make(npts_a, pts_a, &ha)) hull_box(size_a, &ha); } else hull_box(size_a, &ha);
+    if (type_b == 3) { if (!or_hull_make(npts_b, pts_b, &hb)) hull_box(size_b, &hb); } else hull_box(size_b, &hb);
+    return hull_pair(&ha, c_a, R_a, &hb, c_b, R_b, normal, points, depths);
+}
+
 int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
                const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
                double* depths)
@@ -2610,11 +2943,23 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
                         }
                     }
                     double nrm[3], pts[12], deps[4];
-                    /* a mesh collides with other models as its bounding box */
-                    const int ta = A->shape_type[sa] == 3 ? 0 : A->shape_type[sa];
-                    const int tb = B->shape_type[sb] == 3 ? 0 : B->shape_type[sb];
-                    const int np = or_collide(ta, A->shape_size[sa], cA, RA, tb, B->shape_size[sb], cB, RB, nrm, pts,
-                                              deps);
+                    const int ta0 = A->shape_type[sa], tb0 = B->shape_type[sb];
+                    int np;
+                    const int ta1 = mesh_is_box(ta0, A->shape_size[sa], A->shape_npts[sa], &A->shape_pts[sa][0][0])
+                                        ? 0 : ta0;
+                    const int tb1 = mesh_is_box(tb0, B->shape_size[sb], B->shape_npts[sb], &B->shape_pts[sb][0][0])
+                                        ? 0 : tb0;
+                    if ((ta1 == 3 && (tb1 == 0 || tb1 == 3)) || (tb1 == 3 && ta1 == 0)) {
+                        /* a mesh against a box or a mesh: the hull narrow phase */
+                        np = or_collide_hull(ta1, A->shape_size[sa], A->shape_npts[sa], &A->shape_pts[sa][0][0], cA,
+                                             RA, tb1, B->shape_size[sb], B->shape_npts[sb], &B->shape_pts[sb][0][0],
+                                             cB, RB, nrm, pts, deps);
+                    } else {
+                        /* a box-shaped mesh is its box; a mesh against a sphere or a
+                         * cylinder: its bounding box */
+                        const int ta = ta1 == 3 ? 0 : ta1, tb = tb1 == 3 ? 0 : tb1;
+                        np = or_collide(ta, A->shape_size[sa], cA, RA, tb, B->shape_size[sb], cB, RB, nrm, pts, deps);
+                    }
                     for (int i = 0; i < np && nc < OR_SC_MAXC; ++i) {
                         memcpy(cp[nc], pts + 3 * i, sizeof cp[nc]);
                         memcpy(cn[nc], nrm, sizeof nrm);

@@ -157,6 +157,8 @@ int or_free_step(const or_free_model* m, double dt, or_free_state* s, int pgs_it
 #define OR_MAXFS 16
 #define OR_MAXFC (8 * OR_MAXFS)
 #define OR_MESH_MAXP 16
+#define OR_HULL_MAXF 32   /* faces of a hull of <= OR_MESH_MAXP points (<= 2 n - 4 triangles) */
+#define OR_HULL_MAXE 48   /* edges (<= 3 n - 6) */
 
 typedef struct {
     or_model tree;               /* moving bodies; parent -1 = the base body  */
@@ -338,6 +340,27 @@ int or_scene_step(const or_scene_model* m, double dt, or_scene_state* st, const 
 /* shape-frame point of ground-contact slot c (box corner, sphere centre,
  * cylinder rim point); RS = the shape's world rotation */
 void or_slot_point(int type, const double* h, const double* RS, int c, double l[3]);
+/* Convex hull of a mesh shape's support points (np <= OR_MESH_MAXP, fp64,
+ * brute force; coplanar points share one face, counter-clockwise seen from
+ * outside): outward unit normals n, offsets d (inside n . x <= d), the face
+ * polygons and the edges.  Returns the face count, 0 for a flat point set. */
+typedef struct {
+    int32_t nv, nf, ne;
+    double n[OR_HULL_MAXF][3];
+    double d[OR_HULL_MAXF];
+    int32_t fnv[OR_HULL_MAXF];
+    int32_t fv[OR_HULL_MAXF][OR_MESH_MAXP];
+    int32_t e[OR_HULL_MAXE][2];
+    int32_t ef[OR_HULL_MAXE][2];   /* the two faces meeting at each edge */
+} or_hull_info;
+int or_hull_build(int np, const double* pts, or_hull_info* info);
+/* The hull narrow phase of a mesh shape (type 3) against a box (0) or
+ * another mesh: SAT over face normals and edge pairs, reference-face
+ * clipping (same outputs as or_collide: normal from B into A, <= 4 points
+ * with their depths); a mesh's npts / pts are its support points. */
+int or_collide_hull(int type_a, const double* size_a, int npts_a, const double* pts_a, const double* c_a,
+                    const double* R_a, int type_b, const double* size_b, int npts_b, const double* pts_b,
+                    const double* c_b, const double* R_b, double normal[3], double* points, double* depths);
 int or_collide(int type_a, const double* size_a, const double* c_a, const double* R_a, int type_b,
                const double* size_b, const double* c_b, const double* R_b, double normal[3], double* points,
                double* depths);

@@ -1194,6 +1194,47 @@ def collide(type_a, size_a, c_a, R_a, type_b, size_b, c_b, R_b):
     return n, pts[:3 * k].reshape(k, 3), dep[:k]
 
 
+OR_HULL_MAXF, OR_HULL_MAXE = 32, 48
+
+
+class OrHullInfo(ctypes.Structure):
+    _fields_ = [("nv", ctypes.c_int32), ("nf", ctypes.c_int32), ("ne", ctypes.c_int32),
+                ("n", (ctypes.c_double * 3) * OR_HULL_MAXF), ("d", ctypes.c_double * OR_HULL_MAXF),
+                ("fnv", ctypes.c_int32 * OR_HULL_MAXF), ("fv", (ctypes.c_int32 * 16) * OR_HULL_MAXF),
+                ("e", (ctypes.c_int32 * 2) * OR_HULL_MAXE), ("ef", (ctypes.c_int32 * 2) * OR_HULL_MAXE)]
+
+
+def hull(points):
+    """or_hull_build: the convex hull the mesh narrow phase uses for these
+    support points -- dict(n [F, 3] outward normals, d [F], faces: list of
+    vertex-index polygons (counter-clockwise seen from outside), edges [E, 2],
+    edge_faces [E, 2]); None for a flat point set."""
+    pts = np.ascontiguousarray(np.asarray(points, dtype=float).reshape(-1, 3))
+    info = OrHullInfo()
+    f = lib().or_hull_build
+    f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(OrHullInfo)]
+    nf = f(len(pts), _p(pts), ctypes.byref(info))
+    if nf <= 0:
+        return None
+    return dict(n=np.array([info.n[i][:] for i in range(nf)]), d=np.array(info.d[:nf]),
+                faces=[list(info.fv[i][:info.fnv[i]]) for i in range(nf)],
+                edges=np.array([info.e[i][:] for i in range(info.ne)]),
+                edge_faces=np.array([info.ef[i][:] for i in range(info.ne)]))
+
+
+def collide_hull(type_a, size_a, pts_a, c_a, R_a, type_b, size_b, pts_b, c_b, R_b):
+    """or_collide_hull (a mesh against a box or a mesh): (normal from B into
+    A, points [k][3], depths [k]); pts_*: a mesh's support points (shape frame)."""
+    n, pts, dep = np.zeros(3), np.zeros(12), np.zeros(4)
+    f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=float).reshape(-1))
+    pa = f(pts_a if pts_a is not None else np.zeros(3))
+    pb = f(pts_b if pts_b is not None else np.zeros(3))
+    k = lib().or_collide_hull(int(type_a), _p(f(size_a)), len(pa) // 3, _p(pa), _p(f(c_a)), _p(f(R_a)),
+                              int(type_b), _p(f(size_b)), len(pb) // 3, _p(pb), _p(f(c_b)), _p(f(R_b)),
+                              _p(n), _p(pts), _p(dep))
+    return n, pts[:3 * k].reshape(k, 3), dep[:k]
+
+
 class SceneWorld:
     """fp64 scene (or_scene_step): several models in one world, each on a
     fixed or floating base, ground plane, shape-pair contacts between models,

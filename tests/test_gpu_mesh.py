@@ -1,15 +1,21 @@
 """GPU tests of mesh collisions (reference Physics.cpp:897-931) on the scene
 kernel (csrc/scene_kernel.hip: a mesh's ground slots are its support points,
-csrc/mesh.cpp; against other models it is its bounding box) vs the fp64
-scene oracle (oracle.c or_scene_step with pyoracle's independent mesh
-restatement), and through the ScenarI/O mirror:
+csrc/mesh.cpp; against boxes and other meshes it is the convex hull of those
+points, sc_hull_pair) vs the fp64 scene oracle (oracle.c or_scene_step with
+pyoracle's independent mesh restatement, hull_pair), and through the
+ScenarI/O mirror:
 
   * teacher-forced one-step parity over 256 worlds: an irregular mesh "rock"
     at random tilts, heights and velocities next to a box cube that lands on
-    it (support-point ground contacts, bounding-box pair contacts): poses
+    it (support-point ground contacts, hull-box pair contacts): poses
     within 1e-5, velocities within 2e-3, contact points within 1e-5 (the
     tolerances of test_gpu_scene.py; at most 1 % of the pair points may come
-    from another box-box clipping feature at deep overlaps, same normal);
+    from another clipping feature at deep overlaps, same normal);
+  * the same for tetrahedron / hexagonal-prism / rock meshes against boxes
+    and against each other (mesh-mesh pairs) over a welded mesh platform;
+  * closed loop vs the oracle: a tetrahedron mesh settles on its face on a
+    table (centroid h / 4 above it); a cube across the edge of a hexagonal
+    mesh platform rests there, one beyond the edge tips off;
   * a box-shaped mesh steps bit-identically to the box on the GPU too;
   * World.insert_model of a URDF file whose mesh URI (OBJ, COLLADA) is
     relative to the file: the rock falls, comes to rest, and its contact
@@ -62,9 +68,9 @@ def test_rock_and_cube_one_step(require_gpu, oracle, tmp_path):
             n_pair += who[2] >= 0
             err = float(np.abs(row[0:3] - oc[0:3]).max())
             if err > 1e-5 and who[2] >= 0:
-                # box-box clipping at a deep, near-degenerate overlap may pick
-                # another feature in fp32 than in fp64 (same normal, same
-                # dynamics): counted, bounded below, not mesh-specific
+                # clipping at a deep, near-degenerate overlap may pick another
+                # feature in fp32 than in fp64 (same normal, same dynamics):
+                # counted, bounded below
                 assert np.abs(row[3:6] - oc[3:6]).max() < 1e-4, (w, row, oc)
                 dump.append((w, who, np.round(row[0:10], 5).tolist(), np.round(oc[0:10], 5).tolist()))
                 continue
@@ -179,3 +185,141 @@ def test_static_mesh_collider_through_scenario(require_gpu, oracle, tmp_path):
     assert z == pytest.approx(0.55, abs=2e-3)
     assert worst <= 1e-4
     gazebo.close()
+
+
+def _hull_fixtures(tmp_path):
+    from test_mesh_hull import _hexprism, _tetra
+    from mesh_models import rock_vertices
+    paths = {}
+    tv, tt, h = _tetra(0.16)
+    paths["tetra"] = str(tmp_path / "tetra.obj")
+    write_obj(paths["tetra"], tv, tt)
+    hv, ht = _hexprism(0.1, 0.04)
+    paths["hex"] = str(tmp_path / "hex.stl")
+    write_stl_binary(paths["hex"], hv, ht)
+    rv, rt = rock_vertices(4)
+    paths["rock"] = str(tmp_path / "rock.obj")
+    write_obj(paths["rock"], rv, rt)
+    return paths, h
+
+
+def test_mesh_pairs_one_step(require_gpu, oracle, tmp_path):
+    """One step from random piles of a tetrahedron mesh, a hexagonal-prism
+    mesh, a rock mesh and a box cube above a welded hexagonal mesh platform:
+    hull-box, hull-hull and hull-platform pairs (the hull narrow phase in both
+    precisions) against the oracle over 256 worlds."""
+    from test_mesh_hull import _hexprism
+    W, pgs, mu = 256, 50, 0.8
+    rng = np.random.default_rng(21)
+    paths, _ = _hull_fixtures(tmp_path)
+    pv, pt = _hexprism(0.3, 0.05)
+    plat_path = str(tmp_path / "plat.obj")
+    write_obj(plat_path, pv, pt)
+    platform = ('<robot name="platform"><link name="world"/><link name="top"><inertial><mass value="1"/>'
+                '<inertia ixx="1" iyy="1" izz="1" ixy="0" ixz="0" iyz="0"/></inertial><collision>'
+                f'<geometry><mesh filename="{plat_path}"/></geometry></collision></link>'
+                '<joint name="weld" type="fixed"><parent link="world"/><child link="top"/>'
+                '<origin xyz="0 0 0.05"/></joint></robot>')
+    texts = [platform, mesh_body_urdf(paths["tetra"], mass=1.0, half=(0.07, 0.07, 0.07), name="tetra"),
+             mesh_body_urdf(paths["hex"], mass=1.5, half=(0.1, 0.09, 0.04), name="hex"),
+             mesh_body_urdf(paths["rock"], mass=2.0, half=(0.12, 0.08, 0.06), name="rock"),
+             cube_urdf(mass=1.0, edge=0.12)]
+    base = [(0, 0, 0.05), (0.05, 0.0, 0.2), (-0.05, 0.03, 0.3), (0.0, -0.05, 0.42), (0.02, 0.02, 0.55)]
+    names = ["platform", "tetra", "hex", "rock", "cube"]
+    cms = [oracle.load_urdf(t, pose_xyz=b) for t, b in zip(texts, base)]
+    assert [c.base_shapes[0][0] for c in cms[:4]] == [3, 3, 3, 3]
+    sc = _scene([(t, (*b, 1, 0, 0, 0), nm) for t, b, nm in zip(texts, base, names)], W, pgs, mu)
+    for m in range(1, 5):
+        z0 = base[m][2]
+        sc.reset_base_pose(m, np.array([np.concatenate([rng.uniform(-0.06, 0.06, 2) + base[m][:2],
+                                                        [z0 + rng.uniform(-0.04, 0.02)], _rand_quat(rng, np.pi)])
+                                        for _ in range(W)]))
+        sc.reset_base_velocity(m, np.column_stack([rng.uniform(-0.5, 0.5, (W, 3)), rng.uniform(-2, 2, (W, 3))]))
+    sc.run(paused=True)
+    orcs = [_oracle_from_gpu(oracle, cms, sc, w, pgs, mu) for w in range(W)]
+    sc.run()
+    worst = dict(pose=0.0, vel=0.0, point=0.0)
+    n_pair, n_mesh_mesh, ill, dump = 0, 0, [], []
+    for w in range(W):
+        ow = orcs[w]
+        ow.step()
+        e = _compare(oracle, cms, sc, ow, w)
+        gc = sc.contacts(w)
+        assert len(gc) == len(ow.contacts), (w, len(gc), len(ow.contacts))
+        for row, (oc, who) in zip(gc, ow.contacts):
+            assert tuple(int(x) for x in row[10:14]) == who
+            if who[2] >= 0:
+                n_pair += 1
+                n_mesh_mesh += who[0] <= 3 and who[2] <= 3
+            err = float(np.abs(row[0:3] - oc[0:3]).max())
+            if err > 1e-5 and who[2] >= 0:
+                assert np.abs(row[3:6] - oc[3:6]).max() < 1e-4, (w, row, oc)
+                dump.append((w, who, np.round(row[0:10], 5).tolist(), np.round(oc[0:10], 5).tolist()))
+                continue
+            worst["point"] = max(worst["point"], err)
+        if e["vel"] > 2e-3:
+            ill.append((w, round(e["vel"], 5)))
+            continue
+        worst["pose"] = max(worst["pose"], e["pose"])
+        worst["vel"] = max(worst["vel"], e["vel"])
+    print(f"mesh pairs x{W}: one-step " + ", ".join(f"{k} {x:.2e}" for k, x in worst.items()) +
+          f", {n_pair} pair points ({n_mesh_mesh} mesh-mesh), ill {ill[:6]}, point mismatches {len(dump)}")
+    for d in dump[:10]:
+        print("point mismatch (world, who, gpu row, oracle row):", d)
+    assert n_pair > W and n_mesh_mesh > W // 4 and len(dump) <= n_pair // 100
+    assert len(ill) <= W // 50
+    assert worst["pose"] <= 1e-5 and worst["point"] <= 1e-5 and worst["vel"] <= 2e-3
+    assert sc.overflow() == 0
+    sc.close()
+
+
+def test_mesh_hull_closed_loop_kats(require_gpu, oracle, tmp_path):
+    """The oracle's hull KATs (tests/test_mesh_hull.py) on the GPU, closed
+    loop, exact LCP as the ScenarI/O scene runs it: a tetrahedron mesh settles
+    on its face h / 4 above a table; a cube across a slanted edge of a
+    hexagonal mesh platform stays, one beyond that edge (over the platform's
+    bounding box) tips off.  GPU vs oracle within 1e-4 m while on the hull."""
+    from test_mesh_hull import _hexprism, _table
+    paths, h = _hull_fixtures(tmp_path)
+    pv, pt = _hexprism(0.15, 0.05)
+    plat_path = str(tmp_path / "plat.obj")
+    write_obj(plat_path, pv, pt)
+    platform = ('<robot name="platform"><link name="world"/><link name="top"><inertial><mass value="1"/>'
+                '<inertia ixx="1" iyy="1" izz="1" ixy="0" ixz="0" iyz="0"/></inertial><collision>'
+                f'<geometry><mesh filename="{plat_path}"/></geometry></collision></link>'
+                '<joint name="weld" type="fixed"><parent link="world"/><child link="top"/>'
+                '<origin xyz="0 0 0.25"/></joint></robot>')
+    cases = [("tetra", _table(), mesh_body_urdf(paths["tetra"], mass=1.5, half=(0.06,) * 3, name="tetra"),
+              (0.0, 0.0, 0.3 + h / 4 + 0.01))]
+    for dist in (0.10, 0.16):
+        xy = dist * np.array([np.cos(np.pi / 6), np.sin(np.pi / 6)])
+        cases.append((f"cube@{dist}", platform, cube_urdf(mass=1.0, edge=0.1), (xy[0], xy[1], 0.35)))
+    for tag, fixed, body, pose in cases:
+        cms = [oracle.load_urdf(fixed), oracle.load_urdf(body, pose_xyz=pose)]
+        sc = _scene([(fixed, (0, 0, 0, 1, 0, 0, 0), "fixed"), (body, (*pose, 1, 0, 0, 0), "body")], 4, 50, 1.0,
+                    exact=True)
+        ow = oracle.SceneWorld(cms, pgs_iters=oracle.PGS_CONVERGED)
+        p0 = ow.p(1).copy()
+        dps = []
+        for k in range(600):
+            sc.run()
+            ow.step()
+            if k % 50 == 49:
+                dps.append(float(np.abs(sc.base_pose(1, 0, 4)[:, :3] - ow.p(1)).max()))
+        gp = sc.base_pose(1, 0, 4)[0, :3]
+        print(f"{tag}: GPU {np.round(gp, 5)}, oracle {np.round(ow.p(1), 5)}, |dp| every 50 steps "
+              + " ".join(f"{x:.1e}" for x in dps))
+        if tag == "tetra":
+            assert max(dps) <= 1e-4
+            assert gp[2] == pytest.approx(0.3 + h / 4, abs=3e-4)
+        elif tag == "cube@0.1":
+            assert max(dps) <= 1e-4
+            assert np.abs(gp - p0).max() < 2e-3
+        else:
+            # tipping over the edge: fp32 and fp64 agree while the cube rolls
+            # off the hull; the fall and the landing on the ground beyond it
+            # amplify the round-off (chaotic), so only the outcome is compared
+            assert max(dps[:4]) <= 1e-4
+            assert gp[2] < p0[2] - 0.01 and ow.p(1)[2] < p0[2] - 0.01
+            assert gp[2] == pytest.approx(ow.p(1)[2], abs=1e-3)
+        sc.close()

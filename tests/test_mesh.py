@@ -12,7 +12,8 @@ side:
     the same scene with the box cube;
   * KATs on the fp64 scene oracle: an irregular mesh dropped on the ground
     comes to rest with its weight carried by its support points, and a mesh
-    body rests on a box of another model (bounding-box pair contact);
+    body rests on a box of another model (the hull narrow phase against other
+    models is pinned in tests/test_mesh_hull.py);
   * loud failures: unsupported formats, missing files, a free body with more
     shape entries than mw_sim's free-body kernel holds.
 
@@ -221,7 +222,9 @@ def test_rock_comes_to_rest_on_its_support_points(oracle, tmp_path):
 
 
 def test_mesh_body_rests_on_a_box_of_another_model(oracle, tmp_path):
-    """against the shapes of other models a mesh collides as its bounding box"""
+    """a cube-shaped mesh rests on a box of another model (a mesh whose support
+    points are its bounding box corners keeps the box narrow phase; other
+    meshes use their convex hull, tests/test_mesh_hull.py)"""
     path = str(tmp_path / "cube.stl")
     write_stl_binary(path, cube_vertices((0.05, 0.05, 0.05)), CUBE_TRIS)
     table = ('<robot name="table"><link name="world"/><link name="top"><inertial><mass value="1"/>'
