@@ -58,17 +58,23 @@ struct ScNode {
 };
 static_assert(sizeof(ScNode) == 41 * 4, "ScNode layout");
 
+// narrow-phase workspace words per lane (ScWorld::clip): two clipping
+// polygons of <= 8 vertices x {u, v, x, y, z}, then 8 point slots (a pair's
+// output: the first np)
+constexpr int kScWsPoly = 0, kScWsOut = 80, kScWsWords = 112;
+
 template <int MAXNV>
 struct ScWorld {
     static constexpr int kStride = MAXNV + 1;     // odd: lane-strided rows are conflict-free
     static constexpr int kAStride = kScMaxRows + 1;
     ScNode node[kScMaxNodes];
     // phase-disjoint storage (one wave runs the phases in program order):
-    // the ABA's child -> parent accumulators, the response passes' per-lane
-    // stacks, then the Delassus matrix -- 37 KiB instead of 69 KiB, so two
-    // worlds fit in a CU's 160 KiB of LDS instead of one
+    // the ABA's child -> parent accumulators, the narrow phase's workspace,
+    // the response passes' per-lane stacks, then the Delassus matrix -- 37 KiB
+    // instead of 69 KiB, so two worlds fit in a CU's 160 KiB of LDS, not one
     union {
         WaveAcc acc[kScMaxNodes];
+        float clip[kScWsWords][kWaveLanes];          // the narrow phase's per-lane workspace
         float stack[kScMaxDepth][7][kWaveLanes];
         alignas(16) float A[kScMaxRows][kAStride];  // also the exact LCP's pivot rows (16-byte reads)
     };
@@ -146,70 +152,114 @@ __device__ __forceinline__ M3 mul3(const M3& A, const M3& B) {
 // Restatement of oracle.c box_box / box_sphere / or_collide in float32 (same
 // axis order, tie rules, clipping order and point reduction).
 
-__device__ __forceinline__ int sc_reduce(int n, f3* p, float* d) {
+// Point sets of the narrow phase.  ScWsPts: a lane's column of the contact
+// workspace in LDS (ScWorld::clip, slot i = 4 words {x, y, z, depth} at a
+// stride of one wavefront) -- the clipping polygons and the kept points of a
+// pair live there, not in per-lane arrays indexed at run time (those went to
+// scratch: 45.6k of the three-cube scene's 165k cycles per world-step were
+// its three box pairs, r06 profile).  ScArrPts: plain arrays (the hull pair's
+// own clipping buffer).
+struct ScWsPts {
+    float* w;
+    __device__ __forceinline__ f3 pt(int i) const {
+        return {w[(4 * i) * kWaveLanes], w[(4 * i + 1) * kWaveLanes], w[(4 * i + 2) * kWaveLanes]};
+    }
+    __device__ __forceinline__ float dep(int i) const { return w[(4 * i + 3) * kWaveLanes]; }
+    __device__ __forceinline__ void set(int i, f3 x, float d) const {
+        w[(4 * i) * kWaveLanes] = x.x;
+        w[(4 * i + 1) * kWaveLanes] = x.y;
+        w[(4 * i + 2) * kWaveLanes] = x.z;
+        w[(4 * i + 3) * kWaveLanes] = d;
+    }
+    __device__ __forceinline__ void move(int m, int i) const { set(m, pt(i), dep(i)); }
+};
+struct ScArrPts {
+    f3* p;
+    float* d;
+    __device__ __forceinline__ f3 pt(int i) const { return p[i]; }
+    __device__ __forceinline__ float dep(int i) const { return d[i]; }
+    __device__ __forceinline__ void move(int m, int i) const { p[m] = p[i]; d[m] = d[i]; }
+};
+
+// the oracle's reduction to 4 points (deepest, farthest, largest triangle,
+// farthest from its centroid), compacted in place in the original order
+template <class S>
+__device__ __forceinline__ int sc_reduce(int n, const S& s) {
     if (n <= 4) return n;
     int a = 0;
-    for (int i = 1; i < n; ++i) if (d[i] > d[a]) a = i;
+    for (int i = 1; i < n; ++i) if (s.dep(i) > s.dep(a)) a = i;
+    const f3 pa = s.pt(a);
     uint32_t used = 1u << a;
     int b = -1;
     float best = -1.f;
     for (int i = 0; i < n; ++i) {
         if ((used >> i) & 1u) continue;
-        const f3 e = p[i] - p[a];
+        const f3 e = s.pt(i) - pa;
         const float v = dot(e, e);
         if (v > best) { best = v; b = i; }
     }
     used |= 1u << b;
     int c = -1;
     best = -1.f;
-    const f3 ab = p[b] - p[a];
+    const f3 pb = s.pt(b);
+    const f3 ab = pb - pa;
     for (int i = 0; i < n; ++i) {
         if ((used >> i) & 1u) continue;
-        const f3 x = cross(ab, p[i] - p[a]);
+        const f3 x = cross(ab, s.pt(i) - pa);
         const float v = dot(x, x);
         if (v > best) { best = v; c = i; }
     }
     used |= 1u << c;
-    const f3 g = (1.f / 3.f) * (p[a] + p[b] + p[c]);
+    const f3 g = (1.f / 3.f) * (pa + pb + s.pt(c));
     int e4 = -1;
     best = -1.f;
     for (int i = 0; i < n; ++i) {
         if ((used >> i) & 1u) continue;
-        const f3 e = p[i] - g;
+        const f3 e = s.pt(i) - g;
         const float v = dot(e, e);
         if (v > best) { best = v; e4 = i; }
     }
     used |= 1u << e4;
     int m = 0;
     for (int i = 0; i < n; ++i)
-        if ((used >> i) & 1u) { p[m] = p[i]; d[m] = d[i]; ++m; }
+        if ((used >> i) & 1u) { s.move(m, i); ++m; }
     return 4;
 }
 
-__device__ __forceinline__ int sc_box_box(f3 hA, f3 cA, const M3& RA, f3 hB, f3 cB, const M3& RB, f3& n, f3* pts,
-                                          float* deps) {
-    f3 a[3] = {col(RA, 0), col(RA, 1), col(RA, 2)};
-    f3 b[3] = {col(RB, 0), col(RB, 1), col(RB, 2)};
+__device__ __forceinline__ f3 sel3(f3 x0, f3 x1, f3 x2, int k) { return k == 0 ? x0 : (k == 1 ? x1 : x2); }
+__device__ __forceinline__ float self3(float x0, float x1, float x2, int k) { return k == 0 ? x0 : (k == 1 ? x1 : x2); }
+
+// (the axis / half-extent triples are selected, never indexed at run time:
+// a run-time index into a local array puts the array in scratch)
+__device__ __forceinline__ int sc_box_box(f3 hA, f3 cA, const M3& RA, f3 hB, f3 cB, const M3& RB, f3& n,
+                                          const ScWsPts& out, float* ws) {
+    const f3 a[3] = {col(RA, 0), col(RA, 1), col(RA, 2)};
+    const f3 b[3] = {col(RB, 0), col(RB, 1), col(RB, 2)};
     const float ha[3] = {hA.x, hA.y, hA.z}, hb[3] = {hB.x, hB.y, hB.z};
     const f3 T = cB - cA;
     float best_face = 3.0e38f, best_edge = 3.0e38f;
     int face = -1, ei = -1, ej = -1;
     f3 eaxis = {0.f, 0.f, 0.f};
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
         const f3 L = k < 3 ? a[k] : b[k - 3];
         float rA = 0.f, rB = 0.f;
+#pragma unroll
         for (int i = 0; i < 3; ++i) { rA += ha[i] * fabsf(dot(a[i], L)); rB += hb[i] * fabsf(dot(b[i], L)); }
         const float pen = rA + rB - fabsf(dot(T, L));
         if (pen < 0.f) return 0;
         if (pen < best_face) { best_face = pen; face = k; }
     }
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < 3; ++j) {
             f3 L = cross(a[i], b[j]);
             const float len = sqrtf(dot(L, L));
             if (len < 1e-6f) continue;
             L = (1.f / len) * L;
             float rA = 0.f, rB = 0.f;
+#pragma unroll
             for (int k = 0; k < 3; ++k) { rA += ha[k] * fabsf(dot(a[k], L)); rB += hb[k] * fabsf(dot(b[k], L)); }
             const float pen = rA + rB - fabsf(dot(T, L));
             if (pen < 0.f) return 0;
@@ -220,86 +270,96 @@ __device__ __forceinline__ int sc_box_box(f3 hA, f3 cA, const M3& RA, f3 hB, f3 
         if (dot(L, T) > 0.f) L = -L;
         n = L;
         f3 pa = cA, pb = cB;
+#pragma unroll
         for (int k = 0; k < 3; ++k) {
             if (k != ei) pa = pa + ((dot(a[k], n) > 0.f ? -1.f : 1.f) * ha[k]) * a[k];
             if (k != ej) pb = pb + ((dot(b[k], n) > 0.f ? 1.f : -1.f) * hb[k]) * b[k];
         }
-        const f3 u = a[ei], v = b[ej];
+        const f3 u = sel3(a[0], a[1], a[2], ei), v = sel3(b[0], b[1], b[2], ej);
+        const float hae = self3(ha[0], ha[1], ha[2], ei), hbe = self3(hb[0], hb[1], hb[2], ej);
         const f3 w0 = pa - pb;
         const float uv = dot(u, v), uw = dot(u, w0), vw = dot(v, w0);
         const float den = 1.f - uv * uv;
         float s = den > 1e-12f ? (uv * vw - uw) / den : 0.f;
         float t = den > 1e-12f ? (vw - uv * uw) / den : 0.f;
-        s = fminf(fmaxf(s, -ha[ei]), ha[ei]);
-        t = fminf(fmaxf(t, -hb[ej]), hb[ej]);
-        pts[0] = 0.5f * ((pa + s * u) + (pb + t * v));
-        deps[0] = best_edge;
+        s = fminf(fmaxf(s, -hae), hae);
+        t = fminf(fmaxf(t, -hbe), hbe);
+        out.set(0, 0.5f * ((pa + s * u) + (pb + t * v)), best_edge);
         return 1;
     }
     const bool refA = face < 3;
     const int fk = refA ? face : face - 3;
     const f3 cR = refA ? cA : cB, cI = refA ? cB : cA;
-    const float* hR = refA ? ha : hb;
-    const float* hI = refA ? hb : ha;
-    const f3* R = refA ? a : b;
-    const f3* I = refA ? b : a;
-    f3 nr = R[fk];
+    const f3 R0 = refA ? a[0] : b[0], R1 = refA ? a[1] : b[1], R2 = refA ? a[2] : b[2];
+    const f3 I0 = refA ? b[0] : a[0], I1 = refA ? b[1] : a[1], I2 = refA ? b[2] : a[2];
+    const float hR0 = refA ? ha[0] : hb[0], hR1 = refA ? ha[1] : hb[1], hR2 = refA ? ha[2] : hb[2];
+    const float hI0 = refA ? hb[0] : ha[0], hI1 = refA ? hb[1] : ha[1], hI2 = refA ? hb[2] : ha[2];
+    f3 nr = sel3(R0, R1, R2, fk);
     if (dot(nr, cI - cR) < 0.f) nr = -nr;
     n = refA ? -nr : nr;
     int ik = 0;
     float bd = 0.f;
-    for (int k = 0; k < 3; ++k) {
-        const float d = fabsf(dot(I[k], nr));
-        if (d > bd) { bd = d; ik = k; }
+    {
+        const float d0 = fabsf(dot(I0, nr)), d1 = fabsf(dot(I1, nr)), d2 = fabsf(dot(I2, nr));
+        if (d0 > bd) { bd = d0; ik = 0; }
+        if (d1 > bd) { bd = d1; ik = 1; }
+        if (d2 > bd) { bd = d2; ik = 2; }
     }
-    const float sg = dot(I[ik], nr) > 0.f ? -1.f : 1.f;
+    const f3 Iik = sel3(I0, I1, I2, ik);
+    const float sg = dot(Iik, nr) > 0.f ? -1.f : 1.f;
     const int k1 = (ik + 1) % 3, k2 = (ik + 2) % 3;
     const int u1 = (fk + 1) % 3, u2 = (fk + 2) % 3;
-    const f3 fc = cR + hR[fk] * nr;
-    // polygon: (u, v, x, y, z) per vertex, clipped in place (at most 8 vertices)
-    float poly[2][8][5];
+    const f3 Ik1 = sel3(I0, I1, I2, k1), Ik2 = sel3(I0, I1, I2, k2);
+    const float hIik = self3(hI0, hI1, hI2, ik), hIk1 = self3(hI0, hI1, hI2, k1), hIk2 = self3(hI0, hI1, hI2, k2);
+    const f3 Ru1 = sel3(R0, R1, R2, u1), Ru2 = sel3(R0, R1, R2, u2);
+    const float hRu1 = self3(hR0, hR1, hR2, u1), hRu2 = self3(hR0, hR1, hR2, u2);
+    const f3 fc = cR + self3(hR0, hR1, hR2, fk) * nr;
+    // polygon: (u, v, x, y, z) per vertex, clipped between the workspace's two
+    // polygons (at most 8 vertices): word (8 c + i) 5 + k of the lane's column
+    auto poly = [ws](int c, int i, int k) -> float& { return ws[((8 * c + i) * 5 + k) * kWaveLanes]; };
     const float sx[4] = {1.f, -1.f, -1.f, 1.f}, sy[4] = {1.f, 1.f, -1.f, -1.f};
+#pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const f3 x = cI + (sg * hI[ik]) * I[ik] + (sx[q] * hI[k1]) * I[k1] + (sy[q] * hI[k2]) * I[k2];
+        const f3 x = cI + (sg * hIik) * Iik + (sx[q] * hIk1) * Ik1 + (sy[q] * hIk2) * Ik2;
         const f3 rel = x - fc;
-        poly[0][q][0] = dot(rel, R[u1]);
-        poly[0][q][1] = dot(rel, R[u2]);
-        poly[0][q][2] = x.x; poly[0][q][3] = x.y; poly[0][q][4] = x.z;
+        poly(0, q, 0) = dot(rel, Ru1);
+        poly(0, q, 1) = dot(rel, Ru2);
+        poly(0, q, 2) = x.x; poly(0, q, 3) = x.y; poly(0, q, 4) = x.z;
     }
     int cnt = 4, cur = 0;
     for (int plane = 0; plane < 4 && cnt > 0; ++plane) {
         const int axis = plane >> 1;
         const float s2 = (plane & 1) ? -1.f : 1.f;
-        const float h = axis ? hR[u2] : hR[u1];
+        const float h = axis ? hRu2 : hRu1;
         int m = 0;
         for (int i = 0; i < cnt; ++i) {
-            const float* P = poly[cur][i];
-            const float* Q = poly[cur][(i + 1) % cnt];
-            const float dp = s2 * P[axis] - h, dq = s2 * Q[axis] - h;
+            const int j = (i + 1 < cnt) ? i + 1 : 0;
+            const float dp = s2 * poly(cur, i, axis) - h, dq = s2 * poly(cur, j, axis) - h;
             if (dp <= 0.f && m < 8) {
-                for (int k = 0; k < 5; ++k) poly[cur ^ 1][m][k] = P[k];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) poly(cur ^ 1, m, k) = poly(cur, i, k);
                 ++m;
             }
             if (((dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f)) && m < 8) {
                 const float t = dp / (dp - dq);
-                for (int k = 0; k < 5; ++k) poly[cur ^ 1][m][k] = P[k] + t * (Q[k] - P[k]);
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    const float P = poly(cur, i, k);
+                    poly(cur ^ 1, m, k) = P + t * (poly(cur, j, k) - P);
+                }
                 ++m;
             }
         }
         cnt = m;
         cur ^= 1;
     }
-    f3 P8[8];
-    float D8[8];
     int np = 0;
     for (int i = 0; i < cnt; ++i) {
-        const f3 x = {poly[cur][i][2], poly[cur][i][3], poly[cur][i][4]};
+        const f3 x = {poly(cur, i, 2), poly(cur, i, 3), poly(cur, i, 4)};
         const float dep = dot(fc - x, nr);
-        if (dep > 0.f && np < 8) { P8[np] = x; D8[np] = dep; ++np; }
+        if (dep > 0.f && np < 8) { out.set(np, x, dep); ++np; }
     }
-    np = sc_reduce(np, P8, D8);
-    for (int i = 0; i < np; ++i) { pts[i] = P8[i]; deps[i] = D8[i]; }
-    return np;
+    return sc_reduce(np, out);
 }
 
 __device__ __forceinline__ int sc_box_sphere(f3 h, f3 c, const M3& R, float rad, f3 s, f3& nbs, f3& pt, float& dep) {
@@ -428,7 +488,7 @@ __device__ __forceinline__ bool sc_inside(int type, f3 h, f3 c, const M3& R, f3 
 // lane, SGPR spills 547 -> 84).  The one division that could see a zero
 // under -ffinite-math-only (sc_box_sphere's 1 / dist) is guarded.
 __device__ __forceinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& Ra, int tb, f3 hb, f3 cb,
-                                                const M3& Rb, f3& n, f3* pts, float* deps) {
+                                                const M3& Rb, f3& n, const ScWsPts& out) {
     f3 ax[6];
     int na = sc_axes(ta, ca, Ra, cb, ax);
     na += sc_axes(tb, cb, Rb, ca, ax + na);
@@ -443,8 +503,6 @@ __device__ __forceinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& 
     n = dot(ax[best], dab) >= 0.f ? ax[best] : -ax[best];
     const float plane_b = dot(n, cb) + sc_support(tb, hb, Rb, n);
     const float plane_a = dot(n, ca) - sc_support(ta, ha, Ra, n);
-    f3 P8[8];
-    float D8[8];
     int m = 0;
     for (int side = 0; side < 2; ++side)
         for (int k = 0; k < 8 && m < 8; ++k) {
@@ -452,16 +510,10 @@ __device__ __forceinline__ int sc_cylinder_pair(int ta, f3 ha, f3 ca, const M3& 
             const bool in = side ? sc_inside(ta, ha, ca, Ra, q) : sc_inside(tb, hb, cb, Rb, q);
             const float dep = side ? dot(n, q) - plane_a : plane_b - dot(n, q);
             if (!in || dep <= 0.f) continue;
-            P8[m] = q;
-            D8[m] = dep;
+            out.set(m, q, dep);
             ++m;
         }
-    m = sc_reduce(m, P8, D8);
-    for (int i = 0; i < m; ++i) {
-        pts[i] = P8[i];
-        deps[i] = D8[i];
-    }
-    return m;
+    return sc_reduce(m, out);
 }
 
 // ---- the hull narrow phase of mesh shapes (round 6; oracle.c hull_pair) ----
@@ -505,8 +557,7 @@ constexpr int kScClipMax = 24;   // clipped polygon (a hull face has <= 16 verti
 // of the incident face; the float32 restatement of oracle.c hull_pair (same
 // loops, tie rules and reduction).  Normal from B into A.  A call, not
 // inlined: only mesh pairs reach it.
-__device__ __noinline__ int sc_hull_pair(ScPoly A, f3 cA, M3 RA, ScPoly B, f3 cB, M3 RB, f3& n, f3* pts,
-                                         float* deps) {
+__device__ __noinline__ int sc_hull_pair(ScPoly A, f3 cA, M3 RA, ScPoly B, f3 cB, M3 RB, f3& n, ScWsPts out) {
     float pen[2] = {3.0e38f, 3.0e38f};
     int face[2] = {-1, -1};
     for (int side = 0; side < 2; ++side) {
@@ -560,9 +611,9 @@ __device__ __noinline__ int sc_hull_pair(ScPoly A, f3 cA, M3 RA, ScPoly B, f3 cB
     const float pen_f = refB ? pen[1] : pen[0];
     if (ea >= 0 && pen_e < 0.95f * pen_f - 1e-5f) {
         n = -eaxis;
-        pts[0] = sc_segment_mid(cA + mul(RA, A.v(A.H->e[ea][0])), cA + mul(RA, A.v(A.H->e[ea][1])),
-                                cB + mul(RB, B.v(B.H->e[eb][0])), cB + mul(RB, B.v(B.H->e[eb][1])));
-        deps[0] = pen_e;
+        out.set(0, sc_segment_mid(cA + mul(RA, A.v(A.H->e[ea][0])), cA + mul(RA, A.v(A.H->e[ea][1])),
+                                  cB + mul(RB, B.v(B.H->e[eb][0])), cB + mul(RB, B.v(B.H->e[eb][1]))),
+                pen_e);
         return 1;
     }
     const ScPoly& Rp = refB ? B : A;
@@ -608,48 +659,54 @@ __device__ __noinline__ int sc_hull_pair(ScPoly A, f3 cA, M3 RA, ScPoly B, f3 cB
         const float dep = dr - dot(nr, buf[cur][i]);
         if (dep > 0.f) { buf[cur][np] = buf[cur][i]; D8[np] = dep; ++np; }
     }
-    np = sc_reduce(np, buf[cur], D8);
+    np = sc_reduce(np, ScArrPts{buf[cur], D8});
     n = refB ? nr : -nr;
-    for (int i = 0; i < np; ++i) { pts[i] = buf[cur][i]; deps[i] = D8[i]; }
+    for (int i = 0; i < np; ++i) out.set(i, buf[cur][i], D8[i]);
     return np;
 }
 
 // shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius,
 // 2 cylinder: size = {radius, half length}): normal from B into A, up to 4
 // points / depths
+// shapes a, b (type 0 box: size = half extents, 1 sphere: size.x = radius,
+// 2 cylinder: size = {radius, half length}): normal from B into A, up to 4
+// points / depths into the lane's workspace slots (ws: its column of
+// ScWorld::clip)
 __device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, int tb, f3 sb, f3 cb, const M3& Rb,
-                                          f3& n, f3* pts, float* deps) {
+                                          f3& n, float* ws) {
+    const ScWsPts out{ws + kScWsOut * kWaveLanes};
+    f3 pt, nbs;
+    float dep;
     if ((ta == 2 && tb == 1) || (ta == 1 && tb == 2)) {
-        f3 nbs;
         if (ta == 2) {  // cylinder A, sphere B: n from B into A
-            if (!sc_cylinder_sphere(sa, ca, Ra, sb.x, cb, nbs, pts[0], deps[0])) return 0;
+            if (!sc_cylinder_sphere(sa, ca, Ra, sb.x, cb, nbs, pt, dep)) return 0;
             n = -nbs;
-            return 1;
+        } else {
+            if (!sc_cylinder_sphere(sb, cb, Rb, sa.x, ca, nbs, pt, dep)) return 0;
+            n = nbs;
         }
-        if (!sc_cylinder_sphere(sb, cb, Rb, sa.x, ca, nbs, pts[0], deps[0])) return 0;
-        n = nbs;
+        out.set(0, pt, dep);
         return 1;
     }
-    if (ta == 2 || tb == 2) return sc_cylinder_pair(ta, sa, ca, Ra, tb, sb, cb, Rb, n, pts, deps);
-    if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, pts, deps);
+    if (ta == 2 || tb == 2) return sc_cylinder_pair(ta, sa, ca, Ra, tb, sb, cb, Rb, n, out);
+    if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, out, ws + kScWsPoly * kWaveLanes);
     if (ta == 1 && tb == 1) {
         const f3 d = ca - cb;
         const float dist = sqrtf(dot(d, d));
         const float pen = sa.x + sb.x - dist;
         if (pen < 0.f || dist < 1e-12f) return 0;
         n = (1.f / dist) * d;
-        pts[0] = cb + (sb.x - 0.5f * pen) * n;
-        deps[0] = pen;
+        out.set(0, cb + (sb.x - 0.5f * pen) * n, pen);
         return 1;
     }
-    f3 nbs;
     if (ta == 0) {
-        if (!sc_box_sphere(sa, ca, Ra, sb.x, cb, nbs, pts[0], deps[0])) return 0;
+        if (!sc_box_sphere(sa, ca, Ra, sb.x, cb, nbs, pt, dep)) return 0;
         n = -nbs;
-        return 1;
+    } else {
+        if (!sc_box_sphere(sb, cb, Rb, sa.x, ca, nbs, pt, dep)) return 0;
+        n = nbs;
     }
-    if (!sc_box_sphere(sb, cb, Rb, sa.x, ca, nbs, pts[0], deps[0])) return 0;
-    n = nbs;
+    out.set(0, pt, dep);
     return 1;
 }
 
@@ -813,6 +870,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                         float dt, int pgs_iters, int lcp_solves, const ScWarm& warm, const f3 gw, float mu,
                         int& nc_out, int& ovf, int& unconv) {
     const int lane = lane_id();
+    MW_PROF_T(t_in);
 #ifdef MW_SC_NANCHECK
     bool nan_reported = false;
     MW_SC_CHECK(0, 0);
@@ -980,6 +1038,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
 
     MW_SC_CHECK(3, 0);
+    MW_PROF_T(t_aba);
     // ---- contacts: ground slots, then shape pairs
     int nc = 0;
     if (P->ground && (present & kScGroundBit)) {
@@ -1029,11 +1088,16 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             nc += __popcll(bal);
         }
     }
+    MW_PROF_T(t_gnd);
+#ifdef MW_WAVE_PROF
+    long long t_np = t_gnd;
+#endif
     for (int p0 = 0; p0 < P->n_pairs; p0 += kWaveLanes) {
         const int pr = p0 + lane;
         int np = 0;
-        f3 nrm = {0.f, 0.f, 1.f}, pts[4];
-        float deps[4];
+        f3 nrm = {0.f, 0.f, 1.f};
+        float* ws = &L.clip[0][lane];
+        const ScWsPts out{ws + kScWsOut * kWaveLanes};
         int na = 0, nb = 0;
         if (pr < P->n_pairs) {
             const int sa = P->pair_a[pr], sb = P->pair_b[pr];
@@ -1064,20 +1128,24 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                                               : ScPoly{&P->box_hull, za, true};
                     const ScPoly pb = hb >= 0 ? ScPoly{&P->hull[hb], mk(1.f, 1.f, 1.f), false}
                                               : ScPoly{&P->box_hull, zb, true};
-                    np = sc_hull_pair(pa, ca, mul3(A_.Rw, SRa), pb, cb, mul3(B_.Rw, SRb), nrm, pts, deps);
+                    np = sc_hull_pair(pa, ca, mul3(A_.Rw, SRa), pb, cb, mul3(B_.Rw, SRb), nrm, out);
                 } else {
-                    np = sc_collide(ta, za, ca, mul3(A_.Rw, SRa), tb, zb, cb, mul3(B_.Rw, SRb), nrm, pts, deps);
+                    np = sc_collide(ta, za, ca, mul3(A_.Rw, SRa), tb, zb, cb, mul3(B_.Rw, SRb), nrm, ws);
                 }
             }
         }
+#ifdef MW_WAVE_PROF
+        if (p0 == 0) t_np = clock64();
+#endif
         int total = 0;
         const int pre = wave_prefix7(np, total);
         for (int i = 0; i < np; ++i) {
             const int c = nc + pre + i;
             if (c < kScMaxContacts) {
-                L.c_p[c][0] = pts[i].x; L.c_p[c][1] = pts[i].y; L.c_p[c][2] = pts[i].z;
+                const f3 x = out.pt(i);
+                L.c_p[c][0] = x.x; L.c_p[c][1] = x.y; L.c_p[c][2] = x.z;
                 L.c_n[c][0] = nrm.x; L.c_n[c][1] = nrm.y; L.c_n[c][2] = nrm.z;
-                L.c_d[c] = deps[i];
+                L.c_d[c] = out.dep(i);
                 L.c_na[c] = na;
                 L.c_nb[c] = nb;
                 L.c_key[c] = P->n_slots + 4 * pr + i;
@@ -1098,6 +1166,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         L.c_x[lane][0] = L.c_x[lane][1] = L.c_x[lane][2] = 0.f;
     }
 
+    MW_PROF_T(t_pairs);
     MW_SC_CHECK(4, nc);
     // ---- joint rows of body `lane` (bit t: limit / servo / friction)
     uint32_t jbits = 0u;
@@ -1169,6 +1238,11 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
 
     float x1s = 0.f;  // the exact solve's stage-1 impulse of row `lane` (warm record)
+    float x0 = 0.f;   // the impulse of row `lane` (rows 64.. : x1 below)
+    MW_PROF_T(t_rows);
+#ifdef MW_WAVE_PROF
+    long long t_resp = t_rows, t_del = t_rows, t_lcp = t_rows;
+#endif
     if (NR > 0) {
         // ---- responses, lane = row
         for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
@@ -1206,35 +1280,99 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 }
             }
         }
-        // ---- Delassus A = J MJ^T (lane = column, MJ row in registers)
-        for (int c0 = 0; c0 < NR; c0 += kWaveLanes) {
-            const int c = c0 + lane;
-            float mj[MAXNV];
+#ifdef MW_WAVE_PROF
+        t_resp = clock64();
+#endif
+        // ---- Delassus A = J MJ^T.  Up to 64 rows: on the matrix cores
+        // (wave_tree.hpp's tiles, v_mfma_f32_32x32x2_f32: in k-step k lane l
+        // supplies J[m0 + l%32][2k + l/32] and MJ[n0 + l%32][2k + l/32]; the
+        // 32x32 result holds column n0 + l%32 in lane l, rows 8(i/4) + 4(l/32)
+        // + i%4 in accumulator i; one exchange of the 32-lane halves gives
+        // lane c all of column c = row c), straight into the registers the
+        // PGS and the exact solve keep it in.  Columns >= NV of J and MJ are
+        // zero (the response pass clears them); rows / columns >= NR are
+        // masked.  (The lane = column FMA loop over LDS took 21.8k cycles per
+        // world-step on the three-cube scene.)  More rows: that loop, into L.A.
+        float a[kWaveLanes];
+        if (NR <= kWaveLanes) {
+            const int lr = lane & 31, lh = lane >> 5;
+            const bool hi2 = NR > 32;
+            v16f t00 = {}, t01 = {}, t10 = {}, t11 = {};
+            constexpr int kKs = MAXNV / 2;
 #pragma unroll
-            for (int e = 0; e < MAXNV; ++e) mj[e] = (c < NR) ? L.MJ[c][e] : 0.f;
-            for (int r = 0; r < NR; ++r) {
-                float a = 0.f;
+            for (int k0 = 0; k0 < kKs; k0 += 4) {
+                if (2 * k0 >= NV) break;
+                float jv0[4], mv0[4], jv1[4], mv1[4];
 #pragma unroll
-                for (int e = 0; e < MAXNV; ++e) a += L.J[r][e] * mj[e];
-                if (c < NR) {
-                    if (r == c) a *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
-                    L.A[r][c] = a;
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int e = 2 * (k0 + kk) + lh;
+                    jv0[kk] = L.J[lr][e];
+                    mv0[kk] = L.MJ[lr][e];
+                    jv1[kk] = hi2 ? L.J[32 + lr][e] : 0.f;
+                    mv1[kk] = hi2 ? L.MJ[32 + lr][e] : 0.f;
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv0[kk], mv0[kk], t00, 0, 0, 0);
+                    if (hi2) {
+                        t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv0[kk], mv1[kk], t01, 0, 0, 0);
+                        t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv1[kk], mv0[kk], t10, 0, 0, 0);
+                        t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv1[kk], mv1[kk], t11, 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r0 = 8 * (i / 4) + (i % 4);
+                float x0 = t00[i], y0 = t01[i];
+                lane_swap32(x0, y0);
+                a[r0] = x0;
+                a[r0 + 4] = y0;
+                float x1 = t10[i], y1 = t11[i];
+                lane_swap32(x1, y1);
+                a[32 + r0] = x1;
+                a[32 + r0 + 4] = y1;
+            }
+            float dg = 1.f;
+#pragma unroll
+            for (int r = 0; r < kWaveLanes; ++r) {
+                a[r] = (r < NR && lane < NR) ? a[r] : 0.f;
+                if (lane == r && r < NR) {
+                    a[r] *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
+                    dg = a[r];
+                }
+            }
+            if (lane < NR) L.rc[lane] = F4{L.rb[lane], rcp(dg), L.rlo[lane], L.rhi[lane]};
+        } else {
+            for (int c0 = 0; c0 < NR; c0 += kWaveLanes) {
+                const int c = c0 + lane;
+                float mj[MAXNV];
+#pragma unroll
+                for (int e = 0; e < MAXNV; ++e) mj[e] = (c < NR) ? L.MJ[c][e] : 0.f;
+                for (int r = 0; r < NR; ++r) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int e = 0; e < MAXNV; ++e) acc += L.J[r][e] * mj[e];
+                    if (c < NR) {
+                        if (r == c) acc *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
+                        L.A[r][c] = acc;
+                    }
+                }
+            }
+            for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
+                const int r = r0 + lane;
+                if (r < NR) {
+                    F4 cst;
+                    cst.x = L.rb[r];
+                    cst.y = rcp(L.A[r][r]);
+                    cst.z = L.rlo[r];
+                    cst.w = L.rhi[r];
+                    L.rc[r] = cst;
                 }
             }
         }
-        for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
-            const int r = r0 + lane;
-            if (r < NR) {
-                F4 cst;
-                cst.x = L.rb[r];
-                cst.y = rcp(L.A[r][r]);
-                cst.z = L.rlo[r];
-                cst.w = L.rhi[r];
-                L.rc[r] = cst;
-            }
-        }
         // ---- PGS (rows in order; lane c owns rows c and c + 64)
-        float x0 = 0.f, x1 = 0.f, w0 = 0.f, w1 = 0.f;
+        float x1 = 0.f, w0 = 0.f, w1 = 0.f;
         const bool two = NR > kWaveLanes;
         if (NR <= kWaveLanes) {
             // up to 64 rows: the register form of wave_tree.hpp -- lane c holds
@@ -1247,28 +1385,29 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             // warm start (exact mode): every row from the previous step's
             // impulse of the same contact key / joint row, else 0
             float xw = 0.f, xw1 = 0.f;  // final and stage-1 impulses of the previous step
-            if (warm.rec && lane < NR) {
-                const int src = L.src[lane];
-                if (src < kJointRow) {
-                    const int key = L.c_key[src / 3], np = warm.n();
-                    for (int j = 0; j < np; ++j) {
-                        if (warm.key(j) == key) {
-                            xw = warm.x(3 * j + src % 3);
-                            xw1 = warm.x1(3 * j + src % 3);
-                            break;
-                        }
-                    }
-                } else {
-                    xw = warm.x(kScWarmJoint0 + (src - kJointRow));
-                    xw1 = warm.x1(kScWarmJoint0 + (src - kJointRow));
+            if (warm.rec) {
+                // the previous record's keys one per lane (one load, not a
+                // search loop of dependent loads per row), matched by lane reads
+                const int np = warm.n();
+                const int pk = (lane < np) ? warm.key(lane) : -1;
+                const int src = L.src[lane < NR ? lane : 0];
+                const bool crow = lane < NR && src < kJointRow;
+                const int key = crow ? L.c_key[src / 3] : -2;
+                int idx = -1;
+                for (int j = 0; j < np; ++j) {
+                    const int kj = __builtin_amdgcn_readlane(pk, j);
+                    idx = (idx < 0 && kj == key) ? j : idx;
+                }
+                const int wi = (crow && idx >= 0) ? 3 * idx + src % 3
+                                                  : ((lane < NR && !crow) ? kScWarmJoint0 + (src - kJointRow) : -1);
+                if (wi >= 0) {
+                    xw = warm.x(wi);
+                    xw1 = warm.x1(wi);
                 }
             }
-            float a[kWaveLanes], x[kWaveLanes];
+            float x[kWaveLanes];
 #pragma unroll
-            for (int r = 0; r < kWaveLanes; ++r) {
-                a[r] = (r < NR && lane < NR) ? L.A[r][lane] : 0.f;
-                x[r] = read_lane(xw, r);
-            }
+            for (int r = 0; r < kWaveLanes; ++r) x[r] = read_lane(xw, r);
             // exact mode: no coupled sweeps -- each stage of the exact solve
             // runs its own (wave_lcp.hpp), as on the world-per-wavefront kernel
             for (int it = 0; it < (lcp_solves > 0 ? 0 : pgs_iters); ++it) {
@@ -1325,14 +1464,22 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 long long cyc[3] = {0, 0, 0};
                 x1s = xw1;
                 // long-row elimination (wave_lcp.hpp lcp_ge_solve)
-                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true, kScStageSweeps, kLcpMfmaAll>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+#ifdef MW_WAVE_PROF
+                const long long t_ex0 = clock64();
+#endif
+                // (sweeps skipped when every contact has a warm record: 0.730 ->
+                // 0.665 ms, but a resting cube then drifts by 1.7e-4 m/s,
+                // test_gpu_scenario_scene.py::test_cube_contact: kept)
+                const int sweeps = pgs_iters;
+                const bool ok = (NR <= 32) ? wave_lcp_exact<32, true, kScStageSweeps, kLcpMfmaAll>(a, Rw, mu, NR, lcp_solves, sweeps,
                                                                       kScExactPgsTol, L.rc, Uw, x1s, x0, nsolve,
                                                                       nround, nsolve1, cyc)
-                                           : wave_lcp_exact<kWaveMaxRows, true, kScStageSweeps, kLcpMfmaAll>(a, Rw, mu, NR, lcp_solves, pgs_iters,
+                                           : wave_lcp_exact<kWaveMaxRows, true, kScStageSweeps, kLcpMfmaAll>(a, Rw, mu, NR, lcp_solves, sweeps,
                                                                                 kScExactPgsTol, L.rc, Uw, x1s, x0,
                                                                                 nsolve, nround, nsolve1, cyc);
                 if (!ok && lane == 0) unconv += 1;
 #ifdef MW_WAVE_PROF
+                if (lane == 0) atomicAdd(&g_wave_prof[12], static_cast<unsigned long long>(clock64() - t_ex0));
                 // debug dump of up to kDumpSlots hard LCPs (>= 8 solves, or
                 // the unconverged ones with -DMW_DUMP_FAIL): n, A, b, lo, hi,
                 // the two warm records, the result, kind, the stage-1 result
@@ -1420,15 +1567,27 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 x1 = (lane == lr && hi) ? v : x1;
             }
         }
+#ifdef MW_WAVE_PROF
+        t_lcp = clock64();
+#endif
         // ---- nu += MJ^T x (lane = coordinate); impulses of the contacts.
         // The lane reads of x run with every lane active: inside a branch on
         // the lane index the compiler may keep x only in the active lanes.
         {
+            // blocks of 8 rows: the block's MJ loads go out together (a row
+            // at a time waited on each load)
             const int lc = lane < NV ? lane : 0;
             float dnu = 0.f;
-            for (int r = 0; r < NR; ++r) {
-                const float xr = read_lane(r >= kWaveLanes ? x1 : x0, r & (kWaveLanes - 1));
-                dnu += xr * L.MJ[r][lc];
+            for (int r0 = 0; r0 < NR; r0 += 8) {
+                float mj[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) mj[k] = L.MJ[(r0 + k < NR) ? r0 + k : r0][lc];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int r = r0 + k;
+                    const float xr = read_lane(r >= kWaveLanes ? x1 : x0, r & (kWaveLanes - 1));
+                    dnu += (r < NR) ? xr * mj[k] : 0.f;
+                }
             }
             if (lane < NV) L.nu[lane] += dnu;
         }
@@ -1436,25 +1595,32 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             const int r = r0 + lane;
             if (r < ncr && r < NR) L.c_x[r / 3][r % 3] = r0 ? x1 : x0;
         }
-        if (warm.rec) {
-            // the next step's record of the joint rows: this step's (the others 0)
-            for (int e = lane; e < 3 * NB; e += kWaveLanes) {
-                warm.x(kScWarmJoint0 + e) = 0.f;
-                warm.x1(kScWarmJoint0 + e) = 0.f;
-            }
-            __threadfence_block();
-            if (!two && lane >= ncr && lane < NR) {
-                warm.x(kScWarmJoint0 + (L.src[lane] - kJointRow)) = x0;
-                warm.x1(kScWarmJoint0 + (L.src[lane] - kJointRow)) = x1s;
-            }
-        }
-    } else if (warm.rec) {
-        for (int e = lane; e < 3 * NB; e += kWaveLanes) {
-            warm.x(kScWarmJoint0 + e) = 0.f;
-            warm.x1(kScWarmJoint0 + e) = 0.f;
-        }
     }
     if (warm.rec) {
+        // the next step's record, every word written once (no zero-then-
+        // overwrite: each ordering fence waited for all of the wave's stores,
+        // 9.9k cycles per world-step in this tail on the three-cube scene).
+        // Joint rows, lane = body: its three entries, this step's impulse of
+        // each of its rows, 0 without one (the lane reads of x with every lane
+        // active)
+        const bool rec_rows = NR > 0 && NR <= kWaveLanes;
+        float jx[3], jx1[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = ncr + jbefore + __builtin_popcount(jbits & ((1u << t) - 1u));
+            const bool has = rec_rows && ((jbits >> t) & 1u) && r < NR;
+            const int rl = has ? r : 0;
+            const float xv = __shfl(x0, rl), x1v = __shfl(x1s, rl);
+            jx[t] = has ? xv : 0.f;
+            jx1[t] = has ? x1v : 0.f;
+        }
+        if (lane < NB) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                warm.x(kScWarmJoint0 + 3 * lane + t) = jx[t];
+                warm.x1(kScWarmJoint0 + 3 * lane + t) = jx1[t];
+            }
+        }
         // ... and of the contacts, by key (contact c's rows are 3 c + d, so
         // lane r < ncr holds row r's stage-1 impulse in x1s)
         const int nrec = NR > 0 ? nc : 0;
@@ -1464,9 +1630,9 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #pragma unroll
             for (int d = 0; d < 3; ++d) warm.x(3 * lane + d) = L.c_x[lane][d];
         }
-        __threadfence_block();
         for (int r = lane; r < 3 * nrec; r += kWaveLanes)
             warm.x1(r) = (r == lane && r < ncr && r < NR && NR <= kWaveLanes) ? x1s : 0.f;
+        // the next substep reads the record (other lanes' words)
         __threadfence_block();
     }
     nc_out = nc;
@@ -1488,7 +1654,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                                    L.nu[P->body_coord[i0 + 1]], L.nu[P->body_coord[i0 + 2]], dt, bp - 1);
         }
     }
-    __threadfence_block();
+    wave_lds_sync();
     if (isbody && alive) L.q[bi] = q_new;
     if (isbase && alive && md.floating) {
         const int o = md.coff;
@@ -1496,6 +1662,27 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         integrate_pose(Rb0, Vn, dt, base);
         base.V = Vn;
     }
+#ifdef MW_WAVE_PROF
+    // phase cycles per world-step (scripts/wave_prof.py MW_PROF_MODEL=scene3):
+    // [0] ABA + integrateVelocities, [1] contacts + row setup, [2] responses,
+    // [3] Delassus, [4] PGS / exact LCP, [5] impulses .. integratePositions,
+    // [6] the whole step, [7] world-steps; inside [1]: [19] ground slots,
+    // [20] shape pairs
+    const long long t_out = clock64();
+    if (lane == 0) {
+        atomicAdd(&g_wave_prof[0], static_cast<unsigned long long>(t_aba - t_in));
+        atomicAdd(&g_wave_prof[1], static_cast<unsigned long long>(t_rows - t_aba));
+        atomicAdd(&g_wave_prof[2], static_cast<unsigned long long>(t_resp - t_rows));
+        atomicAdd(&g_wave_prof[3], static_cast<unsigned long long>(t_del - t_resp));
+        atomicAdd(&g_wave_prof[4], static_cast<unsigned long long>(t_lcp - t_del));
+        atomicAdd(&g_wave_prof[5], static_cast<unsigned long long>(t_out - (NR > 0 ? t_lcp : t_rows)));
+        atomicAdd(&g_wave_prof[6], static_cast<unsigned long long>(t_out - t_in));
+        atomicAdd(&g_wave_prof[7], 1ull);
+        atomicAdd(&g_wave_prof[19], static_cast<unsigned long long>(t_gnd - t_aba));
+        atomicAdd(&g_wave_prof[20], static_cast<unsigned long long>(t_pairs - t_gnd));
+        atomicAdd(&g_wave_prof[21], static_cast<unsigned long long>(t_np - t_gnd));
+    }
+#endif
 }
 
 template <int MAXNV>

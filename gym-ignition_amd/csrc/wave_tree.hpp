@@ -877,6 +877,10 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             Rw.hi = Rw.live ? c.w : 0.f;
             float xe = x0;
             x1s = x1w;
+            // (skipping the stages' sweeps when every contact has a warm
+            // record: C5 72.2 -> 68.0 us, but a resting cube's friction
+            // answer then drifts by 1.7e-4 m/s (test_cube_contact_kat): kept)
+            const int sweeps = pgs_iters;
             // the elimination's pivot rows go to the responses' stack (dead here)
             static_assert(sizeof(L.stack) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
             float* U = &L.stack[0][0][0];
@@ -891,13 +895,13 @@ __device__ __forceinline__ uint32_t wave_step(const ChainF* __restrict__ P, cons
             // columns took contacts_floating 195 -> 167 us (gpurun_out r04z)
             bool ok;
             if (R <= 16 && kLcpSmall > 0)
-                ok = wave_lcp_exact<16, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
+                ok = wave_lcp_exact<16, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, sweeps, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
                                         nsolve1, cyc);
             else if (R <= kLcpSmall)
-                ok = wave_lcp_exact<32, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
+                ok = wave_lcp_exact<32, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, sweeps, pgs_tol, L.rc, U, x1s, xe, nsolve, nround,
                                         nsolve1, cyc);
             else
-                ok = wave_lcp_exact<kWaveMaxRows, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, pgs_iters, pgs_tol, L.rc, U, x1s, xe,
+                ok = wave_lcp_exact<kWaveMaxRows, false, kLcpStageSweeps, kWaveLcpMfma>(a, Rw, mu, R, lcp_solves, sweeps, pgs_tol, L.rc, U, x1s, xe,
                                                   nsolve, nround, nsolve1, cyc);
 #ifdef MW_WAVE_PROF
             if (MW_DUMP_WHEN(ok, nsolve)) {

@@ -53,7 +53,14 @@ if os.environ.get("MW_PROF_MODEL", "icub") == "scene3":
     print(f"scene 3 cubes x{W}: {dt / T * 1e6:.1f} us per blocking run, {buf[18]} exact solves, unconverged {buf[15]}; "
           f"per solve: {buf[8] / ns:.2f} linear solves ({buf[10] / ns:.2f} in stage 2), {buf[9] / ns:.2f} rounds, "
           f"max {buf[11]}, {buf[13]} > 4; cycles: {buf[14] / ns:.0f} in solves, {buf[16] / ns:.0f} in sweeps, "
-          f"{buf[17] / ns:.0f} in stage 1")
+          f"{buf[17] / ns:.0f} in stage 1, {buf[12] / ns:.0f} in the whole exact solve")
+    nst = max(buf[7], 1)
+    for k, name in enumerate(["ABA + integrateVelocities", "contacts + row setup", "responses (lane = row)",
+                              "Delassus (lane = column)", "PGS / exact LCP", "impulses .. integratePositions",
+                              "whole step"]):
+        print(f"  {name:40s} {buf[k] / nst:12.0f} cycles/world-step")
+    print(f"  inside contacts: ground slots {buf[19] / nst:.0f}, shape pairs {buf[20] / nst:.0f} "
+          f"(their first pass's narrow phase {buf[21] / nst:.0f}) cycles/world-step")
     save_dumps(N.lib().mw_debug_scene_dump, 8, "scene_dump.npz")
     sys.exit(0)
 if os.environ.get("MW_PROF_MODEL", "icub") == "cube":
