@@ -113,7 +113,10 @@ struct mw_scene {
     void* d_base = nullptr;        // [base 13K | rpose 7K | rvel 6K][W] f32 + bflag [K][W]
     void* d_misc = nullptr;        // present [W] | ncontact [W] | overflow | wlast [S][NN][W]
     float* d_wrench = nullptr;     // [S][6][NN][W]
-    float* d_contact = nullptr;    // [C][12][W]
+    float* d_contact = nullptr;    // [contact_cap][12][W]
+    int contact_cap = CMAX;        // contact points per world of the contact output
+    float* d_big = nullptr;        // large-contact workspace (SceneDev::big), big_bytes long
+    size_t big_bytes = 0;
     float* d_wphys = nullptr;      // [4][W]: gravity xyz, ground friction per world
     int32_t* d_warm = nullptr;     // [kScWarmWords][W]: exact-LCP warm-start record (SceneDev::warm)
     mw::PidF* d_pid = nullptr;
@@ -401,6 +404,8 @@ void clear_consumed(mw_scene* s) {
     s->clear_cmd = s->clear_base = false;
 }
 
+int ensure_big(mw_scene* s);
+
 // Upload pending parameters, commands, resets, presence, wrenches and gains
 // (asynchronous copies out of the pinned mirrors).  defer: the caller
 // synchronises later and then calls clear_consumed(); otherwise this waits
@@ -419,6 +424,7 @@ int flush(mw_scene* s, bool defer, bool direct = false) {
     if (!s->idle)
         if (int rc = sync(s)) return rc;
     if (s->params_dirty) {
+        if (int rc = ensure_big(s)) return rc;
         SC_HIP(hipMemcpyAsync(s->dp, &s->hp, sizeof(mw::SceneF), hipMemcpyHostToDevice, s->stream));
         // new slots / pairs: the warm-start keys of the old layout mean nothing
         SC_HIP(hipMemsetAsync(s->d_warm, 0, s->W * sizeof(int32_t), s->stream));
@@ -482,6 +488,57 @@ bool needs_base_readback(const mw_scene* s) {
 }
 bool can_overflow(const mw_scene* s) { return s->hp.n_shapes > 0 || 3 * s->NB > mw::kScMaxRows; }
 
+// The large-contact workspace a scene needs (SceneDev::big; scene_kernel.hip
+// sc_big_constraints), from its worst case: every ground slot touching,
+// kScPairMaxPoints per shape pair, three joint rows per body.  None when that
+// fits the compact path (<= kScMaxContacts points, <= 64 rows).
+void size_big(const mw_scene* s, int& cmax, int& rows) {
+    const mw::SceneF& P = s->hp;
+    const int worst = (P.ground ? P.n_slots : 0) + mw::kScPairMaxPoints * P.n_pairs;
+    const int jrows = 3 * s->NB;
+    cmax = rows = 0;
+    if (worst <= mw::kScMaxContacts && 3 * worst + jrows <= 64) return;
+    cmax = std::min(worst, mw::kScBigContacts);
+    rows = std::min(mw::kScBigRows, (3 * cmax + jrows + 63) / 64 * 64);
+}
+
+// (re)allocate the large-contact workspace and the contact output for the
+// current parameters (the stream is idle: flush synchronised)
+int ensure_big(mw_scene* s) {
+    int cmax = 0, rows = 0;
+    size_big(s, cmax, rows);
+    const int maxnv = s->nv <= 32 ? 32 : 64;   // the kernel instance (launch_scene_run)
+    const int64_t stride = rows ? mw::sc_big_world_floats(cmax, rows, maxnv) : 0;
+    const size_t bytes = static_cast<size_t>(stride) * s->W * sizeof(float);
+    if (bytes != s->big_bytes) {
+        (void)hipFree(s->d_big);
+        s->d_big = nullptr;
+        s->big_bytes = 0;
+        if (bytes) SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_big), bytes));
+        s->big_bytes = bytes;
+    }
+    mw::SceneDev& D = s->dev;
+    D.big = rows ? s->d_big : nullptr;
+    D.big_stride = stride;
+    D.big_cmax = cmax;
+    D.big_rows = rows;
+    const int cap = std::max(CMAX, cmax);
+    if (cap != s->contact_cap) {
+        const size_t n = static_cast<size_t>(cap) * 12 * s->W * sizeof(float);
+        (void)hipFree(s->d_contact);
+        (void)hipHostFree(s->h_contact);
+        s->d_contact = nullptr;
+        s->h_contact = nullptr;
+        SC_HIP(hipMalloc(reinterpret_cast<void**>(&s->d_contact), n));
+        SC_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->h_contact), n, hipHostMallocDefault));
+        s->contact_cap = cap;
+        D.contact = s->d_contact;
+        SC_HIP(hipMemsetAsync(D.ncontact, 0, s->W * sizeof(int32_t), s->stream));
+    }
+    D.contact_cap = cap;
+    return MW_OK;
+}
+
 int queue_readback(mw_scene* s, bool base = true) {
     const size_t plane = s->jrows * sizeof(float), rows = static_cast<size_t>(s->NB) * s->W * sizeof(float);
     if (rows && 3 * plane <= (size_t{1} << 20)) {
@@ -511,7 +568,7 @@ int pull_base(mw_scene* s) { return pull_joints(s); }
 int pull_contacts(mw_scene* s) {
     if (!s->contacts_stale) return MW_OK;
     SC_HIP(hipMemcpyAsync(s->h_ncontact, s->dev.ncontact, s->W * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
-    SC_HIP(hipMemcpyAsync(s->h_contact, s->d_contact, static_cast<size_t>(CMAX) * 12 * s->W * sizeof(float),
+    SC_HIP(hipMemcpyAsync(s->h_contact, s->d_contact, static_cast<size_t>(s->contact_cap) * 12 * s->W * sizeof(float),
                           hipMemcpyDeviceToHost, s->stream));
     if (int rc = sync(s)) return rc;
     s->contacts_stale = false;
@@ -696,6 +753,10 @@ int mw_scene_create(const mw_config* cfg, mw_scene** out) {
     D.diverged = mp + W * sizeof(uint32_t) + W * sizeof(int32_t) + 64 + nwl * sizeof(int32_t);
     D.wrench = s->d_wrench;
     D.contact = s->d_contact;
+    D.contact_cap = CMAX;
+    D.big = nullptr;
+    D.big_stride = 0;
+    D.big_cmax = D.big_rows = 0;
     D.wphys = s->d_wphys;
     D.warm = s->d_warm;
     s->mode.assign(s->jrows, MW_MODE_IDLE);
@@ -716,6 +777,7 @@ void mw_scene_destroy(mw_scene* s) {
     (void)hipFree(s->d_misc);
     (void)hipFree(s->d_wrench);
     (void)hipFree(s->d_contact);
+    (void)hipFree(s->d_big);
     (void)hipFree(s->d_pid);
     (void)hipFree(s->dp);
     (void)hipFree(s->d_wphys);
@@ -1068,7 +1130,8 @@ int mw_scene_run(mw_scene* s, int32_t paused) {
         std::snprintf(msg, sizeof msg,
                       "this run dropped %lld contact points / constraint rows: a world exceeded the per-step "
                       "capacity (%d contact points, %d constraint rows)",
-                      static_cast<long long>(d), CMAX, mw::kScMaxRows);
+                      static_cast<long long>(d), s->dev.big ? s->dev.big_cmax : CMAX,
+                      s->dev.big ? s->dev.big_rows : mw::kScMaxRows);
         return fail(MW_ECAPACITY, msg);
     }
     const int64_t nd = static_cast<int64_t>(*s->h_ndiv);
@@ -1450,7 +1513,7 @@ int mw_scene_get_contacts(const mw_scene* cs, int32_t w, double* out, int32_t ca
     if (int rc = check(s)) return rc;
     if (!n || w < 0 || w >= s->W) return fail(MW_EINVAL, "bad argument");
     if (int rc = pull_contacts(s)) return rc;
-    const int nc = std::min(s->h_ncontact[w], CMAX);
+    const int nc = std::min(s->h_ncontact[w], s->contact_cap);
     *n = nc;
     const mw::SceneF& P = s->hp;
     for (int c = 0; c < nc && c < cap; ++c) {
@@ -1576,5 +1639,21 @@ extern "C" int mw_debug_hull(const double* pts, int32_t n, double* planes, int32
         edges[4 * e + 2] = h.ef[e][0];
         edges[4 * e + 3] = h.ef[e][1];
     }
+    return MW_OK;
+}
+
+// test hook (include/mwstep_testhooks.h): world w's large-contact workspace
+extern "C" int mw_debug_scene_big_ws(mw_scene* s, int32_t w, float* out, int64_t cap, int32_t* cmax, int32_t* rows) {
+    if (int rc = check(s)) return rc;
+    if (!out || !cmax || !rows || w < 0 || w >= s->W) return fail(MW_EINVAL, "bad argument");
+    const mw::SceneDev& D = s->dev;
+    *cmax = D.big ? D.big_cmax : 0;
+    *rows = D.big ? D.big_rows : 0;
+    if (!D.big) return MW_OK;
+    const int64_t n = std::min<int64_t>(cap, static_cast<int64_t>(mw::kScBigContactWords) * D.big_cmax +
+                                                  11LL * D.big_rows);
+    SC_HIP(hipStreamSynchronize(s->stream));
+    SC_HIP(hipMemcpy(out, D.big + static_cast<size_t>(w) * static_cast<size_t>(D.big_stride), n * sizeof(float),
+                     hipMemcpyDeviceToHost));
     return MW_OK;
 }

@@ -861,6 +861,725 @@ __device__ void sc_nancheck(const SceneF* __restrict__ P, const ScWorld<MAXNV>& 
 #define MW_SC_CHECK(ph, ncv)
 #endif
 
+// ---------------------------------------------------------- large-contact steps
+// DART's step has no contact cap (Physics.cpp:1824-1835; World.cpp:70-180
+// inserts any number of models).  A world-step with more contact points than
+// the LDS record holds (kScMaxContacts) or more rows than the 64-lane
+// register LCP runs its constraint phase in the world's workspace in HBM
+// (SceneDev::big, sized by the host from the scene's worst case up to
+// kScBigContacts points / kScBigRows rows): the same rows, responses and
+// Delassus arithmetic as the compact path, in 64-row batches through the LDS
+// rows, and DART's two-stage boxed LCP (wave_lcp.hpp header) by the same
+// primal active-set method as wave_boxqp over the whole system, each linear
+// solve a dense LDL^T of the free rows in 64x64 tiles in the workspace.
+// (Block Gauss-Seidel over 64-row exact blocks was tried first: on a row of
+// eight cubes in face contact, cond(A) ~ 1e6, its fp64 emulation needed 48
+// sweeps for stage 1 and stalled at 100x the tolerance in stage 2.)  Cold
+// start from PGS sweeps (the warm record keys kScMaxContacts points).
+constexpr int kScBigFields = 11;   // per-row fields of the workspace (below)
+struct ScBigWs {
+    float* base;   // this world's workspace, nullptr: none
+    int cmax, R;   // contact and row capacity (R: a multiple of 64)
+    int nvmax;     // the instance's MAXNV (leading dimension of J^T / MJ^T)
+    __device__ float* ct(int c) const { return base + static_cast<size_t>(c) * kScBigContactWords; }
+    // row fields: 0 joint-row source (3 body + type, int bits), 1 b, 2 lo, 3
+    // hi (the rows' own boxes), 4 stage-1 impulse, 5 / 6 the stage's box, 7
+    // active-set state (int bits: 0-1 held at none / lo / hi, 2 frozen, 3
+    // released), 8 gradient A x - b, 9 residual tolerance, 10 LDL^T pivot
+    __device__ float* row(int f) const {
+        return base + static_cast<size_t>(cmax) * kScBigContactWords + static_cast<size_t>(f) * R;
+    }
+    __device__ float* JT() const { return row(kScBigFields); }
+    __device__ float* MJT() const { return row(kScBigFields) + static_cast<size_t>(nvmax) * R; }
+    __device__ float* A() const { return row(kScBigFields) + 2 * static_cast<size_t>(nvmax) * R; }
+    __device__ float* Lf() const { return A() + static_cast<size_t>(R) * R; }
+};
+
+// LDS scratch of the large-contact LCP (inside ScWorld's union)
+struct ScBigLds {
+    float* xs;   // [kScBigRows] impulses
+    float* vs;   // [kScBigRows] the solve's right-hand side / result
+    float* T0;   // [64][64] the current diagonal tile: l_rc below, d_c on the diagonal
+    float* T1;   // [64][64] a panel tile
+};
+constexpr int kScBigLdsFloats = 2 * kScBigRows + 2 * 64 * 64;
+constexpr int kScBigSweeps = 24;   // PGS sweeps before each stage's active-set solve
+
+// contact c of the narrow phase into the workspace
+__device__ __forceinline__ void sc_big_put(const ScBigWs& G, int c, f3 x, f3 n, float dep, int na, int nb, int key) {
+    float* o = G.ct(c);
+    o[0] = x.x; o[1] = x.y; o[2] = x.z;
+    o[3] = n.x; o[4] = n.y; o[5] = n.z;
+    o[12] = dep;
+    o[13] = __int_as_float(na);
+    o[14] = __int_as_float(nb);
+    o[15] = __int_as_float(key);
+}
+
+// one 64x64 Delassus block on the matrix cores (the compact path's tiles):
+// rows from the LDS rows L.J (block i), columns from L.MJ (block j); lane c
+// ends with a[r] = J_r . MJ_c.  Columns >= NV of both are zero.
+template <int MAXNV>
+__device__ __forceinline__ void sc_tile64(const ScWorld<MAXNV>& L, int NV, float (&a)[kWaveLanes]) {
+    const int lane = lane_id();
+    const int lr = lane & 31, lh = lane >> 5;
+    v16f t00 = {}, t01 = {}, t10 = {}, t11 = {};
+    constexpr int kKs = MAXNV / 2;
+#pragma unroll
+    for (int k0 = 0; k0 < kKs; k0 += 4) {
+        if (2 * k0 >= NV) break;
+        float jv0[4], mv0[4], jv1[4], mv1[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int e = 2 * (k0 + kk) + lh;
+            jv0[kk] = L.J[lr][e];
+            mv0[kk] = L.MJ[lr][e];
+            jv1[kk] = L.J[32 + lr][e];
+            mv1[kk] = L.MJ[32 + lr][e];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv0[kk], mv0[kk], t00, 0, 0, 0);
+            t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv0[kk], mv1[kk], t01, 0, 0, 0);
+            t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv1[kk], mv0[kk], t10, 0, 0, 0);
+            t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(jv1[kk], mv1[kk], t11, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r0 = 8 * (i / 4) + (i % 4);
+        float x0 = t00[i], y0 = t01[i];
+        lane_swap32(x0, y0);
+        a[r0] = x0;
+        a[r0 + 4] = y0;
+        float x1 = t10[i], y1 = t11[i];
+        lane_swap32(x1, y1);
+        a[32 + r0] = x1;
+        a[32 + r0 + 4] = y1;
+    }
+}
+
+// (A x)_r for the lane's row r over the first n columns (A symmetric: column
+// r, coalesced over the lanes), compensated as lcp_matvec (Dot2); mag = sum
+// |A_rc x_c|.  Rows are padded to 64, so every read is inside A.
+__device__ __forceinline__ float sc_big_dot(const float* __restrict__ A, int R, const float* __restrict__ xs, int r,
+                                            int n, float& mag) {
+#pragma clang fp contract(off)
+    float w = 0.f, cc = 0.f, m = 0.f;
+    for (int c0 = 0; c0 < n; c0 += 8) {
+        float av[8], xv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            av[k] = A[static_cast<size_t>(c0 + k) * R + r];
+            xv[k] = (c0 + k < n) ? xs[c0 + k] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float p = av[k] * xv[k];
+            const float pe = fmaf(av[k], xv[k], -p);
+            const float t = w + p;
+            const float z = t - w;
+            cc += ((w - (t - z)) + (p - z)) + pe;
+            w = t;
+            m += fabsf(p);
+        }
+    }
+    mag = m;
+    return w + cc;
+}
+
+__device__ __forceinline__ int sc_st(const float* st, int r) { return __float_as_int(st[r]); }
+__device__ __forceinline__ bool sc_free(int st) { return (st & 3) == 0; }
+
+// Dense LDL^T of the free rows (row state 0; NR.. and held rows: identity)
+// in 64x64 tiles, right-looking, lane = column of a tile: Lf's lower
+// triangle ends with l_rc d_c (r > c), the pivots d_c in row field 10.
+__device__ __noinline__ void sc_big_factor(ScBigWs G, int NR, int nb, ScBigLds S) {
+    const int lane = lane_id();
+    const int R = G.R;
+    const float* A = G.A();
+    float* Lf = G.Lf();
+    const float* st = G.row(7);
+    float* dd = G.row(10);
+    for (int bi = 0; bi < nb; ++bi)
+        for (int bj = 0; bj <= bi; ++bj) {
+            const int c = bj * kWaveLanes + lane;
+            const bool fc = c < NR && sc_free(sc_st(st, c));
+            for (int i = 0; i < kWaveLanes; ++i) {
+                const int r = bi * kWaveLanes + i;
+                const bool fr = r < NR && sc_free(sc_st(st, r));
+                const float v = A[static_cast<size_t>(r) * R + c];
+                Lf[static_cast<size_t>(r) * R + c] = (fr && fc) ? v : ((r == c) ? 1.f : 0.f);
+            }
+        }
+    __threadfence_block();
+    for (int k = 0; k < nb; ++k) {
+        const size_t o = static_cast<size_t>(kWaveLanes * k) * R + kWaveLanes * k;   // tile (k, k)
+        // lane c: column c (the upper entries from row c: symmetric)
+        float t[kWaveLanes];
+#pragma unroll
+        for (int r = 0; r < kWaveLanes; ++r)
+            t[r] = (r >= lane) ? Lf[o + static_cast<size_t>(r) * R + lane] : Lf[o + static_cast<size_t>(lane) * R + r];
+#pragma unroll
+        for (int j = 0; j < kWaveLanes; ++j) {
+            float dj = read_lane(t[j], j);
+            dj = (fabsf(dj) < 1e-30f) ? 1e-30f : dj;   // the elimination's zero-pivot guard
+            const float lc = (lane > j) ? t[j] * rcp(dj) : 0.f;
+#pragma unroll
+            for (int r = j + 1; r < kWaveLanes; ++r) t[r] = fmaf(-read_lane(t[r], j), lc, t[r]);
+        }
+        float dc = 1.f;
+#pragma unroll
+        for (int r = 0; r < kWaveLanes; ++r) dc = (r == lane) ? t[r] : dc;
+        dc = (fabsf(dc) < 1e-30f) ? 1e-30f : dc;
+        const float ic = rcp(dc);
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < kWaveLanes; ++r) {
+            if (r > lane) Lf[o + static_cast<size_t>(r) * R + lane] = t[r];
+            S.T0[r * kWaveLanes + lane] = (r > lane) ? t[r] * ic : ((r == lane) ? dc : 0.f);
+        }
+        dd[kWaveLanes * k + lane] = dc;
+        wave_lds_sync();
+        __threadfence_block();
+        // panels below: W_ik = A_ik L_kk^-T (= L_ik D_k), lane = row of tile i
+        for (int i = k + 1; i < nb; ++i) {
+            float* row = Lf + static_cast<size_t>(kWaveLanes * i + lane) * R + kWaveLanes * k;
+            float x[kWaveLanes];
+#pragma unroll
+            for (int c = 0; c < kWaveLanes; ++c) x[c] = row[c];
+#pragma unroll
+            for (int c = 1; c < kWaveLanes; ++c) {
+#pragma unroll
+                for (int j = 0; j < c; ++j) x[c] = fmaf(-x[j], S.T0[c * kWaveLanes + j], x[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < kWaveLanes; ++c) row[c] = x[c];
+        }
+        __threadfence_block();
+        // trailing tiles (i, j), k < j <= i: S_ij -= W_ik D_k^-1 W_jk^T, lane = column of tile j
+        for (int j = k + 1; j < nb; ++j) {
+            const float* wrow = Lf + static_cast<size_t>(kWaveLanes * j + lane) * R + kWaveLanes * k;
+            float wj[kWaveLanes];
+#pragma unroll
+            for (int kk = 0; kk < kWaveLanes; ++kk) wj[kk] = wrow[kk] * rcp(S.T0[kk * kWaveLanes + kk]);
+            for (int i = j; i < nb; ++i) {
+                wave_lds_sync();
+                for (int r = 0; r < kWaveLanes; ++r)
+                    S.T1[r * kWaveLanes + lane] = Lf[static_cast<size_t>(kWaveLanes * i + r) * R + kWaveLanes * k + lane];
+                wave_lds_sync();
+                for (int r = 0; r < kWaveLanes; ++r) {
+                    float* a = Lf + static_cast<size_t>(kWaveLanes * i + r) * R + kWaveLanes * j + lane;
+                    float acc = *a;
+#pragma unroll
+                    for (int kk = 0; kk < kWaveLanes; ++kk) acc = fmaf(-S.T1[r * kWaveLanes + kk], wj[kk], acc);
+                    *a = acc;
+                }
+            }
+        }
+        __threadfence_block();
+    }
+}
+
+// L D L^T v = vs in place (vs: LDS, rows 0 .. 64 nb)
+__device__ __noinline__ void sc_big_solve(ScBigWs G, int nb, ScBigLds S) {
+    const int lane = lane_id();
+    const int R = G.R;
+    const float* Lf = G.Lf();
+    const float* dd = G.row(10);
+    // forward: L z = v (unit lower, L_rc = Lf_rc / d_c)
+    for (int k = 0; k < nb; ++k) {
+        const int r = kWaveLanes * k + lane;
+        const float* row = Lf + static_cast<size_t>(r) * R;
+        float z = S.vs[r];
+        for (int j = 0; j < k; ++j)
+            for (int c = kWaveLanes * j; c < kWaveLanes * (j + 1); ++c) z = fmaf(-row[c], S.vs[c], z);   // vs: y = z / d
+        float lr[kWaveLanes];
+#pragma unroll
+        for (int c = 0; c < kWaveLanes; ++c) lr[c] = row[kWaveLanes * k + c] * rcp(dd[kWaveLanes * k + c]);
+#pragma unroll
+        for (int c = 0; c < kWaveLanes; ++c) {
+            const float zc = read_lane(z, c);
+            z = (lane > c) ? fmaf(-lr[c], zc, z) : z;
+        }
+        wave_lds_sync();
+        S.vs[r] = z * rcp(dd[r]);
+        wave_lds_sync();
+    }
+    // backward: L^T x = y
+    for (int k = nb - 1; k >= 0; --k) {
+        const int r = kWaveLanes * k + lane;
+        const float ir = rcp(dd[r]);
+        float y = S.vs[r];
+        for (int c = kWaveLanes * (k + 1); c < kWaveLanes * nb; ++c)
+            y = fmaf(-Lf[static_cast<size_t>(c) * R + r] * ir, S.vs[c], y);
+        float lc[kWaveLanes];
+#pragma unroll
+        for (int c = 0; c < kWaveLanes; ++c) lc[c] = Lf[static_cast<size_t>(kWaveLanes * k + c) * R + r] * ir;
+#pragma unroll
+        for (int c = kWaveLanes - 1; c >= 0; --c) {
+            const float xc = read_lane(y, c);
+            y = (lane < c) ? fmaf(-lc[c], xc, y) : y;
+        }
+        wave_lds_sync();
+        S.vs[r] = y;
+        wave_lds_sync();
+    }
+}
+
+// PGS sweeps over the whole system (rows in order) from xs: fixed boxes
+// (row fields 5 / 6: the exact solve's start) or, coupled, DART's PGS
+// (friction boxed by the current normal, joint rows by fields 2 / 3).
+// Lane l holds w of rows l + 64 k; the sweep stops once no row moved w by
+// more than tol (tol < 0: never).
+__device__ __noinline__ void sc_big_pgs(ScBigWs G, int NR, int ncr, float mu, int sweeps, bool coupled, float tol,
+                                        ScBigLds S) {
+    const int lane = lane_id();
+    const int R = G.R;
+    const float* A = G.A();
+    const float* b = G.row(1);
+    const float* lo = G.row(coupled ? 2 : 5);
+    const float* hi = G.row(coupled ? 3 : 6);
+    constexpr int KB = kScBigRows / kWaveLanes;
+    for (int it = 0; it < sweeps; ++it) {
+        float wk[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            float mg;
+            wk[k] = (k * kWaveLanes < NR) ? sc_big_dot(A, R, S.xs, k * kWaveLanes + lane, NR, mg) : 0.f;
+        }
+        float h = 0.f, moved = 0.f;
+        for (int r = 0; r < NR; ++r) {
+            const int kr = r / kWaveLanes;
+            float wr = 0.f;
+#pragma unroll
+            for (int k = 0; k < KB; ++k) wr = (k == kr) ? read_lane(wk[k], r % kWaveLanes) : wr;
+            const float xr = S.xs[r];
+            const float arr = A[static_cast<size_t>(r) * R + r];
+            float v = xr + (b[r] - wr) * rcp(arr);
+            if (coupled && r < ncr) {
+                if (r % 3 == 0) {
+                    v = clamp_ordered(v, 0.f, kBig);
+                    h = mu * v;
+                } else {
+                    v = clamp_ordered(v, -h, h);
+                }
+            } else {
+                v = clamp_ordered(v, lo[r], hi[r]);
+            }
+            const float dl = v - xr;
+            moved = fmaxf(moved, fabsf(dl * arr));
+#pragma unroll
+            for (int k = 0; k < KB; ++k)
+                if (k * kWaveLanes < NR) wk[k] = fmaf(A[static_cast<size_t>(r) * R + k * kWaveLanes + lane], dl, wk[k]);
+            if (lane == 0) S.xs[r] = v;   // read again in the next sweep (every lane holds v)
+        }
+        wave_lds_sync();
+        if (moved <= tol) break;
+    }
+}
+
+// One stage's box QP (bounds: row fields 5 / 6) over the whole system by
+// wave_boxqp's primal active-set method (the same rules: several releases at
+// once until a release blocks at zero length, frozen rows, refinement solves
+// to the fp32 floor), from xs; budget linear solves.  Returns true when
+// every row's complementarity residual is within tolerance.
+__device__ __noinline__ bool sc_big_boxqp(ScBigWs G, int NR, int nb, int budget, ScBigLds S, int& solves) {
+    const int lane = lane_id();
+    const int R = G.R;
+    const float* A = G.A();
+    const float* b = G.row(1);
+    const float* Ls = G.row(5);
+    const float* Us = G.row(6);
+    float* st = G.row(7);
+    float* gg = G.row(8);
+    float* tl = G.row(9);
+    float* xs = S.xs;
+    auto set_st = [&](int r, int v) { st[r] = __int_as_float(v); };
+    // working set from the start point (a row on a bound starts held there)
+    {
+        float xm = 0.f;
+        for (int r = lane; r < NR; r += kWaveLanes) xm = fmaxf(xm, fabsf(xs[r]));
+        const float t0 = 2e-6f * (1.f + wave_fmax(xm));
+        for (int r = lane; r < 64 * nb; r += kWaveLanes) {
+            int w = 1;
+            if (r < NR) {
+                const float L = Ls[r], U = Us[r];
+                float x = fminf(fmaxf(xs[r], L), U);
+                const bool pinned = U - L <= 0.f;
+                w = pinned ? 1 : ((x <= L + t0) ? 1 : ((x >= U - t0) ? 2 : 0));
+                x = (w == 1) ? L : ((w == 2) ? U : x);
+                xs[r] = x;
+            }
+            set_st(r, w);
+        }
+    }
+    wave_lds_sync();
+    __threadfence_block();
+    bool at_min = true;
+    for (int r = lane; r < NR; r += kWaveLanes)
+        if (sc_free(sc_st(st, r)) && Us[r] - Ls[r] > 0.f) at_min = false;
+    at_min = __ballot(!at_min) == 0ull;
+    bool stalled = false, fresh = false, single = false, factored = false;
+    float rel = 0.f, xmax = 0.f, rel_refine = 3.4e38f;
+    for (int it = 0; it < 4 * budget + 8 + NR; ++it) {
+        if (!fresh) {
+            float xm = 0.f;
+            for (int r = lane; r < NR; r += kWaveLanes) xm = fmaxf(xm, fabsf(xs[r]));
+            xmax = wave_fmax(xm);
+            float e = 0.f;
+            for (int r = lane; r < 64 * nb; r += kWaveLanes) {
+                const bool live = r < NR;
+                float mg = 0.f;
+                const float w = live ? sc_big_dot(A, R, xs, r, NR, mg) : 0.f;
+                const float br = live ? b[r] : 0.f;
+                gg[r] = w - br;
+                tl[r] = kLcpRelTol * (fabsf(br) + mg) + kLcpAbsTol;
+                float ea;
+                e = fmaxf(e, lcp_row_residual(live, br, live ? xs[r] : 0.f, w, mg,
+                                              live ? A[static_cast<size_t>(r) * R + r] : 1.f, live ? Ls[r] : 0.f,
+                                              live ? Us[r] : 0.f, 2e-6f * (1.f + xmax), ea));
+            }
+            rel = wave_fmax(e);
+            __threadfence_block();
+            if (rel <= 1.f) return true;
+            fresh = true;
+        }
+        if (at_min) {
+            at_min = false;
+            // held rows whose multiplier is wrongly signed beyond tolerance leave
+            float vmax = 0.f, vrow = 3.4e38f;
+            for (int r = lane; r < NR; r += kWaveLanes) {
+                const int s = sc_st(st, r);
+                const bool pinned = Us[r] - Ls[r] <= 0.f;
+                float v = ((s & 3) == 1) ? -gg[r] : (((s & 3) == 2) ? gg[r] : 0.f);
+                v = (pinned || (s & 4)) ? 0.f : v * rcp(tl[r]);
+                if (v > vmax) { vmax = v; vrow = static_cast<float>(r); }
+            }
+            const float vm = wave_fmax(vmax);
+            if (vm > 1.f) {
+                const float first = wave_fmin((vmax == vm) ? vrow : 3.4e38f);
+                for (int r = lane; r < NR; r += kWaveLanes) {
+                    int s = sc_st(st, r) & ~8;
+                    const bool pinned = Us[r] - Ls[r] <= 0.f;
+                    float v = ((s & 3) == 1) ? -gg[r] : (((s & 3) == 2) ? gg[r] : 0.f);
+                    v = (pinned || (s & 4)) ? 0.f : v * rcp(tl[r]);
+                    const bool rel_me = single ? (static_cast<float>(r) == first) : (v > 1.f);
+                    if (rel_me) s = (s & ~3) | 8;
+                    set_st(r, s);
+                }
+                __threadfence_block();
+                factored = false;
+                stalled = false;
+                continue;
+            }
+            if (stalled || rel > 0.5f * rel_refine) return rel <= kLcpFloorAccept;
+            rel_refine = rel;
+        } else {
+            rel_refine = 3.4e38f;
+        }
+        if (solves >= budget) return false;
+        // ---- one linear solve over the free rows
+        if (!factored) {
+            sc_big_factor(G, NR, nb, S);
+            factored = true;
+        }
+        for (int r = lane; r < 64 * nb; r += kWaveLanes) {
+            const bool fr = r < NR && sc_free(sc_st(st, r)) && Us[r] - Ls[r] > 0.f;
+            S.vs[r] = fr ? -gg[r] : 0.f;
+        }
+        wave_lds_sync();
+        sc_big_solve(G, nb, S);
+        ++solves;
+        float dmax = 0.f, dres = 0.f;
+        for (int r = lane; r < NR; r += kWaveLanes) {
+            const bool fr = sc_free(sc_st(st, r)) && Us[r] - Ls[r] > 0.f;
+            const float d = fr ? S.vs[r] : 0.f;
+            dmax = fmaxf(dmax, fabsf(d));
+            dres = fmaxf(dres, fabsf(d) * A[static_cast<size_t>(r) * R + r] * rcp(tl[r]));
+        }
+        dmax = wave_fmax(dmax);
+        dres = wave_fmax(dres);
+        if (dmax <= kLcpStall * (1.f + xmax) && dres <= 1.f) {
+            // the release moved nothing: its rows back to their bounds, frozen
+            bool any = false;
+            for (int r = lane; r < NR; r += kWaveLanes) {
+                int s = sc_st(st, r);
+                if (s & 8) {
+                    s = (s & ~(3 | 8)) | 4 | ((xs[r] <= Ls[r]) ? 1 : 2);
+                    set_st(r, s);
+                    any = true;
+                }
+            }
+            if (__ballot(any)) factored = false;
+            __threadfence_block();
+            at_min = true;
+            stalled = true;
+            continue;
+        }
+        stalled = false;
+        fresh = false;
+        // the longest feasible step along d (at most 1) and the first row it blocks
+        float amin_l = 1.f, arow = 3.4e38f;
+        for (int r = lane; r < NR; r += kWaveLanes) {
+            const bool fr = sc_free(sc_st(st, r)) && Us[r] - Ls[r] > 0.f;
+            const float d = S.vs[r], x = xs[r];
+            float al = 1.f;
+            if (fr && d < 0.f && x + d < Ls[r]) al = (Ls[r] - x) * rcp(d);
+            else if (fr && d > 0.f && x + d > Us[r]) al = (Us[r] - x) * rcp(d);
+            al = fmaxf(al, 0.f);
+            if (al < amin_l) { amin_l = al; arow = static_cast<float>(r); }
+        }
+        const float amin = wave_fmin(amin_l);
+        int nrel = 0;   // released rows
+        for (int k = 0; k < nb; ++k) {
+            const int r = kWaveLanes * k + lane;
+            nrel += __builtin_popcountll(__ballot(r < NR && (sc_st(st, r) & 8)));
+        }
+        wave_lds_sync();
+        if (amin < 1.f) {
+            const int block = static_cast<int>(wave_fmin((amin_l == amin) ? arow : 3.4e38f));
+            bool back = false;
+            const bool block_rel = (sc_st(st, block) & 8) != 0;   // uniform read
+            if (amin <= 0.f && block_rel) {
+                if (nrel > 1) {
+                    single = true;
+                } else {
+                    back = true;   // the single released row blocks at once: frozen, back to the working set before
+                }
+            }
+            for (int r = lane; r < NR; r += kWaveLanes) {
+                int s = sc_st(st, r);
+                const bool fr = sc_free(s) && Us[r] - Ls[r] > 0.f;
+                const float d = S.vs[r];
+                float x = xs[r];
+                if (fr) x += amin * d;
+                int side = 0;
+                float al = 1.f;
+                if (fr && d < 0.f && xs[r] + d < Ls[r]) { al = (Ls[r] - xs[r]) * rcp(d); side = 1; }
+                else if (fr && d > 0.f && xs[r] + d > Us[r]) { al = (Us[r] - xs[r]) * rcp(d); side = 2; }
+                al = fmaxf(al, 0.f);
+                if (r == block) side = (side == 0) ? ((d < 0.f) ? 1 : 2) : side;
+                // the blocking row, and on a zero-length step every row it blocks, join their bound
+                if (r == block || (amin <= 0.f && fr && side != 0 && al <= 0.f)) {
+                    x = (side == 1) ? Ls[r] : Us[r];
+                    s = (s & ~3) | side;
+                }
+                if (back && (s & 8)) s |= 4;
+                s &= ~8;
+                xs[r] = x;
+                set_st(r, s);
+            }
+            at_min = back;
+        } else {
+            for (int r = lane; r < NR; r += kWaveLanes) {
+                const int s = sc_st(st, r);
+                const bool fr = sc_free(s) && Us[r] - Ls[r] > 0.f;
+                if (fr) xs[r] += S.vs[r];
+                set_st(r, s & ~8);
+            }
+            at_min = true;
+            single = false;
+        }
+        factored = factored && amin >= 1.f;
+        wave_lds_sync();
+        __threadfence_block();
+    }
+    return false;
+}
+
+struct ScBigOut {
+    int nc, ovf, unconv;
+};
+
+// The constraint phase of a large-contact world-step (header above): rows,
+// responses, Delassus, LCP, nu += MJ^T x and the contacts' impulses.  Joint
+// rows of body `lane`: jbits (bit t: limit / servo / friction), their b / lo /
+// hi, jbefore of them on lower lanes, tj in all.
+template <int MAXNV>
+__device__ __noinline__ ScBigOut sc_big_constraints(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, ScBigWs G,
+                                                    int nc_all, uint32_t jbits, float jb0, float jb1, float jb2,
+                                                    float jlo0, float jlo1, float jlo2, float jhi0, float jhi1,
+                                                    float jhi2, int jbefore, int tj, float dt, float mu,
+                                                    int pgs_iters, int lcp_solves) {
+    const int lane = lane_id();
+    const int NV = P->nv, R = G.R;
+    ScBigOut out{0, 0, 0};
+    const int nc = nc_all < G.cmax ? nc_all : G.cmax;
+    if (nc_all > G.cmax) out.ovf += nc_all - G.cmax;
+    out.nc = nc;
+    // the first kScMaxContacts points sit in the LDS record
+    if (lane < nc && lane < kScMaxContacts)
+        sc_big_put(G, lane, mk(L.c_p[lane][0], L.c_p[lane][1], L.c_p[lane][2]),
+                   mk(L.c_n[lane][0], L.c_n[lane][1], L.c_n[lane][2]), L.c_d[lane], L.c_na[lane], L.c_nb[lane],
+                   L.c_key[lane]);
+    __threadfence_block();
+    for (int c = lane; c < nc; c += kWaveLanes) {
+        float* o = G.ct(c);
+        f3 t1, t2;
+        plane_space_f(mk(o[3], o[4], o[5]), t1, t2);
+        o[6] = t1.x; o[7] = t1.y; o[8] = t1.z;
+        o[9] = t2.x; o[10] = t2.y; o[11] = t2.z;
+        o[16] = o[17] = o[18] = 0.f;
+    }
+    // ---- rows: contact c's rows 3 c + d, then the joint rows
+    const int ncr = 3 * nc;
+    int NR = ncr + tj;
+    if (NR > R) {
+        out.ovf += NR - R;
+        NR = R;
+    }
+    float* rsrc = G.row(0);
+    float* rb = G.row(1);
+    float* rlo = G.row(2);
+    float* rhi = G.row(3);
+    float* rx1 = G.row(4);
+    float* rL = G.row(5);
+    float* rU = G.row(6);
+    if (jbits) {
+        int r = ncr + jbefore;
+        const float jbv[3] = {jb0, jb1, jb2}, jlov[3] = {jlo0, jlo1, jlo2}, jhiv[3] = {jhi0, jhi1, jhi2};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            if (((jbits >> t) & 1u) && r < NR) {
+                rsrc[r] = __int_as_float(3 * lane + t);
+                rb[r] = jbv[t];
+                rlo[r] = jlov[t];
+                rhi[r] = jhiv[t];
+                ++r;
+            }
+        }
+    }
+    for (int r = lane; r < ncr && r < NR; r += kWaveLanes) {
+        rlo[r] = 0.f;
+        rhi[r] = kBig;
+    }
+    __threadfence_block();
+    float* JT = G.JT();
+    float* MJT = G.MJT();
+    float* A = G.A();
+    // ---- responses, 64 rows at a time through the LDS rows (lane = row)
+    for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
+        const int r = r0 + lane;
+        float* Jr = L.J[lane];
+        float* MJr = L.MJ[lane];
+        for (int e = 0; e < MAXNV; ++e) { Jr[e] = 0.f; MJr[e] = 0.f; }
+        if (r < NR) {
+            if (r < ncr) {
+                const int c = r / 3, d = r % 3;
+                const float* o = G.ct(c);
+                const f3 dw = mk(o[3 + 3 * d], o[4 + 3 * d], o[5 + 3 * d]);
+                const f3 xp = mk(o[0], o[1], o[2]);
+                float jv = 0.f;
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const int k = __float_as_int(o[side ? 14 : 13]);
+                    if (k >= 0) {
+                        const ScNode& nd = L.node[k];
+                        const f3 bpt = mulT(nd.Rw, xp - nd.pw);
+                        const f3 dk = mulT(nd.Rw, dw);
+                        const float sg = side ? -1.f : 1.f;
+                        const SV f = {sg * cross(bpt, dk), sg * dk};
+                        jv += sc_response<MAXNV>(P, L, k, -1, f, Jr, MJr);
+                    }
+                }
+                const float bounce = (d == 0) ? fminf(kContactErp * o[12] * rcp(dt), kContactMaxErv) : 0.f;
+                rb[r] = bounce - jv;
+            } else {
+                const int j = __float_as_int(rsrc[r]) / 3;
+                (void)sc_response<MAXNV>(P, L, -1, j, SV{{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, Jr, MJr);
+                for (int e = 0; e < MAXNV; ++e) Jr[e] = 0.f;
+                Jr[P->body_coord[j]] = 1.f;
+            }
+            for (int e = 0; e < NV; ++e) {
+                JT[static_cast<size_t>(e) * R + r] = Jr[e];
+                MJT[static_cast<size_t>(e) * R + r] = MJr[e];
+            }
+        }
+    }
+    __threadfence_block();
+    // ---- Delassus A = J MJ^T, block by block on the matrix cores (rows and
+    // columns NR .. 64 nb zero)
+    const int nblk = (NR + kWaveLanes - 1) / kWaveLanes;
+    for (int bi = 0; bi < nblk; ++bi) {
+        wave_lds_sync();
+        {
+            const int r = bi * kWaveLanes + lane;
+            for (int e = 0; e < MAXNV; ++e)
+                L.J[lane][e] = (r < NR && e < NV) ? JT[static_cast<size_t>(e) * R + r] : 0.f;
+        }
+        for (int bj = 0; bj < nblk; ++bj) {
+            wave_lds_sync();
+            {
+                const int r = bj * kWaveLanes + lane;
+                for (int e = 0; e < MAXNV; ++e)
+                    L.MJ[lane][e] = (r < NR && e < NV) ? MJT[static_cast<size_t>(e) * R + r] : 0.f;
+            }
+            wave_lds_sync();
+            float a[kWaveLanes];
+            sc_tile64<MAXNV>(L, NV, a);
+            const int gc = bj * kWaveLanes + lane;
+#pragma unroll
+            for (int i = 0; i < kWaveLanes; ++i) {
+                const int gr = bi * kWaveLanes + i;
+                float v = (gr < NR && gc < NR) ? a[i] : 0.f;
+                if (gr == gc && gr < NR) v *= 1.f + ((gr >= ncr) ? kJointCfm : kContactCfm);
+                A[static_cast<size_t>(gr) * R + gc] = v;
+            }
+        }
+    }
+    __threadfence_block();
+    // ---- the LCP (scratch in the LDS union, dead since the responses)
+    static_assert(sizeof(L.A) >= kScBigLdsFloats * sizeof(float), "large-contact LCP scratch");
+    float* base = &L.A[0][0];
+    const ScBigLds S{base, base + kScBigRows, base + 2 * kScBigRows, base + 2 * kScBigRows + 64 * 64};
+    for (int r = lane; r < kWaveLanes * nblk; r += kWaveLanes) S.xs[r] = 0.f;
+    wave_lds_sync();
+    bool ok = true;
+    if (lcp_solves > 0) {
+        for (int s = 1; s <= 2; ++s) {
+            int solves = 0;
+            // the stage's boxes: stage 1 friction pinned at 0; stage 2 friction
+            // boxed by mu x_n of the contact's stage-1 normal
+            for (int r = lane; r < NR; r += kWaveLanes) {
+                float lo = rlo[r], hi = rhi[r];
+                if (r < ncr && r % 3 != 0) {
+                    hi = (s == 1) ? 0.f : mu * fmaxf(rx1[r - r % 3], 0.f);
+                    lo = -hi;
+                }
+                rL[r] = lo;
+                rU[r] = hi;
+                S.xs[r] = fminf(fmaxf(S.xs[r], lo), hi);
+            }
+            wave_lds_sync();
+            __threadfence_block();
+            // (a cold start: more sweeps than the compact path's, and a budget
+            // that grows with the rows -- fp64 emulation on rows of eight
+            // cubes: 6 sweeps then 10-54 solves in stage 2, 24 sweeps then 5-28)
+            sc_big_pgs(G, NR, ncr, mu, kScBigSweeps, false, kScExactPgsTol, S);
+            ok = sc_big_boxqp(G, NR, nblk, lcp_solves + NR / 2, S, solves) && ok;
+            wave_lds_sync();
+            if (s == 1) {
+                for (int r = lane; r < NR; r += kWaveLanes) rx1[r] = S.xs[r];
+                __threadfence_block();
+            }
+        }
+    } else {
+        sc_big_pgs(G, NR, ncr, mu, pgs_iters, true, -1.f, S);
+    }
+    if (!ok) out.unconv = 1;
+    // ---- nu += MJ^T x (lane = coordinate); the contacts' impulses
+    if (lane < NV) {
+        float dnu = 0.f;
+        for (int r = 0; r < NR; ++r) dnu = fmaf(MJT[static_cast<size_t>(lane) * R + r], S.xs[r], dnu);
+        L.nu[lane] += dnu;
+    }
+    for (int r = lane; r < ncr && r < NR; r += kWaveLanes) G.ct(r / 3)[16 + r % 3] = S.xs[r];
+    __threadfence_block();
+    wave_lds_sync();
+    return out;
+}
+
 // ------------------------------------------------------------------- step
 // (a real call, not inlined: __forceinline__ took scratch 944 -> 768 B per
 // lane but the scene leg 0.909 -> 0.976 ms, profiles/r05ag)
@@ -868,7 +1587,7 @@ template <int MAXNV>
 __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeState& base, uint32_t present,
                         const float (&wr)[kScWrenchSlots][6], const int32_t (&wl)[kScWrenchSlots], int iter,
                         float dt, int pgs_iters, int lcp_solves, const ScWarm& warm, const f3 gw, float mu,
-                        int& nc_out, int& ovf, int& unconv) {
+                        ScBigWs big, int& nc_out, bool& big_out, int& ovf, int& unconv) {
     const int lane = lane_id();
     MW_PROF_T(t_in);
 #ifdef MW_SC_NANCHECK
@@ -1084,6 +1803,8 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 L.c_na[c] = na;
                 L.c_nb[c] = -1;
                 L.c_key[c] = slot;
+            } else if (hit && big.base && nc + rank < big.cmax) {
+                sc_big_put(big, nc + rank, xw, mk(0.f, 0.f, 1.f), dep, na, -1, slot);
             }
             nc += __popcll(bal);
         }
@@ -1149,12 +1870,17 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 L.c_na[c] = na;
                 L.c_nb[c] = nb;
                 L.c_key[c] = P->n_slots + 4 * pr + i;
+            } else if (big.base && c < big.cmax) {
+                sc_big_put(big, c, out.pt(i), nrm, out.dep(i), na, nb, P->n_slots + 4 * pr + i);
             }
         }
         nc += total;
     }
+    // more points than the LDS record: the large-contact path when the scene
+    // has its workspace, else the excess is dropped (counted)
+    const int nc_all = nc;
     if (nc > kScMaxContacts) {
-        ovf += nc - kScMaxContacts;
+        if (!big.base) ovf += nc - kScMaxContacts;
         nc = kScMaxContacts;
     }
     if (lane < nc) {
@@ -1209,13 +1935,15 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
     int tj = 0;
     const int jbefore = wave_prefix7(__builtin_popcount(jbits), tj);
+    const bool use_big = big.base != nullptr && (nc_all > kScMaxContacts || 3 * nc_all + tj > kWaveLanes);
+    big_out = use_big;
     const int ncr = 3 * nc;
-    int NR = ncr + tj;
+    int NR = use_big ? 0 : ncr + tj;   // a large-contact step skips the compact constraint phase
     if (NR > kScMaxRows) {
         ovf += NR - kScMaxRows;
         NR = kScMaxRows;
     }
-    if (lane < nc) {
+    if (lane < nc && !use_big) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             L.src[3 * lane + d] = 3 * lane + d;
@@ -1223,7 +1951,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
             L.rhi[3 * lane + d] = kBig;
         }
     }
-    if (jlane) {
+    if (jlane && !use_big) {
         int r = ncr + jbefore;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
@@ -1243,6 +1971,14 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #ifdef MW_WAVE_PROF
     long long t_resp = t_rows, t_del = t_rows, t_lcp = t_rows;
 #endif
+    if (use_big) {
+        const ScBigOut bo = sc_big_constraints<MAXNV>(P, L, big, nc_all, jbits, jb[0], jb[1], jb[2], jlo[0], jlo[1],
+                                                      jlo[2], jhi[0], jhi[1], jhi[2], jbefore, tj, dt, mu, pgs_iters,
+                                                      lcp_solves);
+        nc = bo.nc;
+        ovf += bo.ovf;
+        unconv += bo.unconv;
+    }
     if (NR > 0) {
         // ---- responses, lane = row
         for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
@@ -1771,13 +2507,16 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
         }
     }
     int nc = 0, ovf = 0, unconv = 0;
+    bool big_last = false;   // the last substep took the large-contact path: its contacts are in big
     const ScWarm warm{A.lcp_solves > 0 ? D.warm : nullptr, W, w};
+    const ScBigWs big{D.big ? D.big + static_cast<size_t>(w) * static_cast<size_t>(D.big_stride) : nullptr, D.big_cmax,
+                      D.big_rows, MAXNV};
     if (!A.paused) {
         for (int s = 0; s < A.substeps; ++s) {
             if (lane < NB && ((present >> P->body_model[lane]) & 1u))
                 L.tau[lane] = sc_dof_force(P, D, pid, G, W, w, A, s, lane, act, cmd, vc, L.q[lane], L.qd[lane]);
             sc_step<MAXNV>(P, L, base, present, wr, wl, A.iter0 + s + 1, A.dt, A.pgs_iters, A.lcp_solves, warm, gw,
-                           mu, nc, ovf, unconv);
+                           mu, big, nc, big_last, ovf, unconv);
         }
     }
     bool bad = false;
@@ -1820,7 +2559,20 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
             if (ovf) atomicAdd(D.overflow, ovf);
             if (unconv) atomicAdd(reinterpret_cast<unsigned long long*>(D.overflow + 2), static_cast<unsigned long long>(unconv));
         }
-        if (A.want_contacts && lane < nc) {
+        if (A.want_contacts && big_last) {
+            for (int c = lane; c < nc; c += kWaveLanes) {
+                const float* g = big.ct(c);
+                float* o = D.contact + static_cast<size_t>(c) * 12 * W + w;
+                const f3 n = mk(g[3], g[4], g[5]);
+                const f3 f = A.inv_dt * (g[16] * n + g[17] * mk(g[6], g[7], g[8]) + g[18] * mk(g[9], g[10], g[11]));
+                o[0 * W] = g[0]; o[1 * W] = g[1]; o[2 * W] = g[2];
+                o[3 * W] = n.x; o[4 * W] = n.y; o[5 * W] = n.z;
+                o[6 * W] = f.x; o[7 * W] = f.y; o[8 * W] = f.z;
+                o[9 * W] = g[12];
+                o[10 * W] = g[13];
+                o[11 * W] = g[14];
+            }
+        } else if (A.want_contacts && lane < nc) {
             const float inv_dt = A.inv_dt;
             float* o = D.contact + static_cast<size_t>(lane) * 12 * W + w;
             const f3 n = mk(L.c_n[lane][0], L.c_n[lane][1], L.c_n[lane][2]);

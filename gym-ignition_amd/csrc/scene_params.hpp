@@ -32,6 +32,16 @@ constexpr int kScWrenchSlots = 4;       // concurrent wrenches (distinct expirie
 constexpr int kScMaxDepth = 12;         // tree depth of the response passes' stacks
 constexpr uint32_t kScGroundBit = 1u << 31;  // present mask: the world has a ground plane
 constexpr int kScMaxHulls = 8;          // mesh shapes with a collision hull (hull.hpp)
+// Large-contact world-steps (scene_kernel.hip sc_big_constraints): a step with
+// more than kScMaxContacts contact points, or more constraint rows than the
+// 64-lane register LCP holds, keeps its contacts, Jacobian / response rows and
+// Delassus matrix in a per-world workspace in HBM (SceneDev::big) of up to
+// this capacity, and solves DART's two stages by block Gauss-Seidel over
+// 64-row blocks, each block an exact box QP (wave_lcp.hpp wave_boxqp)
+constexpr int kScBigContacts = 128;
+constexpr int kScBigRows = 512;         // 8 blocks of 64: contact rows 3 c + d, then joint rows
+constexpr int kScBigContactWords = 20;  // p[3] n[3] t1[3] t2[3] depth, node A, node B, key, x[3], pad
+constexpr int kScPairMaxPoints = 8;     // contact points of one shape pair (worst-case sizing)
 
 // A mesh shape's collision hull (hull.hpp build_hull, float32, shape frame):
 // vertices, outward face planes (n, d: inside n . x <= d), face polygons
@@ -146,7 +156,22 @@ struct SceneDev {
     // state so the run needs no readback copy; nullptr otherwise
     float* rb;
     int32_t rb_plane;
+    // large-contact workspace (nullptr: the scene cannot exceed the compact
+    // capacity, or has no shapes): big_stride floats per world -- contacts
+    // [big_cmax][kScBigContactWords], row fields [11][big_rows]
+    // (scene_kernel.hip ScBigWs), J^T and MJ^T [MAXNV][big_rows], A
+    // [big_rows][big_rows] (symmetric, CFM on the diagonal), its LDL^T
+    float* big;
+    int64_t big_stride;
+    int32_t big_cmax, big_rows;
+    int32_t contact_cap;  // contact points per world the contact output holds
 };
+
+// floats of one world's large-contact workspace (host sizing and device views agree)
+inline constexpr int64_t sc_big_world_floats(int cmax, int rows, int maxnv) {
+    return static_cast<int64_t>(kScBigContactWords) * cmax + 11LL * rows + 2LL * maxnv * rows +
+           2 * static_cast<int64_t>(rows) * rows;   // row fields, J^T / MJ^T, A and its LDL^T
+}
 
 constexpr int kScWarmJoint0 = 3 * kScMaxContacts;
 constexpr int kScWarmRows = kScWarmJoint0 + 3 * kScMaxBodies;

@@ -166,6 +166,7 @@ TEST_SIGNATURES = [
     ("mw_debug_lcp_solve", ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                           ctypes.c_uint64, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     ("mw_debug_hull", ctypes.c_int, [_D, _I, _D, _IP, _IP, _IP]),
+    ("mw_debug_scene_big_ws", ctypes.c_int, [_P, _I, ctypes.POINTER(ctypes.c_float), ctypes.c_int64, _IP, _IP]),
 ]
 
 SCENE_SIGNATURES = [

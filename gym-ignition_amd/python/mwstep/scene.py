@@ -332,9 +332,12 @@ class Scene:
     # ---------------------------------------------------- contacts, wrenches
     def contacts(self, w: int = 0) -> np.ndarray:
         """rows: point(3), normal B->A (3), force on A (3), depth, model A, link A, model B, link B"""
-        out = np.zeros((32, 14))
+        out = np.zeros((128, 14))   # kScBigContacts: the large-contact capacity
         n = ctypes.c_int32()
-        N.check(N.lib().mw_scene_get_contacts(self.handle, w, N.dptr(out), 32, ctypes.byref(n)), "contacts")
+        N.check(N.lib().mw_scene_get_contacts(self.handle, w, N.dptr(out), len(out), ctypes.byref(n)), "contacts")
+        if n.value > len(out):
+            out = np.zeros((n.value, 14))
+            N.check(N.lib().mw_scene_get_contacts(self.handle, w, N.dptr(out), len(out), ctypes.byref(n)), "contacts")
         return out[:n.value]
 
     def apply_world_wrench(self, m: int, link: int, wrench, duration: float, w0: int = 0,

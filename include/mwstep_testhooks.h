@@ -29,6 +29,15 @@ int mw_debug_lcp_solve(const float* A, const float* rhs, uint64_t free_mask, int
  * vertices, then the two faces meeting there.  Returns 0 (MW_OK). */
 int mw_debug_hull(const double* pts, int32_t n, double* planes, int32_t* faces, int32_t* edges, int32_t* counts);
 
+/* The large-contact workspace of world w of a scene after its last run
+ * (csrc/scene_kernel.hip ScBigWs: contacts [cmax][20], then the row fields
+ * [11][rows]; the world's last step took the large-contact path when its
+ * contact count exceeds 32 or its rows 64): the first min(cap, 20 cmax + 11
+ * rows) floats into out.  cmax = rows = 0: the scene has no workspace.
+ * Synchronises the scene's stream.  Returns 0 on success. */
+typedef struct mw_scene mw_scene;
+int mw_debug_scene_big_ws(mw_scene* s, int32_t w, float* out, int64_t cap, int32_t* cmax, int32_t* rows);
+
 #ifdef __cplusplus
 }
 #endif

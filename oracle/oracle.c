@@ -519,7 +519,9 @@ void or_rnea(const or_model* m, const double* q, const double* qd,
  * sweeps (+ 1e6 x box-QP iterations) of the latest solve and its final
  * complementarity residual. */
 #define OR_PGS_WARM 300
-#define OR_LCP_MAXN (3 * OR_MAXFC + 3 * OR_MAXB > 3 * OR_MAXCONTACTS ? 3 * OR_MAXFC + 3 * OR_MAXB : 3 * OR_MAXCONTACTS)
+#define OR_LCP_MAXN0 (3 * OR_MAXFC + 3 * OR_MAXB > 3 * OR_MAXCONTACTS ? 3 * OR_MAXFC + 3 * OR_MAXB : 3 * OR_MAXCONTACTS)
+/* ... and the scene step's rows (3 OR_SC_MAXC contact rows + joint rows) */
+#define OR_LCP_MAXN (OR_LCP_MAXN0 > 3 * OR_SC_MAXC + 3 * OR_MAXB ? OR_LCP_MAXN0 : 3 * OR_SC_MAXC + 3 * OR_MAXB)
 static _Thread_local int g_pgs_sweeps = 0;
 static _Thread_local double g_pgs_delta = 0.0;
 
@@ -3120,6 +3122,8 @@ int or_scene_step(const or_scene_model* sm, double dt, or_scene_state* st, const
             static _Thread_local int findex[3 * OR_SC_MAXC + 3 * OR_MAXB];
             for (int r = 0; r < nr; ++r) findex[r] = (kind[r] == K_FRIC) ? r - (r % 3) : -1;
             lcp_dantzig(nr, A, nr, bb, lo, hi, findex, sm->mu, x);
+            if (nr <= OR_CAP_MAXN)
+                for (int r = 0; r < nr; ++r) g_cap_x1[r] = g_last_x1[r];
         }
         if (nr <= OR_CAP_MAXN)
             for (int r = 0; r < nr; ++r) g_cap_x[r] = x[r];

@@ -298,7 +298,7 @@ void or_vec_rollout(const or_model* m, const or_task* t, int W, int T,
 /* LCP over every contact and joint row.                               */
 /* ------------------------------------------------------------------ */
 #define OR_SC_MAXM 8
-#define OR_SC_MAXC 64            /* contact points per step                  */
+#define OR_SC_MAXC 160           /* contact points per step (above the GPU large-contact capacity, 128) */
 #define OR_SC_MAXNV (6 * OR_SC_MAXM + OR_MAXB)
 
 typedef struct {

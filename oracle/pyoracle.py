@@ -1171,7 +1171,7 @@ class FloatWorld:
 
 
 OR_SC_MAXM = 8
-OR_SC_MAXC = 64
+OR_SC_MAXC = 160
 
 
 class OrSceneModel(ctypes.Structure):

@@ -21,3 +21,15 @@ def sphere_urdf(mass: float = 1.0, radius: float = 0.1) -> str:
     return (f'<robot name="ball"><link name="ball"><inertial><mass value="{mass}"/>'
             f'<inertia ixx="{i}" iyy="{i}" izz="{i}" ixy="0" ixz="0" iyz="0"/></inertial>'
             f'<collision><geometry><sphere radius="{radius}"/></geometry></collision></link></robot>')
+
+
+def plank_urdf(k: int = 5, mass: float = 5.0, edge: float = 0.2) -> str:
+    """k cubes of `edge` fused along x into one rigid link (k box collisions)."""
+    L = k * edge
+    ixx = 1 / 12 * mass * (2 * edge ** 2)
+    iyy = 1 / 12 * mass * (L ** 2 + edge ** 2)
+    col = "".join(f'<collision><origin xyz="{(i - (k - 1) / 2) * edge} 0 0" rpy="0 0 0"/><geometry>'
+                  f'<box size="{edge} {edge} {edge}"/></geometry></collision>' for i in range(k))
+    return (f'<robot name="plank"><link name="plank"><inertial><origin rpy="0 0 0" xyz="0 0 0"/>'
+            f'<mass value="{mass}"/><inertia ixx="{ixx}" ixy="0" ixz="0" iyy="{iyy}" iyz="0" izz="{iyy}"/>'
+            f'</inertial>{col}</link></robot>')

@@ -447,23 +447,6 @@ def test_generic_fixed_base_tree_one_step(require_gpu, oracle):
     sim.close()
 
 
-def test_capacity_overflow_fails_loudly(require_gpu):
-    """A world with more contact points than the per-step capacity (8 cubes
-    side by side in face contact on the ground: 32 ground corners plus the
-    box-box face points) drops points; the synchronous run reports it
-    (MW_ECAPACITY -> RuntimeError naming the dropped count) instead of
-    stepping on silently, and the counter keeps the total."""
-    from mwstep import native as N
-    models = [(cube_urdf(), (0.1999 * k, 0.0, 0.0999, 1, 0, 0, 0), f"c{k}") for k in range(8)]
-    sc = _scene(models, 2)
-    with pytest.raises(RuntimeError, match="capacity"):
-        sc.run()
-    assert sc.overflow() > 0
-    err = N.lib().mw_last_error().decode()
-    assert "dropped" in err
-    sc.close()
-
-
 def test_cylinder_sphere_contacts(require_gpu, oracle):
     """Cylinder-sphere contacts on the scene kernel (sc_cylinder_sphere, the
     float32 restatement of oracle.c cylinder_sphere): one step over 256 worlds

@@ -56,7 +56,7 @@ def test_every_test_hook_is_exported(N):
     ScenarI/O header): exported and bound by TEST_SIGNATURES."""
     L = ctypes.CDLL(N.LIB_PATH)
     declared = _declared_symbols(TEST_HEADER)
-    assert declared == ["mw_debug_hull", "mw_debug_lcp_solve"]
+    assert declared == ["mw_debug_hull", "mw_debug_lcp_solve", "mw_debug_scene_big_ws"]
     assert all(hasattr(L, s) for s in declared)
     assert set(declared) == {name for name, _, _ in N.TEST_SIGNATURES}
     assert not set(declared) & set(_declared_symbols())
