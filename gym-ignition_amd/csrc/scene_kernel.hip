@@ -895,12 +895,15 @@ struct ScBigWs {
     __device__ float* Lf() const { return A() + static_cast<size_t>(R) * R; }
 };
 
-// LDS scratch of the large-contact LCP (inside ScWorld's union)
+// LDS scratch of the large-contact LCP (inside ScWorld's union), as LDS
+// pointers: generic ones made the compiler form (and hoist, and spill) a
+// flat -> LDS conversion per address of the unrolled tile loops
+using lds_float = __attribute__((address_space(3))) float;
 struct ScBigLds {
-    float* xs;   // [kScBigRows] impulses
-    float* vs;   // [kScBigRows] the solve's right-hand side / result
-    float* T0;   // [64][64] the current diagonal tile: l_rc below, d_c on the diagonal
-    float* T1;   // [64][64] a panel tile
+    lds_float* xs;   // [kScBigRows] impulses
+    lds_float* vs;   // [kScBigRows] the solve's right-hand side / result
+    lds_float* T0;   // [64][64] the current diagonal tile: l_rc below, d_c on the diagonal
+    lds_float* T1;   // [64][64] a panel tile
 };
 constexpr int kScBigLdsFloats = 2 * kScBigRows + 2 * 64 * 64;
 constexpr int kScBigSweeps = 24;   // PGS sweeps before each stage's active-set solve
@@ -962,7 +965,7 @@ __device__ __forceinline__ void sc_tile64(const ScWorld<MAXNV>& L, int NV, float
 // (A x)_r for the lane's row r over the first n columns (A symmetric: column
 // r, coalesced over the lanes), compensated as lcp_matvec (Dot2); mag = sum
 // |A_rc x_c|.  Rows are padded to 64, so every read is inside A.
-__device__ __forceinline__ float sc_big_dot(const float* __restrict__ A, int R, const float* __restrict__ xs, int r,
+__device__ __forceinline__ float sc_big_dot(const float* __restrict__ A, int R, const lds_float* __restrict__ xs, int r,
                                             int n, float& mag) {
 #pragma clang fp contract(off)
     float w = 0.f, cc = 0.f, m = 0.f;
@@ -1194,7 +1197,7 @@ __device__ __noinline__ bool sc_big_boxqp(ScBigWs G, int NR, int nb, int budget,
     float* st = G.row(7);
     float* gg = G.row(8);
     float* tl = G.row(9);
-    float* xs = S.xs;
+    lds_float* xs = S.xs;
     auto set_st = [&](int r, int v) { st[r] = __int_as_float(v); };
     // working set from the start point (a row on a bound starts held there)
     {
@@ -1531,7 +1534,7 @@ __device__ __noinline__ ScBigOut sc_big_constraints(const SceneF* __restrict__ P
     __threadfence_block();
     // ---- the LCP (scratch in the LDS union, dead since the responses)
     static_assert(sizeof(L.A) >= kScBigLdsFloats * sizeof(float), "large-contact LCP scratch");
-    float* base = &L.A[0][0];
+    lds_float* base = (lds_float*)&L.A[0][0];
     const ScBigLds S{base, base + kScBigRows, base + 2 * kScBigRows, base + 2 * kScBigRows + 64 * 64};
     for (int r = lane; r < kWaveLanes * nblk; r += kWaveLanes) S.xs[r] = 0.f;
     wave_lds_sync();
