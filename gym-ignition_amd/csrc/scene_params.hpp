@@ -41,7 +41,7 @@ constexpr int kScMaxHulls = 8;          // mesh shapes with a collision hull (hu
 constexpr int kScBigContacts = 128;
 constexpr int kScBigRows = 512;         // 8 blocks of 64: contact rows 3 c + d, then joint rows
 constexpr int kScBigContactWords = 20;  // p[3] n[3] t1[3] t2[3] depth, node A, node B, key, x[3], pad
-constexpr int kScPairMaxPoints = 8;     // contact points of one shape pair (worst-case sizing)
+constexpr int kScPairMaxPoints = 4;     // contact points of one shape pair (every pair reduces to <= 4; worst-case sizing)
 
 // A mesh shape's collision hull (hull.hpp build_hull, float32, shape frame):
 // vertices, outward face planes (n, d: inside n . x <= d), face polygons
