@@ -46,7 +46,7 @@ constexpr int kGroupMaxBodies = kGroupLanes;
 
 // Phase timing (debug builds only: EXTRA=-DMW_GROUP_PROF, scripts/group_prof.py):
 // shader-clock cycles per phase, summed over the worlds of a launch.
-constexpr int kGroupProfPhases = 9;
+constexpr int kGroupProfPhases = 10;   // [9]: PGS sweeps
 #ifdef MW_GROUP_PROF
 #define MW_GPROF_T(var) const long long var = clock64()
 #define MW_GPROF_ACC(k, a, b) (prof[k] += static_cast<unsigned long long>((b) - (a)))
@@ -560,6 +560,9 @@ __device__ __forceinline__ void group_substep(const GBody<N>& B, int li, int n, 
                         dq = fmaf(delta, mc[d], dq);
                     }
                 });
+#ifdef MW_GROUP_PROF
+                prof[9] += 1;
+#endif
                 // a sweep that moves no impulse in any world of the wave is a
                 // fixed point of every one of them (chain_dyn.hpp: substep)
                 if (!__any(moved != 0.f)) break;

@@ -33,7 +33,7 @@ tg = tg.contiguous()
 L = N.lib()
 fn = L.mw_debug_group_prof
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 9)()
+buf = (ctypes.c_ulonglong * 10)()
 for k in range(20):
     env.step(tg[k])
 torch.cuda.synchronize()
@@ -45,4 +45,5 @@ fn(buf)
 print(f"{W} worlds, {T} steps")
 for k, name in enumerate(PHASES):
     print(f"  {name:36s} {buf[k] / W / T:10.0f} cycles/world-step")
+print(f"  PGS sweeps {buf[9] / W / T:.2f} per world-step")
 env.close()

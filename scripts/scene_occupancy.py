@@ -16,6 +16,6 @@ import torch  # noqa: E402
 args = types.SimpleNamespace(seed=42)
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-for W in (256, 512, 640, 768, 1024, 1536):
-    o = bench.scene_leg(args, dev, torch, W=W, K=200, warm=20, G=20)
+for W in [int(x) for x in os.environ.get("OCC_W", "256,512,640,768,1024,1536").split(",")]:
+    o = bench.scene_leg(args, dev, torch, W=W, K=int(os.environ.get("OCC_K", "200")), warm=int(os.environ.get("OCC_WARM", "20")), G=20)
     print(json.dumps({"worlds": W, "ms_per_step": o["ms_per_step"]}), flush=True)
