@@ -43,7 +43,7 @@
 namespace mw {
 namespace dev {
 
-// per-node record (41 words, odd: lane-strided parent gathers are conflict-free)
+// per-node record (39 words, odd: lane-strided parent gathers are conflict-free)
 struct ScNode {
     M3 R;        // joint transform parent -> node (bases: unused)
     f3 p;
@@ -54,40 +54,46 @@ struct ScNode {
     M3 Rw;       // world pose
     f3 pw;
     int32_t depth;
-    float pad_[2];
 };
-static_assert(sizeof(ScNode) == 41 * 4, "ScNode layout");
+static_assert(sizeof(ScNode) == 39 * 4, "ScNode layout");
 
 // narrow-phase workspace words per lane (ScWorld::clip): two clipping
 // polygons of <= 8 vertices x {u, v, x, y, z}, then 8 point slots (a pair's
-// output: the first np)
+// output: the first np); columns for 32 lanes, so shape pairs run 32 per pass
+// (half the workspace of one column per lane)
 constexpr int kScWsPoly = 0, kScWsOut = 80, kScWsWords = 112;
+constexpr int kScClipLanes = 32;
 
 template <int MAXNV>
 struct ScWorld {
     static constexpr int kStride = MAXNV + 1;     // odd: lane-strided rows are conflict-free
-    static constexpr int kAStride = kScMaxRows + 1;
     ScNode node[kScMaxNodes];
     // phase-disjoint storage (one wave runs the phases in program order):
     // the ABA's child -> parent accumulators, the narrow phase's workspace,
-    // the response passes' per-lane stacks, then the Delassus matrix -- 37 KiB
-    // instead of 69 KiB, so two worlds fit in a CU's 160 KiB of LDS, not one
+    // the response passes' per-lane stacks, then the exact LCP's pivot rows
+    // (the Delassus matrix of <= 64 rows sits in registers; more rows take the
+    // large-contact path) or that path's LCP scratch -- 21 KiB.  The world's
+    // record is 53,024 B (MAXNV 32): three worlds per CU.  At 54,240 B it
+    // still ran two (the CU's LDS is handed out in blocks: 3 x 54,240 B did
+    // not fit), at 53,024 B three: the three-cube leg 0.739 -> 0.561 ms
+    // 
     union {
         WaveAcc acc[kScMaxNodes];
-        float clip[kScWsWords][kWaveLanes];          // the narrow phase's per-lane workspace
+        float clip[kScWsWords][kScClipLanes];        // the narrow phase's per-lane workspace
         float stack[kScMaxDepth][7][kWaveLanes];
-        alignas(16) float A[kScMaxRows][kAStride];  // also the exact LCP's pivot rows (16-byte reads)
+        alignas(16) float lcp[kLcpWorkFloats];       // the exact LCP's pivot rows (16-byte reads)
+        float big[kScBigRows + 64 * 64];             // the large-contact LCP: vs, T0 (xs in the row arrays)
     };
     float l0[kScMaxModels][28];   // Chol6 (l[21], id[6]) of every floating base
     float q[kScMaxBodies], qd[kScMaxBodies], qdd[kScMaxBodies], tau[kScMaxBodies], vc[kScMaxBodies];
     uint32_t act[kScMaxBodies];
     float nu[MAXNV];
-    float J[kScMaxRows][kStride];
+    float J[kScMaxRows][kStride];     // (J then MJ: also the large-contact LCP's T1 tile)
     float MJ[kScMaxRows][kStride];
-    F4 rc[kScMaxRows];            // {b, 1/A_rr, lo, hi}
+    F4 rc[kScMaxRows];            // {b, 1/A_rr, lo, hi} (rc .. rhi: also the large-contact LCP's impulses)
     int32_t src[kScMaxRows];      // contact rows 3 c + d; joint rows kJointRow + 3 body + type
     float rb[kScMaxRows], rlo[kScMaxRows], rhi[kScMaxRows];
-    float c_p[kScMaxContacts][3], c_n[kScMaxContacts][3], c_t1[kScMaxContacts][3], c_t2[kScMaxContacts][3];
+    float c_p[kScMaxContacts][3], c_n[kScMaxContacts][3];   // (tangents: plane_space_f of the normal where used)
     float c_d[kScMaxContacts];
     int32_t c_na[kScMaxContacts], c_nb[kScMaxContacts];
     int32_t c_key[kScMaxContacts];  // warm-start identity: ground slot, or n_slots + 4 pair + point
@@ -162,14 +168,14 @@ __device__ __forceinline__ M3 mul3(const M3& A, const M3& B) {
 struct ScWsPts {
     float* w;
     __device__ __forceinline__ f3 pt(int i) const {
-        return {w[(4 * i) * kWaveLanes], w[(4 * i + 1) * kWaveLanes], w[(4 * i + 2) * kWaveLanes]};
+        return {w[(4 * i) * kScClipLanes], w[(4 * i + 1) * kScClipLanes], w[(4 * i + 2) * kScClipLanes]};
     }
-    __device__ __forceinline__ float dep(int i) const { return w[(4 * i + 3) * kWaveLanes]; }
+    __device__ __forceinline__ float dep(int i) const { return w[(4 * i + 3) * kScClipLanes]; }
     __device__ __forceinline__ void set(int i, f3 x, float d) const {
-        w[(4 * i) * kWaveLanes] = x.x;
-        w[(4 * i + 1) * kWaveLanes] = x.y;
-        w[(4 * i + 2) * kWaveLanes] = x.z;
-        w[(4 * i + 3) * kWaveLanes] = d;
+        w[(4 * i) * kScClipLanes] = x.x;
+        w[(4 * i + 1) * kScClipLanes] = x.y;
+        w[(4 * i + 2) * kScClipLanes] = x.z;
+        w[(4 * i + 3) * kScClipLanes] = d;
     }
     __device__ __forceinline__ void move(int m, int i) const { set(m, pt(i), dep(i)); }
 };
@@ -316,7 +322,7 @@ __device__ __forceinline__ int sc_box_box(f3 hA, f3 cA, const M3& RA, f3 hB, f3 
     const f3 fc = cR + self3(hR0, hR1, hR2, fk) * nr;
     // polygon: (u, v, x, y, z) per vertex, clipped between the workspace's two
     // polygons (at most 8 vertices): word (8 c + i) 5 + k of the lane's column
-    auto poly = [ws](int c, int i, int k) -> float& { return ws[((8 * c + i) * 5 + k) * kWaveLanes]; };
+    auto poly = [ws](int c, int i, int k) -> float& { return ws[((8 * c + i) * 5 + k) * kScClipLanes]; };
     const float sx[4] = {1.f, -1.f, -1.f, 1.f}, sy[4] = {1.f, 1.f, -1.f, -1.f};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -674,7 +680,7 @@ __device__ __noinline__ int sc_hull_pair(ScPoly A, f3 cA, M3 RA, ScPoly B, f3 cB
 // ScWorld::clip)
 __device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, int tb, f3 sb, f3 cb, const M3& Rb,
                                           f3& n, float* ws) {
-    const ScWsPts out{ws + kScWsOut * kWaveLanes};
+    const ScWsPts out{ws + kScWsOut * kScClipLanes};
     f3 pt, nbs;
     float dep;
     if ((ta == 2 && tb == 1) || (ta == 1 && tb == 2)) {
@@ -689,7 +695,7 @@ __device__ __forceinline__ int sc_collide(int ta, f3 sa, f3 ca, const M3& Ra, in
         return 1;
     }
     if (ta == 2 || tb == 2) return sc_cylinder_pair(ta, sa, ca, Ra, tb, sb, cb, Rb, n, out);
-    if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, out, ws + kScWsPoly * kWaveLanes);
+    if (ta == 0 && tb == 0) return sc_box_box(sa, ca, Ra, sb, cb, Rb, n, out, ws + kScWsPoly * kScClipLanes);
     if (ta == 1 && tb == 1) {
         const f3 d = ca - cb;
         const float dist = sqrtf(dot(d, d));
@@ -1533,9 +1539,17 @@ __device__ __noinline__ ScBigOut sc_big_constraints(const SceneF* __restrict__ P
     }
     __threadfence_block();
     // ---- the LCP (scratch in the LDS union, dead since the responses)
-    static_assert(sizeof(L.A) >= kScBigLdsFloats * sizeof(float), "large-contact LCP scratch");
-    lds_float* base = (lds_float*)&L.A[0][0];
-    const ScBigLds S{base, base + kScBigRows, base + 2 * kScBigRows, base + 2 * kScBigRows + 64 * 64};
+    static_assert(sizeof(L.big) >= (kScBigRows + 64 * 64) * sizeof(float), "large-contact LCP scratch");
+    static_assert(sizeof(L.J) + sizeof(L.MJ) >= 64 * 64 * sizeof(float) &&
+                      offsetof(ScWorld<MAXNV>, MJ) == offsetof(ScWorld<MAXNV>, J) + sizeof(L.J),
+                  "the T1 tile spans J and MJ");
+    static_assert(offsetof(ScWorld<MAXNV>, rhi) + sizeof(L.rhi) - offsetof(ScWorld<MAXNV>, rc) ==
+                      sizeof(L.rc) + sizeof(L.src) + sizeof(L.rb) + sizeof(L.rlo) + sizeof(L.rhi),
+                  "the impulses span the contiguous row arrays");
+    static_assert(sizeof(L.rc) + sizeof(L.src) + sizeof(L.rb) + sizeof(L.rlo) + sizeof(L.rhi) >= kScBigRows * sizeof(float),
+                  "xs spans the compact row arrays");
+    lds_float* base = (lds_float*)L.big;
+    const ScBigLds S{(lds_float*)&L.rc[0], base, base + kScBigRows, (lds_float*)&L.J[0][0]};
     for (int r = lane; r < kWaveLanes * nblk; r += kWaveLanes) S.xs[r] = 0.f;
     wave_lds_sync();
     bool ok = true;
@@ -1816,12 +1830,12 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #ifdef MW_WAVE_PROF
     long long t_np = t_gnd;
 #endif
-    for (int p0 = 0; p0 < P->n_pairs; p0 += kWaveLanes) {
-        const int pr = p0 + lane;
+    for (int p0 = 0; p0 < P->n_pairs; p0 += kScClipLanes) {
+        const int pr = (lane < kScClipLanes) ? p0 + lane : P->n_pairs;
         int np = 0;
         f3 nrm = {0.f, 0.f, 1.f};
-        float* ws = &L.clip[0][lane];
-        const ScWsPts out{ws + kScWsOut * kWaveLanes};
+        float* ws = &L.clip[0][lane & (kScClipLanes - 1)];
+        const ScWsPts out{ws + kScWsOut * kScClipLanes};
         int na = 0, nb = 0;
         if (pr < P->n_pairs) {
             const int sa = P->pair_a[pr], sb = P->pair_b[pr];
@@ -1888,10 +1902,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
     if (lane < nc) {
         const f3 n = mk(L.c_n[lane][0], L.c_n[lane][1], L.c_n[lane][2]);
-        f3 t1, t2;
-        plane_space_f(n, t1, t2);
-        L.c_t1[lane][0] = t1.x; L.c_t1[lane][1] = t1.y; L.c_t1[lane][2] = t1.z;
-        L.c_t2[lane][0] = t2.x; L.c_t2[lane][1] = t2.y; L.c_t2[lane][2] = t2.z;
+        (void)n;
         L.c_x[lane][0] = L.c_x[lane][1] = L.c_x[lane][2] = 0.f;
     }
 
@@ -1969,7 +1980,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
     }
 
     float x1s = 0.f;  // the exact solve's stage-1 impulse of row `lane` (warm record)
-    float x0 = 0.f;   // the impulse of row `lane` (rows 64.. : x1 below)
+    float x0 = 0.f;   // the impulse of row `lane`
     MW_PROF_T(t_rows);
 #ifdef MW_WAVE_PROF
     long long t_resp = t_rows, t_del = t_rows, t_lcp = t_rows;
@@ -1993,8 +2004,10 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 const int src = L.src[r];
                 if (src < kJointRow) {
                     const int c = src / 3, d = src % 3;
-                    const float* dwp = d == 0 ? L.c_n[c] : (d == 1 ? L.c_t1[c] : L.c_t2[c]);
-                    const f3 dw = mk(dwp[0], dwp[1], dwp[2]);
+                    const f3 cn = mk(L.c_n[c][0], L.c_n[c][1], L.c_n[c][2]);
+                    f3 ct1, ct2;
+                    plane_space_f(cn, ct1, ct2);
+                    const f3 dw = d == 0 ? cn : (d == 1 ? ct1 : ct2);
                     const f3 xp = mk(L.c_p[c][0], L.c_p[c][1], L.c_p[c][2]);
                     float jv = 0.f;
 #pragma unroll
@@ -2031,9 +2044,8 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         // PGS and the exact solve keep it in.  Columns >= NV of J and MJ are
         // zero (the response pass clears them); rows / columns >= NR are
         // masked.  (The lane = column FMA loop over LDS took 21.8k cycles per
-        // world-step on the three-cube scene.)  More rows: that loop, into L.A.
         float a[kWaveLanes];
-        if (NR <= kWaveLanes) {
+        {
             const int lr = lane & 31, lh = lane >> 5;
             const bool hi2 = NR > 32;
             v16f t00 = {}, t01 = {}, t10 = {}, t11 = {};
@@ -2082,38 +2094,9 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 }
             }
             if (lane < NR) L.rc[lane] = F4{L.rb[lane], rcp(dg), L.rlo[lane], L.rhi[lane]};
-        } else {
-            for (int c0 = 0; c0 < NR; c0 += kWaveLanes) {
-                const int c = c0 + lane;
-                float mj[MAXNV];
-#pragma unroll
-                for (int e = 0; e < MAXNV; ++e) mj[e] = (c < NR) ? L.MJ[c][e] : 0.f;
-                for (int r = 0; r < NR; ++r) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int e = 0; e < MAXNV; ++e) acc += L.J[r][e] * mj[e];
-                    if (c < NR) {
-                        if (r == c) acc *= 1.f + ((r >= ncr) ? kJointCfm : kContactCfm);
-                        L.A[r][c] = acc;
-                    }
-                }
-            }
-            for (int r0 = 0; r0 < NR; r0 += kWaveLanes) {
-                const int r = r0 + lane;
-                if (r < NR) {
-                    F4 cst;
-                    cst.x = L.rb[r];
-                    cst.y = rcp(L.A[r][r]);
-                    cst.z = L.rlo[r];
-                    cst.w = L.rhi[r];
-                    L.rc[r] = cst;
-                }
-            }
         }
-        // ---- PGS (rows in order; lane c owns rows c and c + 64)
-        float x1 = 0.f, w0 = 0.f, w1 = 0.f;
-        const bool two = NR > kWaveLanes;
-        if (NR <= kWaveLanes) {
+        // ---- PGS (rows in order)
+        {
             // up to 64 rows: the register form of wave_tree.hpp -- lane c holds
             // column c of A (= row c) in registers, the impulses are uniform
             // registers, the residual w_c = sum_r A[c][r] x_r is rebuilt per
@@ -2197,8 +2180,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
                 Rw.b = Rw.live ? c.x : 0.f;
                 Rw.lo = Rw.live ? c.z : 0.f;
                 Rw.hi = Rw.live ? c.w : 0.f;
-                static_assert(sizeof(L.A) >= kLcpWorkFloats * sizeof(float), "LCP workspace");
-                float* Uw = &L.A[0][0];
+                float* Uw = L.lcp;
                 int nsolve = 0, nround = 0, nsolve1 = 0;
                 long long cyc[3] = {0, 0, 0};
                 x1s = xw1;
@@ -2264,47 +2246,6 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #endif
                 x0 = Rw.live ? x0 : 0.f;
             }
-        } else if (lcp_solves > 0 && lane == 0) {
-            unconv += 1;  // more than 64 rows: the PGS sweeps alone (counted as not solved exactly)
-        }
-        for (int it = 0; it < (two ? pgs_iters : 0); ++it) {
-            // the residual w = A x is rebuilt at the start of every sweep (as
-            // the oracle forms b - A x exactly per row): no drift of the
-            // incremental updates across sweeps
-            if (it > 0) {
-                w0 = 0.f;
-                w1 = 0.f;
-                for (int r = 0; r < NR; ++r) {
-                    const float xr = read_lane(r >= kWaveLanes ? x1 : x0, r & (kWaveLanes - 1));
-                    w0 = fmaf(L.A[r][lane], xr, w0);
-                    if (two && kWaveLanes + lane < NR) w1 = fmaf(L.A[r][kWaveLanes + lane], xr, w1);
-                }
-            }
-            float h = 0.f;
-            for (int r = 0; r < NR; ++r) {
-                const F4 cst = L.rc[r];
-                const bool hi = r >= kWaveLanes;
-                const int lr = r & (kWaveLanes - 1);
-                const float xr = read_lane(hi ? x1 : x0, lr);
-                const float wr_ = read_lane(hi ? w1 : w0, lr);
-                float v = fmaf(cst.x - wr_, cst.y, xr);
-                if (r < ncr) {
-                    if (r % 3 == 0) {
-                        v = clamp_ordered(v, 0.f, kBig);
-                        h = mu * v;
-                    } else {
-                        v = clamp_ordered(v, -h, h);
-                    }
-                } else {
-                    v = clamp_ordered(v, cst.z, cst.w);
-                }
-                const float dl = v - xr;
-                w0 = fmaf(L.A[r][lane], dl, w0);
-                if (two && kWaveLanes + lane < NR) w1 = fmaf(L.A[r][kWaveLanes + lane], dl, w1);
-                // branch-free: x stays defined in every lane for the lane reads
-                x0 = (lane == lr && !hi) ? v : x0;
-                x1 = (lane == lr && hi) ? v : x1;
-            }
         }
 #ifdef MW_WAVE_PROF
         t_lcp = clock64();
@@ -2324,7 +2265,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const int r = r0 + k;
-                    const float xr = read_lane(r >= kWaveLanes ? x1 : x0, r & (kWaveLanes - 1));
+                    const float xr = read_lane(x0, r & (kWaveLanes - 1));
                     dnu += (r < NR) ? xr * mj[k] : 0.f;
                 }
             }
@@ -2332,7 +2273,7 @@ __device__ void sc_step(const SceneF* __restrict__ P, ScWorld<MAXNV>& L, FreeSta
         }
         for (int r0 = 0; r0 < NR && r0 < ncr; r0 += kWaveLanes) {
             const int r = r0 + lane;
-            if (r < ncr && r < NR) L.c_x[r / 3][r % 3] = r0 ? x1 : x0;
+            if (r < ncr && r < NR) L.c_x[r / 3][r % 3] = x0;
         }
     }
     if (warm.rec) {
@@ -2579,8 +2520,8 @@ __global__ void __launch_bounds__(64) scene_run_kernel(const SceneF* __restrict_
             const float inv_dt = A.inv_dt;
             float* o = D.contact + static_cast<size_t>(lane) * 12 * W + w;
             const f3 n = mk(L.c_n[lane][0], L.c_n[lane][1], L.c_n[lane][2]);
-            const f3 t1 = mk(L.c_t1[lane][0], L.c_t1[lane][1], L.c_t1[lane][2]);
-            const f3 t2 = mk(L.c_t2[lane][0], L.c_t2[lane][1], L.c_t2[lane][2]);
+            f3 t1, t2;
+            plane_space_f(n, t1, t2);
             const f3 f = inv_dt * (L.c_x[lane][0] * n + L.c_x[lane][1] * t1 + L.c_x[lane][2] * t2);
             o[0 * W] = L.c_p[lane][0]; o[1 * W] = L.c_p[lane][1]; o[2 * W] = L.c_p[lane][2];
             o[3 * W] = n.x; o[4 * W] = n.y; o[5 * W] = n.z;

@@ -27,7 +27,7 @@ constexpr int kScMaxShapes = 48;
 constexpr int kScMaxPairs = 128;        // shape pairs of different models (2 lane passes)
 constexpr int kScMaxGroundSlots = 128;  // 8 per box / cylinder, 1 per sphere, <= 16 per mesh (2 lane passes)
 constexpr int kScMaxContacts = 32;      // contact points per step (3 rows each)
-constexpr int kScMaxRows = 96;
+constexpr int kScMaxRows = 64;         // rows of the compact path (the register LCP); more: the large-contact path
 constexpr int kScWrenchSlots = 4;       // concurrent wrenches (distinct expiries) per link
 constexpr int kScMaxDepth = 12;         // tree depth of the response passes' stacks
 constexpr uint32_t kScGroundBit = 1u << 31;  // present mask: the world has a ground plane
